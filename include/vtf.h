@@ -1,0 +1,114 @@
+/*
+ * vtf.h — C ABI of libvtf_hip.so, the MI355X-native hot path of video-to-faces.
+ *
+ * The reference has no C ABI: its plugin surface is Python.  These entry
+ * points are what that Python surface binds to (video-to-faces_amd/videotofaces/_native.py,
+ * ctypes); each names the reference interface it replaces.  Conventions:
+ *   - every call returns int status: 0 = ok, negative = error (message: vtf_last_error());
+ *   - no exceptions cross the ABI; the caller owns every buffer it passes;
+ *   - "d_" pointers are device (HBM) pointers, others are host pointers;
+ *   - a handle is bound to one GPU and one HIP stream (vtf_*_set_stream) and is not
+ *     thread-safe (the reference calls its models from one Python thread).
+ */
+#ifndef VTF_H
+#define VTF_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define VTF_OK 0
+#define VTF_E_ARG (-1)        /* bad argument (shape, null pointer, ...)           */
+#define VTF_E_HIP (-2)        /* HIP runtime error                                 */
+#define VTF_E_CAPACITY (-3)   /* output buffer too small; *out_total says how big  */
+#define VTF_E_DEGENERATE (-4) /* reference crop loop would skip a box -> IndexError */
+#define VTF_E_LIMIT (-5)      /* an internal size limit was exceeded               */
+
+const char* vtf_last_error(void);
+int vtf_version(void);
+
+typedef struct vtf_mtcnn_s* vtf_mtcnn_t;
+typedef struct vtf_facenet_s* vtf_facenet_t;
+
+/* ---------------------------------------------------------------- MTCNN detector
+ * Replaces RealMTCNN / MTCNN.forward (src/videotofaces/detectors/mtcnn.py:167-252,
+ * 312-326), called by detection.py:131 `detout = model(frames)`.
+ * params: fp32, the reference state_dict order minus num_batches_tracked
+ *         (videotofaces/specs.py mtcnn_spec, 495,850 floats). */
+int vtf_mtcnn_create(const float* params, int64_t n_params, int device, vtf_mtcnn_t* out);
+int vtf_mtcnn_destroy(vtf_mtcnn_t h);
+int vtf_mtcnn_set_stream(vtf_mtcnn_t h, void* hip_stream);
+
+/* frames: uint8 BGR, frame b pixel (y,x) channel c at frames[b*frame_stride + y*row_stride
+ * + x*3 + c] (a borrowed, possibly non-contiguous view, detection.py:114-116).
+ * frames_on_device: 1 if `frames` is a device pointer.
+ * Output (host): boxes [total,5] (x1,y1,x2,y2,score), landmarks [total,10] (x0..x4,y0..y4,
+ * may be NULL), counts[B]; per image in reference order.  If total > cap nothing is
+ * written, *out_total is set and VTF_E_CAPACITY returned. */
+int vtf_mtcnn_detect(vtf_mtcnn_t h, const uint8_t* frames, int frames_on_device, int B, int H, int W,
+                     int64_t frame_stride, int64_t row_stride, double min_face_size,
+                     float* out_boxes, float* out_landmarks, int32_t* out_counts, int64_t cap,
+                     int64_t* out_total);
+
+/* Per-stage counters of the last detect call: [0] levels, [1] stage-1 candidates (all
+ * levels), [2] after per-level NMS, [3] after cross-level NMS (= stage-2 proposals),
+ * [4] stage-2 passing, [5] after stage-2 NMS (= stage-3 refinements), [6] stage-3 passing,
+ * [7] final faces. */
+int vtf_mtcnn_stats(vtf_mtcnn_t h, int64_t* out8);
+
+/* Parity entry points (device pointers, handle stream).
+ * Fused MTCNN._resample + PNet for one pyramid level (mtcnn.py:150-151, 27-38):
+ * d_prob [B,ph,pw], d_reg [B,4,ph,pw] with ph = ceil((lh-2)/2)-4. */
+int vtf_mtcnn_pnet_level(vtf_mtcnn_t h, const uint8_t* d_frames, int B, int H, int W, int64_t frame_stride,
+                         int64_t row_stride, int lh, int lw, float* d_prob, float* d_reg);
+/* MTCNN._resample of the preprocessed frames (mtcnn.py:133-139,150-151): d_out [B,3,lh,lw]. */
+int vtf_mtcnn_resample(vtf_mtcnn_t h, const uint8_t* d_frames, int B, int H, int W, int64_t frame_stride,
+                       int64_t row_stride, int lh, int lw, float* d_out);
+/* RNet / ONet on given fp32 NCHW inputs (mtcnn.py:58-76, 101-121). */
+int vtf_mtcnn_rnet(vtf_mtcnn_t h, const float* d_in, int64_t n, float* d_reg, float* d_prob);
+int vtf_mtcnn_onet(vtf_mtcnn_t h, const float* d_in, int64_t n, float* d_reg, float* d_lm, float* d_prob);
+
+/* ---------------------------------------------------------------- box ops
+ * torchvision.ops.batched_nms as called at mtcnn.py:196,205,219 and
+ * detectors/operations/post.py:8: d_boxes [n,4] fp32, d_scores [n], d_idxs [n] int64.
+ * Writes keep indices (int64, score-descending) to d_keep and their count to *out_nkeep. */
+int vtf_batched_nms(const float* d_boxes, const float* d_scores, const int64_t* d_idxs, int64_t n,
+                    double iou_threshold, int64_t* d_keep, int64_t* out_nkeep, void* hip_stream);
+
+/* ---------------------------------------------------------------- FaceNet encoder
+ * Replaces FaceNet / InceptionResnetV1 (src/videotofaces/encoders/facenet.py:123-183),
+ * called by grouping.py:37 `xk = model(images)`.
+ * precision: 0 = fp32 (parity mode), 1 = bf16 activations/weights with fp32 accumulation. */
+int vtf_facenet_create(const float* params, int64_t n_params, int device, int precision, vtf_facenet_t* out);
+int vtf_facenet_destroy(vtf_facenet_t h);
+int vtf_facenet_set_stream(vtf_facenet_t h, void* hip_stream);
+/* Encoder on blob input: d_x [N,3,160,160] fp32 NCHW RGB (cv2.dnn.blobFromImages output,
+ * facenet.py:179) -> d_emb [N,512] fp32, L2-normalised. */
+int vtf_facenet_forward(vtf_facenet_t h, const float* d_x, int64_t N, float* d_emb);
+/* Crop + resize + normalise faces straight from device frames (blobFromImages(1/128,
+ * 160x160, 127.5, swapRB) on each crop, INTER_LINEAR uint8), then encode.
+ * d_frames as in vtf_mtcnn_detect; crops: host int32 [N,5] (frame index, x1, y1, x2, y2)
+ * in frame pixels (detection.py:161-162 get_crops slices). */
+int vtf_facenet_encode_crops(vtf_facenet_t h, const uint8_t* d_frames, int H, int W, int64_t frame_stride,
+                             int64_t row_stride, const int32_t* crops, int64_t N, float* d_emb);
+/* Blob of uint8 BGR crops (cv2.dnn.blobFromImages, INTER_LINEAR, swapRB): d_out [N,3,S,S].
+ * out = (resized_u8 - mean) * scale. */
+int vtf_blob_from_crops(const uint8_t* d_frames, int H, int W, int64_t frame_stride, int64_t row_stride,
+                        const int32_t* d_crops, int64_t N, int S, float mean, float scale, float* d_out,
+                        void* hip_stream);
+
+/* ---------------------------------------------------------------- grouping
+ * remove_dupes_overall 'enc' branch (dupes.py:51-68 with sklearn cosine_distances):
+ * for each row i, min and argmin over j < i of clip(1 - cos(X_i, X_j), 0, 2); row 0 gets
+ * 10000 / 0 (the reference's masked diagonal).  d_X [N,D] fp32 -> d_min [N], d_arg [N]. */
+int vtf_cosine_dedupe(const float* d_X, int64_t N, int64_t D, float* d_min, int64_t* d_arg, void* hip_stream);
+/* classify (grouping.py:50-66): argmin / min over c of cosine distance(X_i, R_c). */
+int vtf_cosine_classify(const float* d_X, int64_t N, const float* d_R, int64_t C, int64_t D, float* d_min,
+                        int64_t* d_arg, void* hip_stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* VTF_H */

@@ -1,0 +1,82 @@
+"""Calibrate the synthetic MTCNN face-logit biases.
+
+Random weights make the MTCNN gates meaningless, so each face-logit head's bias
+difference is chosen so that a fixed fraction of candidates pass its gate on synthetic 720p
+frames (min_face_size=5, the RealMTCNN default):
+  PNet  prob >= 0.6 : ~0.2% of cells (logit >= ln(0.6/0.4))
+  RNet  prob >  0.7 : ~5% of stage-2 proposals
+  ONet  prob >  0.7 : ~25% of stage-3 refinements
+Run in the survey container; paste the printed values into synth.MTCNN_CALIB.
+Uses only the build's own oracle (no reference code).
+"""
+import math
+import sys
+import os
+
+import numpy as np
+import torch
+import torch.nn.functional as F
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path[:0] = [ROOT, os.path.join(ROOT, 'video-to-faces_amd')]
+from videotofaces import synth  # noqa: E402
+from oracle import mtcnn as om  # noqa: E402
+
+
+def logit_diff_threshold(d, frac, gate):
+    """bias diff b such that fraction `frac` of (d + b) clears the logit gate."""
+    q = float(torch.quantile(d.double(), 1.0 - frac))
+    return gate - q
+
+
+def main(n_frames=2):
+    fr = synth.make_frames(n_frames, seed=0)
+    synth.MTCNN_CALIB['face_bias'] = {}
+    p = synth.make_params('mtcnn')
+    x = om.preprocess(list(fr))
+    # PNet head: d = (w1 - w0) . features
+    scales, sizes = om.scale_pyramid(720, 1280, 5)
+    xi = F.adaptive_avg_pool2d(x, sizes[0])
+    p2 = dict(p)
+    p2['pnet.conv4_1.weight'] = np.stack([np.zeros_like(p['pnet.conv4_1.weight'][0]),
+                                          p['pnet.conv4_1.weight'][1] - p['pnet.conv4_1.weight'][0]])
+    p2['pnet.conv4_1.bias'] = np.zeros(2, np.float32)
+    _, prob = om.pnet(p2, xi)
+    d = torch.logit(prob.flatten().double())
+    b_p = logit_diff_threshold(d[::3], 0.002, math.log(0.6 / 0.4))
+    print('pnet.conv4_1.bias diff', round(b_p, 4))
+    synth.MTCNN_CALIB['face_bias'] = {'pnet.conv4_1.bias': round(b_p, 4)}
+    p = synth.make_params('mtcnn')
+    boxes, imgidx, _ = om.stage1(p, x, 5)
+    prop = om.cropped_candidates(x, imgidx, boxes, (24, 24))
+    p2 = dict(p)
+    p2['rnet.dense5_1.bias'] = np.zeros(2, np.float32)
+    _, s2 = om.rnet(p2, prop)
+    b_r = logit_diff_threshold(torch.logit(s2.double()), 0.05, math.log(0.7 / 0.3))
+    print('rnet.dense5_1.bias diff', round(b_r, 4), 'stage-2 proposals', prop.shape[0])
+    synth.MTCNN_CALIB['face_bias']['rnet.dense5_1.bias'] = round(b_r, 4)
+    synth.MTCNN_CALIB['face_bias']['onet.dense6_1.bias'] = 0.0
+    p = synth.make_params('mtcnn')
+    # stage 3 inputs
+    preds, scores = om.rnet(p, prop)
+    ip = scores > 0.7
+    b3, s3, pr3, i3 = boxes[ip], scores[ip], preds[ip], imgidx[ip]
+    from oracle import nms as onms
+    pick = onms.batched_nms(b3, s3, i3, 0.7)
+    b3, pr3, i3 = b3[pick], pr3[pick], i3[pick]
+    b3 = om.square_bbox(om.refine_bbox(b3, pr3, True))
+    ref = om.cropped_candidates(x, i3, b3, (48, 48))
+    p2 = dict(p)
+    p2['onet.dense6_1.bias'] = np.zeros(2, np.float32)
+    _, _, s3 = om.onet(p2, ref)
+    b_o = logit_diff_threshold(torch.logit(s3.double()), 0.25, math.log(0.7 / 0.3))
+    print('onet.dense6_1.bias diff', round(b_o, 4), 'stage-3 refinements', ref.shape[0])
+    synth.MTCNN_CALIB['face_bias']['onet.dense6_1.bias'] = round(b_o, 4)
+    p = synth.make_params('mtcnn')
+    res = om.forward(p, list(fr), minsize=5)
+    print('faces per frame', [r.shape[0] for r in res])
+    print('MTCNN_CALIB face_bias =', synth.MTCNN_CALIB['face_bias'])
+
+
+if __name__ == '__main__':
+    main()

@@ -1,0 +1,222 @@
+"""Generate golden vectors from the REFERENCE's own modules (survey container only).
+
+The reference package cannot be imported as-is here (``cv2``/``torchvision`` are absent,
+SURVEY.md §8c).  It is loaded under the alias ``ref_vtf`` with import-time shims:
+  * ``cv2``: a stub whose attributes raise (model forwards never touch cv2);
+  * ``torchvision.ops.batched_nms``: a pure-torch restatement of torchvision's published
+    algorithm written here (independent of oracle/nms_oracle.c, so the two cross-check).
+Weights are the build's deterministic synthetic weights (videotofaces.synth) loaded with
+``load_state_dict(strict=True)``.  Outputs are saved as small .npz fixtures; the reference
+never travels to the GPU box, only these arrays do.
+
+    python tests/golden/make_golden.py            # all fixtures
+"""
+import importlib
+import os
+import sys
+import tempfile
+import types
+
+import numpy as np
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+sys.path[:0] = [os.path.join(ROOT, 'video-to-faces_amd')]
+from videotofaces import synth  # noqa: E402
+
+REF_SRC = '/root/reference/src/videotofaces'
+
+
+def _tv_nms(boxes, scores, thr):
+    # torchvision nms_kernel_impl: stable descending sort, greedy, fp32 IoU vs double thr.
+    # The inner loop over j is vectorised with fp32 torch ops (same per-element rounding).
+    boxes = boxes.float()
+    x1, y1, x2, y2 = boxes.unbind(1)
+    areas = (x2 - x1) * (y2 - y1)
+    order = torch.sort(scores, stable=True, descending=True)[1]
+    n = boxes.shape[0]
+    sup = torch.zeros(n, dtype=torch.bool)
+    keep = []
+    zero = torch.tensor(0, dtype=torch.float32)
+    for _i in range(n):
+        i = int(order[_i])
+        if sup[i]:
+            continue
+        keep.append(i)
+        js = order[_i + 1:]
+        js = js[~sup[js]]
+        if js.numel() == 0:
+            continue
+        xx1 = torch.maximum(x1[i], x1[js])
+        yy1 = torch.maximum(y1[i], y1[js])
+        xx2 = torch.minimum(x2[i], x2[js])
+        yy2 = torch.minimum(y2[i], y2[js])
+        w = torch.maximum(zero, xx2 - xx1)
+        h = torch.maximum(zero, yy2 - yy1)
+        inter = w * h
+        ovr = inter / ((areas[i] + areas[js]) - inter)
+        sup[js[ovr.double() > thr]] = True
+    return torch.tensor(keep, dtype=torch.int64)
+
+
+def _tv_batched_nms(boxes, scores, idxs, thr):
+    if boxes.numel() > 4000:
+        keep_mask = torch.zeros_like(scores, dtype=torch.bool)
+        for class_id in torch.unique(idxs):
+            curr = torch.where(idxs == class_id)[0]
+            keep_mask[curr[_tv_nms(boxes[curr], scores[curr], thr)]] = True
+        keep_indices = torch.where(keep_mask)[0]
+        return keep_indices[scores[keep_indices].sort(descending=True)[1]]
+    if boxes.numel() == 0:
+        return torch.empty((0,), dtype=torch.int64)
+    max_coordinate = boxes.max()
+    offsets = idxs.to(boxes) * (max_coordinate + torch.tensor(1).to(boxes))
+    return _tv_nms(boxes + offsets[:, None], scores, thr)
+
+
+def load_ref():
+    if 'ref_vtf' in sys.modules:
+        return sys.modules['ref_vtf']
+    cv2 = types.ModuleType('cv2')
+
+    def _absent(name):
+        def f(*a, **k):
+            raise RuntimeError('cv2.%s is not available in this container' % name)
+        return f
+    cv2.__getattr__ = _absent
+    sys.modules['cv2'] = cv2
+    tv = types.ModuleType('torchvision')
+    ops = types.ModuleType('torchvision.ops')
+    ops.batched_nms = _tv_batched_nms
+    ops.nms = _tv_nms
+    tv.ops = ops
+    sys.modules['torchvision'] = tv
+    sys.modules['torchvision.ops'] = ops
+    pkg = types.ModuleType('ref_vtf')
+    pkg.__path__ = [REF_SRC]
+    sys.modules['ref_vtf'] = pkg
+    return pkg
+
+
+def _load(module, params):
+    sd = {k: torch.from_numpy(np.asarray(v)) for k, v in params.items()}
+    module.load_state_dict(sd, strict=True)
+    module.eval()
+    return module
+
+
+def gen_mtcnn():
+    load_ref()
+    m = importlib.import_module('ref_vtf.detectors.mtcnn')
+    p = synth.make_params('mtcnn')
+    net = _load(m.MTCNN('cpu'), p)
+    g = torch.Generator().manual_seed(7)
+    out = {}
+    with torch.inference_mode():
+        x = torch.rand(2, 3, 40, 56, generator=g) * 2 - 1
+        reg, prob = net.pnet(x)
+        out.update(pnet_in=x.numpy(), pnet_reg=reg.numpy(), pnet_prob=prob.numpy())
+        x = torch.rand(5, 3, 24, 24, generator=g) * 2 - 1
+        reg, prob = net.rnet(x)
+        out.update(rnet_in=x.numpy(), rnet_reg=reg.numpy(), rnet_prob=prob.numpy())
+        x = torch.rand(5, 3, 48, 48, generator=g) * 2 - 1
+        reg, lm, prob = net.onet(x)
+        out.update(onet_in=x.numpy(), onet_reg=reg.numpy(), onet_lm=lm.numpy(), onet_prob=prob.numpy())
+        # pyramid resample (MTCNN._resample == adaptive_avg_pool2d), up- and down-sampling
+        fr = synth.make_frames(1, 90, 160, seed=3)
+        xx = net._preprocess(list(fr), 'cpu')
+        out['pyr_frame'] = fr
+        scales, sizes = net._scale_pyramid(90, 160, 5, 0.709)
+        for i, sz in enumerate(sizes[:4]):
+            out['pyr_level%d' % i] = net._resample(xx, sz).numpy()
+        out['pyr_sizes'] = np.array(sizes[:4], np.int64)
+    # end-to-end: two 720p frames at the RealMTCNN default min_face_size=5, and the
+    # reference tests' min_face_size=20 (tests/test_mtcnn.py:17)
+    frames = synth.make_frames(2, seed=0)
+    out['e2e_frames_seed'] = np.array([0])
+    for ms in (5, 20):
+        with torch.inference_mode():
+            res, ldm = net(list(frames), ms, return_landmarks=True)
+        out['e2e_ms%d_counts' % ms] = np.array([r.shape[0] for r in res], np.int64)
+        out['e2e_ms%d_boxes' % ms] = np.concatenate(res).astype(np.float32) if sum(r.shape[0] for r in res) else np.zeros((0, 5), np.float32)
+        out['e2e_ms%d_landmarks' % ms] = np.concatenate(ldm).astype(np.float32) if len(ldm) else np.zeros((0, 5, 2), np.float32)
+    # small frames (fast to check on CPU in the not-gpu suite)
+    small = synth.make_frames(3, 144, 256, seed=5)
+    out['small_frames'] = small
+    with torch.inference_mode():
+        res = net(list(small), 5)
+    out['small_ms5_counts'] = np.array([r.shape[0] for r in res], np.int64)
+    out['small_ms5_boxes'] = np.concatenate(res).astype(np.float32)
+    np.savez_compressed(os.path.join(HERE, 'mtcnn.npz'), **out)
+    print('mtcnn', {k: v.shape for k, v in out.items()})
+
+
+def gen_facenet():
+    load_ref()
+    f = importlib.import_module('ref_vtf.encoders.facenet')
+    net = _load(f.InceptionResnetV1('cpu'), synth.make_params('facenet'))
+    g = torch.Generator().manual_seed(11)
+    # the encoder input after cv2.dnn.blobFromImages(1/128, 160x160, 127.5, swapRB):
+    # (u8 - 127.5) / 128 of a uint8 image -> exact values
+    u8 = torch.randint(0, 256, (4, 3, 160, 160), generator=g).float()
+    x = (u8 - 127.5) * (1 / 128)
+    with torch.inference_mode():
+        y = net(x)
+    np.savez_compressed(os.path.join(HERE, 'facenet.npz'), u8=u8.to(torch.uint8).numpy(), emb=y.numpy())
+    print('facenet', y.shape, float(y.norm(dim=1).mean()))
+
+
+def gen_grouping():
+    load_ref()
+    dupes = importlib.import_module('ref_vtf.dupes')
+    grouping = importlib.import_module('ref_vtf.grouping')
+    rng = np.random.default_rng(0)
+    N, D = 600, 64
+    centers = rng.normal(0, 1, (8, D)).astype(np.float32)
+    lab = rng.integers(0, 8, N)
+    X = (centers[lab] + 1.0 * rng.normal(0, 1, (N, D))).astype(np.float32)
+    # plant near-duplicates of earlier rows
+    for i in range(20):
+        j = rng.integers(1, N)
+        k = rng.integers(0, j)
+        X[j] = X[k] + 0.01 * rng.normal(0, 1, D).astype(np.float32)
+    out = dict(X=X)
+    with tempfile.TemporaryDirectory() as td:
+        os.makedirs(os.path.join(td, 'faces'))
+        names = ['f%05d.jpg' % i for i in range(N)]
+        for n in names:
+            open(os.path.join(td, 'faces', n), 'w').close()
+        Xk, goods = dupes.remove_dupes_overall(X.copy(), names, ('enc', 0.25, False, td))
+    out['dedupe_keep'] = np.array([int(n[1:6]) for n in goods], np.int64)
+    import sklearn.metrics
+    Dm = sklearn.metrics.pairwise.cosine_distances(X)
+    Dm += (1 - np.tri(N, k=-1).astype(Dm.dtype)) * 10000
+    out['dedupe_mins'] = Dm.min(axis=1)
+    out['dedupe_inds'] = Dm.argmin(axis=1)
+    # cluster_faces internals (grouping.py:97-116): KMeans + three scores per k
+    import sklearn.cluster
+    ks = list(range(2, 10))
+    labels, scores = [], []
+    for k in ks:
+        lb = sklearn.cluster.KMeans(n_clusters=k, random_state=0, n_init='auto').fit(Xk).labels_
+        labels.append(lb)
+        scores.append((sklearn.metrics.silhouette_score(Xk, lb), sklearn.metrics.calinski_harabasz_score(Xk, lb),
+                       sklearn.metrics.davies_bouldin_score(Xk, lb)))
+    out['kmeans_k'] = np.array(ks)
+    out['kmeans_labels'] = np.stack(labels).astype(np.int32)
+    out['cluster_scores'] = np.array(scores, np.float64)
+    # classify (grouping.py:50-66)
+    R = X[[3, 50, 100]] + 0.05
+    with tempfile.TemporaryDirectory() as td:
+        inds, classes = grouping.classify(X, R, ['a', 'b', 'c'], 0.9, False, [], td)
+    out['classify_R'] = R
+    out['classify_inds'] = np.asarray(inds, np.int64)
+    np.savez_compressed(os.path.join(HERE, 'grouping.npz'), **out)
+    print('grouping', {k: v.shape for k, v in out.items()})
+
+
+if __name__ == '__main__':
+    which = sys.argv[1:] or ['mtcnn', 'facenet', 'grouping']
+    for w in which:
+        globals()['gen_' + w]()

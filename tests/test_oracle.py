@@ -1,0 +1,95 @@
+"""CPU: pin the oracle (tests' CPU restatement) against golden vectors made from the
+reference's own modules (tests/golden/make_golden.py)."""
+import os
+
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+from conftest import GOLDEN
+
+
+@pytest.fixture(scope='module')
+def g():
+    return np.load(os.path.join(GOLDEN, 'mtcnn.npz'))
+
+
+@pytest.fixture(scope='module')
+def params():
+    from videotofaces import synth
+    return synth.make_params('mtcnn')
+
+
+def test_synth_weights_deterministic():
+    from videotofaces import synth
+    a = synth.hash_uniform('mtcnn:pnet.conv1.weight', 10)
+    assert a.dtype == np.float32 and a.min() >= -1 and a.max() < 1
+    np.testing.assert_array_equal(a, synth.hash_uniform('mtcnn:pnet.conv1.weight', 10))
+    assert synth.pack(synth.make_params('mtcnn')).size == 495850
+
+
+def test_oracle_nets_vs_golden(g, params):
+    from oracle import mtcnn as om
+    with torch.inference_mode():
+        reg, prob = om.pnet(params, torch.from_numpy(g['pnet_in']))
+        np.testing.assert_array_equal(reg.numpy(), g['pnet_reg'])
+        np.testing.assert_array_equal(prob.numpy(), g['pnet_prob'])
+        reg, prob = om.rnet(params, torch.from_numpy(g['rnet_in']))
+        np.testing.assert_array_equal(reg.numpy(), g['rnet_reg'])
+        np.testing.assert_array_equal(prob.numpy(), g['rnet_prob'])
+        reg, lm, prob = om.onet(params, torch.from_numpy(g['onet_in']))
+        np.testing.assert_array_equal(prob.numpy(), g['onet_prob'])
+        np.testing.assert_array_equal(lm.numpy(), g['onet_lm'])
+
+
+def test_oracle_pyramid_vs_golden(g):
+    from oracle import mtcnn as om
+    x = om.preprocess(list(g['pyr_frame']))
+    scales, sizes = om.scale_pyramid(90, 160, 5)
+    assert [tuple(s) for s in g['pyr_sizes']] == sizes[:4]
+    for i, sz in enumerate(sizes[:4]):
+        np.testing.assert_array_equal(F.adaptive_avg_pool2d(x, sz).numpy(), g['pyr_level%d' % i])
+
+
+def test_oracle_adaptive_pool_restatement_bit_exact():
+    # the kernel's bin-average rule: fp32 row-major sum, then /kh, then /kw
+    rng = np.random.default_rng(0)
+    u8 = rng.integers(0, 256, (1, 3, 37, 53)).astype(np.float32)
+    x = torch.from_numpy((u8 - 127.5) / 128)
+    for (oh, ow) in [(23, 31), (89, 120), (37, 53), (5, 7)]:
+        ref = F.adaptive_avg_pool2d(x, (oh, ow))[0, 1].numpy()
+        H, W = 37, 53
+        for y in range(oh):
+            y0, y1 = (y * H) // oh, -((-(y + 1) * H) // oh)
+            for xx in range(ow):
+                x0, x1 = (xx * W) // ow, -((-(xx + 1) * W) // ow)
+                s = np.float32(0)
+                for a in range(y0, y1):
+                    for b in range(x0, x1):
+                        s = np.float32(s + x[0, 1, a, b].numpy())
+                v = np.float32(np.float32(s / np.float32(y1 - y0)) / np.float32(x1 - x0))
+                assert v == ref[y, xx]
+
+
+def test_oracle_e2e_small_frames_vs_golden(g, params):
+    from oracle import mtcnn as om
+    res = om.forward(params, list(g['small_frames']), minsize=5)
+    k = 0
+    for r, c in zip(res, g['small_ms5_counts']):
+        np.testing.assert_array_equal(r, g['small_ms5_boxes'][k:k + c])
+        k += c
+
+
+def test_oracle_nms_c_core_vs_pure_torch():
+    import sys
+    sys.path.insert(0, GOLDEN)
+    from oracle import nms as onms
+    from make_golden import _tv_batched_nms
+    rng = np.random.default_rng(1)
+    for n, nimg in [(50, 2), (999, 3), (1200, 5)]:
+        xy = rng.integers(0, 100, (n, 2)).astype(np.float32)
+        b = torch.from_numpy(np.concatenate([xy, xy + rng.integers(3, 30, (n, 2))], 1).astype(np.float32))
+        s = torch.from_numpy(rng.uniform(0, 1, n).astype(np.float32))
+        i = torch.from_numpy(rng.integers(0, nimg, n))
+        assert onms.batched_nms(b, s, i, 0.5).tolist() == _tv_batched_nms(b, s, i, 0.5).tolist()

@@ -1,0 +1,72 @@
+// C-ABI glue: error state, version, standalone box ops (include/vtf.h).
+#include <mutex>
+#include <string>
+
+#include "common.hpp"
+#include "nms.hpp"
+
+namespace vtf {
+
+static thread_local std::string g_err;
+void set_error(const std::string& msg) { g_err = msg; }
+
+__global__ void k_i64_to_i32(const int64_t* in, int64_t n, int32_t* out) {
+    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) out[i] = (int32_t)in[i];
+}
+__global__ void k_i32_to_i64(const int32_t* in, int64_t n, int64_t* out) {
+    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) out[i] = (int64_t)in[i];
+}
+
+static Arena& standalone_arena() {
+    static Arena a;
+    return a;
+}
+static std::mutex g_standalone_mu;
+
+}  // namespace vtf
+
+using namespace vtf;
+
+extern "C" {
+
+const char* vtf_last_error(void) { return g_err.c_str(); }
+
+int vtf_version(void) { return 1; }
+
+int vtf_batched_nms(const float* d_boxes, const float* d_scores, const int64_t* d_idxs, int64_t n,
+                    double iou_threshold, int64_t* d_keep, int64_t* out_nkeep, void* hip_stream) {
+    return guarded([&] {
+        VTF_CHECK(out_nkeep && n >= 0, VTF_E_ARG, "bad argument");
+        *out_nkeep = 0;
+        if (n == 0) return;
+        VTF_CHECK(d_boxes && d_scores && d_idxs && d_keep, VTF_E_ARG, "null argument");
+        std::lock_guard<std::mutex> lk(g_standalone_mu);
+        hipStream_t st = (hipStream_t)hip_stream;
+        Arena& ar = standalone_arena();
+        int32_t* img = ar.get<int32_t>(0, n);
+        int32_t* call = ar.get<int32_t>(1, n);
+        int32_t* keep = ar.get<int32_t>(2, n);
+        k_i64_to_i32<<<cdiv(n, 256), 256, 0, st>>>(d_idxs, n, img);
+        VTF_HIP(hipMemsetAsync(call, 0, n * 4, st));
+        // number of distinct class ids bounds the vanilla segment count: use max id + 1
+        int32_t mx = 0;
+        {
+            std::vector<int32_t> h(n);
+            VTF_HIP(hipMemcpyAsync(h.data(), img, n * 4, hipMemcpyDeviceToHost, st));
+            VTF_HIP(hipStreamSynchronize(st));
+            for (int32_t v : h) {
+                VTF_CHECK(v >= 0, VTF_E_ARG, "batched_nms: negative class ids are not supported");
+                mx = v > mx ? v : mx;
+            }
+        }
+        std::vector<int64_t> nk;
+        nms_multi(ar, d_boxes, d_scores, img, call, {n}, mx + 1, iou_threshold, keep, nk, st);
+        k_i32_to_i64<<<cdiv(nk[0] > 0 ? nk[0] : 1, 256), 256, 0, st>>>(keep, nk[0], d_keep);
+        VTF_HIP(hipStreamSynchronize(st));
+        *out_nkeep = nk[0];
+    });
+}
+
+}  // extern "C"

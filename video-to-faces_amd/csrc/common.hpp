@@ -1,0 +1,88 @@
+// Shared runtime pieces of libvtf_hip.so: error state, HIP checks, a grow-only device
+// arena per handle.  Compiled for gfx950 only.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstdio>
+#include <string>
+#include <vector>
+
+#include "../../include/vtf.h"
+
+namespace vtf {
+
+void set_error(const std::string& msg);
+
+struct Error {
+    int code;
+    std::string msg;
+};
+
+#define VTF_HIP(expr)                                                                      \
+    do {                                                                                   \
+        hipError_t _e = (expr);                                                            \
+        if (_e != hipSuccess)                                                              \
+            throw ::vtf::Error{VTF_E_HIP, std::string(#expr) + ": " + hipGetErrorString(_e)}; \
+    } while (0)
+
+#define VTF_CHECK(cond, code, msg)                                                         \
+    do {                                                                                   \
+        if (!(cond)) throw ::vtf::Error{(code), (msg)};                                    \
+    } while (0)
+
+// Catch-all wrapper for C entry points.
+template <class F>
+int guarded(F&& f) {
+    try {
+        f();
+        return VTF_OK;
+    } catch (const Error& e) {
+        set_error(e.msg);
+        return e.code;
+    } catch (const std::exception& e) {
+        set_error(e.what());
+        return VTF_E_ARG;
+    }
+}
+
+// Named grow-only device buffers: get(slot, bytes) returns a pointer valid until the next
+// get() of the same slot with a larger size.  Sized for 288 GB HBM: no pooling games.
+struct Arena {
+    std::vector<void*> ptr;
+    std::vector<size_t> cap;
+    ~Arena() {
+        for (void* p : ptr)
+            if (p) (void)hipFree(p);
+    }
+    void* get(int slot, size_t bytes) {
+        if ((int)ptr.size() <= slot) {
+            ptr.resize(slot + 1, nullptr);
+            cap.resize(slot + 1, 0);
+        }
+        if (bytes == 0) bytes = 16;
+        if (cap[slot] < bytes) {
+            if (ptr[slot]) VTF_HIP(hipFree(ptr[slot]));
+            size_t b = bytes + bytes / 4;
+            VTF_HIP(hipMalloc(&ptr[slot], b));
+            cap[slot] = b;
+        }
+        return ptr[slot];
+    }
+    template <class T>
+    T* get(int slot, size_t n) {
+        return reinterpret_cast<T*>(get(slot, n * sizeof(T)));
+    }
+};
+
+inline int cdiv(int64_t a, int64_t b) { return (int)((a + b - 1) / b); }
+
+// Sortable descending key of a float: larger float -> smaller key (NaN-free inputs).
+__host__ __device__ inline uint32_t desc_key(float f) {
+    uint32_t u = __float_as_uint(f);
+    uint32_t asc = (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+    return ~asc;
+}
+
+}  // namespace vtf

@@ -1,0 +1,64 @@
+#pragma once
+#include "common.hpp"
+
+namespace vtf {
+
+struct PNetLevel {
+    int lh, lw;       // level size (int(H*s+1), int(W*s+1)), mtcnn.py:147
+    int ph, pw;       // PNet output size
+    float scale;      // fp32(s)
+    int tiles_x, tiles_y;
+    int pad;
+    int64_t tile_beg; // first workgroup of this level
+};
+
+// All conv weights transposed to [ci][ky][kx][co]; dense weights to [k][out] where noted.
+struct PNetW {
+    const float *c1w, *c1b, *p1, *c2w, *c2b, *p2, *c3w, *c3b, *p3, *c41w, *c41b, *c42w, *c42b;
+};
+struct PNetOut {
+    // sparse (candidate) mode
+    uint32_t* count;
+    uint32_t* level_count;
+    uint32_t cap;
+    uint64_t* key;
+    float* score;
+    float4* regv;
+    // dense (parity) mode
+    float* prob;
+    float* reg;
+};
+struct RNetW {
+    const float *c1w, *c1b, *p1, *c2w, *c2b, *p2, *c3w, *c3b, *p3, *d4w, *d4b, *p4, *d51w, *d51b, *d52w, *d52b;
+};
+struct ONetW {
+    const float *c1w, *c1b, *p1, *c2w, *c2b, *p2, *c3w, *c3b, *p3, *c4w, *c4b, *p4, *d5w, *d5b, *p5, *d61w, *d61b,
+        *d62w, *d62b, *d63w, *d63b;
+};
+
+void launch_resample(const uint8_t* frames, int64_t frame_stride, int64_t row_stride, int B, int H, int W, int lh,
+                     int lw, float* out, hipStream_t st);
+void launch_pnet(bool dense, const uint8_t* frames, int64_t frame_stride, int64_t row_stride, int H, int W,
+                 const PNetLevel* d_levels, int n_levels, int64_t total_tiles, const PNetW& w, const PNetOut& o,
+                 hipStream_t st);
+void launch_rnet(const uint8_t* frames, int64_t frame_stride, int64_t row_stride, int H, int W, const float4* boxes,
+                 const int32_t* img, const float* xin, int64_t n, const RNetW& w, float4* reg, float* prob,
+                 int32_t* err, hipStream_t st);
+void launch_onet(const uint8_t* frames, int64_t frame_stride, int64_t row_stride, int H, int W, const float4* boxes,
+                 const int32_t* img, const float* xin, int64_t n, const ONetW& w, float4* reg, float* lm, float* prob,
+                 int32_t* err, hipStream_t st);
+void launch_decode_stage1(const uint64_t* key_sorted, const int32_t* slot_sorted, const float* score,
+                          const float4* regv, const PNetLevel* lv, int64_t n, float4* boxes, float* sc, float4* reg,
+                          int32_t* img, int32_t* call, hipStream_t st);
+void launch_gather_refine(const int32_t* idx, int64_t n, const float4* bin, const float* sin, const float4* rin,
+                          const int32_t* iin, int refine, int plus_one, int square, float4* bout, float* sout,
+                          float4* rout, int32_t* iout, hipStream_t st);
+void launch_threshold(const float* s, int64_t n, float thr, int32_t* flag, hipStream_t st);
+void launch_flag_compact(const int32_t* flag, const int32_t* incl, int64_t n, int32_t* out, hipStream_t st);
+void launch_landmarks(const float4* boxes, const float* lm, int64_t n, float* out, hipStream_t st);
+void launch_iom_chain(const float4* boxes, const int32_t* img, const int32_t* order, int64_t n, float thr,
+                      int32_t* keep, hipStream_t st);
+
+constexpr int PNET_TH = 16, PNET_TW = 32;
+
+}  // namespace vtf

@@ -1,0 +1,801 @@
+// MTCNN kernels for gfx950 (fp32; parity with the reference PyTorch-CPU path).
+//
+// Reference: src/videotofaces/detectors/mtcnn.py
+//   _preprocess 133-139, _resample 150-151, PNet 12-38, stage-1 candidates 183-194,
+//   _get_cropped_candidates 153-163, RNet 41-76, ONet 79-121.
+//
+// MI355X design:
+//   * k_pnet: ONE launch per det-batch covers every pyramid level of every frame.  Each
+//     256-thread workgroup owns a 16x32 tile of PNet output cells.  The level pixels it
+//     needs (42x74x3) are computed on the fly from the uint8 BGR frame (preprocess +
+//     adaptive_avg_pool2d, bit-exact: exact (u-127.5)/128, row-major fp32 bin sum, /kh, /kw)
+//     straight into LDS, so the 10.7 Mpx/frame pyramid never exists in HBM.  conv1+PReLU+
+//     maxpool(ceil), conv2+PReLU, conv3+PReLU and both 1x1 heads + softmax run from LDS with
+//     weights streamed through the scalar cache (wave-uniform, transposed to [ci][ky][kx][co]
+//     on the host so one s_load_dwordx16 feeds 16 v_fma).  Cells with p >= 0.6 are appended
+//     with one wave-aggregated atomic -- the dense prob/reg maps are never written.
+//   * k_rnet / k_onet: one workgroup per candidate box; the crop + adaptive pool to 24x24 /
+//     48x48 (replacing the reference's per-box Python loop) feeds the whole network in LDS.
+// Build with -ffp-contract=off: only explicit fmaf() fuses.
+#include "common.hpp"
+#include "mtcnn.hpp"
+
+namespace vtf {
+
+// ----------------------------------------------------------------------------------- helpers
+
+// Level pixel (RGB channel c) of MTCNN._resample(_preprocess(frames)), from uint8 BGR.
+__device__ inline float level_value(const uint8_t* __restrict__ fr, int64_t row_stride, int c, int ly, int lx,
+                                    int H, int W, int lh, int lw) {
+    int y0 = (int)(((int64_t)ly * H) / lh);
+    int y1 = (int)(((int64_t)(ly + 1) * H + lh - 1) / lh);
+    int x0 = (int)(((int64_t)lx * W) / lw);
+    int x1 = (int)(((int64_t)(lx + 1) * W + lw - 1) / lw);
+    const uint8_t* p = fr + (2 - c);
+    float s = 0.f;
+    for (int y = y0; y < y1; y++) {
+        const uint8_t* r = p + (int64_t)y * row_stride;
+        for (int x = x0; x < x1; x++) s = s + ((float)r[x * 3] - 127.5f) * 0.0078125f;
+    }
+    return __fdiv_rn(__fdiv_rn(s, (float)(y1 - y0)), (float)(x1 - x0));
+}
+
+// Crop [y0, y0+hc) x [x0, x0+wc) of the preprocessed frame adaptive-pooled to S x S.
+__device__ inline float crop_value(const uint8_t* __restrict__ fr, int64_t row_stride, int c, int r, int q,
+                                   int y0c, int x0c, int hc, int wc, int S) {
+    int ys = (r * hc) / S, ye = ((r + 1) * hc + S - 1) / S;
+    int xs = (q * wc) / S, xe = ((q + 1) * wc + S - 1) / S;
+    const uint8_t* p = fr + (2 - c);
+    float s = 0.f;
+    for (int y = ys; y < ye; y++) {
+        const uint8_t* row = p + (int64_t)(y0c + y) * row_stride;
+        for (int x = xs; x < xe; x++) s = s + ((float)row[(x0c + x) * 3] - 127.5f) * 0.0078125f;
+    }
+    return __fdiv_rn(__fdiv_rn(s, (float)(ye - ys)), (float)(xe - xs));
+}
+
+__device__ inline float prelu(float x, float a) { return x > 0.f ? x : a * x; }
+
+// Python int() of a float, saturated (values beyond +-2e9 only matter through clamping).
+__device__ inline int trunc_sat(float v) {
+    v = fminf(fmaxf(v, -2.0e9f), 2.0e9f);
+    return (int)v;
+}
+
+// _get_cropped_candidates box -> crop rect; false if the reference would skip the box.
+__device__ inline bool crop_rect(float4 b, int H, int W, int& y0, int& x0, int& hc, int& wc) {
+    int ix1 = max(1, trunc_sat(b.x)), iy1 = max(1, trunc_sat(b.y));
+    int ix2 = min(W, trunc_sat(b.z)), iy2 = min(H, trunc_sat(b.w));
+    if (!(iy2 > iy1 - 1 && ix2 > ix1 - 1)) return false;
+    y0 = iy1 - 1;
+    x0 = ix1 - 1;
+    hc = iy2 - y0;
+    wc = ix2 - x0;
+    return true;
+}
+
+// ----------------------------------------------------------------------------------- resample
+
+__global__ void k_resample(const uint8_t* __restrict__ frames, int64_t frame_stride, int64_t row_stride, int B,
+                           int H, int W, int lh, int lw, float* __restrict__ out) {
+    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    int64_t n = (int64_t)B * 3 * lh * lw;
+    if (i >= n) return;
+    int lx = (int)(i % lw);
+    int ly = (int)((i / lw) % lh);
+    int c = (int)((i / ((int64_t)lw * lh)) % 3);
+    int b = (int)(i / ((int64_t)lw * lh * 3));
+    out[i] = level_value(frames + (int64_t)b * frame_stride, row_stride, c, ly, lx, H, W, lh, lw);
+}
+
+void launch_resample(const uint8_t* frames, int64_t frame_stride, int64_t row_stride, int B, int H, int W, int lh,
+                     int lw, float* out, hipStream_t st) {
+    int64_t n = (int64_t)B * 3 * lh * lw;
+    k_resample<<<cdiv(n, 256), 256, 0, st>>>(frames, frame_stride, row_stride, B, H, W, lh, lw, out);
+}
+
+// ----------------------------------------------------------------------------------- PNet
+
+constexpr int PT_H = 16, PT_W = 32;                   // output cells per tile
+constexpr int PL_H = 2 * PT_H + 10, PL_W = 2 * PT_W + 10;  // level tile 42 x 74
+constexpr int PP_H = PT_H + 4, PP_W = PT_W + 4;       // pooled 20 x 36
+constexpr int PC_H = PT_H + 2, PC_W = PT_W + 2;       // conv2 out 18 x 34
+constexpr int P_LVL = 3 * PL_H * PL_W;                // 9324
+constexpr int P_C2 = 16 * PC_H * PC_W;                // 9792
+constexpr int P_POOL = 10 * PP_H * PP_W;              // 7200
+constexpr int P_A = P_C2 > P_LVL ? P_C2 : P_LVL;
+
+template <bool DENSE>
+__global__ __launch_bounds__(256) void k_pnet(const uint8_t* __restrict__ frames, int64_t frame_stride,
+                                              int64_t row_stride, int H, int W, const PNetLevel* __restrict__ lv,
+                                              int n_levels, PNetW w, PNetOut o) {
+    __shared__ float sA[P_A];     // level tile, later conv2 output
+    __shared__ float sP[P_POOL];  // pooled conv1
+    const int tid = threadIdx.x;
+    // locate (level, frame, tile)
+    int64_t blk = blockIdx.x;
+    int L = 0;
+    while (L + 1 < n_levels && blk >= lv[L + 1].tile_beg) L++;
+    const PNetLevel P = lv[L];
+    int64_t t = blk - P.tile_beg;
+    const int tiles_per_img = P.tiles_x * P.tiles_y;
+    const int b = (int)(t / tiles_per_img);
+    const int tt = (int)(t % tiles_per_img);
+    const int oy0 = (tt / P.tiles_x) * PT_H, ox0 = (tt % P.tiles_x) * PT_W;
+    const uint8_t* fr = frames + (int64_t)b * frame_stride;
+    const int L1h = P.lh - 2, L1w = P.lw - 2;
+
+    // 1. level tile (rows 2*oy0 .. +42, cols 2*ox0 .. +74), zero outside the level
+    for (int i = tid; i < P_LVL; i += 256) {
+        int c = i / (PL_H * PL_W);
+        int r = (i / PL_W) % PL_H;
+        int q = i % PL_W;
+        int ly = 2 * oy0 + r, lx = 2 * ox0 + q;
+        float v = 0.f;
+        if (ly < P.lh && lx < P.lw) v = level_value(fr, row_stride, c, ly, lx, H, W, P.lh, P.lw);
+        sA[i] = v;
+    }
+    __syncthreads();
+
+    // 2. conv1 (3->10, 3x3) + PReLU + maxpool 2x2 ceil -> sP[10][20][36]
+    for (int i = tid; i < PP_H * PP_W; i += 256) {
+        int py = i / PP_W, px = i % PP_W;
+        float in[3][4][4];
+#pragma unroll
+        for (int c = 0; c < 3; c++)
+#pragma unroll
+            for (int dy = 0; dy < 4; dy++)
+#pragma unroll
+                for (int dx = 0; dx < 4; dx++) in[c][dy][dx] = sA[(c * PL_H + 2 * py + dy) * PL_W + 2 * px + dx];
+        float acc[4][10];
+#pragma unroll
+        for (int k = 0; k < 4; k++)
+#pragma unroll
+            for (int co = 0; co < 10; co++) acc[k][co] = w.c1b[co];
+#pragma unroll
+        for (int c = 0; c < 3; c++)
+#pragma unroll
+            for (int ky = 0; ky < 3; ky++)
+#pragma unroll
+                for (int kx = 0; kx < 3; kx++)
+#pragma unroll
+                    for (int co = 0; co < 10; co++) {
+                        float wv = w.c1w[((c * 3 + ky) * 3 + kx) * 10 + co];
+#pragma unroll
+                        for (int k = 0; k < 4; k++) acc[k][co] = fmaf(in[c][ky + (k >> 1)][kx + (k & 1)], wv, acc[k][co]);
+                    }
+        const int gy = 2 * (oy0 + py), gx = 2 * (ox0 + px);
+#pragma unroll
+        for (int co = 0; co < 10; co++) {
+            float m = -3.402823466e38f;
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                bool ok = (gy + (k >> 1) < L1h) && (gx + (k & 1) < L1w);
+                float v = prelu(acc[k][co], w.p1[co]);
+                if (ok) m = fmaxf(m, v);
+            }
+            sP[(co * PP_H + py) * PP_W + px] = m;
+        }
+    }
+    __syncthreads();
+
+    // 3. conv2 (10->16, 3x3) + PReLU -> sA[16][18][34]
+    for (int i = tid; i < PC_H * PC_W; i += 256) {
+        int y = i / PC_W, x = i % PC_W;
+        float acc[16];
+#pragma unroll
+        for (int co = 0; co < 16; co++) acc[co] = w.c2b[co];
+        for (int c = 0; c < 10; c++) {
+#pragma unroll
+            for (int ky = 0; ky < 3; ky++)
+#pragma unroll
+                for (int kx = 0; kx < 3; kx++) {
+                    float v = sP[(c * PP_H + y + ky) * PP_W + x + kx];
+                    const float* wp = w.c2w + ((c * 3 + ky) * 3 + kx) * 16;
+#pragma unroll
+                    for (int co = 0; co < 16; co++) acc[co] = fmaf(v, wp[co], acc[co]);
+                }
+        }
+#pragma unroll
+        for (int co = 0; co < 16; co++) sA[(co * PC_H + y) * PC_W + x] = prelu(acc[co], w.p2[co]);
+    }
+    __syncthreads();
+
+    // 4. conv3 (16->32, 3x3) + PReLU, heads 1x1 (32->2 softmax, 32->4)
+    for (int i = tid; i < PT_H * PT_W; i += 256) {
+        int y = i / PT_W, x = i % PT_W;
+        float acc[32];
+#pragma unroll
+        for (int co = 0; co < 32; co++) acc[co] = w.c3b[co];
+        for (int c = 0; c < 16; c++) {
+#pragma unroll
+            for (int ky = 0; ky < 3; ky++)
+#pragma unroll
+                for (int kx = 0; kx < 3; kx++) {
+                    float v = sA[(c * PC_H + y + ky) * PC_W + x + kx];
+                    const float* wp = w.c3w + ((c * 3 + ky) * 3 + kx) * 32;
+#pragma unroll
+                    for (int co = 0; co < 32; co++) acc[co] = fmaf(v, wp[co], acc[co]);
+                }
+        }
+        float a0 = w.c41b[0], a1 = w.c41b[1];
+        float r0 = w.c42b[0], r1 = w.c42b[1], r2 = w.c42b[2], r3 = w.c42b[3];
+#pragma unroll
+        for (int k = 0; k < 32; k++) {
+            float f = prelu(acc[k], w.p3[k]);
+            a0 = fmaf(f, w.c41w[k], a0);
+            a1 = fmaf(f, w.c41w[32 + k], a1);
+            r0 = fmaf(f, w.c42w[k], r0);
+            r1 = fmaf(f, w.c42w[32 + k], r1);
+            r2 = fmaf(f, w.c42w[64 + k], r2);
+            r3 = fmaf(f, w.c42w[96 + k], r3);
+        }
+        float mx = fmaxf(a0, a1);
+        float e0 = expf(a0 - mx), e1 = expf(a1 - mx);
+        float prob = __fdiv_rn(e1, e0 + e1);
+        const int oy = oy0 + y, ox = ox0 + x;
+        const bool valid = (oy < P.ph) && (ox < P.pw);
+        if (DENSE) {
+            if (valid) {
+                int64_t plane = (int64_t)P.ph * P.pw;
+                int64_t cell = (int64_t)oy * P.pw + ox;
+                o.prob[(int64_t)b * plane + cell] = prob;
+                float* rg = o.reg + (int64_t)b * 4 * plane + cell;
+                rg[0] = r0;
+                rg[plane] = r1;
+                rg[2 * plane] = r2;
+                rg[3 * plane] = r3;
+            }
+        } else {
+            // mask = prob >= 0.6 (mtcnn.py:183; the python scalar compares as fp32)
+            bool pass = valid && (prob >= 0.6f);
+            uint64_t bal = __ballot(pass);
+            if (bal) {
+                int lane = __lane_id();
+                int leader = __builtin_ctzll(bal);
+                uint32_t base = 0;
+                if (lane == leader) base = atomicAdd(o.count, (uint32_t)__popcll(bal));
+                base = __shfl(base, leader);
+                if (pass) {
+                    uint32_t slot = base + (uint32_t)__popcll(bal & ((1ull << lane) - 1ull));
+                    if (slot < o.cap) {
+                        uint32_t lin = (uint32_t)(((int64_t)b * P.ph + oy) * P.pw + ox);
+                        o.key[slot] = ((uint64_t)L << 32) | lin;
+                        o.score[slot] = prob;
+                        o.regv[slot] = make_float4(r0, r1, r2, r3);
+                    }
+                    atomicAdd(&o.level_count[L], 1u);
+                }
+            }
+        }
+    }
+}
+
+void launch_pnet(bool dense, const uint8_t* frames, int64_t frame_stride, int64_t row_stride, int H, int W,
+                 const PNetLevel* d_levels, int n_levels, int64_t total_tiles, const PNetW& w, const PNetOut& o,
+                 hipStream_t st) {
+    if (total_tiles <= 0) return;
+    if (dense)
+        k_pnet<true><<<(unsigned)total_tiles, 256, 0, st>>>(frames, frame_stride, row_stride, H, W, d_levels, n_levels,
+                                                             w, o);
+    else
+        k_pnet<false><<<(unsigned)total_tiles, 256, 0, st>>>(frames, frame_stride, row_stride, H, W, d_levels,
+                                                              n_levels, w, o);
+}
+
+// ----------------------------------------------------------------------------------- RNet
+
+// LDS plan (floats): A 13552 = conv1 [28][22][22]; later conv2 [48][9][9] @0, pool2 [48][4][4]
+// @3888, flat [576] @4656, dense4 [128] @5232.  B 3388 = pool1 [28][11][11].  C 1728 = input.
+template <bool FROM_FRAMES>
+__global__ __launch_bounds__(256) void k_rnet(const uint8_t* __restrict__ frames, int64_t frame_stride,
+                                              int64_t row_stride, int H, int W, const float4* __restrict__ boxes,
+                                              const int32_t* __restrict__ img, const float* __restrict__ xin,
+                                              RNetW w, float4* __restrict__ reg_out, float* __restrict__ prob_out,
+                                              int32_t* __restrict__ err) {
+    __shared__ float sA[13552];
+    __shared__ float sB[3388];
+    __shared__ float sC[1728];
+    const int tid = threadIdx.x;
+    const int64_t n = blockIdx.x;
+    if (FROM_FRAMES) {
+        int y0, x0, hc, wc;
+        if (!crop_rect(boxes[n], H, W, y0, x0, hc, wc)) {
+            if (tid == 0) atomicAdd(err, 1);
+            return;
+        }
+        const uint8_t* fr = frames + (int64_t)img[n] * frame_stride;
+        for (int i = tid; i < 1728; i += 256) {
+            int c = i / 576, r = (i / 24) % 24, q = i % 24;
+            sC[i] = crop_value(fr, row_stride, c, r, q, y0, x0, hc, wc, 24);
+        }
+    } else {
+        for (int i = tid; i < 1728; i += 256) sC[i] = xin[n * 1728 + i];
+    }
+    __syncthreads();
+    // conv1 3->28 3x3: 22x22
+    for (int i = tid; i < 484; i += 256) {
+        int y = i / 22, x = i % 22;
+        float acc[28];
+#pragma unroll
+        for (int co = 0; co < 28; co++) acc[co] = w.c1b[co];
+#pragma unroll
+        for (int c = 0; c < 3; c++)
+#pragma unroll
+            for (int ky = 0; ky < 3; ky++)
+#pragma unroll
+                for (int kx = 0; kx < 3; kx++) {
+                    float v = sC[(c * 24 + y + ky) * 24 + x + kx];
+                    const float* wp = w.c1w + ((c * 3 + ky) * 3 + kx) * 28;
+#pragma unroll
+                    for (int co = 0; co < 28; co++) acc[co] = fmaf(v, wp[co], acc[co]);
+                }
+#pragma unroll
+        for (int co = 0; co < 28; co++) sA[co * 484 + i] = prelu(acc[co], w.p1[co]);
+    }
+    __syncthreads();
+    // maxpool 3/2 ceil: 22 -> 11
+    for (int i = tid; i < 3388; i += 256) {
+        int c = i / 121, y = (i / 11) % 11, x = i % 11;
+        float m = -3.402823466e38f;
+        for (int dy = 0; dy < 3; dy++)
+            for (int dx = 0; dx < 3; dx++) {
+                int yy = 2 * y + dy, xx = 2 * x + dx;
+                if (yy < 22 && xx < 22) m = fmaxf(m, sA[c * 484 + yy * 22 + xx]);
+            }
+        sB[i] = m;
+    }
+    __syncthreads();
+    // conv2 28->48 3x3: 9x9; item = (pos, 16-channel group)
+    for (int i = tid; i < 81 * 3; i += 256) {
+        int pos = i % 81, g = i / 81;
+        int y = pos / 9, x = pos % 9;
+        float acc[16];
+#pragma unroll
+        for (int k = 0; k < 16; k++) acc[k] = w.c2b[g * 16 + k];
+        for (int c = 0; c < 28; c++) {
+#pragma unroll
+            for (int ky = 0; ky < 3; ky++)
+#pragma unroll
+                for (int kx = 0; kx < 3; kx++) {
+                    float v = sB[c * 121 + (y + ky) * 11 + x + kx];
+                    const float* wp = w.c2w + ((c * 3 + ky) * 3 + kx) * 48 + g * 16;
+#pragma unroll
+                    for (int k = 0; k < 16; k++) acc[k] = fmaf(v, wp[k], acc[k]);
+                }
+        }
+#pragma unroll
+        for (int k = 0; k < 16; k++) sA[(g * 16 + k) * 81 + pos] = prelu(acc[k], w.p2[g * 16 + k]);
+    }
+    __syncthreads();
+    // maxpool 3/2 ceil: 9 -> 4
+    for (int i = tid; i < 768; i += 256) {
+        int c = i / 16, y = (i / 4) % 4, x = i % 4;
+        float m = -3.402823466e38f;
+        for (int dy = 0; dy < 3; dy++)
+            for (int dx = 0; dx < 3; dx++) {
+                int yy = 2 * y + dy, xx = 2 * x + dx;
+                if (yy < 9 && xx < 9) m = fmaxf(m, sA[c * 81 + yy * 9 + xx]);
+            }
+        sA[3888 + i] = m;
+    }
+    __syncthreads();
+    // conv3 48->64 2x2: 3x3 -> flat (permute 0,3,2,1: index = x*192 + y*64 + c)
+    for (int i = tid; i < 9 * 8; i += 256) {
+        int pos = i % 9, g = i / 9;
+        int y = pos / 3, x = pos % 3;
+        float acc[8];
+#pragma unroll
+        for (int k = 0; k < 8; k++) acc[k] = w.c3b[g * 8 + k];
+        for (int c = 0; c < 48; c++) {
+#pragma unroll
+            for (int ky = 0; ky < 2; ky++)
+#pragma unroll
+                for (int kx = 0; kx < 2; kx++) {
+                    float v = sA[3888 + c * 16 + (y + ky) * 4 + x + kx];
+                    const float* wp = w.c3w + ((c * 2 + ky) * 2 + kx) * 64 + g * 8;
+#pragma unroll
+                    for (int k = 0; k < 8; k++) acc[k] = fmaf(v, wp[k], acc[k]);
+                }
+        }
+#pragma unroll
+        for (int k = 0; k < 8; k++) sA[4656 + x * 192 + y * 64 + g * 8 + k] = prelu(acc[k], w.p3[g * 8 + k]);
+    }
+    __syncthreads();
+    // dense4 576->128 + PReLU; weights transposed [k][128]
+    if (tid < 128) {
+        float acc = w.d4b[tid];
+        for (int k = 0; k < 576; k++) acc = fmaf(sA[4656 + k], w.d4w[k * 128 + tid], acc);
+        sA[5232 + tid] = prelu(acc, w.p4[tid]);
+    }
+    __syncthreads();
+    if (tid < 64) {
+        // heads: dense5_1 (2) softmax, dense5_2 (4); wave reduction over 128 inputs
+        float part[6];
+#pragma unroll
+        for (int j = 0; j < 6; j++) part[j] = 0.f;
+        for (int k = tid; k < 128; k += 64) {
+            float f = sA[5232 + k];
+            part[0] = fmaf(f, w.d51w[k], part[0]);
+            part[1] = fmaf(f, w.d51w[128 + k], part[1]);
+#pragma unroll
+            for (int j = 0; j < 4; j++) part[2 + j] = fmaf(f, w.d52w[j * 128 + k], part[2 + j]);
+        }
+#pragma unroll
+        for (int j = 0; j < 6; j++)
+            for (int off = 32; off > 0; off >>= 1) part[j] += __shfl_xor(part[j], off);
+        if (tid == 0) {
+            float a0 = part[0] + w.d51b[0], a1 = part[1] + w.d51b[1];
+            float mx = fmaxf(a0, a1);
+            float e0 = expf(a0 - mx), e1 = expf(a1 - mx);
+            prob_out[n] = e1 * __fdiv_rn(1.0f, e0 + e1);
+            reg_out[n] = make_float4(part[2] + w.d52b[0], part[3] + w.d52b[1], part[4] + w.d52b[2], part[5] + w.d52b[3]);
+        }
+    }
+}
+
+void launch_rnet(const uint8_t* frames, int64_t frame_stride, int64_t row_stride, int H, int W, const float4* boxes,
+                 const int32_t* img, const float* xin, int64_t n, const RNetW& w, float4* reg, float* prob,
+                 int32_t* err, hipStream_t st) {
+    if (n <= 0) return;
+    if (xin)
+        k_rnet<false><<<(unsigned)n, 256, 0, st>>>(frames, frame_stride, row_stride, H, W, boxes, img, xin, w, reg,
+                                                    prob, err);
+    else
+        k_rnet<true><<<(unsigned)n, 256, 0, st>>>(frames, frame_stride, row_stride, H, W, boxes, img, xin, w, reg,
+                                                   prob, err);
+}
+
+// ----------------------------------------------------------------------------------- ONet
+
+// LDS plan (floats): X 14112 = input [3][48][48] (6912) / conv2 half [32][21][21] (14112) /
+// later conv3 [64][8][8] @0 (4096), pool3 [64][4][4] @4096 (1024), conv4 flat [1152] @5120,
+// dense5 [256] @6272.  Y 16928 = pool1 [32][23][23].  Z 6400 = pool2 [64][10][10].
+template <bool FROM_FRAMES>
+__global__ __launch_bounds__(512) void k_onet(const uint8_t* __restrict__ frames, int64_t frame_stride,
+                                              int64_t row_stride, int H, int W, const float4* __restrict__ boxes,
+                                              const int32_t* __restrict__ img, const float* __restrict__ xin,
+                                              ONetW w, float4* __restrict__ reg_out, float* __restrict__ lm_out,
+                                              float* __restrict__ prob_out, int32_t* __restrict__ err) {
+    __shared__ float sX[14112];
+    __shared__ float sY[16928];
+    __shared__ float sZ[6400];
+    const int tid = threadIdx.x;
+    const int64_t n = blockIdx.x;
+    if (FROM_FRAMES) {
+        int y0, x0, hc, wc;
+        if (!crop_rect(boxes[n], H, W, y0, x0, hc, wc)) {
+            if (tid == 0) atomicAdd(err, 1);
+            return;
+        }
+        const uint8_t* fr = frames + (int64_t)img[n] * frame_stride;
+        for (int i = tid; i < 6912; i += 512) {
+            int c = i / 2304, r = (i / 48) % 48, q = i % 48;
+            sX[i] = crop_value(fr, row_stride, c, r, q, y0, x0, hc, wc, 48);
+        }
+    } else {
+        for (int i = tid; i < 6912; i += 512) sX[i] = xin[n * 6912 + i];
+    }
+    __syncthreads();
+    // conv1 3->32 3x3 (46x46) + PReLU + maxpool 3/2 ceil (23x23), fused: each item is one
+    // pooled position; its <= 3x3 conv1 window is recomputed (conv1 is cheap: K=27).
+    for (int i = tid; i < 529; i += 512) {
+        int py = i / 23, px = i % 23;
+        float m[32];
+#pragma unroll
+        for (int co = 0; co < 32; co++) m[co] = -3.402823466e38f;
+        for (int dy = 0; dy < 3; dy++) {
+            int y = 2 * py + dy;
+            if (y >= 46) break;
+            for (int dx = 0; dx < 3; dx++) {
+                int x = 2 * px + dx;
+                if (x >= 46) break;
+                float acc[32];
+#pragma unroll
+                for (int co = 0; co < 32; co++) acc[co] = w.c1b[co];
+#pragma unroll
+                for (int c = 0; c < 3; c++)
+#pragma unroll
+                    for (int ky = 0; ky < 3; ky++)
+#pragma unroll
+                        for (int kx = 0; kx < 3; kx++) {
+                            float v = sX[(c * 48 + y + ky) * 48 + x + kx];
+                            const float* wp = w.c1w + ((c * 3 + ky) * 3 + kx) * 32;
+#pragma unroll
+                            for (int co = 0; co < 32; co++) acc[co] = fmaf(v, wp[co], acc[co]);
+                        }
+#pragma unroll
+                for (int co = 0; co < 32; co++) m[co] = fmaxf(m[co], prelu(acc[co], w.p1[co]));
+            }
+        }
+#pragma unroll
+        for (int co = 0; co < 32; co++) sY[co * 529 + i] = m[co];
+    }
+    __syncthreads();
+    // conv2 32->64 3x3 (21x21) in two halves of 32 channels, each + PReLU + maxpool 3/2 ceil (10x10)
+    for (int half = 0; half < 2; half++) {
+        for (int i = tid; i < 441 * 4; i += 512) {
+            int pos = i % 441, g = i / 441;  // 8-channel group within the half
+            int y = pos / 21, x = pos % 21;
+            int cb = half * 32 + g * 8;
+            float acc[8];
+#pragma unroll
+            for (int k = 0; k < 8; k++) acc[k] = w.c2b[cb + k];
+            for (int c = 0; c < 32; c++) {
+#pragma unroll
+                for (int ky = 0; ky < 3; ky++)
+#pragma unroll
+                    for (int kx = 0; kx < 3; kx++) {
+                        float v = sY[c * 529 + (y + ky) * 23 + x + kx];
+                        const float* wp = w.c2w + ((c * 3 + ky) * 3 + kx) * 64 + cb;
+#pragma unroll
+                        for (int k = 0; k < 8; k++) acc[k] = fmaf(v, wp[k], acc[k]);
+                    }
+            }
+#pragma unroll
+            for (int k = 0; k < 8; k++) sX[(g * 8 + k) * 441 + pos] = prelu(acc[k], w.p2[cb + k]);
+        }
+        __syncthreads();
+        for (int i = tid; i < 3200; i += 512) {
+            int c = i / 100, y = (i / 10) % 10, x = i % 10;
+            float m = -3.402823466e38f;
+            for (int dy = 0; dy < 3; dy++)
+                for (int dx = 0; dx < 3; dx++) {
+                    int yy = 2 * y + dy, xx = 2 * x + dx;
+                    if (yy < 21 && xx < 21) m = fmaxf(m, sX[c * 441 + yy * 21 + xx]);
+                }
+            sZ[(half * 32 + c) * 100 + y * 10 + x] = m;
+        }
+        __syncthreads();
+    }
+    // conv3 64->64 3x3 (8x8) + PReLU
+    for (int i = tid; i < 64 * 8; i += 512) {
+        int pos = i % 64, g = i / 64;
+        int y = pos / 8, x = pos % 8;
+        float acc[8];
+#pragma unroll
+        for (int k = 0; k < 8; k++) acc[k] = w.c3b[g * 8 + k];
+        for (int c = 0; c < 64; c++) {
+#pragma unroll
+            for (int ky = 0; ky < 3; ky++)
+#pragma unroll
+                for (int kx = 0; kx < 3; kx++) {
+                    float v = sZ[c * 100 + (y + ky) * 10 + x + kx];
+                    const float* wp = w.c3w + ((c * 3 + ky) * 3 + kx) * 64 + g * 8;
+#pragma unroll
+                    for (int k = 0; k < 8; k++) acc[k] = fmaf(v, wp[k], acc[k]);
+                }
+        }
+#pragma unroll
+        for (int k = 0; k < 8; k++) sX[(g * 8 + k) * 64 + pos] = prelu(acc[k], w.p3[g * 8 + k]);
+    }
+    __syncthreads();
+    // maxpool 2/2 ceil: 8 -> 4
+    for (int i = tid; i < 1024; i += 512) {
+        int c = i / 16, y = (i / 4) % 4, x = i % 4;
+        float m = -3.402823466e38f;
+        for (int dy = 0; dy < 2; dy++)
+            for (int dx = 0; dx < 2; dx++) m = fmaxf(m, sX[c * 64 + (2 * y + dy) * 8 + 2 * x + dx]);
+        sX[4096 + i] = m;
+    }
+    __syncthreads();
+    // conv4 64->128 2x2 (3x3) + PReLU -> flat (x*384 + y*128 + c)
+    for (int i = tid; i < 9 * 16; i += 512) {
+        int pos = i % 9, g = i / 9;
+        int y = pos / 3, x = pos % 3;
+        float acc[8];
+#pragma unroll
+        for (int k = 0; k < 8; k++) acc[k] = w.c4b[g * 8 + k];
+        for (int c = 0; c < 64; c++) {
+#pragma unroll
+            for (int ky = 0; ky < 2; ky++)
+#pragma unroll
+                for (int kx = 0; kx < 2; kx++) {
+                    float v = sX[4096 + c * 16 + (y + ky) * 4 + x + kx];
+                    const float* wp = w.c4w + ((c * 2 + ky) * 2 + kx) * 128 + g * 8;
+#pragma unroll
+                    for (int k = 0; k < 8; k++) acc[k] = fmaf(v, wp[k], acc[k]);
+                }
+        }
+#pragma unroll
+        for (int k = 0; k < 8; k++) sX[5120 + x * 384 + y * 128 + g * 8 + k] = prelu(acc[k], w.p4[g * 8 + k]);
+    }
+    __syncthreads();
+    // dense5 1152->256 + PReLU (weights transposed [k][256])
+    if (tid < 256) {
+        float acc = w.d5b[tid];
+        for (int k = 0; k < 1152; k++) acc = fmaf(sX[5120 + k], w.d5w[k * 256 + tid], acc);
+        sX[6272 + tid] = prelu(acc, w.p5[tid]);
+    }
+    __syncthreads();
+    if (tid < 64) {
+        float part[16];
+#pragma unroll
+        for (int j = 0; j < 16; j++) part[j] = 0.f;
+        for (int k = tid; k < 256; k += 64) {
+            float f = sX[6272 + k];
+            part[0] = fmaf(f, w.d61w[k], part[0]);
+            part[1] = fmaf(f, w.d61w[256 + k], part[1]);
+#pragma unroll
+            for (int j = 0; j < 4; j++) part[2 + j] = fmaf(f, w.d62w[j * 256 + k], part[2 + j]);
+#pragma unroll
+            for (int j = 0; j < 10; j++) part[6 + j] = fmaf(f, w.d63w[j * 256 + k], part[6 + j]);
+        }
+#pragma unroll
+        for (int j = 0; j < 16; j++)
+            for (int off = 32; off > 0; off >>= 1) part[j] += __shfl_xor(part[j], off);
+        if (tid == 0) {
+            float a0 = part[0] + w.d61b[0], a1 = part[1] + w.d61b[1];
+            float mx = fmaxf(a0, a1);
+            float e0 = expf(a0 - mx), e1 = expf(a1 - mx);
+            prob_out[n] = e1 * __fdiv_rn(1.0f, e0 + e1);
+            reg_out[n] = make_float4(part[2] + w.d62b[0], part[3] + w.d62b[1], part[4] + w.d62b[2], part[5] + w.d62b[3]);
+#pragma unroll
+            for (int j = 0; j < 10; j++) lm_out[n * 10 + j] = part[6 + j] + w.d63b[j];
+        }
+    }
+}
+
+void launch_onet(const uint8_t* frames, int64_t frame_stride, int64_t row_stride, int H, int W, const float4* boxes,
+                 const int32_t* img, const float* xin, int64_t n, const ONetW& w, float4* reg, float* lm, float* prob,
+                 int32_t* err, hipStream_t st) {
+    if (n <= 0) return;
+    if (xin)
+        k_onet<false><<<(unsigned)n, 512, 0, st>>>(frames, frame_stride, row_stride, H, W, boxes, img, xin, w, reg, lm,
+                                                    prob, err);
+    else
+        k_onet<true><<<(unsigned)n, 512, 0, st>>>(frames, frame_stride, row_stride, H, W, boxes, img, xin, w, reg, lm,
+                                                   prob, err);
+}
+
+// ----------------------------------------------------------------------------------- box ops
+
+// stage-1 decode of sorted candidates: (level, lin) -> box, score, img, reg (mtcnn.py:183-194)
+__global__ void k_decode_stage1(const uint64_t* __restrict__ key_sorted, const int32_t* __restrict__ slot_sorted,
+                                const float* __restrict__ score, const float4* __restrict__ regv,
+                                const PNetLevel* __restrict__ lv, int64_t n, float4* __restrict__ boxes,
+                                float* __restrict__ sc, float4* __restrict__ reg, int32_t* __restrict__ img,
+                                int32_t* __restrict__ call) {
+    int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= n) return;
+    uint64_t key = key_sorted[k];
+    int L = (int)(key >> 32);
+    uint32_t lin = (uint32_t)key;
+    const PNetLevel P = lv[L];
+    uint32_t plane = (uint32_t)P.ph * (uint32_t)P.pw;
+    int b = (int)(lin / plane);
+    uint32_t cell = lin % plane;
+    int h = (int)(cell / P.pw), wcol = (int)(cell % P.pw);
+    float s = P.scale;
+    // q1 = floor((2*bb + 1) / s), q2 = floor((2*bb + 12) / s): int64 tensor / python float -> fp32
+    float4 bx;
+    bx.x = floorf(__fdiv_rn((float)(2 * wcol + 1), s));
+    bx.y = floorf(__fdiv_rn((float)(2 * h + 1), s));
+    bx.z = floorf(__fdiv_rn((float)(2 * wcol + 12), s));
+    bx.w = floorf(__fdiv_rn((float)(2 * h + 12), s));
+    int32_t slot = slot_sorted[k];
+    boxes[k] = bx;
+    sc[k] = score[slot];
+    reg[k] = regv[slot];
+    img[k] = b;
+    call[k] = L;
+}
+
+// gather by index list, then optional refine (mtcnn.py:254-262) + square (264-271)
+__global__ void k_gather_refine(const int32_t* __restrict__ idx, int64_t n, const float4* __restrict__ bin,
+                                const float* __restrict__ sin, const float4* __restrict__ rin,
+                                const int32_t* __restrict__ iin, int refine, int plus_one, int square,
+                                float4* __restrict__ bout, float* __restrict__ sout, float4* __restrict__ rout,
+                                int32_t* __restrict__ iout) {
+    int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= n) return;
+    int32_t e = idx ? idx[k] : (int32_t)k;
+    float4 b = bin[e];
+    float4 r = rin ? rin[e] : make_float4(0.f, 0.f, 0.f, 0.f);
+    if (refine) {
+        float w = b.z - b.x, h = b.w - b.y;
+        if (plus_one) {
+            w = w + 1.0f;
+            h = h + 1.0f;
+        }
+        float4 o;
+        o.x = b.x + r.x * w;
+        o.y = b.y + r.y * h;
+        o.z = b.z + r.z * w;
+        o.w = b.w + r.w * h;
+        b = o;
+    }
+    if (square) {
+        float h = b.w - b.y, w = b.z - b.x;
+        float l = fmaxf(w, h);
+        b.x = (b.x + w * 0.5f) - l * 0.5f;
+        b.y = (b.y + h * 0.5f) - l * 0.5f;
+        b.z = b.x + l;
+        b.w = b.y + l;
+    }
+    bout[k] = b;
+    if (sout) sout[k] = sin[e];
+    if (rout) rout[k] = r;
+    if (iout) iout[k] = iin[e];
+}
+
+// flag[k] = score[k] > thr (fp32 compare)
+__global__ void k_threshold(const float* __restrict__ s, int64_t n, float thr, int32_t* __restrict__ flag) {
+    int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k < n) flag[k] = s[k] > thr ? 1 : 0;
+}
+
+__global__ void k_flag_compact(const int32_t* __restrict__ flag, const int32_t* __restrict__ incl, int64_t n,
+                               int32_t* __restrict__ out) {
+    int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k < n && flag[k]) out[incl[k] - 1] = (int32_t)k;
+}
+
+// landmarks from pre-refine boxes (mtcnn.py:235-239): out [n][5][2]
+__global__ void k_landmarks(const float4* __restrict__ boxes, const float* __restrict__ lm, int64_t n,
+                            float* __restrict__ out) {
+    int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= n) return;
+    float4 b = boxes[k];
+    float w = (b.z - b.x) + 1.0f, h = (b.w - b.y) + 1.0f;
+    for (int j = 0; j < 5; j++) {
+        out[k * 10 + 2 * j] = (w * lm[k * 10 + j] + b.x) - 1.0f;
+        out[k * 10 + 2 * j + 1] = (h * lm[k * 10 + 5 + j] + b.y) - 1.0f;
+    }
+}
+
+// _nms_vectorized(method='Min', chain_suppression=True) (mtcnn.py:273-309) on score-sorted
+// rows: drop row k if any earlier row of the same image overlaps it with IoM > thr.
+__global__ void k_iom_chain(const float4* __restrict__ boxes, const int32_t* __restrict__ img,
+                            const int32_t* __restrict__ order, int64_t n, float thr, int32_t* __restrict__ keep) {
+    int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= n) return;
+    int32_t j = order[k];
+    float4 b2 = boxes[j];
+    int32_t ij = img[j];
+    int drop = 0;
+    for (int64_t q = 0; q < k && !drop; q++) {
+        int32_t i = order[q];
+        if (img[i] != ij) continue;
+        float4 b1 = boxes[i];
+        float iw = (fminf(b1.z, b2.z) - fmaxf(b1.x, b2.x)) + 1.0f;
+        float ih = (fminf(b1.w, b2.w) - fmaxf(b1.y, b2.y)) + 1.0f;
+        if (!(iw > 0.f && ih > 0.f)) continue;
+        float inter = iw * ih;
+        float a1 = ((b1.z - b1.x) + 1.0f) * ((b1.w - b1.y) + 1.0f);
+        float a2 = ((b2.z - b2.x) + 1.0f) * ((b2.w - b2.y) + 1.0f);
+        float iom = __fdiv_rn(inter, fminf(a1, a2));
+        if (iom > thr) drop = 1;
+    }
+    keep[k] = !drop;
+}
+
+void launch_decode_stage1(const uint64_t* key_sorted, const int32_t* slot_sorted, const float* score,
+                          const float4* regv, const PNetLevel* lv, int64_t n, float4* boxes, float* sc, float4* reg,
+                          int32_t* img, int32_t* call, hipStream_t st) {
+    if (n > 0)
+        k_decode_stage1<<<cdiv(n, 256), 256, 0, st>>>(key_sorted, slot_sorted, score, regv, lv, n, boxes, sc, reg,
+                                                       img, call);
+}
+void launch_gather_refine(const int32_t* idx, int64_t n, const float4* bin, const float* sin, const float4* rin,
+                          const int32_t* iin, int refine, int plus_one, int square, float4* bout, float* sout,
+                          float4* rout, int32_t* iout, hipStream_t st) {
+    if (n > 0)
+        k_gather_refine<<<cdiv(n, 256), 256, 0, st>>>(idx, n, bin, sin, rin, iin, refine, plus_one, square, bout, sout,
+                                                       rout, iout);
+}
+void launch_threshold(const float* s, int64_t n, float thr, int32_t* flag, hipStream_t st) {
+    if (n > 0) k_threshold<<<cdiv(n, 256), 256, 0, st>>>(s, n, thr, flag);
+}
+void launch_flag_compact(const int32_t* flag, const int32_t* incl, int64_t n, int32_t* out, hipStream_t st) {
+    if (n > 0) k_flag_compact<<<cdiv(n, 256), 256, 0, st>>>(flag, incl, n, out);
+}
+void launch_landmarks(const float4* boxes, const float* lm, int64_t n, float* out, hipStream_t st) {
+    if (n > 0) k_landmarks<<<cdiv(n, 256), 256, 0, st>>>(boxes, lm, n, out);
+}
+void launch_iom_chain(const float4* boxes, const int32_t* img, const int32_t* order, int64_t n, float thr,
+                      int32_t* keep, hipStream_t st) {
+    if (n > 0) k_iom_chain<<<cdiv(n, 128), 128, 0, st>>>(boxes, img, order, n, thr, keep);
+}
+
+}  // namespace vtf

@@ -1,0 +1,449 @@
+// MTCNN detector runtime: weights, pyramid plan, stage orchestration (host side).
+// Mirrors MTCNN.forward (src/videotofaces/detectors/mtcnn.py:167-252) step by step; every
+// data-dependent size is read back once per stage (7 host syncs per det-batch).
+#include <cmath>
+#include <cstring>
+#include <numeric>
+#include <vector>
+
+#include "common.hpp"
+#include "mtcnn.hpp"
+#include "nms.hpp"
+
+namespace vtf {
+
+__global__ void k_iota(int32_t* v, int64_t n) {
+    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) v[i] = (int32_t)i;
+}
+__global__ void k_desc_keys(const float* s, int64_t n, uint64_t* k) {
+    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) k[i] = desc_key(s[i]);
+}
+__global__ void k_gather_rows(const int32_t* idx, int64_t n, const float* in, int row, float* out) {
+    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n * row) return;
+    int64_t k = i / row;
+    int j = (int)(i % row);
+    out[i] = in[(int64_t)idx[k] * row + j];
+}
+
+struct Mtcnn {
+    int device = 0;
+    hipStream_t st = 0;
+    float* d_w = nullptr;
+    PNetW pw{};
+    RNetW rw{};
+    ONetW ow{};
+    Arena ar;
+    int64_t stats[8] = {0};
+
+    ~Mtcnn() {
+        if (d_w) (void)hipFree(d_w);
+    }
+};
+
+enum Slot {
+    S_FRAMES = 0, S_LEVELS, S_COUNT, S_KEY, S_SCORE, S_REGV, S_KEY2, S_SLOT, S_SLOT2, S_B1, S_S1, S_R1, S_I1, S_C1,
+    S_KEEP, S_B2, S_S2, S_R2, S_I2, S_C2, S_PROB, S_REG, S_LM, S_ERR, S_FLAG, S_INCL, S_IDX, S_LMK, S_OUTB, S_OUTS,
+    S_OUTL, S_OUTI, S_SORT, S_SCAN
+};
+
+// ---- weights: reference state_dict order (specs.py mtcnn_spec) -> transposed device layout
+static void build_weights(Mtcnn& m, const float* params, int64_t n_params) {
+    struct P {
+        const char* name;
+        int co, ci, kh, kw;  // conv: co,ci,kh,kw; dense: co=out, ci=in, kh=kw=0; vec: co=n, ci=0
+        int kind;            // 0 vec, 1 conv (transpose), 2 dense (keep [out][in]), 3 dense transposed
+    };
+    static const P spec[] = {
+        {"pnet.conv1.w", 10, 3, 3, 3, 1},   {"pnet.conv1.b", 10, 0, 0, 0, 0},   {"pnet.prelu1", 10, 0, 0, 0, 0},
+        {"pnet.conv2.w", 16, 10, 3, 3, 1},  {"pnet.conv2.b", 16, 0, 0, 0, 0},   {"pnet.prelu2", 16, 0, 0, 0, 0},
+        {"pnet.conv3.w", 32, 16, 3, 3, 1},  {"pnet.conv3.b", 32, 0, 0, 0, 0},   {"pnet.prelu3", 32, 0, 0, 0, 0},
+        {"pnet.conv4_1.w", 2, 32, 0, 0, 2}, {"pnet.conv4_1.b", 2, 0, 0, 0, 0},  {"pnet.conv4_2.w", 4, 32, 0, 0, 2},
+        {"pnet.conv4_2.b", 4, 0, 0, 0, 0},
+        {"rnet.conv1.w", 28, 3, 3, 3, 1},   {"rnet.conv1.b", 28, 0, 0, 0, 0},   {"rnet.prelu1", 28, 0, 0, 0, 0},
+        {"rnet.conv2.w", 48, 28, 3, 3, 1},  {"rnet.conv2.b", 48, 0, 0, 0, 0},   {"rnet.prelu2", 48, 0, 0, 0, 0},
+        {"rnet.conv3.w", 64, 48, 2, 2, 1},  {"rnet.conv3.b", 64, 0, 0, 0, 0},   {"rnet.prelu3", 64, 0, 0, 0, 0},
+        {"rnet.dense4.w", 128, 576, 0, 0, 3}, {"rnet.dense4.b", 128, 0, 0, 0, 0}, {"rnet.prelu4", 128, 0, 0, 0, 0},
+        {"rnet.dense5_1.w", 2, 128, 0, 0, 2}, {"rnet.dense5_1.b", 2, 0, 0, 0, 0}, {"rnet.dense5_2.w", 4, 128, 0, 0, 2},
+        {"rnet.dense5_2.b", 4, 0, 0, 0, 0},
+        {"onet.conv1.w", 32, 3, 3, 3, 1},   {"onet.conv1.b", 32, 0, 0, 0, 0},   {"onet.prelu1", 32, 0, 0, 0, 0},
+        {"onet.conv2.w", 64, 32, 3, 3, 1},  {"onet.conv2.b", 64, 0, 0, 0, 0},   {"onet.prelu2", 64, 0, 0, 0, 0},
+        {"onet.conv3.w", 64, 64, 3, 3, 1},  {"onet.conv3.b", 64, 0, 0, 0, 0},   {"onet.prelu3", 64, 0, 0, 0, 0},
+        {"onet.conv4.w", 128, 64, 2, 2, 1}, {"onet.conv4.b", 128, 0, 0, 0, 0},  {"onet.prelu4", 128, 0, 0, 0, 0},
+        {"onet.dense5.w", 256, 1152, 0, 0, 3}, {"onet.dense5.b", 256, 0, 0, 0, 0}, {"onet.prelu5", 256, 0, 0, 0, 0},
+        {"onet.dense6_1.w", 2, 256, 0, 0, 2}, {"onet.dense6_1.b", 2, 0, 0, 0, 0}, {"onet.dense6_2.w", 4, 256, 0, 0, 2},
+        {"onet.dense6_2.b", 4, 0, 0, 0, 0}, {"onet.dense6_3.w", 10, 256, 0, 0, 2}, {"onet.dense6_3.b", 10, 0, 0, 0, 0},
+    };
+    const int NP = sizeof(spec) / sizeof(spec[0]);
+    std::vector<float> host;
+    std::vector<int64_t> off(NP);
+    int64_t src = 0;
+    for (int i = 0; i < NP; i++) {
+        const P& p = spec[i];
+        int64_t n = (p.kind == 0) ? p.co : (p.kind == 1 ? (int64_t)p.co * p.ci * p.kh * p.kw : (int64_t)p.co * p.ci);
+        VTF_CHECK(src + n <= n_params, VTF_E_ARG, "mtcnn: parameter buffer too small");
+        off[i] = (int64_t)host.size();
+        const float* s = params + src;
+        if (p.kind == 1) {
+            int K = p.ci * p.kh * p.kw;
+            for (int k = 0; k < K; k++)
+                for (int co = 0; co < p.co; co++) host.push_back(s[(int64_t)co * K + k]);
+        } else if (p.kind == 3) {
+            for (int k = 0; k < p.ci; k++)
+                for (int co = 0; co < p.co; co++) host.push_back(s[(int64_t)co * p.ci + k]);
+        } else {
+            host.insert(host.end(), s, s + n);
+        }
+        while (host.size() % 4) host.push_back(0.f);  // 16-B alignment for every tensor
+        src += n;
+    }
+    VTF_CHECK(src == n_params, VTF_E_ARG, "mtcnn: expected 495850 parameters");
+    VTF_HIP(hipMalloc(&m.d_w, host.size() * 4));
+    VTF_HIP(hipMemcpy(m.d_w, host.data(), host.size() * 4, hipMemcpyHostToDevice));
+    const float* b = m.d_w;
+    int i = 0;
+    auto nx = [&]() { return b + off[i++]; };
+    m.pw = PNetW{nx(), nx(), nx(), nx(), nx(), nx(), nx(), nx(), nx(), nx(), nx(), nx(), nx()};
+    m.rw = RNetW{nx(), nx(), nx(), nx(), nx(), nx(), nx(), nx(), nx(), nx(), nx(), nx(), nx(), nx(), nx(), nx()};
+    m.ow = ONetW{nx(), nx(), nx(), nx(), nx(), nx(), nx(), nx(), nx(), nx(), nx(),
+                 nx(), nx(), nx(), nx(), nx(), nx(), nx(), nx(), nx(), nx()};
+}
+
+// MTCNN._scale_pyramid (mtcnn.py:141-148): Python double math, int() truncation
+static void plan_levels(int B, int H, int W, double minsize, std::vector<PNetLevel>& lv, int64_t& tiles,
+                        int64_t& cells) {
+    lv.clear();
+    double s = 12.0 / minsize;
+    std::vector<double> scales;
+    while ((double)std::min(H, W) * s >= 12.0) {
+        scales.push_back(s);
+        s *= 0.709;
+    }
+    tiles = 0;
+    cells = 0;
+    for (double sc : scales) {
+        PNetLevel L{};
+        L.lh = (int)((double)H * sc + 1.0);
+        L.lw = (int)((double)W * sc + 1.0);
+        L.ph = (L.lh - 2 + 1) / 2 - 4;
+        L.pw = (L.lw - 2 + 1) / 2 - 4;
+        L.scale = (float)sc;
+        L.tiles_y = cdiv(L.ph, PNET_TH);
+        L.tiles_x = cdiv(L.pw, PNET_TW);
+        L.tile_beg = tiles;
+        tiles += (int64_t)B * L.tiles_x * L.tiles_y;
+        cells += (int64_t)B * L.ph * L.pw;
+        lv.push_back(L);
+    }
+}
+
+static void d2h_sync(void* dst, const void* src, size_t bytes, hipStream_t st) {
+    VTF_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, st));
+    VTF_HIP(hipStreamSynchronize(st));
+}
+
+// compaction of rows whose score passes `> thr`: returns count, indices in d_idx (order kept)
+static int64_t threshold_compact(Mtcnn& m, const float* d_s, int64_t n, float thr, int32_t* d_idx) {
+    int32_t* flag = m.ar.get<int32_t>(S_FLAG, n);
+    int32_t* incl = m.ar.get<int32_t>(S_INCL, n);
+    launch_threshold(d_s, n, thr, flag, m.st);
+    inclusive_scan_i32(m.ar, S_SCAN, flag, incl, n, m.st);
+    launch_flag_compact(flag, incl, n, d_idx, m.st);
+    int32_t cnt = 0;
+    d2h_sync(&cnt, incl + n - 1, 4, m.st);
+    return cnt;
+}
+
+struct DetectOut {
+    std::vector<float> boxes;  // [n,5]
+    std::vector<float> lms;    // [n,10] as [5][2]
+    std::vector<int32_t> img;
+};
+
+static void detect(Mtcnn& m, const uint8_t* frames, int on_dev, int B, int H, int W, int64_t fstride,
+                   int64_t rstride, double minsize, DetectOut& out) {
+    VTF_CHECK(B > 0 && H > 0 && W > 0 && minsize > 0, VTF_E_ARG, "mtcnn: bad shape");
+    hipStream_t st = m.st;
+    std::memset(m.stats, 0, sizeof(m.stats));
+    out.boxes.clear();
+    out.lms.clear();
+    out.img.clear();
+    const uint8_t* fr = frames;
+    if (!on_dev) {
+        uint8_t* d = m.ar.get<uint8_t>(S_FRAMES, (size_t)B * H * W * 3);
+        for (int b = 0; b < B; b++)
+            VTF_HIP(hipMemcpy2DAsync(d + (size_t)b * H * W * 3, (size_t)W * 3, frames + b * fstride, rstride,
+                                     (size_t)W * 3, H, hipMemcpyHostToDevice, st));
+        fr = d;
+        fstride = (int64_t)H * W * 3;
+        rstride = (int64_t)W * 3;
+    }
+    // ---------------- stage 1: pyramid + PNet (one launch), candidates
+    std::vector<PNetLevel> lv;
+    int64_t tiles = 0, cells = 0;
+    plan_levels(B, H, W, minsize, lv, tiles, cells);
+    const int NL = (int)lv.size();
+    m.stats[0] = NL;
+    if (NL == 0) return;
+    VTF_CHECK(NL < 4096 && cells < (int64_t)1 << 31, VTF_E_LIMIT, "mtcnn: pyramid too large for one call");
+    PNetLevel* d_lv = m.ar.get<PNetLevel>(S_LEVELS, NL);
+    VTF_HIP(hipMemcpyAsync(d_lv, lv.data(), NL * sizeof(PNetLevel), hipMemcpyHostToDevice, st));
+    uint32_t* d_cnt = m.ar.get<uint32_t>(S_COUNT, NL + 1);
+    VTF_HIP(hipMemsetAsync(d_cnt, 0, (NL + 1) * 4, st));
+    PNetOut po{};
+    po.count = d_cnt;
+    po.level_count = d_cnt + 1;
+    po.cap = (uint32_t)cells;
+    po.key = m.ar.get<uint64_t>(S_KEY, cells);
+    po.score = m.ar.get<float>(S_SCORE, cells);
+    po.regv = m.ar.get<float4>(S_REGV, cells);
+    launch_pnet(false, fr, fstride, rstride, H, W, d_lv, NL, tiles, m.pw, po, st);
+    std::vector<uint32_t> cnt(NL + 1);
+    d2h_sync(cnt.data(), d_cnt, (NL + 1) * 4, st);
+    const int64_t n1 = cnt[0];
+    m.stats[1] = n1;
+    if (n1 == 0) return;
+    // order candidates by (level, b, h, w) == reference nonzero() order, level by level
+    int32_t* slot = m.ar.get<int32_t>(S_SLOT, n1);
+    int32_t* slot2 = m.ar.get<int32_t>(S_SLOT2, n1);
+    uint64_t* key2 = m.ar.get<uint64_t>(S_KEY2, n1);
+    k_iota<<<cdiv(n1, 256), 256, 0, st>>>(slot, n1);
+    int lvl_bits = 1;
+    while ((1 << lvl_bits) < NL) lvl_bits++;
+    sort_u64_pairs(m.ar, S_SORT, po.key, key2, slot, slot2, n1, 32 + lvl_bits, st);
+    float4* b1 = m.ar.get<float4>(S_B1, n1);
+    float* s1 = m.ar.get<float>(S_S1, n1);
+    float4* r1 = m.ar.get<float4>(S_R1, n1);
+    int32_t* i1 = m.ar.get<int32_t>(S_I1, n1);
+    int32_t* c1 = m.ar.get<int32_t>(S_C1, n1);
+    launch_decode_stage1(key2, slot2, po.score, po.regv, d_lv, n1, b1, s1, r1, i1, c1, st);
+    // per-level batched_nms(0.5) (mtcnn.py:196)
+    std::vector<int64_t> calls(NL), nk;
+    for (int l = 0; l < NL; l++) calls[l] = cnt[l + 1];
+    int32_t* keep = m.ar.get<int32_t>(S_KEEP, n1);
+    nms_multi(m.ar, (const float*)b1, s1, i1, c1, calls, B, 0.5, keep, nk, st);
+    int64_t k1 = std::accumulate(nk.begin(), nk.end(), (int64_t)0);
+    m.stats[2] = k1;
+    // concatenate levels (keep order) -> batched_nms(0.7) (mtcnn.py:203-206)
+    float4* b2 = m.ar.get<float4>(S_B2, k1);
+    float* s2 = m.ar.get<float>(S_S2, k1);
+    float4* r2 = m.ar.get<float4>(S_R2, k1);
+    int32_t* i2 = m.ar.get<int32_t>(S_I2, k1);
+    int32_t* c2 = m.ar.get<int32_t>(S_C2, k1);
+    launch_gather_refine(keep, k1, b1, s1, r1, i1, 0, 0, 0, b2, s2, r2, i2, st);
+    VTF_HIP(hipMemsetAsync(c2, 0, k1 * 4, st));
+    nms_multi(m.ar, (const float*)b2, s2, i2, c2, {k1}, B, 0.7, keep, nk, st);
+    int64_t k2 = nk[0];
+    m.stats[3] = k2;
+    // refine(plus_one=False) + square (mtcnn.py:207-208) -> stage-2 proposals
+    launch_gather_refine(keep, k2, b2, s2, r2, i2, 1, 0, 1, b1, s1, nullptr, i1, st);
+    // ---------------- stage 2: crop 24x24 + RNet (mtcnn.py:213-222)
+    float* prob = m.ar.get<float>(S_PROB, k2);
+    float4* reg = m.ar.get<float4>(S_REG, k2);
+    int32_t* err = m.ar.get<int32_t>(S_ERR, 1);
+    VTF_HIP(hipMemsetAsync(err, 0, 4, st));
+    launch_rnet(fr, fstride, rstride, H, W, b1, i1, nullptr, k2, m.rw, reg, prob, err, st);
+    int32_t nerr = 0;
+    d2h_sync(&nerr, err, 4, st);
+    VTF_CHECK(nerr == 0, VTF_E_DEGENERATE,
+              "stage 2: a candidate box lies outside the frame; the reference skips it in "
+              "_get_cropped_candidates (mtcnn.py:159) and then fails indexing (IndexError)");
+    int32_t* idx = m.ar.get<int32_t>(S_IDX, k2);
+    int64_t n2 = threshold_compact(m, prob, k2, 0.7f, idx);
+    m.stats[4] = n2;
+    if (n2 == 0) return;
+    launch_gather_refine(idx, n2, b1, prob, reg, i1, 0, 0, 0, b2, s2, r2, i2, st);
+    VTF_HIP(hipMemsetAsync(c2, 0, n2 * 4, st));
+    nms_multi(m.ar, (const float*)b2, s2, i2, c2, {n2}, B, 0.7, keep, nk, st);
+    int64_t k3 = nk[0];
+    m.stats[5] = k3;
+    launch_gather_refine(keep, k3, b2, s2, r2, i2, 1, 1, 1, b1, s1, nullptr, i1, st);
+    // ---------------- stage 3: crop 48x48 + ONet (mtcnn.py:228-242)
+    prob = m.ar.get<float>(S_PROB, k3);
+    reg = m.ar.get<float4>(S_REG, k3);
+    float* lm = m.ar.get<float>(S_LM, k3 * 10);
+    VTF_HIP(hipMemsetAsync(err, 0, 4, st));
+    launch_onet(fr, fstride, rstride, H, W, b1, i1, nullptr, k3, m.ow, reg, lm, prob, err, st);
+    d2h_sync(&nerr, err, 4, st);
+    VTF_CHECK(nerr == 0, VTF_E_DEGENERATE,
+              "stage 3: a candidate box lies outside the frame; the reference skips it in "
+              "_get_cropped_candidates (mtcnn.py:159) and then fails indexing (IndexError)");
+    idx = m.ar.get<int32_t>(S_IDX, k3);
+    int64_t n3 = threshold_compact(m, prob, k3, 0.7f, idx);
+    m.stats[6] = n3;
+    if (n3 == 0) return;
+    launch_gather_refine(idx, n3, b1, prob, reg, i1, 0, 0, 0, b2, s2, r2, i2, st);
+    float* lmr = m.ar.get<float>(S_LMK, n3 * 10);
+    k_gather_rows<<<cdiv(n3 * 10, 256), 256, 0, st>>>(idx, n3, lm, 10, lmr);
+    float* lmk = m.ar.get<float>(S_OUTL, n3 * 10);
+    launch_landmarks(b2, lmr, n3, lmk, st);
+    // refine(+1) without square, then IoM chain NMS (mtcnn.py:241-242)
+    float4* b3 = m.ar.get<float4>(S_B1, n3);
+    launch_gather_refine(nullptr, n3, b2, nullptr, r2, nullptr, 1, 1, 0, b3, nullptr, nullptr, nullptr, st);
+    uint64_t* kk = m.ar.get<uint64_t>(S_KEY2, n3);
+    uint64_t* kk2 = m.ar.get<uint64_t>(S_KEY, n3);
+    int32_t* io = m.ar.get<int32_t>(S_SLOT, n3);
+    int32_t* order = m.ar.get<int32_t>(S_SLOT2, n3);
+    k_desc_keys<<<cdiv(n3, 256), 256, 0, st>>>(s2, n3, kk);
+    k_iota<<<cdiv(n3, 256), 256, 0, st>>>(io, n3);
+    sort_u64_pairs(m.ar, S_SORT, kk, kk2, io, order, n3, 32, st);
+    int32_t* kflag = m.ar.get<int32_t>(S_FLAG, n3);
+    launch_iom_chain(b3, i2, order, n3, 0.7f, kflag, st);
+    int32_t* incl = m.ar.get<int32_t>(S_INCL, n3);
+    inclusive_scan_i32(m.ar, S_SCAN, kflag, incl, n3, st);
+    int32_t* pos = m.ar.get<int32_t>(S_IDX, n3);
+    launch_flag_compact(kflag, incl, n3, pos, st);
+    int32_t nf = 0;
+    d2h_sync(&nf, incl + n3 - 1, 4, st);
+    m.stats[7] = nf;
+    if (nf == 0) return;
+    // final rows in IoM keep order: element = order[pos[k]]
+    std::vector<int32_t> h_order(n3), h_pos(nf), h_img(n3);
+    std::vector<float4> h_box(n3);
+    std::vector<float> h_s(n3), h_lm(n3 * 10);
+    VTF_HIP(hipMemcpyAsync(h_order.data(), order, n3 * 4, hipMemcpyDeviceToHost, st));
+    VTF_HIP(hipMemcpyAsync(h_pos.data(), pos, nf * 4, hipMemcpyDeviceToHost, st));
+    VTF_HIP(hipMemcpyAsync(h_img.data(), i2, n3 * 4, hipMemcpyDeviceToHost, st));
+    VTF_HIP(hipMemcpyAsync(h_box.data(), b3, n3 * 16, hipMemcpyDeviceToHost, st));
+    VTF_HIP(hipMemcpyAsync(h_s.data(), s2, n3 * 4, hipMemcpyDeviceToHost, st));
+    VTF_HIP(hipMemcpyAsync(h_lm.data(), lmk, n3 * 40, hipMemcpyDeviceToHost, st));
+    VTF_HIP(hipStreamSynchronize(st));
+    out.boxes.resize(nf * 5);
+    out.lms.resize(nf * 10);
+    out.img.resize(nf);
+    for (int k = 0; k < nf; k++) {
+        int e = h_order[h_pos[k]];
+        float4 bx = h_box[e];
+        float* o = &out.boxes[k * 5];
+        o[0] = bx.x;
+        o[1] = bx.y;
+        o[2] = bx.z;
+        o[3] = bx.w;
+        o[4] = h_s[e];
+        std::memcpy(&out.lms[k * 10], &h_lm[e * 10], 40);
+        out.img[k] = h_img[e];
+    }
+}
+
+}  // namespace vtf
+
+using namespace vtf;
+
+struct vtf_mtcnn_s {
+    Mtcnn m;
+};
+
+extern "C" {
+
+int vtf_mtcnn_create(const float* params, int64_t n_params, int device, vtf_mtcnn_t* out) {
+    return guarded([&] {
+        VTF_CHECK(params && out, VTF_E_ARG, "null argument");
+        VTF_HIP(hipSetDevice(device));
+        auto* h = new vtf_mtcnn_s();
+        h->m.device = device;
+        try {
+            build_weights(h->m, params, n_params);
+        } catch (...) {
+            delete h;
+            throw;
+        }
+        *out = h;
+    });
+}
+
+int vtf_mtcnn_destroy(vtf_mtcnn_t h) {
+    return guarded([&] { delete h; });
+}
+
+int vtf_mtcnn_set_stream(vtf_mtcnn_t h, void* stream) {
+    return guarded([&] {
+        VTF_CHECK(h, VTF_E_ARG, "null handle");
+        h->m.st = (hipStream_t)stream;
+    });
+}
+
+int vtf_mtcnn_stats(vtf_mtcnn_t h, int64_t* out8) {
+    return guarded([&] {
+        VTF_CHECK(h && out8, VTF_E_ARG, "null argument");
+        std::memcpy(out8, h->m.stats, sizeof(h->m.stats));
+    });
+}
+
+int vtf_mtcnn_detect(vtf_mtcnn_t h, const uint8_t* frames, int frames_on_device, int B, int H, int W,
+                     int64_t frame_stride, int64_t row_stride, double min_face_size, float* out_boxes,
+                     float* out_landmarks, int32_t* out_counts, int64_t cap, int64_t* out_total) {
+    return guarded([&] {
+        VTF_CHECK(h && frames && out_counts, VTF_E_ARG, "null argument");
+        VTF_HIP(hipSetDevice(h->m.device));
+        DetectOut r;
+        detect(h->m, frames, frames_on_device, B, H, W, frame_stride, row_stride, min_face_size, r);
+        int64_t n = (int64_t)r.img.size();
+        if (out_total) *out_total = n;
+        VTF_CHECK(n <= cap, VTF_E_CAPACITY, "output capacity too small");
+        for (int b = 0; b < B; b++) out_counts[b] = 0;
+        int64_t k = 0;
+        for (int b = 0; b < B; b++)
+            for (int64_t e = 0; e < n; e++)
+                if (r.img[e] == b) {
+                    if (out_boxes) std::memcpy(out_boxes + k * 5, &r.boxes[e * 5], 20);
+                    if (out_landmarks) std::memcpy(out_landmarks + k * 10, &r.lms[e * 10], 40);
+                    out_counts[b]++;
+                    k++;
+                }
+    });
+}
+
+int vtf_mtcnn_pnet_level(vtf_mtcnn_t h, const uint8_t* d_frames, int B, int H, int W, int64_t frame_stride,
+                         int64_t row_stride, int lh, int lw, float* d_prob, float* d_reg) {
+    return guarded([&] {
+        VTF_CHECK(h && d_frames && d_prob && d_reg && lh >= 12 && lw >= 12, VTF_E_ARG, "bad argument");
+        PNetLevel L{};
+        L.lh = lh;
+        L.lw = lw;
+        L.ph = (lh - 1) / 2 - 4;
+        L.pw = (lw - 1) / 2 - 4;
+        L.scale = 1.f;
+        L.tiles_y = cdiv(L.ph, PNET_TH);
+        L.tiles_x = cdiv(L.pw, PNET_TW);
+        L.tile_beg = 0;
+        PNetLevel* d_lv = h->m.ar.get<PNetLevel>(S_LEVELS, 1);
+        VTF_HIP(hipMemcpyAsync(d_lv, &L, sizeof(L), hipMemcpyHostToDevice, h->m.st));
+        PNetOut po{};
+        po.prob = d_prob;
+        po.reg = d_reg;
+        launch_pnet(true, d_frames, frame_stride, row_stride, H, W, d_lv, 1, (int64_t)B * L.tiles_x * L.tiles_y,
+                    h->m.pw, po, h->m.st);
+        VTF_HIP(hipStreamSynchronize(h->m.st));
+    });
+}
+
+int vtf_mtcnn_resample(vtf_mtcnn_t h, const uint8_t* d_frames, int B, int H, int W, int64_t frame_stride,
+                       int64_t row_stride, int lh, int lw, float* d_out) {
+    return guarded([&] {
+        VTF_CHECK(h && d_frames && d_out, VTF_E_ARG, "null argument");
+        launch_resample(d_frames, frame_stride, row_stride, B, H, W, lh, lw, d_out, h->m.st);
+        VTF_HIP(hipStreamSynchronize(h->m.st));
+    });
+}
+
+int vtf_mtcnn_rnet(vtf_mtcnn_t h, const float* d_in, int64_t n, float* d_reg, float* d_prob) {
+    return guarded([&] {
+        VTF_CHECK(h && d_in && d_reg && d_prob, VTF_E_ARG, "null argument");
+        launch_rnet(nullptr, 0, 0, 0, 0, nullptr, nullptr, d_in, n, h->m.rw, (float4*)d_reg, d_prob, nullptr,
+                    h->m.st);
+        VTF_HIP(hipStreamSynchronize(h->m.st));
+    });
+}
+
+int vtf_mtcnn_onet(vtf_mtcnn_t h, const float* d_in, int64_t n, float* d_reg, float* d_lm, float* d_prob) {
+    return guarded([&] {
+        VTF_CHECK(h && d_in && d_reg && d_lm && d_prob, VTF_E_ARG, "null argument");
+        launch_onet(nullptr, 0, 0, 0, 0, nullptr, nullptr, d_in, n, h->m.ow, (float4*)d_reg, d_lm, d_prob, nullptr,
+                    h->m.st);
+        VTF_HIP(hipStreamSynchronize(h->m.st));
+    });
+}
+
+}  // extern "C"

@@ -1,0 +1,333 @@
+// Greedy NMS with torchvision semantics on gfx950.
+//
+// Replaces torchvision.ops.batched_nms / nms (third-party C++ op; the reference calls it at
+// src/videotofaces/detectors/mtcnn.py:196,205,219 and detectors/operations/post.py:8).
+// Semantics restated (torchvision/ops/boxes.py, csrc/ops/cpu/nms_kernel.cpp):
+//   * n*4 > 4000 -> "vanilla": independent NMS per class id, result sorted by score;
+//     else "coordinate trick": boxes += float(idx) * (max(boxes) + 1), one NMS.
+//   * NMS: stable descending score order; areas (x2-x1)*(y2-y1) in fp32; keep i unless
+//     suppressed; suppress j if inter / ((area_i + area_j) - inter) > thr (fp32 IoU promoted
+//     to double).  Output: keep indices ordered by (score desc, index asc).
+// Design (MI355X): a radix sort gives the stable order; an IoU bitmask kernel (one wave per
+// 64-row block, 64x64 tiles, box broadcast through LDS) writes u64 suppression words; a
+// single-wave scan per segment resolves the greedy dependence 64 rows at a time in
+// registers (readlane) and ORs kept rows into an LDS "removed" bitset -- no barriers.
+// Build with -ffp-contract=off: every IoU op is rounded exactly like the CPU kernel.
+#include <cstring>
+#include <rocprim/device/device_radix_sort.hpp>
+#include <rocprim/device/device_scan.hpp>
+
+#include <algorithm>
+
+#include "common.hpp"
+#include "nms.hpp"
+
+namespace vtf {
+
+__global__ void k_call_max(const float4* __restrict__ boxes, const int64_t* __restrict__ call_beg,
+                           const int64_t* __restrict__ call_n, const int32_t* __restrict__ trick_calls,
+                           float* __restrict__ call_max) {
+    int c = trick_calls[blockIdx.x];
+    int64_t beg = call_beg[c], n = call_n[c];
+    float m = -INFINITY;
+    for (int64_t i = threadIdx.x; i < n; i += blockDim.x) {
+        float4 b = boxes[beg + i];
+        m = fmaxf(m, fmaxf(fmaxf(b.x, b.y), fmaxf(b.z, b.w)));
+    }
+    __shared__ float red[256];
+    red[threadIdx.x] = m;
+    __syncthreads();
+    for (int s = blockDim.x / 2; s > 0; s >>= 1) {
+        if ((int)threadIdx.x < s) red[threadIdx.x] = fmaxf(red[threadIdx.x], red[threadIdx.x + s]);
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) call_max[c] = red[0];
+}
+
+// key = [call:12][seg image:20] [desc score:32]; element order is position order.
+__global__ void k_seg_keys(const float* __restrict__ scores, const int32_t* __restrict__ img,
+                           const int32_t* __restrict__ elem_call, const uint8_t* __restrict__ call_vanilla,
+                           int64_t N, int with_seg, uint64_t* __restrict__ keys, int32_t* __restrict__ vals) {
+    int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= N) return;
+    uint32_t c = (uint32_t)elem_call[e];
+    uint32_t s = (with_seg && call_vanilla[c]) ? (uint32_t)img[e] : 0u;
+    keys[e] = ((uint64_t)((c << 20) | s) << 32) | desc_key(scores[e]);
+    vals[e] = (int32_t)e;
+}
+
+__global__ void k_seg_count(const uint64_t* __restrict__ keys, int64_t N, const int32_t* __restrict__ seg_base,
+                            int32_t* __restrict__ seg_cnt) {
+    int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= N) return;
+    uint32_t hi = (uint32_t)(keys[k] >> 32);
+    int s = seg_base[hi >> 20] + (int)(hi & 0xFFFFF);
+    atomicAdd(&seg_cnt[s], 1);
+}
+
+struct MaskTask {
+    int32_t seg;
+    int32_t rb;
+};
+
+__device__ inline float4 load_box(const float4* __restrict__ boxes, const int32_t* __restrict__ img,
+                                  int32_t e, float off_base) {
+    float4 b = boxes[e];
+    if (off_base != 0.f) {
+        float off = (float)img[e] * off_base;
+        b.x = b.x + off;
+        b.y = b.y + off;
+        b.z = b.z + off;
+        b.w = b.w + off;
+    }
+    return b;
+}
+
+// One wave per (segment, 64-row block); loops over column blocks cb >= rb.
+__global__ __launch_bounds__(64) void k_iou_mask(const float4* __restrict__ boxes, const int32_t* __restrict__ img,
+                                                 const int32_t* __restrict__ order, const MaskTask* __restrict__ tasks,
+                                                 const int64_t* __restrict__ seg_beg, const int32_t* __restrict__ seg_n,
+                                                 const int64_t* __restrict__ seg_mask_off,
+                                                 const float* __restrict__ seg_offbase, double thr,
+                                                 uint64_t* __restrict__ mask) {
+    MaskTask t = tasks[blockIdx.x];
+    const int lane = threadIdx.x;
+    const int64_t beg = seg_beg[t.seg];
+    const int m = seg_n[t.seg];
+    const int nb = (m + 63) >> 6;
+    const float ob = seg_offbase[t.seg];
+    const int row = t.rb * 64 + lane;
+    __shared__ float4 cb_box[64];
+    __shared__ float cb_area[64];
+    float4 bi = make_float4(0.f, 0.f, 0.f, 0.f);
+    float ai = 0.f;
+    if (row < m) {
+        bi = load_box(boxes, img, order[beg + row], ob);
+        ai = (bi.z - bi.x) * (bi.w - bi.y);
+    }
+    uint64_t* out = mask + seg_mask_off[t.seg] + (int64_t)row * nb;
+    for (int cb = t.rb; cb < nb; cb++) {
+        int col = cb * 64 + lane;
+        float4 bj = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (col < m) bj = load_box(boxes, img, order[beg + col], ob);
+        __syncthreads();
+        cb_box[lane] = bj;
+        cb_area[lane] = (bj.z - bj.x) * (bj.w - bj.y);
+        __syncthreads();
+        int ncol = min(64, m - cb * 64);
+        uint64_t bits = 0;
+        if (row < m) {
+            int j0 = (cb == t.rb) ? lane + 1 : 0;
+            for (int j = j0; j < ncol; j++) {
+                float4 b = cb_box[j];
+                float xx1 = fmaxf(bi.x, b.x), yy1 = fmaxf(bi.y, b.y);
+                float xx2 = fminf(bi.z, b.z), yy2 = fminf(bi.w, b.w);
+                float w = fmaxf(0.f, xx2 - xx1), h = fmaxf(0.f, yy2 - yy1);
+                float inter = w * h;
+                float ovr = __fdiv_rn(inter, (ai + cb_area[j]) - inter);
+                if ((double)ovr > thr) bits |= (1ull << j);
+            }
+            out[cb] = bits;
+        }
+    }
+}
+
+// One wave per segment: greedy resolution, 64 rows per step.
+__global__ __launch_bounds__(64) void k_nms_scan(const uint64_t* __restrict__ mask, const int64_t* __restrict__ seg_beg,
+                                                 const int32_t* __restrict__ seg_n,
+                                                 const int64_t* __restrict__ seg_mask_off,
+                                                 uint8_t* __restrict__ keep_sorted) {
+    extern __shared__ uint64_t removed[];
+    const int s = blockIdx.x;
+    const int lane = threadIdx.x;
+    const int m = seg_n[s];
+    if (m == 0) return;
+    const int nb = (m + 63) >> 6;
+    const uint64_t* msk = mask + seg_mask_off[s];
+    const int64_t beg = seg_beg[s];
+    for (int w = lane; w < nb; w += 64) removed[w] = 0;
+    __builtin_amdgcn_wave_barrier();
+    for (int cb = 0; cb < nb; cb++) {
+        const int row = cb * 64 + lane;
+        const int nrow = min(64, m - cb * 64);
+        uint64_t diag = (row < m) ? msk[(int64_t)row * nb + cb] : 0ull;
+        uint64_t rem = removed[cb];
+        uint64_t kept = 0;
+        for (int t = 0; t < nrow; t++) {
+            uint32_t lo = __builtin_amdgcn_readlane((uint32_t)diag, t);
+            uint32_t hi = __builtin_amdgcn_readlane((uint32_t)(diag >> 32), t);
+            if (!((rem >> t) & 1ull)) {
+                kept |= 1ull << t;
+                rem |= ((uint64_t)hi << 32) | lo;
+            }
+        }
+        if (row < m) keep_sorted[beg + row] = (uint8_t)((kept >> lane) & 1ull);
+        uint64_t kk = kept;
+        while (kk) {
+            int t = __builtin_ctzll(kk);
+            kk &= kk - 1;
+            const uint64_t* mr = msk + (int64_t)(cb * 64 + t) * nb;
+            for (int w = cb + 1 + lane; w < nb; w += 64) removed[w] |= mr[w];
+        }
+        __builtin_amdgcn_wave_barrier();
+    }
+}
+
+__global__ void k_scatter_flags(const int32_t* __restrict__ order, const uint8_t* __restrict__ keep_sorted,
+                                int64_t N, uint8_t* __restrict__ keep_elem) {
+    int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k < N) keep_elem[order[k]] = keep_sorted[k];
+}
+
+__global__ void k_flag_in_order(const int32_t* __restrict__ order, const uint8_t* __restrict__ keep_elem,
+                                int64_t N, int32_t* __restrict__ flag) {
+    int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k < N) flag[k] = keep_elem[order[k]];
+}
+
+__global__ void k_compact(const int32_t* __restrict__ order, const int32_t* __restrict__ flag,
+                          const int32_t* __restrict__ incl, const int32_t* __restrict__ elem_call, int64_t N,
+                          int32_t* __restrict__ keep_out, int32_t* __restrict__ call_kept) {
+    int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= N || !flag[k]) return;
+    int32_t e = order[k];
+    keep_out[incl[k] - 1] = e;
+    atomicAdd(&call_kept[elem_call[e]], 1);
+}
+
+template <class K, class V>
+static void radix_pairs(Arena& ar, int slot, const K* kin, K* kout, const V* vin, V* vout, int64_t n, int end_bit,
+                        hipStream_t st) {
+    size_t tmp = 0;
+    VTF_HIP(rocprim::radix_sort_pairs(nullptr, tmp, kin, kout, vin, vout, (size_t)n, 0, end_bit, st));
+    void* t = ar.get(slot, tmp);
+    VTF_HIP(rocprim::radix_sort_pairs(t, tmp, kin, kout, vin, vout, (size_t)n, 0, end_bit, st));
+}
+
+void sort_u64_pairs(Arena& ar, int slot, const uint64_t* kin, uint64_t* kout, const int32_t* vin, int32_t* vout,
+                    int64_t n, int end_bit, hipStream_t st) {
+    radix_pairs(ar, slot, kin, kout, vin, vout, n, end_bit, st);
+}
+
+void inclusive_scan_i32(Arena& ar, int slot, const int32_t* in, int32_t* out, int64_t n, hipStream_t st) {
+    size_t tmp = 0;
+    VTF_HIP(rocprim::inclusive_scan(nullptr, tmp, in, out, (size_t)n, rocprim::plus<int32_t>(), st));
+    void* t = ar.get(slot, tmp);
+    VTF_HIP(rocprim::inclusive_scan(t, tmp, in, out, (size_t)n, rocprim::plus<int32_t>(), st));
+}
+
+// Arena slots used here: 40..59
+void nms_multi(Arena& ar, const float* d_boxes, const float* d_scores, const int32_t* d_img,
+               const int32_t* d_elem_call, const std::vector<int64_t>& call_n, int n_img, double thr,
+               int32_t* d_keep, std::vector<int64_t>& nkeep, hipStream_t st) {
+    const int C = (int)call_n.size();
+    VTF_CHECK(C < 4096, VTF_E_LIMIT, "nms_multi: too many calls");
+    VTF_CHECK(n_img < (1 << 20), VTF_E_LIMIT, "nms_multi: too many images");
+    nkeep.assign(C, 0);
+    int64_t N = 0;
+    std::vector<int64_t> call_beg(C);
+    std::vector<uint8_t> vanilla(C);
+    std::vector<int32_t> seg_base(C + 1);
+    std::vector<int32_t> trick;
+    int S = 0;
+    for (int c = 0; c < C; c++) {
+        call_beg[c] = N;
+        N += call_n[c];
+        vanilla[c] = call_n[c] * 4 > 4000;
+        seg_base[c] = S;
+        S += vanilla[c] ? n_img : 1;
+        if (!vanilla[c] && call_n[c] > 0) trick.push_back(c);
+    }
+    seg_base[C] = S;
+    if (N == 0) return;
+    VTF_CHECK(N < (int64_t)1 << 31, VTF_E_LIMIT, "nms_multi: too many boxes");
+
+    // small host->device tables
+    int64_t* d_cbeg = ar.get<int64_t>(40, C);
+    int64_t* d_cn = ar.get<int64_t>(41, C);
+    uint8_t* d_van = ar.get<uint8_t>(42, C);
+    int32_t* d_sbase = ar.get<int32_t>(43, C + 1);
+    VTF_HIP(hipMemcpyAsync(d_cbeg, call_beg.data(), C * 8, hipMemcpyHostToDevice, st));
+    VTF_HIP(hipMemcpyAsync(d_cn, call_n.data(), C * 8, hipMemcpyHostToDevice, st));
+    VTF_HIP(hipMemcpyAsync(d_van, vanilla.data(), C, hipMemcpyHostToDevice, st));
+    VTF_HIP(hipMemcpyAsync(d_sbase, seg_base.data(), (C + 1) * 4, hipMemcpyHostToDevice, st));
+
+    // per-segment coordinate-trick offset base (max + 1), 0 for vanilla segments
+    float* d_cmax = ar.get<float>(44, C);
+    VTF_HIP(hipMemsetAsync(d_cmax, 0, C * 4, st));
+    if (!trick.empty()) {
+        int32_t* d_trick = ar.get<int32_t>(45, trick.size());
+        VTF_HIP(hipMemcpyAsync(d_trick, trick.data(), trick.size() * 4, hipMemcpyHostToDevice, st));
+        k_call_max<<<(int)trick.size(), 256, 0, st>>>((const float4*)d_boxes, d_cbeg, d_cn, d_trick, d_cmax);
+    }
+
+    // sort 1: (call, segment image, score desc), stable over position order
+    uint64_t* k0 = ar.get<uint64_t>(46, N);
+    uint64_t* k1 = ar.get<uint64_t>(47, N);
+    int32_t* v0 = ar.get<int32_t>(48, N);
+    int32_t* ord = ar.get<int32_t>(49, N);
+    k_seg_keys<<<cdiv(N, 256), 256, 0, st>>>(d_scores, d_img, d_elem_call, d_van, N, 1, k0, v0);
+    sort_u64_pairs(ar, 50, k0, k1, v0, ord, N, 64, st);
+    int32_t* d_scnt = ar.get<int32_t>(51, S);
+    VTF_HIP(hipMemsetAsync(d_scnt, 0, S * 4, st));
+    k_seg_count<<<cdiv(N, 256), 256, 0, st>>>(k1, N, d_sbase, d_scnt);
+    std::vector<int32_t> scnt(S);
+    std::vector<float> cmax(C);
+    VTF_HIP(hipMemcpyAsync(scnt.data(), d_scnt, S * 4, hipMemcpyDeviceToHost, st));
+    VTF_HIP(hipMemcpyAsync(cmax.data(), d_cmax, C * 4, hipMemcpyDeviceToHost, st));
+    VTF_HIP(hipStreamSynchronize(st));
+
+    // segment tables, mask offsets, row-block tasks
+    std::vector<int64_t> sbeg(S), moff(S);
+    std::vector<float> offb(S, 0.f);
+    std::vector<MaskTask> tasks;
+    int64_t pos = 0, mtot = 0;
+    int maxnb = 0;
+    for (int c = 0; c < C; c++) {
+        for (int s = seg_base[c]; s < seg_base[c + 1]; s++) {
+            sbeg[s] = pos;
+            moff[s] = mtot;
+            int m = scnt[s];
+            int nb = (m + 63) / 64;
+            maxnb = std::max(maxnb, nb);
+            if (!vanilla[c]) offb[s] = cmax[c] + 1.0f;
+            for (int rb = 0; rb < nb; rb++) tasks.push_back({s, rb});
+            pos += m;
+            mtot += (int64_t)m * nb;
+        }
+    }
+    VTF_CHECK(maxnb * 8 <= 160 * 1024, VTF_E_LIMIT, "nms_multi: a segment exceeds 1.3M boxes");
+    int64_t* d_sbeg = ar.get<int64_t>(52, S);
+    int64_t* d_moff = ar.get<int64_t>(53, S);
+    float* d_offb = ar.get<float>(54, S);
+    MaskTask* d_tasks = (MaskTask*)ar.get(55, tasks.size() * sizeof(MaskTask));
+    VTF_HIP(hipMemcpyAsync(d_sbeg, sbeg.data(), S * 8, hipMemcpyHostToDevice, st));
+    VTF_HIP(hipMemcpyAsync(d_moff, moff.data(), S * 8, hipMemcpyHostToDevice, st));
+    VTF_HIP(hipMemcpyAsync(d_offb, offb.data(), S * 4, hipMemcpyHostToDevice, st));
+    VTF_HIP(hipMemcpyAsync(d_tasks, tasks.data(), tasks.size() * sizeof(MaskTask), hipMemcpyHostToDevice, st));
+    uint64_t* d_mask = ar.get<uint64_t>(56, mtot);
+    if (!tasks.empty())
+        k_iou_mask<<<(int)tasks.size(), 64, 0, st>>>((const float4*)d_boxes, d_img, ord, d_tasks, d_sbeg, d_scnt,
+                                                      d_moff, d_offb, thr, d_mask);
+    uint8_t* keep_sorted = ar.get<uint8_t>(57, N);
+    k_nms_scan<<<S, 64, maxnb * 8, st>>>(d_mask, d_sbeg, d_scnt, d_moff, keep_sorted);
+    uint8_t* keep_elem = ar.get<uint8_t>(58, N);
+    k_scatter_flags<<<cdiv(N, 256), 256, 0, st>>>(ord, keep_sorted, N, keep_elem);
+
+    // sort 2: (call, score desc), stable over position order -> output order
+    k_seg_keys<<<cdiv(N, 256), 256, 0, st>>>(d_scores, d_img, d_elem_call, d_van, N, 0, k0, v0);
+    sort_u64_pairs(ar, 50, k0, k1, v0, ord, N, 64, st);
+    int32_t* flag = (int32_t*)k0;  // reuse
+    int32_t* incl = ((int32_t*)k0) + N;
+    k_flag_in_order<<<cdiv(N, 256), 256, 0, st>>>(ord, keep_elem, N, flag);
+    inclusive_scan_i32(ar, 59, flag, incl, N, st);
+    int32_t* d_ckept = d_scnt;  // reuse (S >= C)
+    VTF_HIP(hipMemsetAsync(d_ckept, 0, C * 4, st));
+    k_compact<<<cdiv(N, 256), 256, 0, st>>>(ord, flag, incl, d_elem_call, N, d_keep, d_ckept);
+    std::vector<int32_t> ck(C);
+    VTF_HIP(hipMemcpyAsync(ck.data(), d_ckept, C * 4, hipMemcpyDeviceToHost, st));
+    VTF_HIP(hipStreamSynchronize(st));
+    for (int c = 0; c < C; c++) nkeep[c] = ck[c];
+}
+
+}  // namespace vtf

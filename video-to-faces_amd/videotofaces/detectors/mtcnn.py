@@ -1,0 +1,165 @@
+"""MTCNN face detector on MI355X (drop-in for src/videotofaces/detectors/mtcnn.py).
+
+``RealMTCNN(device, min_face_size=5)`` keeps the reference constructor and ``__call__``
+contract (mtcnn.py:312-326): frames ``np.ndarray uint8 [B,H,W,3]`` BGR (any strides, or a
+list of frames, or a CUDA uint8 tensor already in HBM) -> ``list[np.ndarray f32 (n_i,5)]``
+of ``x1,y1,x2,y2,score`` per frame, in the reference's order.  The whole forward
+(preprocess, pyramid, P/R/O-Net, the four NMS passes) runs in libvtf_hip.so.
+"""
+import ctypes
+import os
+
+import numpy as np
+import torch
+
+from .. import _native as nat
+from .. import synth
+
+
+class MTCNN:
+    """Handle around vtf_mtcnn_* (the reference's nn.Module MTCNN, mtcnn.py:124-252)."""
+
+    def __init__(self, device=None, params=None):
+        self.device = nat.require_gpu(device)
+        L = nat.lib()
+        if params is None:
+            params = synth.make_params('mtcnn')
+        flat = np.ascontiguousarray(synth.pack(params), dtype=np.float32)
+        h = ctypes.c_void_p()
+        nat.check(L.vtf_mtcnn_create(flat.ctypes.data, flat.size, self.device.index or 0, ctypes.byref(h)))
+        self._h = h
+        self.last_stats = None
+
+    def __del__(self):
+        h = getattr(self, '_h', None)
+        if h and nat._LIB is not None:
+            nat._LIB.vtf_mtcnn_destroy(h)
+            self._h = None
+
+    def _bind_stream(self):
+        nat.check(nat.lib().vtf_mtcnn_set_stream(self._h, nat.stream_ptr(self.device)))
+
+    def forward(self, imgs, minsize=20, return_landmarks=False):
+        L = nat.lib()
+        self._bind_stream()
+        if isinstance(imgs, torch.Tensor):
+            t = imgs
+            if t.dtype != torch.uint8 or t.dim() != 4 or t.shape[3] != 3:
+                raise ValueError('frames tensor must be uint8 [B,H,W,3]')
+            if t.stride(3) != 1 or t.stride(2) != 3:
+                t = t.contiguous()
+            on_dev = int(t.is_cuda)
+            B, H, W = t.shape[:3]
+            fstride, rstride = t.stride(0), t.stride(1)
+            base = ctypes.c_void_p(t.data_ptr())
+            keep_alive = t
+        else:
+            x = imgs if isinstance(imgs, np.ndarray) else np.stack(imgs)
+            if x.dtype != np.uint8 or x.ndim != 4 or x.shape[3] != 3:
+                raise ValueError('frames must be uint8 [B,H,W,3]')
+            if x.strides[3] != 1 or x.strides[2] != 3 or x.strides[0] < 0 or x.strides[1] < 0:
+                x = np.ascontiguousarray(x)
+            on_dev = 0
+            B, H, W = x.shape[:3]
+            fstride, rstride = x.strides[0], x.strides[1]
+            base = ctypes.c_void_p(x.ctypes.data)
+            keep_alive = x
+        cap = max(64, 256 * B)
+        while True:
+            boxes = np.empty((cap, 5), np.float32)
+            lms = np.empty((cap, 5, 2), np.float32)
+            counts = np.empty(B, np.int32)
+            total = ctypes.c_int64(0)
+            rc = L.vtf_mtcnn_detect(self._h, base, on_dev, B, H, W, fstride, rstride, float(minsize),
+                                    boxes.ctypes.data, lms.ctypes.data, counts.ctypes.data, cap,
+                                    ctypes.byref(total))
+            if rc == nat.VTF_E_CAPACITY:
+                cap = int(total.value)
+                continue
+            nat.check(rc)
+            break
+        del keep_alive
+        st = np.zeros(8, np.int64)
+        nat.check(L.vtf_mtcnn_stats(self._h, st.ctypes.data))
+        self.last_stats = st
+        res, ldm, k = [], [], 0
+        for b in range(B):
+            n = int(counts[b])
+            res.append(boxes[k:k + n].copy())
+            ldm.append(lms[k:k + n].copy())
+            k += n
+        if return_landmarks:
+            return res, ldm
+        return res
+
+    __call__ = forward
+
+    # ---- stage-level entry points (parity tests)
+    def pnet_level(self, frames_dev, lh, lw):
+        B, H, W = frames_dev.shape[:3]
+        ph, pw = (lh - 1) // 2 - 4, (lw - 1) // 2 - 4
+        prob = torch.empty((B, ph, pw), dtype=torch.float32, device=self.device)
+        reg = torch.empty((B, 4, ph, pw), dtype=torch.float32, device=self.device)
+        self._bind_stream()
+        nat.check(nat.lib().vtf_mtcnn_pnet_level(self._h, nat.ptr(frames_dev), B, H, W, frames_dev.stride(0),
+                                                 frames_dev.stride(1), lh, lw, nat.ptr(prob), nat.ptr(reg)))
+        return reg, prob
+
+    def resample(self, frames_dev, lh, lw):
+        B, H, W = frames_dev.shape[:3]
+        out = torch.empty((B, 3, lh, lw), dtype=torch.float32, device=self.device)
+        self._bind_stream()
+        nat.check(nat.lib().vtf_mtcnn_resample(self._h, nat.ptr(frames_dev), B, H, W, frames_dev.stride(0),
+                                               frames_dev.stride(1), lh, lw, nat.ptr(out)))
+        return out
+
+    def rnet(self, x):
+        x = x.to(self.device, torch.float32).contiguous()
+        n = x.shape[0]
+        reg = torch.empty((n, 4), dtype=torch.float32, device=self.device)
+        prob = torch.empty((n,), dtype=torch.float32, device=self.device)
+        self._bind_stream()
+        nat.check(nat.lib().vtf_mtcnn_rnet(self._h, nat.ptr(x), n, nat.ptr(reg), nat.ptr(prob)))
+        return reg, prob
+
+    def onet(self, x):
+        x = x.to(self.device, torch.float32).contiguous()
+        n = x.shape[0]
+        reg = torch.empty((n, 4), dtype=torch.float32, device=self.device)
+        lm = torch.empty((n, 10), dtype=torch.float32, device=self.device)
+        prob = torch.empty((n,), dtype=torch.float32, device=self.device)
+        self._bind_stream()
+        nat.check(nat.lib().vtf_mtcnn_onet(self._h, nat.ptr(x), n, nat.ptr(reg), nat.ptr(lm), nat.ptr(prob)))
+        return reg, lm, prob
+
+
+class RealMTCNN():
+    """Drop-in for RealMTCNN (mtcnn.py:312-326)."""
+
+    def __init__(self, device=None, min_face_size=5, weights=None):
+        print('Initializing MTCNN model for live-action face detection')
+        params = None
+        wf = weights or os.path.join(os.getcwd(), 'weights', 'mtcnn_joined.pt')
+        if os.path.isfile(wf):
+            params = synth.load_real('mtcnn', wf)
+        self.model = MTCNN(device, params)
+        self.minsize = min_face_size
+
+    def __call__(self, frames):
+        with torch.inference_mode():
+            boxes = self.model(frames, self.minsize)
+        return boxes
+
+
+def batched_nms(boxes, scores, idxs, iou_threshold):
+    """torchvision.ops.batched_nms on device tensors, via vtf_batched_nms."""
+    dev = boxes.device
+    b = boxes.to(torch.float32).contiguous()
+    s = scores.to(torch.float32).contiguous()
+    i = idxs.to(torch.int64).contiguous()
+    n = b.shape[0]
+    keep = torch.empty(max(n, 1), dtype=torch.int64, device=dev)
+    nk = ctypes.c_int64(0)
+    nat.check(nat.lib().vtf_batched_nms(nat.ptr(b), nat.ptr(s), nat.ptr(i), n, float(iou_threshold), nat.ptr(keep),
+                                        ctypes.byref(nk), nat.stream_ptr(dev)))
+    return keep[:nk.value]
