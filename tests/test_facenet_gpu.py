@@ -1,0 +1,64 @@
+"""GPU parity: FaceNet (InceptionResnetV1) on libvtf_hip.so vs reference goldens / oracle."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import GOLDEN
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope='module')
+def g():
+    return np.load(os.path.join(GOLDEN, 'facenet.npz'))
+
+
+@pytest.fixture(scope='module')
+def fp32():
+    from videotofaces.encoders.facenet import InceptionResnetV1
+    return InceptionResnetV1('cuda:0', precision='fp32')
+
+
+def test_fp32_vs_golden(g, fp32):
+    x = (torch.from_numpy(g['u8']).float() - 127.5) * (1 / 128)
+    emb = fp32(x).cpu().numpy()
+    # north-star tolerance for fp32 embeddings
+    np.testing.assert_allclose(emb, g['emb'], atol=1e-4, rtol=0)
+    np.testing.assert_allclose(np.linalg.norm(emb, axis=1), 1.0, atol=1e-5)
+
+
+def test_bf16_drift_reported(g):
+    from videotofaces.encoders.facenet import InceptionResnetV1
+    m = InceptionResnetV1('cuda:0', precision='bf16')
+    x = (torch.from_numpy(g['u8']).float() - 127.5) * (1 / 128)
+    emb = m(x).cpu().numpy()
+    cos = (emb * g['emb']).sum(1)
+    print('bf16 vs fp32-reference cosine:', cos, 'max abs', np.abs(emb - g['emb']).max())
+    assert cos.min() > 0.99
+
+
+def test_blob_kernel_matches_restated_inter_linear():
+    from videotofaces.encoders.facenet import blob_from_images
+    from oracle.facenet import resize_linear_u8
+    rng = np.random.default_rng(3)
+    imgs = [rng.integers(0, 256, (h, w, 3), dtype=np.uint8) for (h, w) in [(160, 160), (73, 91), (300, 211), (1, 5), (161, 159)]]
+    out = blob_from_images(imgs, 160, 127.5, 1 / 128, torch.device('cuda:0')).cpu().numpy()
+    for i, im in enumerate(imgs):
+        r = resize_linear_u8(im, 160)[:, :, ::-1].transpose(2, 0, 1).astype(np.float32)
+        np.testing.assert_array_equal(out[i], (r - 127.5) * np.float32(1 / 128))
+
+
+def test_encode_crops_vs_oracle(fp32):
+    from videotofaces import synth
+    from oracle.facenet import resize_linear_u8, inception_resnet_v1
+    fr = synth.make_frames(2, 200, 320, seed=2)
+    crops = np.array([[0, 10, 20, 110, 130], [1, 100, 50, 260, 190], [0, 0, 0, 160, 160], [1, 300, 150, 320, 200]], np.int32)
+    emb = fp32.encode_crops(torch.from_numpy(fr).cuda(), crops).cpu().numpy()
+    blobs = []
+    for f, x1, y1, x2, y2 in crops:
+        r = resize_linear_u8(fr[f, y1:y2, x1:x2], 160)[:, :, ::-1].transpose(2, 0, 1)
+        blobs.append((torch.from_numpy(np.ascontiguousarray(r)).float() - 127.5) * (1 / 128))
+    ref = inception_resnet_v1(synth.make_params('facenet'), torch.stack(blobs)).numpy()
+    np.testing.assert_allclose(emb, ref, atol=1e-4)

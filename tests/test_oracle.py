@@ -93,3 +93,21 @@ def test_oracle_nms_c_core_vs_pure_torch():
         s = torch.from_numpy(rng.uniform(0, 1, n).astype(np.float32))
         i = torch.from_numpy(rng.integers(0, nimg, n))
         assert onms.batched_nms(b, s, i, 0.5).tolist() == _tv_batched_nms(b, s, i, 0.5).tolist()
+
+
+def test_oracle_facenet_vs_golden():
+    from videotofaces import synth
+    from oracle.facenet import inception_resnet_v1
+    gf = np.load(os.path.join(GOLDEN, 'facenet.npz'))
+    x = (torch.from_numpy(gf['u8']).float() - 127.5) * (1 / 128)
+    y = inception_resnet_v1(synth.make_params('facenet'), x).numpy()
+    np.testing.assert_allclose(y, gf['emb'], atol=1e-6, rtol=0)
+
+
+def test_oracle_grouping_vs_golden():
+    from oracle import grouping as og
+    gg = np.load(os.path.join(GOLDEN, 'grouping.npz'))
+    mins, inds = og.cosine_dedupe(gg['X'])
+    np.testing.assert_array_equal(mins, gg['dedupe_mins'])
+    np.testing.assert_array_equal(inds, gg['dedupe_inds'])
+    np.testing.assert_array_equal(np.nonzero(~(mins <= 0.25))[0], gg['dedupe_keep'])

@@ -1,0 +1,134 @@
+// cv2.dnn.blobFromImages on device crops (src/videotofaces/encoders/facenet.py:179,
+// encoders/vit.py:141): each face crop (a slice of a frame in HBM, detection.py:161-162) is
+// resized to S x S with OpenCV's uint8 INTER_LINEAR, converted to float, mean-subtracted,
+// scaled and written RGB (swapRB).  This replaces the reference's JPEG write/read round trip
+// between detection and encoding (detection.py:156 -> grouping.py:34).
+//
+// INTER_LINEAR restated from OpenCV's published resize (resizeGeneric_ with
+// HResizeLinear + the SIMD VResizeLinearVec_32s8u rounding):
+//   fx = (float)((dx + 0.5) * (src/dst) - 0.5); sx = floor(fx); fx -= sx; clamp sx to
+//   [0, w-1] with fx = 0 at the borders; a0 = rint((1-fx)*2048), a1 = rint(fx*2048);
+//   h = S[sx]*a0 + S[sx+1]*a1 (or S[w-1]*2048 at the right border); same for rows;
+//   out = ((((h0 >> 4) * b0) >> 16) + (((h1 >> 4) * b1) >> 16) + 2) >> 2, saturated.
+// cv2 is not installed here, so this step is parity-UNPINNED (tests pin the post-blob
+// tensor -> embedding boundary instead).
+#include "common.hpp"
+#include "blob.hpp"
+
+namespace vtf {
+
+__device__ inline void lin_coef(int d, int src, int dst, int& s0, int& s1, int& c0, int& c1, bool& edge) {
+    double scale = 1.0 / ((double)dst / (double)src);
+    float f = (float)(((double)d + 0.5) * scale - 0.5);
+    int s = (int)floorf(f);
+    f -= (float)s;
+    edge = false;
+    if (s < 0) {
+        f = 0.f;
+        s = 0;
+    }
+    if (s >= src - 1) {
+        f = 0.f;
+        s = src - 1;
+        edge = true;
+    }
+    s0 = s;
+    s1 = min(s + 1, src - 1);
+    c0 = (int)rintf((1.f - f) * 2048.f);
+    c1 = (int)rintf(f * 2048.f);
+}
+
+template <typename T>
+__device__ inline T cvt_out(float v);
+template <>
+__device__ inline float cvt_out<float>(float v) { return v; }
+template <>
+__device__ inline __bf16 cvt_out<__bf16>(float v) { return (__bf16)v; }
+
+// layout 0: NCHW [N,3,S,S]; layout 1: NHWC [N,S,S,Cp] (channels >= 3 zero)
+template <typename T, int LAYOUT>
+__global__ void k_blob(const uint8_t* __restrict__ frames, int H, int W, int64_t fstride, int64_t rstride,
+                       const int32_t* __restrict__ crops, int64_t N, int S, float mean, float scale, int Cp,
+                       T* __restrict__ out) {
+    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= N * S * S) return;
+    int dx = (int)(i % S);
+    int dy = (int)((i / S) % S);
+    int64_t n = i / ((int64_t)S * S);
+    const int32_t* c = crops + n * 5;
+    int f = c[0], x1 = c[1], y1 = c[2], x2 = c[3], y2 = c[4];
+    // numpy slice semantics of img[y1:y2, x1:x2] for in-frame boxes (adjust_boxes clamps)
+    x1 = max(0, min(x1, W));
+    x2 = max(x1, min(x2, W));
+    y1 = max(0, min(y1, H));
+    y2 = max(y1, min(y2, H));
+    int w = x2 - x1, h = y2 - y1;
+    const uint8_t* base = frames + (int64_t)f * fstride + (int64_t)y1 * rstride + (int64_t)x1 * 3;
+    int v[3];
+    if (w <= 0 || h <= 0) {
+        v[0] = v[1] = v[2] = 0;
+    } else if (w == S && h == S) {
+        const uint8_t* p = base + (int64_t)dy * rstride + dx * 3;
+        v[0] = p[0];
+        v[1] = p[1];
+        v[2] = p[2];
+    } else {
+        int sx0, sx1, a0, a1, sy0, sy1, b0, b1;
+        bool ex, ey;
+        lin_coef(dx, w, S, sx0, sx1, a0, a1, ex);
+        lin_coef(dy, h, S, sy0, sy1, b0, b1, ey);
+        (void)ey;
+        const uint8_t* r0 = base + (int64_t)sy0 * rstride;
+        const uint8_t* r1 = base + (int64_t)sy1 * rstride;
+#pragma unroll
+        for (int ch = 0; ch < 3; ch++) {
+            int h0 = ex ? r0[sx0 * 3 + ch] * 2048 : r0[sx0 * 3 + ch] * a0 + r0[sx1 * 3 + ch] * a1;
+            int h1 = ex ? r1[sx0 * 3 + ch] * 2048 : r1[sx0 * 3 + ch] * a0 + r1[sx1 * 3 + ch] * a1;
+            int t = (((h0 >> 4) * b0) >> 16) + (((h1 >> 4) * b1) >> 16);
+            t = (t + 2) >> 2;
+            v[ch] = min(255, max(0, t));
+        }
+    }
+    // swapRB: output channel 0 = R = BGR byte 2
+    for (int oc = 0; oc < 3; oc++) {
+        float val = ((float)v[2 - oc] - mean) * scale;
+        if (LAYOUT == 0)
+            out[((n * 3 + oc) * S + dy) * S + dx] = cvt_out<T>(val);
+        else
+            out[((n * S + dy) * S + dx) * Cp + oc] = cvt_out<T>(val);
+    }
+    if (LAYOUT == 1)
+        for (int oc = 3; oc < Cp; oc++) out[((n * S + dy) * S + dx) * Cp + oc] = cvt_out<T>(0.f);
+}
+
+void launch_blob(const uint8_t* frames, int H, int W, int64_t fstride, int64_t rstride, const int32_t* d_crops,
+                 int64_t N, int S, float mean, float scale, int layout, int Cp, bool bf16, void* out, hipStream_t st) {
+    int64_t tot = N * S * S;
+    if (tot <= 0) return;
+    if (layout == 0)
+        k_blob<float, 0><<<cdiv(tot, 256), 256, 0, st>>>(frames, H, W, fstride, rstride, d_crops, N, S, mean, scale, 3,
+                                                          (float*)out);
+    else if (bf16)
+        k_blob<__bf16, 1><<<cdiv(tot, 256), 256, 0, st>>>(frames, H, W, fstride, rstride, d_crops, N, S, mean, scale,
+                                                           Cp, (__bf16*)out);
+    else
+        k_blob<float, 1><<<cdiv(tot, 256), 256, 0, st>>>(frames, H, W, fstride, rstride, d_crops, N, S, mean, scale, Cp,
+                                                          (float*)out);
+}
+
+}  // namespace vtf
+
+using namespace vtf;
+
+extern "C" int vtf_blob_from_crops(const uint8_t* d_frames, int H, int W, int64_t frame_stride, int64_t row_stride,
+                                   const int32_t* d_crops, int64_t N, int S, float mean, float scale, float* d_out,
+                                   void* hip_stream) {
+    return guarded([&] {
+        VTF_CHECK(N >= 0 && S > 0, VTF_E_ARG, "bad argument");
+        if (N == 0) return;
+        VTF_CHECK(d_frames && d_crops && d_out, VTF_E_ARG, "null argument");
+        launch_blob(d_frames, H, W, frame_stride, row_stride, d_crops, N, S, mean, scale, 0, 3, false, d_out,
+                    (hipStream_t)hip_stream);
+        VTF_HIP(hipGetLastError());
+    });
+}

@@ -78,9 +78,19 @@ struct Arena {
 
 inline int cdiv(int64_t a, int64_t b) { return (int)((a + b - 1) / b); }
 
+// Read-only weights through the constant address space: the compiler then emits scalar
+// (s_load) loads for wave-uniform addresses even in kernels that also store to global memory.
+#define VTF_CONST __attribute__((address_space(4)))
+template <class T>
+__device__ inline const VTF_CONST T* cptr(const T* p) {
+    return (const VTF_CONST T*)p;
+}
+
+__host__ __device__ inline uint32_t f2u(float f) { return __builtin_bit_cast(uint32_t, f); }
+
 // Sortable descending key of a float: larger float -> smaller key (NaN-free inputs).
 __host__ __device__ inline uint32_t desc_key(float f) {
-    uint32_t u = __float_as_uint(f);
+    uint32_t u = f2u(f);
     uint32_t asc = (u & 0x80000000u) ? ~u : (u | 0x80000000u);
     return ~asc;
 }

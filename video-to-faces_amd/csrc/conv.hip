@@ -1,0 +1,341 @@
+// Implicit-GEMM convolution on MFMA for gfx950 (NHWC activations).
+//
+// Replaces the torch.nn.Conv2d + BatchNorm2d + ReLU stacks of ConvUnit
+// (src/videotofaces/backbones/basic.py:5-45) and the residual tails of Block35/17/8
+// (src/videotofaces/encoders/facenet.py:14-81) -- the encoder conv path.
+//   GEMM view: M = N*OH*OW output pixels, N = Cout, K = KH*KW*Cin (k = (kh, kw, ci)).
+//   A = im2col gathered on the fly from NHWC input (16-B vectors along ci),
+//   B = weights [Cout][K] (host re-layout), C -> fused epilogue -> NHWC output slice
+//   (channel offset + stride, so Inception concats are free).
+// Two precisions from one template:
+//   fp32: v_mfma_f32_16x16x4_f32  (exact fp32 products, parity mode, 1e-4 vs the reference)
+//   bf16: v_mfma_f32_16x16x32_bf16 (bf16 operands/activations, fp32 accumulate; perf mode)
+// Tile: BM x BN per 256-thread workgroup (2x2 waves, each (BM/2)x(BN/2) = 16x16 fragments),
+// BK-deep K steps, global->register prefetch of step k+1 while step k runs on MFMA from LDS.
+#include "common.hpp"
+#include "conv.hpp"
+
+namespace vtf {
+
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
+typedef __attribute__((ext_vector_type(4))) float f32x4;
+
+template <typename T>
+struct VecT;
+template <>
+struct VecT<float> {
+    typedef f32x4 type;
+    static constexpr int V = 4;
+};
+template <>
+struct VecT<__bf16> {
+    typedef bf16x8 type;
+    static constexpr int V = 8;
+};
+
+__device__ inline float to_f(float v) { return v; }
+__device__ inline float to_f(__bf16 v) { return (float)v; }
+template <typename T>
+__device__ inline T from_f(float v);
+template <>
+__device__ inline float from_f<float>(float v) { return v; }
+template <>
+__device__ inline __bf16 from_f<__bf16>(float v) { return (__bf16)v; }
+
+template <typename T, int BM, int BN, int BK>
+__global__ __launch_bounds__(256) void k_conv(ConvParams p) {
+    using vec = typename VecT<T>::type;
+    constexpr int V = VecT<T>::V;
+    constexpr int PAD = V;
+    constexpr int LDA = BK + PAD;
+    constexpr int KV = BK / V;                // vectors per tile row
+    constexpr int RA = BM * KV / 256;         // A vectors per thread
+    constexpr int RB = BN * KV / 256;         // B vectors per thread
+    static_assert(RA >= 1 && RB >= 1 && (256 % KV) == 0, "tile config");
+    constexpr int WM = BM / 2, WN = BN / 2, FM = WM / 16, FN = WN / 16;
+    __shared__ __attribute__((aligned(16))) T As[BM * LDA];
+    __shared__ __attribute__((aligned(16))) T Bs[BN * LDA];
+
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wm = wave >> 1, wn = wave & 1;
+    // XCD-friendly order is irrelevant here (weights are L2/MALL resident); plain mapping
+    const int64_t m0 = (int64_t)blockIdx.x * BM;
+    const int n0 = blockIdx.y * BN;
+    const T* __restrict__ in = (const T*)p.in;
+    const T* __restrict__ wt = (const T*)p.w;
+
+    // per-thread A rows and the thread's k-vector position
+    const int kv = tid % KV;
+    int64_t a_base[RA];
+    int a_ih0[RA], a_iw0[RA];
+    bool a_ok[RA];
+#pragma unroll
+    for (int r = 0; r < RA; r++) {
+        int row = (tid + 256 * r) / KV;
+        int64_t m = m0 + row;
+        a_ok[r] = m < p.M;
+        int64_t mm = a_ok[r] ? m : 0;
+        int ow = (int)(mm % p.OW);
+        int64_t t = mm / p.OW;
+        int oh = (int)(t % p.OH);
+        int n = (int)(t / p.OH);
+        a_base[r] = (int64_t)n * p.H * p.W * p.Cin;
+        a_ih0[r] = oh * p.sh - p.ph;
+        a_iw0[r] = ow * p.sw - p.pw;
+    }
+    int k = kv * V;
+    int ci = k % p.Cin, kw_ = (k / p.Cin) % p.KW, kh_ = (k / p.Cin) / p.KW;
+
+    vec ra[RA], rb[RB];
+    auto load_tile = [&](int kcur, int ci_, int kw0, int kh0) {
+#pragma unroll
+        for (int r = 0; r < RA; r++) {
+            vec v = {};
+            int ih = a_ih0[r] + kh0, iw = a_iw0[r] + kw0;
+            if (a_ok[r] && kcur < p.K && ih >= 0 && ih < p.H && iw >= 0 && iw < p.W)
+                v = *(const vec*)(in + a_base[r] + ((int64_t)ih * p.W + iw) * p.Cin + ci_);
+            ra[r] = v;
+        }
+#pragma unroll
+        for (int r = 0; r < RB; r++) {
+            int row = (tid + 256 * r) / KV;
+            int co = n0 + row;
+            vec v = {};
+            if (co < p.Cout && kcur < p.K) v = *(const vec*)(wt + (int64_t)co * p.K + kcur);
+            rb[r] = v;
+        }
+    };
+    auto store_tile = [&]() {
+#pragma unroll
+        for (int r = 0; r < RA; r++) {
+            int row = (tid + 256 * r) / KV;
+            *(vec*)(As + row * LDA + kv * V) = ra[r];
+        }
+#pragma unroll
+        for (int r = 0; r < RB; r++) {
+            int row = (tid + 256 * r) / KV;
+            *(vec*)(Bs + row * LDA + kv * V) = rb[r];
+        }
+    };
+    auto advance = [&]() {
+        k += BK;
+        ci += BK;
+        while (ci >= p.Cin) {
+            ci -= p.Cin;
+            if (++kw_ == p.KW) {
+                kw_ = 0;
+                kh_++;
+            }
+        }
+    };
+
+    f32x4 acc[FM][FN];
+#pragma unroll
+    for (int i = 0; i < FM; i++)
+#pragma unroll
+        for (int j = 0; j < FN; j++) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    const int KT = (p.K + BK - 1) / BK;
+    load_tile(k, ci, kw_, kh_);
+    store_tile();
+    __syncthreads();
+    for (int kt = 0; kt < KT; kt++) {
+        if (kt + 1 < KT) {
+            advance();
+            load_tile(k, ci, kw_, kh_);
+        }
+        const T* Aw = As + (wm * WM + (lane & 15)) * LDA;
+        const T* Bw = Bs + (wn * WN + (lane & 15)) * LDA;
+        if constexpr (sizeof(T) == 2) {
+#pragma unroll
+            for (int ks = 0; ks < BK; ks += 32) {
+                bf16x8 af[FM], bfr[FN];
+#pragma unroll
+                for (int i = 0; i < FM; i++) af[i] = *(const bf16x8*)(Aw + i * 16 * LDA + ks + 8 * (lane >> 4));
+#pragma unroll
+                for (int j = 0; j < FN; j++) bfr[j] = *(const bf16x8*)(Bw + j * 16 * LDA + ks + 8 * (lane >> 4));
+#pragma unroll
+                for (int i = 0; i < FM; i++)
+#pragma unroll
+                    for (int j = 0; j < FN; j++)
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+            }
+        } else {
+#pragma unroll
+            for (int ks = 0; ks < BK; ks += 4) {
+                float af[FM], bfr[FN];
+#pragma unroll
+                for (int i = 0; i < FM; i++) af[i] = to_f(Aw[i * 16 * LDA + ks + (lane >> 4)]);
+#pragma unroll
+                for (int j = 0; j < FN; j++) bfr[j] = to_f(Bw[j * 16 * LDA + ks + (lane >> 4)]);
+#pragma unroll
+                for (int i = 0; i < FM; i++)
+#pragma unroll
+                    for (int j = 0; j < FN; j++)
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[i], bfr[j], acc[i][j], 0, 0, 0);
+            }
+        }
+        __syncthreads();
+        if (kt + 1 < KT) {
+            store_tile();
+            __syncthreads();
+        }
+    }
+
+    // epilogue: C layout col = lane & 15, row = 4 * (lane >> 4) + i
+    T* __restrict__ out = (T*)p.out;
+    const T* __restrict__ res = (const T*)p.res;
+#pragma unroll
+    for (int j = 0; j < FN; j++) {
+        int c = n0 + wn * WN + j * 16 + (lane & 15);
+        if (c >= p.Cout) continue;
+        float bias = p.bias ? p.bias[c] : 0.f;
+        float al = p.alpha ? p.alpha[c] : 1.f;
+        float be = p.alpha ? p.beta[c] : 0.f;
+#pragma unroll
+        for (int i = 0; i < FM; i++) {
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                int64_t m = m0 + wm * WM + i * 16 + 4 * (lane >> 4) + q;
+                if (m >= p.M) continue;
+                float v = acc[i][j][q];
+                if (p.bias) v = v + bias;
+                if (p.alpha) v = fmaf(v, al, be);
+                if (p.scale != 1.f) v = v * p.scale;
+                if (res) v = v + to_f(res[m * p.res_cstride + c]);
+                if (p.relu) v = fmaxf(v, 0.f);
+                out[m * p.out_cstride + p.out_coff + c] = from_f<T>(v);
+            }
+        }
+    }
+}
+
+template <typename T>
+static void launch_t(const ConvParams& p, hipStream_t st) {
+    if (p.Cout <= 32) {
+        dim3 g(cdiv(p.M, 128), cdiv(p.Cout, 32));
+        if constexpr (sizeof(T) == 2)
+            k_conv<T, 128, 32, 64><<<g, 256, 0, st>>>(p);
+        else
+            k_conv<T, 128, 32, 32><<<g, 256, 0, st>>>(p);
+    } else {
+        dim3 g(cdiv(p.M, 128), cdiv(p.Cout, 64));
+        if constexpr (sizeof(T) == 2)
+            k_conv<T, 128, 64, 64><<<g, 256, 0, st>>>(p);
+        else
+            k_conv<T, 128, 64, 32><<<g, 256, 0, st>>>(p);
+    }
+}
+
+void launch_conv(const ConvParams& p, bool bf16, hipStream_t st) {
+    if (p.M <= 0) return;
+    VTF_CHECK(p.Cin % 8 == 0, VTF_E_ARG, "conv: Cin must be a multiple of 8 (pad the input)");
+    if (bf16)
+        launch_t<__bf16>(p, st);
+    else
+        launch_t<float>(p, st);
+}
+
+// ---------------------------------------------------------------- maxpool 3x3 / 2, no padding (NHWC)
+template <typename T>
+__global__ void k_maxpool(const T* __restrict__ in, int N, int H, int W, int C, int OH, int OW, T* __restrict__ out,
+                          int out_cstride, int out_coff) {
+    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    int64_t tot = (int64_t)N * OH * OW * C;
+    if (i >= tot) return;
+    int c = (int)(i % C);
+    int64_t t = i / C;
+    int ow = (int)(t % OW);
+    t /= OW;
+    int oh = (int)(t % OH);
+    int n = (int)(t / OH);
+    float m = -3.402823466e38f;
+    for (int dy = 0; dy < 3; dy++)
+        for (int dx = 0; dx < 3; dx++)
+            m = fmaxf(m, to_f(in[(((int64_t)n * H + 2 * oh + dy) * W + 2 * ow + dx) * C + c]));
+    out[(((int64_t)n * OH + oh) * OW + ow) * out_cstride + out_coff + c] = from_f<T>(m);
+}
+
+void launch_maxpool(const void* in, int N, int H, int W, int C, void* out, int out_cstride, int out_coff, bool bf16,
+                    hipStream_t st) {
+    int OH = (H - 3) / 2 + 1, OW = (W - 3) / 2 + 1;
+    int64_t tot = (int64_t)N * OH * OW * C;
+    if (bf16)
+        k_maxpool<__bf16><<<cdiv(tot, 256), 256, 0, st>>>((const __bf16*)in, N, H, W, C, OH, OW, (__bf16*)out,
+                                                           out_cstride, out_coff);
+    else
+        k_maxpool<float><<<cdiv(tot, 256), 256, 0, st>>>((const float*)in, N, H, W, C, OH, OW, (float*)out,
+                                                          out_cstride, out_coff);
+}
+
+// ---------------------------------------------------------------- NCHW fp32 -> NHWC (C padded to Cp)
+template <typename T>
+__global__ void k_nchw_to_nhwc(const float* __restrict__ in, int N, int C, int H, int W, int Cp, T* __restrict__ out) {
+    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    int64_t tot = (int64_t)N * H * W * Cp;
+    if (i >= tot) return;
+    int c = (int)(i % Cp);
+    int64_t t = i / Cp;
+    int w = (int)(t % W);
+    t /= W;
+    int h = (int)(t % H);
+    int n = (int)(t / H);
+    float v = c < C ? in[(((int64_t)n * C + c) * H + h) * W + w] : 0.f;
+    out[i] = from_f<T>(v);
+}
+
+void launch_nchw_to_nhwc(const float* in, int N, int C, int H, int W, int Cp, void* out, bool bf16, hipStream_t st) {
+    int64_t tot = (int64_t)N * H * W * Cp;
+    if (bf16)
+        k_nchw_to_nhwc<__bf16><<<cdiv(tot, 256), 256, 0, st>>>(in, N, C, H, W, Cp, (__bf16*)out);
+    else
+        k_nchw_to_nhwc<float><<<cdiv(tot, 256), 256, 0, st>>>(in, N, C, H, W, Cp, (float*)out);
+}
+
+// ---------------------------------------------------------------- FaceNet head
+// AdaptiveAvgPool2d(1) -> Linear 1792->512 (no bias) -> BatchNorm1d -> F.normalize
+// (facenet.py:144-147,153).  One workgroup per image; weights fp32 [512][1792].
+template <typename T>
+__global__ __launch_bounds__(512) void k_facenet_head(const T* __restrict__ x, int HW, int C,
+                                                      const float* __restrict__ w, const float* __restrict__ alpha,
+                                                      const float* __restrict__ beta, int D, float* __restrict__ out) {
+    extern __shared__ float sh[];
+    float* pooled = sh;      // C
+    float* red = sh + C;     // 8
+    const int n = blockIdx.x, tid = threadIdx.x;
+    const T* xn = x + (int64_t)n * HW * C;
+    int side = 1;
+    while (side * side < HW) side++;
+    for (int c = tid; c < C; c += blockDim.x) {
+        float s = 0.f;
+        for (int i = 0; i < HW; i++) s = s + to_f(xn[(int64_t)i * C + c]);
+        pooled[c] = __fdiv_rn(__fdiv_rn(s, (float)side), (float)side);
+    }
+    __syncthreads();
+    float y = 0.f, sq = 0.f;
+    if (tid < D) {
+        const float* wr = w + (int64_t)tid * C;
+        float a = 0.f;
+        for (int c = 0; c < C; c++) a = fmaf(pooled[c], wr[c], a);
+        y = fmaf(a, alpha[tid], beta[tid]);
+        sq = y * y;
+    }
+    for (int off = 32; off > 0; off >>= 1) sq += __shfl_xor(sq, off);
+    if ((tid & 63) == 0) red[tid >> 6] = sq;
+    __syncthreads();
+    float tot = 0.f;
+    for (int i = 0; i < (int)(blockDim.x >> 6); i++) tot += red[i];
+    float nrm = fmaxf(sqrtf(tot), 1e-12f);
+    if (tid < D) out[(int64_t)n * D + tid] = __fdiv_rn(y, nrm);
+}
+
+void launch_facenet_head(const void* x, int N, int HW, int C, const float* w, const float* alpha, const float* beta,
+                         int D, float* out, bool bf16, hipStream_t st) {
+    size_t shm = (C + 8) * sizeof(float);
+    if (bf16)
+        k_facenet_head<__bf16><<<N, 512, shm, st>>>((const __bf16*)x, HW, C, w, alpha, beta, D, out);
+    else
+        k_facenet_head<float><<<N, 512, shm, st>>>((const float*)x, HW, C, w, alpha, beta, D, out);
+}
+
+}  // namespace vtf

@@ -1,0 +1,28 @@
+#pragma once
+#include "common.hpp"
+
+namespace vtf {
+
+struct ConvParams {
+    const void* in;      // NHWC [N,H,W,Cin], element type = precision
+    const void* w;       // [Cout][KH*KW*Cin]
+    void* out;           // NHWC, channel stride out_cstride, channel offset out_coff
+    const float* bias;   // conv bias (or null)
+    const float* alpha;  // BN scale (or null) -> v = v*alpha + beta
+    const float* beta;
+    const void* res;     // residual (NHWC, stride res_cstride) added after scale
+    float scale;
+    int relu;
+    int64_t M;           // N*OH*OW
+    int N, H, W, Cin, OH, OW, Cout, KH, KW, sh, sw, ph, pw, K;
+    int out_cstride, out_coff, res_cstride;
+};
+
+void launch_conv(const ConvParams& p, bool bf16, hipStream_t st);
+void launch_maxpool(const void* in, int N, int H, int W, int C, void* out, int out_cstride, int out_coff, bool bf16,
+                    hipStream_t st);
+void launch_nchw_to_nhwc(const float* in, int N, int C, int H, int W, int Cp, void* out, bool bf16, hipStream_t st);
+void launch_facenet_head(const void* x, int N, int HW, int C, const float* w, const float* alpha, const float* beta,
+                         int D, float* out, bool bf16, hipStream_t st);
+
+}  // namespace vtf

@@ -1,0 +1,384 @@
+// FaceNet (InceptionResnetV1) runtime: layer table, buffer plan, forward.
+// Mirrors src/videotofaces/encoders/facenet.py:10-183 layer for layer; every conv is one
+// launch of the implicit-GEMM kernel (conv.hip) with its BN/bias/residual/ReLU epilogue
+// fused; concatenations are written in place as channel slices.
+#include <cmath>
+#include <cstring>
+#include <vector>
+
+#include "blob.hpp"
+#include "common.hpp"
+#include "conv.hpp"
+
+namespace vtf {
+
+struct Layer {
+    int cin, cout, kh, kw, sh, sw, ph, pw;
+    bool bias;       // conv2d with bias (block tail) instead of ConvUnit (BN + ReLU)
+    int cin_pad;
+    void* w;         // [cout][kh*kw*cin_pad], element = precision
+    float* b;        // bias
+    float* alpha;    // BN
+    float* beta;
+};
+
+struct Facenet {
+    int device = 0;
+    bool bf16 = false;
+    hipStream_t st = 0;
+    std::vector<Layer> L;
+    float* head_w = nullptr;  // [512][1792] fp32
+    float* head_alpha = nullptr;
+    float* head_beta = nullptr;
+    std::vector<void*> allocs;
+    Arena ar;
+    ~Facenet() {
+        for (void* p : allocs) (void)hipFree(p);
+    }
+    template <class T>
+    T* upload(const std::vector<T>& v) {
+        void* p = nullptr;
+        VTF_HIP(hipMalloc(&p, v.size() * sizeof(T) + 16));
+        VTF_HIP(hipMemcpy(p, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice));
+        allocs.push_back(p);
+        return (T*)p;
+    }
+};
+
+// geometry of every conv in reference state_dict order (specs.py facenet_spec)
+struct G {
+    int cin, cout, kh, kw, sh, sw, ph, pw;
+    bool bias;
+};
+
+static std::vector<G> facenet_geometry() {
+    std::vector<G> g = {{3, 32, 3, 3, 2, 2, 0, 0, 0},    {32, 32, 3, 3, 1, 1, 0, 0, 0},
+                        {32, 64, 3, 3, 1, 1, 1, 1, 0},   {64, 80, 1, 1, 1, 1, 0, 0, 0},
+                        {80, 192, 3, 3, 1, 1, 0, 0, 0},  {192, 256, 3, 3, 2, 2, 0, 0, 0}};
+    for (int b = 0; b < 5; b++) {  // Block35
+        g.push_back({256, 32, 1, 1, 1, 1, 0, 0, 0});
+        g.push_back({256, 32, 1, 1, 1, 1, 0, 0, 0});
+        g.push_back({32, 32, 3, 3, 1, 1, 1, 1, 0});
+        g.push_back({256, 32, 1, 1, 1, 1, 0, 0, 0});
+        g.push_back({32, 32, 3, 3, 1, 1, 1, 1, 0});
+        g.push_back({32, 32, 3, 3, 1, 1, 1, 1, 0});
+        g.push_back({96, 256, 1, 1, 1, 1, 0, 0, 1});
+    }
+    g.push_back({256, 384, 3, 3, 2, 2, 0, 0, 0});  // Mixed_6a
+    g.push_back({256, 192, 1, 1, 1, 1, 0, 0, 0});
+    g.push_back({192, 192, 3, 3, 1, 1, 1, 1, 0});
+    g.push_back({192, 256, 3, 3, 2, 2, 0, 0, 0});
+    for (int b = 0; b < 10; b++) {  // Block17
+        g.push_back({896, 128, 1, 1, 1, 1, 0, 0, 0});
+        g.push_back({896, 128, 1, 1, 1, 1, 0, 0, 0});
+        g.push_back({128, 128, 1, 7, 1, 1, 0, 3, 0});
+        g.push_back({128, 128, 7, 1, 1, 1, 3, 0, 0});
+        g.push_back({256, 896, 1, 1, 1, 1, 0, 0, 1});
+    }
+    g.push_back({896, 256, 1, 1, 1, 1, 0, 0, 0});  // Mixed_7a
+    g.push_back({256, 384, 3, 3, 2, 2, 0, 0, 0});
+    g.push_back({896, 256, 1, 1, 1, 1, 0, 0, 0});
+    g.push_back({256, 256, 3, 3, 2, 2, 0, 0, 0});
+    g.push_back({896, 256, 1, 1, 1, 1, 0, 0, 0});
+    g.push_back({256, 256, 3, 3, 1, 1, 1, 1, 0});
+    g.push_back({256, 256, 3, 3, 2, 2, 0, 0, 0});
+    for (int b = 0; b < 6; b++) {  // 5 x Block8 + Block8(relu=False)
+        g.push_back({1792, 192, 1, 1, 1, 1, 0, 0, 0});
+        g.push_back({1792, 192, 1, 1, 1, 1, 0, 0, 0});
+        g.push_back({192, 192, 1, 3, 1, 1, 0, 1, 0});
+        g.push_back({192, 192, 3, 1, 1, 1, 1, 0, 0});
+        g.push_back({384, 1792, 1, 1, 1, 1, 0, 0, 1});
+    }
+    return g;
+}
+
+static void bn_fold(const float* w, const float* b, const float* mean, const float* var, int n, float eps,
+                    std::vector<float>& alpha, std::vector<float>& beta) {
+    alpha.resize(n);
+    beta.resize(n);
+    for (int i = 0; i < n; i++) {
+        alpha[i] = w[i] / std::sqrt(var[i] + eps);
+        beta[i] = b[i] - mean[i] * alpha[i];
+    }
+}
+
+static uint16_t f2bf(float f) {
+    uint32_t u = f2u(f);
+    if ((u & 0x7fffffff) > 0x7f800000) return (uint16_t)((u >> 16) | 0x40);  // NaN stays NaN
+    u += 0x7FFF + ((u >> 16) & 1);
+    return (uint16_t)(u >> 16);
+}
+
+static void build(Facenet& F, const float* params, int64_t n_params) {
+    std::vector<G> geo = facenet_geometry();
+    int64_t src = 0;
+    auto take = [&](int64_t n) {
+        VTF_CHECK(src + n <= n_params, VTF_E_ARG, "facenet: parameter buffer too small");
+        const float* p = params + src;
+        src += n;
+        return p;
+    };
+    for (const G& g : geo) {
+        Layer l{};
+        l.cin = g.cin;
+        l.cout = g.cout;
+        l.kh = g.kh;
+        l.kw = g.kw;
+        l.sh = g.sh;
+        l.sw = g.sw;
+        l.ph = g.ph;
+        l.pw = g.pw;
+        l.bias = g.bias;
+        l.cin_pad = (g.cin + 7) / 8 * 8;
+        const float* w = take((int64_t)g.cout * g.cin * g.kh * g.kw);
+        int K = g.kh * g.kw * l.cin_pad;
+        std::vector<float> wt((size_t)g.cout * K, 0.f);
+        for (int co = 0; co < g.cout; co++)
+            for (int ci = 0; ci < g.cin; ci++)
+                for (int y = 0; y < g.kh; y++)
+                    for (int x = 0; x < g.kw; x++)
+                        wt[(size_t)co * K + (y * g.kw + x) * l.cin_pad + ci] =
+                            w[(((size_t)co * g.cin + ci) * g.kh + y) * g.kw + x];
+        if (F.bf16) {
+            std::vector<uint16_t> wb(wt.size());
+            for (size_t i = 0; i < wt.size(); i++) wb[i] = f2bf(wt[i]);
+            l.w = F.upload(wb);
+        } else {
+            l.w = F.upload(wt);
+        }
+        if (g.bias) {
+            const float* b = take(g.cout);
+            l.b = F.upload(std::vector<float>(b, b + g.cout));
+        } else {
+            const float* bw = take(g.cout);
+            const float* bb = take(g.cout);
+            const float* bm = take(g.cout);
+            const float* bv = take(g.cout);
+            std::vector<float> a, be;
+            bn_fold(bw, bb, bm, bv, g.cout, 1e-3f, a, be);  // conv_unit BN eps 1e-3 (facenet.py:11)
+            l.alpha = F.upload(a);
+            l.beta = F.upload(be);
+        }
+        F.L.push_back(l);
+    }
+    const float* hw = take(512 * 1792);
+    F.head_w = F.upload(std::vector<float>(hw, hw + 512 * 1792));
+    const float* bw = take(512);
+    const float* bb = take(512);
+    const float* bm = take(512);
+    const float* bv = take(512);
+    std::vector<float> a, be;
+    bn_fold(bw, bb, bm, bv, 512, 1e-3f, a, be);  // BatchNorm1d(512, 0.001) (facenet.py:147)
+    F.head_alpha = F.upload(a);
+    F.head_beta = F.upload(be);
+    VTF_CHECK(src == n_params, VTF_E_ARG, "facenet: expected 23512224 parameters");
+}
+
+struct Act {
+    void* p;
+    int H, W, C;
+};
+
+static void conv(Facenet& F, int li, const Act& in, int N, void* out, int out_cstride, int out_coff,
+                 const void* res = nullptr, float scale = 1.f, bool relu = true, Act* out_act = nullptr) {
+    const Layer& l = F.L[li];
+    VTF_CHECK(in.C == l.cin_pad, VTF_E_ARG, "facenet: channel mismatch");
+    ConvParams p{};
+    p.in = in.p;
+    p.w = l.w;
+    p.out = out;
+    p.N = N;
+    p.H = in.H;
+    p.W = in.W;
+    p.Cin = l.cin_pad;
+    p.KH = l.kh;
+    p.KW = l.kw;
+    p.sh = l.sh;
+    p.sw = l.sw;
+    p.ph = l.ph;
+    p.pw = l.pw;
+    p.OH = (in.H + 2 * l.ph - l.kh) / l.sh + 1;
+    p.OW = (in.W + 2 * l.pw - l.kw) / l.sw + 1;
+    p.Cout = l.cout;
+    p.K = l.kh * l.kw * l.cin_pad;
+    p.M = (int64_t)N * p.OH * p.OW;
+    p.out_cstride = out_cstride;
+    p.out_coff = out_coff;
+    if (l.bias) {
+        p.bias = l.b;
+        p.scale = scale;
+        p.res = res;
+        p.res_cstride = l.cout;
+        p.relu = relu;
+    } else {
+        p.alpha = l.alpha;
+        p.beta = l.beta;
+        p.scale = 1.f;
+        p.relu = 1;
+    }
+    launch_conv(p, F.bf16, F.st);
+    if (out_act) *out_act = Act{out, p.OH, p.OW, out_cstride};
+}
+
+// x: NHWC [N,160,160,8] (precision dtype) -> emb [N,512] fp32
+static void forward(Facenet& F, const void* x, int N, float* emb) {
+    const size_t es = F.bf16 ? 2 : 4;
+    const size_t big = (size_t)N * 77 * 77 * 64;  // largest activation (stem conv2)
+    const size_t tmp = (size_t)N * 17 * 17 * 192;  // largest branch temp (Mixed_6a)
+    const size_t cat = (size_t)N * 17 * 17 * 96;
+    void* P0 = F.ar.get(0, big * es);
+    void* P1 = F.ar.get(1, big * es);
+    void* T1 = F.ar.get(2, tmp * es);
+    void* T2 = F.ar.get(3, tmp * es);
+    void* CAT = F.ar.get(4, cat * es);
+    Act a{(void*)x, 160, 160, 8}, b{};
+    int li = 0;
+    // stem (facenet.py:126-134)
+    conv(F, li++, a, N, P0, 32, 0, nullptr, 1.f, true, &b);
+    conv(F, li++, b, N, P1, 32, 0, nullptr, 1.f, true, &a);
+    conv(F, li++, a, N, P0, 64, 0, nullptr, 1.f, true, &b);
+    launch_maxpool(P0, N, b.H, b.W, 64, P1, 64, 0, F.bf16, F.st);
+    a = Act{P1, (b.H - 3) / 2 + 1, (b.W - 3) / 2 + 1, 64};
+    conv(F, li++, a, N, P0, 80, 0, nullptr, 1.f, true, &b);
+    conv(F, li++, b, N, P1, 192, 0, nullptr, 1.f, true, &a);
+    conv(F, li++, a, N, P0, 256, 0, nullptr, 1.f, true, &b);
+    Act X = b;
+    void* Y = P1;
+    auto swap = [&](int C) {
+        void* old = X.p;
+        X.p = Y;
+        X.C = C;
+        Y = old;
+    };
+    Act t1{}, t2{};
+    // 5 x Block35 (facenet.py:14-33), scale 0.17
+    for (int k = 0; k < 5; k++) {
+        conv(F, li++, X, N, CAT, 96, 0);
+        conv(F, li++, X, N, T1, 32, 0, nullptr, 1.f, true, &t1);
+        conv(F, li++, t1, N, CAT, 96, 32);
+        conv(F, li++, X, N, T1, 32, 0, nullptr, 1.f, true, &t1);
+        conv(F, li++, t1, N, T2, 32, 0, nullptr, 1.f, true, &t2);
+        conv(F, li++, t2, N, CAT, 96, 64);
+        conv(F, li++, Act{CAT, X.H, X.W, 96}, N, Y, 256, 0, X.p, 0.17f, true);
+        swap(256);
+    }
+    // Mixed_6a (facenet.py:84-101)
+    {
+        Act o{};
+        conv(F, li++, X, N, Y, 896, 0, nullptr, 1.f, true, &o);
+        conv(F, li++, X, N, T1, 192, 0, nullptr, 1.f, true, &t1);
+        conv(F, li++, t1, N, T2, 192, 0, nullptr, 1.f, true, &t2);
+        conv(F, li++, t2, N, Y, 896, 384);
+        launch_maxpool(X.p, N, X.H, X.W, 256, Y, 896, 640, F.bf16, F.st);
+        X.H = o.H;
+        X.W = o.W;
+        swap(896);
+    }
+    // 10 x Block17 (facenet.py:36-56), scale 0.10
+    for (int k = 0; k < 10; k++) {
+        conv(F, li++, X, N, CAT, 256, 0);
+        conv(F, li++, X, N, T1, 128, 0, nullptr, 1.f, true, &t1);
+        conv(F, li++, t1, N, T2, 128, 0, nullptr, 1.f, true, &t2);
+        conv(F, li++, t2, N, CAT, 256, 128);
+        conv(F, li++, Act{CAT, X.H, X.W, 256}, N, Y, 896, 0, X.p, 0.10f, true);
+        swap(896);
+    }
+    // Mixed_7a (facenet.py:104-120)
+    {
+        Act o{};
+        conv(F, li++, X, N, T1, 256, 0, nullptr, 1.f, true, &t1);
+        conv(F, li++, t1, N, Y, 1792, 0, nullptr, 1.f, true, &o);
+        conv(F, li++, X, N, T1, 256, 0, nullptr, 1.f, true, &t1);
+        conv(F, li++, t1, N, Y, 1792, 384);
+        conv(F, li++, X, N, T1, 256, 0, nullptr, 1.f, true, &t1);
+        conv(F, li++, t1, N, T2, 256, 0, nullptr, 1.f, true, &t2);
+        conv(F, li++, t2, N, Y, 1792, 640);
+        launch_maxpool(X.p, N, X.H, X.W, 896, Y, 1792, 896, F.bf16, F.st);
+        X.H = o.H;
+        X.W = o.W;
+        swap(1792);
+    }
+    // 5 x Block8 (scale 0.20) + Block8(scale 1.0, relu=False) (facenet.py:59-81,142-143)
+    for (int k = 0; k < 6; k++) {
+        bool last = k == 5;
+        conv(F, li++, X, N, CAT, 384, 0);
+        conv(F, li++, X, N, T1, 192, 0, nullptr, 1.f, true, &t1);
+        conv(F, li++, t1, N, T2, 192, 0, nullptr, 1.f, true, &t2);
+        conv(F, li++, t2, N, CAT, 384, 192);
+        conv(F, li++, Act{CAT, X.H, X.W, 384}, N, Y, 1792, 0, X.p, last ? 1.0f : 0.20f, !last);
+        swap(1792);
+    }
+    VTF_CHECK(li == (int)F.L.size(), VTF_E_ARG, "facenet: layer walk mismatch");
+    // AdaptiveAvgPool2d(1) + Linear + BatchNorm1d + F.normalize (facenet.py:144-153)
+    launch_facenet_head(X.p, N, X.H * X.W, 1792, F.head_w, F.head_alpha, F.head_beta, 512, emb, F.bf16, F.st);
+}
+
+}  // namespace vtf
+
+using namespace vtf;
+
+struct vtf_facenet_s {
+    Facenet f;
+};
+
+extern "C" {
+
+int vtf_facenet_create(const float* params, int64_t n_params, int device, int precision, vtf_facenet_t* out) {
+    return guarded([&] {
+        VTF_CHECK(params && out && (precision == 0 || precision == 1), VTF_E_ARG, "bad argument");
+        VTF_HIP(hipSetDevice(device));
+        auto* h = new vtf_facenet_s();
+        h->f.device = device;
+        h->f.bf16 = precision == 1;
+        try {
+            build(h->f, params, n_params);
+        } catch (...) {
+            delete h;
+            throw;
+        }
+        *out = h;
+    });
+}
+
+int vtf_facenet_destroy(vtf_facenet_t h) {
+    return guarded([&] { delete h; });
+}
+
+int vtf_facenet_set_stream(vtf_facenet_t h, void* stream) {
+    return guarded([&] {
+        VTF_CHECK(h, VTF_E_ARG, "null handle");
+        h->f.st = (hipStream_t)stream;
+    });
+}
+
+int vtf_facenet_forward(vtf_facenet_t h, const float* d_x, int64_t N, float* d_emb) {
+    return guarded([&] {
+        VTF_CHECK(h && N >= 0, VTF_E_ARG, "bad argument");
+        if (N == 0) return;
+        VTF_CHECK(d_x && d_emb, VTF_E_ARG, "null argument");
+        Facenet& F = h->f;
+        void* xin = F.ar.get(5, (size_t)N * 160 * 160 * 8 * (F.bf16 ? 2 : 4));
+        launch_nchw_to_nhwc(d_x, (int)N, 3, 160, 160, 8, xin, F.bf16, F.st);
+        forward(F, xin, (int)N, d_emb);
+        VTF_HIP(hipGetLastError());
+    });
+}
+
+int vtf_facenet_encode_crops(vtf_facenet_t h, const uint8_t* d_frames, int H, int W, int64_t frame_stride,
+                             int64_t row_stride, const int32_t* crops, int64_t N, float* d_emb) {
+    return guarded([&] {
+        VTF_CHECK(h && N >= 0, VTF_E_ARG, "bad argument");
+        if (N == 0) return;
+        VTF_CHECK(d_frames && crops && d_emb, VTF_E_ARG, "null argument");
+        Facenet& F = h->f;
+        int32_t* dc = F.ar.get<int32_t>(6, N * 5);
+        VTF_HIP(hipMemcpyAsync(dc, crops, N * 5 * 4, hipMemcpyHostToDevice, F.st));
+        void* xin = F.ar.get(5, (size_t)N * 160 * 160 * 8 * (F.bf16 ? 2 : 4));
+        // blobFromImages(images, 1/128, (160,160), (127.5,)*3, swapRB=True) (facenet.py:179)
+        launch_blob(d_frames, H, W, frame_stride, row_stride, dc, N, 160, 127.5f, 0.0078125f, 1, 8, F.bf16, xin, F.st);
+        forward(F, xin, (int)N, d_emb);
+        VTF_HIP(hipGetLastError());
+    });
+}
+
+}  // extern "C"

@@ -1,0 +1,205 @@
+// Grouping math on gfx950: cosine-distance dedupe and classification.
+//
+// remove_dupes_overall 'enc' (src/videotofaces/dupes.py:51-68) computes
+//   D = sklearn cosine_distances(X)               (N x N, materialised, + an fp64 N x N tri)
+//   D += (1 - tri(N, k=-1)) * 10000 ; mins = D.min(1) ; inds = D.argmin(1)
+// i.e. for each face i: min / first argmin over EARLIER faces j < i of clip(1 - <xi,xj>, 0, 2)
+// with xi = X_i / ||X_i|| (sklearn normalize: zero norm -> 1).  Row 0 has no earlier face:
+// its masked row gives min 10000 at index 0.
+// Here: one fused kernel, fp32 MFMA (v_mfma_f32_16x16x4_f32) over 128x128 lower-triangle
+// tiles, distance + clip + row-min in the epilogue, and one 64-bit atomicMin per (row, tile)
+// on the key (dist bits << 32 | j): dist >= 0 so float bits order like the floats, and ties
+// resolve to the smallest j = numpy's first argmin.  Nothing N x N ever touches HBM.
+// classify (grouping.py:50-66): argmin / min over C references of cosine distance.
+#include "common.hpp"
+
+namespace vtf {
+
+typedef __attribute__((ext_vector_type(4))) float f32x4;
+
+// Xn [N][Dp] = X / ||X|| (zero norm -> 1), zero-padded to Dp
+__global__ void k_row_normalize(const float* __restrict__ X, int64_t N, int D, int Dp, float* __restrict__ Xn) {
+    int64_t i = blockIdx.x;
+    if (i >= N) return;
+    const float* x = X + i * D;
+    float s = 0.f;
+    for (int k = threadIdx.x; k < D; k += blockDim.x) s = fmaf(x[k], x[k], s);
+    __shared__ float red[4];
+    for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+    __syncthreads();
+    float tot = 0.f;
+    for (int w = 0; w < (int)(blockDim.x >> 6); w++) tot += red[w];
+    float nrm = sqrtf(tot);
+    if (nrm == 0.f) nrm = 1.f;
+    for (int k = threadIdx.x; k < Dp; k += blockDim.x) Xn[i * Dp + k] = k < D ? __fdiv_rn(x[k], nrm) : 0.f;
+}
+
+__global__ void k_init_keys(uint64_t* key, int64_t N) {
+    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < N) key[i] = ~0ull;
+}
+
+constexpr int CT = 128, CK = 32, CLD = CK + 4;
+
+// grid.x enumerates lower-triangle tile pairs (bi >= bj)
+__global__ __launch_bounds__(256) void k_cos_dedupe(const float* __restrict__ Xn, int64_t N, int Dp,
+                                                    uint64_t* __restrict__ key) {
+    __shared__ __attribute__((aligned(16))) float As[CT * CLD];
+    __shared__ __attribute__((aligned(16))) float Bs[CT * CLD];
+    // tile pair from linear index t: bi = floor((sqrt(8t+1)-1)/2), bj = t - bi(bi+1)/2
+    int64_t t = blockIdx.x;
+    int64_t bi = (int64_t)((sqrt(8.0 * (double)t + 1.0) - 1.0) * 0.5);
+    while ((bi + 1) * (bi + 2) / 2 <= t) bi++;
+    while (bi * (bi + 1) / 2 > t) bi--;
+    int64_t bj = t - bi * (bi + 1) / 2;
+    const int64_t i0 = bi * CT, j0 = bj * CT;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wm = wave >> 1, wn = wave & 1;
+    f32x4 acc[4][4];
+#pragma unroll
+    for (int a = 0; a < 4; a++)
+#pragma unroll
+        for (int b = 0; b < 4; b++) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int k0 = 0; k0 < Dp; k0 += CK) {
+        // 128 rows x 32 floats per operand = 1024 float4; 4 per thread
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+            int v = tid + 256 * r;
+            int row = v >> 3, kq = (v & 7) * 4;
+            f32x4 a = {}, b = {};
+            if (i0 + row < N) a = *(const f32x4*)(Xn + (i0 + row) * Dp + k0 + kq);
+            if (j0 + row < N) b = *(const f32x4*)(Xn + (j0 + row) * Dp + k0 + kq);
+            *(f32x4*)(As + row * CLD + kq) = a;
+            *(f32x4*)(Bs + row * CLD + kq) = b;
+        }
+        __syncthreads();
+        const float* Aw = As + (wm * 64 + (lane & 15)) * CLD + (lane >> 4);
+        const float* Bw = Bs + (wn * 64 + (lane & 15)) * CLD + (lane >> 4);
+#pragma unroll
+        for (int ks = 0; ks < CK; ks += 4) {
+            float af[4], bfr[4];
+#pragma unroll
+            for (int a = 0; a < 4; a++) af[a] = Aw[a * 16 * CLD + ks];
+#pragma unroll
+            for (int b = 0; b < 4; b++) bfr[b] = Bw[b * 16 * CLD + ks];
+#pragma unroll
+            for (int a = 0; a < 4; a++)
+#pragma unroll
+                for (int b = 0; b < 4; b++)
+                    acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[a], bfr[b], acc[a][b], 0, 0, 0);
+        }
+        __syncthreads();
+    }
+    // epilogue: row i = i0 + wm*64 + a*16 + 4*(lane>>4) + q, col j = j0 + wn*64 + b*16 + (lane&15)
+#pragma unroll
+    for (int a = 0; a < 4; a++) {
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            int64_t i = i0 + wm * 64 + a * 16 + 4 * (lane >> 4) + q;
+            uint64_t best = ~0ull;
+#pragma unroll
+            for (int b = 0; b < 4; b++) {
+                int64_t j = j0 + wn * 64 + b * 16 + (lane & 15);
+                if (i < N && j < i) {
+                    float d = 1.0f - acc[a][b][q];
+                    d = fminf(fmaxf(d, 0.f), 2.f);
+                    uint64_t k = ((uint64_t)f2u(d) << 32) | (uint64_t)j;
+                    best = k < best ? k : best;
+                }
+            }
+            // reduce across the 16 lanes that share this row (lane & 15 varies)
+#pragma unroll
+            for (int off = 1; off < 16; off <<= 1) {
+                uint32_t lo = __shfl_xor((uint32_t)best, off), hi = __shfl_xor((uint32_t)(best >> 32), off);
+                uint64_t o = ((uint64_t)hi << 32) | lo;
+                best = o < best ? o : best;
+            }
+            if ((lane & 15) == 0 && best != ~0ull) atomicMin((unsigned long long*)&key[i], (unsigned long long)best);
+        }
+    }
+}
+
+__global__ void k_unpack(const uint64_t* __restrict__ key, int64_t N, float* __restrict__ mn, int64_t* __restrict__ arg) {
+    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= N) return;
+    uint64_t k = key[i];
+    if (k == ~0ull) {  // row 0: every entry masked -> 0 + 10000 at j = 0
+        mn[i] = 10000.f;
+        arg[i] = 0;
+    } else {
+        mn[i] = __builtin_bit_cast(float, (uint32_t)(k >> 32));
+        arg[i] = (int64_t)(uint32_t)k;
+    }
+}
+
+__global__ void k_classify(const float* __restrict__ Xn, const float* __restrict__ Rn, int64_t N, int C, int Dp,
+                           float* __restrict__ mn, int64_t* __restrict__ arg) {
+    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= N) return;
+    float best = 3.4e38f;
+    int bk = 0;
+    for (int c = 0; c < C; c++) {
+        float s = 0.f;
+        for (int k = 0; k < Dp; k++) s = fmaf(Xn[i * Dp + k], Rn[(int64_t)c * Dp + k], s);
+        float d = fminf(fmaxf(1.0f - s, 0.f), 2.f);
+        if (d < best) {
+            best = d;
+            bk = c;
+        }
+    }
+    mn[i] = best;
+    arg[i] = bk;
+}
+
+static Arena& grouping_arena() {
+    static Arena a;
+    return a;
+}
+
+}  // namespace vtf
+
+using namespace vtf;
+
+extern "C" {
+
+int vtf_cosine_dedupe(const float* d_X, int64_t N, int64_t D, float* d_min, int64_t* d_arg, void* hip_stream) {
+    return guarded([&] {
+        VTF_CHECK(N >= 0 && D > 0, VTF_E_ARG, "bad argument");
+        if (N == 0) return;
+        VTF_CHECK(d_X && d_min && d_arg && N < (int64_t)1 << 31, VTF_E_ARG, "bad argument");
+        hipStream_t st = (hipStream_t)hip_stream;
+        Arena& ar = grouping_arena();
+        int Dp = (int)((D + CK - 1) / CK * CK);
+        float* Xn = ar.get<float>(0, N * Dp);
+        uint64_t* key = ar.get<uint64_t>(1, N);
+        k_row_normalize<<<(unsigned)N, 256, 0, st>>>(d_X, N, (int)D, Dp, Xn);
+        k_init_keys<<<cdiv(N, 256), 256, 0, st>>>(key, N);
+        int64_t nt = (N + CT - 1) / CT;
+        int64_t pairs = nt * (nt + 1) / 2;
+        VTF_CHECK(pairs < (int64_t)1 << 31, VTF_E_LIMIT, "cosine_dedupe: N too large");
+        k_cos_dedupe<<<(unsigned)pairs, 256, 0, st>>>(Xn, N, Dp, key);
+        k_unpack<<<cdiv(N, 256), 256, 0, st>>>(key, N, d_min, d_arg);
+        VTF_HIP(hipGetLastError());
+    });
+}
+
+int vtf_cosine_classify(const float* d_X, int64_t N, const float* d_R, int64_t C, int64_t D, float* d_min,
+                        int64_t* d_arg, void* hip_stream) {
+    return guarded([&] {
+        VTF_CHECK(N >= 0 && C > 0 && D > 0, VTF_E_ARG, "bad argument");
+        if (N == 0) return;
+        VTF_CHECK(d_X && d_R && d_min && d_arg, VTF_E_ARG, "null argument");
+        hipStream_t st = (hipStream_t)hip_stream;
+        Arena& ar = grouping_arena();
+        int Dp = (int)((D + CK - 1) / CK * CK);
+        float* Xn = ar.get<float>(2, N * Dp);
+        float* Rn = ar.get<float>(3, C * Dp);
+        k_row_normalize<<<(unsigned)N, 256, 0, st>>>(d_X, N, (int)D, Dp, Xn);
+        k_row_normalize<<<(unsigned)C, 256, 0, st>>>(d_R, C, (int)D, Dp, Rn);
+        k_classify<<<cdiv(N, 128), 128, 0, st>>>(Xn, Rn, N, (int)C, Dp, d_min, d_arg);
+        VTF_HIP(hipGetLastError());
+    });
+}
+
+}  // extern "C"

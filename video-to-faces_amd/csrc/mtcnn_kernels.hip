@@ -74,6 +74,26 @@ __device__ inline bool crop_rect(float4 b, int H, int W, int& y0, int& x0, int& 
     return true;
 }
 
+// constant-address-space views of the weight structs (scalar loads, see common.hpp)
+#define CW const VTF_CONST float*
+struct PNetWC { CW c1w; CW c1b; CW p1; CW c2w; CW c2b; CW p2; CW c3w; CW c3b; CW p3; CW c41w; CW c41b; CW c42w; CW c42b; };
+struct RNetWC { CW c1w; CW c1b; CW p1; CW c2w; CW c2b; CW p2; CW c3w; CW c3b; CW p3; CW d4w; CW d4b; CW p4; CW d51w; CW d51b; CW d52w; CW d52b; };
+struct ONetWC { CW c1w; CW c1b; CW p1; CW c2w; CW c2b; CW p2; CW c3w; CW c3b; CW p3; CW c4w; CW c4b; CW p4; CW d5w; CW d5b; CW p5; CW d61w; CW d61b; CW d62w; CW d62b; CW d63w; CW d63b; };
+#undef CW
+__device__ inline PNetWC to_const(const PNetW& w) {
+    return {cptr(w.c1w), cptr(w.c1b), cptr(w.p1), cptr(w.c2w), cptr(w.c2b), cptr(w.p2), cptr(w.c3w), cptr(w.c3b),
+            cptr(w.p3), cptr(w.c41w), cptr(w.c41b), cptr(w.c42w), cptr(w.c42b)};
+}
+__device__ inline RNetWC to_const(const RNetW& w) {
+    return {cptr(w.c1w), cptr(w.c1b), cptr(w.p1), cptr(w.c2w), cptr(w.c2b), cptr(w.p2), cptr(w.c3w), cptr(w.c3b),
+            cptr(w.p3), cptr(w.d4w), cptr(w.d4b), cptr(w.p4), cptr(w.d51w), cptr(w.d51b), cptr(w.d52w), cptr(w.d52b)};
+}
+__device__ inline ONetWC to_const(const ONetW& w) {
+    return {cptr(w.c1w), cptr(w.c1b), cptr(w.p1),  cptr(w.c2w),  cptr(w.c2b),  cptr(w.p2),  cptr(w.c3w),
+            cptr(w.c3b), cptr(w.p3),  cptr(w.c4w), cptr(w.c4b),  cptr(w.p4),   cptr(w.d5w), cptr(w.d5b),
+            cptr(w.p5),  cptr(w.d61w), cptr(w.d61b), cptr(w.d62w), cptr(w.d62b), cptr(w.d63w), cptr(w.d63b)};
+}
+
 // ----------------------------------------------------------------------------------- resample
 
 __global__ void k_resample(const uint8_t* __restrict__ frames, int64_t frame_stride, int64_t row_stride, int B,
@@ -108,7 +128,8 @@ constexpr int P_A = P_C2 > P_LVL ? P_C2 : P_LVL;
 template <bool DENSE>
 __global__ __launch_bounds__(256) void k_pnet(const uint8_t* __restrict__ frames, int64_t frame_stride,
                                               int64_t row_stride, int H, int W, const PNetLevel* __restrict__ lv,
-                                              int n_levels, PNetW w, PNetOut o) {
+                                              int n_levels, PNetW wg, PNetOut o) {
+    const auto wc = to_const(wg);
     __shared__ float sA[P_A];     // level tile, later conv2 output
     __shared__ float sP[P_POOL];  // pooled conv1
     const int tid = threadIdx.x;
@@ -125,15 +146,35 @@ __global__ __launch_bounds__(256) void k_pnet(const uint8_t* __restrict__ frames
     const uint8_t* fr = frames + (int64_t)b * frame_stride;
     const int L1h = P.lh - 2, L1w = P.lw - 2;
 
-    // 1. level tile (rows 2*oy0 .. +42, cols 2*ox0 .. +74), zero outside the level
-    for (int i = tid; i < P_LVL; i += 256) {
-        int c = i / (PL_H * PL_W);
-        int r = (i / PL_W) % PL_H;
-        int q = i % PL_W;
-        int ly = 2 * oy0 + r, lx = 2 * ox0 + q;
-        float v = 0.f;
-        if (ly < P.lh && lx < P.lw) v = level_value(fr, row_stride, c, ly, lx, H, W, P.lh, P.lw);
-        sA[i] = v;
+    // 1. level tile (rows 2*oy0 .. +42, cols 2*ox0 .. +74), zero outside the level.
+    //    Bin bounds of adaptive_avg_pool2d are tabulated once per tile.
+    __shared__ int2 ybin[PL_H], xbin[PL_W];
+    if (tid < PL_H) {
+        int ly = 2 * oy0 + tid;
+        ybin[tid] = ly < P.lh ? make_int2((ly * H) / P.lh, ((ly + 1) * H + P.lh - 1) / P.lh) : make_int2(0, 0);
+    } else if (tid < PL_H + PL_W) {
+        int q = tid - PL_H, lx = 2 * ox0 + q;
+        xbin[q] = lx < P.lw ? make_int2((lx * W) / P.lw, ((lx + 1) * W + P.lw - 1) / P.lw) : make_int2(0, 0);
+    }
+    __syncthreads();
+    for (int i = tid; i < PL_H * PL_W; i += 256) {
+        int r = i / PL_W, q = i - r * PL_W;
+        int2 yb = ybin[r], xb = xbin[q];
+        float s0 = 0.f, s1 = 0.f, s2 = 0.f;
+        for (int y = yb.x; y < yb.y; y++) {
+            const uint8_t* row = fr + (int64_t)y * row_stride;
+            for (int x = xb.x; x < xb.y; x++) {
+                const uint8_t* px = row + x * 3;  // BGR
+                s0 = s0 + ((float)px[2] - 127.5f) * 0.0078125f;
+                s1 = s1 + ((float)px[1] - 127.5f) * 0.0078125f;
+                s2 = s2 + ((float)px[0] - 127.5f) * 0.0078125f;
+            }
+        }
+        float kh = (float)(yb.y - yb.x), kw = (float)(xb.y - xb.x);
+        bool in = yb.y > yb.x && xb.y > xb.x;
+        sA[i] = in ? __fdiv_rn(__fdiv_rn(s0, kh), kw) : 0.f;
+        sA[PL_H * PL_W + i] = in ? __fdiv_rn(__fdiv_rn(s1, kh), kw) : 0.f;
+        sA[2 * PL_H * PL_W + i] = in ? __fdiv_rn(__fdiv_rn(s2, kh), kw) : 0.f;
     }
     __syncthreads();
 
@@ -151,7 +192,7 @@ __global__ __launch_bounds__(256) void k_pnet(const uint8_t* __restrict__ frames
 #pragma unroll
         for (int k = 0; k < 4; k++)
 #pragma unroll
-            for (int co = 0; co < 10; co++) acc[k][co] = w.c1b[co];
+            for (int co = 0; co < 10; co++) acc[k][co] = wc.c1b[co];
 #pragma unroll
         for (int c = 0; c < 3; c++)
 #pragma unroll
@@ -160,7 +201,7 @@ __global__ __launch_bounds__(256) void k_pnet(const uint8_t* __restrict__ frames
                 for (int kx = 0; kx < 3; kx++)
 #pragma unroll
                     for (int co = 0; co < 10; co++) {
-                        float wv = w.c1w[((c * 3 + ky) * 3 + kx) * 10 + co];
+                        float wv = wc.c1w[((c * 3 + ky) * 3 + kx) * 10 + co];
 #pragma unroll
                         for (int k = 0; k < 4; k++) acc[k][co] = fmaf(in[c][ky + (k >> 1)][kx + (k & 1)], wv, acc[k][co]);
                     }
@@ -171,7 +212,7 @@ __global__ __launch_bounds__(256) void k_pnet(const uint8_t* __restrict__ frames
 #pragma unroll
             for (int k = 0; k < 4; k++) {
                 bool ok = (gy + (k >> 1) < L1h) && (gx + (k & 1) < L1w);
-                float v = prelu(acc[k][co], w.p1[co]);
+                float v = prelu(acc[k][co], wc.p1[co]);
                 if (ok) m = fmaxf(m, v);
             }
             sP[(co * PP_H + py) * PP_W + px] = m;
@@ -184,20 +225,20 @@ __global__ __launch_bounds__(256) void k_pnet(const uint8_t* __restrict__ frames
         int y = i / PC_W, x = i % PC_W;
         float acc[16];
 #pragma unroll
-        for (int co = 0; co < 16; co++) acc[co] = w.c2b[co];
+        for (int co = 0; co < 16; co++) acc[co] = wc.c2b[co];
         for (int c = 0; c < 10; c++) {
 #pragma unroll
             for (int ky = 0; ky < 3; ky++)
 #pragma unroll
                 for (int kx = 0; kx < 3; kx++) {
                     float v = sP[(c * PP_H + y + ky) * PP_W + x + kx];
-                    const float* wp = w.c2w + ((c * 3 + ky) * 3 + kx) * 16;
+                    const VTF_CONST float* wp = wc.c2w + ((c * 3 + ky) * 3 + kx) * 16;
 #pragma unroll
                     for (int co = 0; co < 16; co++) acc[co] = fmaf(v, wp[co], acc[co]);
                 }
         }
 #pragma unroll
-        for (int co = 0; co < 16; co++) sA[(co * PC_H + y) * PC_W + x] = prelu(acc[co], w.p2[co]);
+        for (int co = 0; co < 16; co++) sA[(co * PC_H + y) * PC_W + x] = prelu(acc[co], wc.p2[co]);
     }
     __syncthreads();
 
@@ -206,29 +247,29 @@ __global__ __launch_bounds__(256) void k_pnet(const uint8_t* __restrict__ frames
         int y = i / PT_W, x = i % PT_W;
         float acc[32];
 #pragma unroll
-        for (int co = 0; co < 32; co++) acc[co] = w.c3b[co];
+        for (int co = 0; co < 32; co++) acc[co] = wc.c3b[co];
         for (int c = 0; c < 16; c++) {
 #pragma unroll
             for (int ky = 0; ky < 3; ky++)
 #pragma unroll
                 for (int kx = 0; kx < 3; kx++) {
                     float v = sA[(c * PC_H + y + ky) * PC_W + x + kx];
-                    const float* wp = w.c3w + ((c * 3 + ky) * 3 + kx) * 32;
+                    const VTF_CONST float* wp = wc.c3w + ((c * 3 + ky) * 3 + kx) * 32;
 #pragma unroll
                     for (int co = 0; co < 32; co++) acc[co] = fmaf(v, wp[co], acc[co]);
                 }
         }
-        float a0 = w.c41b[0], a1 = w.c41b[1];
-        float r0 = w.c42b[0], r1 = w.c42b[1], r2 = w.c42b[2], r3 = w.c42b[3];
+        float a0 = wc.c41b[0], a1 = wc.c41b[1];
+        float r0 = wc.c42b[0], r1 = wc.c42b[1], r2 = wc.c42b[2], r3 = wc.c42b[3];
 #pragma unroll
         for (int k = 0; k < 32; k++) {
-            float f = prelu(acc[k], w.p3[k]);
-            a0 = fmaf(f, w.c41w[k], a0);
-            a1 = fmaf(f, w.c41w[32 + k], a1);
-            r0 = fmaf(f, w.c42w[k], r0);
-            r1 = fmaf(f, w.c42w[32 + k], r1);
-            r2 = fmaf(f, w.c42w[64 + k], r2);
-            r3 = fmaf(f, w.c42w[96 + k], r3);
+            float f = prelu(acc[k], wc.p3[k]);
+            a0 = fmaf(f, wc.c41w[k], a0);
+            a1 = fmaf(f, wc.c41w[32 + k], a1);
+            r0 = fmaf(f, wc.c42w[k], r0);
+            r1 = fmaf(f, wc.c42w[32 + k], r1);
+            r2 = fmaf(f, wc.c42w[64 + k], r2);
+            r3 = fmaf(f, wc.c42w[96 + k], r3);
         }
         float mx = fmaxf(a0, a1);
         float e0 = expf(a0 - mx), e1 = expf(a1 - mx);
@@ -291,8 +332,9 @@ template <bool FROM_FRAMES>
 __global__ __launch_bounds__(256) void k_rnet(const uint8_t* __restrict__ frames, int64_t frame_stride,
                                               int64_t row_stride, int H, int W, const float4* __restrict__ boxes,
                                               const int32_t* __restrict__ img, const float* __restrict__ xin,
-                                              RNetW w, float4* __restrict__ reg_out, float* __restrict__ prob_out,
+                                              RNetW wg, float4* __restrict__ reg_out, float* __restrict__ prob_out,
                                               int32_t* __restrict__ err) {
+    const auto wc = to_const(wg);
     __shared__ float sA[13552];
     __shared__ float sB[3388];
     __shared__ float sC[1728];
@@ -318,7 +360,7 @@ __global__ __launch_bounds__(256) void k_rnet(const uint8_t* __restrict__ frames
         int y = i / 22, x = i % 22;
         float acc[28];
 #pragma unroll
-        for (int co = 0; co < 28; co++) acc[co] = w.c1b[co];
+        for (int co = 0; co < 28; co++) acc[co] = wc.c1b[co];
 #pragma unroll
         for (int c = 0; c < 3; c++)
 #pragma unroll
@@ -326,12 +368,12 @@ __global__ __launch_bounds__(256) void k_rnet(const uint8_t* __restrict__ frames
 #pragma unroll
                 for (int kx = 0; kx < 3; kx++) {
                     float v = sC[(c * 24 + y + ky) * 24 + x + kx];
-                    const float* wp = w.c1w + ((c * 3 + ky) * 3 + kx) * 28;
+                    const VTF_CONST float* wp = wc.c1w + ((c * 3 + ky) * 3 + kx) * 28;
 #pragma unroll
                     for (int co = 0; co < 28; co++) acc[co] = fmaf(v, wp[co], acc[co]);
                 }
 #pragma unroll
-        for (int co = 0; co < 28; co++) sA[co * 484 + i] = prelu(acc[co], w.p1[co]);
+        for (int co = 0; co < 28; co++) sA[co * 484 + i] = prelu(acc[co], wc.p1[co]);
     }
     __syncthreads();
     // maxpool 3/2 ceil: 22 -> 11
@@ -352,20 +394,20 @@ __global__ __launch_bounds__(256) void k_rnet(const uint8_t* __restrict__ frames
         int y = pos / 9, x = pos % 9;
         float acc[16];
 #pragma unroll
-        for (int k = 0; k < 16; k++) acc[k] = w.c2b[g * 16 + k];
+        for (int k = 0; k < 16; k++) acc[k] = wc.c2b[g * 16 + k];
         for (int c = 0; c < 28; c++) {
 #pragma unroll
             for (int ky = 0; ky < 3; ky++)
 #pragma unroll
                 for (int kx = 0; kx < 3; kx++) {
                     float v = sB[c * 121 + (y + ky) * 11 + x + kx];
-                    const float* wp = w.c2w + ((c * 3 + ky) * 3 + kx) * 48 + g * 16;
+                    const VTF_CONST float* wp = wc.c2w + ((c * 3 + ky) * 3 + kx) * 48 + g * 16;
 #pragma unroll
                     for (int k = 0; k < 16; k++) acc[k] = fmaf(v, wp[k], acc[k]);
                 }
         }
 #pragma unroll
-        for (int k = 0; k < 16; k++) sA[(g * 16 + k) * 81 + pos] = prelu(acc[k], w.p2[g * 16 + k]);
+        for (int k = 0; k < 16; k++) sA[(g * 16 + k) * 81 + pos] = prelu(acc[k], wc.p2[g * 16 + k]);
     }
     __syncthreads();
     // maxpool 3/2 ceil: 9 -> 4
@@ -386,27 +428,27 @@ __global__ __launch_bounds__(256) void k_rnet(const uint8_t* __restrict__ frames
         int y = pos / 3, x = pos % 3;
         float acc[8];
 #pragma unroll
-        for (int k = 0; k < 8; k++) acc[k] = w.c3b[g * 8 + k];
+        for (int k = 0; k < 8; k++) acc[k] = wc.c3b[g * 8 + k];
         for (int c = 0; c < 48; c++) {
 #pragma unroll
             for (int ky = 0; ky < 2; ky++)
 #pragma unroll
                 for (int kx = 0; kx < 2; kx++) {
                     float v = sA[3888 + c * 16 + (y + ky) * 4 + x + kx];
-                    const float* wp = w.c3w + ((c * 2 + ky) * 2 + kx) * 64 + g * 8;
+                    const VTF_CONST float* wp = wc.c3w + ((c * 2 + ky) * 2 + kx) * 64 + g * 8;
 #pragma unroll
                     for (int k = 0; k < 8; k++) acc[k] = fmaf(v, wp[k], acc[k]);
                 }
         }
 #pragma unroll
-        for (int k = 0; k < 8; k++) sA[4656 + x * 192 + y * 64 + g * 8 + k] = prelu(acc[k], w.p3[g * 8 + k]);
+        for (int k = 0; k < 8; k++) sA[4656 + x * 192 + y * 64 + g * 8 + k] = prelu(acc[k], wc.p3[g * 8 + k]);
     }
     __syncthreads();
     // dense4 576->128 + PReLU; weights transposed [k][128]
     if (tid < 128) {
-        float acc = w.d4b[tid];
-        for (int k = 0; k < 576; k++) acc = fmaf(sA[4656 + k], w.d4w[k * 128 + tid], acc);
-        sA[5232 + tid] = prelu(acc, w.p4[tid]);
+        float acc = wc.d4b[tid];
+        for (int k = 0; k < 576; k++) acc = fmaf(sA[4656 + k], wc.d4w[k * 128 + tid], acc);
+        sA[5232 + tid] = prelu(acc, wc.p4[tid]);
     }
     __syncthreads();
     if (tid < 64) {
@@ -416,20 +458,20 @@ __global__ __launch_bounds__(256) void k_rnet(const uint8_t* __restrict__ frames
         for (int j = 0; j < 6; j++) part[j] = 0.f;
         for (int k = tid; k < 128; k += 64) {
             float f = sA[5232 + k];
-            part[0] = fmaf(f, w.d51w[k], part[0]);
-            part[1] = fmaf(f, w.d51w[128 + k], part[1]);
+            part[0] = fmaf(f, wc.d51w[k], part[0]);
+            part[1] = fmaf(f, wc.d51w[128 + k], part[1]);
 #pragma unroll
-            for (int j = 0; j < 4; j++) part[2 + j] = fmaf(f, w.d52w[j * 128 + k], part[2 + j]);
+            for (int j = 0; j < 4; j++) part[2 + j] = fmaf(f, wc.d52w[j * 128 + k], part[2 + j]);
         }
 #pragma unroll
         for (int j = 0; j < 6; j++)
             for (int off = 32; off > 0; off >>= 1) part[j] += __shfl_xor(part[j], off);
         if (tid == 0) {
-            float a0 = part[0] + w.d51b[0], a1 = part[1] + w.d51b[1];
+            float a0 = part[0] + wc.d51b[0], a1 = part[1] + wc.d51b[1];
             float mx = fmaxf(a0, a1);
             float e0 = expf(a0 - mx), e1 = expf(a1 - mx);
             prob_out[n] = e1 * __fdiv_rn(1.0f, e0 + e1);
-            reg_out[n] = make_float4(part[2] + w.d52b[0], part[3] + w.d52b[1], part[4] + w.d52b[2], part[5] + w.d52b[3]);
+            reg_out[n] = make_float4(part[2] + wc.d52b[0], part[3] + wc.d52b[1], part[4] + wc.d52b[2], part[5] + wc.d52b[3]);
         }
     }
 }
@@ -455,8 +497,9 @@ template <bool FROM_FRAMES>
 __global__ __launch_bounds__(512) void k_onet(const uint8_t* __restrict__ frames, int64_t frame_stride,
                                               int64_t row_stride, int H, int W, const float4* __restrict__ boxes,
                                               const int32_t* __restrict__ img, const float* __restrict__ xin,
-                                              ONetW w, float4* __restrict__ reg_out, float* __restrict__ lm_out,
+                                              ONetW wg, float4* __restrict__ reg_out, float* __restrict__ lm_out,
                                               float* __restrict__ prob_out, int32_t* __restrict__ err) {
+    const auto wc = to_const(wg);
     __shared__ float sX[14112];
     __shared__ float sY[16928];
     __shared__ float sZ[6400];
@@ -492,7 +535,7 @@ __global__ __launch_bounds__(512) void k_onet(const uint8_t* __restrict__ frames
                 if (x >= 46) break;
                 float acc[32];
 #pragma unroll
-                for (int co = 0; co < 32; co++) acc[co] = w.c1b[co];
+                for (int co = 0; co < 32; co++) acc[co] = wc.c1b[co];
 #pragma unroll
                 for (int c = 0; c < 3; c++)
 #pragma unroll
@@ -500,12 +543,12 @@ __global__ __launch_bounds__(512) void k_onet(const uint8_t* __restrict__ frames
 #pragma unroll
                         for (int kx = 0; kx < 3; kx++) {
                             float v = sX[(c * 48 + y + ky) * 48 + x + kx];
-                            const float* wp = w.c1w + ((c * 3 + ky) * 3 + kx) * 32;
+                            const VTF_CONST float* wp = wc.c1w + ((c * 3 + ky) * 3 + kx) * 32;
 #pragma unroll
                             for (int co = 0; co < 32; co++) acc[co] = fmaf(v, wp[co], acc[co]);
                         }
 #pragma unroll
-                for (int co = 0; co < 32; co++) m[co] = fmaxf(m[co], prelu(acc[co], w.p1[co]));
+                for (int co = 0; co < 32; co++) m[co] = fmaxf(m[co], prelu(acc[co], wc.p1[co]));
             }
         }
 #pragma unroll
@@ -520,20 +563,20 @@ __global__ __launch_bounds__(512) void k_onet(const uint8_t* __restrict__ frames
             int cb = half * 32 + g * 8;
             float acc[8];
 #pragma unroll
-            for (int k = 0; k < 8; k++) acc[k] = w.c2b[cb + k];
+            for (int k = 0; k < 8; k++) acc[k] = wc.c2b[cb + k];
             for (int c = 0; c < 32; c++) {
 #pragma unroll
                 for (int ky = 0; ky < 3; ky++)
 #pragma unroll
                     for (int kx = 0; kx < 3; kx++) {
                         float v = sY[c * 529 + (y + ky) * 23 + x + kx];
-                        const float* wp = w.c2w + ((c * 3 + ky) * 3 + kx) * 64 + cb;
+                        const VTF_CONST float* wp = wc.c2w + ((c * 3 + ky) * 3 + kx) * 64 + cb;
 #pragma unroll
                         for (int k = 0; k < 8; k++) acc[k] = fmaf(v, wp[k], acc[k]);
                     }
             }
 #pragma unroll
-            for (int k = 0; k < 8; k++) sX[(g * 8 + k) * 441 + pos] = prelu(acc[k], w.p2[cb + k]);
+            for (int k = 0; k < 8; k++) sX[(g * 8 + k) * 441 + pos] = prelu(acc[k], wc.p2[cb + k]);
         }
         __syncthreads();
         for (int i = tid; i < 3200; i += 512) {
@@ -554,20 +597,20 @@ __global__ __launch_bounds__(512) void k_onet(const uint8_t* __restrict__ frames
         int y = pos / 8, x = pos % 8;
         float acc[8];
 #pragma unroll
-        for (int k = 0; k < 8; k++) acc[k] = w.c3b[g * 8 + k];
+        for (int k = 0; k < 8; k++) acc[k] = wc.c3b[g * 8 + k];
         for (int c = 0; c < 64; c++) {
 #pragma unroll
             for (int ky = 0; ky < 3; ky++)
 #pragma unroll
                 for (int kx = 0; kx < 3; kx++) {
                     float v = sZ[c * 100 + (y + ky) * 10 + x + kx];
-                    const float* wp = w.c3w + ((c * 3 + ky) * 3 + kx) * 64 + g * 8;
+                    const VTF_CONST float* wp = wc.c3w + ((c * 3 + ky) * 3 + kx) * 64 + g * 8;
 #pragma unroll
                     for (int k = 0; k < 8; k++) acc[k] = fmaf(v, wp[k], acc[k]);
                 }
         }
 #pragma unroll
-        for (int k = 0; k < 8; k++) sX[(g * 8 + k) * 64 + pos] = prelu(acc[k], w.p3[g * 8 + k]);
+        for (int k = 0; k < 8; k++) sX[(g * 8 + k) * 64 + pos] = prelu(acc[k], wc.p3[g * 8 + k]);
     }
     __syncthreads();
     // maxpool 2/2 ceil: 8 -> 4
@@ -585,27 +628,27 @@ __global__ __launch_bounds__(512) void k_onet(const uint8_t* __restrict__ frames
         int y = pos / 3, x = pos % 3;
         float acc[8];
 #pragma unroll
-        for (int k = 0; k < 8; k++) acc[k] = w.c4b[g * 8 + k];
+        for (int k = 0; k < 8; k++) acc[k] = wc.c4b[g * 8 + k];
         for (int c = 0; c < 64; c++) {
 #pragma unroll
             for (int ky = 0; ky < 2; ky++)
 #pragma unroll
                 for (int kx = 0; kx < 2; kx++) {
                     float v = sX[4096 + c * 16 + (y + ky) * 4 + x + kx];
-                    const float* wp = w.c4w + ((c * 2 + ky) * 2 + kx) * 128 + g * 8;
+                    const VTF_CONST float* wp = wc.c4w + ((c * 2 + ky) * 2 + kx) * 128 + g * 8;
 #pragma unroll
                     for (int k = 0; k < 8; k++) acc[k] = fmaf(v, wp[k], acc[k]);
                 }
         }
 #pragma unroll
-        for (int k = 0; k < 8; k++) sX[5120 + x * 384 + y * 128 + g * 8 + k] = prelu(acc[k], w.p4[g * 8 + k]);
+        for (int k = 0; k < 8; k++) sX[5120 + x * 384 + y * 128 + g * 8 + k] = prelu(acc[k], wc.p4[g * 8 + k]);
     }
     __syncthreads();
     // dense5 1152->256 + PReLU (weights transposed [k][256])
     if (tid < 256) {
-        float acc = w.d5b[tid];
-        for (int k = 0; k < 1152; k++) acc = fmaf(sX[5120 + k], w.d5w[k * 256 + tid], acc);
-        sX[6272 + tid] = prelu(acc, w.p5[tid]);
+        float acc = wc.d5b[tid];
+        for (int k = 0; k < 1152; k++) acc = fmaf(sX[5120 + k], wc.d5w[k * 256 + tid], acc);
+        sX[6272 + tid] = prelu(acc, wc.p5[tid]);
     }
     __syncthreads();
     if (tid < 64) {
@@ -614,24 +657,24 @@ __global__ __launch_bounds__(512) void k_onet(const uint8_t* __restrict__ frames
         for (int j = 0; j < 16; j++) part[j] = 0.f;
         for (int k = tid; k < 256; k += 64) {
             float f = sX[6272 + k];
-            part[0] = fmaf(f, w.d61w[k], part[0]);
-            part[1] = fmaf(f, w.d61w[256 + k], part[1]);
+            part[0] = fmaf(f, wc.d61w[k], part[0]);
+            part[1] = fmaf(f, wc.d61w[256 + k], part[1]);
 #pragma unroll
-            for (int j = 0; j < 4; j++) part[2 + j] = fmaf(f, w.d62w[j * 256 + k], part[2 + j]);
+            for (int j = 0; j < 4; j++) part[2 + j] = fmaf(f, wc.d62w[j * 256 + k], part[2 + j]);
 #pragma unroll
-            for (int j = 0; j < 10; j++) part[6 + j] = fmaf(f, w.d63w[j * 256 + k], part[6 + j]);
+            for (int j = 0; j < 10; j++) part[6 + j] = fmaf(f, wc.d63w[j * 256 + k], part[6 + j]);
         }
 #pragma unroll
         for (int j = 0; j < 16; j++)
             for (int off = 32; off > 0; off >>= 1) part[j] += __shfl_xor(part[j], off);
         if (tid == 0) {
-            float a0 = part[0] + w.d61b[0], a1 = part[1] + w.d61b[1];
+            float a0 = part[0] + wc.d61b[0], a1 = part[1] + wc.d61b[1];
             float mx = fmaxf(a0, a1);
             float e0 = expf(a0 - mx), e1 = expf(a1 - mx);
             prob_out[n] = e1 * __fdiv_rn(1.0f, e0 + e1);
-            reg_out[n] = make_float4(part[2] + w.d62b[0], part[3] + w.d62b[1], part[4] + w.d62b[2], part[5] + w.d62b[3]);
+            reg_out[n] = make_float4(part[2] + wc.d62b[0], part[3] + wc.d62b[1], part[4] + wc.d62b[2], part[5] + wc.d62b[3]);
 #pragma unroll
-            for (int j = 0; j < 10; j++) lm_out[n * 10 + j] = part[6 + j] + w.d63b[j];
+            for (int j = 0; j < 10; j++) lm_out[n * 10 + j] = part[6 + j] + wc.d63b[j];
         }
     }
 }

@@ -56,13 +56,23 @@ __global__ void k_seg_keys(const float* __restrict__ scores, const int32_t* __re
     vals[e] = (int32_t)e;
 }
 
-__global__ void k_seg_count(const uint64_t* __restrict__ keys, int64_t N, const int32_t* __restrict__ seg_base,
-                            int32_t* __restrict__ seg_cnt) {
-    int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (k >= N) return;
-    uint32_t hi = (uint32_t)(keys[k] >> 32);
-    int s = seg_base[hi >> 20] + (int)(hi & 0xFFFFF);
-    atomicAdd(&seg_cnt[s], 1);
+// lower_bound of (hi << 32) in the sorted keys for every segment id (no atomics: a
+// segment's elements are contiguous after the sort)
+__global__ void k_seg_bounds(const uint64_t* __restrict__ keys, int64_t N, const uint32_t* __restrict__ seg_hi,
+                             int S, int64_t* __restrict__ seg_start) {
+    int s = blockIdx.x * blockDim.x + threadIdx.x;
+    if (s > S) return;
+    if (s == S) {
+        seg_start[S] = N;
+        return;
+    }
+    uint64_t target = (uint64_t)seg_hi[s] << 32;
+    int64_t lo = 0, hi = N;
+    while (lo < hi) {
+        int64_t mid = (lo + hi) >> 1;
+        if (keys[mid] < target) lo = mid + 1; else hi = mid;
+    }
+    seg_start[s] = lo;
 }
 
 struct MaskTask {
@@ -105,7 +115,8 @@ __global__ __launch_bounds__(64) void k_iou_mask(const float4* __restrict__ boxe
         bi = load_box(boxes, img, order[beg + row], ob);
         ai = (bi.z - bi.x) * (bi.w - bi.y);
     }
-    uint64_t* out = mask + seg_mask_off[t.seg] + (int64_t)row * nb;
+    // layout: word (rb, cb, r) at ((rb * nb + cb) * 64 + r): coalesced writes and scan loads
+    uint64_t* out = mask + seg_mask_off[t.seg] + (int64_t)t.rb * nb * 64 + lane;
     for (int cb = t.rb; cb < nb; cb++) {
         int col = cb * 64 + lane;
         float4 bj = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -127,12 +138,24 @@ __global__ __launch_bounds__(64) void k_iou_mask(const float4* __restrict__ boxe
                 float ovr = __fdiv_rn(inter, (ai + cb_area[j]) - inter);
                 if ((double)ovr > thr) bits |= (1ull << j);
             }
-            out[cb] = bits;
         }
+        out[(int64_t)cb * 64] = bits;
     }
 }
 
-// One wave per segment: greedy resolution, 64 rows per step.
+__device__ inline uint64_t wave_or(uint64_t v) {
+    uint32_t lo = (uint32_t)v, hi = (uint32_t)(v >> 32);
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        lo |= __shfl_xor(lo, off);
+        hi |= __shfl_xor(hi, off);
+    }
+    return ((uint64_t)hi << 32) | lo;
+}
+
+// One wave per segment: greedy resolution, 64 rows per step.  The diagonal 64x64 block is
+// resolved in registers (readlane); the kept rows' words of every later column block are
+// loaded coalesced (64 rows x 8 B) and OR-reduced across the wave into the LDS bitset.
 __global__ __launch_bounds__(64) void k_nms_scan(const uint64_t* __restrict__ mask, const int64_t* __restrict__ seg_beg,
                                                  const int32_t* __restrict__ seg_n,
                                                  const int64_t* __restrict__ seg_mask_off,
@@ -150,7 +173,8 @@ __global__ __launch_bounds__(64) void k_nms_scan(const uint64_t* __restrict__ ma
     for (int cb = 0; cb < nb; cb++) {
         const int row = cb * 64 + lane;
         const int nrow = min(64, m - cb * 64);
-        uint64_t diag = (row < m) ? msk[(int64_t)row * nb + cb] : 0ull;
+        const uint64_t* blk = msk + (int64_t)cb * nb * 64 + lane;
+        uint64_t diag = (row < m) ? blk[(int64_t)cb * 64] : 0ull;
         uint64_t rem = removed[cb];
         uint64_t kept = 0;
         for (int t = 0; t < nrow; t++) {
@@ -162,12 +186,28 @@ __global__ __launch_bounds__(64) void k_nms_scan(const uint64_t* __restrict__ ma
             }
         }
         if (row < m) keep_sorted[beg + row] = (uint8_t)((kept >> lane) & 1ull);
-        uint64_t kk = kept;
-        while (kk) {
-            int t = __builtin_ctzll(kk);
-            kk &= kk - 1;
-            const uint64_t* mr = msk + (int64_t)(cb * 64 + t) * nb;
-            for (int w = cb + 1 + lane; w < nb; w += 64) removed[w] |= mr[w];
+        if (kept == 0) continue;
+        const bool mine = (kept >> lane) & 1ull;
+        int w = cb + 1;
+        for (; w + 3 < nb; w += 4) {
+            uint64_t v0 = mine ? blk[(int64_t)w * 64] : 0ull;
+            uint64_t v1 = mine ? blk[(int64_t)(w + 1) * 64] : 0ull;
+            uint64_t v2 = mine ? blk[(int64_t)(w + 2) * 64] : 0ull;
+            uint64_t v3 = mine ? blk[(int64_t)(w + 3) * 64] : 0ull;
+            v0 = wave_or(v0);
+            v1 = wave_or(v1);
+            v2 = wave_or(v2);
+            v3 = wave_or(v3);
+            if (lane == 0) {
+                removed[w] |= v0;
+                removed[w + 1] |= v1;
+                removed[w + 2] |= v2;
+                removed[w + 3] |= v3;
+            }
+        }
+        for (; w < nb; w++) {
+            uint64_t v = wave_or(mine ? blk[(int64_t)w * 64] : 0ull);
+            if (lane == 0) removed[w] |= v;
         }
         __builtin_amdgcn_wave_barrier();
     }
@@ -186,13 +226,21 @@ __global__ void k_flag_in_order(const int32_t* __restrict__ order, const uint8_t
 }
 
 __global__ void k_compact(const int32_t* __restrict__ order, const int32_t* __restrict__ flag,
-                          const int32_t* __restrict__ incl, const int32_t* __restrict__ elem_call, int64_t N,
-                          int32_t* __restrict__ keep_out, int32_t* __restrict__ call_kept) {
+                          const int32_t* __restrict__ incl, int64_t N, int32_t* __restrict__ keep_out) {
     int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (k >= N || !flag[k]) return;
-    int32_t e = order[k];
-    keep_out[incl[k] - 1] = e;
-    atomicAdd(&call_kept[elem_call[e]], 1);
+    keep_out[incl[k] - 1] = order[k];
+}
+
+// kept count of call c = incl[end_c - 1] - incl[beg_c - 1], bounds from the sorted keys
+__global__ void k_call_kept(const int64_t* __restrict__ call_start, const int32_t* __restrict__ incl, int C,
+                            int32_t* __restrict__ out) {
+    int c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= C) return;
+    int64_t b = call_start[c], e = call_start[c + 1];
+    int32_t lo = b > 0 ? incl[b - 1] : 0;
+    int32_t hi = e > 0 ? incl[e - 1] : 0;
+    out[c] = hi - lo;
 }
 
 template <class K, class V>
@@ -268,14 +316,21 @@ void nms_multi(Arena& ar, const float* d_boxes, const float* d_scores, const int
     int32_t* ord = ar.get<int32_t>(49, N);
     k_seg_keys<<<cdiv(N, 256), 256, 0, st>>>(d_scores, d_img, d_elem_call, d_van, N, 1, k0, v0);
     sort_u64_pairs(ar, 50, k0, k1, v0, ord, N, 64, st);
-    int32_t* d_scnt = ar.get<int32_t>(51, S);
-    VTF_HIP(hipMemsetAsync(d_scnt, 0, S * 4, st));
-    k_seg_count<<<cdiv(N, 256), 256, 0, st>>>(k1, N, d_sbase, d_scnt);
-    std::vector<int32_t> scnt(S);
+    // segment bounds by binary search on the sorted keys
+    std::vector<uint32_t> seg_hi(S);
+    for (int c = 0; c < C; c++)
+        for (int s2 = seg_base[c]; s2 < seg_base[c + 1]; s2++) seg_hi[s2] = ((uint32_t)c << 20) | (uint32_t)(s2 - seg_base[c]);
+    uint32_t* d_seghi = (uint32_t*)ar.get(51, (S + C + 2) * 4);
+    VTF_HIP(hipMemcpyAsync(d_seghi, seg_hi.data(), S * 4, hipMemcpyHostToDevice, st));
+    int64_t* d_sstart = ar.get<int64_t>(52, S + 1);
+    k_seg_bounds<<<cdiv(S + 1, 256), 256, 0, st>>>(k1, N, d_seghi, S, d_sstart);
+    std::vector<int64_t> sstart(S + 1);
     std::vector<float> cmax(C);
-    VTF_HIP(hipMemcpyAsync(scnt.data(), d_scnt, S * 4, hipMemcpyDeviceToHost, st));
+    VTF_HIP(hipMemcpyAsync(sstart.data(), d_sstart, (S + 1) * 8, hipMemcpyDeviceToHost, st));
     VTF_HIP(hipMemcpyAsync(cmax.data(), d_cmax, C * 4, hipMemcpyDeviceToHost, st));
     VTF_HIP(hipStreamSynchronize(st));
+    std::vector<int32_t> scnt(S);
+    for (int s2 = 0; s2 < S; s2++) scnt[s2] = (int32_t)(sstart[s2 + 1] - sstart[s2]);
 
     // segment tables, mask offsets, row-block tasks
     std::vector<int64_t> sbeg(S), moff(S);
@@ -293,12 +348,14 @@ void nms_multi(Arena& ar, const float* d_boxes, const float* d_scores, const int
             if (!vanilla[c]) offb[s] = cmax[c] + 1.0f;
             for (int rb = 0; rb < nb; rb++) tasks.push_back({s, rb});
             pos += m;
-            mtot += (int64_t)m * nb;
+            mtot += (int64_t)nb * nb * 64;
         }
     }
     VTF_CHECK(maxnb * 8 <= 160 * 1024, VTF_E_LIMIT, "nms_multi: a segment exceeds 1.3M boxes");
-    int64_t* d_sbeg = ar.get<int64_t>(52, S);
+    int64_t* d_sbeg = ar.get<int64_t>(60, S);
     int64_t* d_moff = ar.get<int64_t>(53, S);
+    int32_t* d_scnt = ar.get<int32_t>(61, S);
+    VTF_HIP(hipMemcpyAsync(d_scnt, scnt.data(), S * 4, hipMemcpyHostToDevice, st));
     float* d_offb = ar.get<float>(54, S);
     MaskTask* d_tasks = (MaskTask*)ar.get(55, tasks.size() * sizeof(MaskTask));
     VTF_HIP(hipMemcpyAsync(d_sbeg, sbeg.data(), S * 8, hipMemcpyHostToDevice, st));
@@ -321,9 +378,14 @@ void nms_multi(Arena& ar, const float* d_boxes, const float* d_scores, const int
     int32_t* incl = ((int32_t*)k0) + N;
     k_flag_in_order<<<cdiv(N, 256), 256, 0, st>>>(ord, keep_elem, N, flag);
     inclusive_scan_i32(ar, 59, flag, incl, N, st);
+    k_compact<<<cdiv(N, 256), 256, 0, st>>>(ord, flag, incl, N, d_keep);
+    std::vector<uint32_t> call_hi(C);
+    for (int c = 0; c < C; c++) call_hi[c] = (uint32_t)c << 20;
+    uint32_t* d_callhi = d_seghi + S;
+    VTF_HIP(hipMemcpyAsync(d_callhi, call_hi.data(), C * 4, hipMemcpyHostToDevice, st));
+    k_seg_bounds<<<cdiv(C + 1, 256), 256, 0, st>>>(k1, N, d_callhi, C, d_sstart);
     int32_t* d_ckept = d_scnt;  // reuse (S >= C)
-    VTF_HIP(hipMemsetAsync(d_ckept, 0, C * 4, st));
-    k_compact<<<cdiv(N, 256), 256, 0, st>>>(ord, flag, incl, d_elem_call, N, d_keep, d_ckept);
+    k_call_kept<<<cdiv(C, 256), 256, 0, st>>>(d_sstart, incl, C, d_ckept);
     std::vector<int32_t> ck(C);
     VTF_HIP(hipMemcpyAsync(ck.data(), d_ckept, C * 4, hipMemcpyDeviceToHost, st));
     VTF_HIP(hipStreamSynchronize(st));
