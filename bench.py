@@ -1,0 +1,197 @@
+"""Benchmark: faces/sec end-to-end (detect + encode) on synthetic 1280x720 frames.
+
+Workload (BASELINE.json configs[1]): MTCNN (min_face_size=5, RealMTCNN default) + FaceNet,
+det-batch 16, enc-batch 128, frames resident in HBM.  One step = one det-batch per GPU:
+  MTCNN detect (fp32 parity mode; pyramid + P/R/O-Net + NMS on device)
+  -> reference box post-processing (filter_boxes / adjust_boxes, detection.py:174-262, host)
+  -> crop + INTER_LINEAR resize + FaceNet on device (bf16 by default; --enc-precision fp32).
+The timed region ends with the RCCL all-gather-v of every rank's embeddings (the exchange
+step before grouping).  value = faces encoded by all ranks / max-over-ranks wall time.
+
+  python bench.py [--gpus N --steps K --warmup W]
+  torchrun --nproc-per-node N bench.py --gpus N ...   (one process per GPU, RCCL)
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path[:0] = [ROOT, os.path.join(ROOT, 'video-to-faces_amd')]
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+FP32_PEAK_TFLOPS = 157.3  # MI355X dense fp32 (vector = f32 MFMA), MI355X_MICROARCH.md
+H, W = 720, 1280
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--gpus', type=int, default=1)
+    ap.add_argument('--steps', type=int, default=20)
+    ap.add_argument('--warmup', type=int, default=3)
+    ap.add_argument('--det-batch', type=int, default=16)
+    ap.add_argument('--enc-batch', type=int, default=128)
+    ap.add_argument('--enc-precision', default='bf16', choices=['bf16', 'fp32'])
+    ap.add_argument('--min-face-size', type=float, default=5.0)
+    ap.add_argument('--pool', type=int, default=32, help='distinct synthetic frames per rank (cycled)')
+    ap.add_argument('--cpu-frames', type=int, default=6, help='frames in the bounded CPU-baseline sample')
+    ap.add_argument('--no-cpu-baseline', action='store_true')
+    # box post-processing (detection.py:174-262): reference defaults except det_min_size,
+    # because synthetic-weight detections are mostly < 50 px and would never reach the encoder
+    ap.add_argument('--det-min-score', type=float, default=0.4)
+    ap.add_argument('--det-min-size', type=int, default=0)
+    ap.add_argument('--det-min-border', type=int, default=5)
+    return ap.parse_args()
+
+
+def det_params(args):
+    return dict(mscore=args.det_min_score, msize=args.det_min_size, mborder=args.det_min_border,
+                scale=(1.5, 1.5, 2.2, 1.2), square=True)
+
+
+def cpu_baseline(frames, args):
+    """The oracle (CPU restatement of the reference path, torch-CPU + C NMS) on a bounded
+    sample of the same workload, rank 0 only."""
+    from oracle import mtcnn as om
+    from oracle.facenet import inception_resnet_v1, resize_linear_u8
+    from videotofaces import synth
+    from videotofaces.detection import boxes_to_crops
+    cores = len(os.sched_getaffinity(0))
+    env = os.environ.get('OMP_NUM_THREADS')
+    if env and env.isdigit():
+        cores = min(cores, int(env))
+    torch.set_num_threads(cores)
+    pm, pf = synth.make_params('mtcnn'), synth.make_params('facenet')
+    n = min(args.cpu_frames, frames.shape[0])
+    sample = frames[:n]
+    t0 = time.time()
+    res = om.forward(pm, list(sample), minsize=args.min_face_size)
+    crops = boxes_to_crops(res, (H, W), **det_params(args))
+    faces = 0
+    for i in range(0, crops.shape[0], args.enc_batch):
+        blobs = []
+        for f, x1, y1, x2, y2 in crops[i:i + args.enc_batch]:
+            r = resize_linear_u8(sample[f, y1:y2, x1:x2], 160)[:, :, ::-1].transpose(2, 0, 1)
+            blobs.append((torch.from_numpy(np.ascontiguousarray(r)).float() - 127.5) * (1 / 128))
+        inception_resnet_v1(pf, torch.stack(blobs))
+        faces += len(blobs)
+    dt = time.time() - t0
+    return {'value': round(faces / dt, 3), 'unit': 'faces/s', 'cores': cores, 'kind': 'port',
+            'sample': '%d synthetic 720p frames (%d faces), oracle MTCNN(min_face_size=%g)+FaceNet fp32 on CPU, %.1f s'
+                      % (n, faces, args.min_face_size, dt)}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get('WORLD_SIZE', '1'))
+    rank = int(os.environ.get('RANK', '0'))
+    local = int(os.environ.get('LOCAL_RANK', '0'))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group('nccl', device_id=torch.device('cuda', local))
+    dev = torch.device('cuda', local)
+    from videotofaces import synth
+    from videotofaces.detectors.mtcnn import MTCNN
+    from videotofaces.encoders.facenet import InceptionResnetV1
+    from videotofaces.detection import boxes_to_crops
+
+    B = args.det_batch
+    pool_n = max(B, args.pool // B * B)
+    frames_np = synth.make_frames(pool_n, H, W, seed=1000 + rank)
+    frames = torch.from_numpy(frames_np).to(dev)
+    det = MTCNN(dev)
+    enc = InceptionResnetV1(dev, precision=args.enc_precision)
+
+    def step(i):
+        j = (i * B) % pool_n
+        fb = frames[j:j + B]
+        res = det(fb, args.min_face_size)
+        crops = boxes_to_crops(res, (H, W), **det_params(args))
+        embs = [enc.encode_crops(fb, crops[k:k + args.enc_batch]) for k in range(0, crops.shape[0], args.enc_batch)]
+        return embs, crops.shape[0], sum(r.shape[0] for r in res)
+
+    for i in range(args.warmup):
+        step(i)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    det.profile(True)
+    t0 = time.perf_counter()
+    faces, dets, embs = 0, 0, []
+    for i in range(args.steps):
+        e, nf, nd = step(args.warmup + i)
+        embs.extend(e)
+        faces += nf
+        dets += nd
+    local_emb = torch.cat(embs) if embs else torch.zeros((0, 512), device=dev)
+    if world > 1:
+        from videotofaces.parallel import all_gather_rows
+        gathered = all_gather_rows(local_emb)
+    else:
+        gathered = local_emb
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t0
+    pnet_ms, pnet_launches, pnet_flops, pnet_frames = det.profile(False)
+    tot = torch.tensor([faces, dets, pnet_frames], dtype=torch.float64, device=dev)
+    el = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(tot, op=dist.ReduceOp.SUM)
+        dist.all_reduce(el, op=dist.ReduceOp.MAX)
+    faces_all, dets_all, frames_all = [float(x) for x in tot.tolist()]
+    elapsed = float(el.item())
+    if rank == 0:
+        avg_ms = pnet_ms / max(1, pnet_launches)
+        flops_per_launch = pnet_flops / max(1, pnet_launches)
+        achieved = flops_per_launch / (avg_ms / 1e3) / 1e12 if avg_ms > 0 else 0.0
+        traffic = None
+        tf = os.path.join(ROOT, 'profiles', 'pnet_traffic.json')
+        if os.path.exists(tf):
+            traffic = json.load(open(tf)).get('hbm_bytes_per_launch')
+        out = {
+            'metric': 'faces/sec end-to-end (detect+encode) on 1280x720 synthetic frames',
+            'value': round(faces_all / elapsed, 2),
+            'unit': 'faces/s',
+            'n_gpus': world,
+            'steps': args.steps,
+            'warmup': args.warmup,
+            'ms_per_step': round(elapsed * 1e3 / args.steps, 3),
+            'higher_is_better': True,
+            'scaling': 'weak',
+            'vs_baseline': None,
+            'dtype': 'fp32 det / %s enc' % args.enc_precision,
+            'data': 'synthetic (seeded 720p value-noise frames with face blobs; hash-seeded synthetic weights, '
+                    'MTCNN heads calibrated to ~4 faces/frame)',
+            'config': {'workload': 'MTCNN(min_face_size=%g)+FaceNet, det-batch %d, enc-batch %d, 720p, frames in HBM, '
+                                   'box filter min_score %g min_size %d min_border %d, det_scale (1.5,1.5,2.2,1.2), square'
+                                   % (args.min_face_size, B, args.enc_batch, args.det_min_score, args.det_min_size,
+                                      args.det_min_border),
+                       'det_batch': B, 'enc_batch': args.enc_batch, 'frames_per_step_per_gpu': B,
+                       'parallelism': 'dp%d (frame-sharded, RCCL all-gather of embeddings)' % world},
+            'frames_per_s': round(world * args.steps * B / elapsed, 2),
+            'faces_per_frame': round(faces_all / max(1.0, world * args.steps * B), 3),
+            'detections_per_frame': round(dets_all / max(1.0, world * args.steps * B), 3),
+            'roofline': {'kernel': 'k_pnet (fused pyramid resample + PNet, fp32)', 'bound': 'mfma',
+                         'achieved': round(achieved, 3), 'peak': FP32_PEAK_TFLOPS, 'unit': 'TFLOP/s',
+                         'frac': round(achieved / FP32_PEAK_TFLOPS, 4), 'traffic': traffic,
+                         'avg_launch_ms': round(avg_ms, 4), 'flops_per_launch': flops_per_launch,
+                         'launches': pnet_launches},
+            'cpu_baseline': None,
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            out['cpu_baseline'] = cpu_baseline(frames_np, args)
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == '__main__':
+    main()

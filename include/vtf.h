@@ -44,8 +44,8 @@ int vtf_mtcnn_set_stream(vtf_mtcnn_t h, void* hip_stream);
 /* frames: uint8 BGR, frame b pixel (y,x) channel c at frames[b*frame_stride + y*row_stride
  * + x*3 + c] (a borrowed, possibly non-contiguous view, detection.py:114-116).
  * frames_on_device: 1 if `frames` is a device pointer.
- * Output (host): boxes [total,5] (x1,y1,x2,y2,score), landmarks [total,10] (x0..x4,y0..y4,
- * may be NULL), counts[B]; per image in reference order.  If total > cap nothing is
+ * Output (host): boxes [total,5] (x1,y1,x2,y2,score), landmarks [total,5,2] ((x,y) per point, as
+ * mtcnn.py:239 stacks them; may be NULL), counts[B]; per image in reference order.  If total > cap nothing is
  * written, *out_total is set and VTF_E_CAPACITY returned. */
 int vtf_mtcnn_detect(vtf_mtcnn_t h, const uint8_t* frames, int frames_on_device, int B, int H, int W,
                      int64_t frame_stride, int64_t row_stride, double min_face_size,
@@ -57,6 +57,13 @@ int vtf_mtcnn_detect(vtf_mtcnn_t h, const uint8_t* frames, int frames_on_device,
  * [4] stage-2 passing, [5] after stage-2 NMS (= stage-3 refinements), [6] stage-3 passing,
  * [7] final faces. */
 int vtf_mtcnn_stats(vtf_mtcnn_t h, int64_t* out8);
+
+/* Kernel timing of the dominant kernel (fused pyramid+PNet) with HIP events recorded on the
+ * handle's stream around each launch.  enable=1 resets and starts accumulating; the call
+ * returns the totals so far: elapsed ms, launches, algorithmic FLOPs (2*MAC of conv1-3 and
+ * the heads over every pyramid level) and frames. */
+int vtf_mtcnn_profile(vtf_mtcnn_t h, int enable, double* out_ms, int64_t* out_launches, double* out_flops,
+                      int64_t* out_frames);
 
 /* Parity entry points (device pointers, handle stream).
  * Fused MTCNN._resample + PNet for one pyramid level (mtcnn.py:150-151, 27-38):

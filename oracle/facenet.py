@@ -89,40 +89,35 @@ def blob_from_u8_nchw(u8, mean=127.5, scale=1 / 128):
     return (u8.float() - mean) * scale
 
 
+def _coefs(src, dst):
+    d = np.arange(dst, dtype=np.float64)
+    f = ((d + 0.5) * (1.0 / (dst / src)) - 0.5).astype(np.float32)
+    s = np.floor(f).astype(np.int64)
+    f = (f - s.astype(np.float32)).astype(np.float32)
+    lo = s < 0
+    f[lo], s[lo] = 0, 0
+    edge = s >= src - 1
+    f[edge], s[edge] = 0, src - 1
+    c0 = np.rint((np.float32(1) - f) * np.float32(2048)).astype(np.int64)
+    c1 = np.rint(f * np.float32(2048)).astype(np.int64)
+    return s, np.minimum(s + 1, src - 1), c0, c1, edge
+
+
 def resize_linear_u8(img, S):
     """OpenCV uint8 INTER_LINEAR (resizeGeneric_ fixed point + SIMD vertical rounding), numpy.
     cv2 is absent here: this restatement is parity-UNPINNED (used to check the GPU kernel)."""
     h, w = img.shape[:2]
     if (h, w) == (S, S):
         return img.copy()
-
-    def coefs(src, dst):
-        scale = 1.0 / (dst / src)
-        out = []
-        for d in range(dst):
-            f = np.float32((d + 0.5) * scale - 0.5)
-            s = int(np.floor(f))
-            f = np.float32(f - np.float32(s))
-            edge = False
-            if s < 0:
-                f, s = np.float32(0), 0
-            if s >= src - 1:
-                f, s, edge = np.float32(0), src - 1, True
-            c0 = int(np.rint(np.float32(np.float32(1) - f) * np.float32(2048)))
-            c1 = int(np.rint(f * np.float32(2048)))
-            out.append((s, min(s + 1, src - 1), c0, c1, edge))
-        return out
-    cx, cy = coefs(w, S), coefs(h, S)
+    sx0, sx1, a0, a1, ex = _coefs(w, S)
+    sy0, sy1, b0, b1, _ = _coefs(h, S)
     src = img.astype(np.int64)
-    out = np.empty((S, S, img.shape[2]), np.uint8)
-    for dy, (sy0, sy1, b0, b1, _) in enumerate(cy):
-        for dx, (sx0, sx1, a0, a1, ex) in enumerate(cx):
-            if ex:
-                h0 = src[sy0, sx0] * 2048
-                h1 = src[sy1, sx0] * 2048
-            else:
-                h0 = src[sy0, sx0] * a0 + src[sy0, sx1] * a1
-                h1 = src[sy1, sx0] * a0 + src[sy1, sx1] * a1
-            t = (((h0 >> 4) * b0) >> 16) + (((h1 >> 4) * b1) >> 16)
-            out[dy, dx] = np.clip((t + 2) >> 2, 0, 255)
-    return out
+
+    def hrow(rows):
+        r = src[rows]                                   # [S, w, C]
+        v = r[:, sx0] * a0[None, :, None] + r[:, sx1] * a1[None, :, None]
+        v[:, ex] = r[:, sx0[ex]] * 2048
+        return v
+    h0, h1 = hrow(sy0), hrow(sy1)
+    t = (((h0 >> 4) * b0[:, None, None]) >> 16) + (((h1 >> 4) * b1[:, None, None]) >> 16)
+    return np.clip((t + 2) >> 2, 0, 255).astype(np.uint8)

@@ -1,0 +1,61 @@
+"""CPU: multi-process (gloo, world_size 2) coverage of the frame sharding and the rank-ordered
+all-gather-v of embeddings used by bench.py / the N>1 path."""
+import os
+import socket
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+
+def test_shard_batches_cover_and_align():
+    from videotofaces.parallel import shard_batches
+    for n, bs, world in [(100, 16, 2), (10000, 16, 8), (5, 4, 3), (0, 4, 2), (33, 16, 4)]:
+        ranges = [shard_batches(n, bs, r, world) for r in range(world)]
+        assert ranges[0][0] == 0 and ranges[-1][1] == n
+        for (a, b), (c, d) in zip(ranges, ranges[1:]):
+            assert b == c
+        for a, b in ranges:
+            assert (a % bs == 0 or a == n) and (b % bs == 0 or b == n)
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(('127.0.0.1', 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, q):
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [root, os.path.join(root, 'video-to-faces_amd')]
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    from videotofaces.parallel import all_gather_rows, shard_batches
+    n_frames, bs = 70, 16
+    lo, hi = shard_batches(n_frames, bs, rank, world)
+    # a stand-in for per-frame embeddings: row = [frame index, face index]; frame f has f % 3 faces
+    rows = [[f, k] for f in range(lo, hi) for k in range(f % 3)]
+    local = torch.tensor(rows, dtype=torch.float32).reshape(-1, 2)
+    out = all_gather_rows(local)
+    q.put((rank, out.tolist()))
+    dist.destroy_process_group()
+
+
+def test_all_gather_rows_rank_order_gloo():
+    world = 2
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in range(world))
+    for p in ps:
+        p.join(timeout=60)
+    expect = [[f, k] for f in range(70) for k in range(f % 3)]
+    for r in range(world):
+        assert res[r] == expect

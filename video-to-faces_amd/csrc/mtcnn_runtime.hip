@@ -37,8 +37,15 @@ struct Mtcnn {
     ONetW ow{};
     Arena ar;
     int64_t stats[8] = {0};
+    // kernel timing (vtf_mtcnn_profile)
+    bool prof = false;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    double prof_ms = 0, prof_flops = 0;
+    int64_t prof_launches = 0, prof_frames = 0;
 
     ~Mtcnn() {
+        if (ev0) (void)hipEventDestroy(ev0);
+        if (ev1) (void)hipEventDestroy(ev1);
         if (d_w) (void)hipFree(d_w);
     }
 };
@@ -139,6 +146,20 @@ static void plan_levels(int B, int H, int W, double minsize, std::vector<PNetLev
     }
 }
 
+// algorithmic FLOPs of PNet per frame over the pyramid (2*MAC; conv1, conv2, conv3, heads)
+static double pnet_flops(const std::vector<PNetLevel>& lv) {
+    double f = 0;
+    for (const PNetLevel& L : lv) {
+        double c1 = (double)(L.lh - 2) * (L.lw - 2);
+        double p1 = (double)(L.ph + 4) * (L.pw + 4);
+        double c2 = (double)(L.ph + 2) * (L.pw + 2);
+        double c3 = (double)L.ph * L.pw;
+        f += 2.0 * (c1 * 10 * 27 + c2 * 16 * 90 + c3 * 32 * 144 + c3 * 6 * 32);
+        (void)p1;
+    }
+    return f;
+}
+
 static void d2h_sync(void* dst, const void* src, size_t bytes, hipStream_t st) {
     VTF_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, st));
     VTF_HIP(hipStreamSynchronize(st));
@@ -199,9 +220,19 @@ static void detect(Mtcnn& m, const uint8_t* frames, int on_dev, int B, int H, in
     po.key = m.ar.get<uint64_t>(S_KEY, cells);
     po.score = m.ar.get<float>(S_SCORE, cells);
     po.regv = m.ar.get<float4>(S_REGV, cells);
+    if (m.prof) VTF_HIP(hipEventRecord(m.ev0, st));
     launch_pnet(false, fr, fstride, rstride, H, W, d_lv, NL, tiles, m.pw, po, st);
+    if (m.prof) VTF_HIP(hipEventRecord(m.ev1, st));
     std::vector<uint32_t> cnt(NL + 1);
     d2h_sync(cnt.data(), d_cnt, (NL + 1) * 4, st);
+    if (m.prof) {
+        float ms = 0.f;
+        VTF_HIP(hipEventElapsedTime(&ms, m.ev0, m.ev1));
+        m.prof_ms += ms;
+        m.prof_launches += 1;
+        m.prof_frames += B;
+        m.prof_flops += pnet_flops(lv) * B;
+    }
     const int64_t n1 = cnt[0];
     m.stats[1] = n1;
     if (n1 == 0) return;
@@ -368,6 +399,25 @@ int vtf_mtcnn_stats(vtf_mtcnn_t h, int64_t* out8) {
     return guarded([&] {
         VTF_CHECK(h && out8, VTF_E_ARG, "null argument");
         std::memcpy(out8, h->m.stats, sizeof(h->m.stats));
+    });
+}
+
+int vtf_mtcnn_profile(vtf_mtcnn_t h, int enable, double* out_ms, int64_t* out_launches, double* out_flops,
+                      int64_t* out_frames) {
+    return guarded([&] {
+        VTF_CHECK(h, VTF_E_ARG, "null handle");
+        Mtcnn& m = h->m;
+        if (out_ms) *out_ms = m.prof_ms;
+        if (out_launches) *out_launches = m.prof_launches;
+        if (out_flops) *out_flops = m.prof_flops;
+        if (out_frames) *out_frames = m.prof_frames;
+        if (enable) {
+            if (!m.ev0) VTF_HIP(hipEventCreate(&m.ev0));
+            if (!m.ev1) VTF_HIP(hipEventCreate(&m.ev1));
+            m.prof_ms = m.prof_flops = 0;
+            m.prof_launches = m.prof_frames = 0;
+        }
+        m.prof = enable != 0;
     });
 }
 

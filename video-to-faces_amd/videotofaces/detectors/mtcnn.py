@@ -94,6 +94,14 @@ class MTCNN:
 
     __call__ = forward
 
+    def profile(self, enable):
+        """Start (enable=True, resets) or stop kernel timing of the fused pyramid+PNet kernel;
+        returns (ms, launches, algorithmic flops, frames) accumulated so far."""
+        ms, n, fl, fr = ctypes.c_double(), ctypes.c_int64(), ctypes.c_double(), ctypes.c_int64()
+        nat.check(nat.lib().vtf_mtcnn_profile(self._h, int(enable), ctypes.byref(ms), ctypes.byref(n),
+                                              ctypes.byref(fl), ctypes.byref(fr)))
+        return ms.value, n.value, fl.value, fr.value
+
     # ---- stage-level entry points (parity tests)
     def pnet_level(self, frames_dev, lh, lw):
         B, H, W = frames_dev.shape[:3]
