@@ -10,6 +10,7 @@ struct PNetLevel {
     int tiles_x, tiles_y;
     int pad;
     int64_t tile_beg; // first workgroup of this level
+    const float* pre; // precomputed level [B][3][lh][lw] (large-bin downsampled levels) or null
 };
 
 // All conv weights transposed to [ci][ky][kx][co]; dense weights to [k][out] where noted.
@@ -27,6 +28,7 @@ struct PNetOut {
     // dense (parity) mode
     float* prob;
     float* reg;
+    int dbg;  // phase-skip mask for profiling (env VTF_PNET_DEBUG): 1 fill, 2 conv1, 4 conv2, 8 conv3
 };
 struct RNetW {
     const float *c1w, *c1b, *p1, *c2w, *c2b, *p2, *c3w, *c3b, *p3, *d4w, *d4b, *p4, *d51w, *d51b, *d52w, *d52b;
@@ -40,7 +42,7 @@ void launch_resample(const uint8_t* frames, int64_t frame_stride, int64_t row_st
                      int lw, float* out, hipStream_t st);
 void launch_pnet(bool dense, const uint8_t* frames, int64_t frame_stride, int64_t row_stride, int H, int W,
                  const PNetLevel* d_levels, int n_levels, int64_t total_tiles, const PNetW& w, const PNetOut& o,
-                 hipStream_t st);
+                 uint32_t* d_tile_ctr, hipStream_t st);
 void launch_rnet(const uint8_t* frames, int64_t frame_stride, int64_t row_stride, int H, int W, const float4* boxes,
                  const int32_t* img, const float* xin, int64_t n, const RNetW& w, float4* reg, float* prob,
                  int32_t* err, hipStream_t st);

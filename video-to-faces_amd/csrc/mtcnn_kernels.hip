@@ -17,10 +17,14 @@
 //   * k_rnet / k_onet: one workgroup per candidate box; the crop + adaptive pool to 24x24 /
 //     48x48 (replacing the reference's per-box Python loop) feeds the whole network in LDS.
 // Build with -ffp-contract=off: only explicit fmaf() fuses.
+#include <algorithm>
+
 #include "common.hpp"
 #include "mtcnn.hpp"
 
 namespace vtf {
+
+typedef __attribute__((ext_vector_type(4))) float f32x4;
 
 // ----------------------------------------------------------------------------------- helpers
 
@@ -125,203 +129,341 @@ constexpr int P_C2 = 16 * PC_H * PC_W;                // 9792
 constexpr int P_POOL = 10 * PP_H * PP_W;              // 7200
 constexpr int P_A = P_C2 > P_LVL ? P_C2 : P_LVL;
 
+// exact x / k for the bin averages: power-of-two k is an exact multiply (bit-identical to the
+// IEEE division), other k take the correctly-rounded division
+__device__ inline float div_bin(float x, int k) {
+    return (k & (k - 1)) == 0 ? x * __int_as_float((127 - __builtin_ctz(k)) << 23) : __fdiv_rn(x, (float)k);
+}
+
+constexpr int PNET_GROUPS_PER_CU = 2;
+constexpr int PATCH_BYTES = P_POOL * 4;  // frame patch staged in the (not yet used) pooled buffer
+
 template <bool DENSE>
-__global__ __launch_bounds__(256) void k_pnet(const uint8_t* __restrict__ frames, int64_t frame_stride,
-                                              int64_t row_stride, int H, int W, const PNetLevel* __restrict__ lv,
-                                              int n_levels, PNetW wg, PNetOut o) {
+__global__ __launch_bounds__(256, 2) void k_pnet(const uint8_t* __restrict__ frames, int64_t frame_stride,
+                                                 int64_t row_stride, int H, int W,
+                                                 const PNetLevel* __restrict__ lv, int n_levels,
+                                                 int64_t total_tiles, uint32_t* __restrict__ tile_ctr, PNetW wg,
+                                                 PNetOut o) {
     const auto wc = to_const(wg);
     __shared__ float sA[P_A];     // level tile, later conv2 output
-    __shared__ float sP[P_POOL];  // pooled conv1
-    const int tid = threadIdx.x;
-    // locate (level, frame, tile)
-    int64_t blk = blockIdx.x;
-    int L = 0;
-    while (L + 1 < n_levels && blk >= lv[L + 1].tile_beg) L++;
-    const PNetLevel P = lv[L];
-    int64_t t = blk - P.tile_beg;
-    const int tiles_per_img = P.tiles_x * P.tiles_y;
-    const int b = (int)(t / tiles_per_img);
-    const int tt = (int)(t % tiles_per_img);
-    const int oy0 = (tt / P.tiles_x) * PT_H, ox0 = (tt % P.tiles_x) * PT_W;
-    const uint8_t* fr = frames + (int64_t)b * frame_stride;
-    const int L1h = P.lh - 2, L1w = P.lw - 2;
-
-    // 1. level tile (rows 2*oy0 .. +42, cols 2*ox0 .. +74), zero outside the level.
-    //    Bin bounds of adaptive_avg_pool2d are tabulated once per tile.
+    __shared__ float sP[P_POOL];  // frame patch (u8) during the fill, then pooled conv1
     __shared__ int2 ybin[PL_H], xbin[PL_W];
-    if (tid < PL_H) {
-        int ly = 2 * oy0 + tid;
-        ybin[tid] = ly < P.lh ? make_int2((ly * H) / P.lh, ((ly + 1) * H + P.lh - 1) / P.lh) : make_int2(0, 0);
-    } else if (tid < PL_H + PL_W) {
-        int q = tid - PL_H, lx = 2 * ox0 + q;
-        xbin[q] = lx < P.lw ? make_int2((lx * W) / P.lw, ((lx + 1) * W + P.lw - 1) / P.lw) : make_int2(0, 0);
+    __shared__ int s_tile;
+    const int tid = threadIdx.x;
+    const int lane = tid & 63, wave = tid >> 6;
+    const int lr = lane & 15, lk = lane >> 4;
+
+    // ---- weights and im2col offsets, loaded once per persistent workgroup
+    float w1[7];
+#pragma unroll
+    for (int s = 0; s < 7; s++) {
+        int k = 4 * s + lk;
+        w1[s] = (k < 27 && lr < 10) ? wc.c1w[k * 10 + lr] : 0.f;
     }
-    __syncthreads();
-    for (int i = tid; i < PL_H * PL_W; i += 256) {
-        int r = i / PL_W, q = i - r * PL_W;
-        int2 yb = ybin[r], xb = xbin[q];
-        float s0 = 0.f, s1 = 0.f, s2 = 0.f;
-        for (int y = yb.x; y < yb.y; y++) {
-            const uint8_t* row = fr + (int64_t)y * row_stride;
-            for (int x = xb.x; x < xb.y; x++) {
-                const uint8_t* px = row + x * 3;  // BGR
-                s0 = s0 + ((float)px[2] - 127.5f) * 0.0078125f;
-                s1 = s1 + ((float)px[1] - 127.5f) * 0.0078125f;
-                s2 = s2 + ((float)px[0] - 127.5f) * 0.0078125f;
+    const float b1 = lr < 10 ? wc.c1b[lr] : 0.f, a1 = lr < 10 ? wc.p1[lr] : 0.f;
+    const float b2 = wc.c2b[lr], a2 = wc.p2[lr];
+    for (;;) {
+        // ---- fetch the next tile (dynamic: pyramid tiles differ in cost)
+        if (tid == 0) s_tile = (int)atomicAdd(tile_ctr, 1u);
+        __syncthreads();
+        const int64_t blk = s_tile;
+        if (blk >= total_tiles) break;
+        int L = 0;
+        while (L + 1 < n_levels && blk >= lv[L + 1].tile_beg) L++;
+        const PNetLevel P = lv[L];
+        const int64_t t = blk - P.tile_beg;
+        const int tiles_per_img = P.tiles_x * P.tiles_y;
+        const int b = (int)(t / tiles_per_img);
+        const int tt = (int)(t % tiles_per_img);
+        const int oy0 = (tt / P.tiles_x) * PT_H, ox0 = (tt % P.tiles_x) * PT_W;
+        const uint8_t* fr = frames + (int64_t)b * frame_stride;
+        const int L1h = P.lh - 2, L1w = P.lw - 2;
+
+        // ---- 1. level tile (rows 2*oy0 .. +42, cols 2*ox0 .. +74) = MTCNN._resample of the
+        //         preprocessed frame, bit-exact; zero outside the level.
+        if (tid < PL_H) {
+            int ly = 2 * oy0 + tid;
+            ybin[tid] = ly < P.lh ? make_int2((ly * H) / P.lh, ((ly + 1) * H + P.lh - 1) / P.lh) : make_int2(0, 0);
+        } else if (tid < PL_H + PL_W) {
+            int q = tid - PL_H, lx = 2 * ox0 + q;
+            xbin[q] = lx < P.lw ? make_int2((lx * W) / P.lw, ((lx + 1) * W + P.lw - 1) / P.lw) : make_int2(0, 0);
+        }
+        __syncthreads();
+        // frame patch covering every bin of the tile; staged to LDS with coalesced loads when it fits
+        int fy0 = ybin[0].x, fx0 = xbin[0].x, fy1 = fy0, fx1 = fx0;
+        {
+            int ry = min(PL_H - 1, P.lh - 1 - 2 * oy0), rx = min(PL_W - 1, P.lw - 1 - 2 * ox0);
+            fy1 = ybin[ry].y;
+            fx1 = xbin[rx].y;
+        }
+        const int pw3 = (fx1 - fx0) * 3;
+        const bool staged = !P.pre && (int64_t)(fy1 - fy0) * pw3 <= PATCH_BYTES;
+        uint8_t* patch = (uint8_t*)sP;
+        if (staged) {
+            const int nbytes = (fy1 - fy0) * pw3;
+            for (int i = tid; i < nbytes; i += 256) {
+                int r = i / pw3, q = i - r * pw3;
+                patch[i] = fr[(int64_t)(fy0 + r) * row_stride + fx0 * 3 + q];
             }
         }
-        float kh = (float)(yb.y - yb.x), kw = (float)(xb.y - xb.x);
-        bool in = yb.y > yb.x && xb.y > xb.x;
-        sA[i] = in ? __fdiv_rn(__fdiv_rn(s0, kh), kw) : 0.f;
-        sA[PL_H * PL_W + i] = in ? __fdiv_rn(__fdiv_rn(s1, kh), kw) : 0.f;
-        sA[2 * PL_H * PL_W + i] = in ? __fdiv_rn(__fdiv_rn(s2, kh), kw) : 0.f;
-    }
-    __syncthreads();
-
-    // 2. conv1 (3->10, 3x3) + PReLU + maxpool 2x2 ceil -> sP[10][20][36]
-    for (int i = tid; i < PP_H * PP_W; i += 256) {
-        int py = i / PP_W, px = i % PP_W;
-        float in[3][4][4];
-#pragma unroll
-        for (int c = 0; c < 3; c++)
-#pragma unroll
-            for (int dy = 0; dy < 4; dy++)
-#pragma unroll
-                for (int dx = 0; dx < 4; dx++) in[c][dy][dx] = sA[(c * PL_H + 2 * py + dy) * PL_W + 2 * px + dx];
-        float acc[4][10];
-#pragma unroll
-        for (int k = 0; k < 4; k++)
-#pragma unroll
-            for (int co = 0; co < 10; co++) acc[k][co] = wc.c1b[co];
-#pragma unroll
-        for (int c = 0; c < 3; c++)
-#pragma unroll
-            for (int ky = 0; ky < 3; ky++)
-#pragma unroll
-                for (int kx = 0; kx < 3; kx++)
-#pragma unroll
-                    for (int co = 0; co < 10; co++) {
-                        float wv = wc.c1w[((c * 3 + ky) * 3 + kx) * 10 + co];
-#pragma unroll
-                        for (int k = 0; k < 4; k++) acc[k][co] = fmaf(in[c][ky + (k >> 1)][kx + (k & 1)], wv, acc[k][co]);
+        __syncthreads();
+        if (P.pre) {
+            // large-bin level precomputed by k_resample (bit-identical values)
+            const float* pre = P.pre + (int64_t)b * 3 * P.lh * P.lw;
+            for (int i = tid; i < ((o.dbg & 1) ? 0 : P_LVL); i += 256) {
+                int c = i / (PL_H * PL_W), rq = i - c * (PL_H * PL_W);
+                int r = rq / PL_W, q = rq - r * PL_W;
+                int ly = 2 * oy0 + r, lx = 2 * ox0 + q;
+                sA[i] = (ly < P.lh && lx < P.lw) ? pre[((int64_t)c * P.lh + ly) * P.lw + lx] : 0.f;
+            }
+        }
+        for (int i = tid; i < ((o.dbg & 1) || P.pre ? 0 : PL_H * PL_W); i += 256) {
+            int r = i / PL_W, q = i - r * PL_W;
+            int2 yb = ybin[r], xb = xbin[q];
+            float s0 = 0.f, s1 = 0.f, s2 = 0.f;
+            if (staged) {
+                for (int y = yb.x; y < yb.y; y++) {
+                    const uint8_t* row = patch + (y - fy0) * pw3 + (xb.x - fx0) * 3;
+                    for (int x = 0; x < xb.y - xb.x; x++) {
+                        s0 = s0 + ((float)row[3 * x + 2] - 127.5f) * 0.0078125f;
+                        s1 = s1 + ((float)row[3 * x + 1] - 127.5f) * 0.0078125f;
+                        s2 = s2 + ((float)row[3 * x] - 127.5f) * 0.0078125f;
                     }
-        const int gy = 2 * (oy0 + py), gx = 2 * (ox0 + px);
-#pragma unroll
-        for (int co = 0; co < 10; co++) {
-            float m = -3.402823466e38f;
-#pragma unroll
-            for (int k = 0; k < 4; k++) {
-                bool ok = (gy + (k >> 1) < L1h) && (gx + (k & 1) < L1w);
-                float v = prelu(acc[k][co], wc.p1[co]);
-                if (ok) m = fmaxf(m, v);
-            }
-            sP[(co * PP_H + py) * PP_W + px] = m;
-        }
-    }
-    __syncthreads();
-
-    // 3. conv2 (10->16, 3x3) + PReLU -> sA[16][18][34]
-    for (int i = tid; i < PC_H * PC_W; i += 256) {
-        int y = i / PC_W, x = i % PC_W;
-        float acc[16];
-#pragma unroll
-        for (int co = 0; co < 16; co++) acc[co] = wc.c2b[co];
-        for (int c = 0; c < 10; c++) {
-#pragma unroll
-            for (int ky = 0; ky < 3; ky++)
-#pragma unroll
-                for (int kx = 0; kx < 3; kx++) {
-                    float v = sP[(c * PP_H + y + ky) * PP_W + x + kx];
-                    const VTF_CONST float* wp = wc.c2w + ((c * 3 + ky) * 3 + kx) * 16;
-#pragma unroll
-                    for (int co = 0; co < 16; co++) acc[co] = fmaf(v, wp[co], acc[co]);
                 }
-        }
-#pragma unroll
-        for (int co = 0; co < 16; co++) sA[(co * PC_H + y) * PC_W + x] = prelu(acc[co], wc.p2[co]);
-    }
-    __syncthreads();
-
-    // 4. conv3 (16->32, 3x3) + PReLU, heads 1x1 (32->2 softmax, 32->4)
-    for (int i = tid; i < PT_H * PT_W; i += 256) {
-        int y = i / PT_W, x = i % PT_W;
-        float acc[32];
-#pragma unroll
-        for (int co = 0; co < 32; co++) acc[co] = wc.c3b[co];
-        for (int c = 0; c < 16; c++) {
-#pragma unroll
-            for (int ky = 0; ky < 3; ky++)
-#pragma unroll
-                for (int kx = 0; kx < 3; kx++) {
-                    float v = sA[(c * PC_H + y + ky) * PC_W + x + kx];
-                    const VTF_CONST float* wp = wc.c3w + ((c * 3 + ky) * 3 + kx) * 32;
-#pragma unroll
-                    for (int co = 0; co < 32; co++) acc[co] = fmaf(v, wp[co], acc[co]);
-                }
-        }
-        float a0 = wc.c41b[0], a1 = wc.c41b[1];
-        float r0 = wc.c42b[0], r1 = wc.c42b[1], r2 = wc.c42b[2], r3 = wc.c42b[3];
-#pragma unroll
-        for (int k = 0; k < 32; k++) {
-            float f = prelu(acc[k], wc.p3[k]);
-            a0 = fmaf(f, wc.c41w[k], a0);
-            a1 = fmaf(f, wc.c41w[32 + k], a1);
-            r0 = fmaf(f, wc.c42w[k], r0);
-            r1 = fmaf(f, wc.c42w[32 + k], r1);
-            r2 = fmaf(f, wc.c42w[64 + k], r2);
-            r3 = fmaf(f, wc.c42w[96 + k], r3);
-        }
-        float mx = fmaxf(a0, a1);
-        float e0 = expf(a0 - mx), e1 = expf(a1 - mx);
-        float prob = __fdiv_rn(e1, e0 + e1);
-        const int oy = oy0 + y, ox = ox0 + x;
-        const bool valid = (oy < P.ph) && (ox < P.pw);
-        if (DENSE) {
-            if (valid) {
-                int64_t plane = (int64_t)P.ph * P.pw;
-                int64_t cell = (int64_t)oy * P.pw + ox;
-                o.prob[(int64_t)b * plane + cell] = prob;
-                float* rg = o.reg + (int64_t)b * 4 * plane + cell;
-                rg[0] = r0;
-                rg[plane] = r1;
-                rg[2 * plane] = r2;
-                rg[3 * plane] = r3;
-            }
-        } else {
-            // mask = prob >= 0.6 (mtcnn.py:183; the python scalar compares as fp32)
-            bool pass = valid && (prob >= 0.6f);
-            uint64_t bal = __ballot(pass);
-            if (bal) {
-                int lane = __lane_id();
-                int leader = __builtin_ctzll(bal);
-                uint32_t base = 0;
-                if (lane == leader) base = atomicAdd(o.count, (uint32_t)__popcll(bal));
-                base = __shfl(base, leader);
-                if (pass) {
-                    uint32_t slot = base + (uint32_t)__popcll(bal & ((1ull << lane) - 1ull));
-                    if (slot < o.cap) {
-                        uint32_t lin = (uint32_t)(((int64_t)b * P.ph + oy) * P.pw + ox);
-                        o.key[slot] = ((uint64_t)L << 32) | lin;
-                        o.score[slot] = prob;
-                        o.regv[slot] = make_float4(r0, r1, r2, r3);
+            } else {
+                for (int y = yb.x; y < yb.y; y++) {
+                    const uint8_t* row = fr + (int64_t)y * row_stride;
+                    for (int x = xb.x; x < xb.y; x++) {
+                        const uint8_t* px = row + x * 3;  // BGR
+                        s0 = s0 + ((float)px[2] - 127.5f) * 0.0078125f;
+                        s1 = s1 + ((float)px[1] - 127.5f) * 0.0078125f;
+                        s2 = s2 + ((float)px[0] - 127.5f) * 0.0078125f;
                     }
-                    atomicAdd(&o.level_count[L], 1u);
+                }
+            }
+            int kh = yb.y - yb.x, kw = xb.y - xb.x;
+            bool in = kh > 0 && kw > 0;
+            sA[i] = in ? div_bin(div_bin(s0, kh), kw) : 0.f;
+            sA[PL_H * PL_W + i] = in ? div_bin(div_bin(s1, kh), kw) : 0.f;
+            sA[2 * PL_H * PL_W + i] = in ? div_bin(div_bin(s2, kh), kw) : 0.f;
+        }
+        __syncthreads();
+
+        // ---- 2. conv1 (3->10, 3x3) + PReLU + maxpool 2x2 ceil on MFMA.  A row r of fragment
+        //         f is conv1 position (2py+dy, 2px+dx) of pooled cell pp = 4f + r/4, corner r%4,
+        //         so each lane's 4 accumulators (rows 4*lk..4*lk+3) ARE one pooling window.
+        {
+            constexpr int NPP = PP_H * PP_W;  // 720 pooled cells
+            constexpr int NF1 = NPP / 4;      // 180 fragments
+            const int corner = lr & 3, dy = corner >> 1, dx = corner & 1;
+            for (int f0 = wave; f0 < ((o.dbg & 2) ? 0 : NF1); f0 += 8) {
+                const int f1 = f0 + 4;
+                const bool two = f1 < NF1;
+                int pp0 = f0 * 4 + (lr >> 2), pp1 = (two ? f1 : f0) * 4 + (lr >> 2);
+                int ab0 = (2 * (pp0 / PP_W) + dy) * PL_W + 2 * (pp0 % PP_W) + dx;
+                int ab1 = (2 * (pp1 / PP_W) + dy) * PL_W + 2 * (pp1 % PP_W) + dx;
+                f32x4 c0 = {0.f, 0.f, 0.f, 0.f}, c1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                for (int s = 0; s < 7; s++) {
+                    const int k = min(4 * s + lk, 26);
+                    const int c = k / 9, r = k - 9 * c;
+                    const int ko = c * PL_H * PL_W + (r / 3) * PL_W + (r % 3);
+                    c0 = __builtin_amdgcn_mfma_f32_16x16x4f32(sA[ab0 + ko], w1[s], c0, 0, 0, 0);
+                    c1 = __builtin_amdgcn_mfma_f32_16x16x4f32(sA[ab1 + ko], w1[s], c1, 0, 0, 0);
+                }
+                if (lr < 10) {
+#pragma unroll
+                    for (int h = 0; h < 2; h++) {
+                        if (h == 1 && !two) break;
+                        const int pp = (h ? f1 : f0) * 4 + lk;
+                        const int py = pp / PP_W, px = pp % PP_W;
+                        const int gy = 2 * (oy0 + py), gx = 2 * (ox0 + px);
+                        float m = -3.402823466e38f;
+                        bool any = false;
+#pragma unroll
+                        for (int i = 0; i < 4; i++) {
+                            bool ok = (gy + (i >> 1) < L1h) && (gx + (i & 1) < L1w);
+                            float v = prelu((h ? c1[i] : c0[i]) + b1, a1);
+                            if (ok) {
+                                m = fmaxf(m, v);
+                                any = true;
+                            }
+                        }
+                        // outside the valid pooled map (only feeds discarded cells): keep finite
+                        sP[lr * NPP + pp] = any ? m : 0.f;
+                    }
                 }
             }
         }
+        __syncthreads();
+
+        // ---- 3. conv2 (10->16, 3x3) + PReLU on MFMA: M = 18*34 positions (39 frags), N = 16,
+        //         K = 90 (+2 zero) in 23 steps; A gathered from the pooled map.
+        {
+            constexpr int NPOS = PC_H * PC_W;      // 612
+            constexpr int NF = (NPOS + 15) / 16;   // 39
+            float w2[23];  // per tile (L1-resident): keeps the persistent register set small
+#pragma unroll
+            for (int s = 0; s < 23; s++) {
+                int k = 4 * s + lk;
+                w2[s] = k < 90 ? wc.c2w[k * 16 + lr] : 0.f;
+            }
+            for (int f0 = wave; f0 < ((o.dbg & 4) ? 0 : NF); f0 += 8) {
+                const int f1 = f0 + 4;
+                const bool two = f1 < NF;
+                int p0 = min(f0 * 16 + lr, NPOS - 1), p1 = min((two ? f1 : f0) * 16 + lr, NPOS - 1);
+                const int ab0 = (p0 / PC_W) * PP_W + (p0 % PC_W), ab1 = (p1 / PC_W) * PP_W + (p1 % PC_W);
+                f32x4 c0 = {0.f, 0.f, 0.f, 0.f}, c1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                for (int s = 0; s < 23; s++) {
+                    const int k = min(4 * s + lk, 89);
+                    const int c = k / 9, r = k - 9 * c;
+                    const int ko = c * PP_H * PP_W + (r / 3) * PP_W + (r % 3);
+                    c0 = __builtin_amdgcn_mfma_f32_16x16x4f32(sP[ab0 + ko], w2[s], c0, 0, 0, 0);
+                    c1 = __builtin_amdgcn_mfma_f32_16x16x4f32(sP[ab1 + ko], w2[s], c1, 0, 0, 0);
+                }
+#pragma unroll
+                for (int i = 0; i < 4; i++) {
+                    int q0 = f0 * 16 + 4 * lk + i;
+                    if (q0 < NPOS) sA[lr * NPOS + q0] = prelu(c0[i] + b2, a2);
+                    int q1 = f1 * 16 + 4 * lk + i;
+                    if (two && q1 < NPOS) sA[lr * NPOS + q1] = prelu(c1[i] + b2, a2);
+                }
+            }
+        }
+        __syncthreads();
+
+        // ---- 4. conv3 (16->32, 3x3) + PReLU on MFMA, computed TRANSPOSED (C = W3^T x im2col:
+        //         rows = 32 channels in 2 frags, cols = 16 cells per frag, K = 144 in 36 steps) so
+        //         the 1x1 heads are one more MFMA chain summing over the accumulator rows with no
+        //         lane movement: Heads^T (16 x cells) = Wh^T (16 x 32) x F (32 x cells), the
+        //         k-slot of lane group g at step i being channel 16*mf + 4g + i.
+        //         Each wave owns 8 cell fragments (64 accumulator VGPRs); the weights stream
+        //         through registers in 4 chunks of 9 k-steps.
+        {
+            f32x4 acc[8][2];
+#pragma unroll
+            for (int j = 0; j < 8; j++) acc[j][0] = acc[j][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+            int ab[8];
+#pragma unroll
+            for (int j = 0; j < 8; j++) {
+                const int f = wave * 8 + j;
+                ab[j] = (f >> 1) * PC_W + (f & 1) * 16 + lr;
+            }
+            const int nchunk = (o.dbg & 8) ? 0 : 4;
+            for (int sc = 0; sc < nchunk; sc++) {
+                float w3[9][2];
+#pragma unroll
+                for (int t = 0; t < 9; t++) {
+                    const int k = 4 * (9 * sc + t) + lk;
+                    w3[t][0] = wc.c3w[k * 32 + lr];
+                    w3[t][1] = wc.c3w[k * 32 + 16 + lr];
+                }
+#pragma unroll
+                for (int t = 0; t < 9; t++) {
+                    const int k = 4 * (9 * sc + t) + lk;
+                    const int c = k / 9, r = k - 9 * c;
+                    const int ko = c * PC_H * PC_W + (r / 3) * PC_W + (r % 3);
+#pragma unroll
+                    for (int j = 0; j < 8; j++) {
+                        const float bv = sA[ab[j] + ko];
+                        acc[j][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(w3[t][0], bv, acc[j][0], 0, 0, 0);
+                        acc[j][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(w3[t][1], bv, acc[j][1], 0, 0, 0);
+                    }
+                }
+            }
+            // accumulator row (mf, lk, i) = channel 16*mf + 4*lk + i
+            float cb3[2][4], ca3[2][4], hwA[2][4];
+#pragma unroll
+            for (int mf = 0; mf < 2; mf++)
+#pragma unroll
+                for (int i = 0; i < 4; i++) {
+                    const int ch = 16 * mf + 4 * lk + i;
+                    cb3[mf][i] = wc.c3b[ch];
+                    ca3[mf][i] = wc.p3[ch];
+                    // heads as the A operand: row = head lr (0,1 conv4_1; 2..5 conv4_2), k-slot = ch
+                    const int hrow = lr < 2 ? lr * 32 + ch : (lr < 6 ? (lr - 2) * 32 + ch : 0);
+                    const float hv = lr < 2 ? wc.c41w[hrow] : wc.c42w[hrow];
+                    hwA[mf][i] = lr < 6 ? hv : 0.f;
+                }
+            const float hb0 = wc.c41b[0], hb1 = wc.c41b[1], hb2 = wc.c42b[0], hb3 = wc.c42b[1];
+            const float hb4 = wc.c42b[2], hb5 = wc.c42b[3];
+#pragma unroll
+            for (int j = 0; j < 8; j++) {
+                const int f = wave * 8 + j;
+                f32x4 hacc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                for (int i = 0; i < 4; i++) {
+                    const float fa = prelu(acc[j][0][i] + cb3[0][i], ca3[0][i]);
+                    const float fb = prelu(acc[j][1][i] + cb3[1][i], ca3[1][i]);
+                    hacc = __builtin_amdgcn_mfma_f32_16x16x4f32(hwA[0][i], fa, hacc, 0, 0, 0);
+                    hacc = __builtin_amdgcn_mfma_f32_16x16x4f32(hwA[1][i], fb, hacc, 0, 0, 0);
+                }
+                // hacc: lane (cell lr, heads 4*lk + i): group 0 = (a0, a1, r0, r1), group 1 = (r2, r3, -, -)
+                const float r2 = __shfl_down(hacc[0], 16), r3 = __shfl_down(hacc[1], 16);
+                const int y = f >> 1, x = (f & 1) * 16 + lr;
+                const int oy = oy0 + y, ox = ox0 + x;
+                const bool valid = (lk == 0) && (oy < P.ph) && (ox < P.pw);
+                const float a0 = hacc[0] + hb0, a1v = hacc[1] + hb1;
+                const float mx = fmaxf(a0, a1v);
+                const float e0 = expf(a0 - mx), e1 = expf(a1v - mx);
+                const float prob = __fdiv_rn(e1, e0 + e1);
+                const float q0 = hacc[2] + hb2, q1 = hacc[3] + hb3, q2 = r2 + hb4, q3 = r3 + hb5;
+                if (DENSE) {
+                    if (valid) {
+                        int64_t plane = (int64_t)P.ph * P.pw;
+                        int64_t cell = (int64_t)oy * P.pw + ox;
+                        o.prob[(int64_t)b * plane + cell] = prob;
+                        float* rg = o.reg + (int64_t)b * 4 * plane + cell;
+                        rg[0] = q0;
+                        rg[plane] = q1;
+                        rg[2 * plane] = q2;
+                        rg[3 * plane] = q3;
+                    }
+                } else {
+                    // mask = prob >= 0.6 (mtcnn.py:183; the python scalar compares as fp32)
+                    bool pass = valid && (prob >= 0.6f) && !(o.dbg & 16);
+                    uint64_t bal = __ballot(pass);
+                    if (bal) {
+                        int leader = __builtin_ctzll(bal);
+                        uint32_t base = 0;
+                        if (lane == leader) {
+                            base = atomicAdd(o.count, (uint32_t)__popcll(bal));
+                            atomicAdd(&o.level_count[L], (uint32_t)__popcll(bal));
+                        }
+                        base = __shfl(base, leader);
+                        if (pass) {
+                            uint32_t slot = base + (uint32_t)__popcll(bal & ((1ull << lane) - 1ull));
+                            if (slot < o.cap) {
+                                uint32_t lin = (uint32_t)(((int64_t)b * P.ph + oy) * P.pw + ox);
+                                o.key[slot] = ((uint64_t)L << 32) | lin;
+                                o.score[slot] = prob;
+                                o.regv[slot] = make_float4(q0, q1, q2, q3);
+                            }
+                        }
+                    }
+                }
+            }
+        }
+        __syncthreads();  // sA/sP are rewritten by the next tile
     }
 }
 
 void launch_pnet(bool dense, const uint8_t* frames, int64_t frame_stride, int64_t row_stride, int H, int W,
                  const PNetLevel* d_levels, int n_levels, int64_t total_tiles, const PNetW& w, const PNetOut& o,
-                 hipStream_t st) {
+                 uint32_t* d_tile_ctr, hipStream_t st) {
     if (total_tiles <= 0) return;
+    VTF_HIP(hipMemsetAsync(d_tile_ctr, 0, 4, st));
+    int dev = 0, cus = 256;
+    VTF_HIP(hipGetDevice(&dev));
+    VTF_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+    int64_t grid = std::min<int64_t>(total_tiles, (int64_t)cus * PNET_GROUPS_PER_CU);
     if (dense)
-        k_pnet<true><<<(unsigned)total_tiles, 256, 0, st>>>(frames, frame_stride, row_stride, H, W, d_levels, n_levels,
-                                                             w, o);
+        k_pnet<true><<<(unsigned)grid, 256, 0, st>>>(frames, frame_stride, row_stride, H, W, d_levels, n_levels,
+                                                      total_tiles, d_tile_ctr, w, o);
     else
-        k_pnet<false><<<(unsigned)total_tiles, 256, 0, st>>>(frames, frame_stride, row_stride, H, W, d_levels,
-                                                              n_levels, w, o);
+        k_pnet<false><<<(unsigned)grid, 256, 0, st>>>(frames, frame_stride, row_stride, H, W, d_levels, n_levels,
+                                                       total_tiles, d_tile_ctr, w, o);
 }
 
 // ----------------------------------------------------------------------------------- RNet

@@ -2,6 +2,7 @@
 // Mirrors MTCNN.forward (src/videotofaces/detectors/mtcnn.py:167-252) step by step; every
 // data-dependent size is read back once per stage (7 host syncs per det-batch).
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <numeric>
 #include <vector>
@@ -53,7 +54,7 @@ struct Mtcnn {
 enum Slot {
     S_FRAMES = 0, S_LEVELS, S_COUNT, S_KEY, S_SCORE, S_REGV, S_KEY2, S_SLOT, S_SLOT2, S_B1, S_S1, S_R1, S_I1, S_C1,
     S_KEEP, S_B2, S_S2, S_R2, S_I2, S_C2, S_PROB, S_REG, S_LM, S_ERR, S_FLAG, S_INCL, S_IDX, S_LMK, S_OUTB, S_OUTS,
-    S_OUTL, S_OUTI, S_SORT, S_SCAN
+    S_OUTL, S_OUTI, S_SORT, S_SCAN, S_PRE
 };
 
 // ---- weights: reference state_dict order (specs.py mtcnn_spec) -> transposed device layout
@@ -209,10 +210,27 @@ static void detect(Mtcnn& m, const uint8_t* frames, int on_dev, int B, int H, in
     m.stats[0] = NL;
     if (NL == 0) return;
     VTF_CHECK(NL < 4096 && cells < (int64_t)1 << 31, VTF_E_LIMIT, "mtcnn: pyramid too large for one call");
+    // downsampled levels whose adaptive-pool bins exceed 2 frame pixels are resampled by a
+    // separate fully parallel kernel (one thread per level value) into HBM; inside the fused
+    // tile kernel their long serial bin sums would leave a few workgroups as a long tail.
+    {
+        int64_t pre_elems = 0;
+        for (auto& L : lv)
+            if ((int64_t)H > 2 * (int64_t)L.lh) pre_elems += (int64_t)B * 3 * L.lh * L.lw;
+        float* pre = pre_elems ? m.ar.get<float>(S_PRE, pre_elems) : nullptr;
+        for (auto& L : lv) {
+            L.pre = nullptr;
+            if ((int64_t)H > 2 * (int64_t)L.lh) {
+                L.pre = pre;
+                launch_resample(fr, fstride, rstride, B, H, W, L.lh, L.lw, pre, st);
+                pre += (int64_t)B * 3 * L.lh * L.lw;
+            }
+        }
+    }
     PNetLevel* d_lv = m.ar.get<PNetLevel>(S_LEVELS, NL);
     VTF_HIP(hipMemcpyAsync(d_lv, lv.data(), NL * sizeof(PNetLevel), hipMemcpyHostToDevice, st));
-    uint32_t* d_cnt = m.ar.get<uint32_t>(S_COUNT, NL + 1);
-    VTF_HIP(hipMemsetAsync(d_cnt, 0, (NL + 1) * 4, st));
+    uint32_t* d_cnt = m.ar.get<uint32_t>(S_COUNT, NL + 2);
+    VTF_HIP(hipMemsetAsync(d_cnt, 0, (NL + 2) * 4, st));
     PNetOut po{};
     po.count = d_cnt;
     po.level_count = d_cnt + 1;
@@ -220,8 +238,9 @@ static void detect(Mtcnn& m, const uint8_t* frames, int on_dev, int B, int H, in
     po.key = m.ar.get<uint64_t>(S_KEY, cells);
     po.score = m.ar.get<float>(S_SCORE, cells);
     po.regv = m.ar.get<float4>(S_REGV, cells);
+    if (const char* e = getenv("VTF_PNET_DEBUG")) po.dbg = atoi(e);
     if (m.prof) VTF_HIP(hipEventRecord(m.ev0, st));
-    launch_pnet(false, fr, fstride, rstride, H, W, d_lv, NL, tiles, m.pw, po, st);
+    launch_pnet(false, fr, fstride, rstride, H, W, d_lv, NL, tiles, m.pw, po, d_cnt + NL + 1, st);
     if (m.prof) VTF_HIP(hipEventRecord(m.ev1, st));
     std::vector<uint32_t> cnt(NL + 1);
     d2h_sync(cnt.data(), d_cnt, (NL + 1) * 4, st);
@@ -458,13 +477,20 @@ int vtf_mtcnn_pnet_level(vtf_mtcnn_t h, const uint8_t* d_frames, int B, int H, i
         L.tiles_y = cdiv(L.ph, PNET_TH);
         L.tiles_x = cdiv(L.pw, PNET_TW);
         L.tile_beg = 0;
+        L.pre = nullptr;
+        if ((int64_t)H > 2 * (int64_t)lh) {
+            float* pre = h->m.ar.get<float>(S_PRE, (int64_t)B * 3 * lh * lw);
+            launch_resample(d_frames, frame_stride, row_stride, B, H, W, lh, lw, pre, h->m.st);
+            L.pre = pre;
+        }
         PNetLevel* d_lv = h->m.ar.get<PNetLevel>(S_LEVELS, 1);
         VTF_HIP(hipMemcpyAsync(d_lv, &L, sizeof(L), hipMemcpyHostToDevice, h->m.st));
         PNetOut po{};
         po.prob = d_prob;
         po.reg = d_reg;
+        uint32_t* ctr = h->m.ar.get<uint32_t>(S_COUNT, 4);
         launch_pnet(true, d_frames, frame_stride, row_stride, H, W, d_lv, 1, (int64_t)B * L.tiles_x * L.tiles_y,
-                    h->m.pw, po, h->m.st);
+                    h->m.pw, po, ctr, h->m.st);
         VTF_HIP(hipStreamSynchronize(h->m.st));
     });
 }
