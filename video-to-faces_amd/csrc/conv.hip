@@ -204,6 +204,7 @@ __global__ __launch_bounds__(256) void k_conv(ConvParams p) {
                 if (p.scale != 1.f) v = v * p.scale;
                 if (res) v = v + to_f(res[m * p.res_cstride + c]);
                 if (p.relu) v = fmaxf(v, 0.f);
+                if (p.prelu) v = v > 0.f ? v : p.prelu[c] * v;
                 out[m * p.out_cstride + p.out_coff + c] = from_f<T>(v);
             }
         }
@@ -266,6 +267,46 @@ void launch_maxpool(const void* in, int N, int H, int W, int C, void* out, int o
     else
         k_maxpool<float><<<cdiv(tot, 256), 256, 0, st>>>((const float*)in, N, H, W, C, OH, OW, (float*)out,
                                                           out_cstride, out_coff);
+}
+
+// ---------------------------------------------------------------- maxpool k/s with ceil_mode (NHWC fp32)
+__global__ void k_maxpool_ks(const float* __restrict__ in, int N, int H, int W, int C, int k, int s, int OH, int OW,
+                             float* __restrict__ out) {
+    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    int64_t tot = (int64_t)N * OH * OW * C;
+    if (i >= tot) return;
+    int c = (int)(i % C);
+    int64_t t = i / C;
+    int ow = (int)(t % OW);
+    t /= OW;
+    int oh = (int)(t % OH);
+    int n = (int)(t / OH);
+    float m = -3.402823466e38f;
+    for (int dy = 0; dy < k; dy++) {
+        int y = oh * s + dy;
+        if (y >= H) break;
+        for (int dx = 0; dx < k; dx++) {
+            int x = ow * s + dx;
+            if (x >= W) break;
+            m = fmaxf(m, in[(((int64_t)n * H + y) * W + x) * C + c]);
+        }
+    }
+    out[i] = m;
+}
+
+static int pool_out(int L, int k, int s, bool ceil_mode) {
+    // torch pooling_output_shape with padding 0, dilation 1
+    int o = ((L - k + (ceil_mode ? s - 1 : 0)) / s) + 1;
+    if (ceil_mode && (o - 1) * s >= L) o--;
+    return o;
+}
+
+void launch_maxpool_ks(const float* in, int N, int H, int W, int C, int k, int s, bool ceil_mode, float* out,
+                       int& OH, int& OW, hipStream_t st) {
+    OH = pool_out(H, k, s, ceil_mode);
+    OW = pool_out(W, k, s, ceil_mode);
+    int64_t tot = (int64_t)N * OH * OW * C;
+    if (tot > 0) k_maxpool_ks<<<cdiv(tot, 256), 256, 0, st>>>(in, N, H, W, C, k, s, OH, OW, out);
 }
 
 // ---------------------------------------------------------------- NCHW fp32 -> NHWC (C padded to Cp)

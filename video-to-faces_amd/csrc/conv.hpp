@@ -11,6 +11,7 @@ struct ConvParams {
     const float* alpha;  // BN scale (or null) -> v = v*alpha + beta
     const float* beta;
     const void* res;     // residual (NHWC, stride res_cstride) added after scale
+    const float* prelu;  // per-channel PReLU slope (or null), applied last
     float scale;
     int relu;
     int64_t M;           // N*OH*OW
@@ -21,6 +22,9 @@ struct ConvParams {
 void launch_conv(const ConvParams& p, bool bf16, hipStream_t st);
 void launch_maxpool(const void* in, int N, int H, int W, int C, void* out, int out_cstride, int out_coff, bool bf16,
                     hipStream_t st);
+// torch MaxPool2d(k, s, ceil_mode) without padding, NHWC fp32; returns (OH, OW)
+void launch_maxpool_ks(const float* in, int N, int H, int W, int C, int k, int s, bool ceil_mode, float* out,
+                       int& OH, int& OW, hipStream_t st);
 void launch_nchw_to_nhwc(const float* in, int N, int C, int H, int W, int Cp, void* out, bool bf16, hipStream_t st);
 void launch_facenet_head(const void* x, int N, int HW, int C, const float* w, const float* alpha, const float* beta,
                          int D, float* out, bool bf16, hipStream_t st);

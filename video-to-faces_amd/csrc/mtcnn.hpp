@@ -30,25 +30,18 @@ struct PNetOut {
     float* reg;
     int dbg;  // phase-skip mask for profiling (env VTF_PNET_DEBUG): 1 fill, 2 conv1, 4 conv2, 8 conv3
 };
-struct RNetW {
-    const float *c1w, *c1b, *p1, *c2w, *c2b, *p2, *c3w, *c3b, *p3, *d4w, *d4b, *p4, *d51w, *d51b, *d52w, *d52b;
-};
-struct ONetW {
-    const float *c1w, *c1b, *p1, *c2w, *c2b, *p2, *c3w, *c3b, *p3, *c4w, *c4b, *p4, *d5w, *d5b, *p5, *d61w, *d61b,
-        *d62w, *d62b, *d63w, *d63b;
-};
 
 void launch_resample(const uint8_t* frames, int64_t frame_stride, int64_t row_stride, int B, int H, int W, int lh,
                      int lw, float* out, hipStream_t st);
 void launch_pnet(bool dense, const uint8_t* frames, int64_t frame_stride, int64_t row_stride, int H, int W,
                  const PNetLevel* d_levels, int n_levels, int64_t total_tiles, const PNetW& w, const PNetOut& o,
                  uint32_t* d_tile_ctr, hipStream_t st);
-void launch_rnet(const uint8_t* frames, int64_t frame_stride, int64_t row_stride, int H, int W, const float4* boxes,
-                 const int32_t* img, const float* xin, int64_t n, const RNetW& w, float4* reg, float* prob,
-                 int32_t* err, hipStream_t st);
-void launch_onet(const uint8_t* frames, int64_t frame_stride, int64_t row_stride, int H, int W, const float4* boxes,
-                 const int32_t* img, const float* xin, int64_t n, const ONetW& w, float4* reg, float* lm, float* prob,
-                 int32_t* err, hipStream_t st);
+void launch_crop_nhwc(const uint8_t* frames, int64_t frame_stride, int64_t row_stride, int H, int W,
+                      const float4* boxes, const int32_t* img, int64_t n, int S, float* out, int32_t* err,
+                      hipStream_t st);
+void launch_heads(const float* x, int64_t n, int D, const float* w1, const float* b1, const float* w2,
+                  const float* b2, const float* w3, const float* b3, float* prob, float4* reg, float* lm,
+                  hipStream_t st);
 void launch_decode_stage1(const uint64_t* key_sorted, const int32_t* slot_sorted, const float* score,
                           const float4* regv, const PNetLevel* lv, int64_t n, float4* boxes, float* sc, float4* reg,
                           int32_t* img, int32_t* call, hipStream_t st);

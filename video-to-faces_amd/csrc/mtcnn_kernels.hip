@@ -81,21 +81,10 @@ __device__ inline bool crop_rect(float4 b, int H, int W, int& y0, int& x0, int& 
 // constant-address-space views of the weight structs (scalar loads, see common.hpp)
 #define CW const VTF_CONST float*
 struct PNetWC { CW c1w; CW c1b; CW p1; CW c2w; CW c2b; CW p2; CW c3w; CW c3b; CW p3; CW c41w; CW c41b; CW c42w; CW c42b; };
-struct RNetWC { CW c1w; CW c1b; CW p1; CW c2w; CW c2b; CW p2; CW c3w; CW c3b; CW p3; CW d4w; CW d4b; CW p4; CW d51w; CW d51b; CW d52w; CW d52b; };
-struct ONetWC { CW c1w; CW c1b; CW p1; CW c2w; CW c2b; CW p2; CW c3w; CW c3b; CW p3; CW c4w; CW c4b; CW p4; CW d5w; CW d5b; CW p5; CW d61w; CW d61b; CW d62w; CW d62b; CW d63w; CW d63b; };
 #undef CW
 __device__ inline PNetWC to_const(const PNetW& w) {
     return {cptr(w.c1w), cptr(w.c1b), cptr(w.p1), cptr(w.c2w), cptr(w.c2b), cptr(w.p2), cptr(w.c3w), cptr(w.c3b),
             cptr(w.p3), cptr(w.c41w), cptr(w.c41b), cptr(w.c42w), cptr(w.c42b)};
-}
-__device__ inline RNetWC to_const(const RNetW& w) {
-    return {cptr(w.c1w), cptr(w.c1b), cptr(w.p1), cptr(w.c2w), cptr(w.c2b), cptr(w.p2), cptr(w.c3w), cptr(w.c3b),
-            cptr(w.p3), cptr(w.d4w), cptr(w.d4b), cptr(w.p4), cptr(w.d51w), cptr(w.d51b), cptr(w.d52w), cptr(w.d52b)};
-}
-__device__ inline ONetWC to_const(const ONetW& w) {
-    return {cptr(w.c1w), cptr(w.c1b), cptr(w.p1),  cptr(w.c2w),  cptr(w.c2b),  cptr(w.p2),  cptr(w.c3w),
-            cptr(w.c3b), cptr(w.p3),  cptr(w.c4w), cptr(w.c4b),  cptr(w.p4),   cptr(w.d5w), cptr(w.d5b),
-            cptr(w.p5),  cptr(w.d61w), cptr(w.d61b), cptr(w.d62w), cptr(w.d62b), cptr(w.d63w), cptr(w.d63b)};
 }
 
 // ----------------------------------------------------------------------------------- resample
@@ -466,371 +455,82 @@ void launch_pnet(bool dense, const uint8_t* frames, int64_t frame_stride, int64_
                                                        total_tiles, d_tile_ctr, w, o);
 }
 
-// ----------------------------------------------------------------------------------- RNet
+// ----------------------------------------------------------------------------------- RNet / ONet
+// The candidate networks run as batched layers on the MFMA implicit-GEMM conv kernel
+// (conv.hip, fp32, PReLU epilogue); here: the crop front end and the tiny heads.
 
-// LDS plan (floats): A 13552 = conv1 [28][22][22]; later conv2 [48][9][9] @0, pool2 [48][4][4]
-// @3888, flat [576] @4656, dense4 [128] @5232.  B 3388 = pool1 [28][11][11].  C 1728 = input.
-template <bool FROM_FRAMES>
-__global__ __launch_bounds__(256) void k_rnet(const uint8_t* __restrict__ frames, int64_t frame_stride,
-                                              int64_t row_stride, int H, int W, const float4* __restrict__ boxes,
-                                              const int32_t* __restrict__ img, const float* __restrict__ xin,
-                                              RNetW wg, float4* __restrict__ reg_out, float* __restrict__ prob_out,
-                                              int32_t* __restrict__ err) {
-    const auto wc = to_const(wg);
-    __shared__ float sA[13552];
-    __shared__ float sB[3388];
-    __shared__ float sC[1728];
-    const int tid = threadIdx.x;
-    const int64_t n = blockIdx.x;
-    if (FROM_FRAMES) {
-        int y0, x0, hc, wc;
-        if (!crop_rect(boxes[n], H, W, y0, x0, hc, wc)) {
-            if (tid == 0) atomicAdd(err, 1);
-            return;
+// _get_cropped_candidates (mtcnn.py:153-163): crop of the preprocessed frame, adaptive-pooled
+// to S x S, written NHWC with 8 channels (RGB + zero pad) for the conv kernel.
+__global__ void k_crop_nhwc(const uint8_t* __restrict__ frames, int64_t frame_stride, int64_t row_stride, int H,
+                            int W, const float4* __restrict__ boxes, const int32_t* __restrict__ img, int64_t n,
+                            int S, float* __restrict__ out, int32_t* __restrict__ err) {
+    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n * S * S) return;
+    int q = (int)(i % S), r = (int)((i / S) % S);
+    int64_t k = i / ((int64_t)S * S);
+    int y0, x0, hc, wc;
+    float* o = out + i * 8;
+    if (!crop_rect(boxes[k], H, W, y0, x0, hc, wc)) {
+        if (r == 0 && q == 0) atomicAdd(err, 1);
+        for (int c = 0; c < 8; c++) o[c] = 0.f;
+        return;
+    }
+    const uint8_t* fr = frames + (int64_t)img[k] * frame_stride;
+    for (int c = 0; c < 3; c++) o[c] = crop_value(fr, row_stride, c, r, q, y0, x0, hc, wc, S);
+    for (int c = 3; c < 8; c++) o[c] = 0.f;
+}
+
+void launch_crop_nhwc(const uint8_t* frames, int64_t frame_stride, int64_t row_stride, int H, int W,
+                      const float4* boxes, const int32_t* img, int64_t n, int S, float* out, int32_t* err,
+                      hipStream_t st) {
+    if (n > 0) k_crop_nhwc<<<cdiv(n * S * S, 256), 256, 0, st>>>(frames, frame_stride, row_stride, H, W, boxes, img, n,
+                                                                  S, out, err);
+}
+
+// heads: x [n, D] -> softmax(x W1^T + b1)[:, 1], x W2^T + b2 (4), optional x W3^T + b3 (10).
+// One wave per candidate; lanes split D, wave-reduced.  RNet's softmax is over the last dim
+// (torch multiplies by the reciprocal sum), ONet's too.
+__global__ __launch_bounds__(64) void k_heads(const float* __restrict__ x, int64_t n, int D,
+                                              const float* __restrict__ w1, const float* __restrict__ b1,
+                                              const float* __restrict__ w2, const float* __restrict__ b2,
+                                              const float* __restrict__ w3, const float* __restrict__ b3,
+                                              float* __restrict__ prob, float4* __restrict__ reg,
+                                              float* __restrict__ lm) {
+    const int64_t k = blockIdx.x;
+    const int lane = threadIdx.x;
+    const float* xk = x + k * D;
+    float part[16];
+#pragma unroll
+    for (int j = 0; j < 16; j++) part[j] = 0.f;
+    for (int d = lane; d < D; d += 64) {
+        float f = xk[d];
+        part[0] = fmaf(f, w1[d], part[0]);
+        part[1] = fmaf(f, w1[D + d], part[1]);
+#pragma unroll
+        for (int j = 0; j < 4; j++) part[2 + j] = fmaf(f, w2[j * D + d], part[2 + j]);
+        if (w3) {
+#pragma unroll
+            for (int j = 0; j < 10; j++) part[6 + j] = fmaf(f, w3[j * D + d], part[6 + j]);
         }
-        const uint8_t* fr = frames + (int64_t)img[n] * frame_stride;
-        for (int i = tid; i < 1728; i += 256) {
-            int c = i / 576, r = (i / 24) % 24, q = i % 24;
-            sC[i] = crop_value(fr, row_stride, c, r, q, y0, x0, hc, wc, 24);
-        }
-    } else {
-        for (int i = tid; i < 1728; i += 256) sC[i] = xin[n * 1728 + i];
     }
-    __syncthreads();
-    // conv1 3->28 3x3: 22x22
-    for (int i = tid; i < 484; i += 256) {
-        int y = i / 22, x = i % 22;
-        float acc[28];
 #pragma unroll
-        for (int co = 0; co < 28; co++) acc[co] = wc.c1b[co];
-#pragma unroll
-        for (int c = 0; c < 3; c++)
-#pragma unroll
-            for (int ky = 0; ky < 3; ky++)
-#pragma unroll
-                for (int kx = 0; kx < 3; kx++) {
-                    float v = sC[(c * 24 + y + ky) * 24 + x + kx];
-                    const VTF_CONST float* wp = wc.c1w + ((c * 3 + ky) * 3 + kx) * 28;
-#pragma unroll
-                    for (int co = 0; co < 28; co++) acc[co] = fmaf(v, wp[co], acc[co]);
-                }
-#pragma unroll
-        for (int co = 0; co < 28; co++) sA[co * 484 + i] = prelu(acc[co], wc.p1[co]);
-    }
-    __syncthreads();
-    // maxpool 3/2 ceil: 22 -> 11
-    for (int i = tid; i < 3388; i += 256) {
-        int c = i / 121, y = (i / 11) % 11, x = i % 11;
-        float m = -3.402823466e38f;
-        for (int dy = 0; dy < 3; dy++)
-            for (int dx = 0; dx < 3; dx++) {
-                int yy = 2 * y + dy, xx = 2 * x + dx;
-                if (yy < 22 && xx < 22) m = fmaxf(m, sA[c * 484 + yy * 22 + xx]);
-            }
-        sB[i] = m;
-    }
-    __syncthreads();
-    // conv2 28->48 3x3: 9x9; item = (pos, 16-channel group)
-    for (int i = tid; i < 81 * 3; i += 256) {
-        int pos = i % 81, g = i / 81;
-        int y = pos / 9, x = pos % 9;
-        float acc[16];
-#pragma unroll
-        for (int k = 0; k < 16; k++) acc[k] = wc.c2b[g * 16 + k];
-        for (int c = 0; c < 28; c++) {
-#pragma unroll
-            for (int ky = 0; ky < 3; ky++)
-#pragma unroll
-                for (int kx = 0; kx < 3; kx++) {
-                    float v = sB[c * 121 + (y + ky) * 11 + x + kx];
-                    const VTF_CONST float* wp = wc.c2w + ((c * 3 + ky) * 3 + kx) * 48 + g * 16;
-#pragma unroll
-                    for (int k = 0; k < 16; k++) acc[k] = fmaf(v, wp[k], acc[k]);
-                }
-        }
-#pragma unroll
-        for (int k = 0; k < 16; k++) sA[(g * 16 + k) * 81 + pos] = prelu(acc[k], wc.p2[g * 16 + k]);
-    }
-    __syncthreads();
-    // maxpool 3/2 ceil: 9 -> 4
-    for (int i = tid; i < 768; i += 256) {
-        int c = i / 16, y = (i / 4) % 4, x = i % 4;
-        float m = -3.402823466e38f;
-        for (int dy = 0; dy < 3; dy++)
-            for (int dx = 0; dx < 3; dx++) {
-                int yy = 2 * y + dy, xx = 2 * x + dx;
-                if (yy < 9 && xx < 9) m = fmaxf(m, sA[c * 81 + yy * 9 + xx]);
-            }
-        sA[3888 + i] = m;
-    }
-    __syncthreads();
-    // conv3 48->64 2x2: 3x3 -> flat (permute 0,3,2,1: index = x*192 + y*64 + c)
-    for (int i = tid; i < 9 * 8; i += 256) {
-        int pos = i % 9, g = i / 9;
-        int y = pos / 3, x = pos % 3;
-        float acc[8];
-#pragma unroll
-        for (int k = 0; k < 8; k++) acc[k] = wc.c3b[g * 8 + k];
-        for (int c = 0; c < 48; c++) {
-#pragma unroll
-            for (int ky = 0; ky < 2; ky++)
-#pragma unroll
-                for (int kx = 0; kx < 2; kx++) {
-                    float v = sA[3888 + c * 16 + (y + ky) * 4 + x + kx];
-                    const VTF_CONST float* wp = wc.c3w + ((c * 2 + ky) * 2 + kx) * 64 + g * 8;
-#pragma unroll
-                    for (int k = 0; k < 8; k++) acc[k] = fmaf(v, wp[k], acc[k]);
-                }
-        }
-#pragma unroll
-        for (int k = 0; k < 8; k++) sA[4656 + x * 192 + y * 64 + g * 8 + k] = prelu(acc[k], wc.p3[g * 8 + k]);
-    }
-    __syncthreads();
-    // dense4 576->128 + PReLU; weights transposed [k][128]
-    if (tid < 128) {
-        float acc = wc.d4b[tid];
-        for (int k = 0; k < 576; k++) acc = fmaf(sA[4656 + k], wc.d4w[k * 128 + tid], acc);
-        sA[5232 + tid] = prelu(acc, wc.p4[tid]);
-    }
-    __syncthreads();
-    if (tid < 64) {
-        // heads: dense5_1 (2) softmax, dense5_2 (4); wave reduction over 128 inputs
-        float part[6];
-#pragma unroll
-        for (int j = 0; j < 6; j++) part[j] = 0.f;
-        for (int k = tid; k < 128; k += 64) {
-            float f = sA[5232 + k];
-            part[0] = fmaf(f, wc.d51w[k], part[0]);
-            part[1] = fmaf(f, wc.d51w[128 + k], part[1]);
-#pragma unroll
-            for (int j = 0; j < 4; j++) part[2 + j] = fmaf(f, wc.d52w[j * 128 + k], part[2 + j]);
-        }
-#pragma unroll
-        for (int j = 0; j < 6; j++)
-            for (int off = 32; off > 0; off >>= 1) part[j] += __shfl_xor(part[j], off);
-        if (tid == 0) {
-            float a0 = part[0] + wc.d51b[0], a1 = part[1] + wc.d51b[1];
-            float mx = fmaxf(a0, a1);
-            float e0 = expf(a0 - mx), e1 = expf(a1 - mx);
-            prob_out[n] = e1 * __fdiv_rn(1.0f, e0 + e1);
-            reg_out[n] = make_float4(part[2] + wc.d52b[0], part[3] + wc.d52b[1], part[4] + wc.d52b[2], part[5] + wc.d52b[3]);
-        }
+    for (int j = 0; j < 16; j++)
+        for (int off = 32; off > 0; off >>= 1) part[j] += __shfl_xor(part[j], off);
+    if (lane == 0) {
+        float a0 = part[0] + b1[0], a1 = part[1] + b1[1];
+        float mx = fmaxf(a0, a1);
+        float e0 = expf(a0 - mx), e1 = expf(a1 - mx);
+        prob[k] = e1 * __fdiv_rn(1.0f, e0 + e1);
+        reg[k] = make_float4(part[2] + b2[0], part[3] + b2[1], part[4] + b2[2], part[5] + b2[3]);
+        if (w3)
+            for (int j = 0; j < 10; j++) lm[k * 10 + j] = part[6 + j] + b3[j];
     }
 }
 
-void launch_rnet(const uint8_t* frames, int64_t frame_stride, int64_t row_stride, int H, int W, const float4* boxes,
-                 const int32_t* img, const float* xin, int64_t n, const RNetW& w, float4* reg, float* prob,
-                 int32_t* err, hipStream_t st) {
-    if (n <= 0) return;
-    if (xin)
-        k_rnet<false><<<(unsigned)n, 256, 0, st>>>(frames, frame_stride, row_stride, H, W, boxes, img, xin, w, reg,
-                                                    prob, err);
-    else
-        k_rnet<true><<<(unsigned)n, 256, 0, st>>>(frames, frame_stride, row_stride, H, W, boxes, img, xin, w, reg,
-                                                   prob, err);
-}
-
-// ----------------------------------------------------------------------------------- ONet
-
-// LDS plan (floats): X 14112 = input [3][48][48] (6912) / conv2 half [32][21][21] (14112) /
-// later conv3 [64][8][8] @0 (4096), pool3 [64][4][4] @4096 (1024), conv4 flat [1152] @5120,
-// dense5 [256] @6272.  Y 16928 = pool1 [32][23][23].  Z 6400 = pool2 [64][10][10].
-template <bool FROM_FRAMES>
-__global__ __launch_bounds__(512) void k_onet(const uint8_t* __restrict__ frames, int64_t frame_stride,
-                                              int64_t row_stride, int H, int W, const float4* __restrict__ boxes,
-                                              const int32_t* __restrict__ img, const float* __restrict__ xin,
-                                              ONetW wg, float4* __restrict__ reg_out, float* __restrict__ lm_out,
-                                              float* __restrict__ prob_out, int32_t* __restrict__ err) {
-    const auto wc = to_const(wg);
-    __shared__ float sX[14112];
-    __shared__ float sY[16928];
-    __shared__ float sZ[6400];
-    const int tid = threadIdx.x;
-    const int64_t n = blockIdx.x;
-    if (FROM_FRAMES) {
-        int y0, x0, hc, wc;
-        if (!crop_rect(boxes[n], H, W, y0, x0, hc, wc)) {
-            if (tid == 0) atomicAdd(err, 1);
-            return;
-        }
-        const uint8_t* fr = frames + (int64_t)img[n] * frame_stride;
-        for (int i = tid; i < 6912; i += 512) {
-            int c = i / 2304, r = (i / 48) % 48, q = i % 48;
-            sX[i] = crop_value(fr, row_stride, c, r, q, y0, x0, hc, wc, 48);
-        }
-    } else {
-        for (int i = tid; i < 6912; i += 512) sX[i] = xin[n * 6912 + i];
-    }
-    __syncthreads();
-    // conv1 3->32 3x3 (46x46) + PReLU + maxpool 3/2 ceil (23x23), fused: each item is one
-    // pooled position; its <= 3x3 conv1 window is recomputed (conv1 is cheap: K=27).
-    for (int i = tid; i < 529; i += 512) {
-        int py = i / 23, px = i % 23;
-        float m[32];
-#pragma unroll
-        for (int co = 0; co < 32; co++) m[co] = -3.402823466e38f;
-        for (int dy = 0; dy < 3; dy++) {
-            int y = 2 * py + dy;
-            if (y >= 46) break;
-            for (int dx = 0; dx < 3; dx++) {
-                int x = 2 * px + dx;
-                if (x >= 46) break;
-                float acc[32];
-#pragma unroll
-                for (int co = 0; co < 32; co++) acc[co] = wc.c1b[co];
-#pragma unroll
-                for (int c = 0; c < 3; c++)
-#pragma unroll
-                    for (int ky = 0; ky < 3; ky++)
-#pragma unroll
-                        for (int kx = 0; kx < 3; kx++) {
-                            float v = sX[(c * 48 + y + ky) * 48 + x + kx];
-                            const VTF_CONST float* wp = wc.c1w + ((c * 3 + ky) * 3 + kx) * 32;
-#pragma unroll
-                            for (int co = 0; co < 32; co++) acc[co] = fmaf(v, wp[co], acc[co]);
-                        }
-#pragma unroll
-                for (int co = 0; co < 32; co++) m[co] = fmaxf(m[co], prelu(acc[co], wc.p1[co]));
-            }
-        }
-#pragma unroll
-        for (int co = 0; co < 32; co++) sY[co * 529 + i] = m[co];
-    }
-    __syncthreads();
-    // conv2 32->64 3x3 (21x21) in two halves of 32 channels, each + PReLU + maxpool 3/2 ceil (10x10)
-    for (int half = 0; half < 2; half++) {
-        for (int i = tid; i < 441 * 4; i += 512) {
-            int pos = i % 441, g = i / 441;  // 8-channel group within the half
-            int y = pos / 21, x = pos % 21;
-            int cb = half * 32 + g * 8;
-            float acc[8];
-#pragma unroll
-            for (int k = 0; k < 8; k++) acc[k] = wc.c2b[cb + k];
-            for (int c = 0; c < 32; c++) {
-#pragma unroll
-                for (int ky = 0; ky < 3; ky++)
-#pragma unroll
-                    for (int kx = 0; kx < 3; kx++) {
-                        float v = sY[c * 529 + (y + ky) * 23 + x + kx];
-                        const VTF_CONST float* wp = wc.c2w + ((c * 3 + ky) * 3 + kx) * 64 + cb;
-#pragma unroll
-                        for (int k = 0; k < 8; k++) acc[k] = fmaf(v, wp[k], acc[k]);
-                    }
-            }
-#pragma unroll
-            for (int k = 0; k < 8; k++) sX[(g * 8 + k) * 441 + pos] = prelu(acc[k], wc.p2[cb + k]);
-        }
-        __syncthreads();
-        for (int i = tid; i < 3200; i += 512) {
-            int c = i / 100, y = (i / 10) % 10, x = i % 10;
-            float m = -3.402823466e38f;
-            for (int dy = 0; dy < 3; dy++)
-                for (int dx = 0; dx < 3; dx++) {
-                    int yy = 2 * y + dy, xx = 2 * x + dx;
-                    if (yy < 21 && xx < 21) m = fmaxf(m, sX[c * 441 + yy * 21 + xx]);
-                }
-            sZ[(half * 32 + c) * 100 + y * 10 + x] = m;
-        }
-        __syncthreads();
-    }
-    // conv3 64->64 3x3 (8x8) + PReLU
-    for (int i = tid; i < 64 * 8; i += 512) {
-        int pos = i % 64, g = i / 64;
-        int y = pos / 8, x = pos % 8;
-        float acc[8];
-#pragma unroll
-        for (int k = 0; k < 8; k++) acc[k] = wc.c3b[g * 8 + k];
-        for (int c = 0; c < 64; c++) {
-#pragma unroll
-            for (int ky = 0; ky < 3; ky++)
-#pragma unroll
-                for (int kx = 0; kx < 3; kx++) {
-                    float v = sZ[c * 100 + (y + ky) * 10 + x + kx];
-                    const VTF_CONST float* wp = wc.c3w + ((c * 3 + ky) * 3 + kx) * 64 + g * 8;
-#pragma unroll
-                    for (int k = 0; k < 8; k++) acc[k] = fmaf(v, wp[k], acc[k]);
-                }
-        }
-#pragma unroll
-        for (int k = 0; k < 8; k++) sX[(g * 8 + k) * 64 + pos] = prelu(acc[k], wc.p3[g * 8 + k]);
-    }
-    __syncthreads();
-    // maxpool 2/2 ceil: 8 -> 4
-    for (int i = tid; i < 1024; i += 512) {
-        int c = i / 16, y = (i / 4) % 4, x = i % 4;
-        float m = -3.402823466e38f;
-        for (int dy = 0; dy < 2; dy++)
-            for (int dx = 0; dx < 2; dx++) m = fmaxf(m, sX[c * 64 + (2 * y + dy) * 8 + 2 * x + dx]);
-        sX[4096 + i] = m;
-    }
-    __syncthreads();
-    // conv4 64->128 2x2 (3x3) + PReLU -> flat (x*384 + y*128 + c)
-    for (int i = tid; i < 9 * 16; i += 512) {
-        int pos = i % 9, g = i / 9;
-        int y = pos / 3, x = pos % 3;
-        float acc[8];
-#pragma unroll
-        for (int k = 0; k < 8; k++) acc[k] = wc.c4b[g * 8 + k];
-        for (int c = 0; c < 64; c++) {
-#pragma unroll
-            for (int ky = 0; ky < 2; ky++)
-#pragma unroll
-                for (int kx = 0; kx < 2; kx++) {
-                    float v = sX[4096 + c * 16 + (y + ky) * 4 + x + kx];
-                    const VTF_CONST float* wp = wc.c4w + ((c * 2 + ky) * 2 + kx) * 128 + g * 8;
-#pragma unroll
-                    for (int k = 0; k < 8; k++) acc[k] = fmaf(v, wp[k], acc[k]);
-                }
-        }
-#pragma unroll
-        for (int k = 0; k < 8; k++) sX[5120 + x * 384 + y * 128 + g * 8 + k] = prelu(acc[k], wc.p4[g * 8 + k]);
-    }
-    __syncthreads();
-    // dense5 1152->256 + PReLU (weights transposed [k][256])
-    if (tid < 256) {
-        float acc = wc.d5b[tid];
-        for (int k = 0; k < 1152; k++) acc = fmaf(sX[5120 + k], wc.d5w[k * 256 + tid], acc);
-        sX[6272 + tid] = prelu(acc, wc.p5[tid]);
-    }
-    __syncthreads();
-    if (tid < 64) {
-        float part[16];
-#pragma unroll
-        for (int j = 0; j < 16; j++) part[j] = 0.f;
-        for (int k = tid; k < 256; k += 64) {
-            float f = sX[6272 + k];
-            part[0] = fmaf(f, wc.d61w[k], part[0]);
-            part[1] = fmaf(f, wc.d61w[256 + k], part[1]);
-#pragma unroll
-            for (int j = 0; j < 4; j++) part[2 + j] = fmaf(f, wc.d62w[j * 256 + k], part[2 + j]);
-#pragma unroll
-            for (int j = 0; j < 10; j++) part[6 + j] = fmaf(f, wc.d63w[j * 256 + k], part[6 + j]);
-        }
-#pragma unroll
-        for (int j = 0; j < 16; j++)
-            for (int off = 32; off > 0; off >>= 1) part[j] += __shfl_xor(part[j], off);
-        if (tid == 0) {
-            float a0 = part[0] + wc.d61b[0], a1 = part[1] + wc.d61b[1];
-            float mx = fmaxf(a0, a1);
-            float e0 = expf(a0 - mx), e1 = expf(a1 - mx);
-            prob_out[n] = e1 * __fdiv_rn(1.0f, e0 + e1);
-            reg_out[n] = make_float4(part[2] + wc.d62b[0], part[3] + wc.d62b[1], part[4] + wc.d62b[2], part[5] + wc.d62b[3]);
-#pragma unroll
-            for (int j = 0; j < 10; j++) lm_out[n * 10 + j] = part[6 + j] + wc.d63b[j];
-        }
-    }
-}
-
-void launch_onet(const uint8_t* frames, int64_t frame_stride, int64_t row_stride, int H, int W, const float4* boxes,
-                 const int32_t* img, const float* xin, int64_t n, const ONetW& w, float4* reg, float* lm, float* prob,
-                 int32_t* err, hipStream_t st) {
-    if (n <= 0) return;
-    if (xin)
-        k_onet<false><<<(unsigned)n, 512, 0, st>>>(frames, frame_stride, row_stride, H, W, boxes, img, xin, w, reg, lm,
-                                                    prob, err);
-    else
-        k_onet<true><<<(unsigned)n, 512, 0, st>>>(frames, frame_stride, row_stride, H, W, boxes, img, xin, w, reg, lm,
-                                                   prob, err);
+void launch_heads(const float* x, int64_t n, int D, const float* w1, const float* b1, const float* w2,
+                  const float* b2, const float* w3, const float* b3, float* prob, float4* reg, float* lm,
+                  hipStream_t st) {
+    if (n > 0) k_heads<<<(unsigned)n, 64, 0, st>>>(x, n, D, w1, b1, w2, b2, w3, b3, prob, reg, lm);
 }
 
 // ----------------------------------------------------------------------------------- box ops

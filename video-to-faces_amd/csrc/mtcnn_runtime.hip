@@ -8,6 +8,7 @@
 #include <vector>
 
 #include "common.hpp"
+#include "conv.hpp"
 #include "mtcnn.hpp"
 #include "nms.hpp"
 
@@ -34,8 +35,14 @@ struct Mtcnn {
     hipStream_t st = 0;
     float* d_w = nullptr;
     PNetW pw{};
-    RNetW rw{};
-    ONetW ow{};
+    // RNet / ONet as conv-kernel layers (fp32, [Cout_p][KH][KW][Cin_p]) + heads
+    struct CL {
+        int cin, cout, k;
+        const float *w, *b, *a;
+    };
+    std::vector<CL> rl, ol;
+    const float *rh1w, *rh1b, *rh2w, *rh2b;                    // rnet dense5_1 / dense5_2
+    const float *oh1w, *oh1b, *oh2w, *oh2b, *oh3w, *oh3b;      // onet dense6_1 / 6_2 / 6_3
     Arena ar;
     int64_t stats[8] = {0};
     // kernel timing (vtf_mtcnn_profile)
@@ -44,7 +51,9 @@ struct Mtcnn {
     double prof_ms = 0, prof_flops = 0;
     int64_t prof_launches = 0, prof_frames = 0;
 
+    std::vector<void*> allocs;
     ~Mtcnn() {
+        for (void* p : allocs) (void)hipFree(p);
         if (ev0) (void)hipEventDestroy(ev0);
         if (ev1) (void)hipEventDestroy(ev1);
         if (d_w) (void)hipFree(d_w);
@@ -54,7 +63,7 @@ struct Mtcnn {
 enum Slot {
     S_FRAMES = 0, S_LEVELS, S_COUNT, S_KEY, S_SCORE, S_REGV, S_KEY2, S_SLOT, S_SLOT2, S_B1, S_S1, S_R1, S_I1, S_C1,
     S_KEEP, S_B2, S_S2, S_R2, S_I2, S_C2, S_PROB, S_REG, S_LM, S_ERR, S_FLAG, S_INCL, S_IDX, S_LMK, S_OUTB, S_OUTS,
-    S_OUTL, S_OUTI, S_SORT, S_SCAN, S_PRE
+    S_OUTL, S_OUTI, S_SORT, S_SCAN, S_PRE, S_CROP
 };
 
 // ---- weights: reference state_dict order (specs.py mtcnn_spec) -> transposed device layout
@@ -110,13 +119,120 @@ static void build_weights(Mtcnn& m, const float* params, int64_t n_params) {
     VTF_CHECK(src == n_params, VTF_E_ARG, "mtcnn: expected 495850 parameters");
     VTF_HIP(hipMalloc(&m.d_w, host.size() * 4));
     VTF_HIP(hipMemcpy(m.d_w, host.data(), host.size() * 4, hipMemcpyHostToDevice));
-    const float* b = m.d_w;
-    int i = 0;
-    auto nx = [&]() { return b + off[i++]; };
-    m.pw = PNetW{nx(), nx(), nx(), nx(), nx(), nx(), nx(), nx(), nx(), nx(), nx(), nx(), nx()};
-    m.rw = RNetW{nx(), nx(), nx(), nx(), nx(), nx(), nx(), nx(), nx(), nx(), nx(), nx(), nx(), nx(), nx(), nx()};
-    m.ow = ONetW{nx(), nx(), nx(), nx(), nx(), nx(), nx(), nx(), nx(), nx(), nx(),
-                 nx(), nx(), nx(), nx(), nx(), nx(), nx(), nx(), nx(), nx()};
+    {
+        const float* b = m.d_w;
+        int i = 0;
+        auto nx = [&]() { return b + off[i++]; };
+        m.pw = PNetW{nx(), nx(), nx(), nx(), nx(), nx(), nx(), nx(), nx(), nx(), nx(), nx(), nx()};
+    }
+    // raw (reference layout) tensors by spec index
+    std::vector<const float*> raw(NP);
+    {
+        int64_t o = 0;
+        for (int i = 0; i < NP; i++) {
+            const P& p = spec[i];
+            raw[i] = params + o;
+            o += (p.kind == 0) ? p.co : (p.kind == 1 ? (int64_t)p.co * p.ci * p.kh * p.kw : (int64_t)p.co * p.ci);
+        }
+    }
+    // conv-kernel layers: weights [Cout_p][kh][kw][Cin_p], zero padded; bias, prelu padded.
+    // flat=true: a dense layer over a [3,3,C] map whose reference flatten order is
+    // permute(0,3,2,1) -> (w, h, c) (mtcnn.py:68,113); the conv kernel's k order is (h, w, c).
+    auto layer = [&](int wi, int cin, int cin_p, int cout, int k, bool flat) {
+        int cout_p = (cout + 7) / 8 * 8;
+        std::vector<float> w((size_t)cout_p * k * k * cin_p, 0.f), b(cout_p, 0.f), a(cout_p, 0.f);
+        const float* W = raw[wi];
+        for (int co = 0; co < cout; co++)
+            for (int y = 0; y < k; y++)
+                for (int x = 0; x < k; x++)
+                    for (int ci = 0; ci < cin; ci++) {
+                        float v = flat ? W[(size_t)co * (k * k * cin) + (x * k + y) * cin + ci]
+                                       : W[(((size_t)co * cin + ci) * k + y) * k + x];
+                        w[(((size_t)co * k + y) * k + x) * cin_p + ci] = v;
+                    }
+        for (int co = 0; co < cout; co++) {
+            b[co] = raw[wi + 1][co];
+            a[co] = raw[wi + 2][co];
+        }
+        Mtcnn::CL L{cin_p, cout_p, k, nullptr, nullptr, nullptr};
+        float* d = nullptr;
+        VTF_HIP(hipMalloc(&d, (w.size() + b.size() + a.size()) * 4));
+        VTF_HIP(hipMemcpy(d, w.data(), w.size() * 4, hipMemcpyHostToDevice));
+        VTF_HIP(hipMemcpy(d + w.size(), b.data(), b.size() * 4, hipMemcpyHostToDevice));
+        VTF_HIP(hipMemcpy(d + w.size() + b.size(), a.data(), a.size() * 4, hipMemcpyHostToDevice));
+        m.allocs.push_back(d);
+        L.w = d;
+        L.b = d + w.size();
+        L.a = d + w.size() + b.size();
+        return L;
+    };
+    // spec indices: rnet.conv1.w = 13 ... (see the table above)
+    m.rl = {layer(13, 3, 8, 28, 3, false), layer(16, 28, 32, 48, 3, false), layer(19, 48, 48, 64, 2, false),
+            layer(22, 64, 64, 128, 3, true)};
+    m.ol = {layer(29, 3, 8, 32, 3, false),  layer(32, 32, 32, 64, 3, false), layer(35, 64, 64, 64, 3, false),
+            layer(38, 64, 64, 128, 2, false), layer(41, 128, 128, 256, 3, true)};
+    auto dev = [&](int i) { return m.d_w + off[i]; };
+    m.rh1w = dev(25); m.rh1b = dev(26); m.rh2w = dev(27); m.rh2b = dev(28);
+    m.oh1w = dev(44); m.oh1b = dev(45); m.oh2w = dev(46); m.oh2b = dev(47); m.oh3w = dev(48); m.oh3b = dev(49);
+}
+
+// RNet / ONet on NHWC fp32 crops x0 [n,S,S,8] (mtcnn.py:58-76 / 101-121), layer by layer on
+// the MFMA conv kernel; pools are torch MaxPool2d(ceil_mode=True).
+enum RSlot { S_RA = 70, S_RB = 71 };  // nms_multi owns slots 40-61
+static void run_candidates(Mtcnn& m, bool onet, const float* x0, int64_t n, float4* reg, float* lm, float* prob) {
+    if (n <= 0) return;
+    const int S = onet ? 48 : 24;
+    const auto& Ls = onet ? m.ol : m.rl;
+    // pools after each conv except the last two of RNet / last two of ONet
+    const int pk[5] = {3, 3, onet ? 2 : 0, 0, 0};
+    const int npool = onet ? 3 : 2;
+    size_t big = (size_t)n * (S - 2) * (S - 2) * 32;
+    float* X = m.ar.get<float>(S_RA, big);
+    float* Y = m.ar.get<float>(S_RB, big);
+    const float* cur = x0;
+    int H = S, W = S, C = 8;
+    for (size_t li = 0; li < Ls.size(); li++) {
+        const auto& L = Ls[li];
+        float* out = (cur == X) ? Y : X;
+        ConvParams p{};
+        p.in = cur;
+        p.w = L.w;
+        p.out = out;
+        p.bias = L.b;
+        p.prelu = L.a;
+        p.scale = 1.f;
+        p.N = (int)n;
+        p.H = H;
+        p.W = W;
+        p.Cin = C;
+        p.KH = p.KW = L.k;
+        p.sh = p.sw = 1;
+        p.OH = H - L.k + 1;
+        p.OW = W - L.k + 1;
+        p.Cout = L.cout;
+        p.K = L.k * L.k * C;
+        p.M = (int64_t)n * p.OH * p.OW;
+        p.out_cstride = L.cout;
+        VTF_CHECK(C == L.cin, VTF_E_ARG, "candidate net channel mismatch");
+        launch_conv(p, false, m.st);
+        H = p.OH;
+        W = p.OW;
+        C = L.cout;
+        cur = out;
+        if ((int)li < npool) {
+            float* pout = (out == X) ? Y : X;
+            int OH, OW;
+            launch_maxpool_ks(out, (int)n, H, W, C, pk[li], 2, true, pout, OH, OW, m.st);
+            H = OH;
+            W = OW;
+            cur = pout;
+        }
+    }
+    VTF_CHECK(H == 1 && W == 1, VTF_E_ARG, "candidate net shape walk mismatch");
+    if (onet)
+        launch_heads(cur, n, C, m.oh1w, m.oh1b, m.oh2w, m.oh2b, m.oh3w, m.oh3b, prob, reg, lm, m.st);
+    else
+        launch_heads(cur, n, C, m.rh1w, m.rh1b, m.rh2w, m.rh2b, nullptr, nullptr, prob, reg, nullptr, m.st);
 }
 
 // MTCNN._scale_pyramid (mtcnn.py:141-148): Python double math, int() truncation
@@ -294,7 +410,11 @@ static void detect(Mtcnn& m, const uint8_t* frames, int on_dev, int B, int H, in
     float4* reg = m.ar.get<float4>(S_REG, k2);
     int32_t* err = m.ar.get<int32_t>(S_ERR, 1);
     VTF_HIP(hipMemsetAsync(err, 0, 4, st));
-    launch_rnet(fr, fstride, rstride, H, W, b1, i1, nullptr, k2, m.rw, reg, prob, err, st);
+    {
+        float* x0 = m.ar.get<float>(S_CROP, (size_t)k2 * 24 * 24 * 8);
+        launch_crop_nhwc(fr, fstride, rstride, H, W, b1, i1, k2, 24, x0, err, st);
+        run_candidates(m, false, x0, k2, reg, nullptr, prob);
+    }
     int32_t nerr = 0;
     d2h_sync(&nerr, err, 4, st);
     VTF_CHECK(nerr == 0, VTF_E_DEGENERATE,
@@ -315,7 +435,11 @@ static void detect(Mtcnn& m, const uint8_t* frames, int on_dev, int B, int H, in
     reg = m.ar.get<float4>(S_REG, k3);
     float* lm = m.ar.get<float>(S_LM, k3 * 10);
     VTF_HIP(hipMemsetAsync(err, 0, 4, st));
-    launch_onet(fr, fstride, rstride, H, W, b1, i1, nullptr, k3, m.ow, reg, lm, prob, err, st);
+    {
+        float* x0 = m.ar.get<float>(S_CROP, (size_t)k3 * 48 * 48 * 8);
+        launch_crop_nhwc(fr, fstride, rstride, H, W, b1, i1, k3, 48, x0, err, st);
+        run_candidates(m, true, x0, k3, reg, lm, prob);
+    }
     d2h_sync(&nerr, err, 4, st);
     VTF_CHECK(nerr == 0, VTF_E_DEGENERATE,
               "stage 3: a candidate box lies outside the frame; the reference skips it in "
@@ -507,8 +631,9 @@ int vtf_mtcnn_resample(vtf_mtcnn_t h, const uint8_t* d_frames, int B, int H, int
 int vtf_mtcnn_rnet(vtf_mtcnn_t h, const float* d_in, int64_t n, float* d_reg, float* d_prob) {
     return guarded([&] {
         VTF_CHECK(h && d_in && d_reg && d_prob, VTF_E_ARG, "null argument");
-        launch_rnet(nullptr, 0, 0, 0, 0, nullptr, nullptr, d_in, n, h->m.rw, (float4*)d_reg, d_prob, nullptr,
-                    h->m.st);
+        float* x0 = h->m.ar.get<float>(S_CROP, (size_t)n * 24 * 24 * 8);
+        launch_nchw_to_nhwc(d_in, (int)n, 3, 24, 24, 8, x0, false, h->m.st);
+        run_candidates(h->m, false, x0, n, (float4*)d_reg, nullptr, d_prob);
         VTF_HIP(hipStreamSynchronize(h->m.st));
     });
 }
@@ -516,8 +641,9 @@ int vtf_mtcnn_rnet(vtf_mtcnn_t h, const float* d_in, int64_t n, float* d_reg, fl
 int vtf_mtcnn_onet(vtf_mtcnn_t h, const float* d_in, int64_t n, float* d_reg, float* d_lm, float* d_prob) {
     return guarded([&] {
         VTF_CHECK(h && d_in && d_reg && d_lm && d_prob, VTF_E_ARG, "null argument");
-        launch_onet(nullptr, 0, 0, 0, 0, nullptr, nullptr, d_in, n, h->m.ow, (float4*)d_reg, d_lm, d_prob, nullptr,
-                    h->m.st);
+        float* x0 = h->m.ar.get<float>(S_CROP, (size_t)n * 48 * 48 * 8);
+        launch_nchw_to_nhwc(d_in, (int)n, 3, 48, 48, 8, x0, false, h->m.st);
+        run_candidates(h->m, true, x0, n, (float4*)d_reg, d_lm, d_prob);
         VTF_HIP(hipStreamSynchronize(h->m.st));
     });
 }
