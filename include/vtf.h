@@ -31,6 +31,7 @@ int vtf_version(void);
 
 typedef struct vtf_mtcnn_s* vtf_mtcnn_t;
 typedef struct vtf_facenet_s* vtf_facenet_t;
+typedef struct vtf_vit_s* vtf_vit_t;
 
 /* ---------------------------------------------------------------- MTCNN detector
  * Replaces RealMTCNN / MTCNN.forward (src/videotofaces/detectors/mtcnn.py:167-252,
@@ -105,6 +106,20 @@ int vtf_facenet_encode_crops(vtf_facenet_t h, const uint8_t* d_frames, int H, in
 int vtf_blob_from_crops(const uint8_t* d_frames, int H, int W, int64_t frame_stride, int64_t row_stride,
                         const int32_t* d_crops, int64_t N, int S, float mean, float scale, float* d_out,
                         void* hip_stream);
+
+/* ---------------------------------------------------------------- ViT encoder
+ * Replaces ViT / AnimeVIT (src/videotofaces/encoders/vit.py:80-146), called by grouping.py:37.
+ * dim 768 / depth 12 (B16) or 1024 / 24 (L16); params in the reference state_dict order
+ * (specs.py vit_spec).  fp32. */
+int vtf_vit_create(const float* params, int64_t n_params, int dim, int depth, int device, vtf_vit_t* out);
+int vtf_vit_destroy(vtf_vit_t h);
+int vtf_vit_set_stream(vtf_vit_t h, void* hip_stream);
+/* d_x [N,3,128,128] fp32 blob (blobFromImages(1/127.5, 128x128, 127.5, swapRB)) -> d_emb [N,dim]
+ * (LayerNorm of the CLS token, not L2-normalised). */
+int vtf_vit_forward(vtf_vit_t h, const float* d_x, int64_t N, float* d_emb);
+/* crops as in vtf_facenet_encode_crops, resized to 128x128 (vit.py:141). */
+int vtf_vit_encode_crops(vtf_vit_t h, const uint8_t* d_frames, int H, int W, int64_t frame_stride,
+                         int64_t row_stride, const int32_t* crops, int64_t N, float* d_emb);
 
 /* ---------------------------------------------------------------- grouping
  * remove_dupes_overall 'enc' branch (dupes.py:51-68 with sklearn cosine_distances):

@@ -167,6 +167,22 @@ def gen_facenet():
     print('facenet', y.shape, float(y.norm(dim=1).mean()))
 
 
+def gen_vit():
+    load_ref()
+    v = importlib.import_module('ref_vtf.encoders.vit')
+    g = torch.Generator().manual_seed(13)
+    out = {}
+    u8 = torch.randint(0, 256, (2, 3, 128, 128), generator=g)
+    x = (u8.float() - 127.5) * np.float32(1 / 127.5)  # blobFromImages(1/127.5, 128x128, 127.5)
+    out['u8'] = u8.to(torch.uint8).numpy()
+    for name, dim, depth in (('vit_b', 768, 12), ('vit_l', 1024, 24)):
+        net = _load(v.ViT('cpu', 128, 16, dim, depth), synth.make_params(name))
+        with torch.inference_mode():
+            out[name] = net(x if name == 'vit_b' else x[:1]).numpy()
+        print(name, out[name].shape, float(np.abs(out[name]).mean()))
+    np.savez_compressed(os.path.join(HERE, 'vit.npz'), **out)
+
+
 def gen_grouping():
     load_ref()
     dupes = importlib.import_module('ref_vtf.dupes')
@@ -217,6 +233,6 @@ def gen_grouping():
 
 
 if __name__ == '__main__':
-    which = sys.argv[1:] or ['mtcnn', 'facenet', 'grouping']
+    which = sys.argv[1:] or ['mtcnn', 'facenet', 'vit', 'grouping']
     for w in which:
         globals()['gen_' + w]()

@@ -111,3 +111,12 @@ def test_oracle_grouping_vs_golden():
     np.testing.assert_array_equal(mins, gg['dedupe_mins'])
     np.testing.assert_array_equal(inds, gg['dedupe_inds'])
     np.testing.assert_array_equal(np.nonzero(~(mins <= 0.25))[0], gg['dedupe_keep'])
+
+
+def test_oracle_vit_vs_golden():
+    from videotofaces import synth
+    from oracle.vit import vit
+    gv = np.load(os.path.join(GOLDEN, 'vit.npz'))
+    x = (torch.from_numpy(gv['u8']).float() - 127.5) * np.float32(1 / 127.5)
+    y = vit(synth.make_params('vit_b'), x, 768, 12).numpy()
+    np.testing.assert_allclose(y, gv['vit_b'], atol=1e-5, rtol=0)

@@ -205,6 +205,7 @@ __global__ __launch_bounds__(256) void k_conv(ConvParams p) {
                 if (res) v = v + to_f(res[m * p.res_cstride + c]);
                 if (p.relu) v = fmaxf(v, 0.f);
                 if (p.prelu) v = v > 0.f ? v : p.prelu[c] * v;
+                if (p.gelu) v = 0.5f * v * (1.0f + erff(v * 0.70710678118654752f));
                 out[m * p.out_cstride + p.out_coff + c] = from_f<T>(v);
             }
         }
@@ -270,28 +271,35 @@ void launch_maxpool(const void* in, int N, int H, int W, int C, void* out, int o
 }
 
 // ---------------------------------------------------------------- maxpool k/s with ceil_mode (NHWC fp32)
+// one thread per (output pixel, 4 channels): 16-B loads/stores along C (C % 4 == 0)
 __global__ void k_maxpool_ks(const float* __restrict__ in, int N, int H, int W, int C, int k, int s, int OH, int OW,
                              float* __restrict__ out) {
     int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    int64_t tot = (int64_t)N * OH * OW * C;
+    const int C4 = C >> 2;
+    int64_t tot = (int64_t)N * OH * OW * C4;
     if (i >= tot) return;
-    int c = (int)(i % C);
-    int64_t t = i / C;
+    int c4 = (int)(i % C4);
+    int64_t t = i / C4;
     int ow = (int)(t % OW);
     t /= OW;
     int oh = (int)(t % OH);
     int n = (int)(t / OH);
-    float m = -3.402823466e38f;
+    f32x4 m = {-3.402823466e38f, -3.402823466e38f, -3.402823466e38f, -3.402823466e38f};
+    const f32x4* src = (const f32x4*)in + (int64_t)n * H * W * C4 + c4;
     for (int dy = 0; dy < k; dy++) {
         int y = oh * s + dy;
         if (y >= H) break;
         for (int dx = 0; dx < k; dx++) {
             int x = ow * s + dx;
             if (x >= W) break;
-            m = fmaxf(m, in[(((int64_t)n * H + y) * W + x) * C + c]);
+            f32x4 v = src[((int64_t)y * W + x) * C4];
+            m.x = fmaxf(m.x, v.x);
+            m.y = fmaxf(m.y, v.y);
+            m.z = fmaxf(m.z, v.z);
+            m.w = fmaxf(m.w, v.w);
         }
     }
-    out[i] = m;
+    ((f32x4*)out)[i] = m;
 }
 
 static int pool_out(int L, int k, int s, bool ceil_mode) {
@@ -305,7 +313,8 @@ void launch_maxpool_ks(const float* in, int N, int H, int W, int C, int k, int s
                        int& OH, int& OW, hipStream_t st) {
     OH = pool_out(H, k, s, ceil_mode);
     OW = pool_out(W, k, s, ceil_mode);
-    int64_t tot = (int64_t)N * OH * OW * C;
+    VTF_CHECK(C % 4 == 0, VTF_E_ARG, "maxpool: C must be a multiple of 4");
+    int64_t tot = (int64_t)N * OH * OW * (C / 4);
     if (tot > 0) k_maxpool_ks<<<cdiv(tot, 256), 256, 0, st>>>(in, N, H, W, C, k, s, OH, OW, out);
 }
 

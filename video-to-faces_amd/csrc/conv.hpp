@@ -14,6 +14,7 @@ struct ConvParams {
     const float* prelu;  // per-channel PReLU slope (or null), applied last
     float scale;
     int relu;
+    int gelu;            // exact erf GELU (ViT MLP, vit.py:37)
     int64_t M;           // N*OH*OW
     int N, H, W, Cin, OH, OW, Cout, KH, KW, sh, sw, ph, pw, K;
     int out_cstride, out_coff, res_cstride;

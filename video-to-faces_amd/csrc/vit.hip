@@ -1,0 +1,329 @@
+// ViT-B/16 and ViT-L/16 encoders on gfx950 (fp32 parity mode).
+//
+// Replaces ViT / AnimeVIT (src/videotofaces/encoders/vit.py:9-146):
+//   patch conv 16x16/16 -> [N,64,D]; CLS + pos -> [N,65,D]; depth x pre-LN blocks
+//   (LN eps 1e-12 -> fused q|k|v GEMM -> 65-token softmax(q k^T / 8) v per head -> proj +
+//   residual -> LN -> fc1 + exact GELU -> fc2 + residual); LN of the CLS row -> [N,D].
+// Every GEMM (patch embed as a 16x16 stride-16 conv, q|k|v, proj, fc1, fc2) is the MFMA
+// implicit-GEMM kernel (conv.hip) as a 1x1 conv over M = N*65 token rows, with bias /
+// residual / GELU fused in the epilogue.  Attention: one workgroup per (image, head) keeps
+// Q, K, V (65 x 64 each) and the 65 x 65 scores in LDS; row softmax by wave reductions.
+#include <cmath>
+#include <vector>
+
+#include "common.hpp"
+#include "conv.hpp"
+
+namespace vtf {
+
+constexpr int VT = 65;   // tokens: 64 patches + CLS (img 128, patch 16)
+constexpr int VHD = 64;  // head dim (dim // 64 heads)
+
+// x [N,65,D]: row 0 = cls + pos[0], row 1+p = patch[p] + pos[1+p]  (vit.py:96-99)
+__global__ void k_vit_tokens(const float* __restrict__ patches, const float* __restrict__ cls,
+                             const float* __restrict__ pos, int64_t N, int D, float* __restrict__ x) {
+    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= N * VT * D) return;
+    int d = (int)(i % D);
+    int t = (int)((i / D) % VT);
+    int64_t n = i / ((int64_t)VT * D);
+    float v = t == 0 ? cls[d] : patches[(n * 64 + (t - 1)) * D + d];
+    x[i] = v + pos[t * D + d];
+}
+
+// LayerNorm over the last dim (eps), rows of length D with row stride `ld`; one workgroup per row.
+__global__ __launch_bounds__(256) void k_layernorm(const float* __restrict__ x, int64_t rows, int D, int64_t ld,
+                                                   const float* __restrict__ g, const float* __restrict__ b, float eps,
+                                                   float* __restrict__ y, int64_t ldy) {
+    const int64_t r = blockIdx.x;
+    const float* xr = x + r * ld;
+    __shared__ float red[8];
+    float s = 0.f;
+    for (int d = threadIdx.x; d < D; d += 256) s += xr[d];
+    for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+    __syncthreads();
+    const float mean = (red[0] + red[1] + red[2] + red[3]) / (float)D;
+    __syncthreads();
+    float q = 0.f;
+    for (int d = threadIdx.x; d < D; d += 256) {
+        float t = xr[d] - mean;
+        q = fmaf(t, t, q);
+    }
+    for (int off = 32; off > 0; off >>= 1) q += __shfl_xor(q, off);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = q;
+    __syncthreads();
+    const float var = (red[0] + red[1] + red[2] + red[3]) / (float)D;
+    const float rstd = 1.0f / sqrtf(var + eps);
+    float* yr = y + r * ldy;
+    for (int d = threadIdx.x; d < D; d += 256) yr[d] = fmaf((xr[d] - mean) * rstd, g[d], b[d]);
+}
+
+// qkv [N,65,3D] (q | k | v, head-major inside each) -> out [N,65,D]; one workgroup per (n, head)
+__global__ __launch_bounds__(256) void k_vit_attention(const float* __restrict__ qkv, int64_t N, int D, int heads,
+                                                       float* __restrict__ out) {
+    __shared__ float Q[VT * (VHD + 1)], K[VT * (VHD + 1)], V[VT * VHD], S[VT * 68];
+    const int64_t n = blockIdx.x / heads;
+    const int h = blockIdx.x % heads;
+    const int tid = threadIdx.x;
+    const float* base = qkv + n * VT * 3 * D + h * VHD;
+    for (int i = tid; i < VT * VHD; i += 256) {
+        int t = i / VHD, d = i % VHD;
+        const float* row = base + (int64_t)t * 3 * D + d;
+        Q[t * (VHD + 1) + d] = row[0];
+        K[t * (VHD + 1) + d] = row[D];
+        V[t * VHD + d] = row[2 * D];
+    }
+    __syncthreads();
+    // scores = q k^T / sqrt(64)  (vit.py:24; division by 8 is exact as * 0.125)
+    for (int i = tid; i < VT * VT; i += 256) {
+        int a = i / VT, c = i % VT;
+        float s = 0.f;
+#pragma unroll 16
+        for (int d = 0; d < VHD; d++) s = fmaf(Q[a * (VHD + 1) + d], K[c * (VHD + 1) + d], s);
+        S[a * 68 + c] = s * 0.125f;
+    }
+    __syncthreads();
+    // row softmax: one wave per row (65 entries -> lanes 0..63 + lane 0 takes the 65th)
+    const int lane = tid & 63, wave = tid >> 6;
+    for (int a = wave; a < VT; a += 4) {
+        float v0 = S[a * 68 + lane];
+        float v1 = lane == 0 ? S[a * 68 + 64] : -INFINITY;
+        float m = fmaxf(v0, v1);
+        for (int off = 32; off > 0; off >>= 1) m = fmaxf(m, __shfl_xor(m, off));
+        float e0 = expf(v0 - m), e1 = lane == 0 ? expf(v1 - m) : 0.f;
+        float s = e0 + e1;
+        for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off);
+        float inv = 1.0f / s;
+        S[a * 68 + lane] = e0 * inv;
+        if (lane == 0) S[a * 68 + 64] = e1 * inv;
+    }
+    __syncthreads();
+    // out = scores @ v, written back head-major: [N,65,D] feature h*64 + d
+    float* ob = out + n * VT * D + h * VHD;
+    for (int i = tid; i < VT * VHD; i += 256) {
+        int a = i / VHD, d = i % VHD;
+        float s = 0.f;
+#pragma unroll 13
+        for (int c = 0; c < VT; c++) s = fmaf(S[a * 68 + c], V[c * VHD + d], s);
+        ob[(int64_t)a * D + d] = s;
+    }
+}
+
+struct Lin {
+    const float *w, *b;  // [out][in], [out]
+    int in, out;
+};
+
+struct Vit {
+    int device = 0, D = 768, depth = 12, heads = 12;
+    hipStream_t st = 0;
+    const float *cls = nullptr, *pos = nullptr, *pw = nullptr, *pb = nullptr;  // patch conv [D][16][16][8]
+    struct Block {
+        const float *n1w, *n1b, *n2w, *n2b;
+        Lin qkv, proj, fc1, fc2;
+    };
+    std::vector<Block> blocks;
+    const float *nw = nullptr, *nb = nullptr;
+    std::vector<void*> allocs;
+    Arena ar;
+    ~Vit() {
+        for (void* p : allocs) (void)hipFree(p);
+    }
+    const float* up(const std::vector<float>& v) {
+        void* p = nullptr;
+        VTF_HIP(hipMalloc(&p, v.size() * 4 + 16));
+        VTF_HIP(hipMemcpy(p, v.data(), v.size() * 4, hipMemcpyHostToDevice));
+        allocs.push_back(p);
+        return (const float*)p;
+    }
+};
+
+static void vit_build(Vit& V, const float* params, int64_t n_params) {
+    const int D = V.D;
+    int64_t src = 0;
+    auto take = [&](int64_t n) {
+        VTF_CHECK(src + n <= n_params, VTF_E_ARG, "vit: parameter buffer too small");
+        std::vector<float> v(params + src, params + src + n);
+        src += n;
+        return v;
+    };
+    V.cls = V.up(take(D));
+    V.pos = V.up(take((int64_t)VT * D));
+    {
+        std::vector<float> w = take((int64_t)D * 3 * 256), wt((size_t)D * 256 * 8, 0.f);
+        for (int o = 0; o < D; o++)
+            for (int c = 0; c < 3; c++)
+                for (int y = 0; y < 16; y++)
+                    for (int x = 0; x < 16; x++)
+                        wt[(((size_t)o * 16 + y) * 16 + x) * 8 + c] = w[(((size_t)o * 3 + c) * 16 + y) * 16 + x];
+        V.pw = V.up(wt);
+        V.pb = V.up(take(D));
+    }
+    for (int l = 0; l < V.depth; l++) {
+        Vit::Block B{};
+        B.n1w = V.up(take(D));
+        B.n1b = V.up(take(D));
+        std::vector<float> qw = take((int64_t)D * D), qb = take(D), kw = take((int64_t)D * D), kb = take(D),
+                           vw = take((int64_t)D * D), vb = take(D);
+        std::vector<float> w(qw);
+        w.insert(w.end(), kw.begin(), kw.end());
+        w.insert(w.end(), vw.begin(), vw.end());
+        std::vector<float> b(qb);
+        b.insert(b.end(), kb.begin(), kb.end());
+        b.insert(b.end(), vb.begin(), vb.end());
+        B.qkv = Lin{V.up(w), V.up(b), D, 3 * D};
+        { auto pw = take((int64_t)D * D); auto pb = take(D); B.proj = Lin{V.up(pw), V.up(pb), D, D}; }
+        B.n2w = V.up(take(D));
+        B.n2b = V.up(take(D));
+        { auto w1 = take((int64_t)4 * D * D); auto b1 = take(4 * D); B.fc1 = Lin{V.up(w1), V.up(b1), D, 4 * D}; }
+        { auto w2 = take((int64_t)4 * D * D); auto b2 = take(D); B.fc2 = Lin{V.up(w2), V.up(b2), 4 * D, D}; }
+        V.blocks.push_back(B);
+    }
+    V.nw = V.up(take(D));
+    V.nb = V.up(take(D));
+    VTF_CHECK(src == n_params, VTF_E_ARG, "vit: parameter count mismatch");
+}
+
+// y[M,out] = x[M,in] W^T + b (+ res) (+ GELU): a 1x1 conv over M rows on the MFMA kernel
+static void linear(Vit& V, const Lin& L, const float* x, int64_t M, float* y, const float* res, bool gelu) {
+    ConvParams p{};
+    p.in = x;
+    p.w = L.w;
+    p.out = y;
+    p.bias = L.b;
+    p.res = res;
+    p.res_cstride = L.out;
+    p.scale = 1.f;
+    p.gelu = gelu;
+    p.N = (int)M;
+    p.H = p.W = p.OH = p.OW = 1;
+    p.Cin = L.in;
+    p.KH = p.KW = 1;
+    p.sh = p.sw = 1;
+    p.Cout = L.out;
+    p.K = L.in;
+    p.M = M;
+    p.out_cstride = L.out;
+    launch_conv(p, false, V.st);
+}
+
+static void vit_forward(Vit& V, const float* x_nhwc8, int64_t N, float* emb) {
+    const int D = V.D;
+    const int64_t M = N * VT;
+    float* patches = V.ar.get<float>(0, N * 64 * D);
+    float* X = V.ar.get<float>(1, M * D);
+    float* Hn = V.ar.get<float>(2, M * D);
+    float* QKV = V.ar.get<float>(3, M * 3 * D);
+    float* A = V.ar.get<float>(4, M * D);
+    float* F = V.ar.get<float>(5, M * 4 * D);
+    // patch embedding: Conv2d(3, D, 16, stride 16) (vit.py:88,94)
+    ConvParams p{};
+    p.in = x_nhwc8;
+    p.w = V.pw;
+    p.out = patches;
+    p.bias = V.pb;
+    p.scale = 1.f;
+    p.N = (int)N;
+    p.H = p.W = 128;
+    p.Cin = 8;
+    p.KH = p.KW = 16;
+    p.sh = p.sw = 16;
+    p.OH = p.OW = 8;
+    p.Cout = D;
+    p.K = 16 * 16 * 8;
+    p.M = N * 64;
+    p.out_cstride = D;
+    launch_conv(p, false, V.st);
+    k_vit_tokens<<<cdiv(M * D, 256), 256, 0, V.st>>>(patches, V.cls, V.pos, N, D, X);
+    for (const auto& B : V.blocks) {
+        k_layernorm<<<(unsigned)M, 256, 0, V.st>>>(X, M, D, D, B.n1w, B.n1b, 1e-12f, Hn, D);
+        linear(V, B.qkv, Hn, M, QKV, nullptr, false);
+        k_vit_attention<<<(unsigned)(N * V.heads), 256, 0, V.st>>>(QKV, N, D, V.heads, A);
+        linear(V, B.proj, A, M, Hn, X, false);  // x + proj(attn)
+        std::swap(X, Hn);
+        k_layernorm<<<(unsigned)M, 256, 0, V.st>>>(X, M, D, D, B.n2w, B.n2b, 1e-12f, A, D);
+        linear(V, B.fc1, A, M, F, nullptr, true);
+        linear(V, B.fc2, F, M, Hn, X, false);   // x + fc2(gelu(fc1(...)))
+        std::swap(X, Hn);
+    }
+    // LayerNorm of the CLS rows (vit.py:100-101)
+    k_layernorm<<<(unsigned)N, 256, 0, V.st>>>(X, N, D, (int64_t)VT * D, V.nw, V.nb, 1e-12f, emb, D);
+}
+
+}  // namespace vtf
+
+// blob / layout helpers from other units
+namespace vtf {
+void launch_blob(const uint8_t* frames, int H, int W, int64_t fstride, int64_t rstride, const int32_t* d_crops,
+                 int64_t N, int S, float mean, float scale, int layout, int Cp, bool bf16, void* out, hipStream_t st);
+}
+
+using namespace vtf;
+
+struct vtf_vit_s {
+    Vit v;
+};
+
+extern "C" {
+
+int vtf_vit_create(const float* params, int64_t n_params, int dim, int depth, int device, vtf_vit_t* out) {
+    return guarded([&] {
+        VTF_CHECK(params && out && dim % 64 == 0 && depth > 0, VTF_E_ARG, "bad argument");
+        VTF_HIP(hipSetDevice(device));
+        auto* h = new vtf_vit_s();
+        h->v.device = device;
+        h->v.D = dim;
+        h->v.depth = depth;
+        h->v.heads = dim / 64;
+        try {
+            vit_build(h->v, params, n_params);
+        } catch (...) {
+            delete h;
+            throw;
+        }
+        *out = h;
+    });
+}
+
+int vtf_vit_destroy(vtf_vit_t h) {
+    return guarded([&] { delete h; });
+}
+
+int vtf_vit_set_stream(vtf_vit_t h, void* stream) {
+    return guarded([&] {
+        VTF_CHECK(h, VTF_E_ARG, "null handle");
+        h->v.st = (hipStream_t)stream;
+    });
+}
+
+int vtf_vit_forward(vtf_vit_t h, const float* d_x, int64_t N, float* d_emb) {
+    return guarded([&] {
+        VTF_CHECK(h && N >= 0, VTF_E_ARG, "bad argument");
+        if (N == 0) return;
+        VTF_CHECK(d_x && d_emb, VTF_E_ARG, "null argument");
+        float* x8 = h->v.ar.get<float>(6, N * 128 * 128 * 8);
+        launch_nchw_to_nhwc(d_x, (int)N, 3, 128, 128, 8, x8, false, h->v.st);
+        vit_forward(h->v, x8, N, d_emb);
+        VTF_HIP(hipGetLastError());
+    });
+}
+
+int vtf_vit_encode_crops(vtf_vit_t h, const uint8_t* d_frames, int H, int W, int64_t frame_stride,
+                         int64_t row_stride, const int32_t* crops, int64_t N, float* d_emb) {
+    return guarded([&] {
+        VTF_CHECK(h && N >= 0, VTF_E_ARG, "bad argument");
+        if (N == 0) return;
+        VTF_CHECK(d_frames && crops && d_emb, VTF_E_ARG, "null argument");
+        int32_t* dc = h->v.ar.get<int32_t>(7, N * 5);
+        VTF_HIP(hipMemcpyAsync(dc, crops, N * 5 * 4, hipMemcpyHostToDevice, h->v.st));
+        float* x8 = h->v.ar.get<float>(6, N * 128 * 128 * 8);
+        // blobFromImages(images, 1/127.5, (128,128), (127.5,)*3, swapRB=True) (vit.py:141)
+        launch_blob(d_frames, H, W, frame_stride, row_stride, dc, N, 128, 127.5f, (float)(1.0 / 127.5), 1, 8, false,
+                    x8, h->v.st);
+        vit_forward(h->v, x8, N, d_emb);
+        VTF_HIP(hipGetLastError());
+    });
+}
+
+}  // extern "C"

@@ -43,6 +43,11 @@ SIGNATURES = {
     'vtf_facenet_set_stream': [_p, _p],
     'vtf_facenet_forward': [_p, _p, _i64, _p],
     'vtf_facenet_encode_crops': [_p, _p, _i32, _i32, _i64, _i64, _p, _i64, _p],
+    'vtf_vit_create': [_p, _i64, _i32, _i32, _i32, _p],
+    'vtf_vit_destroy': [_p],
+    'vtf_vit_set_stream': [_p, _p],
+    'vtf_vit_forward': [_p, _p, _i64, _p],
+    'vtf_vit_encode_crops': [_p, _p, _i32, _i32, _i64, _i64, _p, _i64, _p],
     'vtf_blob_from_crops': [_p, _i32, _i32, _i64, _i64, _p, _i64, _i32, _f32, _f32, _p, _p],
     'vtf_cosine_dedupe': [_p, _i64, _i64, _p, _p, _p],
     'vtf_cosine_classify': [_p, _i64, _p, _i64, _i64, _p, _p, _p],
