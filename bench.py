@@ -5,6 +5,8 @@ det-batch 16, enc-batch 128, frames resident in HBM.  One step = one det-batch p
   MTCNN detect (fp32 parity mode; pyramid + P/R/O-Net + NMS on device)
   -> reference box post-processing (filter_boxes / adjust_boxes, detection.py:174-262, host)
   -> crop + INTER_LINEAR resize + FaceNet on device (bf16 by default; --enc-precision fp32).
+--det-model yolo runs configs[2] instead: YOLOv3 (letterbox + Darknet53 + decode + NMS on
+device, fp32 or --det-precision bf16) + FaceNet, det-batch 32.
 The timed region ends with the RCCL all-gather-v of every rank's embeddings (the exchange
 step before grouping).  value = faces encoded by all ranks / max-over-ranks wall time.
 
@@ -25,6 +27,7 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 FP32_PEAK_TFLOPS = 157.3  # MI355X dense fp32 (vector = f32 MFMA), MI355X_MICROARCH.md
+BF16_PEAK_TFLOPS = 2500.0  # MI355X dense bf16 MFMA (no sparsity), MI355X_MICROARCH.md
 H, W = 720, 1280
 
 
@@ -33,7 +36,9 @@ def parse():
     ap.add_argument('--gpus', type=int, default=1)
     ap.add_argument('--steps', type=int, default=20)
     ap.add_argument('--warmup', type=int, default=3)
-    ap.add_argument('--det-batch', type=int, default=16)
+    ap.add_argument('--det-model', default='mtcnn', choices=['mtcnn', 'yolo'])
+    ap.add_argument('--det-precision', default='fp32', choices=['fp32', 'bf16'], help='YOLO conv precision')
+    ap.add_argument('--det-batch', type=int, default=None, help='default 16 (mtcnn) / 32 (yolo)')
     ap.add_argument('--enc-batch', type=int, default=128)
     ap.add_argument('--enc-precision', default='bf16', choices=['bf16', 'fp32'])
     ap.add_argument('--min-face-size', type=float, default=5.0)
@@ -43,9 +48,15 @@ def parse():
     # box post-processing (detection.py:174-262): reference defaults except det_min_size,
     # because synthetic-weight detections are mostly < 50 px and would never reach the encoder
     ap.add_argument('--det-min-score', type=float, default=0.4)
-    ap.add_argument('--det-min-size', type=int, default=0)
+    ap.add_argument('--det-min-size', type=int, default=None, help='default 0 (mtcnn) / 50 (yolo)')
     ap.add_argument('--det-min-border', type=int, default=5)
-    return ap.parse_args()
+    a = ap.parse_args()
+    yolo = a.det_model == 'yolo'
+    if a.det_batch is None:
+        a.det_batch = 32 if yolo else 16
+    if a.det_min_size is None:
+        a.det_min_size = 50 if yolo else 0
+    return a
 
 
 def det_params(args):
@@ -57,6 +68,7 @@ def cpu_baseline(frames, args):
     """The oracle (CPU restatement of the reference path, torch-CPU + C NMS) on a bounded
     sample of the same workload, rank 0 only."""
     from oracle import mtcnn as om
+    from oracle import yolo as oy
     from oracle.facenet import inception_resnet_v1, resize_linear_u8
     from videotofaces import synth
     from videotofaces.detection import boxes_to_crops
@@ -65,11 +77,15 @@ def cpu_baseline(frames, args):
     if env and env.isdigit():
         cores = min(cores, int(env))
     torch.set_num_threads(cores)
-    pm, pf = synth.make_params('mtcnn'), synth.make_params('facenet')
+    yolo = args.det_model == 'yolo'
+    pm, pf = synth.make_params(args.det_model), synth.make_params('facenet')
     n = min(args.cpu_frames, frames.shape[0])
     sample = frames[:n]
     t0 = time.time()
-    res = om.forward(pm, list(sample), minsize=args.min_face_size)
+    if yolo:
+        res = oy.forward(pm, list(sample))
+    else:
+        res = om.forward(pm, list(sample), minsize=args.min_face_size)
     crops = boxes_to_crops(res, (H, W), **det_params(args))
     faces = 0
     for i in range(0, crops.shape[0], args.enc_batch):
@@ -81,8 +97,8 @@ def cpu_baseline(frames, args):
         faces += len(blobs)
     dt = time.time() - t0
     return {'value': round(faces / dt, 3), 'unit': 'faces/s', 'cores': cores, 'kind': 'port',
-            'sample': '%d synthetic 720p frames (%d faces), oracle MTCNN(min_face_size=%g)+FaceNet fp32 on CPU, %.1f s'
-                      % (n, faces, args.min_face_size, dt)}
+            'sample': '%d synthetic 720p frames (%d faces), oracle %s+FaceNet fp32 on CPU, %.1f s'
+                      % (n, faces, 'YOLOv3' if yolo else 'MTCNN(min_face_size=%g)' % args.min_face_size, dt)}
 
 
 def main():
@@ -96,6 +112,8 @@ def main():
     dev = torch.device('cuda', local)
     from videotofaces import synth
     from videotofaces.detectors.mtcnn import MTCNN
+    from videotofaces.detectors.yolo import YOLOv3
+    from videotofaces.detection import normalize_detout
     from videotofaces.encoders.facenet import InceptionResnetV1
     from videotofaces.detection import boxes_to_crops
 
@@ -103,13 +121,14 @@ def main():
     pool_n = max(B, args.pool // B * B)
     frames_np = synth.make_frames(pool_n, H, W, seed=1000 + rank)
     frames = torch.from_numpy(frames_np).to(dev)
-    det = MTCNN(dev)
+    yolo = args.det_model == 'yolo'
+    det = YOLOv3(dev, precision=args.det_precision) if yolo else MTCNN(dev)
     enc = InceptionResnetV1(dev, precision=args.enc_precision)
 
     def step(i):
         j = (i * B) % pool_n
         fb = frames[j:j + B]
-        res = det(fb, args.min_face_size)
+        res = normalize_detout(det(fb)) if yolo else det(fb, args.min_face_size)
         crops = boxes_to_crops(res, (H, W), **det_params(args))
         embs = [enc.encode_crops(fb, crops[k:k + args.enc_batch]) for k in range(0, crops.shape[0], args.enc_batch)]
         return embs, crops.shape[0], sum(r.shape[0] for r in res)
@@ -139,8 +158,8 @@ def main():
         dist.barrier()
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t0
-    pnet_ms, pnet_launches, pnet_flops, pnet_frames = det.profile(False)
-    tot = torch.tensor([faces, dets, pnet_frames], dtype=torch.float64, device=dev)
+    k_ms, k_launches, k_flops, k_frames = det.profile(False)
+    tot = torch.tensor([faces, dets, k_frames], dtype=torch.float64, device=dev)
     el = torch.tensor([elapsed], dtype=torch.float64, device=dev)
     if world > 1:
         dist.all_reduce(tot, op=dist.ReduceOp.SUM)
@@ -148,13 +167,21 @@ def main():
     faces_all, dets_all, frames_all = [float(x) for x in tot.tolist()]
     elapsed = float(el.item())
     if rank == 0:
-        avg_ms = pnet_ms / max(1, pnet_launches)
-        flops_per_launch = pnet_flops / max(1, pnet_launches)
+        avg_ms = k_ms / max(1, k_launches)
+        flops_per_launch = k_flops / max(1, k_launches)
         achieved = flops_per_launch / (avg_ms / 1e3) / 1e12 if avg_ms > 0 else 0.0
         traffic = None
-        tf = os.path.join(ROOT, 'profiles', 'pnet_traffic.json')
+        tf = os.path.join(ROOT, 'profiles', ('yolo' if yolo else 'pnet') + '_traffic.json')
         if os.path.exists(tf):
             traffic = json.load(open(tf)).get('hbm_bytes_per_launch')
+        if yolo:
+            peak = BF16_PEAK_TFLOPS if args.det_precision == 'bf16' else FP32_PEAK_TFLOPS
+            kname = 'k_conv (YOLOv3 Darknet53+neck+head, 75 implicit-GEMM launches per det-batch, %s)' % args.det_precision
+            wl = 'YOLOv3(%s)+FaceNet' % args.det_precision
+        else:
+            peak = FP32_PEAK_TFLOPS
+            kname = 'k_pnet (fused pyramid resample + PNet, fp32)'
+            wl = 'MTCNN(min_face_size=%g)+FaceNet' % args.min_face_size
         out = {
             'metric': 'faces/sec end-to-end (detect+encode) on 1280x720 synthetic frames',
             'value': round(faces_all / elapsed, 2),
@@ -166,23 +193,23 @@ def main():
             'higher_is_better': True,
             'scaling': 'weak',
             'vs_baseline': None,
-            'dtype': 'fp32 det / %s enc' % args.enc_precision,
+            'dtype': '%s det / %s enc' % (args.det_precision if yolo else 'fp32', args.enc_precision),
             'data': 'synthetic (seeded 720p value-noise frames with face blobs; hash-seeded synthetic weights, '
-                    'MTCNN heads calibrated to ~4 faces/frame)',
-            'config': {'workload': 'MTCNN(min_face_size=%g)+FaceNet, det-batch %d, enc-batch %d, 720p, frames in HBM, '
+                    'detector heads calibrated to a few faces/frame)',
+            'config': {'workload': '%s, det-batch %d, enc-batch %d, 720p, frames in HBM, '
                                    'box filter min_score %g min_size %d min_border %d, det_scale (1.5,1.5,2.2,1.2), square'
-                                   % (args.min_face_size, B, args.enc_batch, args.det_min_score, args.det_min_size,
+                                   % (wl, B, args.enc_batch, args.det_min_score, args.det_min_size,
                                       args.det_min_border),
                        'det_batch': B, 'enc_batch': args.enc_batch, 'frames_per_step_per_gpu': B,
                        'parallelism': 'dp%d (frame-sharded, RCCL all-gather of embeddings)' % world},
             'frames_per_s': round(world * args.steps * B / elapsed, 2),
             'faces_per_frame': round(faces_all / max(1.0, world * args.steps * B), 3),
             'detections_per_frame': round(dets_all / max(1.0, world * args.steps * B), 3),
-            'roofline': {'kernel': 'k_pnet (fused pyramid resample + PNet, fp32)', 'bound': 'mfma',
-                         'achieved': round(achieved, 3), 'peak': FP32_PEAK_TFLOPS, 'unit': 'TFLOP/s',
-                         'frac': round(achieved / FP32_PEAK_TFLOPS, 4), 'traffic': traffic,
+            'roofline': {'kernel': kname, 'bound': 'mfma',
+                         'achieved': round(achieved, 3), 'peak': peak, 'unit': 'TFLOP/s',
+                         'frac': round(achieved / peak, 4), 'traffic': traffic,
                          'avg_launch_ms': round(avg_ms, 4), 'flops_per_launch': flops_per_launch,
-                         'launches': pnet_launches},
+                         'launches': k_launches},
             'cpu_baseline': None,
         }
         if world == 1 and not args.no_cpu_baseline:

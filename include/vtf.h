@@ -32,6 +32,7 @@ int vtf_version(void);
 typedef struct vtf_mtcnn_s* vtf_mtcnn_t;
 typedef struct vtf_facenet_s* vtf_facenet_t;
 typedef struct vtf_vit_s* vtf_vit_t;
+typedef struct vtf_yolo_s* vtf_yolo_t;
 
 /* ---------------------------------------------------------------- MTCNN detector
  * Replaces RealMTCNN / MTCNN.forward (src/videotofaces/detectors/mtcnn.py:167-252,
@@ -129,6 +130,39 @@ int vtf_cosine_dedupe(const float* d_X, int64_t N, int64_t D, float* d_min, int6
 /* classify (grouping.py:50-66): argmin / min over c of cosine distance(X_i, R_c). */
 int vtf_cosine_classify(const float* d_X, int64_t N, const float* d_R, int64_t C, int64_t D, float* d_min,
                         int64_t* d_arg, void* hip_stream);
+
+/* ---------------------------------------------------------------- YOLOv3 detector
+ * Replaces RealYOLO / YOLOv3.forward (src/videotofaces/detectors/yolo.py:131-191), called by
+ * detection.py:131 `detout = model(frames)`.
+ * params: fp32, reference state_dict order minus num_batches_tracked (specs.py yolo_spec,
+ *         61,576,342 floats).  precision 0 = fp32 (parity), 1 = bf16 operands/activations. */
+int vtf_yolo_create(const float* params, int64_t n_params, int device, int precision, vtf_yolo_t* out);
+int vtf_yolo_destroy(vtf_yolo_t h);
+int vtf_yolo_set_stream(vtf_yolo_t h, void* hip_stream);
+/* frames as in vtf_mtcnn_detect.  Output (host): boxes [total,4] (x1,y1,x2,y2 in frame
+ * pixels, unclamped), scores [total], counts[B] (<= 100 each); per image in the reference's
+ * order (score desc).  Classes are all 0 (num_classes=1).  VTF_E_CAPACITY as in mtcnn. */
+int vtf_yolo_detect(vtf_yolo_t h, const uint8_t* frames, int frames_on_device, int B, int H, int W,
+                    int64_t frame_stride, int64_t row_stride, float* out_boxes, float* out_scores,
+                    int32_t* out_counts, int64_t cap, int64_t* out_total);
+/* resize_cv2 keep-ratio size (prep.py:71-73) and the x32 padded net input: {h, w, Hp, Wp}. */
+int vtf_yolo_input_size(int H, int W, int* out4);
+/* Parity entries.  letterbox: preprocess (prep.py:12-92) -> d_out NHWC fp32 [B,Hp,Wp,8]
+ * (channels 3..7 zero).  net: d_x NCHW fp32 [B,3,Hp,Wp] -> pred maps NHWC fp32
+ * [B,Hp/32,Wp/32,18], [B,Hp/16,Wp/16,18], [B,Hp/8,Wp/8,18] (yolo.py:143-145).
+ * postprocess: the maps of frames of size HxW -> detect's outputs (yolo.py:146-147). */
+int vtf_yolo_letterbox(vtf_yolo_t h, const uint8_t* d_frames, int B, int H, int W, int64_t frame_stride,
+                       int64_t row_stride, float* d_out);
+int vtf_yolo_net(vtf_yolo_t h, const float* d_x, int B, int Hp, int Wp, float* d_map0, float* d_map1,
+                 float* d_map2);
+int vtf_yolo_postprocess(vtf_yolo_t h, const float* d_map0, const float* d_map1, const float* d_map2, int B,
+                         int H, int W, float* out_boxes, float* out_scores, int32_t* out_counts, int64_t cap,
+                         int64_t* out_total);
+/* Conv-stack timing (HIP events around the 75 conv launches of each detect/net call):
+ * accumulated ms, launches, algorithmic FLOPs and frames since the last call; enable != 0
+ * turns timing on for the following calls. */
+int vtf_yolo_profile(vtf_yolo_t h, int enable, double* out_ms, int64_t* out_launches, double* out_flops,
+                     int64_t* out_frames);
 
 #ifdef __cplusplus
 }

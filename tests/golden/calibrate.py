@@ -78,5 +78,44 @@ def main(n_frames=2):
     print('MTCNN_CALIB face_bias =', synth.MTCNN_CALIB['face_bias'])
 
 
+
+
+def calibrate_yolo(n_frames=2):
+    """Row gains and obj bias for the YOLO pred convs.  Darknet's residual stacks grow the
+    bridge activations to O(1e3-1e4), so every row is normalised by its measured std:
+    regression/cls rows to std 0.3 (cls bias +3 -> sigmoid ~0.95), and the obj row so that
+    0.5% of priors reach obj >= 0.005 (logit -5.2933, into NMS) and 0.05% reach obj > 0.5
+    (logit 0, survive a 0.4 score filter), pooled over the 3 levels."""
+    from oracle import yolo as oy
+    fr = synth.make_frames(n_frames, seed=0)
+    synth.YOLO_CALIB['row_gain'] = {r: 1.0 for r in range(6)}
+    synth.YOLO_CALIB['row_bias'] = {}
+    p = synth.make_params('yolo')
+    for i in range(3):
+        p['head.convs_pred.%d.bias' % i][:] = 0.0
+    x, _, _ = oy.preprocess(list(fr))
+    maps = oy.net(p, x)
+    gains = {}
+    for r in range(6):
+        d = torch.cat([m[:, r::6].flatten() for m in maps]).double()
+        gains[r] = float('%.6g' % (0.3 / float(d.std())))
+        if r == 4:
+            q1, q2 = float(torch.quantile(d, 1 - 0.005)), float(torch.quantile(d, 1 - 0.0005))
+            g = 5.2933 / (q2 - q1)
+            gains[4] = float('%.6g' % g)
+            b = float('%.6g' % (-g * q2))
+            print('obj raw std %.4f q99.5 %.4f q99.95 %.4f -> gain %.6g bias %.6g' % (float(d.std()), q1, q2, g, b))
+    synth.YOLO_CALIB['row_gain'] = gains
+    synth.YOLO_CALIB['row_bias'] = {4: b, 5: 3.0}
+    p = synth.make_params('yolo')
+    bx, sc, _ = oy.forward(p, list(fr))
+    print('per frame kept', [len(s) for s in sc], 'score>0.4', [int((s > 0.4).sum()) for s in sc])
+    print('box sizes', [np.round(np.median(b[:, 2:] - b[:, :2], 0), 1) for b in bx])
+    print('YOLO_CALIB =', synth.YOLO_CALIB)
+
+
 if __name__ == '__main__':
-    main()
+    if sys.argv[1:] == ['yolo']:
+        calibrate_yolo()
+    else:
+        main()

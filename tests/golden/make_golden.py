@@ -232,7 +232,44 @@ def gen_grouping():
     print('grouping', {k: v.shape for k, v in out.items()})
 
 
+def gen_yolo():
+    """YOLOv3 (yolo.py:131-176) from the letterboxed tensor on: the reference's preprocess
+    calls cv2.resize (absent), so the resized uint8 images are made with the build's
+    INTER_LINEAR restatement (oracle/yolo.py, parity-unpinned step) and stored as the
+    golden INPUT; to_tensors/pad_and_batch, the net, priors, postprocess and scale_boxes
+    are the reference's own code."""
+    load_ref()
+    y = importlib.import_module('ref_vtf.detectors.yolo')
+    prep = importlib.import_module('ref_vtf.detectors.operations.prep')
+    sys.path.insert(0, ROOT)
+    from oracle import yolo as oy
+    net = _load(y.YOLOv3('cpu'), synth.make_params('yolo'))
+    frames = synth.make_frames(2, seed=0)
+    resized, szo, szu = [], [], []
+    for f in frames:
+        sz = f.shape[:2]
+        scl = min(608 / min(sz), 608 / max(sz))
+        n = int(sz[0] * scl + 0.5), int(sz[1] * scl + 0.5)
+        resized.append(oy.resize_linear_u8_hw(f, n))
+        szo.append(sz)
+        szu.append(n)
+    with torch.inference_mode():
+        ts = prep.to_tensors(resized, 'cpu', None, 255, True)
+        x = prep.pad_and_batch(ts, 32)
+        xs = net.head(net.neck(net.backbone(x)))
+        pri = y.get_priors(x.shape[-2:], y.YOLOv3.bases, 'cpu', 'center')
+        b, s, c = net.postprocess(xs, pri, num_classes=1)
+        b = y.scale_boxes(b, szo, szu)
+    out = dict(resized=np.stack(resized), szo=np.array(szo), szu=np.array(szu),
+               counts=np.array([len(t) for t in s], np.int64),
+               boxes=torch.cat(b).numpy(), scores=torch.cat(s).numpy(), classes=torch.cat(c).numpy())
+    for i, m in enumerate(xs):
+        out['map%d' % i] = m.numpy()
+    np.savez_compressed(os.path.join(HERE, 'yolo.npz'), **out)
+    print('yolo', {k: v.shape for k, v in out.items()}, 'counts', out['counts'])
+
+
 if __name__ == '__main__':
-    which = sys.argv[1:] or ['mtcnn', 'facenet', 'vit', 'grouping']
+    which = sys.argv[1:] or ['mtcnn', 'facenet', 'vit', 'grouping', 'yolo']
     for w in which:
         globals()['gen_' + w]()

@@ -17,27 +17,6 @@
 
 namespace vtf {
 
-__device__ inline void lin_coef(int d, int src, int dst, int& s0, int& s1, int& c0, int& c1, bool& edge) {
-    double scale = 1.0 / ((double)dst / (double)src);
-    float f = (float)(((double)d + 0.5) * scale - 0.5);
-    int s = (int)floorf(f);
-    f -= (float)s;
-    edge = false;
-    if (s < 0) {
-        f = 0.f;
-        s = 0;
-    }
-    if (s >= src - 1) {
-        f = 0.f;
-        s = src - 1;
-        edge = true;
-    }
-    s0 = s;
-    s1 = min(s + 1, src - 1);
-    c0 = (int)rintf((1.f - f) * 2048.f);
-    c1 = (int)rintf(f * 2048.f);
-}
-
 template <typename T>
 __device__ inline T cvt_out(float v);
 template <>

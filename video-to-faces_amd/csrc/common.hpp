@@ -87,6 +87,13 @@ __device__ inline const VTF_CONST T* cptr(const T* p) {
 }
 
 __host__ __device__ inline uint32_t f2u(float f) { return __builtin_bit_cast(uint32_t, f); }
+// fp32 -> bf16 bits, round to nearest even (host-side weight packing)
+inline uint16_t f2bf(float f) {
+    uint32_t u = f2u(f);
+    if ((u & 0x7fffffff) > 0x7f800000) return (uint16_t)((u >> 16) | 0x40);  // NaN stays NaN
+    u += 0x7FFF + ((u >> 16) & 1);
+    return (uint16_t)(u >> 16);
+}
 
 // Sortable descending key of a float: larger float -> smaller key (NaN-free inputs).
 __host__ __device__ inline uint32_t desc_key(float f) {

@@ -63,6 +63,7 @@ __global__ __launch_bounds__(256) void k_conv(ConvParams p) {
     const int n0 = blockIdx.y * BN;
     const T* __restrict__ in = (const T*)p.in;
     const T* __restrict__ wt = (const T*)p.w;
+    const int ics = p.in_cstride ? p.in_cstride : p.Cin;
 
     // per-thread A rows and the thread's k-vector position
     const int kv = tid % KV;
@@ -79,7 +80,7 @@ __global__ __launch_bounds__(256) void k_conv(ConvParams p) {
         int64_t t = mm / p.OW;
         int oh = (int)(t % p.OH);
         int n = (int)(t / p.OH);
-        a_base[r] = (int64_t)n * p.H * p.W * p.Cin;
+        a_base[r] = (int64_t)n * p.H * p.W * ics;
         a_ih0[r] = oh * p.sh - p.ph;
         a_iw0[r] = ow * p.sw - p.pw;
     }
@@ -93,7 +94,7 @@ __global__ __launch_bounds__(256) void k_conv(ConvParams p) {
             vec v = {};
             int ih = a_ih0[r] + kh0, iw = a_iw0[r] + kw0;
             if (a_ok[r] && kcur < p.K && ih >= 0 && ih < p.H && iw >= 0 && iw < p.W)
-                v = *(const vec*)(in + a_base[r] + ((int64_t)ih * p.W + iw) * p.Cin + ci_);
+                v = *(const vec*)(in + a_base[r] + ((int64_t)ih * p.W + iw) * ics + ci_);
             ra[r] = v;
         }
 #pragma unroll
@@ -202,11 +203,29 @@ __global__ __launch_bounds__(256) void k_conv(ConvParams p) {
                 if (p.bias) v = v + bias;
                 if (p.alpha) v = fmaf(v, al, be);
                 if (p.scale != 1.f) v = v * p.scale;
-                if (res) v = v + to_f(res[m * p.res_cstride + c]);
+                if (res && !p.res_post) v = v + to_f(res[m * p.res_cstride + c]);
                 if (p.relu) v = fmaxf(v, 0.f);
+                if (p.leaky) v = v > 0.f ? v : v * p.slope;
                 if (p.prelu) v = v > 0.f ? v : p.prelu[c] * v;
                 if (p.gelu) v = 0.5f * v * (1.0f + erff(v * 0.70710678118654752f));
-                out[m * p.out_cstride + p.out_coff + c] = from_f<T>(v);
+                if (res && p.res_post) v = v + to_f(res[m * p.res_cstride + c]);
+                if (p.up2) {
+                    int ow = (int)(m % p.OW);
+                    int64_t t = m / p.OW;
+                    int oh = (int)(t % p.OH);
+                    int64_t n = t / p.OH;
+                    int64_t o = ((n * 2 * p.OH + 2 * oh) * 2 * p.OW + 2 * ow) * p.out_cstride + p.out_coff + c;
+                    int64_t rs = (int64_t)2 * p.OW * p.out_cstride;
+                    T tv = from_f<T>(v);
+                    out[o] = tv;
+                    out[o + p.out_cstride] = tv;
+                    out[o + rs] = tv;
+                    out[o + rs + p.out_cstride] = tv;
+                } else if (p.out_f32) {
+                    ((float*)p.out)[m * p.out_cstride + p.out_coff + c] = v;
+                } else {
+                    out[m * p.out_cstride + p.out_coff + c] = from_f<T>(v);
+                }
             }
         }
     }
@@ -232,6 +251,8 @@ static void launch_t(const ConvParams& p, hipStream_t st) {
 void launch_conv(const ConvParams& p, bool bf16, hipStream_t st) {
     if (p.M <= 0) return;
     VTF_CHECK(p.Cin % 8 == 0, VTF_E_ARG, "conv: Cin must be a multiple of 8 (pad the input)");
+    VTF_CHECK(p.in_cstride == 0 || (p.in_cstride >= p.Cin && p.in_cstride % 8 == 0), VTF_E_ARG,
+              "conv: bad input channel stride");
     if (bf16)
         launch_t<__bf16>(p, st);
     else

@@ -15,6 +15,13 @@ struct ConvParams {
     float scale;
     int relu;
     int gelu;            // exact erf GELU (ViT MLP, vit.py:37)
+    int leaky;           // LeakyReLU(slope) (YOLO conv_unit 'lrelu_0.1', yolo.py:17-18)
+    float slope;
+    int res_post;        // residual added AFTER the activation (Darknet ResBlock y + x, yolo.py:28-31)
+    int up2;             // write each output pixel to a 2x2 block of a (2*OH, 2*OW) tensor
+                         // (F.interpolate(scale_factor=2) nearest, yolo.py:87,91)
+    int in_cstride;      // input channel stride (0 = Cin): read a channel slice of a concat buffer
+    int out_f32;         // output is fp32 whatever the operand precision (detector heads)
     int64_t M;           // N*OH*OW
     int N, H, W, Cin, OH, OW, Cout, KH, KW, sh, sw, ph, pw, K;
     int out_cstride, out_coff, res_cstride;

@@ -102,12 +102,6 @@ static void bn_fold(const float* w, const float* b, const float* mean, const flo
     }
 }
 
-static uint16_t f2bf(float f) {
-    uint32_t u = f2u(f);
-    if ((u & 0x7fffffff) > 0x7f800000) return (uint16_t)((u >> 16) | 0x40);  // NaN stays NaN
-    u += 0x7FFF + ((u >> 16) & 1);
-    return (uint16_t)(u >> 16);
-}
 
 static void build(Facenet& F, const float* params, int64_t n_params) {
     std::vector<G> geo = facenet_geometry();

@@ -50,6 +50,15 @@ SIGNATURES = {
     'vtf_vit_encode_crops': [_p, _p, _i32, _i32, _i64, _i64, _p, _i64, _p],
     'vtf_blob_from_crops': [_p, _i32, _i32, _i64, _i64, _p, _i64, _i32, _f32, _f32, _p, _p],
     'vtf_cosine_dedupe': [_p, _i64, _i64, _p, _p, _p],
+    'vtf_yolo_create': [_p, _i64, _i32, _i32, _p],
+    'vtf_yolo_destroy': [_p],
+    'vtf_yolo_set_stream': [_p, _p],
+    'vtf_yolo_detect': [_p, _p, _i32, _i32, _i32, _i32, _i64, _i64, _p, _p, _p, _i64, _p],
+    'vtf_yolo_input_size': [_i32, _i32, _p],
+    'vtf_yolo_letterbox': [_p, _p, _i32, _i32, _i32, _i64, _i64, _p],
+    'vtf_yolo_net': [_p, _p, _i32, _i32, _i32, _p, _p, _p],
+    'vtf_yolo_postprocess': [_p, _p, _p, _p, _i32, _i32, _i32, _p, _p, _p, _i64, _p],
+    'vtf_yolo_profile': [_p, _i32, _p, _p, _p, _p],
     'vtf_cosine_classify': [_p, _i64, _p, _i64, _i64, _p, _p, _p],
 }
 _RESTYPE = {'vtf_last_error': _c.c_char_p}
@@ -103,3 +112,26 @@ def ptr(t):
 
 def stream_ptr(device):
     return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+def frames_view(imgs):
+    """Frames argument of the detectors: np.ndarray uint8 [B,H,W,3] (any non-negative
+    strides with packed pixels), a list of frames, or a uint8 CUDA tensor in HBM.
+    Returns (base pointer, on_device, B, H, W, frame_stride, row_stride, owner)."""
+    import numpy as np
+    import torch
+    if isinstance(imgs, torch.Tensor):
+        t = imgs
+        if t.dtype != torch.uint8 or t.dim() != 4 or t.shape[3] != 3:
+            raise ValueError('frames tensor must be uint8 [B,H,W,3]')
+        if t.stride(3) != 1 or t.stride(2) != 3:
+            t = t.contiguous()
+        B, H, W = t.shape[:3]
+        return _c.c_void_p(t.data_ptr()), int(t.is_cuda), B, H, W, t.stride(0), t.stride(1), t
+    x = imgs if isinstance(imgs, np.ndarray) else np.stack(imgs)
+    if x.dtype != np.uint8 or x.ndim != 4 or x.shape[3] != 3:
+        raise ValueError('frames must be uint8 [B,H,W,3]')
+    if x.strides[3] != 1 or x.strides[2] != 3 or x.strides[0] < 0 or x.strides[1] < 0:
+        x = np.ascontiguousarray(x)
+    B, H, W = x.shape[:3]
+    return _c.c_void_p(x.ctypes.data), 0, B, H, W, x.strides[0], x.strides[1], x

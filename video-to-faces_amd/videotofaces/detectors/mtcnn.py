@@ -42,28 +42,7 @@ class MTCNN:
     def forward(self, imgs, minsize=20, return_landmarks=False):
         L = nat.lib()
         self._bind_stream()
-        if isinstance(imgs, torch.Tensor):
-            t = imgs
-            if t.dtype != torch.uint8 or t.dim() != 4 or t.shape[3] != 3:
-                raise ValueError('frames tensor must be uint8 [B,H,W,3]')
-            if t.stride(3) != 1 or t.stride(2) != 3:
-                t = t.contiguous()
-            on_dev = int(t.is_cuda)
-            B, H, W = t.shape[:3]
-            fstride, rstride = t.stride(0), t.stride(1)
-            base = ctypes.c_void_p(t.data_ptr())
-            keep_alive = t
-        else:
-            x = imgs if isinstance(imgs, np.ndarray) else np.stack(imgs)
-            if x.dtype != np.uint8 or x.ndim != 4 or x.shape[3] != 3:
-                raise ValueError('frames must be uint8 [B,H,W,3]')
-            if x.strides[3] != 1 or x.strides[2] != 3 or x.strides[0] < 0 or x.strides[1] < 0:
-                x = np.ascontiguousarray(x)
-            on_dev = 0
-            B, H, W = x.shape[:3]
-            fstride, rstride = x.strides[0], x.strides[1]
-            base = ctypes.c_void_p(x.ctypes.data)
-            keep_alive = x
+        base, on_dev, B, H, W, fstride, rstride, keep_alive = nat.frames_view(imgs)
         cap = max(64, 256 * B)
         while True:
             boxes = np.empty((cap, 5), np.float32)
