@@ -33,6 +33,7 @@ typedef struct vtf_mtcnn_s* vtf_mtcnn_t;
 typedef struct vtf_facenet_s* vtf_facenet_t;
 typedef struct vtf_vit_s* vtf_vit_t;
 typedef struct vtf_yolo_s* vtf_yolo_t;
+typedef struct vtf_group_s* vtf_group_t;
 
 /* ---------------------------------------------------------------- MTCNN detector
  * Replaces RealMTCNN / MTCNN.forward (src/videotofaces/detectors/mtcnn.py:167-252,
@@ -163,6 +164,45 @@ int vtf_yolo_postprocess(vtf_yolo_t h, const float* d_map0, const float* d_map1,
  * turns timing on for the following calls. */
 int vtf_yolo_profile(vtf_yolo_t h, int enable, double* out_ms, int64_t* out_launches, double* out_flops,
                      int64_t* out_frames);
+
+/* ---------------------------------------------------------------- grouping: K-means, scores
+ * Replace the sklearn calls of cluster_faces (src/videotofaces/grouping.py:92-120):
+ * KMeans(n_clusters=k, random_state, n_init='auto').fit(X), silhouette_score,
+ * calinski_harabasz_score, davies_bouldin_score.  The host mirror (videotofaces/kmeans.py)
+ * keeps sklearn's scalar control flow; these are its device passes.  All device arrays are
+ * row-major, X float32 [N,D]. */
+int vtf_group_create(int device, vtf_group_t* out);
+int vtf_group_destroy(vtf_group_t h);
+int vtf_group_set_stream(vtf_group_t h, void* hip_stream);
+/* X.mean(axis=0), np.var(X, axis=0) (numpy's sequential fp32 axis-0 sums) and, if d_Xc is
+ * not NULL, the centred copy X - mean (KMeans.fit, sklearn/cluster/_kmeans.py:1479-1481). */
+int vtf_colstats(vtf_group_t h, const float* d_X, int64_t N, int64_t D, float* d_Xc, float* d_mean, float* d_var);
+/* k-means++ distances (_kmeans.py:_kmeans_plusplus): d_out [T,N] = squared euclidean
+ * distances of rows[0..T) (host int64 indices) to every row, sklearn's float64-upcast
+ * formula rounded to fp32 and clipped at 0.  T <= 16. */
+int vtf_sqdist_rows(vtf_group_t h, const float* d_X, int64_t N, int64_t D, const int64_t* rows, int T, float* d_out);
+/* One Lloyd iteration (_k_means_lloyd.pyx lloyd_iter_chunked_dense): labels (in/out, int32)
+ * from centers [k,D]; if d_sums: per-cluster sums [k,D] (float64-accumulated, fp32) and
+ * weights [k] (counts).  *out_changed = number of labels that changed.  k <= 64. */
+int vtf_kmeans_step(vtf_group_t h, const float* d_X, int64_t N, int64_t D, const float* d_centers, int k,
+                    int32_t* d_labels, float* d_sums, float* d_weights, int64_t* out_changed);
+/* _average_centers + _center_shift: sums -> centers in place, shift[k] = |new - old|. */
+int vtf_kmeans_average(vtf_group_t h, float* d_sums, const float* d_weights, const float* d_centers_old, int k,
+                       int64_t D, float* d_shift);
+/* ((X - centers[labels])**2).sum(1) (empty-cluster relocation, _k_means_common.pyx). */
+int vtf_center_dist(vtf_group_t h, const float* d_X, int64_t N, int64_t D, const float* d_centers,
+                    const int32_t* d_labels, float* d_out);
+/* pairwise_distances(X) euclidean [N,N] fp32 (float64-upcast, sqrt, zero diagonal). */
+int vtf_pairwise_euclidean(vtf_group_t h, const float* d_X, int64_t N, int64_t D, float* d_out);
+/* silhouette_samples from the distance matrix; labels encoded 0..k-1, freq int64 [k]. */
+int vtf_silhouette_samples(vtf_group_t h, const float* d_D, int64_t N, const int32_t* d_labels, int k,
+                           const int64_t* d_freq, float* d_sil);
+/* Per-cluster float64 sums [k,D], sum of |x|^2 [k] and counts [k] (calinski_harabasz). */
+int vtf_cluster_sums(vtf_group_t h, const float* d_X, int64_t N, int64_t D, const int32_t* d_labels, int k,
+                     double* d_sums, double* d_sqnorm, int64_t* d_counts);
+/* dsum[c] = sum over members of |x - centroid_c| in float64 (davies_bouldin intra_dists). */
+int vtf_cluster_dist(vtf_group_t h, const float* d_X, int64_t N, int64_t D, const int32_t* d_labels, int k,
+                     const double* d_centroids, double* d_dsum);
 
 #ifdef __cplusplus
 }

@@ -269,7 +269,28 @@ def gen_yolo():
     print('yolo', {k: v.shape for k, v in out.items()}, 'counts', out['counts'])
 
 
+def gen_kmeans():
+    """cluster_faces internals at N=2000, D=512, k=2..16 (grouping.py:97-107) with the
+    reference's sklearn (1.7.2 here): KMeans labels and the three scores per k."""
+    import hashlib
+    import sklearn.cluster
+    import sklearn.metrics
+    X = synth.planted_clusters()
+    ks = list(range(2, 17))
+    labels, scores = [], []
+    for k in ks:
+        lb = sklearn.cluster.KMeans(n_clusters=k, random_state=0, n_init='auto').fit(X).labels_
+        labels.append(lb)
+        scores.append((sklearn.metrics.silhouette_score(X, lb), sklearn.metrics.calinski_harabasz_score(X, lb),
+                       sklearn.metrics.davies_bouldin_score(X, lb)))
+    sil = sklearn.metrics.silhouette_samples(X, labels[6])
+    np.savez_compressed(os.path.join(HERE, 'kmeans.npz'), X_sha256=np.frombuffer(
+        hashlib.sha256(X.tobytes()).digest(), np.uint8), k=np.array(ks), labels=np.stack(labels).astype(np.int8),
+        scores=np.array(scores, np.float64), sil_k8=sil.astype(np.float32))
+    print('kmeans', X.shape, 'best k', ks[int(np.argmax([s[0] for s in scores]))])
+
+
 if __name__ == '__main__':
-    which = sys.argv[1:] or ['mtcnn', 'facenet', 'vit', 'grouping', 'yolo']
+    which = sys.argv[1:] or ['mtcnn', 'facenet', 'vit', 'grouping', 'yolo', 'kmeans']
     for w in which:
         globals()['gen_' + w]()

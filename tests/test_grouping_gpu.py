@@ -45,3 +45,60 @@ def test_classify_vs_golden(g):
     inds, classes = grouping.classify(g['X'], g['classify_R'], ['a', 'b', 'c'], 0.9, False, [], None)
     np.testing.assert_array_equal(inds, g['classify_inds'])
     assert classes == ['a', 'b', 'c', 'other']
+
+
+@pytest.fixture(scope='module')
+def km():
+    from videotofaces import synth
+    return np.load(os.path.join(GOLDEN, 'kmeans.npz')), synth.planted_clusters()
+
+
+def test_kmeans_labels_vs_sklearn(km):
+    """KMeans(k, random_state=0, n_init='auto') labels for k = 2..16 (N=2000, D=512):
+    bit-exact integer labels against sklearn."""
+    from videotofaces.kmeans import Grouper
+    g, X = km
+    gr = Grouper('cuda:0')
+    prep = gr.prepare(X)
+    for i, k in enumerate(g['k']):
+        np.testing.assert_array_equal(gr.kmeans(X, int(k), prep=prep), g['labels'][i], err_msg='k=%d' % k)
+
+
+def test_kmeans_small_golden(g):
+    """grouping.npz: the reference-path sweep (k=2..9) on the deduped 600-row set."""
+    from videotofaces import dupes
+    from videotofaces.kmeans import Grouper
+    mins, _ = dupes.cosine_dedupe_device(torch.from_numpy(g['X']).cuda())
+    Xk = g['X'][~(mins <= 0.25)]
+    gr = Grouper('cuda:0')
+    for i, k in enumerate(g['kmeans_k']):
+        lb = gr.kmeans(Xk, int(k))
+        np.testing.assert_array_equal(lb, g['kmeans_labels'][i], err_msg='k=%d' % k)
+        s1 = gr.silhouette_score(Xk, lb)
+        s2 = gr.calinski_harabasz_score(Xk, lb)
+        s3 = gr.davies_bouldin_score(Xk, lb)
+        np.testing.assert_allclose([s1, s2, s3], g['cluster_scores'][i], rtol=1e-5)
+
+
+def test_silhouette_and_scores_vs_sklearn(km):
+    from videotofaces.kmeans import Grouper
+    g, X = km
+    gr = Grouper('cuda:0')
+    sil = gr.silhouette_samples(X, g['labels'][6])
+    np.testing.assert_allclose(sil, g['sil_k8'], rtol=0, atol=2e-7)
+    print('silhouette samples exact:', np.array_equal(sil, g['sil_k8']))
+    for i in (0, 6, 14):
+        lb = g['labels'][i]
+        got = [gr.silhouette_score(X, lb), gr.calinski_harabasz_score(X, lb), gr.davies_bouldin_score(X, lb)]
+        np.testing.assert_allclose(got, g['scores'][i], rtol=1e-5)
+
+
+def test_cluster_sweep_best_k(km):
+    from videotofaces.grouping import cluster_sweep
+    g, X = km
+    ks = [int(k) for k in g['k']]
+    labels, scores = cluster_sweep(X, ks, 0)
+    best = max(scores, key=lambda x: x[1])[0]
+    assert best == ks[int(np.argmax(g['scores'][:, 0]))]
+    for i in range(len(ks)):
+        np.testing.assert_array_equal(labels[i], g['labels'][i])

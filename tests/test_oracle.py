@@ -151,3 +151,32 @@ def test_oracle_yolo_vs_golden():
     np.testing.assert_array_equal(torch.cat(b).numpy(), gy['boxes'])
     np.testing.assert_array_equal(torch.cat(s).numpy(), gy['scores'])
     np.testing.assert_array_equal(torch.cat(c).numpy(), gy['classes'])
+
+
+@pytest.fixture(scope='module')
+def km():
+    import hashlib
+    from videotofaces import synth
+    g = np.load(os.path.join(GOLDEN, 'kmeans.npz'))
+    X = synth.planted_clusters()
+    assert hashlib.sha256(X.tobytes()).digest() == g['X_sha256'].tobytes(), 'planted_clusters drifted'
+    return g, X
+
+
+def test_kmeans_host_control_flow_vs_sklearn(km):
+    """videotofaces.kmeans.Grouper's sklearn control flow, driven by the numpy restatement of
+    its device passes, reproduces sklearn's KMeans labels for k = 2..16 bit-exactly."""
+    from oracle.kmeans import CpuGrouper
+    g, X = km
+    cg = CpuGrouper()
+    prep = cg.prepare(X)
+    for i, k in enumerate(g['k']):
+        np.testing.assert_array_equal(cg.kmeans(X, int(k), prep=prep), g['labels'][i], err_msg='k=%d' % k)
+
+
+def test_silhouette_restatement_vs_sklearn(km):
+    from oracle.kmeans import silhouette_samples
+    g, X = km
+    sil = silhouette_samples(X, g['labels'][6])
+    np.testing.assert_array_equal(sil, g['sil_k8'])
+    assert float(np.mean(sil)) == g['scores'][6][0]

@@ -59,3 +59,48 @@ def test_all_gather_rows_rank_order_gloo():
     expect = [[f, k] for f in range(70) for k in range(f % 3)]
     for r in range(world):
         assert res[r] == expect
+
+
+def _sweep_worker(rank, world, port, q):
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [root, os.path.join(root, 'video-to-faces_amd')]
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    from oracle.kmeans import CpuGrouper
+    from videotofaces import synth
+    from videotofaces.grouping import cluster_sweep
+    X = synth.planted_clusters(N=400, D=32)
+    g = CpuGrouper()
+    prep = g.prepare(X)
+    done = []
+
+    def compute(k):
+        done.append(k)
+        return g.kmeans(X, k, prep=prep), (float(k), 0.0, 0.0)
+    labels, scores = cluster_sweep(X, [2, 3, 4, 5, 6], 0, compute)
+    q.put((rank, done, [lb.tolist() for lb in labels], scores))
+    dist.destroy_process_group()
+
+
+def test_cluster_sweep_sharded_by_k_gloo():
+    """The k sweep is split across ranks (i % world) and all-gathered in k order; every rank
+    ends with the full, identical result."""
+    world = 2
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_sweep_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    res = {r: (d, lb, sc) for r, d, lb, sc in (q.get(timeout=180) for _ in range(world))}
+    for p in ps:
+        p.join(timeout=60)
+    assert res[0][0] == [2, 4, 6] and res[1][0] == [3, 5]
+    assert res[0][1] == res[1][1] and res[0][2] == res[1][2]
+    assert [s[0] for s in res[0][2]] == [2, 3, 4, 5, 6]
+    from oracle.kmeans import CpuGrouper
+    from videotofaces import synth
+    X = synth.planted_clusters(N=400, D=32)
+    for k, lb in zip([2, 3, 4, 5, 6], res[0][1]):
+        assert lb == CpuGrouper().kmeans(X, k).tolist()

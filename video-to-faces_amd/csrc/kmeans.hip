@@ -1,0 +1,566 @@
+// Grouping on gfx950 (src/videotofaces/grouping.py:92-120 -> sklearn KMeans / silhouette /
+// Calinski-Harabasz / Davies-Bouldin).  The Python mirror (videotofaces/kmeans.py) runs the
+// scalar control flow of sklearn 1.7 (RandomState draws, searchsorted, convergence tests)
+// on host numpy; every O(N*D) / O(N^2*D) pass is one of these kernels.
+//
+//   k_colstats     X.mean(axis=0), X - mean, np.var(X, axis=0): per-column sequential fp32
+//                  sums in row order -- bit-identical to numpy's axis-0 reduction.
+//   k_sqdist_rows  _euclidean_distances(X[ids], X, squared=True) for float32 X: the
+//                  float64-upcast formula (-2 x.y + |x|^2 + |y|^2 in double, then float32,
+//                  max 0; sklearn/metrics/pairwise.py:391-441,582-660).
+//   k_estep        Lloyd E-step (_k_means_lloyd.pyx:_update_chunk_dense): |c|^2 - 2 x.c in
+//                  fp32, first strict minimum; counts label changes.
+//   k_msum/k_mred  M-step sums: float64 per-(row block, cluster, feature) partials reduced in
+//                  a fixed order (deterministic), rounded to fp32; counts as weights.
+//   k_average      _average_centers (c *= 1/w) and _center_shift (4-way unrolled fp32).
+//   k_pdist        full N x N euclidean matrix (pairwise_distances_chunked): float64 tile
+//                  GEMM + norms, rounded to fp32, sqrt, zero diagonal.  Kept resident in HBM
+//                  and reused for every k of a sweep.
+//   k_silhouette   _silhouette_reduce + silhouette_samples per row (one wave per row).
+//   k_csum/k_cdist cluster sums / |x|^2 / distance-to-centroid sums in float64 (CH, DB).
+#include <cmath>
+#include <vector>
+
+#include "common.hpp"
+
+namespace vtf {
+
+// ------------------------------------------------------------------ column statistics
+__global__ void k_colstats(const float* __restrict__ X, int64_t N, int D, float* __restrict__ Xc,
+                           float* __restrict__ mean, float* __restrict__ var) {
+    int d = blockIdx.x * blockDim.x + threadIdx.x;
+    if (d >= D) return;
+    float acc = 0.f;
+    for (int64_t i = 0; i < N; i++) acc += X[i * D + d];
+    float m = acc / (float)N;
+    float a2 = 0.f;
+    for (int64_t i = 0; i < N; i++) {
+        float x = X[i * D + d] - m;
+        if (Xc) Xc[i * D + d] = x;
+        a2 += x * x;
+    }
+    mean[d] = m;
+    var[d] = a2 / (float)N;
+}
+
+// ------------------------------------------------------------------ wave helpers
+__device__ inline double wave_sum_f64(double v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+__device__ inline float wave_sum_f32(float v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
+// ------------------------------------------------------------------ k-means++ distance rows
+// out[t][j] = max(0, f32((-2 * x_r.x_j + |x_r|^2) + |x_j|^2)), r = rows[t], all in double
+template <int TMAX>
+__global__ __launch_bounds__(256) void k_sqdist_rows(const float* __restrict__ X, int64_t N, int D,
+                                                     const int64_t* __restrict__ rows, int T, float* __restrict__ out) {
+    extern __shared__ float sR[];  // [T][D]
+    for (int e = threadIdx.x; e < T * D; e += blockDim.x) sR[e] = X[rows[e / D] * D + (e % D)];
+    __syncthreads();
+    const int lane = threadIdx.x & 63;
+    double rn[TMAX];
+#pragma unroll
+    for (int t = 0; t < TMAX; t++) {
+        double s = 0.0;
+        if (t < T)
+            for (int d = lane; d < D; d += 64) s += (double)sR[t * D + d] * (double)sR[t * D + d];
+        rn[t] = wave_sum_f64(s);
+    }
+    const int64_t wid = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
+    for (int64_t j = wid; j < N; j += nw) {
+        double dot[TMAX], yy = 0.0;
+#pragma unroll
+        for (int t = 0; t < TMAX; t++) dot[t] = 0.0;
+        for (int d = lane; d < D; d += 64) {
+            double y = (double)X[j * D + d];
+            yy += y * y;
+#pragma unroll
+            for (int t = 0; t < TMAX; t++)
+                if (t < T) dot[t] += (double)sR[t * D + d] * y;
+        }
+        yy = wave_sum_f64(yy);
+#pragma unroll
+        for (int t = 0; t < TMAX; t++) {
+            if (t < T) {
+                double s = wave_sum_f64(dot[t]);
+                double dd = -2.0 * s;
+                dd += rn[t];
+                dd += yy;
+                float f = (float)dd;
+                if (lane == 0) out[(int64_t)t * N + j] = fmaxf(f, 0.f);
+            }
+        }
+    }
+}
+
+// ------------------------------------------------------------------ Lloyd
+__global__ void k_csq(const float* __restrict__ C, int k, int D, float* __restrict__ csq) {
+    int j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= k) return;
+    float s = 0.f;
+    for (int d = 0; d < D; d++) s += C[(int64_t)j * D + d] * C[(int64_t)j * D + d];
+    csq[j] = s;
+}
+
+// one wave per sample; centers staged in LDS
+__global__ __launch_bounds__(256) void k_estep(const float* __restrict__ X, int64_t N, int D,
+                                               const float* __restrict__ C, const float* __restrict__ csq, int k,
+                                               int32_t* __restrict__ labels, unsigned long long* __restrict__ changed) {
+    extern __shared__ float sC[];  // [k][D]
+    for (int e = threadIdx.x; e < k * D; e += blockDim.x) sC[e] = C[e];
+    __syncthreads();
+    const int lane = threadIdx.x & 63;
+    const int64_t wid = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
+    unsigned long long nchg = 0;
+    for (int64_t i = wid; i < N; i += nw) {
+        float best = 0.f;
+        int lab = 0;
+        for (int j = 0; j < k; j++) {
+            float s = 0.f;
+            for (int d = lane; d < D; d += 64) s = fmaf(X[i * D + d], sC[j * D + d], s);
+            s = wave_sum_f32(s);
+            float dist = csq[j] + (-2.f * s);
+            if (j == 0 || dist < best) {
+                best = dist;
+                lab = j;
+            }
+        }
+        if (lane == 0) {
+            if (labels[i] != lab) nchg++;
+            labels[i] = lab;
+        }
+    }
+    if (lane == 0 && nchg) atomicAdd(changed, nchg);
+}
+
+// M-step partial sums: grid (cdiv(D, 64), nb); thread = (column, cluster group of 16)
+template <int KC>
+__global__ __launch_bounds__(256) void k_msum(const float* __restrict__ X, int64_t N, int D,
+                                              const int32_t* __restrict__ labels, int k, int64_t rows_per_block,
+                                              double* __restrict__ part, int64_t* __restrict__ cpart) {
+    const int d = blockIdx.x * 64 + (threadIdx.x & 63);
+    const int j0 = (threadIdx.x >> 6) * KC;  // 4 groups of KC clusters per block
+    const int64_t b = blockIdx.y;
+    const int64_t i0 = b * rows_per_block, i1 = min(N, i0 + rows_per_block);
+    double acc[KC];
+    int64_t cnt[KC];
+#pragma unroll
+    for (int c = 0; c < KC; c++) {
+        acc[c] = 0.0;
+        cnt[c] = 0;
+    }
+    for (int64_t i = i0; i < i1; i++) {
+        int l = labels[i] - j0;
+        float v = d < D ? X[i * D + d] : 0.f;
+#pragma unroll
+        for (int c = 0; c < KC; c++)
+            if (l == c) {
+                acc[c] += (double)v;
+                cnt[c]++;
+            }
+    }
+#pragma unroll
+    for (int c = 0; c < KC; c++) {
+        int j = j0 + c;
+        if (j < k && d < D) part[(b * k + j) * D + d] = acc[c];
+        if (j < k && blockIdx.x == 0 && (threadIdx.x & 63) == 0) cpart[b * k + j] = cnt[c];
+    }
+}
+
+__global__ void k_mred(const double* __restrict__ part, const int64_t* __restrict__ cpart, int64_t nb, int k, int D,
+                       float* __restrict__ sums, float* __restrict__ w) {
+    int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= (int64_t)k * D) return;
+    int j = (int)(e / D), d = (int)(e % D);
+    double s = 0.0;
+    for (int64_t b = 0; b < nb; b++) s += part[(b * k + j) * D + d];
+    sums[e] = (float)s;
+    if (d == 0) {
+        int64_t c = 0;
+        for (int64_t b = 0; b < nb; b++) c += cpart[b * k + j];
+        w[j] = (float)c;
+    }
+}
+
+// _average_centers + _center_shift (_k_means_common.pyx:274-311), one block: each thread
+// owns feature columns (the reference's sequential j loop, including its copy of the
+// argmax-weight center into still-empty clusters), then one thread per cluster for the shift
+__global__ void k_average(float* __restrict__ Cn, const float* __restrict__ w, const float* __restrict__ Co, int k,
+                          int D, float* __restrict__ shift) {
+    int amax = 0;
+    for (int j = 1; j < k; j++)
+        if (w[j] > w[amax]) amax = j;
+    for (int d = threadIdx.x; d < D; d += blockDim.x) {
+        for (int j = 0; j < k; j++) {
+            float* c = Cn + (int64_t)j * D;
+            if (w[j] > 0.f) {
+                float alpha = 1.0f / w[j];
+                c[d] *= alpha;
+            } else {
+                c[d] = Cn[(int64_t)amax * D + d];
+            }
+        }
+    }
+    __syncthreads();
+    for (int j = threadIdx.x; j < k; j += blockDim.x) {
+        const float* a = Cn + (int64_t)j * D;
+        const float* o = Co + (int64_t)j * D;
+        float r = 0.f;
+        int n4 = D / 4, rem = D % 4, d = 0;
+        for (int q = 0; q < n4; q++, d += 4) {
+            float t0 = a[d] - o[d], t1 = a[d + 1] - o[d + 1], t2 = a[d + 2] - o[d + 2], t3 = a[d + 3] - o[d + 3];
+            r += ((t0 * t0 + t1 * t1) + t2 * t2) + t3 * t3;
+        }
+        for (int q = 0; q < rem; q++, d++) r += (a[d] - o[d]) * (a[d] - o[d]);
+        shift[j] = sqrtf(r);
+    }
+}
+
+// ((X - centers[labels])**2).sum(axis=1) for empty-cluster relocation
+__global__ void k_center_dist(const float* __restrict__ X, int64_t N, int D, const float* __restrict__ C,
+                              const int32_t* __restrict__ labels, float* __restrict__ out) {
+    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= N) return;
+    const float* c = C + (int64_t)labels[i] * D;
+    float s = 0.f;
+    for (int d = 0; d < D; d++) {
+        float t = X[i * D + d] - c[d];
+        s += t * t;
+    }
+    out[i] = s;
+}
+
+// ------------------------------------------------------------------ pairwise euclidean (N x N)
+__global__ void k_rownorm64(const float* __restrict__ X, int64_t N, int D, double* __restrict__ out) {
+    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= N) return;
+    double s = 0.0;
+    for (int d = 0; d < D; d++) {
+        double x = (double)X[i * D + d];
+        s += x * x;
+    }
+    out[i] = s;
+}
+
+// 64x64 output tile per 256-thread block, 4x4 doubles per thread, K staged through LDS
+__global__ __launch_bounds__(256) void k_pdist(const float* __restrict__ X, int64_t N, int D,
+                                               const double* __restrict__ nrm, float* __restrict__ out) {
+    constexpr int T = 64, KB = 16;
+    __shared__ double sA[KB][T + 1], sB[KB][T + 1];
+    const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
+    const int64_t i0 = (int64_t)blockIdx.y * T, j0 = (int64_t)blockIdx.x * T;
+    double acc[4][4] = {};
+    for (int k0 = 0; k0 < D; k0 += KB) {
+        for (int e = threadIdx.x; e < T * KB; e += 256) {
+            int r = e / KB, kk = e % KB;
+            int64_t ia = i0 + r, jb = j0 + r;
+            sA[kk][r] = (ia < N && k0 + kk < D) ? (double)X[ia * D + k0 + kk] : 0.0;
+            sB[kk][r] = (jb < N && k0 + kk < D) ? (double)X[jb * D + k0 + kk] : 0.0;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int kk = 0; kk < KB; kk++) {
+            double a[4], b[4];
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                a[q] = sA[kk][ty + 16 * q];
+                b[q] = sB[kk][tx + 16 * q];
+            }
+#pragma unroll
+            for (int p = 0; p < 4; p++)
+#pragma unroll
+                for (int q = 0; q < 4; q++) acc[p][q] = fma(a[p], b[q], acc[p][q]);
+        }
+        __syncthreads();
+    }
+#pragma unroll
+    for (int p = 0; p < 4; p++) {
+        int64_t i = i0 + ty + 16 * p;
+        if (i >= N) continue;
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            int64_t j = j0 + tx + 16 * q;
+            if (j >= N) continue;
+            double dd = -2.0 * acc[p][q];
+            dd += nrm[i];
+            dd += nrm[j];
+            float f = fmaxf((float)dd, 0.f);
+            out[i * N + j] = i == j ? 0.f : sqrtf(f);
+        }
+    }
+}
+
+// ------------------------------------------------------------------ silhouette
+// one wave per row i: per-cluster sums of D[i, :] (np.bincount, float64) -> float32, then the
+// silhouette_samples arithmetic in numpy's dtypes (float32 arrays divided by int64 counts
+// through float64; np.maximum; nan_to_num).
+template <int KMAX>
+__global__ __launch_bounds__(256) void k_silhouette(const float* __restrict__ Dm, int64_t N,
+                                                    const int32_t* __restrict__ labels, int k,
+                                                    const int64_t* __restrict__ freq, float* __restrict__ sil) {
+    const int lane = threadIdx.x & 63;
+    const int64_t wid = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
+    for (int64_t i = wid; i < N; i += nw) {
+        double acc[KMAX];
+#pragma unroll
+        for (int c = 0; c < KMAX; c++) acc[c] = 0.0;
+        const float* row = Dm + i * N;
+        for (int64_t j = lane; j < N; j += 64) {
+            double v = (double)row[j];
+            int l = labels[j];
+#pragma unroll
+            for (int c = 0; c < KMAX; c++)
+                if (l == c) acc[c] += v;
+        }
+        float inter = INFINITY, intra = 0.f;
+        int li = labels[i];
+#pragma unroll
+        for (int c = 0; c < KMAX; c++) {
+            if (c < k) {
+                float cd = (float)wave_sum_f64(acc[c]);
+                if (c == li) {
+                    intra = cd;
+                } else {
+                    float m = (float)((double)cd / (double)freq[c]);
+                    inter = fminf(inter, m);
+                }
+            }
+        }
+        if (lane == 0) {
+            float a = (float)((double)intra / (double)(freq[li] - 1));
+            float s = inter - a;
+            float mx = (isnan(a) || isnan(inter)) ? NAN : fmaxf(a, inter);
+            s = s / mx;
+            if (isnan(s)) s = 0.f;
+            else if (isinf(s)) s = s > 0 ? 3.402823466e38f : -3.402823466e38f;
+            sil[i] = s;
+        }
+    }
+}
+
+// ------------------------------------------------------------------ cluster statistics (CH, DB)
+// sums[k][D] (double), sqn[k] = sum |x|^2 (double), cnt[k]: one block per row chunk,
+// atomics on double (order-independent up to float64 rounding)
+__global__ void k_csum(const float* __restrict__ X, int64_t N, int D, const int32_t* __restrict__ labels,
+                       double* __restrict__ sums, double* __restrict__ sqn, unsigned long long* __restrict__ cnt) {
+    int64_t i = blockIdx.x;
+    if (i >= N) return;
+    int l = labels[i];
+    double q = 0.0;
+    for (int d = threadIdx.x; d < D; d += blockDim.x) {
+        double x = (double)X[i * D + d];
+        atomicAdd(&sums[(int64_t)l * D + d], x);
+        q += x * x;
+    }
+    __shared__ double red[256];
+    red[threadIdx.x] = q;
+    __syncthreads();
+    for (int s = blockDim.x / 2; s > 0; s >>= 1) {
+        if (threadIdx.x < s) red[threadIdx.x] += red[threadIdx.x + s];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        atomicAdd(&sqn[l], red[0]);
+        atomicAdd(&cnt[l], 1ull);
+    }
+}
+
+// dsum[k] += |x_i - centroid_{l_i}| (float64), Davies-Bouldin intra distances
+__global__ void k_cdist(const float* __restrict__ X, int64_t N, int D, const int32_t* __restrict__ labels,
+                        const double* __restrict__ cent, double* __restrict__ dsum) {
+    const int lane = threadIdx.x & 63;
+    const int64_t wid = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
+    for (int64_t i = wid; i < N; i += nw) {
+        int l = labels[i];
+        double s = 0.0;
+        for (int d = lane; d < D; d += 64) {
+            double t = (double)X[i * D + d] - cent[(int64_t)l * D + d];
+            s += t * t;
+        }
+        s = wave_sum_f64(s);
+        if (lane == 0) atomicAdd(&dsum[l], sqrt(s));
+    }
+}
+
+struct Group {
+    int device = 0;
+    hipStream_t st = 0;
+    Arena ar;
+};
+
+static int waves_grid(int64_t n) { return (int)std::min<int64_t>(cdiv(n, 4), 256 * 16); }
+
+}  // namespace vtf
+
+using namespace vtf;
+
+struct vtf_group_s {
+    Group g;
+};
+
+extern "C" {
+
+int vtf_group_create(int device, vtf_group_t* out) {
+    return guarded([&] {
+        VTF_CHECK(out, VTF_E_ARG, "null argument");
+        VTF_HIP(hipSetDevice(device));
+        auto* h = new vtf_group_s();
+        h->g.device = device;
+        *out = h;
+    });
+}
+
+int vtf_group_destroy(vtf_group_t h) {
+    return guarded([&] { delete h; });
+}
+
+int vtf_group_set_stream(vtf_group_t h, void* stream) {
+    return guarded([&] {
+        VTF_CHECK(h, VTF_E_ARG, "null handle");
+        h->g.st = (hipStream_t)stream;
+    });
+}
+
+int vtf_colstats(vtf_group_t h, const float* d_X, int64_t N, int64_t D, float* d_Xc, float* d_mean, float* d_var) {
+    return guarded([&] {
+        VTF_CHECK(h && d_X && d_mean && d_var && N > 0 && D > 0 && D < (1 << 20), VTF_E_ARG, "bad argument");
+        k_colstats<<<cdiv(D, 64), 64, 0, h->g.st>>>(d_X, N, (int)D, d_Xc, d_mean, d_var);
+        VTF_HIP(hipGetLastError());
+    });
+}
+
+int vtf_sqdist_rows(vtf_group_t h, const float* d_X, int64_t N, int64_t D, const int64_t* rows, int T, float* d_out) {
+    return guarded([&] {
+        VTF_CHECK(h && d_X && rows && d_out && N > 0 && D > 0 && T > 0 && T <= 16, VTF_E_ARG, "bad argument");
+        VTF_CHECK((size_t)T * D * 4 <= 64 * 1024, VTF_E_LIMIT, "sqdist_rows: T*D too large");
+        for (int t = 0; t < T; t++) VTF_CHECK(rows[t] >= 0 && rows[t] < N, VTF_E_ARG, "row index out of range");
+        int64_t* dr = h->g.ar.get<int64_t>(0, T);
+        VTF_HIP(hipMemcpyAsync(dr, rows, T * 8, hipMemcpyHostToDevice, h->g.st));
+        size_t sh = (size_t)T * D * 4;
+        if (T <= 4)
+            k_sqdist_rows<4><<<waves_grid(N), 256, sh, h->g.st>>>(d_X, N, (int)D, dr, T, d_out);
+        else
+            k_sqdist_rows<16><<<waves_grid(N), 256, sh, h->g.st>>>(d_X, N, (int)D, dr, T, d_out);
+        VTF_HIP(hipGetLastError());
+        VTF_HIP(hipStreamSynchronize(h->g.st));
+    });
+}
+
+// E-step (+ M-step sums when d_sums != NULL).  d_labels in/out; *out_changed = labels changed.
+int vtf_kmeans_step(vtf_group_t h, const float* d_X, int64_t N, int64_t D, const float* d_centers, int k,
+                    int32_t* d_labels, float* d_sums, float* d_weights, int64_t* out_changed) {
+    return guarded([&] {
+        VTF_CHECK(h && d_X && d_centers && d_labels && N > 0 && D > 0 && k > 0 && k <= 256, VTF_E_ARG,
+                  "bad argument");
+        VTF_CHECK((size_t)k * D * 4 <= 128 * 1024, VTF_E_LIMIT, "kmeans: k*D too large for LDS");
+        Group& G = h->g;
+        float* csq = G.ar.get<float>(1, k);
+        unsigned long long* chg = G.ar.get<unsigned long long>(2, 1);
+        VTF_HIP(hipMemsetAsync(chg, 0, 8, G.st));
+        k_csq<<<cdiv(k, 64), 64, 0, G.st>>>(d_centers, k, (int)D, csq);
+        k_estep<<<waves_grid(N), 256, (size_t)k * D * 4, G.st>>>(d_X, N, (int)D, d_centers, csq, k, d_labels, chg);
+        if (d_sums) {
+            VTF_CHECK(d_weights, VTF_E_ARG, "null weights");
+            const int64_t rpb = 256;
+            const int64_t nb = (N + rpb - 1) / rpb;
+            VTF_CHECK(k <= 64, VTF_E_LIMIT, "kmeans: k > 64");
+            double* part = G.ar.get<double>(3, (size_t)nb * k * D);
+            int64_t* cpart = G.ar.get<int64_t>(4, (size_t)nb * k);
+            // 4 waves x 16 clusters per block (k <= 64)
+            dim3 grid(cdiv(D, 64), (unsigned)nb);
+            k_msum<16><<<grid, 256, 0, G.st>>>(d_X, N, (int)D, d_labels, k, rpb, part, cpart);
+            k_mred<<<cdiv((int64_t)k * D, 256), 256, 0, G.st>>>(part, cpart, nb, k, (int)D, d_sums, d_weights);
+        }
+        unsigned long long c = 0;
+        VTF_HIP(hipMemcpyAsync(&c, chg, 8, hipMemcpyDeviceToHost, G.st));
+        VTF_HIP(hipStreamSynchronize(G.st));
+        if (out_changed) *out_changed = (int64_t)c;
+    });
+}
+
+int vtf_kmeans_average(vtf_group_t h, float* d_sums, const float* d_weights, const float* d_centers_old, int k,
+                       int64_t D, float* d_shift) {
+    return guarded([&] {
+        VTF_CHECK(h && d_sums && d_weights && d_centers_old && d_shift && k > 0 && D > 0, VTF_E_ARG, "bad argument");
+        k_average<<<1, 256, 0, h->g.st>>>(d_sums, d_weights, d_centers_old, k, (int)D, d_shift);
+        VTF_HIP(hipGetLastError());
+    });
+}
+
+int vtf_center_dist(vtf_group_t h, const float* d_X, int64_t N, int64_t D, const float* d_centers,
+                    const int32_t* d_labels, float* d_out) {
+    return guarded([&] {
+        VTF_CHECK(h && d_X && d_centers && d_labels && d_out && N > 0 && D > 0, VTF_E_ARG, "bad argument");
+        k_center_dist<<<cdiv(N, 256), 256, 0, h->g.st>>>(d_X, N, (int)D, d_centers, d_labels, d_out);
+        VTF_HIP(hipGetLastError());
+    });
+}
+
+int vtf_pairwise_euclidean(vtf_group_t h, const float* d_X, int64_t N, int64_t D, float* d_out) {
+    return guarded([&] {
+        VTF_CHECK(h && d_X && d_out && N > 0 && D > 0, VTF_E_ARG, "bad argument");
+        VTF_CHECK(N <= (1 << 20), VTF_E_LIMIT, "pairwise: N too large");
+        double* nrm = h->g.ar.get<double>(5, N);
+        k_rownorm64<<<cdiv(N, 256), 256, 0, h->g.st>>>(d_X, N, (int)D, nrm);
+        dim3 grid(cdiv(N, 64), cdiv(N, 64));
+        k_pdist<<<grid, 256, 0, h->g.st>>>(d_X, N, (int)D, nrm, d_out);
+        VTF_HIP(hipGetLastError());
+    });
+}
+
+int vtf_silhouette_samples(vtf_group_t h, const float* d_D, int64_t N, const int32_t* d_labels, int k,
+                           const int64_t* d_freq, float* d_sil) {
+    return guarded([&] {
+        VTF_CHECK(h && d_D && d_labels && d_freq && d_sil && N > 1 && k >= 2, VTF_E_ARG, "bad argument");
+        VTF_CHECK(k <= 64, VTF_E_LIMIT, "silhouette: more than 64 labels");
+        hipStream_t st = h->g.st;
+        int grid = waves_grid(N);
+        if (k <= 8)
+            k_silhouette<8><<<grid, 256, 0, st>>>(d_D, N, d_labels, k, d_freq, d_sil);
+        else if (k <= 16)
+            k_silhouette<16><<<grid, 256, 0, st>>>(d_D, N, d_labels, k, d_freq, d_sil);
+        else if (k <= 32)
+            k_silhouette<32><<<grid, 256, 0, st>>>(d_D, N, d_labels, k, d_freq, d_sil);
+        else
+            k_silhouette<64><<<grid, 256, 0, st>>>(d_D, N, d_labels, k, d_freq, d_sil);
+        VTF_HIP(hipGetLastError());
+    });
+}
+
+int vtf_cluster_sums(vtf_group_t h, const float* d_X, int64_t N, int64_t D, const int32_t* d_labels, int k,
+                     double* d_sums, double* d_sqnorm, int64_t* d_counts) {
+    return guarded([&] {
+        VTF_CHECK(h && d_X && d_labels && d_sums && d_sqnorm && d_counts && N > 0 && D > 0 && k > 0, VTF_E_ARG,
+                  "bad argument");
+        hipStream_t st = h->g.st;
+        VTF_HIP(hipMemsetAsync(d_sums, 0, (size_t)k * D * 8, st));
+        VTF_HIP(hipMemsetAsync(d_sqnorm, 0, (size_t)k * 8, st));
+        VTF_HIP(hipMemsetAsync(d_counts, 0, (size_t)k * 8, st));
+        k_csum<<<(unsigned)N, 256, 0, st>>>(d_X, N, (int)D, d_labels, d_sums, d_sqnorm,
+                                           (unsigned long long*)d_counts);
+        VTF_HIP(hipGetLastError());
+    });
+}
+
+int vtf_cluster_dist(vtf_group_t h, const float* d_X, int64_t N, int64_t D, const int32_t* d_labels, int k,
+                     const double* d_centroids, double* d_dsum) {
+    return guarded([&] {
+        VTF_CHECK(h && d_X && d_labels && d_centroids && d_dsum && N > 0 && D > 0 && k > 0, VTF_E_ARG,
+                  "bad argument");
+        VTF_HIP(hipMemsetAsync(d_dsum, 0, (size_t)k * 8, h->g.st));
+        k_cdist<<<waves_grid(N), 256, 0, h->g.st>>>(d_X, N, (int)D, d_labels, d_centroids, d_dsum);
+        VTF_HIP(hipGetLastError());
+    });
+}
+
+}  // extern "C"

@@ -50,6 +50,18 @@ SIGNATURES = {
     'vtf_vit_encode_crops': [_p, _p, _i32, _i32, _i64, _i64, _p, _i64, _p],
     'vtf_blob_from_crops': [_p, _i32, _i32, _i64, _i64, _p, _i64, _i32, _f32, _f32, _p, _p],
     'vtf_cosine_dedupe': [_p, _i64, _i64, _p, _p, _p],
+    'vtf_group_create': [_i32, _p],
+    'vtf_group_destroy': [_p],
+    'vtf_group_set_stream': [_p, _p],
+    'vtf_colstats': [_p, _p, _i64, _i64, _p, _p, _p],
+    'vtf_sqdist_rows': [_p, _p, _i64, _i64, _p, _i32, _p],
+    'vtf_kmeans_step': [_p, _p, _i64, _i64, _p, _i32, _p, _p, _p, _p],
+    'vtf_kmeans_average': [_p, _p, _p, _p, _i32, _i64, _p],
+    'vtf_center_dist': [_p, _p, _i64, _i64, _p, _p, _p],
+    'vtf_pairwise_euclidean': [_p, _p, _i64, _i64, _p],
+    'vtf_silhouette_samples': [_p, _p, _i64, _p, _i32, _p, _p],
+    'vtf_cluster_sums': [_p, _p, _i64, _i64, _p, _i32, _p, _p, _p],
+    'vtf_cluster_dist': [_p, _p, _i64, _i64, _p, _i32, _p, _p],
     'vtf_yolo_create': [_p, _i64, _i32, _i32, _p],
     'vtf_yolo_destroy': [_p],
     'vtf_yolo_set_stream': [_p, _p],

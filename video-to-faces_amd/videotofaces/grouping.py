@@ -1,9 +1,10 @@
 """Encoding and grouping (drop-in for src/videotofaces/grouping.py).
 
 classify (grouping.py:50-66) runs its cosine distances / argmin on the GPU
-(vtf_cosine_classify).  cluster_faces keeps sklearn's KMeans and scores on the host (the
-reference's own dependency, sklearn 1.7.2 here); the K-means / silhouette kernels are
-the next §8 rows.
+(vtf_cosine_classify).  cluster_faces (grouping.py:92-137) runs KMeans and the three
+scores per k on the GPU (videotofaces.kmeans.Grouper, sklearn-faithful); under
+torch.distributed the k sweep is sharded across ranks and the per-k labels
+and scores are all-gathered.
 """
 import math
 import os
@@ -82,19 +83,43 @@ def classify(X, R, classes, thr, log, paths, out_dir):
     return inds, classes
 
 
+def sweep_scores(X, k, random_state, grouper, prep=None):
+    """One k of cluster_faces (grouping.py:97-107): labels and (silhouette, CH, DB)."""
+    lb = grouper.kmeans(X, k, random_state=random_state, prep=prep)
+    return lb, (grouper.silhouette_score(X, lb), grouper.calinski_harabasz_score(X, lb),
+                grouper.davies_bouldin_score(X, lb))
+
+
+def cluster_sweep(X, clusters, random_state, compute=None):
+    """KMeans + scores for every k in `clusters`, in order.  With torch.distributed
+    initialised, rank r computes the k at positions i % world == r (each rank holds the
+    replicated X) and the results are all-gathered -- the parity-preserving sharding of
+    SURVEY.md §8e (no cross-rank reduction inside a fit)."""
+    import torch.distributed as dist
+    if compute is None:
+        from .kmeans import Grouper
+        g = Grouper()
+        prep = g.prepare(X)
+        compute = lambda k: sweep_scores(X, k, random_state, g, prep)  # noqa: E731
+    world = dist.get_world_size() if dist.is_available() and dist.is_initialized() else 1
+    rank = dist.get_rank() if world > 1 else 0
+    mine = {i: compute(k) for i, k in enumerate(clusters) if i % world == rank}
+    if world > 1:
+        parts = [None] * world
+        dist.all_gather_object(parts, {i: (np.asarray(lb), sc) for i, (lb, sc) in mine.items()})
+        for p in parts:
+            mine.update(p)
+    labels = [np.asarray(mine[i][0]) for i in range(len(clusters))]
+    scores = [(clusters[i],) + tuple(float(v) for v in mine[i][1]) for i in range(len(clusters))]
+    return labels, scores
+
+
 def cluster_faces(paths, X, cluster_params):
-    """grouping.py:92-137 (sklearn KMeans + silhouette / CH / DB on the host)."""
-    import sklearn.cluster
-    import sklearn.metrics
+    """grouping.py:92-137 with the KMeans / score sweep on the GPU (cluster_sweep)."""
     clusters, save_all, rstate, log, out_dir = cluster_params
     clusters = [c for c in clusters if c <= len(paths)]
     print('Clustering images into %s groups' % ', '.join([str(cl) for cl in clusters]))
-    labels = [sklearn.cluster.KMeans(n_clusters=k, random_state=rstate, n_init='auto').fit(X).labels_ for k in clusters]
-    scores = []
-    for i in range(len(clusters)):
-        scores.append((clusters[i], sklearn.metrics.silhouette_score(X, labels[i]),
-                       sklearn.metrics.calinski_harabasz_score(X, labels[i]),
-                       sklearn.metrics.davies_bouldin_score(X, labels[i])))
+    labels, scores = cluster_sweep(X, clusters, rstate)
     if log:
         with open(osp.join(out_dir, 'faces', 'log_clustering.csv'), 'w') as f:
             f.write('n_clusters,silhouette_score,calinski_harabasz_score,davies_bouldin_score\n')
@@ -105,6 +130,7 @@ def cluster_faces(paths, X, cluster_params):
         i = clusters.index(best_k)
         clusters, labels = [clusters[i]], [labels[i]]
         print('The number of groups chosen: %u' % best_k)
+    print('Grouped %u images into %s folders:' % (len(paths), '/'.join([str(cl) for cl in clusters])))
     img_dir = osp.dirname(osp.abspath(paths[0]))
     for i in range(len(clusters)):
         k = clusters[i]
@@ -113,6 +139,9 @@ def cluster_faces(paths, X, cluster_params):
             os.makedirs(osp.join(img_dir, sub, str(j)), exist_ok=True)
         for j in range(len(paths)):
             shutil.copyfile(paths[j], osp.join(img_dir, sub, str(labels[i][j]), osp.basename(paths[j])))
+        values, counts = np.unique(labels[i], return_counts=True)
+        print((sub + ': ' if sub else '') + ', '.join(['%u: %u' % (v, c) for v, c in zip(values, counts)]))
+    print()
     for p in paths:
         os.remove(p)
     return clusters, labels, scores
