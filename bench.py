@@ -43,7 +43,8 @@ def parse():
     ap.add_argument('--enc-precision', default='bf16', choices=['bf16', 'fp32'])
     ap.add_argument('--min-face-size', type=float, default=5.0)
     ap.add_argument('--pool', type=int, default=32, help='distinct synthetic frames per rank (cycled)')
-    ap.add_argument('--cpu-frames', type=int, default=6, help='frames in the bounded CPU-baseline sample')
+    ap.add_argument('--cpu-frames', type=int, default=None,
+                    help='frames in the bounded CPU-baseline sample (default 12 mtcnn / 32 yolo, ~10 s of CPU work)')
     ap.add_argument('--no-cpu-baseline', action='store_true')
     # box post-processing (detection.py:174-262): reference defaults except det_min_size,
     # because synthetic-weight detections are mostly < 50 px and would never reach the encoder
@@ -56,6 +57,8 @@ def parse():
         a.det_batch = 32 if yolo else 16
     if a.det_min_size is None:
         a.det_min_size = 50 if yolo else 0
+    if a.cpu_frames is None:
+        a.cpu_frames = 32 if yolo else 12
     return a
 
 
