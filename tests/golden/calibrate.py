@@ -114,8 +114,53 @@ def calibrate_yolo(n_frames=2):
     print('YOLO_CALIB =', synth.YOLO_CALIB)
 
 
+def calibrate_rcnn(n_frames=2):
+    """Gains for the RPN and RoI heads of the Faster R-CNN (rcnn.py:34-124) and the face-class
+    bias: RPN logits to std 2, RPN deltas to std 0.1, RoI deltas to std 0.5 (x0.1/x0.2 in
+    decode); face score = sigmoid(g*u + c) with ~8% of proposals over 0.05 and ~1% over 0.4."""
+    from oracle import rcnn as orc
+    fr = synth.make_frames(n_frames, seed=0)
+    synth.RCNN_CALIB['gain'] = {}
+    synth.RCNN_CALIB['face_bias'] = {}
+    p = synth.make_params('rcnn')
+    x, so, su = orc.preprocess(list(fr))
+    P = orc.params_t(p)
+    with torch.inference_mode():
+        xs = orc.fpn(P, orc.body(P, x))
+        regs, logs = zip(*[orc.rpn_head(P, t) for t in xs])
+    lg = torch.cat([t.flatten() for t in logs]).double()
+    rg = torch.cat([t.flatten() for t in regs]).double()
+    print('feature std per level', [round(float(t.std()), 3) for t in xs])
+    g_log = float('%.6g' % (2.0 / float(lg.std())))
+    g_reg = float('%.6g' % (0.1 / float(rg.std())))
+    synth.RCNN_CALIB['gain'] = {'rpn.log.weight': g_log, 'rpn.reg.weight': g_reg}
+    p = synth.make_params('rcnn')
+    P = orc.params_t(p)
+    with torch.inference_mode():
+        props, imidx = orc.rpn(P, xs, orc.priors(x.shape[2:]), su)
+        print('proposals', props.shape[0], 'median wh', np.median((props[:, 2:] - props[:, :2]).numpy(), 0))
+        f = orc.roi_maps(props, imidx, xs[:-1]).flatten(start_dim=1)
+        for i in range(2):
+            f = F.relu(F.linear(f, P['roi.fc.%d.weight' % i], P['roi.fc.%d.bias' % i]))
+        w = P['roi.cls.weight']
+        u = (f @ (w[0] - w[1])).double()
+        reg = F.linear(f, P['roi.reg.weight']).double()
+    q92, q99 = float(torch.quantile(u, 0.92)), float(torch.quantile(u, 0.99))
+    g = (math.log(0.4 / 0.6) - math.log(0.05 / 0.95)) / (q99 - q92)
+    c = math.log(0.05 / 0.95) - g * q92
+    synth.RCNN_CALIB['gain'].update({'roi.cls.weight': float('%.6g' % g),
+                                     'roi.reg.weight': float('%.6g' % (0.5 / float(reg.std())))})
+    synth.RCNN_CALIB['face_bias'] = {'roi.cls.bias': float('%.6g' % -c)}
+    p = synth.make_params('rcnn')
+    bx, sc, _ = orc.forward(p, list(fr))
+    print('per frame kept', [len(s) for s in sc], 'score>0.4', [int((s > 0.4).sum()) for s in sc])
+    print('RCNN_CALIB =', synth.RCNN_CALIB)
+
+
 if __name__ == '__main__':
-    if sys.argv[1:] == ['yolo']:
+    if sys.argv[1:] == ['rcnn']:
+        calibrate_rcnn()
+    elif sys.argv[1:] == ['yolo']:
         calibrate_yolo()
     else:
         main()

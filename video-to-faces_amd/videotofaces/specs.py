@@ -160,8 +160,34 @@ def vit_spec(dim=768, depth=12, img=128, patch=16):
     return s
 
 
+def rcnn_spec():
+    """FasterRCNN (detectors/rcnn.py:127-139): ResNet50 body (backbones/resnet.py:11-54,
+    BN eps 1e-5), FPN (rcnn.py:16-31, ConvUnits with bias and no BN), RPN (34-47), RoI head
+    (85-92)."""
+    s = _conv_unit('body.layers.0.0', 3, 64, 7, 7)
+    cin = 64
+    for li, (w, n) in enumerate(zip((64, 128, 256, 512), (3, 4, 6, 3))):
+        for b in range(n):
+            p = 'body.layers.%d.%d' % (li + 1, b)
+            stride = 2 if (b == 0 and li > 0) else 1
+            s += _conv_unit(p + '.u1', cin, w, 1, 1) + _conv_unit(p + '.u2', w, w, 3, 3)
+            s += _conv_unit(p + '.u3', w, w * 4, 1, 1)
+            if stride > 1 or cin != w * 4:
+                s += _conv_unit(p + '.downsample', cin, w * 4, 1, 1)
+            cin = w * 4
+    for i, c in enumerate((256, 512, 1024, 2048)):
+        s += _conv('fpn.conv_laterals.%d.conv' % i, c, 256, 1, 1)
+    for i in range(4):
+        s += _conv('fpn.conv_smooths.%d.conv' % i, 256, 256, 3, 3)
+    s += _conv('rpn.conv.conv', 256, 256, 3, 3) + _conv('rpn.log', 256, 3, 1, 1) + _conv('rpn.reg', 256, 12, 1, 1)
+    s += _lin('roi.fc.0', 256 * 7 * 7, 1024) + _lin('roi.fc.1', 1024, 1024)
+    s += _lin('roi.cls', 1024, 2) + _lin('roi.reg', 1024, 4)
+    return s
+
+
 SPECS = {
     'mtcnn': mtcnn_spec,
+    'rcnn': rcnn_spec,
     'facenet': facenet_spec,
     'yolo': yolo_spec,
     'vit_b': lambda: vit_spec(768, 12),
