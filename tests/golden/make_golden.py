@@ -75,6 +75,65 @@ def _tv_batched_nms(boxes, scores, idxs, thr):
     return _tv_nms(boxes + offsets[:, None], scores, thr)
 
 
+def _tv_roi_align(input, boxes, output_size, spatial_scale=1.0, sampling_ratio=-1, aligned=False):
+    # torchvision roi_align CPU kernel (roi_align_kernel.cpp), restated sample by sample with
+    # fp32 scalars (independent of oracle/rcnn.py's bin-vectorised restatement; the two
+    # cross-check in tests/test_oracle.py).
+    import math
+    f32 = np.float32
+    ph_n, pw_n = output_size
+    N, C, H, W = input.shape
+    fm = input.numpy()
+    bx = boxes.numpy().astype(np.float32)
+    out = np.zeros((bx.shape[0], C, ph_n, pw_n), np.float32)
+    off = f32(0.5) if aligned else f32(0)
+    sc = f32(spatial_scale)
+    for r in range(bx.shape[0]):
+        img = fm[int(bx[r, 0])]
+        sw, sh = f32(bx[r, 1] * sc - off), f32(bx[r, 2] * sc - off)
+        ew, eh = f32(bx[r, 3] * sc - off), f32(bx[r, 4] * sc - off)
+        rw, rh = f32(ew - sw), f32(eh - sh)
+        if not aligned:
+            rw, rh = max(rw, f32(1)), max(rh, f32(1))
+        bsh, bsw = f32(rh / f32(ph_n)), f32(rw / f32(pw_n))
+        gh = sampling_ratio if sampling_ratio > 0 else int(math.ceil(f32(rh / f32(ph_n))))
+        gw = sampling_ratio if sampling_ratio > 0 else int(math.ceil(f32(rw / f32(pw_n))))
+        count = f32(max(gh * gw, 1))
+        for ph in range(ph_n):
+            for pw in range(pw_n):
+                val = np.zeros(C, np.float32)
+                for iy in range(gh):
+                    y = f32(f32(sh + f32(f32(ph) * bsh)) + f32(f32(f32(iy + 0.5) * bsh) / f32(gh)))
+                    for ix in range(gw):
+                        x = f32(f32(sw + f32(f32(pw) * bsw)) + f32(f32(f32(ix + 0.5) * bsw) / f32(gw)))
+                        if y < -1.0 or y > H or x < -1.0 or x > W:
+                            w1 = w2 = w3 = w4 = f32(0)
+                            p1 = p2 = p3 = p4 = (0, 0)
+                        else:
+                            yy, xx = (f32(0) if y <= 0 else y), (f32(0) if x <= 0 else x)
+                            yl, xl = int(yy), int(xx)
+                            if yl >= H - 1:
+                                yh = yl = H - 1
+                                yy = f32(yl)
+                            else:
+                                yh = yl + 1
+                            if xl >= W - 1:
+                                xh = xl = W - 1
+                                xx = f32(xl)
+                            else:
+                                xh = xl + 1
+                            ly, lx = f32(yy - f32(yl)), f32(xx - f32(xl))
+                            hy, hx = f32(1.0 - float(ly)), f32(1.0 - float(lx))
+                            w1, w2, w3, w4 = f32(hy * hx), f32(hy * lx), f32(ly * hx), f32(ly * lx)
+                            p1, p2, p3, p4 = (yl, xl), (yl, xh), (yh, xl), (yh, xh)
+                        t = (((w1 * img[:, p1[0], p1[1]]).astype(np.float32) + (w2 * img[:, p2[0], p2[1]]))
+                             .astype(np.float32) + (w3 * img[:, p3[0], p3[1]])).astype(np.float32)
+                        t = (t + (w4 * img[:, p4[0], p4[1]])).astype(np.float32)
+                        val = (val + t).astype(np.float32)
+                out[r, :, ph, pw] = val / count
+    return torch.from_numpy(out)
+
+
 def load_ref():
     if 'ref_vtf' in sys.modules:
         return sys.modules['ref_vtf']
@@ -90,6 +149,7 @@ def load_ref():
     ops = types.ModuleType('torchvision.ops')
     ops.batched_nms = _tv_batched_nms
     ops.nms = _tv_nms
+    ops.roi_align = _tv_roi_align
     tv.ops = ops
     sys.modules['torchvision'] = tv
     sys.modules['torchvision.ops'] = ops
@@ -290,7 +350,64 @@ def gen_kmeans():
     print('kmeans', X.shape, 'best k', ks[int(np.argmax([s[0] for s in scores]))])
 
 
+def gen_rcnn():
+    """Faster R-CNN (rcnn.py:127-151) from the letterboxed tensor on, with the reference's
+    own modules; cv2.resize is the build's INTER_LINEAR restatement (parity-unpinned step,
+    pinned here by a hash of the resized images) and roi_align the shim above.
+    Also: RPN head maps of a small input (conv-stack parity at tight tolerance) and
+    roi_align on random maps with edge-case boxes."""
+    import hashlib
+    load_ref()
+    r = importlib.import_module('ref_vtf.detectors.rcnn')
+    prep = importlib.import_module('ref_vtf.detectors.operations.prep')
+    bbox = importlib.import_module('ref_vtf.detectors.operations.bbox')
+    sys.path.insert(0, ROOT)
+    from oracle import yolo as oy
+    net = _load(r.FasterRCNN('cpu'), synth.make_params('rcnn'))
+    out = {}
+    g = torch.Generator().manual_seed(17)
+    with torch.inference_mode():
+        xs = torch.randn(1, 3, 64, 96, generator=g)
+        fm = net.fpn(net.body(xs))
+        for i, f in enumerate(fm):
+            reg, log = net.rpn.head(f)
+            out['small_reg%d' % i] = reg.numpy()
+            out['small_log%d' % i] = log.numpy()
+        out['small_x'] = xs.numpy()
+        # roi_align on random maps (aligned, adaptive grid); boxes cover interior, edges,
+        # outside the map, degenerate and large
+        fmap = torch.randn(2, 16, 20, 24, generator=g)
+        rois = torch.tensor([[0, 3.2, 4.7, 40.1, 33.3], [1, 0, 0, 96, 80], [0, -10, -8, 5, 6],
+                             [1, 90, 70, 130, 100], [0, 10, 10, 10.5, 30], [1, 20, 15, 20, 15],
+                             [0, 1.3, 2.9, 79.8, 77.7], [1, 50.5, 20.25, 60.75, 41]], dtype=torch.float32)
+        out['ra_fmap'], out['ra_rois'] = fmap.numpy(), rois.numpy()
+        out['ra_out'] = _tv_roi_align(fmap, rois, (7, 7), 0.25, 0, True).numpy()
+    frames = synth.make_frames(2, seed=0)
+    resized, szo, szu = [], [], []
+    for f in frames:
+        sz = f.shape[:2]
+        scl = min(800 / min(sz), 1333 / max(sz))
+        n = int(sz[0] * scl + 0.5), int(sz[1] * scl + 0.5)
+        resized.append(oy.resize_linear_u8_hw(f, n))
+        szo.append(sz)
+        szu.append(n)
+    with torch.inference_mode():
+        ts = prep.to_tensors(resized, 'cpu', 'imagenet', 'imagenet', True)
+        x = prep.pad_and_batch(ts, 32)
+        pri = r.get_priors(x.shape[2:], net.bases, 'cpu', 'corner', 'as_is', concat=False)
+        fm = net.fpn(net.body(x))
+        p, imidx = net.rpn(fm, pri, szu)
+        out['proposals'], out['prop_imidx'] = p.numpy().copy(), imidx.numpy().copy()
+        b, s, c = net.roi(p, imidx, fm[:-1], net.strides[:-1], szu)
+        b = bbox.scale_boxes(b, szo, szu)
+    out.update(resized_sha256=np.frombuffer(hashlib.sha256(np.stack(resized).tobytes()).digest(), np.uint8),
+               szo=np.array(szo), szu=np.array(szu), counts=np.array([len(t) for t in s], np.int64),
+               boxes=torch.cat(b).numpy(), scores=torch.cat(s).numpy(), classes=torch.cat(c).numpy())
+    np.savez_compressed(os.path.join(HERE, 'rcnn.npz'), **out)
+    print('rcnn', {k: v.shape for k, v in out.items()}, 'counts', out['counts'])
+
+
 if __name__ == '__main__':
-    which = sys.argv[1:] or ['mtcnn', 'facenet', 'vit', 'grouping', 'yolo', 'kmeans']
+    which = sys.argv[1:] or ['mtcnn', 'facenet', 'vit', 'grouping', 'yolo', 'kmeans', 'rcnn']
     for w in which:
         globals()['gen_' + w]()

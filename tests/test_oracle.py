@@ -180,3 +180,45 @@ def test_silhouette_restatement_vs_sklearn(km):
     sil = silhouette_samples(X, g['labels'][6])
     np.testing.assert_array_equal(sil, g['sil_k8'])
     assert float(np.mean(sil)) == g['scores'][6][0]
+
+
+@pytest.fixture(scope='module')
+def grc():
+    return np.load(os.path.join(GOLDEN, 'rcnn.npz'))
+
+
+def test_oracle_roi_align_vs_golden(grc):
+    """oracle/rcnn.py's bin-vectorised torchvision roi_align restatement == the golden shim's
+    sample-by-sample one (edge cases: outside the map, degenerate, large boxes)."""
+    from oracle import rcnn as orc
+    out = orc.roi_align(torch.from_numpy(grc['ra_fmap']), torch.from_numpy(grc['ra_rois']), 7, 0.25, True)
+    np.testing.assert_array_equal(out.numpy(), grc['ra_out'])
+
+
+def test_oracle_rcnn_small_heads_vs_golden(grc):
+    from oracle import rcnn as orc
+    from videotofaces import synth
+    P = orc.params_t(synth.make_params('rcnn'))
+    with torch.inference_mode():
+        fm = orc.fpn(P, orc.body(P, torch.from_numpy(grc['small_x'])))
+        for i, f in enumerate(fm):
+            reg, log = orc.rpn_head(P, f)
+            np.testing.assert_allclose(reg.numpy(), grc['small_reg%d' % i], rtol=0,
+                                       atol=1e-5 * np.abs(grc['small_reg%d' % i]).max())
+            np.testing.assert_allclose(log.numpy(), grc['small_log%d' % i], rtol=0,
+                                       atol=1e-5 * np.abs(grc['small_log%d' % i]).max())
+
+
+def test_oracle_rcnn_e2e_vs_golden(grc):
+    """oracle/rcnn.py end to end (preprocess restated cv2 resize, ResNet50/FPN, RPN, RoIAlign,
+    RoI head, NMS, scale_boxes) against the reference FasterRCNN on the same weights."""
+    import hashlib
+    from oracle import rcnn as orc
+    from videotofaces import synth
+    fr = synth.make_frames(2, seed=0)
+    rs = [orc.resize_linear_u8_hw(f, orc.used_size(*f.shape[:2])) for f in fr]
+    assert hashlib.sha256(np.stack(rs).tobytes()).digest() == grc['resized_sha256'].tobytes()
+    b, s, c = orc.forward(synth.make_params('rcnn'), list(fr))
+    np.testing.assert_array_equal([len(t) for t in s], grc['counts'])
+    np.testing.assert_allclose(np.concatenate(b), grc['boxes'], rtol=0, atol=1e-3)
+    np.testing.assert_allclose(np.concatenate(s), grc['scores'], rtol=0, atol=1e-5)
