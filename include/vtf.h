@@ -34,6 +34,7 @@ typedef struct vtf_facenet_s* vtf_facenet_t;
 typedef struct vtf_vit_s* vtf_vit_t;
 typedef struct vtf_yolo_s* vtf_yolo_t;
 typedef struct vtf_group_s* vtf_group_t;
+typedef struct vtf_rcnn_s* vtf_rcnn_t;
 
 /* ---------------------------------------------------------------- MTCNN detector
  * Replaces RealMTCNN / MTCNN.forward (src/videotofaces/detectors/mtcnn.py:167-252,
@@ -163,6 +164,43 @@ int vtf_yolo_postprocess(vtf_yolo_t h, const float* d_map0, const float* d_map1,
  * accumulated ms, launches, algorithmic FLOPs and frames since the last call; enable != 0
  * turns timing on for the following calls. */
 int vtf_yolo_profile(vtf_yolo_t h, int enable, double* out_ms, int64_t* out_launches, double* out_flops,
+                     int64_t* out_frames);
+
+/* ---------------------------------------------------------------- Faster R-CNN detector
+ * Replaces AnimeFRCNN / FasterRCNN.forward (src/videotofaces/detectors/rcnn.py:127-177),
+ * called by detection.py:131 `detout = model(frames)` for style='anime'.
+ * params: fp32, reference state_dict order minus num_batches_tracked (specs.py rcnn_spec,
+ *         41,401,301 floats).  precision 0 = fp32 (parity), 1 = bf16 operands/activations. */
+int vtf_rcnn_create(const float* params, int64_t n_params, int device, int precision, vtf_rcnn_t* out);
+int vtf_rcnn_destroy(vtf_rcnn_t h);
+int vtf_rcnn_set_stream(vtf_rcnn_t h, void* hip_stream);
+/* frames as in vtf_mtcnn_detect.  Output (host): boxes [total,4] (x1,y1,x2,y2 in frame pixels),
+ * scores [total], counts[B] (<= 100 each), per image in the reference's order (score desc).
+ * counts[b] = -1 for images after the last one holding an RPN proposal: the reference returns
+ * only max(imidx)+1 lists (rcnn.py:111).  Classes are all 0.  VTF_E_CAPACITY as in mtcnn. */
+int vtf_rcnn_detect(vtf_rcnn_t h, const uint8_t* frames, int frames_on_device, int B, int H, int W,
+                    int64_t frame_stride, int64_t row_stride, float* out_boxes, float* out_scores,
+                    int32_t* out_counts, int64_t cap, int64_t* out_total);
+/* resize_cv2 keep-ratio size for resize=(800, 1333) (prep.py:71-74) and the x32 padded net
+ * input: {h, w, Hp, Wp}. */
+int vtf_rcnn_input_size(int H, int W, int* out4);
+/* Parity entries.  preprocess (prep.py:12-92, imagenet mean/std) -> d_out NHWC fp32
+ * [B,Hp,Wp,8] (channels 3..7 zero).  rpn_heads: body + FPN + RPN head on d_x NCHW fp32
+ * [B,3,Hp,Wp] -> per level l (strides 4..64) NHWC fp32 [B,h_l,w_l,15]: 3 logits
+ * (RegionProposalNetwork.log) then 3 x 4 deltas (.reg), rcnn.py:42-47. */
+int vtf_rcnn_preprocess(vtf_rcnn_t h, const uint8_t* d_frames, int B, int H, int W, int64_t frame_stride,
+                        int64_t row_stride, float* d_out);
+int vtf_rcnn_rpn_heads(vtf_rcnn_t h, const float* d_x, int B, int Hp, int Wp, float* d_head0, float* d_head1,
+                       float* d_head2, float* d_head3, float* d_head4);
+/* RPN proposals of the last detect call (rcnn.py:82): host [n,5] (image, x1, y1, x2, y2). */
+int vtf_rcnn_proposals(vtf_rcnn_t h, float* out, int64_t cap, int64_t* out_n);
+/* torchvision.ops.roi_align(fmap, rois, (7,7), spatial_scale, sampling_ratio=0, aligned=True)
+ * as roi.py:31 calls it: d_fmap NHWC fp32 [N,H,W,C], d_rois fp32 [R,5] (image, x1, y1, x2, y2)
+ * -> d_out NHWC fp32 [R,7,7,C]. */
+int vtf_roi_align(const float* d_fmap, int N, int H, int W, int C, const float* d_rois, int64_t R,
+                  float spatial_scale, float* d_out, void* hip_stream);
+/* Timing of the body + FPN + RPN-head conv stack, as vtf_yolo_profile. */
+int vtf_rcnn_profile(vtf_rcnn_t h, int enable, double* out_ms, int64_t* out_launches, double* out_flops,
                      int64_t* out_frames);
 
 /* ---------------------------------------------------------------- grouping: K-means, scores

@@ -203,12 +203,20 @@ __global__ __launch_bounds__(256) void k_conv(ConvParams p) {
                 if (p.bias) v = v + bias;
                 if (p.alpha) v = fmaf(v, al, be);
                 if (p.scale != 1.f) v = v * p.scale;
-                if (res && !p.res_post) v = v + to_f(res[m * p.res_cstride + c]);
+                int64_t ridx = m * p.res_cstride + c;
+                if (p.res_up2) {
+                    int ow = (int)(m % p.OW);
+                    int64_t t = m / p.OW;
+                    int oh = (int)(t % p.OH);
+                    int64_t n = t / p.OH;
+                    ridx = ((n * (p.OH >> 1) + (oh >> 1)) * (p.OW >> 1) + (ow >> 1)) * p.res_cstride + c;
+                }
+                if (res && !p.res_post) v = v + to_f(res[ridx]);
                 if (p.relu) v = fmaxf(v, 0.f);
                 if (p.leaky) v = v > 0.f ? v : v * p.slope;
                 if (p.prelu) v = v > 0.f ? v : p.prelu[c] * v;
                 if (p.gelu) v = 0.5f * v * (1.0f + erff(v * 0.70710678118654752f));
-                if (res && p.res_post) v = v + to_f(res[m * p.res_cstride + c]);
+                if (res && p.res_post) v = v + to_f(res[ridx]);
                 if (p.up2) {
                     int ow = (int)(m % p.OW);
                     int64_t t = m / p.OW;
@@ -253,6 +261,7 @@ void launch_conv(const ConvParams& p, bool bf16, hipStream_t st) {
     VTF_CHECK(p.Cin % 8 == 0, VTF_E_ARG, "conv: Cin must be a multiple of 8 (pad the input)");
     VTF_CHECK(p.in_cstride == 0 || (p.in_cstride >= p.Cin && p.in_cstride % 8 == 0), VTF_E_ARG,
               "conv: bad input channel stride");
+    VTF_CHECK(!p.res_up2 || (p.OH % 2 == 0 && p.OW % 2 == 0), VTF_E_ARG, "conv: half-resolution residual needs even OH/OW");
     if (bf16)
         launch_t<__bf16>(p, st);
     else

@@ -20,6 +20,8 @@ struct ConvParams {
     int res_post;        // residual added AFTER the activation (Darknet ResBlock y + x, yolo.py:28-31)
     int up2;             // write each output pixel to a 2x2 block of a (2*OH, 2*OW) tensor
                          // (F.interpolate(scale_factor=2) nearest, yolo.py:87,91)
+    int res_up2;         // residual read at half resolution (nearest x2 upsample of a [N,OH/2,OW/2]
+                         // map: the FPN top-down add, rcnn.py:26-27)
     int in_cstride;      // input channel stride (0 = Cin): read a channel slice of a concat buffer
     int out_f32;         // output is fp32 whatever the operand precision (detector heads)
     int64_t M;           // N*OH*OW

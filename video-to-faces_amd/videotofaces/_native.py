@@ -72,6 +72,16 @@ SIGNATURES = {
     'vtf_yolo_postprocess': [_p, _p, _p, _p, _i32, _i32, _i32, _p, _p, _p, _i64, _p],
     'vtf_yolo_profile': [_p, _i32, _p, _p, _p, _p],
     'vtf_cosine_classify': [_p, _i64, _p, _i64, _i64, _p, _p, _p],
+    'vtf_rcnn_create': [_p, _i64, _i32, _i32, _p],
+    'vtf_rcnn_destroy': [_p],
+    'vtf_rcnn_set_stream': [_p, _p],
+    'vtf_rcnn_detect': [_p, _p, _i32, _i32, _i32, _i32, _i64, _i64, _p, _p, _p, _i64, _p],
+    'vtf_rcnn_input_size': [_i32, _i32, _p],
+    'vtf_rcnn_preprocess': [_p, _p, _i32, _i32, _i32, _i64, _i64, _p],
+    'vtf_rcnn_rpn_heads': [_p, _p, _i32, _i32, _i32, _p, _p, _p, _p, _p],
+    'vtf_rcnn_proposals': [_p, _p, _i64, _p],
+    'vtf_roi_align': [_p, _i32, _i32, _i32, _i32, _p, _i64, _f32, _p, _p],
+    'vtf_rcnn_profile': [_p, _i32, _p, _p, _p, _p],
 }
 _RESTYPE = {'vtf_last_error': _c.c_char_p}
 
