@@ -17,6 +17,7 @@ import argparse
 import json
 import os
 import sys
+import threading
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
@@ -43,6 +44,7 @@ def parse():
     ap.add_argument('--enc-precision', default='bf16', choices=['bf16', 'fp32'])
     ap.add_argument('--min-face-size', type=float, default=5.0)
     ap.add_argument('--pool', type=int, default=32, help='distinct synthetic frames per rank (cycled)')
+    ap.add_argument('--lanes', type=int, default=2, help='concurrent det-batch pipelines (threads + HIP streams) per GPU')
     ap.add_argument('--cpu-frames', type=int, default=None,
                     help='frames in the bounded CPU-baseline sample (default 12 mtcnn / 32 yolo, ~10 s of CPU work)')
     ap.add_argument('--no-cpu-baseline', action='store_true')
@@ -125,31 +127,60 @@ def main():
     frames_np = synth.make_frames(pool_n, H, W, seed=1000 + rank)
     frames = torch.from_numpy(frames_np).to(dev)
     yolo = args.det_model == 'yolo'
-    det = YOLOv3(dev, precision=args.det_precision) if yolo else MTCNN(dev)
-    enc = InceptionResnetV1(dev, precision=args.enc_precision)
+    # `lanes` independent (detector, encoder, HIP stream) sets work on alternate det-batches
+    # from host threads (the ctypes calls release the GIL): one lane's host syncs and small
+    # stage-2/3 kernels overlap the other lane's pyramid kernel.  Batches stay whole and
+    # independent, so per-batch results are exactly the single-lane results.
+    L = max(1, args.lanes)
+    dets = [YOLOv3(dev, precision=args.det_precision) if yolo else MTCNN(dev) for _ in range(L)]
+    encs = [InceptionResnetV1(dev, precision=args.enc_precision) for _ in range(L)]
+    streams = [torch.cuda.Stream(dev) for _ in range(L)]
+    torch.cuda.synchronize(dev)
 
-    def step(i):
+    def step(lane, i):
         j = (i * B) % pool_n
         fb = frames[j:j + B]
+        det, enc = dets[lane], encs[lane]
         res = normalize_detout(det(fb)) if yolo else det(fb, args.min_face_size)
         crops = boxes_to_crops(res, (H, W), **det_params(args))
         embs = [enc.encode_crops(fb, crops[k:k + args.enc_batch]) for k in range(0, crops.shape[0], args.enc_batch)]
         return embs, crops.shape[0], sum(r.shape[0] for r in res)
 
-    for i in range(args.warmup):
-        step(i)
+    def run(first, n):
+        """steps first..first+n-1, step i on lane i % L; returns per-step results in order."""
+        out = [None] * n
+        errs = []
+
+        def lane_fn(lane):
+            try:
+                with torch.cuda.stream(streams[lane]):
+                    for k in range(lane, n, L):
+                        out[k] = step(lane, first + k)
+            except BaseException as e:  # surfaced after join
+                errs.append(e)
+        ths = [threading.Thread(target=lane_fn, args=(l,)) for l in range(L)]
+        for t in ths:
+            t.start()
+        for t in ths:
+            t.join()
+        if errs:
+            raise errs[0]
+        for s in streams:
+            s.synchronize()
+        return out
+
+    run(0, max(args.warmup, L))
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
-    det.profile(True)
+    for d in dets:
+        d.profile(True)
     t0 = time.perf_counter()
-    faces, dets, embs = 0, 0, []
-    for i in range(args.steps):
-        e, nf, nd = step(args.warmup + i)
-        embs.extend(e)
-        faces += nf
-        dets += nd
+    results = run(args.warmup, args.steps)
+    embs = [e for r in results for e in r[0]]
+    faces = sum(r[1] for r in results)
+    dets_n = sum(r[2] for r in results)
     local_emb = torch.cat(embs) if embs else torch.zeros((0, 512), device=dev)
     if world > 1:
         from videotofaces.parallel import all_gather_rows
@@ -161,7 +192,11 @@ def main():
         dist.barrier()
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t0
-    k_ms, k_launches, k_flops, k_frames = det.profile(False)
+    k_ms = k_launches = k_flops = k_frames = 0
+    for d in dets:
+        a, b_, c, e = d.profile(False)
+        k_ms, k_launches, k_flops, k_frames = k_ms + a, k_launches + b_, k_flops + c, k_frames + e
+    dets = dets_n
     tot = torch.tensor([faces, dets, k_frames], dtype=torch.float64, device=dev)
     el = torch.tensor([elapsed], dtype=torch.float64, device=dev)
     if world > 1:
@@ -204,6 +239,7 @@ def main():
                                    % (wl, B, args.enc_batch, args.det_min_score, args.det_min_size,
                                       args.det_min_border),
                        'det_batch': B, 'enc_batch': args.enc_batch, 'frames_per_step_per_gpu': B,
+                       'lanes': L,
                        'parallelism': 'dp%d (frame-sharded, RCCL all-gather of embeddings)' % world},
             'frames_per_s': round(world * args.steps * B / elapsed, 2),
             'faces_per_frame': round(faces_all / max(1.0, world * args.steps * B), 3),

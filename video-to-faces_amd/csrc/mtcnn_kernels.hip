@@ -487,6 +487,109 @@ void launch_crop_nhwc(const uint8_t* frames, int64_t frame_stride, int64_t row_s
                                                                   S, out, err);
 }
 
+// Fused candidate front end: _get_cropped_candidates (mtcnn.py:153-163) + conv1 (3->28/32,
+// 3x3) + PReLU + MaxPool2d(3, 2, ceil_mode) of RNet (S=24) / ONet (S=48), one candidate per
+// workgroup.  The S x S crop is adaptive-pooled from the uint8 frame straight into LDS
+// (bit-exact bins), conv1 runs on fp32 MFMA with the true K = 27 (im2col order (c, ky, kx),
+// no channel padding), and the pool reads the conv1 band from LDS: only the pooled
+// [n, P, P, 32] map reaches HBM (P = 11 / 23).  Conv rows are produced in bands of 2*PB+1.
+// w1: [28][32] (k, co; row 27 and channels >= Cout zero); b1, a1: [32].
+template <int S, int PB>
+__global__ __launch_bounds__(256) void k_cand_front(const uint8_t* __restrict__ frames, int64_t frame_stride,
+                                                    int64_t row_stride, int H, int W, const float4* __restrict__ boxes,
+                                                    const int32_t* __restrict__ img, const float* __restrict__ w1,
+                                                    const float* __restrict__ b1, const float* __restrict__ a1,
+                                                    float* __restrict__ out, int32_t* __restrict__ err) {
+    constexpr int O = S - 2;                // conv1 output side
+    constexpr int P = (O - 3 + 1) / 2 + 1;  // ceil-mode pool output side
+    constexpr int BR = 2 * PB + 1;          // conv rows per band
+    __shared__ float crop[3 * S * S];
+    __shared__ float cv[32 * BR * O];
+    const int64_t k = blockIdx.x;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, lr = lane & 15, lk = lane >> 4;
+    float* o = out + k * (P * P * 32);
+    int y0, x0, hc, wc;
+    if (!crop_rect(boxes[k], H, W, y0, x0, hc, wc)) {
+        // the reference skips this box and then fails indexing (IndexError): flag it
+        if (tid == 0) atomicAdd(err, 1);
+        for (int i = tid; i < P * P * 32; i += 256) o[i] = 0.f;
+        return;
+    }
+    const uint8_t* fr = frames + (int64_t)img[k] * frame_stride;
+    for (int i = tid; i < 3 * S * S; i += 256) {
+        const int c = i / (S * S), rq = i - c * (S * S);
+        crop[i] = crop_value(fr, row_stride, c, rq / S, rq - (rq / S) * S, y0, x0, hc, wc, S);
+    }
+    float wb[7][2];
+#pragma unroll
+    for (int s = 0; s < 7; s++) {
+        wb[s][0] = w1[(4 * s + lk) * 32 + lr];
+        wb[s][1] = w1[(4 * s + lk) * 32 + 16 + lr];
+    }
+    const float bb0 = b1[lr], bb1 = b1[16 + lr], aa0 = a1[lr], aa1 = a1[16 + lr];
+    __syncthreads();
+    for (int pr0 = 0; pr0 < P; pr0 += PB) {
+        const int cr0 = 2 * pr0;
+        const int ncr = min(BR, O - cr0);
+        const int npos = ncr * O;
+        const int nf = (npos + 15) / 16;
+        for (int f = wave; f < nf; f += 4) {
+            const int p = min(f * 16 + lr, npos - 1);
+            const int y = cr0 + p / O, x = p % O;
+            f32x4 c0 = {0.f, 0.f, 0.f, 0.f}, c1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int s = 0; s < 7; s++) {
+                const int kk = 4 * s + lk;
+                const int kc = min(kk, 26);
+                const int c = kc / 9, r = kc - 9 * c;
+                const float av = kk < 27 ? crop[c * S * S + (y + r / 3) * S + x + r % 3] : 0.f;
+                c0 = __builtin_amdgcn_mfma_f32_16x16x4f32(av, wb[s][0], c0, 0, 0, 0);
+                c1 = __builtin_amdgcn_mfma_f32_16x16x4f32(av, wb[s][1], c1, 0, 0, 0);
+            }
+#pragma unroll
+            for (int i = 0; i < 4; i++) {
+                const int q = f * 16 + 4 * lk + i;
+                if (q < npos) {
+                    cv[lr * BR * O + q] = prelu(c0[i] + bb0, aa0);
+                    cv[(16 + lr) * BR * O + q] = prelu(c1[i] + bb1, aa1);
+                }
+            }
+        }
+        __syncthreads();
+        const int npr = min(PB, P - pr0);
+        for (int i = tid; i < npr * P * 32; i += 256) {
+            const int c = i & 31, t = i >> 5;
+            const int px = t % P, pyl = t / P;
+            float m = -3.402823466e38f;
+            for (int dy = 0; dy < 3; dy++) {
+                const int yy = 2 * (pr0 + pyl) + dy;
+                if (yy >= O) break;
+                for (int dx = 0; dx < 3; dx++) {
+                    const int xx = 2 * px + dx;
+                    if (xx >= O) break;
+                    m = fmaxf(m, cv[c * BR * O + (yy - cr0) * O + xx]);
+                }
+            }
+            o[((pr0 + pyl) * P + px) * 32 + c] = m;
+        }
+        __syncthreads();
+    }
+}
+
+int cand_front_side(bool onet) { return onet ? 23 : 11; }
+
+void launch_cand_front(bool onet, const uint8_t* frames, int64_t frame_stride, int64_t row_stride, int H, int W,
+                       const float4* boxes, const int32_t* img, int64_t n, const float* w1, const float* b1,
+                       const float* a1, float* out, int32_t* err, hipStream_t st) {
+    if (n <= 0) return;
+    if (onet)
+        k_cand_front<48, 3><<<(unsigned)n, 256, 0, st>>>(frames, frame_stride, row_stride, H, W, boxes, img, w1, b1,
+                                                          a1, out, err);
+    else
+        k_cand_front<24, 6><<<(unsigned)n, 256, 0, st>>>(frames, frame_stride, row_stride, H, W, boxes, img, w1, b1,
+                                                          a1, out, err);
+}
+
 // heads: x [n, D] -> softmax(x W1^T + b1)[:, 1], x W2^T + b2 (4), optional x W3^T + b3 (10).
 // One wave per candidate; lanes split D, wave-reduced.  RNet's softmax is over the last dim
 // (torch multiplies by the reciprocal sum), ONet's too.

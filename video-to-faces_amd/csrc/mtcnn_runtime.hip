@@ -41,6 +41,7 @@ struct Mtcnn {
         const float *w, *b, *a;
     };
     std::vector<CL> rl, ol;
+    const float* fw[2] = {nullptr, nullptr};  // conv1 of RNet / ONet for k_cand_front: [28][32]
     const float *rh1w, *rh1b, *rh2w, *rh2b;                    // rnet dense5_1 / dense5_2
     const float *oh1w, *oh1b, *oh2w, *oh2b, *oh3w, *oh3b;      // onet dense6_1 / 6_2 / 6_3
     Arena ar;
@@ -171,6 +172,19 @@ static void build_weights(Mtcnn& m, const float* params, int64_t n_params) {
             layer(22, 64, 64, 128, 3, true)};
     m.ol = {layer(29, 3, 8, 32, 3, false),  layer(32, 32, 32, 64, 3, false), layer(35, 64, 64, 64, 3, false),
             layer(38, 64, 64, 128, 2, false), layer(41, 128, 128, 256, 3, true)};
+    // conv1 of RNet / ONet as [k = (c, ky, kx)][co] (k = 27 and co >= Cout zero) for the
+    // fused candidate front end (k_cand_front)
+    for (int net = 0; net < 2; net++) {
+        const int wi = net ? 29 : 13, cout = net ? 32 : 28;
+        std::vector<float> w(28 * 32, 0.f);
+        for (int co = 0; co < cout; co++)
+            for (int kk = 0; kk < 27; kk++) w[kk * 32 + co] = raw[wi][(size_t)co * 27 + kk];
+        float* d = nullptr;
+        VTF_HIP(hipMalloc(&d, w.size() * 4));
+        VTF_HIP(hipMemcpy(d, w.data(), w.size() * 4, hipMemcpyHostToDevice));
+        m.allocs.push_back(d);
+        m.fw[net] = d;
+    }
     auto dev = [&](int i) { return m.d_w + off[i]; };
     m.rh1w = dev(25); m.rh1b = dev(26); m.rh2w = dev(27); m.rh2b = dev(28);
     m.oh1w = dev(44); m.oh1b = dev(45); m.oh2w = dev(46); m.oh2b = dev(47); m.oh3w = dev(48); m.oh3b = dev(49);
@@ -179,7 +193,9 @@ static void build_weights(Mtcnn& m, const float* params, int64_t n_params) {
 // RNet / ONet on NHWC fp32 crops x0 [n,S,S,8] (mtcnn.py:58-76 / 101-121), layer by layer on
 // the MFMA conv kernel; pools are torch MaxPool2d(ceil_mode=True).
 enum RSlot { S_RA = 70, S_RB = 71 };  // nms_multi owns slots 40-61
-static void run_candidates(Mtcnn& m, bool onet, const float* x0, int64_t n, float4* reg, float* lm, float* prob) {
+// first = 1: x0 is the fused front end's pooled conv1 map [n,P,P,32] (k_cand_front)
+static void run_candidates(Mtcnn& m, bool onet, const float* x0, int64_t n, float4* reg, float* lm, float* prob,
+                           int first = 0) {
     if (n <= 0) return;
     const int S = onet ? 48 : 24;
     const auto& Ls = onet ? m.ol : m.rl;
@@ -191,7 +207,11 @@ static void run_candidates(Mtcnn& m, bool onet, const float* x0, int64_t n, floa
     float* Y = m.ar.get<float>(S_RB, big);
     const float* cur = x0;
     int H = S, W = S, C = 8;
-    for (size_t li = 0; li < Ls.size(); li++) {
+    if (first == 1) {
+        H = W = cand_front_side(onet);
+        C = 32;
+    }
+    for (size_t li = first; li < Ls.size(); li++) {
         const auto& L = Ls[li];
         float* out = (cur == X) ? Y : X;
         ConvParams p{};
@@ -411,9 +431,10 @@ static void detect(Mtcnn& m, const uint8_t* frames, int on_dev, int B, int H, in
     int32_t* err = m.ar.get<int32_t>(S_ERR, 1);
     VTF_HIP(hipMemsetAsync(err, 0, 4, st));
     {
-        float* x0 = m.ar.get<float>(S_CROP, (size_t)k2 * 24 * 24 * 8);
-        launch_crop_nhwc(fr, fstride, rstride, H, W, b1, i1, k2, 24, x0, err, st);
-        run_candidates(m, false, x0, k2, reg, nullptr, prob);
+        const int P = cand_front_side(false);
+        float* x0 = m.ar.get<float>(S_CROP, (size_t)k2 * P * P * 32);
+        launch_cand_front(false, fr, fstride, rstride, H, W, b1, i1, k2, m.fw[0], m.rl[0].b, m.rl[0].a, x0, err, st);
+        run_candidates(m, false, x0, k2, reg, nullptr, prob, 1);
     }
     int32_t nerr = 0;
     d2h_sync(&nerr, err, 4, st);
@@ -436,9 +457,10 @@ static void detect(Mtcnn& m, const uint8_t* frames, int on_dev, int B, int H, in
     float* lm = m.ar.get<float>(S_LM, k3 * 10);
     VTF_HIP(hipMemsetAsync(err, 0, 4, st));
     {
-        float* x0 = m.ar.get<float>(S_CROP, (size_t)k3 * 48 * 48 * 8);
-        launch_crop_nhwc(fr, fstride, rstride, H, W, b1, i1, k3, 48, x0, err, st);
-        run_candidates(m, true, x0, k3, reg, lm, prob);
+        const int P = cand_front_side(true);
+        float* x0 = m.ar.get<float>(S_CROP, (size_t)k3 * P * P * 32);
+        launch_cand_front(true, fr, fstride, rstride, H, W, b1, i1, k3, m.fw[1], m.ol[0].b, m.ol[0].a, x0, err, st);
+        run_candidates(m, true, x0, k3, reg, lm, prob, 1);
     }
     d2h_sync(&nerr, err, 4, st);
     VTF_CHECK(nerr == 0, VTF_E_DEGENERATE,
