@@ -31,18 +31,15 @@ struct PNetOut {
     int dbg;  // phase-skip mask for profiling (env VTF_PNET_DEBUG): 1 fill, 2 conv1, 4 conv2, 8 conv3
 };
 
-void launch_resample(const uint8_t* frames, int64_t frame_stride, int64_t row_stride, int B, int H, int W, int lh,
-                     int lw, float* out, hipStream_t st);
+void launch_sat(const uint8_t* frames, int64_t frame_stride, int64_t row_stride, int B, int H, int W, int4* sat,
+                hipStream_t st);
+void launch_resample_sat(const int4* sat, int B, int H, int W, int lh, int lw, float* out, hipStream_t st);
 void launch_pnet(bool dense, const uint8_t* frames, int64_t frame_stride, int64_t row_stride, int H, int W,
                  const PNetLevel* d_levels, int n_levels, int64_t total_tiles, const PNetW& w, const PNetOut& o,
                  uint32_t* d_tile_ctr, hipStream_t st);
-void launch_crop_nhwc(const uint8_t* frames, int64_t frame_stride, int64_t row_stride, int H, int W,
-                      const float4* boxes, const int32_t* img, int64_t n, int S, float* out, int32_t* err,
-                      hipStream_t st);
 int cand_front_side(bool onet);
-void launch_cand_front(bool onet, const uint8_t* frames, int64_t frame_stride, int64_t row_stride, int H, int W,
-                       const float4* boxes, const int32_t* img, int64_t n, const float* w1, const float* b1,
-                       const float* a1, float* out, int32_t* err, hipStream_t st);
+void launch_cand_front(bool onet, const int4* sat, int H, int W, const float4* boxes, const int32_t* img, int64_t n,
+                       const float* w1, const float* b1, const float* a1, float* out, int32_t* err, hipStream_t st);
 void launch_heads(const float* x, int64_t n, int D, const float* w1, const float* b1, const float* w2,
                   const float* b2, const float* w3, const float* b3, float* prob, float4* reg, float* lm,
                   hipStream_t st);

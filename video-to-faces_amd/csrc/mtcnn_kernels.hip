@@ -9,7 +9,8 @@
 //     256-thread workgroup owns a 16x32 tile of PNet output cells.  The level pixels it
 //     needs (42x74x3) are computed on the fly from the uint8 BGR frame (preprocess +
 //     adaptive_avg_pool2d, bit-exact: exact (u-127.5)/128, row-major fp32 bin sum, /kh, /kw)
-//     straight into LDS, so the 10.7 Mpx/frame pyramid never exists in HBM.  conv1+PReLU+
+//     straight into LDS, so the 10.7 Mpx/frame pyramid never exists in HBM (large-bin
+//     downsampled levels come from the frame's summed-area table, k_resample_sat).  conv1+PReLU+
 //     maxpool(ceil), conv2+PReLU, conv3+PReLU and both 1x1 heads + softmax run from LDS with
 //     weights streamed through the scalar cache (wave-uniform, transposed to [ci][ky][kx][co]
 //     on the host so one s_load_dwordx16 feeds 16 v_fma).  Cells with p >= 0.6 are appended
@@ -28,34 +29,20 @@ typedef __attribute__((ext_vector_type(4))) float f32x4;
 
 // ----------------------------------------------------------------------------------- helpers
 
-// Level pixel (RGB channel c) of MTCNN._resample(_preprocess(frames)), from uint8 BGR.
-__device__ inline float level_value(const uint8_t* __restrict__ fr, int64_t row_stride, int c, int ly, int lx,
-                                    int H, int W, int lh, int lw) {
-    int y0 = (int)(((int64_t)ly * H) / lh);
-    int y1 = (int)(((int64_t)(ly + 1) * H + lh - 1) / lh);
-    int x0 = (int)(((int64_t)lx * W) / lw);
-    int x1 = (int)(((int64_t)(lx + 1) * W + lw - 1) / lw);
-    const uint8_t* p = fr + (2 - c);
-    float s = 0.f;
-    for (int y = y0; y < y1; y++) {
-        const uint8_t* r = p + (int64_t)y * row_stride;
-        for (int x = x0; x < x1; x++) s = s + ((float)r[x * 3] - 127.5f) * 0.0078125f;
-    }
-    return __fdiv_rn(__fdiv_rn(s, (float)(y1 - y0)), (float)(x1 - x0));
+// Summed-area table of the preprocessed frame.  (u - 127.5) / 128 = (2u - 255) / 256 is exact
+// in fp32, and so is every partial sum of such values over an adaptive-pool bin (|sum| < 2^16
+// with 8 fractional bits), so the reference's sequential fp32 bin sum (adaptive_avg_pool2d,
+// row-major) equals the integer box sum of v = 2u - 255 times 2^-8, bit for bit.
+// sat[b][y][x] = (R, G, B, 0) sums over rows < y, cols < x; y in [0,H], x in [0,W].
+__device__ inline int4 sat_box(const int4* __restrict__ s, int W1, int y0, int y1, int x0, int x1) {
+    const int4 a = s[(int64_t)y0 * W1 + x0], b = s[(int64_t)y0 * W1 + x1];
+    const int4 c = s[(int64_t)y1 * W1 + x0], d = s[(int64_t)y1 * W1 + x1];
+    return make_int4(d.x - b.x - c.x + a.x, d.y - b.y - c.y + a.y, d.z - b.z - c.z + a.z, 0);
 }
 
-// Crop [y0, y0+hc) x [x0, x0+wc) of the preprocessed frame adaptive-pooled to S x S.
-__device__ inline float crop_value(const uint8_t* __restrict__ fr, int64_t row_stride, int c, int r, int q,
-                                   int y0c, int x0c, int hc, int wc, int S) {
-    int ys = (r * hc) / S, ye = ((r + 1) * hc + S - 1) / S;
-    int xs = (q * wc) / S, xe = ((q + 1) * wc + S - 1) / S;
-    const uint8_t* p = fr + (2 - c);
-    float s = 0.f;
-    for (int y = ys; y < ye; y++) {
-        const uint8_t* row = p + (int64_t)(y0c + y) * row_stride;
-        for (int x = xs; x < xe; x++) s = s + ((float)row[(x0c + x) * 3] - 127.5f) * 0.0078125f;
-    }
-    return __fdiv_rn(__fdiv_rn(s, (float)(ye - ys)), (float)(xe - xs));
+// bin average from an exact integer bin sum: s / kh / kw with the reference's roundings
+__device__ inline float bin_avg(int sum, int kh, int kw) {
+    return __fdiv_rn(__fdiv_rn((float)sum * 0.00390625f, (float)kh), (float)kw);
 }
 
 __device__ inline float prelu(float x, float a) { return x > 0.f ? x : a * x; }
@@ -89,22 +76,129 @@ __device__ inline PNetWC to_const(const PNetW& w) {
 
 // ----------------------------------------------------------------------------------- resample
 
-__global__ void k_resample(const uint8_t* __restrict__ frames, int64_t frame_stride, int64_t row_stride, int B,
-                           int H, int W, int lh, int lw, float* __restrict__ out) {
-    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    int64_t n = (int64_t)B * 3 * lh * lw;
-    if (i >= n) return;
-    int lx = (int)(i % lw);
-    int ly = (int)((i / lw) % lh);
-    int c = (int)((i / ((int64_t)lw * lh)) % 3);
-    int b = (int)(i / ((int64_t)lw * lh * 3));
-    out[i] = level_value(frames + (int64_t)b * frame_stride, row_stride, c, ly, lx, H, W, lh, lw);
+// row pass: block per frame row, thread-contiguous chunks, block scan of the chunk totals
+__global__ __launch_bounds__(256) void k_sat_rows(const uint8_t* __restrict__ frames, int64_t frame_stride,
+                                                  int64_t row_stride, int H, int W, int4* __restrict__ sat) {
+    const int y = blockIdx.x % H, b = blockIdx.x / H;
+    const int W1 = W + 1;
+    const uint8_t* row = frames + (int64_t)b * frame_stride + (int64_t)y * row_stride;
+    int4* out = sat + ((int64_t)b * (H + 1) + y + 1) * W1;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int per = (W + 255) / 256, xs = tid * per;
+    int r = 0, g = 0, bl = 0;
+    for (int i = 0; i < per; i++) {
+        const int x = xs + i;
+        if (x < W) {
+            r += 2 * row[3 * x + 2] - 255;
+            g += 2 * row[3 * x + 1] - 255;
+            bl += 2 * row[3 * x] - 255;
+        }
+    }
+    // inclusive wave scan, then wave offsets
+    int ir = r, ig = g, ib = bl;
+    for (int off = 1; off < 64; off <<= 1) {
+        const int tr = __shfl_up(ir, off), tg = __shfl_up(ig, off), tb = __shfl_up(ib, off);
+        if (lane >= off) {
+            ir += tr;
+            ig += tg;
+            ib += tb;
+        }
+    }
+    __shared__ int3 wt[4];
+    if (lane == 63) wt[wave] = make_int3(ir, ig, ib);
+    __syncthreads();
+    int3 base = make_int3(0, 0, 0);
+    for (int w = 0; w < wave; w++) {
+        base.x += wt[w].x;
+        base.y += wt[w].y;
+        base.z += wt[w].z;
+    }
+    r = base.x + ir - r;  // exclusive prefix of this thread's chunk
+    g = base.y + ig - g;
+    bl = base.z + ib - bl;
+    for (int i = 0; i < per; i++) {
+        const int x = xs + i;
+        if (x < W) {
+            r += 2 * row[3 * x + 2] - 255;
+            g += 2 * row[3 * x + 1] - 255;
+            bl += 2 * row[3 * x] - 255;
+            out[x + 1] = make_int4(r, g, bl, 0);
+        }
+    }
+    if (tid == 0) {
+        out[0] = make_int4(0, 0, 0, 0);
+        if (y == 0) {
+            int4* r0 = sat + (int64_t)b * (H + 1) * W1;
+            for (int x = 0; x < W1; x++) r0[x] = make_int4(0, 0, 0, 0);
+        }
+    }
 }
 
-void launch_resample(const uint8_t* frames, int64_t frame_stride, int64_t row_stride, int B, int H, int W, int lh,
-                     int lw, float* out, hipStream_t st) {
-    int64_t n = (int64_t)B * 3 * lh * lw;
-    k_resample<<<cdiv(n, 256), 256, 0, st>>>(frames, frame_stride, row_stride, B, H, W, lh, lw, out);
+// column pass, in place: block = 64 columns x 4 row groups (group totals combined in LDS)
+__global__ __launch_bounds__(256) void k_sat_cols(int H, int W, int4* __restrict__ sat) {
+    const int W1 = W + 1;
+    const int ncb = (W1 + 63) / 64;
+    const int b = blockIdx.x / ncb, cb = blockIdx.x % ncb;
+    const int lane = threadIdx.x & 63, g = threadIdx.x >> 6;
+    const int x = cb * 64 + lane;
+    const int per = (H + 3) / 4;
+    const int ys = 1 + g * per, ye = min(H + 1, ys + per);
+    int4* col = sat + (int64_t)b * (H + 1) * W1 + x;
+    __shared__ int4 tot[4][64];
+    int4 acc = make_int4(0, 0, 0, 0);
+    if (x < W1)
+        for (int y = ys; y < ye; y++) {
+            const int4 v = col[(int64_t)y * W1];
+            acc.x += v.x;
+            acc.y += v.y;
+            acc.z += v.z;
+        }
+    tot[g][lane] = acc;
+    __syncthreads();
+    int4 off = make_int4(0, 0, 0, 0);
+    for (int k = 0; k < g; k++) {
+        off.x += tot[k][lane].x;
+        off.y += tot[k][lane].y;
+        off.z += tot[k][lane].z;
+    }
+    if (x < W1)
+        for (int y = ys; y < ye; y++) {
+            const int4 v = col[(int64_t)y * W1];
+            off.x += v.x;
+            off.y += v.y;
+            off.z += v.z;
+            col[(int64_t)y * W1] = off;
+        }
+}
+
+void launch_sat(const uint8_t* frames, int64_t frame_stride, int64_t row_stride, int B, int H, int W, int4* sat,
+                hipStream_t st) {
+    k_sat_rows<<<(unsigned)((int64_t)B * H), 256, 0, st>>>(frames, frame_stride, row_stride, H, W, sat);
+    k_sat_cols<<<(unsigned)(B * ((W + 64) / 64)), 256, 0, st>>>(H, W, sat);
+}
+
+// MTCNN._resample of the preprocessed frames (mtcnn.py:133-139, 150-151) from the SAT:
+// out [B][3][lh][lw], one thread per level pixel (all three channels)
+__global__ void k_resample_sat(const int4* __restrict__ sat, int B, int H, int W, int lh, int lw,
+                               float* __restrict__ out) {
+    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    int64_t n = (int64_t)B * lh * lw;
+    if (i >= n) return;
+    const int lx = (int)(i % lw);
+    const int ly = (int)((i / lw) % lh);
+    const int b = (int)(i / ((int64_t)lw * lh));
+    const int y0 = (int)(((int64_t)ly * H) / lh), y1 = (int)(((int64_t)(ly + 1) * H + lh - 1) / lh);
+    const int x0 = (int)(((int64_t)lx * W) / lw), x1 = (int)(((int64_t)(lx + 1) * W + lw - 1) / lw);
+    const int4 s = sat_box(sat + (int64_t)b * (H + 1) * (W + 1), W + 1, y0, y1, x0, x1);
+    const int64_t plane = (int64_t)lh * lw, o = (int64_t)b * 3 * plane + (int64_t)ly * lw + lx;
+    out[o] = bin_avg(s.x, y1 - y0, x1 - x0);
+    out[o + plane] = bin_avg(s.y, y1 - y0, x1 - x0);
+    out[o + 2 * plane] = bin_avg(s.z, y1 - y0, x1 - x0);
+}
+
+void launch_resample_sat(const int4* sat, int B, int H, int W, int lh, int lw, float* out, hipStream_t st) {
+    int64_t n = (int64_t)B * lh * lw;
+    k_resample_sat<<<cdiv(n, 256), 256, 0, st>>>(sat, B, H, W, lh, lw, out);
 }
 
 // ----------------------------------------------------------------------------------- PNet
@@ -459,34 +553,6 @@ void launch_pnet(bool dense, const uint8_t* frames, int64_t frame_stride, int64_
 // The candidate networks run as batched layers on the MFMA implicit-GEMM conv kernel
 // (conv.hip, fp32, PReLU epilogue); here: the crop front end and the tiny heads.
 
-// _get_cropped_candidates (mtcnn.py:153-163): crop of the preprocessed frame, adaptive-pooled
-// to S x S, written NHWC with 8 channels (RGB + zero pad) for the conv kernel.
-__global__ void k_crop_nhwc(const uint8_t* __restrict__ frames, int64_t frame_stride, int64_t row_stride, int H,
-                            int W, const float4* __restrict__ boxes, const int32_t* __restrict__ img, int64_t n,
-                            int S, float* __restrict__ out, int32_t* __restrict__ err) {
-    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n * S * S) return;
-    int q = (int)(i % S), r = (int)((i / S) % S);
-    int64_t k = i / ((int64_t)S * S);
-    int y0, x0, hc, wc;
-    float* o = out + i * 8;
-    if (!crop_rect(boxes[k], H, W, y0, x0, hc, wc)) {
-        if (r == 0 && q == 0) atomicAdd(err, 1);
-        for (int c = 0; c < 8; c++) o[c] = 0.f;
-        return;
-    }
-    const uint8_t* fr = frames + (int64_t)img[k] * frame_stride;
-    for (int c = 0; c < 3; c++) o[c] = crop_value(fr, row_stride, c, r, q, y0, x0, hc, wc, S);
-    for (int c = 3; c < 8; c++) o[c] = 0.f;
-}
-
-void launch_crop_nhwc(const uint8_t* frames, int64_t frame_stride, int64_t row_stride, int H, int W,
-                      const float4* boxes, const int32_t* img, int64_t n, int S, float* out, int32_t* err,
-                      hipStream_t st) {
-    if (n > 0) k_crop_nhwc<<<cdiv(n * S * S, 256), 256, 0, st>>>(frames, frame_stride, row_stride, H, W, boxes, img, n,
-                                                                  S, out, err);
-}
-
 // Fused candidate front end: _get_cropped_candidates (mtcnn.py:153-163) + conv1 (3->28/32,
 // 3x3) + PReLU + MaxPool2d(3, 2, ceil_mode) of RNet (S=24) / ONet (S=48), one candidate per
 // workgroup.  The S x S crop is adaptive-pooled from the uint8 frame straight into LDS
@@ -495,8 +561,8 @@ void launch_crop_nhwc(const uint8_t* frames, int64_t frame_stride, int64_t row_s
 // [n, P, P, 32] map reaches HBM (P = 11 / 23).  Conv rows are produced in bands of 2*PB+1.
 // w1: [28][32] (k, co; row 27 and channels >= Cout zero); b1, a1: [32].
 template <int S, int PB>
-__global__ __launch_bounds__(256) void k_cand_front(const uint8_t* __restrict__ frames, int64_t frame_stride,
-                                                    int64_t row_stride, int H, int W, const float4* __restrict__ boxes,
+__global__ __launch_bounds__(256) void k_cand_front(const int4* __restrict__ sat, int H, int W,
+                                                    const float4* __restrict__ boxes,
                                                     const int32_t* __restrict__ img, const float* __restrict__ w1,
                                                     const float* __restrict__ b1, const float* __restrict__ a1,
                                                     float* __restrict__ out, int32_t* __restrict__ err) {
@@ -515,10 +581,15 @@ __global__ __launch_bounds__(256) void k_cand_front(const uint8_t* __restrict__ 
         for (int i = tid; i < P * P * 32; i += 256) o[i] = 0.f;
         return;
     }
-    const uint8_t* fr = frames + (int64_t)img[k] * frame_stride;
-    for (int i = tid; i < 3 * S * S; i += 256) {
-        const int c = i / (S * S), rq = i - c * (S * S);
-        crop[i] = crop_value(fr, row_stride, c, rq / S, rq - (rq / S) * S, y0, x0, hc, wc, S);
+    const int4* sk = sat + (int64_t)img[k] * (H + 1) * (W + 1);
+    for (int i = tid; i < S * S; i += 256) {
+        const int r = i / S, q = i - r * S;
+        const int ys = (r * hc) / S, ye = ((r + 1) * hc + S - 1) / S;
+        const int xs = (q * wc) / S, xe = ((q + 1) * wc + S - 1) / S;
+        const int4 sm = sat_box(sk, W + 1, y0 + ys, y0 + ye, x0 + xs, x0 + xe);
+        crop[i] = bin_avg(sm.x, ye - ys, xe - xs);
+        crop[S * S + i] = bin_avg(sm.y, ye - ys, xe - xs);
+        crop[2 * S * S + i] = bin_avg(sm.z, ye - ys, xe - xs);
     }
     float wb[7][2];
 #pragma unroll
@@ -578,16 +649,13 @@ __global__ __launch_bounds__(256) void k_cand_front(const uint8_t* __restrict__ 
 
 int cand_front_side(bool onet) { return onet ? 23 : 11; }
 
-void launch_cand_front(bool onet, const uint8_t* frames, int64_t frame_stride, int64_t row_stride, int H, int W,
-                       const float4* boxes, const int32_t* img, int64_t n, const float* w1, const float* b1,
-                       const float* a1, float* out, int32_t* err, hipStream_t st) {
+void launch_cand_front(bool onet, const int4* sat, int H, int W, const float4* boxes, const int32_t* img, int64_t n,
+                       const float* w1, const float* b1, const float* a1, float* out, int32_t* err, hipStream_t st) {
     if (n <= 0) return;
     if (onet)
-        k_cand_front<48, 3><<<(unsigned)n, 256, 0, st>>>(frames, frame_stride, row_stride, H, W, boxes, img, w1, b1,
-                                                          a1, out, err);
+        k_cand_front<48, 3><<<(unsigned)n, 256, 0, st>>>(sat, H, W, boxes, img, w1, b1, a1, out, err);
     else
-        k_cand_front<24, 6><<<(unsigned)n, 256, 0, st>>>(frames, frame_stride, row_stride, H, W, boxes, img, w1, b1,
-                                                          a1, out, err);
+        k_cand_front<24, 6><<<(unsigned)n, 256, 0, st>>>(sat, H, W, boxes, img, w1, b1, a1, out, err);
 }
 
 // heads: x [n, D] -> softmax(x W1^T + b1)[:, 1], x W2^T + b2 (4), optional x W3^T + b3 (10).

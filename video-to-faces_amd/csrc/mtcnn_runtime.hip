@@ -64,7 +64,7 @@ struct Mtcnn {
 enum Slot {
     S_FRAMES = 0, S_LEVELS, S_COUNT, S_KEY, S_SCORE, S_REGV, S_KEY2, S_SLOT, S_SLOT2, S_B1, S_S1, S_R1, S_I1, S_C1,
     S_KEEP, S_B2, S_S2, S_R2, S_I2, S_C2, S_PROB, S_REG, S_LM, S_ERR, S_FLAG, S_INCL, S_IDX, S_LMK, S_OUTB, S_OUTS,
-    S_OUTL, S_OUTI, S_SORT, S_SCAN, S_PRE, S_CROP
+    S_OUTL, S_OUTI, S_SORT, S_SCAN, S_PRE, S_CROP, S_SAT
 };
 
 // ---- weights: reference state_dict order (specs.py mtcnn_spec) -> transposed device layout
@@ -349,6 +349,10 @@ static void detect(Mtcnn& m, const uint8_t* frames, int on_dev, int B, int H, in
     // downsampled levels whose adaptive-pool bins exceed 2 frame pixels are resampled by a
     // separate fully parallel kernel (one thread per level value) into HBM; inside the fused
     // tile kernel their long serial bin sums would leave a few workgroups as a long tail.
+    // summed-area table of the preprocessed frames: O(1) exact bin sums for the downsampled
+    // levels and the stage-2/3 candidate crops
+    int4* sat = m.ar.get<int4>(S_SAT, (size_t)B * (H + 1) * (W + 1));
+    launch_sat(fr, fstride, rstride, B, H, W, sat, st);
     {
         int64_t pre_elems = 0;
         for (auto& L : lv)
@@ -358,7 +362,7 @@ static void detect(Mtcnn& m, const uint8_t* frames, int on_dev, int B, int H, in
             L.pre = nullptr;
             if ((int64_t)H > 2 * (int64_t)L.lh) {
                 L.pre = pre;
-                launch_resample(fr, fstride, rstride, B, H, W, L.lh, L.lw, pre, st);
+                launch_resample_sat(sat, B, H, W, L.lh, L.lw, pre, st);
                 pre += (int64_t)B * 3 * L.lh * L.lw;
             }
         }
@@ -433,7 +437,7 @@ static void detect(Mtcnn& m, const uint8_t* frames, int on_dev, int B, int H, in
     {
         const int P = cand_front_side(false);
         float* x0 = m.ar.get<float>(S_CROP, (size_t)k2 * P * P * 32);
-        launch_cand_front(false, fr, fstride, rstride, H, W, b1, i1, k2, m.fw[0], m.rl[0].b, m.rl[0].a, x0, err, st);
+        launch_cand_front(false, sat, H, W, b1, i1, k2, m.fw[0], m.rl[0].b, m.rl[0].a, x0, err, st);
         run_candidates(m, false, x0, k2, reg, nullptr, prob, 1);
     }
     int32_t nerr = 0;
@@ -459,7 +463,7 @@ static void detect(Mtcnn& m, const uint8_t* frames, int on_dev, int B, int H, in
     {
         const int P = cand_front_side(true);
         float* x0 = m.ar.get<float>(S_CROP, (size_t)k3 * P * P * 32);
-        launch_cand_front(true, fr, fstride, rstride, H, W, b1, i1, k3, m.fw[1], m.ol[0].b, m.ol[0].a, x0, err, st);
+        launch_cand_front(true, sat, H, W, b1, i1, k3, m.fw[1], m.ol[0].b, m.ol[0].a, x0, err, st);
         run_candidates(m, true, x0, k3, reg, lm, prob, 1);
     }
     d2h_sync(&nerr, err, 4, st);
@@ -625,8 +629,10 @@ int vtf_mtcnn_pnet_level(vtf_mtcnn_t h, const uint8_t* d_frames, int B, int H, i
         L.tile_beg = 0;
         L.pre = nullptr;
         if ((int64_t)H > 2 * (int64_t)lh) {
+            int4* sat = h->m.ar.get<int4>(S_SAT, (size_t)B * (H + 1) * (W + 1));
+            launch_sat(d_frames, frame_stride, row_stride, B, H, W, sat, h->m.st);
             float* pre = h->m.ar.get<float>(S_PRE, (int64_t)B * 3 * lh * lw);
-            launch_resample(d_frames, frame_stride, row_stride, B, H, W, lh, lw, pre, h->m.st);
+            launch_resample_sat(sat, B, H, W, lh, lw, pre, h->m.st);
             L.pre = pre;
         }
         PNetLevel* d_lv = h->m.ar.get<PNetLevel>(S_LEVELS, 1);
@@ -645,7 +651,9 @@ int vtf_mtcnn_resample(vtf_mtcnn_t h, const uint8_t* d_frames, int B, int H, int
                        int64_t row_stride, int lh, int lw, float* d_out) {
     return guarded([&] {
         VTF_CHECK(h && d_frames && d_out, VTF_E_ARG, "null argument");
-        launch_resample(d_frames, frame_stride, row_stride, B, H, W, lh, lw, d_out, h->m.st);
+        int4* sat = h->m.ar.get<int4>(S_SAT, (size_t)B * (H + 1) * (W + 1));
+        launch_sat(d_frames, frame_stride, row_stride, B, H, W, sat, h->m.st);
+        launch_resample_sat(sat, B, H, W, lh, lw, d_out, h->m.st);
         VTF_HIP(hipStreamSynchronize(h->m.st));
     });
 }
