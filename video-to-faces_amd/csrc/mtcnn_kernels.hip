@@ -19,6 +19,7 @@
 //     48x48 (replacing the reference's per-box Python loop) feeds the whole network in LDS.
 // Build with -ffp-contract=off: only explicit fmaf() fuses.
 #include <algorithm>
+#include <cstdlib>
 
 #include "common.hpp"
 #include "mtcnn.hpp"
@@ -282,22 +283,40 @@ __global__ __launch_bounds__(256, 2) void k_pnet(const uint8_t* __restrict__ fra
         const int pw3 = (fx1 - fx0) * 3;
         const bool staged = !P.pre && (int64_t)(fy1 - fy0) * pw3 <= PATCH_BYTES;
         uint8_t* patch = (uint8_t*)sP;
+        // (gathers below issue 8 loads per thread before the first use: latency-bound otherwise)
         if (staged) {
             const int nbytes = (fy1 - fy0) * pw3;
-            for (int i = tid; i < nbytes; i += 256) {
-                int r = i / pw3, q = i - r * pw3;
-                patch[i] = fr[(int64_t)(fy0 + r) * row_stride + fx0 * 3 + q];
+            for (int i0 = tid; i0 < nbytes; i0 += 256 * 8) {
+                uint8_t v[8];
+#pragma unroll
+                for (int j = 0; j < 8; j++) {
+                    const int i = min(i0 + j * 256, nbytes - 1);
+                    const int r = i / pw3, q = i - r * pw3;
+                    v[j] = fr[(int64_t)(fy0 + r) * row_stride + fx0 * 3 + q];
+                }
+#pragma unroll
+                for (int j = 0; j < 8; j++)
+                    if (i0 + j * 256 < nbytes) patch[i0 + j * 256] = v[j];
             }
         }
         __syncthreads();
         if (P.pre) {
-            // large-bin level precomputed by k_resample (bit-identical values)
+            // large-bin level precomputed by k_resample_sat (bit-identical values)
             const float* pre = P.pre + (int64_t)b * 3 * P.lh * P.lw;
-            for (int i = tid; i < ((o.dbg & 1) ? 0 : P_LVL); i += 256) {
-                int c = i / (PL_H * PL_W), rq = i - c * (PL_H * PL_W);
-                int r = rq / PL_W, q = rq - r * PL_W;
-                int ly = 2 * oy0 + r, lx = 2 * ox0 + q;
-                sA[i] = (ly < P.lh && lx < P.lw) ? pre[((int64_t)c * P.lh + ly) * P.lw + lx] : 0.f;
+            for (int i0 = tid; i0 < ((o.dbg & 1) ? 0 : P_LVL); i0 += 256 * 8) {
+                float v[8];
+#pragma unroll
+                for (int j = 0; j < 8; j++) {
+                    const int i = min(i0 + j * 256, P_LVL - 1);
+                    const int c = i / (PL_H * PL_W), rq = i - c * (PL_H * PL_W);
+                    const int r = rq / PL_W, q = rq - r * PL_W;
+                    const int ly = 2 * oy0 + r, lx = 2 * ox0 + q;
+                    const float t = pre[((int64_t)c * P.lh + min(ly, P.lh - 1)) * P.lw + min(lx, P.lw - 1)];
+                    v[j] = (ly < P.lh && lx < P.lw) ? t : 0.f;
+                }
+#pragma unroll
+                for (int j = 0; j < 8; j++)
+                    if (i0 + j * 256 < P_LVL) sA[i0 + j * 256] = v[j];
             }
         }
         for (int i = tid; i < ((o.dbg & 1) || P.pre ? 0 : PL_H * PL_W); i += 256) {
@@ -560,15 +579,17 @@ void launch_pnet(bool dense, const uint8_t* frames, int64_t frame_stride, int64_
 // no channel padding), and the pool reads the conv1 band from LDS: only the pooled
 // [n, P, P, 32] map reaches HBM (P = 11 / 23).  Conv rows are produced in bands of 2*PB+1.
 // w1: [28][32] (k, co; row 27 and channels >= Cout zero); b1, a1: [32].
-template <int S, int PB>
-__global__ __launch_bounds__(256) void k_cand_front(const int4* __restrict__ sat, int H, int W,
-                                                    const float4* __restrict__ boxes,
-                                                    const int32_t* __restrict__ img, const float* __restrict__ w1,
-                                                    const float* __restrict__ b1, const float* __restrict__ a1,
-                                                    float* __restrict__ out, int32_t* __restrict__ err) {
+template <int S, int PB, int NT>
+__global__ __launch_bounds__(NT) void k_cand_front(const int4* __restrict__ sat, int H, int W,
+                                                   const float4* __restrict__ boxes, const int32_t* __restrict__ img,
+                                                   const float* __restrict__ w1, const float* __restrict__ b1,
+                                                   const float* __restrict__ a1, float* __restrict__ out,
+                                                   int32_t* __restrict__ err) {
     constexpr int O = S - 2;                // conv1 output side
     constexpr int P = (O - 3 + 1) / 2 + 1;  // ceil-mode pool output side
     constexpr int BR = 2 * PB + 1;          // conv rows per band
+    constexpr int NW = NT / 64;
+    constexpr int PIX = (S * S + NT - 1) / NT;  // crop pixels per thread
     __shared__ float crop[3 * S * S];
     __shared__ float cv[32 * BR * O];
     const int64_t k = blockIdx.x;
@@ -578,18 +599,40 @@ __global__ __launch_bounds__(256) void k_cand_front(const int4* __restrict__ sat
     if (!crop_rect(boxes[k], H, W, y0, x0, hc, wc)) {
         // the reference skips this box and then fails indexing (IndexError): flag it
         if (tid == 0) atomicAdd(err, 1);
-        for (int i = tid; i < P * P * 32; i += 256) o[i] = 0.f;
+        for (int i = tid; i < P * P * 32; i += NT) o[i] = 0.f;
         return;
     }
+    // crop bins from the SAT: every thread issues all of its corner loads before using any
+    // (the gathers are latency-bound; PIX * 4 loads in flight per thread)
     const int4* sk = sat + (int64_t)img[k] * (H + 1) * (W + 1);
-    for (int i = tid; i < S * S; i += 256) {
-        const int r = i / S, q = i - r * S;
-        const int ys = (r * hc) / S, ye = ((r + 1) * hc + S - 1) / S;
-        const int xs = (q * wc) / S, xe = ((q + 1) * wc + S - 1) / S;
-        const int4 sm = sat_box(sk, W + 1, y0 + ys, y0 + ye, x0 + xs, x0 + xe);
-        crop[i] = bin_avg(sm.x, ye - ys, xe - xs);
-        crop[S * S + i] = bin_avg(sm.y, ye - ys, xe - xs);
-        crop[2 * S * S + i] = bin_avg(sm.z, ye - ys, xe - xs);
+    {
+        int4 cn[PIX][4];
+        int kh[PIX], kw[PIX];
+#pragma unroll
+        for (int j = 0; j < PIX; j++) {
+            const int i = min(tid + j * NT, S * S - 1);
+            const int r = i / S, q = i - r * S;
+            const int ys = (r * hc) / S, ye = ((r + 1) * hc + S - 1) / S;
+            const int xs = (q * wc) / S, xe = ((q + 1) * wc + S - 1) / S;
+            kh[j] = ye - ys;
+            kw[j] = xe - xs;
+            const int4* a = sk + (int64_t)(y0 + ys) * (W + 1) + x0;
+            const int4* b = sk + (int64_t)(y0 + ye) * (W + 1) + x0;
+            cn[j][0] = a[xs];
+            cn[j][1] = a[xe];
+            cn[j][2] = b[xs];
+            cn[j][3] = b[xe];
+        }
+#pragma unroll
+        for (int j = 0; j < PIX; j++) {
+            const int i = tid + j * NT;
+            if (i < S * S) {
+                const int4 &a = cn[j][0], &b = cn[j][1], &c = cn[j][2], &d = cn[j][3];
+                crop[i] = bin_avg(d.x - b.x - c.x + a.x, kh[j], kw[j]);
+                crop[S * S + i] = bin_avg(d.y - b.y - c.y + a.y, kh[j], kw[j]);
+                crop[2 * S * S + i] = bin_avg(d.z - b.z - c.z + a.z, kh[j], kw[j]);
+            }
+        }
     }
     float wb[7][2];
 #pragma unroll
@@ -604,7 +647,7 @@ __global__ __launch_bounds__(256) void k_cand_front(const int4* __restrict__ sat
         const int ncr = min(BR, O - cr0);
         const int npos = ncr * O;
         const int nf = (npos + 15) / 16;
-        for (int f = wave; f < nf; f += 4) {
+        for (int f = wave; f < nf; f += NW) {
             const int p = min(f * 16 + lr, npos - 1);
             const int y = cr0 + p / O, x = p % O;
             f32x4 c0 = {0.f, 0.f, 0.f, 0.f}, c1 = {0.f, 0.f, 0.f, 0.f};
@@ -628,7 +671,7 @@ __global__ __launch_bounds__(256) void k_cand_front(const int4* __restrict__ sat
         }
         __syncthreads();
         const int npr = min(PB, P - pr0);
-        for (int i = tid; i < npr * P * 32; i += 256) {
+        for (int i = tid; i < npr * P * 32; i += NT) {
             const int c = i & 31, t = i >> 5;
             const int px = t % P, pyl = t / P;
             float m = -3.402823466e38f;
@@ -653,9 +696,9 @@ void launch_cand_front(bool onet, const int4* sat, int H, int W, const float4* b
                        const float* w1, const float* b1, const float* a1, float* out, int32_t* err, hipStream_t st) {
     if (n <= 0) return;
     if (onet)
-        k_cand_front<48, 3><<<(unsigned)n, 256, 0, st>>>(sat, H, W, boxes, img, w1, b1, a1, out, err);
+        k_cand_front<48, 3, 512><<<(unsigned)n, 512, 0, st>>>(sat, H, W, boxes, img, w1, b1, a1, out, err);
     else
-        k_cand_front<24, 6><<<(unsigned)n, 256, 0, st>>>(sat, H, W, boxes, img, w1, b1, a1, out, err);
+        k_cand_front<24, 6, 256><<<(unsigned)n, 256, 0, st>>>(sat, H, W, boxes, img, w1, b1, a1, out, err);
 }
 
 // heads: x [n, D] -> softmax(x W1^T + b1)[:, 1], x W2^T + b2 (4), optional x W3^T + b3 (10).
