@@ -133,6 +133,18 @@ int vtf_cosine_dedupe(const float* d_X, int64_t N, int64_t D, float* d_min, int6
 int vtf_cosine_classify(const float* d_X, int64_t N, const float* d_R, int64_t C, int64_t D, float* d_min,
                         int64_t* d_arg, void* hip_stream);
 
+/* ---------------------------------------------------------------- hash dedupe
+ * dupes.ahash (dupes.py:11-15) of N face crops of device frames (frames as in
+ * vtf_mtcnn_detect, crops host int32 [N,5] = frame, x1, y1, x2, y2 as get_crops slices them,
+ * detection.py:161-162): out_hashes host uint64 [N], bit k = 8x8 thumbnail pixel k (row-major)
+ * > mean.  cvtColor(BGR2GRAY) + resize INTER_LINEAR restated from OpenCV's fixed point. */
+int vtf_ahash_crops(const uint8_t* d_frames, int H, int W, int64_t frame_stride, int64_t row_stride,
+                    const int32_t* crops, int64_t N, uint64_t* out_hashes, void* hip_stream);
+/* remove_dupes_overall('hash') distances (dupes.py:55-64): for row i, min and first argmin over
+ * j < i of popcount(h_i ^ h_j); row 0 -> 10000, 0.  d_hashes uint64 [N] -> d_min int32 [N],
+ * d_arg int64 [N]. */
+int vtf_hamming_dedupe(const uint64_t* d_hashes, int64_t N, int32_t* d_min, int64_t* d_arg, void* hip_stream);
+
 /* ---------------------------------------------------------------- YOLOv3 detector
  * Replaces RealYOLO / YOLOv3.forward (src/videotofaces/detectors/yolo.py:131-191), called by
  * detection.py:131 `detout = model(frames)`.

@@ -407,7 +407,35 @@ def gen_rcnn():
     print('rcnn', {k: v.shape for k, v in out.items()}, 'counts', out['counts'])
 
 
+def gen_dupes():
+    """remove_dupes_overall('hash') (dupes.py:51-93) of the reference on 64-bit average-hash
+    bit arrays with planted near-duplicates (the cv2 ahash itself is not runnable here)."""
+    import sklearn.metrics
+    load_ref()
+    dupes = importlib.import_module('ref_vtf.dupes')
+    rng = np.random.default_rng(21)
+    N = 400
+    X = rng.integers(0, 2, (N, 64))
+    for i in range(60):
+        j = int(rng.integers(1, N))
+        k = int(rng.integers(0, j))
+        X[j] = X[k]
+        flip = rng.choice(64, int(rng.integers(0, 12)), replace=False)
+        X[j, flip] ^= 1
+    with tempfile.TemporaryDirectory() as td:
+        os.makedirs(os.path.join(td, 'faces'))
+        names = ['f%05d.jpg' % i for i in range(N)]
+        for n in names:
+            open(os.path.join(td, 'faces', n), 'w').close()
+        _, goods = dupes.remove_dupes_overall(X.copy(), names, ('hash', 8, False, td))
+    D = sklearn.metrics.pairwise_distances(X, metric=lambda a, b: np.count_nonzero(a != b)).astype(np.uint16)
+    D += (1 - np.tri(N, k=-1).astype(D.dtype)) * 10000
+    np.savez_compressed(os.path.join(HERE, 'dupes.npz'), X=X.astype(np.uint8), keep=np.array(
+        [int(n[1:6]) for n in goods], np.int64), mins=D.min(axis=1), inds=D.argmin(axis=1))
+    print('dupes', N, 'kept', len(goods))
+
+
 if __name__ == '__main__':
-    which = sys.argv[1:] or ['mtcnn', 'facenet', 'vit', 'grouping', 'yolo', 'kmeans', 'rcnn']
+    which = sys.argv[1:] or ['mtcnn', 'facenet', 'vit', 'grouping', 'yolo', 'kmeans', 'rcnn', 'dupes']
     for w in which:
         globals()['gen_' + w]()

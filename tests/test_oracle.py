@@ -222,3 +222,34 @@ def test_oracle_rcnn_e2e_vs_golden(grc):
     np.testing.assert_array_equal([len(t) for t in s], grc['counts'])
     np.testing.assert_allclose(np.concatenate(b), grc['boxes'], rtol=0, atol=1e-3)
     np.testing.assert_allclose(np.concatenate(s), grc['scores'], rtol=0, atol=1e-5)
+
+
+def test_oracle_hash_dedupe_vs_golden():
+    """remove_dupes_overall('hash') distances (dupes.py:55-65): oracle == reference."""
+    from oracle import dupes as od
+    gd = np.load(os.path.join(GOLDEN, 'dupes.npz'))
+    mins, inds = od.hamming_lower(gd['X'])
+    np.testing.assert_array_equal(mins, gd['mins'])
+    np.testing.assert_array_equal(inds, gd['inds'])
+    np.testing.assert_array_equal(np.nonzero(~(mins <= 8))[0], gd['keep'])
+
+
+def test_oracle_ahash_properties():
+    """ahash restatement: identity at 8x8, 2x INTER_AREA path, hash = thumbnail > mean."""
+    from oracle import dupes as od
+    rng = np.random.default_rng(2)
+    img = rng.integers(0, 256, (8, 8, 3)).astype(np.uint8)
+    g = od.gray(img)
+    np.testing.assert_array_equal(od.ahash(img), 1 * (g > g.mean()).flatten())
+    big = np.repeat(np.repeat(img, 2, 0), 2, 1)
+    np.testing.assert_array_equal(od.resize8(od.gray(big)), g)
+
+
+def test_pack_hashes_roundtrip():
+    from videotofaces.dupes import pack_hashes, unpack_hash
+    rng = np.random.default_rng(3)
+    H = rng.integers(0, 2, (5, 64))
+    P = pack_hashes(H)
+    assert P.dtype == np.uint64
+    for h, p in zip(H, P):
+        np.testing.assert_array_equal(unpack_hash(p), h)

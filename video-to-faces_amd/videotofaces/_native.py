@@ -72,6 +72,8 @@ SIGNATURES = {
     'vtf_yolo_postprocess': [_p, _p, _p, _p, _i32, _i32, _i32, _p, _p, _p, _i64, _p],
     'vtf_yolo_profile': [_p, _i32, _p, _p, _p, _p],
     'vtf_cosine_classify': [_p, _i64, _p, _i64, _i64, _p, _p, _p],
+    'vtf_ahash_crops': [_p, _i32, _i32, _i64, _i64, _p, _i64, _p, _p],
+    'vtf_hamming_dedupe': [_p, _i64, _p, _p, _p],
     'vtf_rcnn_create': [_p, _i64, _i32, _i32, _p],
     'vtf_rcnn_destroy': [_p],
     'vtf_rcnn_set_stream': [_p, _p],

@@ -2,7 +2,10 @@
 
 The embedding branch of remove_dupes_overall (dupes.py:51-68) runs on the GPU as one fused
 cosine-distance + strict-lower-triangle row-min kernel (vtf_cosine_dedupe): no N x N
-matrix (the reference materialises an fp32 N x N plus an fp64 N x N mask).
+matrix (the reference materialises an fp32 N x N plus an fp64 N x N mask).  The hash branch
+(dupes.py:11-59): average hashes of the face crops straight from the frames in HBM
+(vtf_ahash_crops) and the all-pairs Hamming row-min as a popcount kernel
+(vtf_hamming_dedupe) instead of a Python-lambda pairwise_distances.
 """
 import ctypes
 import os
@@ -25,14 +28,76 @@ def cosine_dedupe_device(X):
     return mins.cpu().numpy(), inds.cpu().numpy()
 
 
+def pack_hashes(H):
+    """ahash bit arrays [N,64] (0/1, dupes.py:15 `1 * diff.flatten()`) -> uint64 [N], bit k =
+    element k; packed uint64 input passes through."""
+    H = np.asarray(H)
+    if H.dtype == np.uint64 and H.ndim == 1:
+        return H
+    H = H.reshape(-1, 64).astype(np.uint64)
+    return (H << np.arange(64, dtype=np.uint64)).sum(axis=1, dtype=np.uint64) if len(H) else np.zeros(0, np.uint64)
+
+
+def unpack_hash(h):
+    """uint64 -> the reference's 64-element 0/1 int array."""
+    return ((np.uint64(h) >> np.arange(64, dtype=np.uint64)) & np.uint64(1)).astype(np.int64)
+
+
+def ahash_crops(frames_dev, crops):
+    """dupes.ahash (dupes.py:11-15) of every crop (int [N,5] frame, x1, y1, x2, y2) of the
+    CUDA uint8 frames [B,H,W,3] -> uint64 [N] (vtf_ahash_crops)."""
+    c = np.ascontiguousarray(crops, dtype=np.int32).reshape(-1, 5)
+    out = np.zeros(c.shape[0], np.uint64)
+    if c.shape[0] == 0:
+        return out
+    B, H, W = frames_dev.shape[:3]
+    nat.check(nat.lib().vtf_ahash_crops(nat.ptr(frames_dev), H, W, frames_dev.stride(0), frames_dev.stride(1),
+                                        c.ctypes.data, c.shape[0], out.ctypes.data, nat.stream_ptr(frames_dev.device)))
+    return out
+
+
+def ahash(img):
+    """dupes.ahash (dupes.py:11-15) of one uint8 BGR image -> 64-element 0/1 array."""
+    t = torch.from_numpy(np.ascontiguousarray(img)[None]).cuda()
+    h, w = img.shape[:2]
+    return unpack_hash(ahash_crops(t, [[0, 0, 0, w, h]])[0])
+
+
 def hamming_lower(H):
-    """hash branch (dupes.py:55-57): Hamming distances of 64-bit average hashes, strict lower
-    triangle min/argmin (host numpy; the GPU popcount kernel is the next §8f item)."""
-    H = np.asarray(H).astype(np.uint8)
-    n = H.shape[0]
-    D = (H[:, None, :] != H[None, :, :]).sum(2).astype(np.uint16) if n else np.zeros((0, 0), np.uint16)
-    D = D + (1 - np.tri(n, k=-1).astype(D.dtype)) * 10000
-    return D.min(axis=1), D.argmin(axis=1)
+    """hash branch distances (dupes.py:55-64) on the GPU: min / first argmin over j < i of the
+    Hamming distance of the 64-bit average hashes; row 0 -> (10000, 0)."""
+    h = pack_hashes(H)
+    n = h.shape[0]
+    if n == 0:
+        return np.zeros(0, np.int32), np.zeros(0, np.int64)
+    dev = torch.device('cuda:0')
+    d = torch.from_numpy(h.view(np.int64)).to(dev)
+    mins = torch.empty(n, dtype=torch.int32, device=dev)
+    inds = torch.empty(n, dtype=torch.int64, device=dev)
+    nat.check(nat.lib().vtf_hamming_dedupe(nat.ptr(d), n, nat.ptr(mins), nat.ptr(inds), nat.stream_ptr(dev)))
+    return mins.cpu().numpy(), inds.cpu().numpy()
+
+
+def nearest_dupes(hashes, prev, hash_thr):
+    """remove_dupes_nearest's decision loop (dupes.py:18-36) on packed hashes: `prev` is the
+    running list of (hash, name) of kept faces (the reference's `hashes`), updated in place.
+    Returns (dupe flags, log rows (fn, nearest fn, diff, is_dupe))."""
+    flags, log = [], []
+    for h, fn in hashes:
+        h = int(h)
+        if not prev:
+            prev.append((h, fn))
+            flags.append(False)
+            continue
+        diffs = [(bin(h ^ p).count('1'), pfn) for (p, pfn) in prev[-5:]]
+        md, md_fn = min(diffs, key=lambda a: a[0])
+        log.append((fn, md_fn, md, md <= hash_thr))
+        if md <= hash_thr:
+            flags.append(True)
+        else:
+            prev.append((h, fn))
+            flags.append(False)
+    return flags, log
 
 
 def remove_dupes_overall(X, filenames, dup_params):
