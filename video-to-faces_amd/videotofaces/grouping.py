@@ -145,3 +145,29 @@ def cluster_faces(paths, X, cluster_params):
     for p in paths:
         os.remove(p)
     return clusters, labels, scores
+
+
+def encode_refs(refs, model):
+    """grouping.py:43-47: the first image of every reference class."""
+    return model([_imread(ps[0]) for (_, ps) in refs])
+
+
+def classify_faces(paths, X, model, classif_params):
+    """grouping.py:69-89: classify against reference images, move files into class folders."""
+    refs, thr, log, out_dir = classif_params
+    classes = [c for (c, _) in refs]
+    print('Found %u classes in ref_dir: %s' % (len(classes), ', '.join(classes)))
+    print('Extracting features from reference images')
+    R = encode_refs(refs, model)
+    print('Classifying images')
+    inds, classes = classify(X, R, classes, thr, log, paths, out_dir)
+    img_dir = osp.dirname(osp.abspath(paths[0]))
+    for c in classes:
+        os.makedirs(osp.join(img_dir, c), exist_ok=True)
+    for p, i in zip(paths, inds):
+        os.replace(p, osp.join(img_dir, classes[i], osp.basename(p)))
+    print('Grouped %u images into %u folders:' % (len(paths), len(classes)))
+    for i, c in enumerate(classes):
+        print('%s: %u' % (c, np.count_nonzero(inds == i)))
+    print()
+    return inds, classes
