@@ -36,7 +36,7 @@ def test_video_to_faces_in_memory(tmp_path):
     from videotofaces import synth, video_to_faces
     frames = synth.make_frames(8, seed=3)
     video_to_faces(frames, style='live', out_dir=str(tmp_path), det_batch_size=4, det_min_size=10,
-                   clusters='2-3', enc_batch_size=16)
+                   clusters='2-3', enc_batch_size=16, enc_dup_thr=-1)  # synthetic encoders: near-identical embeddings
     faces = os.path.join(str(tmp_path), 'faces')
     got = [os.path.join(dp, f) for dp, _, fs in os.walk(faces) for f in fs if f.endswith('.jpg')]
     assert got, 'no faces written'
