@@ -246,12 +246,16 @@ __global__ __launch_bounds__(256, 2) void k_pnet(const uint8_t* __restrict__ fra
     }
     const float b1 = lr < 10 ? wc.c1b[lr] : 0.f, a1 = lr < 10 ? wc.p1[lr] : 0.f;
     const float b2 = wc.c2b[lr], a2 = wc.p2[lr];
+    // ---- tiles come from an atomic counter (dynamic: pyramid tiles differ in cost); the next
+    //      index is requested as soon as the current one is known, so the atomic's round trip
+    //      overlaps the tile's work instead of opening it
+    if (tid == 0) s_tile = (int)atomicAdd(tile_ctr, 1u);
     for (;;) {
-        // ---- fetch the next tile (dynamic: pyramid tiles differ in cost)
-        if (tid == 0) s_tile = (int)atomicAdd(tile_ctr, 1u);
         __syncthreads();
         const int64_t blk = s_tile;
         if (blk >= total_tiles) break;
+        uint32_t next_tile = 0;
+        if (tid == 0) next_tile = atomicAdd(tile_ctr, 1u);
         int L = 0;
         while (L + 1 < n_levels && blk >= lv[L + 1].tile_beg) L++;
         const PNetLevel P = lv[L];
@@ -358,41 +362,64 @@ __global__ __launch_bounds__(256, 2) void k_pnet(const uint8_t* __restrict__ fra
             constexpr int NPP = PP_H * PP_W;  // 720 pooled cells
             constexpr int NF1 = NPP / 4;      // 180 fragments
             const int corner = lr & 3, dy = corner >> 1, dx = corner & 1;
+            // the tile's conv1 window lies inside the level: no per-corner bounds checks
+            const bool interior = 2 * (oy0 + PP_H - 1) + 1 < L1h && 2 * (ox0 + PP_W - 1) + 1 < L1w;
+            // PReLU with a non-negative slope is monotone, so max(prelu(v)) == prelu(max(v))
+            // bit for bit (rounding is monotone too): pool first, activate once
+            const bool mono = a1 >= 0.f;
+            int ko[7];
+#pragma unroll
+            for (int s = 0; s < 7; s++) {
+                const int k = min(4 * s + lk, 26);
+                const int c = k / 9, r = k - 9 * c;
+                ko[s] = c * PL_H * PL_W + (r / 3) * PL_W + (r % 3);
+            }
             for (int f0 = wave; f0 < ((o.dbg & 2) ? 0 : NF1); f0 += 8) {
                 const int f1 = f0 + 4;
                 const bool two = f1 < NF1;
                 int pp0 = f0 * 4 + (lr >> 2), pp1 = (two ? f1 : f0) * 4 + (lr >> 2);
                 int ab0 = (2 * (pp0 / PP_W) + dy) * PL_W + 2 * (pp0 % PP_W) + dx;
                 int ab1 = (2 * (pp1 / PP_W) + dy) * PL_W + 2 * (pp1 % PP_W) + dx;
+                float av0[7], av1[7];
+#pragma unroll
+                for (int s = 0; s < 7; s++) {
+                    av0[s] = sA[ab0 + ko[s]];
+                    av1[s] = sA[ab1 + ko[s]];
+                }
+                __builtin_amdgcn_sched_barrier(0);
                 f32x4 c0 = {0.f, 0.f, 0.f, 0.f}, c1 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
                 for (int s = 0; s < 7; s++) {
-                    const int k = min(4 * s + lk, 26);
-                    const int c = k / 9, r = k - 9 * c;
-                    const int ko = c * PL_H * PL_W + (r / 3) * PL_W + (r % 3);
-                    c0 = __builtin_amdgcn_mfma_f32_16x16x4f32(sA[ab0 + ko], w1[s], c0, 0, 0, 0);
-                    c1 = __builtin_amdgcn_mfma_f32_16x16x4f32(sA[ab1 + ko], w1[s], c1, 0, 0, 0);
+                    c0 = __builtin_amdgcn_mfma_f32_16x16x4f32(av0[s], w1[s], c0, 0, 0, 0);
+                    c1 = __builtin_amdgcn_mfma_f32_16x16x4f32(av1[s], w1[s], c1, 0, 0, 0);
                 }
                 if (lr < 10) {
 #pragma unroll
                     for (int h = 0; h < 2; h++) {
                         if (h == 1 && !two) break;
+                        const f32x4 cc = h ? c1 : c0;
                         const int pp = (h ? f1 : f0) * 4 + lk;
-                        const int py = pp / PP_W, px = pp % PP_W;
-                        const int gy = 2 * (oy0 + py), gx = 2 * (ox0 + px);
-                        float m = -3.402823466e38f;
-                        bool any = false;
+                        float out;
+                        if (interior && mono) {
+                            out = prelu(fmaxf(fmaxf(cc[0], cc[1]), fmaxf(cc[2], cc[3])) + b1, a1);
+                        } else {
+                            const int py = pp / PP_W, px = pp % PP_W;
+                            const int gy = 2 * (oy0 + py), gx = 2 * (ox0 + px);
+                            float m = -3.402823466e38f;
+                            bool any = false;
 #pragma unroll
-                        for (int i = 0; i < 4; i++) {
-                            bool ok = (gy + (i >> 1) < L1h) && (gx + (i & 1) < L1w);
-                            float v = prelu((h ? c1[i] : c0[i]) + b1, a1);
-                            if (ok) {
-                                m = fmaxf(m, v);
-                                any = true;
+                            for (int i = 0; i < 4; i++) {
+                                bool ok = (gy + (i >> 1) < L1h) && (gx + (i & 1) < L1w);
+                                float v = prelu(cc[i] + b1, a1);
+                                if (ok) {
+                                    m = fmaxf(m, v);
+                                    any = true;
+                                }
                             }
+                            // outside the valid pooled map (only feeds discarded cells): keep finite
+                            out = any ? m : 0.f;
                         }
-                        // outside the valid pooled map (only feeds discarded cells): keep finite
-                        sP[lr * NPP + pp] = any ? m : 0.f;
+                        sP[lr * NPP + pp] = out;
                     }
                 }
             }
@@ -416,13 +443,25 @@ __global__ __launch_bounds__(256, 2) void k_pnet(const uint8_t* __restrict__ fra
                 int p0 = min(f0 * 16 + lr, NPOS - 1), p1 = min((two ? f1 : f0) * 16 + lr, NPOS - 1);
                 const int ab0 = (p0 / PC_W) * PP_W + (p0 % PC_W), ab1 = (p1 / PC_W) * PP_W + (p1 % PC_W);
                 f32x4 c0 = {0.f, 0.f, 0.f, 0.f}, c1 = {0.f, 0.f, 0.f, 0.f};
+                // operands of a whole group of k-steps are read before its MFMAs (LDS latency
+                // overlapped instead of one wait per MFMA)
 #pragma unroll
-                for (int s = 0; s < 23; s++) {
-                    const int k = min(4 * s + lk, 89);
-                    const int c = k / 9, r = k - 9 * c;
-                    const int ko = c * PP_H * PP_W + (r / 3) * PP_W + (r % 3);
-                    c0 = __builtin_amdgcn_mfma_f32_16x16x4f32(sP[ab0 + ko], w2[s], c0, 0, 0, 0);
-                    c1 = __builtin_amdgcn_mfma_f32_16x16x4f32(sP[ab1 + ko], w2[s], c1, 0, 0, 0);
+                for (int g = 0; g < 23; g += 12) {
+                    float av0[12], av1[12];
+#pragma unroll
+                    for (int s = g; s < min(g + 12, 23); s++) {
+                        const int k = min(4 * s + lk, 89);
+                        const int c = k / 9, r = k - 9 * c;
+                        const int ko = c * PP_H * PP_W + (r / 3) * PP_W + (r % 3);
+                        av0[s - g] = sP[ab0 + ko];
+                        av1[s - g] = sP[ab1 + ko];
+                    }
+                    __builtin_amdgcn_sched_barrier(0);  // keep the reads ahead of the MFMAs
+#pragma unroll
+                    for (int s = g; s < min(g + 12, 23); s++) {
+                        c0 = __builtin_amdgcn_mfma_f32_16x16x4f32(av0[s - g], w2[s], c0, 0, 0, 0);
+                        c1 = __builtin_amdgcn_mfma_f32_16x16x4f32(av1[s - g], w2[s], c1, 0, 0, 0);
+                    }
                 }
 #pragma unroll
                 for (int i = 0; i < 4; i++) {
@@ -547,6 +586,7 @@ __global__ __launch_bounds__(256, 2) void k_pnet(const uint8_t* __restrict__ fra
                 }
             }
         }
+        if (tid == 0) s_tile = (int)next_tile;  // every thread read s_tile before this tile's barriers
         __syncthreads();  // sA/sP are rewritten by the next tile
     }
 }
