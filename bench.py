@@ -137,25 +137,36 @@ def main():
     streams = [torch.cuda.Stream(dev) for _ in range(L)]
     torch.cuda.synchronize(dev)
 
-    def step(lane, i):
+    def detect_step(lane, i):
+        """one det-batch: detect + box post-processing -> crops with frame indices into the
+        resident frame pool (so faces of consecutive det-batches can share encoder batches)."""
         j = (i * B) % pool_n
         fb = frames[j:j + B]
-        det, enc = dets[lane], encs[lane]
-        res = normalize_detout(det(fb)) if yolo else det(fb, args.min_face_size)
-        crops = boxes_to_crops(res, (H, W), **det_params(args))
-        embs = [enc.encode_crops(fb, crops[k:k + args.enc_batch]) for k in range(0, crops.shape[0], args.enc_batch)]
-        return embs, crops.shape[0], sum(r.shape[0] for r in res)
+        res = normalize_detout(dets[lane](fb)) if yolo else dets[lane](fb, args.min_face_size)
+        return boxes_to_crops(res, (H, W), frame_offset=j, **det_params(args)), sum(r.shape[0] for r in res)
 
     def run(first, n):
-        """steps first..first+n-1, step i on lane i % L; returns per-step results in order."""
-        out = [None] * n
+        """steps first..first+n-1, step i on lane i % L.  Each lane feeds its face stream to its
+        encoder in batches of exactly enc_batch (encode_faces, grouping.py:29-40), flushing the
+        remainder at the end.  Returns per-step (n faces, n detections) and the embeddings in
+        global (step, face) order."""
+        stats = [None] * n
+        lane_embs = [[] for _ in range(L)]
         errs = []
 
         def lane_fn(lane):
             try:
                 with torch.cuda.stream(streams[lane]):
+                    pend = []
                     for k in range(lane, n, L):
-                        out[k] = step(lane, first + k)
+                        crops, nd = detect_step(lane, first + k)
+                        stats[k] = (crops.shape[0], nd)
+                        pend.extend(crops.tolist())
+                        while len(pend) >= args.enc_batch:
+                            lane_embs[lane].append(encs[lane].encode_crops(frames, pend[:args.enc_batch]))
+                            pend = pend[args.enc_batch:]
+                    if pend:
+                        lane_embs[lane].append(encs[lane].encode_crops(frames, pend))
             except BaseException as e:  # surfaced after join
                 errs.append(e)
         ths = [threading.Thread(target=lane_fn, args=(l,)) for l in range(L)]
@@ -167,7 +178,14 @@ def main():
             raise errs[0]
         for s in streams:
             s.synchronize()
-        return out
+        # lane streams -> global (step, face) order
+        parts, offs = [], [0] * L
+        flat = [torch.cat(e) if e else torch.zeros((0, 512), device=dev) for e in lane_embs]
+        for k in range(n):
+            lane, nf = k % L, stats[k][0]
+            parts.append(flat[lane][offs[lane]:offs[lane] + nf])
+            offs[lane] += nf
+        return stats, parts
 
     run(0, max(args.warmup, L))
     torch.cuda.synchronize(dev)
@@ -177,10 +195,9 @@ def main():
     for d in dets:
         d.profile(True)
     t0 = time.perf_counter()
-    results = run(args.warmup, args.steps)
-    embs = [e for r in results for e in r[0]]
-    faces = sum(r[1] for r in results)
-    dets_n = sum(r[2] for r in results)
+    stats, embs = run(args.warmup, args.steps)
+    faces = sum(s_[0] for s_ in stats)
+    dets_n = sum(s_[1] for s_ in stats)
     local_emb = torch.cat(embs) if embs else torch.zeros((0, 512), device=dev)
     if world > 1:
         from videotofaces.parallel import all_gather_rows
