@@ -117,10 +117,12 @@ __global__ __launch_bounds__(64) void k_iou_mask(const float4* __restrict__ boxe
     }
     // layout: word (rb, cb, r) at ((rb * nb + cb) * 64 + r): coalesced writes and scan loads
     uint64_t* out = mask + seg_mask_off[t.seg] + (int64_t)t.rb * nb * 64 + lane;
+    // software-pipelined: the next column block's box is loaded while this one is compared
+    float4 bnext = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (t.rb * 64 + lane < m) bnext = load_box(boxes, img, order[beg + t.rb * 64 + lane], ob);
     for (int cb = t.rb; cb < nb; cb++) {
-        int col = cb * 64 + lane;
-        float4 bj = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (col < m) bj = load_box(boxes, img, order[beg + col], ob);
+        const float4 bj = bnext;
+        if (cb + 1 < nb && (cb + 1) * 64 + lane < m) bnext = load_box(boxes, img, order[beg + (cb + 1) * 64 + lane], ob);
         __syncthreads();
         cb_box[lane] = bj;
         cb_area[lane] = (bj.z - bj.x) * (bj.w - bj.y);
@@ -143,14 +145,19 @@ __global__ __launch_bounds__(64) void k_iou_mask(const float4* __restrict__ boxe
     }
 }
 
+// OR over the 64 lanes with DPP row shifts and row broadcasts (VALU, no LDS crossbar):
+// inclusive row scans, then rows folded into lane 63, read back as a wave-uniform value
+__device__ inline uint32_t wave_or32(uint32_t v) {
+    v |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, true);  // row_shr:1
+    v |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, true);  // row_shr:2
+    v |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xf, 0xf, true);  // row_shr:4
+    v |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xf, 0xf, true);  // row_shr:8
+    v |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xa, 0xf, false); // row_bcast:15
+    v |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xc, 0xf, false); // row_bcast:31
+    return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
+}
 __device__ inline uint64_t wave_or(uint64_t v) {
-    uint32_t lo = (uint32_t)v, hi = (uint32_t)(v >> 32);
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) {
-        lo |= __shfl_xor(lo, off);
-        hi |= __shfl_xor(hi, off);
-    }
-    return ((uint64_t)hi << 32) | lo;
+    return ((uint64_t)wave_or32((uint32_t)(v >> 32)) << 32) | wave_or32((uint32_t)v);
 }
 
 // One wave per segment: greedy resolution, 64 rows per step.  The diagonal 64x64 block is
@@ -188,26 +195,21 @@ __global__ __launch_bounds__(64) void k_nms_scan(const uint64_t* __restrict__ ma
         if (row < m) keep_sorted[beg + row] = (uint8_t)((kept >> lane) & 1ull);
         if (kept == 0) continue;
         const bool mine = (kept >> lane) & 1ull;
-        int w = cb + 1;
-        for (; w + 3 < nb; w += 4) {
-            uint64_t v0 = mine ? blk[(int64_t)w * 64] : 0ull;
-            uint64_t v1 = mine ? blk[(int64_t)(w + 1) * 64] : 0ull;
-            uint64_t v2 = mine ? blk[(int64_t)(w + 2) * 64] : 0ull;
-            uint64_t v3 = mine ? blk[(int64_t)(w + 3) * 64] : 0ull;
-            v0 = wave_or(v0);
-            v1 = wave_or(v1);
-            v2 = wave_or(v2);
-            v3 = wave_or(v3);
-            if (lane == 0) {
-                removed[w] |= v0;
-                removed[w + 1] |= v1;
-                removed[w + 2] |= v2;
-                removed[w + 3] |= v3;
+        // the words of all later column blocks are independent loads: issue 8 at a time so one
+        // memory latency covers 8 blocks (the scan is a serial chain of these groups)
+        constexpr int G = 8;
+        for (int w0 = cb + 1; w0 < nb; w0 += G) {
+            uint64_t v[G];
+#pragma unroll
+            for (int g = 0; g < G; g++) {
+                const int w = min(w0 + g, nb - 1);
+                v[g] = blk[(int64_t)w * 64];
             }
-        }
-        for (; w < nb; w++) {
-            uint64_t v = wave_or(mine ? blk[(int64_t)w * 64] : 0ull);
-            if (lane == 0) removed[w] |= v;
+#pragma unroll
+            for (int g = 0; g < G; g++) {
+                const uint64_t r = wave_or(mine ? v[g] : 0ull);
+                if (lane == 0 && w0 + g < nb) removed[w0 + g] |= r;
+            }
         }
         __builtin_amdgcn_wave_barrier();
     }
