@@ -12,6 +12,10 @@
 //   bf16: v_mfma_f32_16x16x32_bf16 (bf16 operands/activations, fp32 accumulate; perf mode)
 // Tile: BM x BN per 256-thread workgroup (2x2 waves, each (BM/2)x(BN/2) = 16x16 fragments),
 // BK-deep K steps, global->register prefetch of step k+1 while step k runs on MFMA from LDS.
+#include <algorithm>
+#include <mutex>
+#include <unordered_map>
+
 #include "common.hpp"
 #include "conv.hpp"
 
@@ -42,7 +46,48 @@ __device__ inline float from_f<float>(float v) { return v; }
 template <>
 __device__ inline __bf16 from_f<__bf16>(float v) { return (__bf16)v; }
 
-template <typename T, int BM, int BN, int BK>
+// fused epilogue of one output element (bias / BN / scale / residual / activation / layout)
+template <typename T>
+__device__ inline void conv_epilogue(const ConvParams& p, int64_t m, int c, float v, float bias, float al, float be) {
+    T* __restrict__ out = (T*)p.out;
+    const T* __restrict__ res = (const T*)p.res;
+    if (p.bias) v = v + bias;
+    if (p.alpha) v = fmaf(v, al, be);
+    if (p.scale != 1.f) v = v * p.scale;
+    int64_t ridx = m * p.res_cstride + c;
+    if (p.res_up2) {
+        int ow = (int)(m % p.OW);
+        int64_t t = m / p.OW;
+        int oh = (int)(t % p.OH);
+        int64_t n = t / p.OH;
+        ridx = ((n * (p.OH >> 1) + (oh >> 1)) * (p.OW >> 1) + (ow >> 1)) * p.res_cstride + c;
+    }
+    if (res && !p.res_post) v = v + to_f(res[ridx]);
+    if (p.relu) v = fmaxf(v, 0.f);
+    if (p.leaky) v = v > 0.f ? v : v * p.slope;
+    if (p.prelu) v = v > 0.f ? v : p.prelu[c] * v;
+    if (p.gelu) v = 0.5f * v * (1.0f + erff(v * 0.70710678118654752f));
+    if (res && p.res_post) v = v + to_f(res[ridx]);
+    if (p.up2) {
+        int ow = (int)(m % p.OW);
+        int64_t t = m / p.OW;
+        int oh = (int)(t % p.OH);
+        int64_t n = t / p.OH;
+        int64_t o = ((n * 2 * p.OH + 2 * oh) * 2 * p.OW + 2 * ow) * p.out_cstride + p.out_coff + c;
+        int64_t rs = (int64_t)2 * p.OW * p.out_cstride;
+        T tv = from_f<T>(v);
+        out[o] = tv;
+        out[o + p.out_cstride] = tv;
+        out[o + rs] = tv;
+        out[o + rs + p.out_cstride] = tv;
+    } else if (p.out_f32) {
+        ((float*)p.out)[m * p.out_cstride + p.out_coff + c] = v;
+    } else {
+        out[m * p.out_cstride + p.out_coff + c] = from_f<T>(v);
+    }
+}
+
+template <typename T, int BM, int BN, int BK, bool SPLIT>
 __global__ __launch_bounds__(256) void k_conv(ConvParams p) {
     using vec = typename VecT<T>::type;
     constexpr int V = VecT<T>::V;
@@ -84,7 +129,11 @@ __global__ __launch_bounds__(256) void k_conv(ConvParams p) {
         a_ih0[r] = oh * p.sh - p.ph;
         a_iw0[r] = ow * p.sw - p.pw;
     }
-    int k = kv * V;
+    // split-K slice z covers k-tiles [kt0, kt1)
+    const int KT_all = (p.K + BK - 1) / BK;
+    const int kt0 = SPLIT ? (int)((int64_t)blockIdx.z * KT_all / p.split) : 0;
+    const int kt1 = SPLIT ? (int)((int64_t)(blockIdx.z + 1) * KT_all / p.split) : KT_all;
+    int k = kt0 * BK + kv * V;
     int ci = k % p.Cin, kw_ = (k / p.Cin) % p.KW, kh_ = (k / p.Cin) / p.KW;
 
     vec ra[RA], rb[RB];
@@ -136,7 +185,7 @@ __global__ __launch_bounds__(256) void k_conv(ConvParams p) {
 #pragma unroll
         for (int j = 0; j < FN; j++) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-    const int KT = (p.K + BK - 1) / BK;
+    const int KT = kt1 - kt0;
     load_tile(k, ci, kw_, kh_);
     store_tile();
     __syncthreads();
@@ -184,75 +233,101 @@ __global__ __launch_bounds__(256) void k_conv(ConvParams p) {
     }
 
     // epilogue: C layout col = lane & 15, row = 4 * (lane >> 4) + i
-    T* __restrict__ out = (T*)p.out;
-    const T* __restrict__ res = (const T*)p.res;
 #pragma unroll
     for (int j = 0; j < FN; j++) {
         int c = n0 + wn * WN + j * 16 + (lane & 15);
         if (c >= p.Cout) continue;
-        float bias = p.bias ? p.bias[c] : 0.f;
-        float al = p.alpha ? p.alpha[c] : 1.f;
-        float be = p.alpha ? p.beta[c] : 0.f;
+        const float bias = !SPLIT && p.bias ? p.bias[c] : 0.f;
+        const float al = !SPLIT && p.alpha ? p.alpha[c] : 1.f;
+        const float be = !SPLIT && p.alpha ? p.beta[c] : 0.f;
 #pragma unroll
         for (int i = 0; i < FM; i++) {
 #pragma unroll
             for (int q = 0; q < 4; q++) {
                 int64_t m = m0 + wm * WM + i * 16 + 4 * (lane >> 4) + q;
                 if (m >= p.M) continue;
-                float v = acc[i][j][q];
-                if (p.bias) v = v + bias;
-                if (p.alpha) v = fmaf(v, al, be);
-                if (p.scale != 1.f) v = v * p.scale;
-                int64_t ridx = m * p.res_cstride + c;
-                if (p.res_up2) {
-                    int ow = (int)(m % p.OW);
-                    int64_t t = m / p.OW;
-                    int oh = (int)(t % p.OH);
-                    int64_t n = t / p.OH;
-                    ridx = ((n * (p.OH >> 1) + (oh >> 1)) * (p.OW >> 1) + (ow >> 1)) * p.res_cstride + c;
-                }
-                if (res && !p.res_post) v = v + to_f(res[ridx]);
-                if (p.relu) v = fmaxf(v, 0.f);
-                if (p.leaky) v = v > 0.f ? v : v * p.slope;
-                if (p.prelu) v = v > 0.f ? v : p.prelu[c] * v;
-                if (p.gelu) v = 0.5f * v * (1.0f + erff(v * 0.70710678118654752f));
-                if (res && p.res_post) v = v + to_f(res[ridx]);
-                if (p.up2) {
-                    int ow = (int)(m % p.OW);
-                    int64_t t = m / p.OW;
-                    int oh = (int)(t % p.OH);
-                    int64_t n = t / p.OH;
-                    int64_t o = ((n * 2 * p.OH + 2 * oh) * 2 * p.OW + 2 * ow) * p.out_cstride + p.out_coff + c;
-                    int64_t rs = (int64_t)2 * p.OW * p.out_cstride;
-                    T tv = from_f<T>(v);
-                    out[o] = tv;
-                    out[o + p.out_cstride] = tv;
-                    out[o + rs] = tv;
-                    out[o + rs + p.out_cstride] = tv;
-                } else if (p.out_f32) {
-                    ((float*)p.out)[m * p.out_cstride + p.out_coff + c] = v;
-                } else {
-                    out[m * p.out_cstride + p.out_coff + c] = from_f<T>(v);
-                }
+                if constexpr (SPLIT)
+                    p.ws[((int64_t)blockIdx.z * p.M + m) * p.Cout + c] = acc[i][j][q];
+                else
+                    conv_epilogue<T>(p, m, c, acc[i][j][q], bias, al, be);
             }
         }
     }
 }
 
+// split-K: sum the partial slabs in slice order (deterministic), then the fused epilogue
+template <typename T>
+__global__ void k_conv_splitk_epi(ConvParams p) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= p.M * p.Cout) return;
+    const int c = (int)(i % p.Cout);
+    const int64_t m = i / p.Cout;
+    float v = 0.f;
+    for (int z = 0; z < p.split; z++) v += p.ws[((int64_t)z * p.M + m) * p.Cout + c];
+    conv_epilogue<T>(p, m, c, v, p.bias ? p.bias[c] : 0.f, p.alpha ? p.alpha[c] : 1.f, p.alpha ? p.beta[c] : 0.f);
+}
+
+// per-stream split-K workspace (lanes run concurrently on their own streams); grows, never shrinks
+static float* splitk_workspace(hipStream_t st, size_t bytes) {
+    static std::mutex mu;
+    static std::unordered_map<hipStream_t, std::pair<float*, size_t>> ws;
+    std::lock_guard<std::mutex> g(mu);
+    auto& e = ws[st];
+    if (e.second < bytes) {
+        if (e.first) {
+            VTF_HIP(hipStreamSynchronize(st));
+            VTF_HIP(hipFree(e.first));
+        }
+        e.first = nullptr;
+        e.second = 0;
+        VTF_HIP(hipMalloc((void**)&e.first, bytes));
+        e.second = bytes;
+    }
+    return e.first;
+}
+
+// split factor: grids far below the CU count (FaceNet Block17/Block8, YOLO/R-CNN deep stages at
+// small batch) are split along K into up to 8 slices so ~2 workgroups land on every CU. bf16
+// (perf) mode only: the fp32 parity mode keeps the single-pass summation order.
+static int pick_split(int64_t tiles, int KT, bool bf16) {
+    if (!bf16 || tiles >= 192 || KT < 8) return 1;
+    int s = (int)std::min<int64_t>(8, (512 + tiles - 1) / tiles);
+    s = std::min(s, KT / 4);
+    return s < 2 ? 1 : s;
+}
+
+template <typename T, int BM, int BN, int BK>
+static void launch_tile(const ConvParams& p0, hipStream_t st) {
+    ConvParams p = p0;
+    const int64_t gx = cdiv(p.M, BM), gy = cdiv(p.Cout, BN);
+    const int KT = (p.K + BK - 1) / BK;
+    p.split = pick_split(gx * gy, KT, sizeof(T) == 2);
+    p.ws = nullptr;
+    if (p.split > 1) p.ws = splitk_workspace(st, (size_t)p.split * p.M * p.Cout * sizeof(float));
+    dim3 g((unsigned)gx, (unsigned)gy, (unsigned)p.split);
+    if constexpr (sizeof(T) == 2) {
+        if (p.split > 1) {
+            k_conv<T, BM, BN, BK, true><<<g, 256, 0, st>>>(p);
+            const int64_t n = p.M * p.Cout;
+            k_conv_splitk_epi<T><<<(unsigned)cdiv(n, 256), 256, 0, st>>>(p);
+            return;
+        }
+    }
+    k_conv<T, BM, BN, BK, false><<<g, 256, 0, st>>>(p);
+}
+
 template <typename T>
 static void launch_t(const ConvParams& p, hipStream_t st) {
     if (p.Cout <= 32) {
-        dim3 g(cdiv(p.M, 128), cdiv(p.Cout, 32));
         if constexpr (sizeof(T) == 2)
-            k_conv<T, 128, 32, 64><<<g, 256, 0, st>>>(p);
+            launch_tile<T, 128, 32, 64>(p, st);
         else
-            k_conv<T, 128, 32, 32><<<g, 256, 0, st>>>(p);
+            launch_tile<T, 128, 32, 32>(p, st);
     } else {
-        dim3 g(cdiv(p.M, 128), cdiv(p.Cout, 64));
         if constexpr (sizeof(T) == 2)
-            k_conv<T, 128, 64, 64><<<g, 256, 0, st>>>(p);
+            launch_tile<T, 128, 64, 64>(p, st);
         else
-            k_conv<T, 128, 64, 32><<<g, 256, 0, st>>>(p);
+            launch_tile<T, 128, 64, 32>(p, st);
     }
 }
 

@@ -24,6 +24,8 @@ struct ConvParams {
                          // map: the FPN top-down add, rcnn.py:26-27)
     int in_cstride;      // input channel stride (0 = Cin): read a channel slice of a concat buffer
     int out_f32;         // output is fp32 whatever the operand precision (detector heads)
+    int split;           // split-K factor (set by launch_conv; > 1: raw partial sums to ws)
+    float* ws;           // fp32 [split][M][Cout] partial sums (split-K only)
     int64_t M;           // N*OH*OW
     int N, H, W, Cin, OH, OW, Cout, KH, KW, sh, sw, ph, pw, K;
     int out_cstride, out_coff, res_cstride;
