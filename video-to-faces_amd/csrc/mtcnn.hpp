@@ -55,6 +55,6 @@ void launch_landmarks(const float4* boxes, const float* lm, int64_t n, float* ou
 void launch_iom_chain(const float4* boxes, const int32_t* img, const int32_t* order, int64_t n, float thr,
                       int32_t* keep, hipStream_t st);
 
-constexpr int PNET_TH = 16, PNET_TW = 32;
+constexpr int PNET_TH = 24, PNET_TW = 16;  // k_pnet output cells per tile (rows, cols)
 
 }  // namespace vtf

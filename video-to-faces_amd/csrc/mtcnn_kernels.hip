@@ -6,8 +6,8 @@
 //
 // MI355X design:
 //   * k_pnet: ONE launch per det-batch covers every pyramid level of every frame.  Each
-//     256-thread workgroup owns a 16x32 tile of PNet output cells.  The level pixels it
-//     needs (42x74x3) are computed on the fly from the uint8 BGR frame (preprocess +
+//     256-thread workgroup owns a PNET_TH x PNET_TW (24x16) tile of PNet output cells.  The
+//     level pixels it needs ((2TH+10)x(2TW+10)x3) are computed on the fly from the uint8 BGR frame (preprocess +
 //     adaptive_avg_pool2d, bit-exact: exact (u-127.5)/128, row-major fp32 bin sum, /kh, /kw)
 //     straight into LDS, so the 10.7 Mpx/frame pyramid never exists in HBM (large-bin
 //     downsampled levels come from the frame's summed-area table, k_resample_sat).  conv1+PReLU+
@@ -204,7 +204,8 @@ void launch_resample_sat(const int4* sat, int B, int H, int W, int lh, int lw, f
 
 // ----------------------------------------------------------------------------------- PNet
 
-constexpr int PT_H = 16, PT_W = 32;                   // output cells per tile
+constexpr int PT_H = PNET_TH, PT_W = PNET_TW;         // output cells per tile (mtcnn.hpp)
+static_assert(PT_W % 16 == 0 && (PT_H * PT_W) % 64 == 0, "conv3 fragments are 16-cell row runs, 4 waves");
 constexpr int PL_H = 2 * PT_H + 10, PL_W = 2 * PT_W + 10;  // level tile 42 x 74
 constexpr int PP_H = PT_H + 4, PP_W = PT_W + 4;       // pooled 20 x 36
 constexpr int PC_H = PT_H + 2, PC_W = PT_W + 2;       // conv2 out 18 x 34
@@ -219,16 +220,24 @@ __device__ inline float div_bin(float x, int k) {
     return (k & (k - 1)) == 0 ? x * __int_as_float((127 - __builtin_ctz(k)) << 23) : __fdiv_rn(x, (float)k);
 }
 
-constexpr int PNET_GROUPS_PER_CU = 2;
+// workgroups per CU from the LDS footprint (160 KB per CU)
+constexpr int PNET_LDS = (P_A + P_POOL) * 4 + (PL_H + PL_W) * 8 + 16;
+constexpr int PNET_GROUPS_PER_CU = (160 * 1024) / PNET_LDS;
+static_assert(PNET_GROUPS_PER_CU >= 2, "k_pnet tile too large for 2 workgroups per CU");
 constexpr int PATCH_BYTES = P_POOL * 4;  // frame patch staged in the (not yet used) pooled buffer
 
 template <bool DENSE>
-__global__ __launch_bounds__(256, 2) void k_pnet(const uint8_t* __restrict__ frames, int64_t frame_stride,
+__global__ __launch_bounds__(256, PNET_GROUPS_PER_CU) void k_pnet(const uint8_t* __restrict__ frames, int64_t frame_stride,
                                                  int64_t row_stride, int H, int W,
                                                  const PNetLevel* __restrict__ lv, int n_levels,
                                                  int64_t total_tiles, uint32_t* __restrict__ tile_ctr, PNetW wg,
                                                  PNetOut o) {
     const auto wc = to_const(wg);
+    // conv2 / conv3 weights through buffer loads: one lane VGPR offset + constant SGPR offsets,
+    // instead of a 64-bit address per k-step (which the compiler would keep live across tiles);
+    // (k rows 90, 91 of conv2 are zeroed explicitly: soffset is outside the range check)
+    const __amdgpu_buffer_rsrc_t rw2 = __builtin_amdgcn_make_buffer_rsrc((void*)wg.c2w, 0, 90 * 16 * 4, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rw3 = __builtin_amdgcn_make_buffer_rsrc((void*)wg.c3w, 0, 144 * 32 * 4, 0x00020000);
     __shared__ float sA[P_A];     // level tile, later conv2 output
     __shared__ float sP[P_POOL];  // frame patch (u8) during the fill, then pooled conv1
     __shared__ int2 ybin[PL_H], xbin[PL_W];
@@ -238,13 +247,6 @@ __global__ __launch_bounds__(256, 2) void k_pnet(const uint8_t* __restrict__ fra
     const int lr = lane & 15, lk = lane >> 4;
 
     // ---- weights and im2col offsets, loaded once per persistent workgroup
-    float w1[7];
-#pragma unroll
-    for (int s = 0; s < 7; s++) {
-        int k = 4 * s + lk;
-        w1[s] = (k < 27 && lr < 10) ? wc.c1w[k * 10 + lr] : 0.f;
-    }
-    const float b1 = lr < 10 ? wc.c1b[lr] : 0.f, a1 = lr < 10 ? wc.p1[lr] : 0.f;
     const float b2 = wc.c2b[lr], a2 = wc.p2[lr];
     // ---- tiles come from an atomic counter (dynamic: pyramid tiles differ in cost); the next
     //      index is requested as soon as the current one is known, so the atomic's round trip
@@ -266,6 +268,10 @@ __global__ __launch_bounds__(256, 2) void k_pnet(const uint8_t* __restrict__ fra
         const int oy0 = (tt / P.tiles_x) * PT_H, ox0 = (tt % P.tiles_x) * PT_W;
         const uint8_t* fr = frames + (int64_t)b * frame_stride;
         const int L1h = P.lh - 2, L1w = P.lw - 2;
+        // lane coordinates laundered per tile: per-lane addressing below is recomputed inside the
+        // tile instead of being hoisted out of the persistent loop into long-lived registers
+        int lrx = lr, lkx = lk;
+        asm volatile("" : "+v"(lrx), "+v"(lkx));
 
         // ---- 1. level tile (rows 2*oy0 .. +42, cols 2*ox0 .. +74) = MTCNN._resample of the
         //         preprocessed frame, bit-exact; zero outside the level.
@@ -355,72 +361,72 @@ __global__ __launch_bounds__(256, 2) void k_pnet(const uint8_t* __restrict__ fra
         }
         __syncthreads();
 
-        // ---- 2. conv1 (3->10, 3x3) + PReLU + maxpool 2x2 ceil on MFMA.  A row r of fragment
-        //         f is conv1 position (2py+dy, 2px+dx) of pooled cell pp = 4f + r/4, corner r%4,
-        //         so each lane's 4 accumulators (rows 4*lk..4*lk+3) ARE one pooling window.
+        // ---- 2. conv1 (3->10, 3x3) + PReLU + maxpool 2x2 ceil on the VALU.  conv1 has N = 10
+        //         output channels: on a 16-wide MFMA tile 6/16 of the matrix pipe would be padding,
+        //         so it runs as fmaf chains with the weights wave-uniform in SGPRs (scalar loads),
+        //         one lane per pooled cell (its 2x2 conv1 window from a 3x4x4 input patch in
+        //         registers), 5 channels per wave task -- and leaves the matrix pipe to the other
+        //         workgroups' conv2 / conv3 on the same CU.
         {
-            constexpr int NPP = PP_H * PP_W;  // 720 pooled cells
-            constexpr int NF1 = NPP / 4;      // 180 fragments
-            const int corner = lr & 3, dy = corner >> 1, dx = corner & 1;
+            constexpr int NPP = PP_H * PP_W;        // pooled cells
+            constexpr int NCH = (NPP + 63) / 64;    // 64-cell chunks
+            constexpr int CG = 5;                   // channels per wave task
+            constexpr int NWT = (10 / CG) * NCH;    // wave tasks
             // the tile's conv1 window lies inside the level: no per-corner bounds checks
             const bool interior = 2 * (oy0 + PP_H - 1) + 1 < L1h && 2 * (ox0 + PP_W - 1) + 1 < L1w;
-            // PReLU with a non-negative slope is monotone, so max(prelu(v)) == prelu(max(v))
-            // bit for bit (rounding is monotone too): pool first, activate once
-            const bool mono = a1 >= 0.f;
-            int ko[7];
+            const int wv = __builtin_amdgcn_readfirstlane(wave);
+            for (int wt = wv; wt < ((o.dbg & 2) ? 0 : NWT); wt += 4) {
+                const int g = wt / NCH, chunk = wt - g * NCH;
+                const bool live = chunk * 64 + lane < NPP;
+                const int pp = min(chunk * 64 + lane, NPP - 1);
+                const int py = pp / PP_W, px = pp - py * PP_W;
+                const float* src = sA + (2 * py) * PL_W + 2 * px;
+                float x[3][4][4];
 #pragma unroll
-            for (int s = 0; s < 7; s++) {
-                const int k = min(4 * s + lk, 26);
-                const int c = k / 9, r = k - 9 * c;
-                ko[s] = c * PL_H * PL_W + (r / 3) * PL_W + (r % 3);
-            }
-            for (int f0 = wave; f0 < ((o.dbg & 2) ? 0 : NF1); f0 += 8) {
-                const int f1 = f0 + 4;
-                const bool two = f1 < NF1;
-                int pp0 = f0 * 4 + (lr >> 2), pp1 = (two ? f1 : f0) * 4 + (lr >> 2);
-                int ab0 = (2 * (pp0 / PP_W) + dy) * PL_W + 2 * (pp0 % PP_W) + dx;
-                int ab1 = (2 * (pp1 / PP_W) + dy) * PL_W + 2 * (pp1 % PP_W) + dx;
-                float av0[7], av1[7];
+                for (int c = 0; c < 3; c++)
 #pragma unroll
-                for (int s = 0; s < 7; s++) {
-                    av0[s] = sA[ab0 + ko[s]];
-                    av1[s] = sA[ab1 + ko[s]];
-                }
-                __builtin_amdgcn_sched_barrier(0);
-                f32x4 c0 = {0.f, 0.f, 0.f, 0.f}, c1 = {0.f, 0.f, 0.f, 0.f};
+                    for (int r = 0; r < 4; r++)
 #pragma unroll
-                for (int s = 0; s < 7; s++) {
-                    c0 = __builtin_amdgcn_mfma_f32_16x16x4f32(av0[s], w1[s], c0, 0, 0, 0);
-                    c1 = __builtin_amdgcn_mfma_f32_16x16x4f32(av1[s], w1[s], c1, 0, 0, 0);
-                }
-                if (lr < 10) {
+                        for (int q = 0; q < 4; q++) x[c][r][q] = src[c * PL_H * PL_W + r * PL_W + q];
+                const int gy = 2 * (oy0 + py), gx = 2 * (ox0 + px);
 #pragma unroll
-                    for (int h = 0; h < 2; h++) {
-                        if (h == 1 && !two) break;
-                        const f32x4 cc = h ? c1 : c0;
-                        const int pp = (h ? f1 : f0) * 4 + lk;
-                        float out;
-                        if (interior && mono) {
-                            out = prelu(fmaxf(fmaxf(cc[0], cc[1]), fmaxf(cc[2], cc[3])) + b1, a1);
-                        } else {
-                            const int py = pp / PP_W, px = pp % PP_W;
-                            const int gy = 2 * (oy0 + py), gx = 2 * (ox0 + px);
-                            float m = -3.402823466e38f;
-                            bool any = false;
+                for (int j = 0; j < CG; j++) {
+                    const int co = g * CG + j;
+                    float acc[4] = {0.f, 0.f, 0.f, 0.f};  // corners (dy, dx) = (0,0) (0,1) (1,0) (1,1)
 #pragma unroll
-                            for (int i = 0; i < 4; i++) {
-                                bool ok = (gy + (i >> 1) < L1h) && (gx + (i & 1) < L1w);
-                                float v = prelu(cc[i] + b1, a1);
-                                if (ok) {
-                                    m = fmaxf(m, v);
-                                    any = true;
-                                }
+                    for (int c = 0; c < 3; c++)
+#pragma unroll
+                        for (int ky = 0; ky < 3; ky++)
+#pragma unroll
+                            for (int kx = 0; kx < 3; kx++) {
+                                const float w = wc.c1w[co * 27 + (c * 3 + ky) * 3 + kx];  // [co][ci][ky][kx]
+                                acc[0] = fmaf(x[c][ky][kx], w, acc[0]);
+                                acc[1] = fmaf(x[c][ky][kx + 1], w, acc[1]);
+                                acc[2] = fmaf(x[c][ky + 1][kx], w, acc[2]);
+                                acc[3] = fmaf(x[c][ky + 1][kx + 1], w, acc[3]);
                             }
-                            // outside the valid pooled map (only feeds discarded cells): keep finite
-                            out = any ? m : 0.f;
+                    const float bb = wc.c1b[co], aa = wc.p1[co];
+                    float out;
+                    if (interior && aa >= 0.f) {
+                        // PReLU with a non-negative slope is monotone, so max(prelu(v)) ==
+                        // prelu(max(v)) bit for bit (rounding is monotone too): pool, then activate
+                        out = prelu(fmaxf(fmaxf(acc[0], acc[1]), fmaxf(acc[2], acc[3])) + bb, aa);
+                    } else {
+                        float m = -3.402823466e38f;
+                        bool any = false;
+#pragma unroll
+                        for (int i = 0; i < 4; i++) {
+                            const bool ok = (gy + (i >> 1) < L1h) && (gx + (i & 1) < L1w);
+                            const float v = prelu(acc[i] + bb, aa);
+                            if (ok) {
+                                m = fmaxf(m, v);
+                                any = true;
+                            }
                         }
-                        sP[lr * NPP + pp] = out;
+                        // outside the valid pooled map (only feeds discarded cells): keep finite
+                        out = any ? m : 0.f;
                     }
+                    if (live) sP[co * NPP + pp] = out;
                 }
             }
         }
@@ -432,15 +438,15 @@ __global__ __launch_bounds__(256, 2) void k_pnet(const uint8_t* __restrict__ fra
             constexpr int NPOS = PC_H * PC_W;      // 612
             constexpr int NF = (NPOS + 15) / 16;   // 39
             float w2[23];  // per tile (L1-resident): keeps the persistent register set small
+            const int w2off = (16 * lkx + lrx) * 4;
 #pragma unroll
-            for (int s = 0; s < 23; s++) {
-                int k = 4 * s + lk;
-                w2[s] = k < 90 ? wc.c2w[k * 16 + lr] : 0.f;
-            }
+            for (int s = 0; s < 23; s++)
+                w2[s] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rw2, w2off, 256 * s, 0));
+            if (lkx >= 2) w2[22] = 0.f;  // k = 90, 91: zero padding
             for (int f0 = wave; f0 < ((o.dbg & 4) ? 0 : NF); f0 += 8) {
                 const int f1 = f0 + 4;
                 const bool two = f1 < NF;
-                int p0 = min(f0 * 16 + lr, NPOS - 1), p1 = min((two ? f1 : f0) * 16 + lr, NPOS - 1);
+                int p0 = min(f0 * 16 + lrx, NPOS - 1), p1 = min((two ? f1 : f0) * 16 + lrx, NPOS - 1);
                 const int ab0 = (p0 / PC_W) * PP_W + (p0 % PC_W), ab1 = (p1 / PC_W) * PP_W + (p1 % PC_W);
                 f32x4 c0 = {0.f, 0.f, 0.f, 0.f}, c1 = {0.f, 0.f, 0.f, 0.f};
                 // operands of a whole group of k-steps are read before its MFMAs (LDS latency
@@ -450,7 +456,7 @@ __global__ __launch_bounds__(256, 2) void k_pnet(const uint8_t* __restrict__ fra
                     float av0[12], av1[12];
 #pragma unroll
                     for (int s = g; s < min(g + 12, 23); s++) {
-                        const int k = min(4 * s + lk, 89);
+                        const int k = min(4 * s + lkx, 89);
                         const int c = k / 9, r = k - 9 * c;
                         const int ko = c * PP_H * PP_W + (r / 3) * PP_W + (r % 3);
                         av0[s - g] = sP[ab0 + ko];
@@ -465,10 +471,10 @@ __global__ __launch_bounds__(256, 2) void k_pnet(const uint8_t* __restrict__ fra
                 }
 #pragma unroll
                 for (int i = 0; i < 4; i++) {
-                    int q0 = f0 * 16 + 4 * lk + i;
-                    if (q0 < NPOS) sA[lr * NPOS + q0] = prelu(c0[i] + b2, a2);
-                    int q1 = f1 * 16 + 4 * lk + i;
-                    if (two && q1 < NPOS) sA[lr * NPOS + q1] = prelu(c1[i] + b2, a2);
+                    int q0 = f0 * 16 + 4 * lkx + i;
+                    if (q0 < NPOS) sA[lrx * NPOS + q0] = prelu(c0[i] + b2, a2);
+                    int q1 = f1 * 16 + 4 * lkx + i;
+                    if (two && q1 < NPOS) sA[lrx * NPOS + q1] = prelu(c1[i] + b2, a2);
                 }
             }
         }
@@ -479,59 +485,66 @@ __global__ __launch_bounds__(256, 2) void k_pnet(const uint8_t* __restrict__ fra
         //         the 1x1 heads are one more MFMA chain summing over the accumulator rows with no
         //         lane movement: Heads^T (16 x cells) = Wh^T (16 x 32) x F (32 x cells), the
         //         k-slot of lane group g at step i being channel 16*mf + 4g + i.
-        //         Each wave owns 8 cell fragments (64 accumulator VGPRs); the weights stream
-        //         through registers in 4 chunks of 9 k-steps.
+        //         Each wave owns FPW cell fragments (8*FPW accumulator VGPRs); the weights
+        //         stream through registers in 4 chunks of 9 k-steps.
         {
-            f32x4 acc[8][2];
+            constexpr int FPW = PT_H * PT_W / 64;  // 16-cell fragments per wave
+            f32x4 acc[FPW][2];
 #pragma unroll
-            for (int j = 0; j < 8; j++) acc[j][0] = acc[j][1] = f32x4{0.f, 0.f, 0.f, 0.f};
-            int ab[8];
+            for (int j = 0; j < FPW; j++) acc[j][0] = acc[j][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+            int ab[FPW];
 #pragma unroll
-            for (int j = 0; j < 8; j++) {
-                const int f = wave * 8 + j;
-                ab[j] = (f >> 1) * PC_W + (f & 1) * 16 + lr;
+            for (int j = 0; j < FPW; j++) {
+                const int cell = (wave * FPW + j) * 16 + lrx;
+                ab[j] = (cell / PT_W) * PC_W + (cell % PT_W);
             }
             const int nchunk = (o.dbg & 8) ? 0 : 4;
-            for (int sc = 0; sc < nchunk; sc++) {
+            // k-step s = (tap s/4, channel 4*(s%4) + lkx): the LDS offset is the lane-group base
+            // lkx * plane plus a compile-time constant (an instruction immediate, no registers)
+            const float* sAl = sA + lkx * (PC_H * PC_W);
+            const int w3off = (lkx * 9 * 32 + lrx) * 4;
+#pragma unroll
+            for (int sc = 0; sc < 4; sc++) {
+                if (sc >= nchunk) break;
                 float w3[9][2];
 #pragma unroll
                 for (int t = 0; t < 9; t++) {
-                    const int k = 4 * (9 * sc + t) + lk;
-                    w3[t][0] = wc.c3w[k * 32 + lr];
-                    w3[t][1] = wc.c3w[k * 32 + 16 + lr];
+                    const int st = 9 * sc + t, tap = st >> 2, cq = st & 3;
+                    w3[t][0] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rw3, w3off, ((4 * cq * 9 + tap) * 32) * 4, 0));
+                    w3[t][1] = __uint_as_float(
+                        __builtin_amdgcn_raw_buffer_load_b32(rw3, w3off, ((4 * cq * 9 + tap) * 32 + 16) * 4, 0));
                 }
 #pragma unroll
                 for (int t = 0; t < 9; t++) {
-                    const int k = 4 * (9 * sc + t) + lk;
-                    const int c = k / 9, r = k - 9 * c;
-                    const int ko = c * PC_H * PC_W + (r / 3) * PC_W + (r % 3);
+                    const int st = 9 * sc + t, tap = st >> 2, cq = st & 3;
+                    const int ko = 4 * cq * PC_H * PC_W + (tap / 3) * PC_W + (tap % 3);
 #pragma unroll
-                    for (int j = 0; j < 8; j++) {
-                        const float bv = sA[ab[j] + ko];
+                    for (int j = 0; j < FPW; j++) {
+                        const float bv = sAl[ab[j] + ko];
                         acc[j][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(w3[t][0], bv, acc[j][0], 0, 0, 0);
                         acc[j][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(w3[t][1], bv, acc[j][1], 0, 0, 0);
                     }
                 }
             }
-            // accumulator row (mf, lk, i) = channel 16*mf + 4*lk + i
+            // accumulator row (mf, lkx, i) = channel 16*mf + 4*lkx + i
             float cb3[2][4], ca3[2][4], hwA[2][4];
 #pragma unroll
             for (int mf = 0; mf < 2; mf++)
 #pragma unroll
                 for (int i = 0; i < 4; i++) {
-                    const int ch = 16 * mf + 4 * lk + i;
+                    const int ch = 16 * mf + 4 * lkx + i;
                     cb3[mf][i] = wc.c3b[ch];
                     ca3[mf][i] = wc.p3[ch];
-                    // heads as the A operand: row = head lr (0,1 conv4_1; 2..5 conv4_2), k-slot = ch
-                    const int hrow = lr < 2 ? lr * 32 + ch : (lr < 6 ? (lr - 2) * 32 + ch : 0);
-                    const float hv = lr < 2 ? wc.c41w[hrow] : wc.c42w[hrow];
-                    hwA[mf][i] = lr < 6 ? hv : 0.f;
+                    // heads as the A operand: row = head lrx (0,1 conv4_1; 2..5 conv4_2), k-slot = ch
+                    const int hrow = lrx < 2 ? lrx * 32 + ch : (lrx < 6 ? (lrx - 2) * 32 + ch : 0);
+                    const float hv = lrx < 2 ? wc.c41w[hrow] : wc.c42w[hrow];
+                    hwA[mf][i] = lrx < 6 ? hv : 0.f;
                 }
             const float hb0 = wc.c41b[0], hb1 = wc.c41b[1], hb2 = wc.c42b[0], hb3 = wc.c42b[1];
             const float hb4 = wc.c42b[2], hb5 = wc.c42b[3];
 #pragma unroll
-            for (int j = 0; j < 8; j++) {
-                const int f = wave * 8 + j;
+            for (int j = 0; j < FPW; j++) {
+                const int cell = (wave * FPW + j) * 16 + lrx;
                 f32x4 hacc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
                 for (int i = 0; i < 4; i++) {
@@ -540,11 +553,11 @@ __global__ __launch_bounds__(256, 2) void k_pnet(const uint8_t* __restrict__ fra
                     hacc = __builtin_amdgcn_mfma_f32_16x16x4f32(hwA[0][i], fa, hacc, 0, 0, 0);
                     hacc = __builtin_amdgcn_mfma_f32_16x16x4f32(hwA[1][i], fb, hacc, 0, 0, 0);
                 }
-                // hacc: lane (cell lr, heads 4*lk + i): group 0 = (a0, a1, r0, r1), group 1 = (r2, r3, -, -)
+                // hacc: lane (cell lrx, heads 4*lkx + i): group 0 = (a0, a1, r0, r1), group 1 = (r2, r3, -, -)
                 const float r2 = __shfl_down(hacc[0], 16), r3 = __shfl_down(hacc[1], 16);
-                const int y = f >> 1, x = (f & 1) * 16 + lr;
+                const int y = cell / PT_W, x = cell % PT_W;
                 const int oy = oy0 + y, ox = ox0 + x;
-                const bool valid = (lk == 0) && (oy < P.ph) && (ox < P.pw);
+                const bool valid = (lkx == 0) && (oy < P.ph) && (ox < P.pw);
                 const float a0 = hacc[0] + hb0, a1v = hacc[1] + hb1;
                 const float mx = fmaxf(a0, a1v);
                 const float e0 = expf(a0 - mx), e1 = expf(a1v - mx);

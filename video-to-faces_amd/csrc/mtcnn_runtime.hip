@@ -72,10 +72,11 @@ static void build_weights(Mtcnn& m, const float* params, int64_t n_params) {
     struct P {
         const char* name;
         int co, ci, kh, kw;  // conv: co,ci,kh,kw; dense: co=out, ci=in, kh=kw=0; vec: co=n, ci=0
-        int kind;            // 0 vec, 1 conv (transpose), 2 dense (keep [out][in]), 3 dense transposed
+        int kind;            // 0 vec, 1 conv (transpose), 2 dense (keep [out][in]), 3 dense transposed,
+                             // 4 conv kept [co][ci][kh][kw] (PNet conv1: per-channel rows for scalar loads)
     };
     static const P spec[] = {
-        {"pnet.conv1.w", 10, 3, 3, 3, 1},   {"pnet.conv1.b", 10, 0, 0, 0, 0},   {"pnet.prelu1", 10, 0, 0, 0, 0},
+        {"pnet.conv1.w", 10, 3, 3, 3, 4},   {"pnet.conv1.b", 10, 0, 0, 0, 0},   {"pnet.prelu1", 10, 0, 0, 0, 0},
         {"pnet.conv2.w", 16, 10, 3, 3, 1},  {"pnet.conv2.b", 16, 0, 0, 0, 0},   {"pnet.prelu2", 16, 0, 0, 0, 0},
         {"pnet.conv3.w", 32, 16, 3, 3, 1},  {"pnet.conv3.b", 32, 0, 0, 0, 0},   {"pnet.prelu3", 32, 0, 0, 0, 0},
         {"pnet.conv4_1.w", 2, 32, 0, 0, 2}, {"pnet.conv4_1.b", 2, 0, 0, 0, 0},  {"pnet.conv4_2.w", 4, 32, 0, 0, 2},
@@ -100,7 +101,7 @@ static void build_weights(Mtcnn& m, const float* params, int64_t n_params) {
     int64_t src = 0;
     for (int i = 0; i < NP; i++) {
         const P& p = spec[i];
-        int64_t n = (p.kind == 0) ? p.co : (p.kind == 1 ? (int64_t)p.co * p.ci * p.kh * p.kw : (int64_t)p.co * p.ci);
+        int64_t n = (p.kind == 0) ? p.co : (p.kind == 1 || p.kind == 4 ? (int64_t)p.co * p.ci * p.kh * p.kw : (int64_t)p.co * p.ci);
         VTF_CHECK(src + n <= n_params, VTF_E_ARG, "mtcnn: parameter buffer too small");
         off[i] = (int64_t)host.size();
         const float* s = params + src;
@@ -111,7 +112,7 @@ static void build_weights(Mtcnn& m, const float* params, int64_t n_params) {
         } else if (p.kind == 3) {
             for (int k = 0; k < p.ci; k++)
                 for (int co = 0; co < p.co; co++) host.push_back(s[(int64_t)co * p.ci + k]);
-        } else {
+        } else {  // kinds 0, 2, 4: reference layout
             host.insert(host.end(), s, s + n);
         }
         while (host.size() % 4) host.push_back(0.f);  // 16-B alignment for every tensor
@@ -133,7 +134,7 @@ static void build_weights(Mtcnn& m, const float* params, int64_t n_params) {
         for (int i = 0; i < NP; i++) {
             const P& p = spec[i];
             raw[i] = params + o;
-            o += (p.kind == 0) ? p.co : (p.kind == 1 ? (int64_t)p.co * p.ci * p.kh * p.kw : (int64_t)p.co * p.ci);
+            o += (p.kind == 0) ? p.co : (p.kind == 1 || p.kind == 4 ? (int64_t)p.co * p.ci * p.kh * p.kw : (int64_t)p.co * p.ci);
         }
     }
     // conv-kernel layers: weights [Cout_p][kh][kw][Cin_p], zero padded; bias, prelu padded.
