@@ -16,6 +16,9 @@ struct PNetLevel {
 // All conv weights transposed to [ci][ky][kx][co]; dense weights to [k][out] where noted.
 struct PNetW {
     const float *c1w, *c1b, *p1, *c2w, *c2b, *p2, *c3w, *c3b, *p3, *c41w, *c41b, *c42w, *c42b;
+    // conv3 as fp16 split planes [2][32][160] (w = w0 + w1 * 2^-11, k = tap * 16 + ci, zero
+    // padded 144 -> 160) for the fp16 matrix-core path; null -> fp32 MFMA path (see k_pnet)
+    const uint16_t* c3h;
 };
 struct PNetOut {
     // sparse (candidate) mode

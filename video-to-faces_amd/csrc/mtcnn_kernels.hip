@@ -27,6 +27,7 @@
 namespace vtf {
 
 typedef __attribute__((ext_vector_type(4))) float f32x4;
+typedef __attribute__((ext_vector_type(8))) _Float16 f16x8;
 
 // ----------------------------------------------------------------------------------- helpers
 
@@ -238,6 +239,8 @@ __global__ __launch_bounds__(256, PNET_GROUPS_PER_CU) void k_pnet(const uint8_t*
     // (k rows 90, 91 of conv2 are zeroed explicitly: soffset is outside the range check)
     const __amdgpu_buffer_rsrc_t rw2 = __builtin_amdgcn_make_buffer_rsrc((void*)wg.c2w, 0, 90 * 16 * 4, 0x00020000);
     const __amdgpu_buffer_rsrc_t rw3 = __builtin_amdgcn_make_buffer_rsrc((void*)wg.c3w, 0, 144 * 32 * 4, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rw3h = __builtin_amdgcn_make_buffer_rsrc((void*)wg.c3h, 0, 2 * 32 * 160 * 2, 0x00020000);
+    const bool split3 = wg.c3h != nullptr;  // conv3 on fp16 matrix cores (mtcnn_runtime: range bound)
     __shared__ float sA[P_A];     // level tile, later conv2 output
     __shared__ float sP[P_POOL];  // frame patch (u8) during the fill, then pooled conv1
     __shared__ int2 ybin[PL_H], xbin[PL_W];
@@ -469,12 +472,31 @@ __global__ __launch_bounds__(256, PNET_GROUPS_PER_CU) void k_pnet(const uint8_t*
                         c1 = __builtin_amdgcn_mfma_f32_16x16x4f32(av1[s - g], w2[s], c1, 0, 0, 0);
                     }
                 }
+                if (split3) {
+                    // fp16 split planes [2][pos][16 ch]: v = x0 + x1 * 2^-11 (x0 = fp16(v), x1 =
+                    // fp16((v - x0) * 2^11), the residual exact in fp32)
+                    _Float16* sH = (_Float16*)sA;
 #pragma unroll
-                for (int i = 0; i < 4; i++) {
-                    int q0 = f0 * 16 + 4 * lkx + i;
-                    if (q0 < NPOS) sA[lrx * NPOS + q0] = prelu(c0[i] + b2, a2);
-                    int q1 = f1 * 16 + 4 * lkx + i;
-                    if (two && q1 < NPOS) sA[lrx * NPOS + q1] = prelu(c1[i] + b2, a2);
+                    for (int i = 0; i < 4; i++) {
+#pragma unroll
+                        for (int h = 0; h < 2; h++) {
+                            const int q = (h ? f1 : f0) * 16 + 4 * lkx + i;
+                            if (q < NPOS && (h == 0 || two)) {
+                                const float v = prelu((h ? c1[i] : c0[i]) + b2, a2);
+                                const _Float16 x0 = (_Float16)v;
+                                sH[q * 16 + lrx] = x0;
+                                sH[NPOS * 16 + q * 16 + lrx] = (_Float16)((v - (float)x0) * 2048.f);
+                            }
+                        }
+                    }
+                } else {
+#pragma unroll
+                    for (int i = 0; i < 4; i++) {
+                        int q0 = f0 * 16 + 4 * lkx + i;
+                        if (q0 < NPOS) sA[lrx * NPOS + q0] = prelu(c0[i] + b2, a2);
+                        int q1 = f1 * 16 + 4 * lkx + i;
+                        if (two && q1 < NPOS) sA[lrx * NPOS + q1] = prelu(c1[i] + b2, a2);
+                    }
                 }
             }
         }
@@ -485,47 +507,18 @@ __global__ __launch_bounds__(256, PNET_GROUPS_PER_CU) void k_pnet(const uint8_t*
         //         the 1x1 heads are one more MFMA chain summing over the accumulator rows with no
         //         lane movement: Heads^T (16 x cells) = Wh^T (16 x 32) x F (32 x cells), the
         //         k-slot of lane group g at step i being channel 16*mf + 4g + i.
-        //         Each wave owns FPW cell fragments (8*FPW accumulator VGPRs); the weights
-        //         stream through registers in 4 chunks of 9 k-steps.
+        //         Default path: fp16 matrix cores on split operands (x = x0 + x1 * 2^-11 from
+        //         conv2's epilogue, w = w0 + w1 * 2^-11 prepared on the host): x0 w0 + 2^-11 (x0 w1 +
+        //         x1 w0) is exact to ~2^-24 relative (the dropped x1 w1 is below that), 3 MFMAs of
+        //         16x16x32 per 32-deep k-step instead of 8 fp32 16x16x4 ones (2.7x less matrix
+        //         time).  Fallback (conv2 activations could leave the fp16 range, host bound):
+        //         fp32 MFMA with the weights streamed in 4 chunks of 9 k-steps.
         {
             constexpr int FPW = PT_H * PT_W / 64;  // 16-cell fragments per wave
-            f32x4 acc[FPW][2];
-#pragma unroll
-            for (int j = 0; j < FPW; j++) acc[j][0] = acc[j][1] = f32x4{0.f, 0.f, 0.f, 0.f};
-            int ab[FPW];
-#pragma unroll
-            for (int j = 0; j < FPW; j++) {
-                const int cell = (wave * FPW + j) * 16 + lrx;
-                ab[j] = (cell / PT_W) * PC_W + (cell % PT_W);
-            }
-            const int nchunk = (o.dbg & 8) ? 0 : 4;
-            // k-step s = (tap s/4, channel 4*(s%4) + lkx): the LDS offset is the lane-group base
-            // lkx * plane plus a compile-time constant (an instruction immediate, no registers)
-            const float* sAl = sA + lkx * (PC_H * PC_W);
-            const int w3off = (lkx * 9 * 32 + lrx) * 4;
-#pragma unroll
-            for (int sc = 0; sc < 4; sc++) {
-                if (sc >= nchunk) break;
-                float w3[9][2];
-#pragma unroll
-                for (int t = 0; t < 9; t++) {
-                    const int st = 9 * sc + t, tap = st >> 2, cq = st & 3;
-                    w3[t][0] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rw3, w3off, ((4 * cq * 9 + tap) * 32) * 4, 0));
-                    w3[t][1] = __uint_as_float(
-                        __builtin_amdgcn_raw_buffer_load_b32(rw3, w3off, ((4 * cq * 9 + tap) * 32 + 16) * 4, 0));
-                }
-#pragma unroll
-                for (int t = 0; t < 9; t++) {
-                    const int st = 9 * sc + t, tap = st >> 2, cq = st & 3;
-                    const int ko = 4 * cq * PC_H * PC_W + (tap / 3) * PC_W + (tap % 3);
-#pragma unroll
-                    for (int j = 0; j < FPW; j++) {
-                        const float bv = sAl[ab[j] + ko];
-                        acc[j][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(w3[t][0], bv, acc[j][0], 0, 0, 0);
-                        acc[j][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(w3[t][1], bv, acc[j][1], 0, 0, 0);
-                    }
-                }
-            }
+            // two passes of FPW/2 fragments each: conv3 + heads per pass keeps the accumulators
+            // (main + correction on the fp16 path) within the 3-workgroup register budget
+            constexpr int NHALF = FPW % 2 == 0 ? 2 : 1;
+            constexpr int FH = FPW / NHALF;
             // accumulator row (mf, lkx, i) = channel 16*mf + 4*lkx + i
             float cb3[2][4], ca3[2][4], hwA[2][4];
 #pragma unroll
@@ -542,57 +535,139 @@ __global__ __launch_bounds__(256, PNET_GROUPS_PER_CU) void k_pnet(const uint8_t*
                 }
             const float hb0 = wc.c41b[0], hb1 = wc.c41b[1], hb2 = wc.c42b[0], hb3 = wc.c42b[1];
             const float hb4 = wc.c42b[2], hb5 = wc.c42b[3];
-#pragma unroll
-            for (int j = 0; j < FPW; j++) {
-                const int cell = (wave * FPW + j) * 16 + lrx;
-                f32x4 hacc = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-                for (int i = 0; i < 4; i++) {
-                    const float fa = prelu(acc[j][0][i] + cb3[0][i], ca3[0][i]);
-                    const float fb = prelu(acc[j][1][i] + cb3[1][i], ca3[1][i]);
-                    hacc = __builtin_amdgcn_mfma_f32_16x16x4f32(hwA[0][i], fa, hacc, 0, 0, 0);
-                    hacc = __builtin_amdgcn_mfma_f32_16x16x4f32(hwA[1][i], fb, hacc, 0, 0, 0);
+#pragma unroll 1
+            for (int hh = 0; hh < NHALF; hh++) {
+                f32x4 acc[FH][2];
+    #pragma unroll
+                for (int j = 0; j < FH; j++) acc[j][0] = acc[j][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+                int ab[FH];
+    #pragma unroll
+                for (int j = 0; j < FH; j++) {
+                    const int cell = (wave * FPW + hh * FH + j) * 16 + lrx;
+                    ab[j] = (cell / PT_W) * PC_W + (cell % PT_W);
                 }
-                // hacc: lane (cell lrx, heads 4*lkx + i): group 0 = (a0, a1, r0, r1), group 1 = (r2, r3, -, -)
-                const float r2 = __shfl_down(hacc[0], 16), r3 = __shfl_down(hacc[1], 16);
-                const int y = cell / PT_W, x = cell % PT_W;
-                const int oy = oy0 + y, ox = ox0 + x;
-                const bool valid = (lkx == 0) && (oy < P.ph) && (ox < P.pw);
-                const float a0 = hacc[0] + hb0, a1v = hacc[1] + hb1;
-                const float mx = fmaxf(a0, a1v);
-                const float e0 = expf(a0 - mx), e1 = expf(a1v - mx);
-                const float prob = __fdiv_rn(e1, e0 + e1);
-                const float q0 = hacc[2] + hb2, q1 = hacc[3] + hb3, q2 = r2 + hb4, q3 = r3 + hb5;
-                if (DENSE) {
-                    if (valid) {
-                        int64_t plane = (int64_t)P.ph * P.pw;
-                        int64_t cell = (int64_t)oy * P.pw + ox;
-                        o.prob[(int64_t)b * plane + cell] = prob;
-                        float* rg = o.reg + (int64_t)b * 4 * plane + cell;
-                        rg[0] = q0;
-                        rg[plane] = q1;
-                        rg[2 * plane] = q2;
-                        rg[3 * plane] = q3;
-                    }
-                } else {
-                    // mask = prob >= 0.6 (mtcnn.py:183; the python scalar compares as fp32)
-                    bool pass = valid && (prob >= 0.6f) && !(o.dbg & 16);
-                    uint64_t bal = __ballot(pass);
-                    if (bal) {
-                        int leader = __builtin_ctzll(bal);
-                        uint32_t base = 0;
-                        if (lane == leader) {
-                            base = atomicAdd(o.count, (uint32_t)__popcll(bal));
-                            atomicAdd(&o.level_count[L], (uint32_t)__popcll(bal));
+                const int nchunk = (o.dbg & 8) || split3 ? 0 : 4;
+                if (split3 && !(o.dbg & 8)) {
+                    // fp16 matrix cores, K = 9 taps x 16 ch in 5 steps of 32 (tap 9 = zero weights):
+                    // lane group lkx holds 8 channels (8 * (lkx & 1) ...) of tap 2s + (lkx >> 1), one
+                    // 16-byte LDS read per part; main products x0 w0 and the 2^11-scaled cross terms
+                    // x0 w1 + x1 w0 go to separate accumulators, combined once at the end
+                    constexpr int NPOS = PC_H * PC_W;
+                    const _Float16* sH = (const _Float16*)sA;
+                    f32x4 accc[FH][2];
+    #pragma unroll
+                    for (int j = 0; j < FH; j++) accc[j][0] = accc[j][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+                    const int woff = (lrx * 160 + 8 * lkx) * 2;
+    #pragma unroll
+                    for (int s5 = 0; s5 < 5; s5++) {
+                        f16x8 w0[2], w1[2];
+    #pragma unroll
+                        for (int mf = 0; mf < 2; mf++) {
+                            w0[mf] = __builtin_bit_cast(
+                                f16x8, __builtin_amdgcn_raw_buffer_load_b128(rw3h, woff, (mf * 16 * 160 + 32 * s5) * 2, 0));
+                            w1[mf] = __builtin_bit_cast(
+                                f16x8, __builtin_amdgcn_raw_buffer_load_b128(rw3h, woff, ((32 + mf * 16) * 160 + 32 * s5) * 2, 0));
                         }
-                        base = __shfl(base, leader);
-                        if (pass) {
-                            uint32_t slot = base + (uint32_t)__popcll(bal & ((1ull << lane) - 1ull));
-                            if (slot < o.cap) {
-                                uint32_t lin = (uint32_t)(((int64_t)b * P.ph + oy) * P.pw + ox);
-                                o.key[slot] = ((uint64_t)L << 32) | lin;
-                                o.score[slot] = prob;
-                                o.regv[slot] = make_float4(q0, q1, q2, q3);
+                        const int tap = min(2 * s5 + (lkx >> 1), 8);
+                        const int xo = ((tap / 3) * PC_W + (tap % 3)) * 16 + 8 * (lkx & 1);
+    #pragma unroll
+                        for (int j = 0; j < FH; j++) {
+                            const f16x8 x0 = *(const f16x8*)(sH + ab[j] * 16 + xo);
+                            const f16x8 x1 = *(const f16x8*)(sH + NPOS * 16 + ab[j] * 16 + xo);
+    #pragma unroll
+                            for (int mf = 0; mf < 2; mf++) {
+                                acc[j][mf] = __builtin_amdgcn_mfma_f32_16x16x32_f16(w0[mf], x0, acc[j][mf], 0, 0, 0);
+                                accc[j][mf] = __builtin_amdgcn_mfma_f32_16x16x32_f16(w1[mf], x0, accc[j][mf], 0, 0, 0);
+                                accc[j][mf] = __builtin_amdgcn_mfma_f32_16x16x32_f16(w0[mf], x1, accc[j][mf], 0, 0, 0);
+                            }
+                        }
+                    }
+    #pragma unroll
+                    for (int j = 0; j < FH; j++)
+    #pragma unroll
+                        for (int mf = 0; mf < 2; mf++)
+    #pragma unroll
+                            for (int i = 0; i < 4; i++) acc[j][mf][i] = acc[j][mf][i] + accc[j][mf][i] * 0.00048828125f;
+                }
+                // k-step s = (tap s/4, channel 4*(s%4) + lkx): the LDS offset is the lane-group base
+                // lkx * plane plus a compile-time constant (an instruction immediate, no registers)
+                const float* sAl = sA + lkx * (PC_H * PC_W);
+                const int w3off = (lkx * 9 * 32 + lrx) * 4;
+    #pragma unroll
+                for (int sc = 0; sc < 4; sc++) {
+                    if (sc >= nchunk) break;
+                    float w3[9][2];
+    #pragma unroll
+                    for (int t = 0; t < 9; t++) {
+                        const int st = 9 * sc + t, tap = st >> 2, cq = st & 3;
+                        w3[t][0] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rw3, w3off, ((4 * cq * 9 + tap) * 32) * 4, 0));
+                        w3[t][1] = __uint_as_float(
+                            __builtin_amdgcn_raw_buffer_load_b32(rw3, w3off, ((4 * cq * 9 + tap) * 32 + 16) * 4, 0));
+                    }
+    #pragma unroll
+                    for (int t = 0; t < 9; t++) {
+                        const int st = 9 * sc + t, tap = st >> 2, cq = st & 3;
+                        const int ko = 4 * cq * PC_H * PC_W + (tap / 3) * PC_W + (tap % 3);
+    #pragma unroll
+                        for (int j = 0; j < FH; j++) {
+                            const float bv = sAl[ab[j] + ko];
+                            acc[j][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(w3[t][0], bv, acc[j][0], 0, 0, 0);
+                            acc[j][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(w3[t][1], bv, acc[j][1], 0, 0, 0);
+                        }
+                    }
+                }
+    #pragma unroll
+                for (int j = 0; j < FH; j++) {
+                    const int cell = (wave * FPW + hh * FH + j) * 16 + lrx;
+                    f32x4 hacc = {0.f, 0.f, 0.f, 0.f};
+    #pragma unroll
+                    for (int i = 0; i < 4; i++) {
+                        const float fa = prelu(acc[j][0][i] + cb3[0][i], ca3[0][i]);
+                        const float fb = prelu(acc[j][1][i] + cb3[1][i], ca3[1][i]);
+                        hacc = __builtin_amdgcn_mfma_f32_16x16x4f32(hwA[0][i], fa, hacc, 0, 0, 0);
+                        hacc = __builtin_amdgcn_mfma_f32_16x16x4f32(hwA[1][i], fb, hacc, 0, 0, 0);
+                    }
+                    // hacc: lane (cell lrx, heads 4*lkx + i): group 0 = (a0, a1, r0, r1), group 1 = (r2, r3, -, -)
+                    const float r2 = __shfl_down(hacc[0], 16), r3 = __shfl_down(hacc[1], 16);
+                    const int y = cell / PT_W, x = cell % PT_W;
+                    const int oy = oy0 + y, ox = ox0 + x;
+                    const bool valid = (lkx == 0) && (oy < P.ph) && (ox < P.pw);
+                    const float a0 = hacc[0] + hb0, a1v = hacc[1] + hb1;
+                    const float mx = fmaxf(a0, a1v);
+                    const float e0 = expf(a0 - mx), e1 = expf(a1v - mx);
+                    const float prob = __fdiv_rn(e1, e0 + e1);
+                    const float q0 = hacc[2] + hb2, q1 = hacc[3] + hb3, q2 = r2 + hb4, q3 = r3 + hb5;
+                    if (DENSE) {
+                        if (valid) {
+                            int64_t plane = (int64_t)P.ph * P.pw;
+                            int64_t cell = (int64_t)oy * P.pw + ox;
+                            o.prob[(int64_t)b * plane + cell] = prob;
+                            float* rg = o.reg + (int64_t)b * 4 * plane + cell;
+                            rg[0] = q0;
+                            rg[plane] = q1;
+                            rg[2 * plane] = q2;
+                            rg[3 * plane] = q3;
+                        }
+                    } else {
+                        // mask = prob >= 0.6 (mtcnn.py:183; the python scalar compares as fp32)
+                        bool pass = valid && (prob >= 0.6f) && !(o.dbg & 16);
+                        uint64_t bal = __ballot(pass);
+                        if (bal) {
+                            int leader = __builtin_ctzll(bal);
+                            uint32_t base = 0;
+                            if (lane == leader) {
+                                base = atomicAdd(o.count, (uint32_t)__popcll(bal));
+                                atomicAdd(&o.level_count[L], (uint32_t)__popcll(bal));
+                            }
+                            base = __shfl(base, leader);
+                            if (pass) {
+                                uint32_t slot = base + (uint32_t)__popcll(bal & ((1ull << lane) - 1ull));
+                                if (slot < o.cap) {
+                                    uint32_t lin = (uint32_t)(((int64_t)b * P.ph + oy) * P.pw + ox);
+                                    o.key[slot] = ((uint64_t)L << 32) | lin;
+                                    o.score[slot] = prob;
+                                    o.regv[slot] = make_float4(q0, q1, q2, q3);
+                                }
                             }
                         }
                     }

@@ -125,7 +125,7 @@ static void build_weights(Mtcnn& m, const float* params, int64_t n_params) {
         const float* b = m.d_w;
         int i = 0;
         auto nx = [&]() { return b + off[i++]; };
-        m.pw = PNetW{nx(), nx(), nx(), nx(), nx(), nx(), nx(), nx(), nx(), nx(), nx(), nx(), nx()};
+        m.pw = PNetW{nx(), nx(), nx(), nx(), nx(), nx(), nx(), nx(), nx(), nx(), nx(), nx(), nx(), nullptr};
     }
     // raw (reference layout) tensors by spec index
     std::vector<const float*> raw(NP);
@@ -185,6 +185,43 @@ static void build_weights(Mtcnn& m, const float* params, int64_t n_params) {
         VTF_HIP(hipMemcpy(d, w.data(), w.size() * 4, hipMemcpyHostToDevice));
         m.allocs.push_back(d);
         m.fw[net] = d;
+    }
+    // PNet conv3 on the fp16 matrix cores (k_pnet): x = x0 + x1 * 2^-11 and w = w0 + w1 * 2^-11
+    // with fp16 parts represent both operands to ~2^-24 relative and x*w = x0 w0 + 2^-11 (x0 w1 +
+    // x1 w0) drops only x1 w1 (<= 2^-24 relative): fp32-grade products.  The conv2 activations
+    // must stay inside the fp16 range: bound them from the weights (level inputs lie in
+    // [-1, 1]); beyond the bound k_pnet keeps the fp32 MFMA path.
+    {
+        auto bound = [&](int wi, int co, int K, double in) {
+            const float* W = raw[wi];
+            double b = 0.0, amax = 1.0;
+            for (int c = 0; c < co; c++) {
+                double s = std::fabs((double)raw[wi + 1][c]);
+                for (int k = 0; k < K; k++) s += std::fabs((double)W[(size_t)c * K + k]) * in;
+                b = std::max(b, s);
+                amax = std::max(amax, std::fabs((double)raw[wi + 2][c]));
+            }
+            return b * amax;
+        };
+        const double b2 = bound(3, 16, 90, bound(0, 10, 27, 1.0));
+        if (b2 < 16384.0) {
+            std::vector<uint16_t> h(2 * 32 * 160, 0);
+            const float* W = raw[6];  // [32][16][3][3]
+            for (int co = 0; co < 32; co++)
+                for (int tap = 0; tap < 9; tap++)
+                    for (int ci = 0; ci < 16; ci++) {
+                        const float w = W[((size_t)co * 16 + ci) * 9 + tap];
+                        const _Float16 w0 = (_Float16)w;
+                        const _Float16 w1 = (_Float16)((w - (float)w0) * 2048.f);
+                        std::memcpy(&h[(size_t)co * 160 + tap * 16 + ci], &w0, 2);
+                        std::memcpy(&h[(size_t)(32 + co) * 160 + tap * 16 + ci], &w1, 2);
+                    }
+            uint16_t* d = nullptr;
+            VTF_HIP(hipMalloc((void**)&d, h.size() * 2));
+            VTF_HIP(hipMemcpy(d, h.data(), h.size() * 2, hipMemcpyHostToDevice));
+            m.allocs.push_back((float*)d);
+            m.pw.c3h = d;
+        }
     }
     auto dev = [&](int i) { return m.d_w + off[i]; };
     m.rh1w = dev(25); m.rh1b = dev(26); m.rh2w = dev(27); m.rh2b = dev(28);
