@@ -50,6 +50,27 @@ def test_pnet_level_vs_oracle(model, params):
         np.testing.assert_allclose(reg.cpu().numpy(), rref.numpy(), rtol=0, atol=2e-5)
 
 
+@pytest.mark.parametrize('force_fp32', ['0', '1'])
+def test_pnet_paths_vs_oracle(params, force_fp32, monkeypatch):
+    # conv2/conv3 of k_pnet run on fp16 matrix cores with split operands by default and on fp32
+    # MFMA when VTF_PNET_FP32=1 (the fallback for weights whose activations could leave the
+    # fp16 range): both within the same fp32-grade tolerance of the oracle
+    from videotofaces import synth
+    from videotofaces.detectors.mtcnn import MTCNN
+    from oracle import mtcnn as om
+    import torch.nn.functional as F
+    monkeypatch.setenv('VTF_PNET_FP32', force_fp32)
+    m = MTCNN('cuda:0')
+    fr = synth.make_frames(2, 120, 200, seed=21)
+    x = om.preprocess(list(fr))
+    dev = torch.from_numpy(fr).cuda()
+    for (lh, lw) in [(288, 480), (101, 168), (31, 40)]:
+        reg, prob = m.pnet_level(dev, lh, lw)
+        rref, pref = om.pnet(params, F.adaptive_avg_pool2d(x, (lh, lw)))
+        np.testing.assert_allclose(prob.cpu().numpy(), pref.numpy(), rtol=0, atol=2e-5)
+        np.testing.assert_allclose(reg.cpu().numpy(), rref.numpy(), rtol=0, atol=2e-5)
+
+
 def test_rnet_onet_vs_golden(g, model):
     reg, prob = model.rnet(torch.from_numpy(g['rnet_in']))
     np.testing.assert_allclose(reg.cpu().numpy(), g['rnet_reg'], atol=2e-5)

@@ -19,6 +19,7 @@ struct PNetW {
     // conv3 as fp16 split planes [2][32][160] (w = w0 + w1 * 2^-11, k = tap * 16 + ci, zero
     // padded 144 -> 160) for the fp16 matrix-core path; null -> fp32 MFMA path (see k_pnet)
     const uint16_t* c3h;
+    const uint16_t* c2h;  // conv2 likewise: [2][16][160], k = tap * 16 + ci (ci >= 10 zero)
 };
 struct PNetOut {
     // sparse (candidate) mode
@@ -58,6 +59,6 @@ void launch_landmarks(const float4* boxes, const float* lm, int64_t n, float* ou
 void launch_iom_chain(const float4* boxes, const int32_t* img, const int32_t* order, int64_t n, float thr,
                       int32_t* keep, hipStream_t st);
 
-constexpr int PNET_TH = 24, PNET_TW = 16;  // k_pnet output cells per tile (rows, cols)
+constexpr int PNET_TH = 16, PNET_TW = 16;  // k_pnet output cells per tile (rows, cols)
 
 }  // namespace vtf

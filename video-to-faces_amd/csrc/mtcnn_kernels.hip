@@ -212,7 +212,7 @@ constexpr int PP_H = PT_H + 4, PP_W = PT_W + 4;       // pooled 20 x 36
 constexpr int PC_H = PT_H + 2, PC_W = PT_W + 2;       // conv2 out 18 x 34
 constexpr int P_LVL = 3 * PL_H * PL_W;                // 9324
 constexpr int P_C2 = 16 * PC_H * PC_W;                // 9792
-constexpr int P_POOL = 10 * PP_H * PP_W;              // 7200
+constexpr int P_POOL = 16 * PP_H * PP_W;              // pooled conv1: fp32 [10][cells] or fp16 split [2][cells][16]
 constexpr int P_A = P_C2 > P_LVL ? P_C2 : P_LVL;
 
 // exact x / k for the bin averages: power-of-two k is an exact multiply (bit-identical to the
@@ -240,6 +240,7 @@ __global__ __launch_bounds__(256, PNET_GROUPS_PER_CU) void k_pnet(const uint8_t*
     const __amdgpu_buffer_rsrc_t rw2 = __builtin_amdgcn_make_buffer_rsrc((void*)wg.c2w, 0, 90 * 16 * 4, 0x00020000);
     const __amdgpu_buffer_rsrc_t rw3 = __builtin_amdgcn_make_buffer_rsrc((void*)wg.c3w, 0, 144 * 32 * 4, 0x00020000);
     const __amdgpu_buffer_rsrc_t rw3h = __builtin_amdgcn_make_buffer_rsrc((void*)wg.c3h, 0, 2 * 32 * 160 * 2, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rw2h = __builtin_amdgcn_make_buffer_rsrc((void*)wg.c2h, 0, 2 * 16 * 160 * 2, 0x00020000);
     const bool split3 = wg.c3h != nullptr;  // conv3 on fp16 matrix cores (mtcnn_runtime: range bound)
     __shared__ float sA[P_A];     // level tile, later conv2 output
     __shared__ float sP[P_POOL];  // frame patch (u8) during the fill, then pooled conv1
@@ -429,7 +430,23 @@ __global__ __launch_bounds__(256, PNET_GROUPS_PER_CU) void k_pnet(const uint8_t*
                         // outside the valid pooled map (only feeds discarded cells): keep finite
                         out = any ? m : 0.f;
                     }
-                    if (live) sP[co * NPP + pp] = out;
+                    if (live) {
+                        if (split3) {
+                            // fp16 split planes [2][cell][16 ch] (conv2's matrix-core operand)
+                            _Float16* sH = (_Float16*)sP;
+                            const _Float16 x0 = (_Float16)out;
+                            sH[pp * 16 + co] = x0;
+                            sH[NPP * 16 + pp * 16 + co] = (_Float16)((out - (float)x0) * 2048.f);
+                        } else {
+                            sP[co * NPP + pp] = out;
+                        }
+                    }
+                }
+                if (split3 && g == 1 && live) {  // channels 10..15 of the padded planes: zero
+                    uint32_t* z0 = (uint32_t*)((_Float16*)sP + pp * 16 + 10);
+                    uint32_t* z1 = (uint32_t*)((_Float16*)sP + NPP * 16 + pp * 16 + 10);
+#pragma unroll
+                    for (int q = 0; q < 3; q++) z0[q] = z1[q] = 0u;
                 }
             }
         }
@@ -440,13 +457,66 @@ __global__ __launch_bounds__(256, PNET_GROUPS_PER_CU) void k_pnet(const uint8_t*
         {
             constexpr int NPOS = PC_H * PC_W;      // 612
             constexpr int NF = (NPOS + 15) / 16;   // 39
+            if (split3 && !(o.dbg & 4)) {
+                // fp16 matrix cores on split operands (as conv3): K = 9 taps x 16 ch (10 real) in 5
+                // steps of 32; rows = conv2 positions, lane group lkx reads 8 channels of tap
+                // 2s + (lkx >> 1) of both planes (16 B each); main and 2^11-scaled cross products
+                // in separate accumulators
+                constexpr int NPP = PP_H * PP_W;
+                const _Float16* sH = (const _Float16*)sP;
+                f16x8 w0[5], w1[5];
+                const int woff = (lrx * 160 + 8 * lkx) * 2;
+#pragma unroll
+                for (int s5 = 0; s5 < 5; s5++) {
+                    w0[s5] = __builtin_bit_cast(f16x8, __builtin_amdgcn_raw_buffer_load_b128(rw2h, woff, 64 * s5, 0));
+                    w1[s5] = __builtin_bit_cast(f16x8,
+                                                __builtin_amdgcn_raw_buffer_load_b128(rw2h, woff, 16 * 160 * 2 + 64 * s5, 0));
+                }
+                _Float16* sO = (_Float16*)sA;
+                for (int f0 = wave; f0 < NF; f0 += 8) {
+                    const int f1 = f0 + 4;
+                    const bool two = f1 < NF;
+                    const int p0 = min(f0 * 16 + lrx, NPOS - 1), p1 = min((two ? f1 : f0) * 16 + lrx, NPOS - 1);
+                    const int ab0 = (p0 / PC_W) * PP_W + (p0 % PC_W), ab1 = (p1 / PC_W) * PP_W + (p1 % PC_W);
+                    f32x4 c0 = {0.f, 0.f, 0.f, 0.f}, c1 = c0, d0 = c0, d1 = c0;
+#pragma unroll
+                    for (int s5 = 0; s5 < 5; s5++) {
+                        const int tap = min(2 * s5 + (lkx >> 1), 8);
+                        const int xo = ((tap / 3) * PP_W + (tap % 3)) * 16 + 8 * (lkx & 1);
+                        const f16x8 a00 = *(const f16x8*)(sH + ab0 * 16 + xo);
+                        const f16x8 a01 = *(const f16x8*)(sH + NPP * 16 + ab0 * 16 + xo);
+                        const f16x8 a10 = *(const f16x8*)(sH + ab1 * 16 + xo);
+                        const f16x8 a11 = *(const f16x8*)(sH + NPP * 16 + ab1 * 16 + xo);
+                        c0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a00, w0[s5], c0, 0, 0, 0);
+                        d0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a00, w1[s5], d0, 0, 0, 0);
+                        d0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a01, w0[s5], d0, 0, 0, 0);
+                        c1 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a10, w0[s5], c1, 0, 0, 0);
+                        d1 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a10, w1[s5], d1, 0, 0, 0);
+                        d1 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a11, w0[s5], d1, 0, 0, 0);
+                    }
+#pragma unroll
+                    for (int i = 0; i < 4; i++) {
+#pragma unroll
+                        for (int h = 0; h < 2; h++) {
+                            const int q = (h ? f1 : f0) * 16 + 4 * lkx + i;
+                            if (q < NPOS && (h == 0 || two)) {
+                                const float acc2 = h ? c1[i] + d1[i] * 0.00048828125f : c0[i] + d0[i] * 0.00048828125f;
+                                const float v = prelu(acc2 + b2, a2);
+                                const _Float16 x0 = (_Float16)v;
+                                sO[q * 16 + lrx] = x0;
+                                sO[NPOS * 16 + q * 16 + lrx] = (_Float16)((v - (float)x0) * 2048.f);
+                            }
+                        }
+                    }
+                }
+            }
             float w2[23];  // per tile (L1-resident): keeps the persistent register set small
             const int w2off = (16 * lkx + lrx) * 4;
 #pragma unroll
             for (int s = 0; s < 23; s++)
                 w2[s] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rw2, w2off, 256 * s, 0));
             if (lkx >= 2) w2[22] = 0.f;  // k = 90, 91: zero padding
-            for (int f0 = wave; f0 < ((o.dbg & 4) ? 0 : NF); f0 += 8) {
+            for (int f0 = wave; f0 < ((o.dbg & 4) || split3 ? 0 : NF); f0 += 8) {
                 const int f1 = f0 + 4;
                 const bool two = f1 < NF;
                 int p0 = min(f0 * 16 + lrx, NPOS - 1), p1 = min((two ? f1 : f0) * 16 + lrx, NPOS - 1);

@@ -125,7 +125,7 @@ static void build_weights(Mtcnn& m, const float* params, int64_t n_params) {
         const float* b = m.d_w;
         int i = 0;
         auto nx = [&]() { return b + off[i++]; };
-        m.pw = PNetW{nx(), nx(), nx(), nx(), nx(), nx(), nx(), nx(), nx(), nx(), nx(), nx(), nx(), nullptr};
+        m.pw = PNetW{nx(), nx(), nx(), nx(), nx(), nx(), nx(), nx(), nx(), nx(), nx(), nx(), nx(), nullptr, nullptr};
     }
     // raw (reference layout) tensors by spec index
     std::vector<const float*> raw(NP);
@@ -203,24 +203,29 @@ static void build_weights(Mtcnn& m, const float* params, int64_t n_params) {
             }
             return b * amax;
         };
-        const double b2 = bound(3, 16, 90, bound(0, 10, 27, 1.0));
-        if (b2 < 16384.0) {
-            std::vector<uint16_t> h(2 * 32 * 160, 0);
-            const float* W = raw[6];  // [32][16][3][3]
-            for (int co = 0; co < 32; co++)
-                for (int tap = 0; tap < 9; tap++)
-                    for (int ci = 0; ci < 16; ci++) {
-                        const float w = W[((size_t)co * 16 + ci) * 9 + tap];
-                        const _Float16 w0 = (_Float16)w;
-                        const _Float16 w1 = (_Float16)((w - (float)w0) * 2048.f);
-                        std::memcpy(&h[(size_t)co * 160 + tap * 16 + ci], &w0, 2);
-                        std::memcpy(&h[(size_t)(32 + co) * 160 + tap * 16 + ci], &w1, 2);
-                    }
-            uint16_t* d = nullptr;
-            VTF_HIP(hipMalloc((void**)&d, h.size() * 2));
-            VTF_HIP(hipMemcpy(d, h.data(), h.size() * 2, hipMemcpyHostToDevice));
-            m.allocs.push_back((float*)d);
-            m.pw.c3h = d;
+        const double b1 = bound(0, 10, 27, 1.0), b2 = bound(3, 16, 90, b1);
+        const char* force = std::getenv("VTF_PNET_FP32");  // tests: force the fp32 MFMA paths
+        if (b1 < 16384.0 && b2 < 16384.0 && !(force && force[0] == '1')) {
+            // [2][co][160] split planes of a [co][ci][3][3] conv, k = tap * 16 + ci
+            auto split = [&](const float* W, int co_n, int ci_n) {
+                std::vector<uint16_t> h((size_t)2 * co_n * 160, 0);
+                for (int co = 0; co < co_n; co++)
+                    for (int tap = 0; tap < 9; tap++)
+                        for (int ci = 0; ci < ci_n; ci++) {
+                            const float w = W[((size_t)co * ci_n + ci) * 9 + tap];
+                            const _Float16 w0 = (_Float16)w;
+                            const _Float16 w1 = (_Float16)((w - (float)w0) * 2048.f);
+                            std::memcpy(&h[(size_t)co * 160 + tap * 16 + ci], &w0, 2);
+                            std::memcpy(&h[(size_t)(co_n + co) * 160 + tap * 16 + ci], &w1, 2);
+                        }
+                uint16_t* d = nullptr;
+                VTF_HIP(hipMalloc((void**)&d, h.size() * 2));
+                VTF_HIP(hipMemcpy(d, h.data(), h.size() * 2, hipMemcpyHostToDevice));
+                m.allocs.push_back((void*)d);
+                return (const uint16_t*)d;
+            };
+            m.pw.c2h = split(raw[3], 16, 10);
+            m.pw.c3h = split(raw[6], 32, 16);
         }
     }
     auto dev = [&](int i) { return m.d_w + off[i]; };
