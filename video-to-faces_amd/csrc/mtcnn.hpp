@@ -20,6 +20,7 @@ struct PNetW {
     // padded 144 -> 160) for the fp16 matrix-core path; null -> fp32 MFMA path (see k_pnet)
     const uint16_t* c3h;
     const uint16_t* c2h;  // conv2 likewise: [2][16][160], k = tap * 16 + ci (ci >= 10 zero)
+    const uint16_t* c1h;  // conv1: [2][16][64], k = ky * 16 + kx * 4 + c (c = 3, kx = 3, ky = 3, co >= 10 zero)
 };
 struct PNetOut {
     // sparse (candidate) mode

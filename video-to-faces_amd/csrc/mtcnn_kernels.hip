@@ -212,8 +212,13 @@ constexpr int PP_H = PT_H + 4, PP_W = PT_W + 4;       // pooled 20 x 36
 constexpr int PC_H = PT_H + 2, PC_W = PT_W + 2;       // conv2 out 18 x 34
 constexpr int P_LVL = 3 * PL_H * PL_W;                // 9324
 constexpr int P_C2 = 16 * PC_H * PC_W;                // 9792
-constexpr int P_POOL = 16 * PP_H * PP_W;              // pooled conv1: fp32 [10][cells] or fp16 split [2][cells][16]
-constexpr int P_A = P_C2 > P_LVL ? P_C2 : P_LVL;
+// pooled conv1: fp32 [10][cells], or fp16 split planes [2][cells][12] (ch 10, 11 zero; conv2 reads
+// 8 halves from channel 8 into the next cell, against zero weights) + 4 halves of end padding
+constexpr int PQ_C = 12;
+constexpr int P_POOL = (10 * PP_H * PP_W > PQ_C * PP_H * PP_W + 4) ? 10 * PP_H * PP_W : PQ_C * PP_H * PP_W + 4;
+constexpr int P_LVLH = PL_H * PL_W * 4;                // level as fp16 split planes [2][y][x][4] (in floats)
+constexpr int P_A0 = P_C2 > P_LVL ? P_C2 : P_LVL;
+constexpr int P_A = P_A0 > P_LVLH ? P_A0 : P_LVLH;
 
 // exact x / k for the bin averages: power-of-two k is an exact multiply (bit-identical to the
 // IEEE division), other k take the correctly-rounded division
@@ -222,8 +227,41 @@ __device__ inline float div_bin(float x, int k) {
 }
 
 // workgroups per CU from the LDS footprint (160 KB per CU)
-constexpr int PNET_LDS = (P_A + P_POOL) * 4 + (PL_H + PL_W) * 8 + 16;
-constexpr int PNET_GROUPS_PER_CU = (160 * 1024) / PNET_LDS;
+constexpr int PNET_LDS = (P_A + P_POOL) * 4 + (PL_H + PL_W) * 4 + 16;
+// fp16 split of an fp32 value: v = x0 + x1 * 2^-11 to ~2^-24 relative (x0 = fp16(v), the
+// residual v - x0 exact in fp32), the operand form of k_pnet's fp16 matrix-core convolutions
+__device__ inline void split_f16(float v, _Float16& x0, _Float16& x1) {
+    x0 = (_Float16)v;
+    x1 = (_Float16)((v - (float)x0) * 2048.f);
+}
+
+// 8 halves from an 8-byte aligned LDS address (two ds_read_b64)
+typedef __attribute__((ext_vector_type(4))) _Float16 f16x4;
+__device__ inline f16x8 ld_h8(const _Float16* p) {
+    const f16x4 lo = *(const f16x4*)p, hi = *(const f16x4*)(p + 4);
+    return f16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+}
+
+// level pixel i of the tile: fp32 channel planes [3][PL_H*PL_W] (fp32 conv1), or fp16 split
+// planes [2][PL_H*PL_W][4] (channel 3 zero) for conv1 on the matrix cores
+__device__ inline void store_level(float* sA, bool split, int i, float r, float g, float b) {
+    if (split) {
+        _Float16 r0, r1, g0, g1, b0, b1;
+        split_f16(r, r0, r1);
+        split_f16(g, g0, g1);
+        split_f16(b, b0, b1);
+        typedef __attribute__((ext_vector_type(4))) _Float16 h4;
+        h4* p = (h4*)sA;
+        p[i] = h4{r0, g0, b0, (_Float16)0.f};
+        p[PL_H * PL_W + i] = h4{r1, g1, b1, (_Float16)0.f};
+    } else {
+        sA[i] = r;
+        sA[PL_H * PL_W + i] = g;
+        sA[2 * PL_H * PL_W + i] = b;
+    }
+}
+
+constexpr int PNET_GROUPS_PER_CU = (160 * 1024) / ((PNET_LDS + 511) / 512 * 512);  // LDS granule: 512 B
 static_assert(PNET_GROUPS_PER_CU >= 2, "k_pnet tile too large for 2 workgroups per CU");
 constexpr int PATCH_BYTES = P_POOL * 4;  // frame patch staged in the (not yet used) pooled buffer
 
@@ -241,10 +279,11 @@ __global__ __launch_bounds__(256, PNET_GROUPS_PER_CU) void k_pnet(const uint8_t*
     const __amdgpu_buffer_rsrc_t rw3 = __builtin_amdgcn_make_buffer_rsrc((void*)wg.c3w, 0, 144 * 32 * 4, 0x00020000);
     const __amdgpu_buffer_rsrc_t rw3h = __builtin_amdgcn_make_buffer_rsrc((void*)wg.c3h, 0, 2 * 32 * 160 * 2, 0x00020000);
     const __amdgpu_buffer_rsrc_t rw2h = __builtin_amdgcn_make_buffer_rsrc((void*)wg.c2h, 0, 2 * 16 * 160 * 2, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rw1h = __builtin_amdgcn_make_buffer_rsrc((void*)wg.c1h, 0, 2 * 16 * 64 * 2, 0x00020000);
     const bool split3 = wg.c3h != nullptr;  // conv3 on fp16 matrix cores (mtcnn_runtime: range bound)
     __shared__ float sA[P_A];     // level tile, later conv2 output
     __shared__ float sP[P_POOL];  // frame patch (u8) during the fill, then pooled conv1
-    __shared__ int2 ybin[PL_H], xbin[PL_W];
+    __shared__ ushort2 ybin[PL_H], xbin[PL_W];  // frame bin [start, end) of each level row / column
     __shared__ int s_tile;
     const int tid = threadIdx.x;
     const int lane = tid & 63, wave = tid >> 6;
@@ -281,10 +320,10 @@ __global__ __launch_bounds__(256, PNET_GROUPS_PER_CU) void k_pnet(const uint8_t*
         //         preprocessed frame, bit-exact; zero outside the level.
         if (tid < PL_H) {
             int ly = 2 * oy0 + tid;
-            ybin[tid] = ly < P.lh ? make_int2((ly * H) / P.lh, ((ly + 1) * H + P.lh - 1) / P.lh) : make_int2(0, 0);
+            ybin[tid] = ly < P.lh ? make_ushort2((ly * H) / P.lh, ((ly + 1) * H + P.lh - 1) / P.lh) : make_ushort2(0, 0);
         } else if (tid < PL_H + PL_W) {
             int q = tid - PL_H, lx = 2 * ox0 + q;
-            xbin[q] = lx < P.lw ? make_int2((lx * W) / P.lw, ((lx + 1) * W + P.lw - 1) / P.lw) : make_int2(0, 0);
+            xbin[q] = lx < P.lw ? make_ushort2((lx * W) / P.lw, ((lx + 1) * W + P.lw - 1) / P.lw) : make_ushort2(0, 0);
         }
         __syncthreads();
         // frame patch covering every bin of the tile; staged to LDS with coalesced loads when it fits
@@ -317,25 +356,30 @@ __global__ __launch_bounds__(256, PNET_GROUPS_PER_CU) void k_pnet(const uint8_t*
         if (P.pre) {
             // large-bin level precomputed by k_resample_sat (bit-identical values)
             const float* pre = P.pre + (int64_t)b * 3 * P.lh * P.lw;
-            for (int i0 = tid; i0 < ((o.dbg & 1) ? 0 : P_LVL); i0 += 256 * 8) {
-                float v[8];
+            const int64_t pl = (int64_t)P.lh * P.lw;
+            for (int i0 = tid; i0 < ((o.dbg & 1) ? 0 : PL_H * PL_W); i0 += 256 * 4) {
+                float v[4][3];
 #pragma unroll
-                for (int j = 0; j < 8; j++) {
-                    const int i = min(i0 + j * 256, P_LVL - 1);
-                    const int c = i / (PL_H * PL_W), rq = i - c * (PL_H * PL_W);
-                    const int r = rq / PL_W, q = rq - r * PL_W;
+                for (int j = 0; j < 4; j++) {
+                    const int i = min(i0 + j * 256, PL_H * PL_W - 1);
+                    const int r = i / PL_W, q = i - r * PL_W;
                     const int ly = 2 * oy0 + r, lx = 2 * ox0 + q;
-                    const float t = pre[((int64_t)c * P.lh + min(ly, P.lh - 1)) * P.lw + min(lx, P.lw - 1)];
-                    v[j] = (ly < P.lh && lx < P.lw) ? t : 0.f;
+                    const bool in = ly < P.lh && lx < P.lw;
+                    const int64_t o0 = (int64_t)min(ly, P.lh - 1) * P.lw + min(lx, P.lw - 1);
+#pragma unroll
+                    for (int c = 0; c < 3; c++) {
+                        const float t = pre[c * pl + o0];
+                        v[j][c] = in ? t : 0.f;
+                    }
                 }
 #pragma unroll
-                for (int j = 0; j < 8; j++)
-                    if (i0 + j * 256 < P_LVL) sA[i0 + j * 256] = v[j];
+                for (int j = 0; j < 4; j++)
+                    if (i0 + j * 256 < PL_H * PL_W) store_level(sA, split3, i0 + j * 256, v[j][0], v[j][1], v[j][2]);
             }
         }
         for (int i = tid; i < ((o.dbg & 1) || P.pre ? 0 : PL_H * PL_W); i += 256) {
             int r = i / PL_W, q = i - r * PL_W;
-            int2 yb = ybin[r], xb = xbin[q];
+            const int2 yb = make_int2(ybin[r].x, ybin[r].y), xb = make_int2(xbin[q].x, xbin[q].y);
             float s0 = 0.f, s1 = 0.f, s2 = 0.f;
             if (staged) {
                 for (int y = yb.x; y < yb.y; y++) {
@@ -359,18 +403,99 @@ __global__ __launch_bounds__(256, PNET_GROUPS_PER_CU) void k_pnet(const uint8_t*
             }
             int kh = yb.y - yb.x, kw = xb.y - xb.x;
             bool in = kh > 0 && kw > 0;
-            sA[i] = in ? div_bin(div_bin(s0, kh), kw) : 0.f;
-            sA[PL_H * PL_W + i] = in ? div_bin(div_bin(s1, kh), kw) : 0.f;
-            sA[2 * PL_H * PL_W + i] = in ? div_bin(div_bin(s2, kh), kw) : 0.f;
+            store_level(sA, split3, i, in ? div_bin(div_bin(s0, kh), kw) : 0.f, in ? div_bin(div_bin(s1, kh), kw) : 0.f,
+                        in ? div_bin(div_bin(s2, kh), kw) : 0.f);
         }
         __syncthreads();
 
-        // ---- 2. conv1 (3->10, 3x3) + PReLU + maxpool 2x2 ceil on the VALU.  conv1 has N = 10
-        //         output channels: on a 16-wide MFMA tile 6/16 of the matrix pipe would be padding,
-        //         so it runs as fmaf chains with the weights wave-uniform in SGPRs (scalar loads),
-        //         one lane per pooled cell (its 2x2 conv1 window from a 3x4x4 input patch in
-        //         registers), 5 channels per wave task -- and leaves the matrix pipe to the other
-        //         workgroups' conv2 / conv3 on the same CU.
+        // ---- 2. conv1 (3->10, 3x3) + PReLU + maxpool 2x2 ceil.  Default: fp16 matrix cores on
+        //         split operands (below).  fp32 fallback: the VALU -- with N = 10 output channels
+        //         6/16 of an fp32 MFMA tile would be padding, so fmaf chains with the weights
+        //         wave-uniform in SGPRs (scalar loads), one lane per pooled cell (its 2x2 conv1
+        //         window from a 3x4x4 input patch in registers), 5 channels per wave task.
+        if (split3 && !(o.dbg & 2)) {
+            // conv1 on fp16 matrix cores (split level planes [2][y][x][4], split weights):
+            // K = 3 rows x 16 (kx, c) slots (12 real) in 2 steps of 32; A row r of fragment f is
+            // conv1 position (2py+dy, 2px+dx) of pooled cell 4f + r/4, corner r%4, so each lane's
+            // 4 accumulators are one pooling window (column = output channel, lane lrx)
+            constexpr int NPP = PP_H * PP_W;
+            constexpr int NF1 = NPP / 4;
+            constexpr int PLN = PL_H * PL_W * 4;  // halves per plane
+            static_assert(NPP % 4 == 0, "pool cells per fragment");
+            const _Float16* sL = (const _Float16*)sA;
+            _Float16* sQ = (_Float16*)sP;
+            const int woff = (lrx * 64 + 8 * lkx) * 2;
+            f16x8 w0[2], w1[2];
+#pragma unroll
+            for (int s2 = 0; s2 < 2; s2++) {
+                w0[s2] = __builtin_bit_cast(f16x8, __builtin_amdgcn_raw_buffer_load_b128(rw1h, woff, 64 * s2, 0));
+                w1[s2] = __builtin_bit_cast(f16x8, __builtin_amdgcn_raw_buffer_load_b128(rw1h, woff, 16 * 64 * 2 + 64 * s2, 0));
+            }
+            const float b1 = lrx < 10 ? wc.c1b[lrx] : 0.f, a1 = lrx < 10 ? wc.p1[lrx] : 0.f;
+            const int corner = lrx & 3, dy = corner >> 1, dx = corner & 1;
+            // the tile's conv1 window lies inside the level: no per-corner bounds checks
+            const bool interior = 2 * (oy0 + PP_H - 1) + 1 < L1h && 2 * (ox0 + PP_W - 1) + 1 < L1w;
+            const bool mono = a1 >= 0.f;
+            for (int f0 = wave; f0 < NF1; f0 += 8) {
+                const int f1 = f0 + 4;
+                const bool two = f1 < NF1;
+                const int pp0 = f0 * 4 + (lrx >> 2), pp1 = (two ? f1 : f0) * 4 + (lrx >> 2);
+                const int ab0 = (2 * (pp0 / PP_W) + dy) * PL_W + 2 * (pp0 % PP_W) + dx;
+                const int ab1 = (2 * (pp1 / PP_W) + dy) * PL_W + 2 * (pp1 % PP_W) + dx;
+                f32x4 c0 = {0.f, 0.f, 0.f, 0.f}, c1 = c0, d0 = c0, d1 = c0;
+#pragma unroll
+                for (int s2 = 0; s2 < 2; s2++) {
+                    // slots 8*(lkx&1) .. +7 of row ky = pixels x + 2*(lkx&1), +1 (4 halves each);
+                    // row 3 (s2 = 1, lkx >= 2) has zero weights: read row 2 instead
+                    const int ky = min(2 * s2 + (lkx >> 1), 2);
+                    const int xo = (ky * PL_W + 2 * (lkx & 1)) * 4;
+                    const f16x8 a00 = ld_h8(sL + ab0 * 4 + xo), a01 = ld_h8(sL + PLN + ab0 * 4 + xo);
+                    const f16x8 a10 = ld_h8(sL + ab1 * 4 + xo), a11 = ld_h8(sL + PLN + ab1 * 4 + xo);
+                    c0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a00, w0[s2], c0, 0, 0, 0);
+                    d0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a00, w1[s2], d0, 0, 0, 0);
+                    d0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a01, w0[s2], d0, 0, 0, 0);
+                    c1 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a10, w0[s2], c1, 0, 0, 0);
+                    d1 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a10, w1[s2], d1, 0, 0, 0);
+                    d1 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a11, w0[s2], d1, 0, 0, 0);
+                }
+#pragma unroll
+                for (int h = 0; h < 2; h++) {
+                    if (h == 1 && !two) break;
+                    f32x4 cc;
+#pragma unroll
+                    for (int i = 0; i < 4; i++) cc[i] = h ? c1[i] + d1[i] * 0.00048828125f : c0[i] + d0[i] * 0.00048828125f;
+                    const int pp = (h ? f1 : f0) * 4 + lkx;
+                    float out = 0.f;  // channels 10..15 of the padded planes: zero
+                    if (lrx < 10) {
+                        if (interior && mono) {
+                            // PReLU with a non-negative slope is monotone: pool, then activate
+                            out = prelu(fmaxf(fmaxf(cc[0], cc[1]), fmaxf(cc[2], cc[3])) + b1, a1);
+                        } else {
+                            const int py = pp / PP_W, px = pp % PP_W;
+                            const int gy = 2 * (oy0 + py), gx = 2 * (ox0 + px);
+                            float m = -3.402823466e38f;
+                            bool any = false;
+#pragma unroll
+                            for (int i = 0; i < 4; i++) {
+                                const bool ok = (gy + (i >> 1) < L1h) && (gx + (i & 1) < L1w);
+                                const float v = prelu(cc[i] + b1, a1);
+                                if (ok) {
+                                    m = fmaxf(m, v);
+                                    any = true;
+                                }
+                            }
+                            out = any ? m : 0.f;  // outside the valid pooled map: keep finite
+                        }
+                    }
+                    if (lrx < PQ_C) {
+                        _Float16 x0, x1;
+                        split_f16(out, x0, x1);
+                        sQ[pp * PQ_C + lrx] = x0;
+                        sQ[NPP * PQ_C + pp * PQ_C + lrx] = x1;
+                    }
+                }
+            }
+        }
         {
             constexpr int NPP = PP_H * PP_W;        // pooled cells
             constexpr int NCH = (NPP + 63) / 64;    // 64-cell chunks
@@ -379,7 +504,7 @@ __global__ __launch_bounds__(256, PNET_GROUPS_PER_CU) void k_pnet(const uint8_t*
             // the tile's conv1 window lies inside the level: no per-corner bounds checks
             const bool interior = 2 * (oy0 + PP_H - 1) + 1 < L1h && 2 * (ox0 + PP_W - 1) + 1 < L1w;
             const int wv = __builtin_amdgcn_readfirstlane(wave);
-            for (int wt = wv; wt < ((o.dbg & 2) ? 0 : NWT); wt += 4) {
+            for (int wt = wv; wt < ((o.dbg & 2) || split3 ? 0 : NWT); wt += 4) {
                 const int g = wt / NCH, chunk = wt - g * NCH;
                 const bool live = chunk * 64 + lane < NPP;
                 const int pp = min(chunk * 64 + lane, NPP - 1);
@@ -430,23 +555,7 @@ __global__ __launch_bounds__(256, PNET_GROUPS_PER_CU) void k_pnet(const uint8_t*
                         // outside the valid pooled map (only feeds discarded cells): keep finite
                         out = any ? m : 0.f;
                     }
-                    if (live) {
-                        if (split3) {
-                            // fp16 split planes [2][cell][16 ch] (conv2's matrix-core operand)
-                            _Float16* sH = (_Float16*)sP;
-                            const _Float16 x0 = (_Float16)out;
-                            sH[pp * 16 + co] = x0;
-                            sH[NPP * 16 + pp * 16 + co] = (_Float16)((out - (float)x0) * 2048.f);
-                        } else {
-                            sP[co * NPP + pp] = out;
-                        }
-                    }
-                }
-                if (split3 && g == 1 && live) {  // channels 10..15 of the padded planes: zero
-                    uint32_t* z0 = (uint32_t*)((_Float16*)sP + pp * 16 + 10);
-                    uint32_t* z1 = (uint32_t*)((_Float16*)sP + NPP * 16 + pp * 16 + 10);
-#pragma unroll
-                    for (int q = 0; q < 3; q++) z0[q] = z1[q] = 0u;
+                    if (live) sP[co * NPP + pp] = out;
                 }
             }
         }
@@ -482,11 +591,11 @@ __global__ __launch_bounds__(256, PNET_GROUPS_PER_CU) void k_pnet(const uint8_t*
 #pragma unroll
                     for (int s5 = 0; s5 < 5; s5++) {
                         const int tap = min(2 * s5 + (lkx >> 1), 8);
-                        const int xo = ((tap / 3) * PP_W + (tap % 3)) * 16 + 8 * (lkx & 1);
-                        const f16x8 a00 = *(const f16x8*)(sH + ab0 * 16 + xo);
-                        const f16x8 a01 = *(const f16x8*)(sH + NPP * 16 + ab0 * 16 + xo);
-                        const f16x8 a10 = *(const f16x8*)(sH + ab1 * 16 + xo);
-                        const f16x8 a11 = *(const f16x8*)(sH + NPP * 16 + ab1 * 16 + xo);
+                        const int xo = ((tap / 3) * PP_W + (tap % 3)) * PQ_C + 8 * (lkx & 1);
+                        const f16x8 a00 = ld_h8(sH + ab0 * PQ_C + xo);
+                        const f16x8 a01 = ld_h8(sH + NPP * PQ_C + ab0 * PQ_C + xo);
+                        const f16x8 a10 = ld_h8(sH + ab1 * PQ_C + xo);
+                        const f16x8 a11 = ld_h8(sH + NPP * PQ_C + ab1 * PQ_C + xo);
                         c0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a00, w0[s5], c0, 0, 0, 0);
                         d0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a00, w1[s5], d0, 0, 0, 0);
                         d0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a01, w0[s5], d0, 0, 0, 0);
@@ -753,6 +862,7 @@ void launch_pnet(bool dense, const uint8_t* frames, int64_t frame_stride, int64_
                  const PNetLevel* d_levels, int n_levels, int64_t total_tiles, const PNetW& w, const PNetOut& o,
                  uint32_t* d_tile_ctr, hipStream_t st) {
     if (total_tiles <= 0) return;
+    VTF_CHECK(H < 65536 && W < 65536, VTF_E_LIMIT, "mtcnn: frames must be smaller than 65536 px per side");
     VTF_HIP(hipMemsetAsync(d_tile_ctr, 0, 4, st));
     int dev = 0, cus = 256;
     VTF_HIP(hipGetDevice(&dev));

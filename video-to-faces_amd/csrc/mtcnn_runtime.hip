@@ -125,7 +125,7 @@ static void build_weights(Mtcnn& m, const float* params, int64_t n_params) {
         const float* b = m.d_w;
         int i = 0;
         auto nx = [&]() { return b + off[i++]; };
-        m.pw = PNetW{nx(), nx(), nx(), nx(), nx(), nx(), nx(), nx(), nx(), nx(), nx(), nx(), nx(), nullptr, nullptr};
+        m.pw = PNetW{nx(), nx(), nx(), nx(), nx(), nx(), nx(), nx(), nx(), nx(), nx(), nx(), nx(), nullptr, nullptr, nullptr};
     }
     // raw (reference layout) tensors by spec index
     std::vector<const float*> raw(NP);
@@ -224,6 +224,26 @@ static void build_weights(Mtcnn& m, const float* params, int64_t n_params) {
                 m.allocs.push_back((void*)d);
                 return (const uint16_t*)d;
             };
+            {
+                std::vector<uint16_t> h((size_t)2 * 16 * 64, 0);
+                const float* W = raw[0];  // [10][3][3][3]
+                for (int co = 0; co < 10; co++)
+                    for (int c = 0; c < 3; c++)
+                        for (int ky = 0; ky < 3; ky++)
+                            for (int kx = 0; kx < 3; kx++) {
+                                const float w = W[((co * 3 + c) * 3 + ky) * 3 + kx];
+                                const _Float16 w0 = (_Float16)w;
+                                const _Float16 w1 = (_Float16)((w - (float)w0) * 2048.f);
+                                const int k = ky * 16 + kx * 4 + c;
+                                std::memcpy(&h[(size_t)co * 64 + k], &w0, 2);
+                                std::memcpy(&h[(size_t)(16 + co) * 64 + k], &w1, 2);
+                            }
+                uint16_t* d = nullptr;
+                VTF_HIP(hipMalloc((void**)&d, h.size() * 2));
+                VTF_HIP(hipMemcpy(d, h.data(), h.size() * 2, hipMemcpyHostToDevice));
+                m.allocs.push_back((void*)d);
+                m.pw.c1h = d;
+            }
             m.pw.c2h = split(raw[3], 16, 10);
             m.pw.c3h = split(raw[6], 32, 16);
         }
