@@ -218,7 +218,10 @@ constexpr int PQ_C = 12;
 constexpr int P_POOL = (10 * PP_H * PP_W > PQ_C * PP_H * PP_W + 4) ? 10 * PP_H * PP_W : PQ_C * PP_H * PP_W + 4;
 constexpr int P_LVLH = PL_H * PL_W * 4;                // level as fp16 split planes [2][y][x][4] (in floats)
 constexpr int P_A0 = P_C2 > P_LVL ? P_C2 : P_LVL;
-constexpr int P_A = P_A0 > P_LVLH ? P_A0 : P_LVLH;
+// + 4 floats of zero padding after the split level planes: conv1's 16-byte operand reads run one
+// pixel past the last level pixel (against zero weights, so the bytes there must be finite)
+constexpr int P_A = P_LVLH + 4;
+static_assert(P_A0 <= P_LVLH, "the level pad must lie past every other use of sA");
 
 // exact x / k for the bin averages: power-of-two k is an exact multiply (bit-identical to the
 // IEEE division), other k take the correctly-rounded division
@@ -263,7 +266,7 @@ __device__ inline void store_level(float* sA, bool split, int i, float r, float 
 
 constexpr int PNET_GROUPS_PER_CU = (160 * 1024) / ((PNET_LDS + 511) / 512 * 512);  // LDS granule: 512 B
 static_assert(PNET_GROUPS_PER_CU >= 2, "k_pnet tile too large for 2 workgroups per CU");
-constexpr int PATCH_BYTES = P_POOL * 4;  // frame patch staged in the (not yet used) pooled buffer
+constexpr int PATCH_BYTES = (P_POOL - 4) * 4;  // frame patch staged in the (not yet used) pooled buffer, pad excluded
 
 template <bool DENSE>
 __global__ __launch_bounds__(256, PNET_GROUPS_PER_CU) void k_pnet(const uint8_t* __restrict__ frames, int64_t frame_stride,
@@ -294,6 +297,9 @@ __global__ __launch_bounds__(256, PNET_GROUPS_PER_CU) void k_pnet(const uint8_t*
     // ---- tiles come from an atomic counter (dynamic: pyramid tiles differ in cost); the next
     //      index is requested as soon as the current one is known, so the atomic's round trip
     //      overlaps the tile's work instead of opening it
+    // zero pads read (against zero weights) past the split level planes and the pooled planes
+    if (tid < 4) sA[P_A - 4 + tid] = 0.f;
+    else if (tid < 8) sP[P_POOL - 8 + tid] = 0.f;
     if (tid == 0) s_tile = (int)atomicAdd(tile_ctr, 1u);
     for (;;) {
         __syncthreads();
@@ -436,36 +442,52 @@ __global__ __launch_bounds__(256, PNET_GROUPS_PER_CU) void k_pnet(const uint8_t*
             // the tile's conv1 window lies inside the level: no per-corner bounds checks
             const bool interior = 2 * (oy0 + PP_H - 1) + 1 < L1h && 2 * (ox0 + PP_W - 1) + 1 < L1w;
             const bool mono = a1 >= 0.f;
-            for (int f0 = wave; f0 < NF1; f0 += 8) {
-                const int f1 = f0 + 4;
-                const bool two = f1 < NF1;
-                const int pp0 = f0 * 4 + (lrx >> 2), pp1 = (two ? f1 : f0) * 4 + (lrx >> 2);
-                const int ab0 = (2 * (pp0 / PP_W) + dy) * PL_W + 2 * (pp0 % PP_W) + dx;
-                const int ab1 = (2 * (pp1 / PP_W) + dy) * PL_W + 2 * (pp1 % PP_W) + dx;
-                f32x4 c0 = {0.f, 0.f, 0.f, 0.f}, c1 = c0, d0 = c0, d1 = c0;
+            constexpr int NU = 2;  // fragments per iteration
+            for (int f0 = wave; f0 < NF1; f0 += 4 * NU) {
+                int ab[NU];
+#pragma unroll
+                for (int u = 0; u < NU; u++) {
+                    const int pp = min(f0 + 4 * u, NF1 - 1) * 4 + (lrx >> 2);
+                    ab[u] = (2 * (pp / PP_W) + dy) * PL_W + 2 * (pp % PP_W) + dx;
+                }
+                // slots 8*(lkx&1) .. +7 of row ky = pixels x + 2*(lkx&1), +1 (4 halves each); row 3
+                // (s2 = 1, lkx >= 2) has zero weights: read row 2 instead
+                f16x8 xa[2][NU], xb[2][NU];  // level planes 0 / 1
 #pragma unroll
                 for (int s2 = 0; s2 < 2; s2++) {
-                    // slots 8*(lkx&1) .. +7 of row ky = pixels x + 2*(lkx&1), +1 (4 halves each);
-                    // row 3 (s2 = 1, lkx >= 2) has zero weights: read row 2 instead
                     const int ky = min(2 * s2 + (lkx >> 1), 2);
                     const int xo = (ky * PL_W + 2 * (lkx & 1)) * 4;
-                    const f16x8 a00 = ld_h8(sL + ab0 * 4 + xo), a01 = ld_h8(sL + PLN + ab0 * 4 + xo);
-                    const f16x8 a10 = ld_h8(sL + ab1 * 4 + xo), a11 = ld_h8(sL + PLN + ab1 * 4 + xo);
-                    c0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a00, w0[s2], c0, 0, 0, 0);
-                    d0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a00, w1[s2], d0, 0, 0, 0);
-                    d0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a01, w0[s2], d0, 0, 0, 0);
-                    c1 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a10, w0[s2], c1, 0, 0, 0);
-                    d1 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a10, w1[s2], d1, 0, 0, 0);
-                    d1 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a11, w0[s2], d1, 0, 0, 0);
+#pragma unroll
+                    for (int u = 0; u < NU; u++) {
+                        xa[s2][u] = ld_h8(sL + ab[u] * 4 + xo);
+                        xb[s2][u] = ld_h8(sL + PLN + ab[u] * 4 + xo);
+                    }
+                }
+                // cross terms first, scaled by 2^-11 (exact) into the main chain's accumulator:
+                // one accumulator per fragment, no combine step
+                f32x4 cm[NU];
+#pragma unroll
+                for (int u = 0; u < NU; u++) {
+                    f32x4 cd = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                    for (int s2 = 0; s2 < 2; s2++) {
+                        cd = __builtin_amdgcn_mfma_f32_16x16x32_f16(xa[s2][u], w1[s2], cd, 0, 0, 0);
+                        cd = __builtin_amdgcn_mfma_f32_16x16x32_f16(xb[s2][u], w0[s2], cd, 0, 0, 0);
+                    }
+                    cm[u] = cd * 0.00048828125f;
                 }
 #pragma unroll
-                for (int h = 0; h < 2; h++) {
-                    if (h == 1 && !two) break;
-                    f32x4 cc;
+                for (int s2 = 0; s2 < 2; s2++)
 #pragma unroll
-                    for (int i = 0; i < 4; i++) cc[i] = h ? c1[i] + d1[i] * 0.00048828125f : c0[i] + d0[i] * 0.00048828125f;
-                    const int pp = (h ? f1 : f0) * 4 + lkx;
-                    float out = 0.f;  // channels 10..15 of the padded planes: zero
+                    for (int u = 0; u < NU; u++)
+                        cm[u] = __builtin_amdgcn_mfma_f32_16x16x32_f16(xa[s2][u], w0[s2], cm[u], 0, 0, 0);
+#pragma unroll
+                for (int u = 0; u < NU; u++) {
+                    const int f = f0 + 4 * u;
+                    if (f >= NF1) break;
+                    const f32x4 cc = cm[u];
+                    const int pp = f * 4 + lkx;
+                    float out = 0.f;  // channels 10, 11 of the padded planes: zero
                     if (lrx < 10) {
                         if (interior && mono) {
                             // PReLU with a non-negative slope is monotone: pool, then activate
