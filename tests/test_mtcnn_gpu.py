@@ -53,13 +53,13 @@ def test_pnet_level_vs_oracle(model, params):
 @pytest.mark.parametrize('force_fp32', ['0', '1'])
 def test_pnet_paths_vs_oracle(params, force_fp32, monkeypatch):
     # conv2/conv3 of k_pnet run on fp16 matrix cores with split operands by default and on fp32
-    # MFMA when VTF_PNET_FP32=1 (the fallback for weights whose activations could leave the
+    # MFMA when VTF_MTCNN_FP32=1 (the fallback for weights whose activations could leave the
     # fp16 range): both within the same fp32-grade tolerance of the oracle
     from videotofaces import synth
     from videotofaces.detectors.mtcnn import MTCNN
     from oracle import mtcnn as om
     import torch.nn.functional as F
-    monkeypatch.setenv('VTF_PNET_FP32', force_fp32)
+    monkeypatch.setenv('VTF_MTCNN_FP32', force_fp32)
     m = MTCNN('cuda:0')
     fr = synth.make_frames(2, 120, 200, seed=21)
     x = om.preprocess(list(fr))
@@ -71,7 +71,12 @@ def test_pnet_paths_vs_oracle(params, force_fp32, monkeypatch):
         np.testing.assert_allclose(reg.cpu().numpy(), rref.numpy(), rtol=0, atol=2e-5)
 
 
-def test_rnet_onet_vs_golden(g, model):
+@pytest.mark.parametrize('force_fp32', ['0', '1'])
+def test_rnet_onet_vs_golden(g, force_fp32, monkeypatch):
+    # RNet / ONet convs: split-fp16 conv mode by default, fp32 MFMA with VTF_MTCNN_FP32=1
+    from videotofaces.detectors.mtcnn import MTCNN
+    monkeypatch.setenv('VTF_MTCNN_FP32', force_fp32)
+    model = MTCNN('cuda:0')
     reg, prob = model.rnet(torch.from_numpy(g['rnet_in']))
     np.testing.assert_allclose(reg.cpu().numpy(), g['rnet_reg'], atol=2e-5)
     np.testing.assert_allclose(prob.cpu().numpy(), g['rnet_prob'], atol=2e-5)

@@ -87,7 +87,7 @@ __device__ inline void conv_epilogue(const ConvParams& p, int64_t m, int c, floa
     }
 }
 
-template <typename T, int BM, int BN, int BK, bool SPLIT>
+template <typename T, int BM, int BN, int BK, bool SPLIT, bool X = false>
 __global__ __launch_bounds__(256) void k_conv(ConvParams p) {
     using vec = typename VecT<T>::type;
     constexpr int V = VecT<T>::V;
@@ -97,9 +97,16 @@ __global__ __launch_bounds__(256) void k_conv(ConvParams p) {
     constexpr int RA = BM * KV / 256;         // A vectors per thread
     constexpr int RB = BN * KV / 256;         // B vectors per thread
     static_assert(RA >= 1 && RB >= 1 && (256 % KV) == 0, "tile config");
+    static_assert(!X || (sizeof(T) == 4 && BK == 32), "split-fp16 mode: fp32 operands, one 32-deep step");
     constexpr int WM = BM / 2, WN = BN / 2, FM = WM / 16, FN = WN / 16;
-    __shared__ __attribute__((aligned(16))) T As[BM * LDA];
-    __shared__ __attribute__((aligned(16))) T Bs[BN * LDA];
+    // X: fp16 split planes [2][rows][LDH] (row stride 80 B keeps 16-B fragment reads aligned)
+    constexpr int LDH = BK + 8;
+    constexpr int A_BYTES = X ? 2 * BM * LDH * 2 : BM * LDA * (int)sizeof(T);
+    constexpr int B_BYTES = X ? 2 * BN * LDH * 2 : BN * LDA * (int)sizeof(T);
+    __shared__ __attribute__((aligned(16))) char As_raw[A_BYTES];
+    __shared__ __attribute__((aligned(16))) char Bs_raw[B_BYTES];
+    T* As = (T*)As_raw;
+    T* Bs = (T*)Bs_raw;
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int wm = wave >> 1, wn = wave & 1;
@@ -156,15 +163,34 @@ __global__ __launch_bounds__(256) void k_conv(ConvParams p) {
         }
     };
     auto store_tile = [&]() {
+        if constexpr (X) {
+            typedef __attribute__((ext_vector_type(4))) _Float16 h4;
+            auto put = [&](char* base, int rows, int row, const vec& v) {
+                h4 x0, x1;
 #pragma unroll
-        for (int r = 0; r < RA; r++) {
-            int row = (tid + 256 * r) / KV;
-            *(vec*)(As + row * LDA + kv * V) = ra[r];
-        }
+                for (int e = 0; e < 4; e++) {
+                    x0[e] = (_Float16)to_f(v[e]);
+                    x1[e] = (_Float16)((to_f(v[e]) - (float)x0[e]) * 2048.f);
+                }
+                _Float16* h = (_Float16*)base;
+                *(h4*)(h + row * LDH + kv * 4) = x0;
+                *(h4*)(h + rows * LDH + row * LDH + kv * 4) = x1;
+            };
 #pragma unroll
-        for (int r = 0; r < RB; r++) {
-            int row = (tid + 256 * r) / KV;
-            *(vec*)(Bs + row * LDA + kv * V) = rb[r];
+            for (int r = 0; r < RA; r++) put(As_raw, BM, (tid + 256 * r) / KV, ra[r]);
+#pragma unroll
+            for (int r = 0; r < RB; r++) put(Bs_raw, BN, (tid + 256 * r) / KV, rb[r]);
+        } else {
+#pragma unroll
+            for (int r = 0; r < RA; r++) {
+                int row = (tid + 256 * r) / KV;
+                *(vec*)(As + row * LDA + kv * V) = ra[r];
+            }
+#pragma unroll
+            for (int r = 0; r < RB; r++) {
+                int row = (tid + 256 * r) / KV;
+                *(vec*)(Bs + row * LDA + kv * V) = rb[r];
+            }
         }
     };
     auto advance = [&]() {
@@ -179,11 +205,17 @@ __global__ __launch_bounds__(256) void k_conv(ConvParams p) {
         }
     };
 
-    f32x4 acc[FM][FN];
+    f32x4 acc[FM][FN], accx[X ? FM : 1][X ? FN : 1];
 #pragma unroll
     for (int i = 0; i < FM; i++)
 #pragma unroll
         for (int j = 0; j < FN; j++) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    if constexpr (X) {
+#pragma unroll
+        for (int i = 0; i < FM; i++)
+#pragma unroll
+            for (int j = 0; j < FN; j++) accx[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
 
     const int KT = kt1 - kt0;
     load_tile(k, ci, kw_, kh_);
@@ -196,7 +228,31 @@ __global__ __launch_bounds__(256) void k_conv(ConvParams p) {
         }
         const T* Aw = As + (wm * WM + (lane & 15)) * LDA;
         const T* Bw = Bs + (wn * WN + (lane & 15)) * LDA;
-        if constexpr (sizeof(T) == 2) {
+        if constexpr (X) {
+            // x*w = x0 w0 + 2^-11 (x0 w1 + x1 w0): main and cross products in separate accumulators
+            typedef __attribute__((ext_vector_type(8))) _Float16 h8;
+            const _Float16* A0 = (const _Float16*)As_raw + (wm * WM + (lane & 15)) * LDH + 8 * (lane >> 4);
+            const _Float16* B0 = (const _Float16*)Bs_raw + (wn * WN + (lane & 15)) * LDH + 8 * (lane >> 4);
+            h8 a0[FM], a1[FM], b0[FN], b1[FN];
+#pragma unroll
+            for (int i = 0; i < FM; i++) {
+                a0[i] = *(const h8*)(A0 + i * 16 * LDH);
+                a1[i] = *(const h8*)(A0 + BM * LDH + i * 16 * LDH);
+            }
+#pragma unroll
+            for (int j = 0; j < FN; j++) {
+                b0[j] = *(const h8*)(B0 + j * 16 * LDH);
+                b1[j] = *(const h8*)(B0 + BN * LDH + j * 16 * LDH);
+            }
+#pragma unroll
+            for (int i = 0; i < FM; i++)
+#pragma unroll
+                for (int j = 0; j < FN; j++) {
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a0[i], b0[j], acc[i][j], 0, 0, 0);
+                    accx[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a0[i], b1[j], accx[i][j], 0, 0, 0);
+                    accx[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a1[i], b0[j], accx[i][j], 0, 0, 0);
+                }
+        } else if constexpr (sizeof(T) == 2) {
 #pragma unroll
             for (int ks = 0; ks < BK; ks += 32) {
                 bf16x8 af[FM], bfr[FN];
@@ -232,6 +288,12 @@ __global__ __launch_bounds__(256) void k_conv(ConvParams p) {
         }
     }
 
+    if constexpr (X) {
+#pragma unroll
+        for (int i = 0; i < FM; i++)
+#pragma unroll
+            for (int j = 0; j < FN; j++) acc[i][j] = acc[i][j] + accx[i][j] * 0.00048828125f;
+    }
     // epilogue: C layout col = lane & 15, row = 4 * (lane >> 4) + i
 #pragma unroll
     for (int j = 0; j < FN; j++) {
@@ -310,6 +372,12 @@ static void launch_tile(const ConvParams& p0, hipStream_t st) {
             k_conv<T, BM, BN, BK, true><<<g, 256, 0, st>>>(p);
             const int64_t n = p.M * p.Cout;
             k_conv_splitk_epi<T><<<(unsigned)cdiv(n, 256), 256, 0, st>>>(p);
+            return;
+        }
+    }
+    if constexpr (sizeof(T) == 4) {
+        if (p.f16x) {
+            k_conv<T, BM, BN, BK, false, true><<<g, 256, 0, st>>>(p);
             return;
         }
     }

@@ -24,6 +24,8 @@ struct ConvParams {
                          // map: the FPN top-down add, rcnn.py:26-27)
     int in_cstride;      // input channel stride (0 = Cin): read a channel slice of a concat buffer
     int out_f32;         // output is fp32 whatever the operand precision (detector heads)
+    int f16x;            // fp32 operands on the fp16 matrix cores, split x = x0 + x1 * 2^-11 (fp32-grade
+                         // products; the caller guarantees |operands| < 2^14, e.g. MTCNN's bounded nets)
     int split;           // split-K factor (set by launch_conv; > 1: raw partial sums to ws)
     float* ws;           // fp32 [split][M][Cout] partial sums (split-K only)
     int64_t M;           // N*OH*OW

@@ -53,6 +53,7 @@ struct Mtcnn {
     int64_t prof_launches = 0, prof_frames = 0;
 
     std::vector<void*> allocs;
+    bool cand_x[2] = {false, false};  // RNet / ONet convs on the split-fp16 conv mode (range bound)
     ~Mtcnn() {
         for (void* p : allocs) (void)hipFree(p);
         if (ev0) (void)hipEventDestroy(ev0);
@@ -191,21 +192,31 @@ static void build_weights(Mtcnn& m, const float* params, int64_t n_params) {
     // x1 w0) drops only x1 w1 (<= 2^-24 relative): fp32-grade products.  The conv2 activations
     // must stay inside the fp16 range: bound them from the weights (level inputs lie in
     // [-1, 1]); beyond the bound k_pnet keeps the fp32 MFMA path.
+    // operand bound of a conv / dense layer with PReLU: max_co (sum_k |w| * in + |b|) * max(1, |slope|)
+    auto bound = [&](int wi, int co, int K, double in) {
+        const float* W = raw[wi];
+        double b = 0.0, amax = 1.0;
+        for (int c = 0; c < co; c++) {
+            double s = std::fabs((double)raw[wi + 1][c]);
+            for (int k = 0; k < K; k++) s += std::fabs((double)W[(size_t)c * K + k]) * in;
+            b = std::max(b, s);
+            amax = std::max(amax, std::fabs((double)raw[wi + 2][c]));
+        }
+        return b * amax;
+    };
+    const char* force = std::getenv("VTF_MTCNN_FP32");  // tests: force the fp32 MFMA paths
+    const bool allow_x = !(force && force[0] == '1');
+    // RNet / ONet layers on the conv kernel's split-fp16 mode when every operand stays < 2^14
     {
-        auto bound = [&](int wi, int co, int K, double in) {
-            const float* W = raw[wi];
-            double b = 0.0, amax = 1.0;
-            for (int c = 0; c < co; c++) {
-                double s = std::fabs((double)raw[wi + 1][c]);
-                for (int k = 0; k < K; k++) s += std::fabs((double)W[(size_t)c * K + k]) * in;
-                b = std::max(b, s);
-                amax = std::max(amax, std::fabs((double)raw[wi + 2][c]));
-            }
-            return b * amax;
-        };
+        const double r1 = bound(13, 28, 27, 1.0), r2 = bound(16, 48, 28 * 9, r1), r3 = bound(19, 64, 48 * 4, r2);
+        m.cand_x[0] = allow_x && r1 < 16384.0 && r2 < 16384.0 && r3 < 16384.0;
+        const double o1 = bound(29, 32, 27, 1.0), o2 = bound(32, 64, 32 * 9, o1), o3 = bound(35, 64, 64 * 9, o2),
+                     o4 = bound(38, 128, 64 * 4, o3);
+        m.cand_x[1] = allow_x && o1 < 16384.0 && o2 < 16384.0 && o3 < 16384.0 && o4 < 16384.0;
+    }
+    {
         const double b1 = bound(0, 10, 27, 1.0), b2 = bound(3, 16, 90, b1);
-        const char* force = std::getenv("VTF_PNET_FP32");  // tests: force the fp32 MFMA paths
-        if (b1 < 16384.0 && b2 < 16384.0 && !(force && force[0] == '1')) {
+        if (b1 < 16384.0 && b2 < 16384.0 && allow_x) {
             // [2][co][160] split planes of a [co][ci][3][3] conv, k = tap * 16 + ci
             auto split = [&](const float* W, int co_n, int ci_n) {
                 std::vector<uint16_t> h((size_t)2 * co_n * 160, 0);
@@ -296,6 +307,7 @@ static void run_candidates(Mtcnn& m, bool onet, const float* x0, int64_t n, floa
         p.K = L.k * L.k * C;
         p.M = (int64_t)n * p.OH * p.OW;
         p.out_cstride = L.cout;
+        p.f16x = m.cand_x[onet ? 1 : 0];
         VTF_CHECK(C == L.cin, VTF_E_ARG, "candidate net channel mismatch");
         launch_conv(p, false, m.st);
         H = p.OH;
