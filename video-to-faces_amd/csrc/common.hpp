@@ -49,12 +49,18 @@ int guarded(F&& f) {
 
 // Named grow-only device buffers: get(slot, bytes) returns a pointer valid until the next
 // get() of the same slot with a larger size.  Sized for 288 GB HBM: no pooling games.
+// Per-handle scratch slots that grow (x1.5) and never shrink.  An outgrown buffer is retired,
+// not freed: hipFree synchronizes the whole device, which stalls every other stream (the
+// concurrent lanes of the bench / a serving process) and would wait on kernels still queued
+// on this buffer; retired buffers are released with the handle.
 struct Arena {
     std::vector<void*> ptr;
     std::vector<size_t> cap;
+    std::vector<void*> retired;
     ~Arena() {
         for (void* p : ptr)
             if (p) (void)hipFree(p);
+        for (void* p : retired) (void)hipFree(p);
     }
     void* get(int slot, size_t bytes) {
         if ((int)ptr.size() <= slot) {
@@ -63,8 +69,8 @@ struct Arena {
         }
         if (bytes == 0) bytes = 16;
         if (cap[slot] < bytes) {
-            if (ptr[slot]) VTF_HIP(hipFree(ptr[slot]));
-            size_t b = bytes + bytes / 4;
+            if (ptr[slot]) retired.push_back(ptr[slot]);
+            size_t b = bytes + bytes / 2;
             VTF_HIP(hipMalloc(&ptr[slot], b));
             cap[slot] = b;
         }

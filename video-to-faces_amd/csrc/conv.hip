@@ -329,21 +329,22 @@ __global__ void k_conv_splitk_epi(ConvParams p) {
     conv_epilogue<T>(p, m, c, v, p.bias ? p.bias[c] : 0.f, p.alpha ? p.alpha[c] : 1.f, p.alpha ? p.beta[c] : 0.f);
 }
 
-// per-stream split-K workspace (lanes run concurrently on their own streams); grows, never shrinks
+// per-stream split-K workspace (lanes run concurrently on their own streams); grows x1.5, never
+// shrinks; an outgrown buffer is retired rather than freed (hipFree would synchronize the device
+// and queued kernels may still use it) -- bounded by the geometric growth, process lifetime
 static float* splitk_workspace(hipStream_t st, size_t bytes) {
     static std::mutex mu;
     static std::unordered_map<hipStream_t, std::pair<float*, size_t>> ws;
+    static std::vector<float*> retired;
     std::lock_guard<std::mutex> g(mu);
     auto& e = ws[st];
     if (e.second < bytes) {
-        if (e.first) {
-            VTF_HIP(hipStreamSynchronize(st));
-            VTF_HIP(hipFree(e.first));
-        }
+        if (e.first) retired.push_back(e.first);
         e.first = nullptr;
         e.second = 0;
-        VTF_HIP(hipMalloc((void**)&e.first, bytes));
-        e.second = bytes;
+        const size_t b = bytes + bytes / 2;
+        VTF_HIP(hipMalloc((void**)&e.first, b));
+        e.second = b;
     }
     return e.first;
 }

@@ -78,7 +78,9 @@ __global__ void k_seg_bounds(const uint64_t* __restrict__ keys, int64_t N, const
 struct MaskTask {
     int32_t seg;
     int32_t rb;
+    int32_t cb0, cb1;  // column blocks [cb0, cb1) of row block rb (long rows are split over waves)
 };
+constexpr int MASK_CHUNK = 8;  // column blocks per mask task
 
 __device__ inline float4 load_box(const float4* __restrict__ boxes, const int32_t* __restrict__ img,
                                   int32_t e, float off_base) {
@@ -93,7 +95,7 @@ __device__ inline float4 load_box(const float4* __restrict__ boxes, const int32_
     return b;
 }
 
-// One wave per (segment, 64-row block); loops over column blocks cb >= rb.
+// One wave per (segment, 64-row block, chunk of column blocks >= rb).
 __global__ __launch_bounds__(64) void k_iou_mask(const float4* __restrict__ boxes, const int32_t* __restrict__ img,
                                                  const int32_t* __restrict__ order, const MaskTask* __restrict__ tasks,
                                                  const int64_t* __restrict__ seg_beg, const int32_t* __restrict__ seg_n,
@@ -119,10 +121,10 @@ __global__ __launch_bounds__(64) void k_iou_mask(const float4* __restrict__ boxe
     uint64_t* out = mask + seg_mask_off[t.seg] + (int64_t)t.rb * nb * 64 + lane;
     // software-pipelined: the next column block's box is loaded while this one is compared
     float4 bnext = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (t.rb * 64 + lane < m) bnext = load_box(boxes, img, order[beg + t.rb * 64 + lane], ob);
-    for (int cb = t.rb; cb < nb; cb++) {
+    if (t.cb0 * 64 + lane < m) bnext = load_box(boxes, img, order[beg + t.cb0 * 64 + lane], ob);
+    for (int cb = t.cb0; cb < t.cb1; cb++) {
         const float4 bj = bnext;
-        if (cb + 1 < nb && (cb + 1) * 64 + lane < m) bnext = load_box(boxes, img, order[beg + (cb + 1) * 64 + lane], ob);
+        if (cb + 1 < t.cb1 && (cb + 1) * 64 + lane < m) bnext = load_box(boxes, img, order[beg + (cb + 1) * 64 + lane], ob);
         __syncthreads();
         cb_box[lane] = bj;
         cb_area[lane] = (bj.z - bj.x) * (bj.w - bj.y);
@@ -160,58 +162,71 @@ __device__ inline uint64_t wave_or(uint64_t v) {
     return ((uint64_t)wave_or32((uint32_t)(v >> 32)) << 32) | wave_or32((uint32_t)v);
 }
 
-// One wave per segment: greedy resolution, 64 rows per step.  The diagonal 64x64 block is
-// resolved in registers (readlane); the kept rows' words of every later column block are
-// loaded coalesced (64 rows x 8 B) and OR-reduced across the wave into the LDS bitset.
-__global__ __launch_bounds__(64) void k_nms_scan(const uint64_t* __restrict__ mask, const int64_t* __restrict__ seg_beg,
-                                                 const int32_t* __restrict__ seg_n,
-                                                 const int64_t* __restrict__ seg_mask_off,
-                                                 uint8_t* __restrict__ keep_sorted) {
+// One workgroup (8 waves) per segment: greedy resolution, 64 rows per step.  Wave 0 resolves
+// the diagonal 64x64 block in registers (readlane); then the kept rows' words of every later
+// column block are loaded coalesced (64 rows x 8 B) and OR-reduced across each wave into the LDS
+// bitset -- the 8 waves take interleaved groups of column blocks, so 8x the loads are in flight
+// (the scan is a serial chain of these steps).
+constexpr int SCAN_WAVES = 8;
+__global__ __launch_bounds__(64 * SCAN_WAVES) void k_nms_scan(const uint64_t* __restrict__ mask,
+                                                              const int64_t* __restrict__ seg_beg,
+                                                              const int32_t* __restrict__ seg_n,
+                                                              const int64_t* __restrict__ seg_mask_off,
+                                                              uint8_t* __restrict__ keep_sorted) {
     extern __shared__ uint64_t removed[];
+    __shared__ uint64_t s_kept;
     const int s = blockIdx.x;
-    const int lane = threadIdx.x;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int m = seg_n[s];
     if (m == 0) return;
     const int nb = (m + 63) >> 6;
     const uint64_t* msk = mask + seg_mask_off[s];
     const int64_t beg = seg_beg[s];
-    for (int w = lane; w < nb; w += 64) removed[w] = 0;
-    __builtin_amdgcn_wave_barrier();
+    for (int w = threadIdx.x; w < nb; w += 64 * SCAN_WAVES) removed[w] = 0;
+    __syncthreads();
     for (int cb = 0; cb < nb; cb++) {
-        const int row = cb * 64 + lane;
-        const int nrow = min(64, m - cb * 64);
         const uint64_t* blk = msk + (int64_t)cb * nb * 64 + lane;
-        uint64_t diag = (row < m) ? blk[(int64_t)cb * 64] : 0ull;
-        uint64_t rem = removed[cb];
-        uint64_t kept = 0;
-        for (int t = 0; t < nrow; t++) {
-            uint32_t lo = __builtin_amdgcn_readlane((uint32_t)diag, t);
-            uint32_t hi = __builtin_amdgcn_readlane((uint32_t)(diag >> 32), t);
-            if (!((rem >> t) & 1ull)) {
+        if (wave == 0) {
+            const int row = cb * 64 + lane;
+            const int nrow = min(64, m - cb * 64);
+            const uint64_t diag = (row < m) ? blk[(int64_t)cb * 64] : 0ull;
+            const uint64_t valid = nrow == 64 ? ~0ull : ((1ull << nrow) - 1ull);
+            uint64_t rem = removed[cb];
+            uint64_t kept = 0;
+            // visit only the rows still alive, in order: each kept row t ORs its diagonal word
+            // (lane t, read with a uniform lane index) into the removed set
+            uint64_t alive = valid & ~rem;
+            while (alive) {
+                const int t = __builtin_ctzll(alive);
+                const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)diag, t);
+                const uint32_t hi = __builtin_amdgcn_readlane((uint32_t)(diag >> 32), t);
                 kept |= 1ull << t;
                 rem |= ((uint64_t)hi << 32) | lo;
+                alive = valid & ~rem & (t == 63 ? 0ull : (~0ull << (t + 1)));
+            }
+            if (row < m) keep_sorted[beg + row] = (uint8_t)((kept >> lane) & 1ull);
+            if (lane == 0) s_kept = kept;
+        }
+        __syncthreads();
+        const uint64_t kept = s_kept;
+        if (kept != 0) {
+            const bool mine = (kept >> lane) & 1ull;
+            constexpr int G = 8;
+            for (int w0 = cb + 1 + wave * G; w0 < nb; w0 += SCAN_WAVES * G) {
+                uint64_t v[G];
+#pragma unroll
+                for (int g = 0; g < G; g++) {
+                    const int w = min(w0 + g, nb - 1);
+                    v[g] = mine ? blk[(int64_t)w * 64] : 0ull;
+                }
+#pragma unroll
+                for (int g = 0; g < G; g++) {
+                    const uint64_t r = wave_or(v[g]);
+                    if (lane == 0 && w0 + g < nb) removed[w0 + g] |= r;
+                }
             }
         }
-        if (row < m) keep_sorted[beg + row] = (uint8_t)((kept >> lane) & 1ull);
-        if (kept == 0) continue;
-        const bool mine = (kept >> lane) & 1ull;
-        // the words of all later column blocks are independent loads: issue 8 at a time so one
-        // memory latency covers 8 blocks (the scan is a serial chain of these groups)
-        constexpr int G = 8;
-        for (int w0 = cb + 1; w0 < nb; w0 += G) {
-            uint64_t v[G];
-#pragma unroll
-            for (int g = 0; g < G; g++) {
-                const int w = min(w0 + g, nb - 1);
-                v[g] = blk[(int64_t)w * 64];
-            }
-#pragma unroll
-            for (int g = 0; g < G; g++) {
-                const uint64_t r = wave_or(mine ? v[g] : 0ull);
-                if (lane == 0 && w0 + g < nb) removed[w0 + g] |= r;
-            }
-        }
-        __builtin_amdgcn_wave_barrier();
+        __syncthreads();
     }
 }
 
@@ -348,7 +363,8 @@ void nms_multi(Arena& ar, const float* d_boxes, const float* d_scores, const int
             int nb = (m + 63) / 64;
             maxnb = std::max(maxnb, nb);
             if (!vanilla[c]) offb[s] = cmax[c] + 1.0f;
-            for (int rb = 0; rb < nb; rb++) tasks.push_back({s, rb});
+            for (int rb = 0; rb < nb; rb++)
+                for (int c0 = rb; c0 < nb; c0 += MASK_CHUNK) tasks.push_back({s, rb, c0, std::min(nb, c0 + MASK_CHUNK)});
             pos += m;
             mtot += (int64_t)nb * nb * 64;
         }
@@ -369,7 +385,7 @@ void nms_multi(Arena& ar, const float* d_boxes, const float* d_scores, const int
         k_iou_mask<<<(int)tasks.size(), 64, 0, st>>>((const float4*)d_boxes, d_img, ord, d_tasks, d_sbeg, d_scnt,
                                                       d_moff, d_offb, thr, d_mask);
     uint8_t* keep_sorted = ar.get<uint8_t>(57, N);
-    k_nms_scan<<<S, 64, maxnb * 8, st>>>(d_mask, d_sbeg, d_scnt, d_moff, keep_sorted);
+    k_nms_scan<<<S, 64 * SCAN_WAVES, maxnb * 8, st>>>(d_mask, d_sbeg, d_scnt, d_moff, keep_sorted);
     uint8_t* keep_elem = ar.get<uint8_t>(58, N);
     k_scatter_flags<<<cdiv(N, 256), 256, 0, st>>>(ord, keep_sorted, N, keep_elem);
 
