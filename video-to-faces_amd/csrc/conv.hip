@@ -364,17 +364,15 @@ static void launch_tile(const ConvParams& p0, hipStream_t st) {
     ConvParams p = p0;
     const int64_t gx = cdiv(p.M, BM), gy = cdiv(p.Cout, BN);
     const int KT = (p.K + BK - 1) / BK;
-    p.split = pick_split(gx * gy, KT, sizeof(T) == 2);
+    p.split = pick_split(gx * gy, KT, sizeof(T) == 2 || (p.split_fp32 && !p.f16x));
     p.ws = nullptr;
     if (p.split > 1) p.ws = splitk_workspace(st, (size_t)p.split * p.M * p.Cout * sizeof(float));
     dim3 g((unsigned)gx, (unsigned)gy, (unsigned)p.split);
-    if constexpr (sizeof(T) == 2) {
-        if (p.split > 1) {
-            k_conv<T, BM, BN, BK, true><<<g, 256, 0, st>>>(p);
-            const int64_t n = p.M * p.Cout;
-            k_conv_splitk_epi<T><<<(unsigned)cdiv(n, 256), 256, 0, st>>>(p);
-            return;
-        }
+    if (p.split > 1) {
+        k_conv<T, BM, BN, BK, true><<<g, 256, 0, st>>>(p);
+        const int64_t n = p.M * p.Cout;
+        k_conv_splitk_epi<T><<<(unsigned)cdiv(n, 256), 256, 0, st>>>(p);
+        return;
     }
     if constexpr (sizeof(T) == 4) {
         if (p.f16x) {
@@ -518,48 +516,66 @@ void launch_nchw_to_nhwc(const float* in, int N, int C, int H, int W, int Cp, vo
 
 // ---------------------------------------------------------------- FaceNet head
 // AdaptiveAvgPool2d(1) -> Linear 1792->512 (no bias) -> BatchNorm1d -> F.normalize
-// (facenet.py:144-147,153).  One workgroup per image; weights fp32 [512][1792].
+// (facenet.py:144-147,153); weights fp32 [512][1792].  Pool, FC + BN on the fp32 GEMM, normalise.
 template <typename T>
-__global__ __launch_bounds__(512) void k_facenet_head(const T* __restrict__ x, int HW, int C,
-                                                      const float* __restrict__ w, const float* __restrict__ alpha,
-                                                      const float* __restrict__ beta, int D, float* __restrict__ out) {
-    extern __shared__ float sh[];
-    float* pooled = sh;      // C
-    float* red = sh + C;     // 8
-    const int n = blockIdx.x, tid = threadIdx.x;
-    const T* xn = x + (int64_t)n * HW * C;
+__global__ __launch_bounds__(256) void k_facenet_pool(const T* __restrict__ x, int N, int HW, int C,
+                                                      float* __restrict__ pooled) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= (int64_t)N * C) return;
+    const int c = (int)(i % C);
+    const int64_t n = i / C;
     int side = 1;
     while (side * side < HW) side++;
-    for (int c = tid; c < C; c += blockDim.x) {
-        float s = 0.f;
-        for (int i = 0; i < HW; i++) s = s + to_f(xn[(int64_t)i * C + c]);
-        pooled[c] = __fdiv_rn(__fdiv_rn(s, (float)side), (float)side);
-    }
-    __syncthreads();
-    float y = 0.f, sq = 0.f;
-    if (tid < D) {
-        const float* wr = w + (int64_t)tid * C;
-        float a = 0.f;
-        for (int c = 0; c < C; c++) a = fmaf(pooled[c], wr[c], a);
-        y = fmaf(a, alpha[tid], beta[tid]);
-        sq = y * y;
+    const T* xn = x + n * HW * C;
+    float s = 0.f;
+    for (int k = 0; k < HW; k++) s = s + to_f(xn[(int64_t)k * C + c]);
+    pooled[i] = __fdiv_rn(__fdiv_rn(s, (float)side), (float)side);
+}
+
+// F.normalize(p=2, dim=1): one wave per embedding
+__global__ __launch_bounds__(64) void k_l2_normalize(const float* __restrict__ y, int D, float* __restrict__ out) {
+    const int64_t n = blockIdx.x;
+    const int lane = threadIdx.x;
+    float sq = 0.f;
+    for (int d = lane; d < D; d += 64) {
+        const float v = y[n * D + d];
+        sq = fmaf(v, v, sq);
     }
     for (int off = 32; off > 0; off >>= 1) sq += __shfl_xor(sq, off);
-    if ((tid & 63) == 0) red[tid >> 6] = sq;
-    __syncthreads();
-    float tot = 0.f;
-    for (int i = 0; i < (int)(blockDim.x >> 6); i++) tot += red[i];
-    float nrm = fmaxf(sqrtf(tot), 1e-12f);
-    if (tid < D) out[(int64_t)n * D + tid] = __fdiv_rn(y, nrm);
+    const float nrm = fmaxf(sqrtf(sq), 1e-12f);
+    for (int d = lane; d < D; d += 64) out[n * D + d] = __fdiv_rn(y[n * D + d], nrm);
 }
 
 void launch_facenet_head(const void* x, int N, int HW, int C, const float* w, const float* alpha, const float* beta,
-                         int D, float* out, bool bf16, hipStream_t st) {
-    size_t shm = (C + 8) * sizeof(float);
+                         int D, float* out, float* scratch, bool bf16, hipStream_t st) {
+    if (N <= 0) return;
+    float* pooled = scratch;                 // [N][C]
+    float* y = scratch + (size_t)N * C;      // [N][D] before the L2 normalisation
+    const int64_t nc = (int64_t)N * C;
     if (bf16)
-        k_facenet_head<__bf16><<<N, 512, shm, st>>>((const __bf16*)x, HW, C, w, alpha, beta, D, out);
+        k_facenet_pool<__bf16><<<cdiv(nc, 256), 256, 0, st>>>((const __bf16*)x, N, HW, C, pooled);
     else
-        k_facenet_head<float><<<N, 512, shm, st>>>((const float*)x, HW, C, w, alpha, beta, D, out);
+        k_facenet_pool<float><<<cdiv(nc, 256), 256, 0, st>>>((const float*)x, N, HW, C, pooled);
+    // last_linear + last_bn: a 1x1 "conv" over the pooled rows on the fp32 MFMA GEMM (split-K
+    // over the 1792-deep K for a full grid), BN folded into the epilogue
+    ConvParams p{};
+    p.in = pooled;
+    p.w = w;
+    p.out = y;
+    p.alpha = alpha;
+    p.beta = beta;
+    p.scale = 1.f;
+    p.N = N;
+    p.H = p.W = p.OH = p.OW = 1;
+    p.Cin = C;
+    p.KH = p.KW = p.sh = p.sw = 1;
+    p.Cout = D;
+    p.K = C;
+    p.M = N;
+    p.out_cstride = D;
+    p.split_fp32 = 1;
+    launch_conv(p, false, st);
+    k_l2_normalize<<<N, 64, 0, st>>>(y, D, out);
 }
 
 }  // namespace vtf

@@ -26,6 +26,8 @@ struct ConvParams {
     int out_f32;         // output is fp32 whatever the operand precision (detector heads)
     int f16x;            // fp32 operands on the fp16 matrix cores, split x = x0 + x1 * 2^-11 (fp32-grade
                          // products; the caller guarantees |operands| < 2^14, e.g. MTCNN's bounded nets)
+    int split_fp32;      // allow split-K in fp32 mode too (slice-order reduction: deterministic, but the
+                         // summation order differs from the single pass; used where parity is a tolerance)
     int split;           // split-K factor (set by launch_conv; > 1: raw partial sums to ws)
     float* ws;           // fp32 [split][M][Cout] partial sums (split-K only)
     int64_t M;           // N*OH*OW
@@ -40,7 +42,8 @@ void launch_maxpool(const void* in, int N, int H, int W, int C, void* out, int o
 void launch_maxpool_ks(const float* in, int N, int H, int W, int C, int k, int s, bool ceil_mode, float* out,
                        int& OH, int& OW, hipStream_t st);
 void launch_nchw_to_nhwc(const float* in, int N, int C, int H, int W, int Cp, void* out, bool bf16, hipStream_t st);
+// scratch: N * (C + D) floats
 void launch_facenet_head(const void* x, int N, int HW, int C, const float* w, const float* alpha, const float* beta,
-                         int D, float* out, bool bf16, hipStream_t st);
+                         int D, float* out, float* scratch, bool bf16, hipStream_t st);
 
 }  // namespace vtf

@@ -304,7 +304,8 @@ static void forward(Facenet& F, const void* x, int N, float* emb) {
     }
     VTF_CHECK(li == (int)F.L.size(), VTF_E_ARG, "facenet: layer walk mismatch");
     // AdaptiveAvgPool2d(1) + Linear + BatchNorm1d + F.normalize (facenet.py:144-153)
-    launch_facenet_head(X.p, N, X.H * X.W, 1792, F.head_w, F.head_alpha, F.head_beta, 512, emb, F.bf16, F.st);
+    float* hs = F.ar.get<float>(7, (size_t)N * (1792 + 512));
+    launch_facenet_head(X.p, N, X.H * X.W, 1792, F.head_w, F.head_alpha, F.head_beta, 512, emb, hs, F.bf16, F.st);
 }
 
 }  // namespace vtf
