@@ -29,6 +29,9 @@ import torch.distributed as dist  # noqa: E402
 
 FP32_PEAK_TFLOPS = 157.3  # MI355X dense fp32 (vector = f32 MFMA), MI355X_MICROARCH.md
 BF16_PEAK_TFLOPS = 2500.0  # MI355X dense bf16 MFMA (no sparsity), MI355X_MICROARCH.md
+# k_pnet's convs run on the fp16 matrix cores with split operands (x0 w0 + 2^-11 (x0 w1 + x1 w0):
+# three fp16 products per fp32-grade product), so its fp32-equivalent ceiling is fp16 dense / 3
+F16X_PEAK_TFLOPS = round(BF16_PEAK_TFLOPS / 3, 1)
 H, W = 720, 1280
 
 
@@ -234,8 +237,9 @@ def main():
             kname = 'k_conv (YOLOv3 Darknet53+neck+head, 75 implicit-GEMM launches per det-batch, %s)' % args.det_precision
             wl = 'YOLOv3(%s)+FaceNet' % args.det_precision
         else:
-            peak = FP32_PEAK_TFLOPS
-            kname = 'k_pnet (fused pyramid resample + PNet, fp32)'
+            peak = F16X_PEAK_TFLOPS
+            kname = ('k_pnet (fused pyramid resample + PNet; convs on fp16 matrix cores with split operands, '
+                     'fp32-grade; peak = fp16 dense / 3 products)')
             wl = 'MTCNN(min_face_size=%g)+FaceNet' % args.min_face_size
         out = {
             'metric': 'faces/sec end-to-end (detect+encode) on 1280x720 synthetic frames',
@@ -248,7 +252,7 @@ def main():
             'higher_is_better': True,
             'scaling': 'weak',
             'vs_baseline': None,
-            'dtype': '%s det / %s enc' % (args.det_precision if yolo else 'fp32', args.enc_precision),
+            'dtype': '%s det / %s enc' % (args.det_precision if yolo else 'fp32 (split-fp16 MFMA)', args.enc_precision),
             'data': 'synthetic (seeded 720p value-noise frames with face blobs; hash-seeded synthetic weights, '
                     'detector heads calibrated to a few faces/frame)',
             'config': {'workload': '%s, det-batch %d, enc-batch %d, 720p, frames in HBM, '
@@ -265,7 +269,7 @@ def main():
                          'achieved': round(achieved, 3), 'peak': peak, 'unit': 'TFLOP/s',
                          'frac': round(achieved / peak, 4), 'traffic': traffic,
                          'avg_launch_ms': round(avg_ms, 4), 'flops_per_launch': flops_per_launch,
-                         'launches': k_launches},
+                         'launches': k_launches, 'concurrent_lanes': L},
             'cpu_baseline': None,
         }
         if world == 1 and not args.no_cpu_baseline:
