@@ -33,7 +33,8 @@ struct PNetOut {
     // dense (parity) mode
     float* prob;
     float* reg;
-    int dbg;  // phase-skip mask for profiling (env VTF_PNET_DEBUG): 1 fill, 2 conv1, 4 conv2, 8 conv3
+    int dbg;  // phase-skip mask for profiling (env VTF_PNET_DEBUG): 1 fill, 2 conv1, 4 conv2, 8 conv3,
+              // 16 no candidate output, 32 no heads, 64 no frame-patch staging
 };
 
 void launch_sat(const uint8_t* frames, int64_t frame_stride, int64_t row_stride, int B, int H, int W, int4* sat,

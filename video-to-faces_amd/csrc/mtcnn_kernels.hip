@@ -264,6 +264,7 @@ __device__ inline void store_level(float* sA, bool split, int i, float r, float 
     }
 }
 
+constexpr int PNET_TILE_CHUNK = 4;
 constexpr int PNET_GROUPS_PER_CU = (160 * 1024) / ((PNET_LDS + 511) / 512 * 512);  // LDS granule: 512 B
 static_assert(PNET_GROUPS_PER_CU >= 2, "k_pnet tile too large for 2 workgroups per CU");
 constexpr int PATCH_BYTES = (P_POOL - 4) * 4;  // frame patch staged in the (not yet used) pooled buffer, pad excluded
@@ -287,8 +288,9 @@ __global__ __launch_bounds__(256, PNET_GROUPS_PER_CU) void k_pnet(const uint8_t*
     __shared__ float sA[P_A];     // level tile, later conv2 output
     __shared__ float sP[P_POOL];  // frame patch (u8) during the fill, then pooled conv1
     __shared__ ushort2 ybin[PL_H], xbin[PL_W];  // frame bin [start, end) of each level row / column
-    __shared__ int s_tile;
+    __shared__ int s_tile, s_next, s_cend;
     const int tid = threadIdx.x;
+    bool pf_done = false;  // the first 2 KB of this tile's frame patch were staged by the previous tile
     const int lane = tid & 63, wave = tid >> 6;
     const int lr = lane & 15, lk = lane >> 4;
 
@@ -300,13 +302,28 @@ __global__ __launch_bounds__(256, PNET_GROUPS_PER_CU) void k_pnet(const uint8_t*
     // zero pads read (against zero weights) past the split level planes and the pooled planes
     if (tid < 4) sA[P_A - 4 + tid] = 0.f;
     else if (tid < 8) sP[P_POOL - 8 + tid] = 0.f;
-    if (tid == 0) s_tile = (int)atomicAdd(tile_ctr, 1u);
+    // tiles are handed out in chunks of PNET_TILE_CHUNK: one same-address atomic per chunk (a
+    // single counter hit once per tile serialises ~166k atomics per launch at the L2)
+    if (tid == 0) {
+        s_tile = (int)atomicAdd(tile_ctr, (uint32_t)PNET_TILE_CHUNK);
+        s_cend = s_tile + PNET_TILE_CHUNK;
+    }
     for (;;) {
         __syncthreads();
         const int64_t blk = s_tile;
         if (blk >= total_tiles) break;
-        uint32_t next_tile = 0;
-        if (tid == 0) next_tile = atomicAdd(tile_ctr, 1u);
+        uint32_t next_tile = 0, next_cend = 0;
+        if (tid == 0) {
+            const int cend = s_cend;
+            if (blk + 1 < cend) {
+                next_tile = (uint32_t)(blk + 1);
+                next_cend = (uint32_t)cend;
+            } else {  // last tile of the chunk: request the next chunk now, used at the tile's end
+                next_tile = atomicAdd(tile_ctr, (uint32_t)PNET_TILE_CHUNK);
+                next_cend = next_tile + PNET_TILE_CHUNK;
+            }
+            s_next = (int)next_tile;  // read at conv3 (several barriers later) for the prefetch
+        }
         int L = 0;
         while (L + 1 < n_levels && blk >= lv[L + 1].tile_beg) L++;
         const PNetLevel P = lv[L];
@@ -343,9 +360,9 @@ __global__ __launch_bounds__(256, PNET_GROUPS_PER_CU) void k_pnet(const uint8_t*
         const bool staged = !P.pre && (int64_t)(fy1 - fy0) * pw3 <= PATCH_BYTES;
         uint8_t* patch = (uint8_t*)sP;
         // (gathers below issue 8 loads per thread before the first use: latency-bound otherwise)
-        if (staged) {
+        if (staged && !(o.dbg & 64)) {
             const int nbytes = (fy1 - fy0) * pw3;
-            for (int i0 = tid; i0 < nbytes; i0 += 256 * 8) {
+            for (int i0 = tid + (pf_done ? 256 * 8 : 0); i0 < nbytes; i0 += 256 * 8) {
                 uint8_t v[8];
 #pragma unroll
                 for (int j = 0; j < 8; j++) {
@@ -714,6 +731,41 @@ __global__ __launch_bounds__(256, PNET_GROUPS_PER_CU) void k_pnet(const uint8_t*
         //         16x16x32 per 32-deep k-step instead of 8 fp32 16x16x4 ones (2.7x less matrix
         //         time).  Fallback (conv2 activations could leave the fp16 range, host bound):
         //         fp32 MFMA with the weights streamed in 4 chunks of 9 k-steps.
+        // ---- next tile's frame patch: the first 8 bytes per thread (2 KB, the whole patch of the
+        //      upsampled levels that dominate the tile count) are loaded here, in flight during
+        //      conv3, and stored to the (now free) patch buffer after it -- the next tile's
+        //      staging latency hides behind this tile's matrix work
+        uint8_t pfv[8];
+        int pf_n = 0;
+        {
+            const int64_t nt = s_next;
+            if (nt < total_tiles && !(o.dbg & 64)) {
+                int L2 = 0;
+                while (L2 + 1 < n_levels && nt >= lv[L2 + 1].tile_beg) L2++;
+                const PNetLevel Q = lv[L2];
+                if (!Q.pre) {
+                    const int64_t t2 = nt - Q.tile_beg;
+                    const int tpi = Q.tiles_x * Q.tiles_y;
+                    const int b2i = (int)(t2 / tpi), tt2 = (int)(t2 % tpi);
+                    const int oy2 = (tt2 / Q.tiles_x) * PT_H, ox2 = (tt2 % Q.tiles_x) * PT_W;
+                    const int ry = min(PL_H - 1, Q.lh - 1 - 2 * oy2), rx = min(PL_W - 1, Q.lw - 1 - 2 * ox2);
+                    const int gy0 = (2 * oy2 * H) / Q.lh, gy1 = ((2 * oy2 + ry + 1) * H + Q.lh - 1) / Q.lh;
+                    const int gx0 = (2 * ox2 * W) / Q.lw, gx1 = ((2 * ox2 + rx + 1) * W + Q.lw - 1) / Q.lw;
+                    const int qw3 = (gx1 - gx0) * 3;
+                    const int nb2 = (gy1 - gy0) * qw3;
+                    if ((int64_t)(gy1 - gy0) * qw3 <= PATCH_BYTES && nb2 > 0) {
+                        const uint8_t* fr2 = frames + (int64_t)b2i * frame_stride;
+#pragma unroll
+                        for (int j = 0; j < 8; j++) {
+                            const int i = min(tid + j * 256, nb2 - 1);
+                            const int r = i / qw3, q = i - r * qw3;
+                            pfv[j] = fr2[(int64_t)(gy0 + r) * row_stride + gx0 * 3 + q];
+                        }
+                        pf_n = nb2;
+                    }
+                }
+            }
+        }
         {
             constexpr int FPW = PT_H * PT_W / 64;  // 16-cell fragments per wave
             // two passes of FPW/2 fragments each: conv3 + heads per pass keeps the accumulators
@@ -818,7 +870,7 @@ __global__ __launch_bounds__(256, PNET_GROUPS_PER_CU) void k_pnet(const uint8_t*
                     }
                 }
     #pragma unroll
-                for (int j = 0; j < FH; j++) {
+                for (int j = 0; j < ((o.dbg & 32) ? 0 : FH); j++) {
                     const int cell = (wave * FPW + hh * FH + j) * 16 + lrx;
                     f32x4 hacc = {0.f, 0.f, 0.f, 0.f};
     #pragma unroll
@@ -875,7 +927,17 @@ __global__ __launch_bounds__(256, PNET_GROUPS_PER_CU) void k_pnet(const uint8_t*
                 }
             }
         }
-        if (tid == 0) s_tile = (int)next_tile;  // every thread read s_tile before this tile's barriers
+        if (pf_n > 0) {
+            uint8_t* patch2 = (uint8_t*)sP;
+#pragma unroll
+            for (int j = 0; j < 8; j++)
+                if (tid + j * 256 < pf_n) patch2[tid + j * 256] = pfv[j];
+        }
+        pf_done = pf_n > 0;
+        if (tid == 0) {  // every thread read s_tile / s_cend before this tile's barriers
+            s_tile = (int)next_tile;
+            s_cend = (int)next_cend;
+        }
         __syncthreads();  // sA/sP are rewritten by the next tile
     }
 }
