@@ -167,11 +167,14 @@ __global__ __launch_bounds__(256) void k_conv(ConvParams p) {
             typedef __attribute__((ext_vector_type(4))) _Float16 h4;
             auto put = [&](char* base, int rows, int row, const vec& v) {
                 h4 x0, x1;
+                float mx = 0.f;
 #pragma unroll
                 for (int e = 0; e < 4; e++) {
                     x0[e] = (_Float16)to_f(v[e]);
                     x1[e] = (_Float16)((to_f(v[e]) - (float)x0[e]) * 2048.f);
+                    mx = fmaxf(mx, fabsf(to_f(v[e])));
                 }
+                if (p.ovf && !(mx < 16384.f)) atomicOr(p.ovf, 1);  // also catches NaN
                 _Float16* h = (_Float16*)base;
                 *(h4*)(h + row * LDH + kv * 4) = x0;
                 *(h4*)(h + rows * LDH + row * LDH + kv * 4) = x1;

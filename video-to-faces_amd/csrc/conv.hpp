@@ -26,6 +26,8 @@ struct ConvParams {
     int out_f32;         // output is fp32 whatever the operand precision (detector heads)
     int f16x;            // fp32 operands on the fp16 matrix cores, split x = x0 + x1 * 2^-11 (fp32-grade
                          // products; the caller guarantees |operands| < 2^14, e.g. MTCNN's bounded nets)
+    int* ovf;            // f16x mode: if set, an operand of magnitude >= 2^14 sets *ovf = 1 (the caller
+                         // then re-runs in fp32: results are fp32-grade either way)
     int split_fp32;      // allow split-K in fp32 mode too (slice-order reduction: deterministic, but the
                          // summation order differs from the single pass; used where parity is a tolerance)
     int split;           // split-K factor (set by launch_conv; > 1: raw partial sums to ws)

@@ -53,12 +53,17 @@ struct Mtcnn {
     int64_t prof_launches = 0, prof_frames = 0;
 
     std::vector<void*> allocs;
-    bool cand_x[2] = {false, false};  // RNet / ONet convs on the split-fp16 conv mode (range bound)
+    // RNet / ONet convs: 0 fp32 MFMA; 1 split-fp16 conv mode, operand range proven from the
+    // weights; 2 split-fp16 guarded: a device flag reports an operand >= 2^14 and the net re-runs
+    // in fp32
+    int cand_x[2] = {0, 0};
+    int* d_ovf = nullptr;
     ~Mtcnn() {
         for (void* p : allocs) (void)hipFree(p);
         if (ev0) (void)hipEventDestroy(ev0);
         if (ev1) (void)hipEventDestroy(ev1);
         if (d_w) (void)hipFree(d_w);
+        if (d_ovf) (void)hipFree(d_ovf);
     }
 };
 
@@ -209,10 +214,11 @@ static void build_weights(Mtcnn& m, const float* params, int64_t n_params) {
     // RNet / ONet layers on the conv kernel's split-fp16 mode when every operand stays < 2^14
     {
         const double r1 = bound(13, 28, 27, 1.0), r2 = bound(16, 48, 28 * 9, r1), r3 = bound(19, 64, 48 * 4, r2);
-        m.cand_x[0] = allow_x && r1 < 16384.0 && r2 < 16384.0 && r3 < 16384.0;
+        m.cand_x[0] = !allow_x ? 0 : (r1 < 16384.0 && r2 < 16384.0 && r3 < 16384.0 ? 1 : 2);
         const double o1 = bound(29, 32, 27, 1.0), o2 = bound(32, 64, 32 * 9, o1), o3 = bound(35, 64, 64 * 9, o2),
                      o4 = bound(38, 128, 64 * 4, o3);
-        m.cand_x[1] = allow_x && o1 < 16384.0 && o2 < 16384.0 && o3 < 16384.0 && o4 < 16384.0;
+        m.cand_x[1] = !allow_x ? 0 : (o1 < 16384.0 && o2 < 16384.0 && o3 < 16384.0 && o4 < 16384.0 ? 1 : 2);
+        VTF_HIP(hipMalloc((void**)&m.d_ovf, 4));
     }
     {
         const double b1 = bound(0, 10, 27, 1.0), b2 = bound(3, 16, 90, b1);
@@ -269,8 +275,10 @@ static void build_weights(Mtcnn& m, const float* params, int64_t n_params) {
 enum RSlot { S_RA = 70, S_RB = 71 };  // nms_multi owns slots 40-61
 // first = 1: x0 is the fused front end's pooled conv1 map [n,P,P,32] (k_cand_front)
 static void run_candidates(Mtcnn& m, bool onet, const float* x0, int64_t n, float4* reg, float* lm, float* prob,
-                           int first = 0) {
+                           int first = 0, int force_fp32 = 0) {
     if (n <= 0) return;
+    const int xmode = force_fp32 ? 0 : m.cand_x[onet ? 1 : 0];
+    if (xmode == 2) VTF_HIP(hipMemsetAsync(m.d_ovf, 0, 4, m.st));
     const int S = onet ? 48 : 24;
     const auto& Ls = onet ? m.ol : m.rl;
     // pools after each conv except the last two of RNet / last two of ONet
@@ -307,7 +315,8 @@ static void run_candidates(Mtcnn& m, bool onet, const float* x0, int64_t n, floa
         p.K = L.k * L.k * C;
         p.M = (int64_t)n * p.OH * p.OW;
         p.out_cstride = L.cout;
-        p.f16x = m.cand_x[onet ? 1 : 0];
+        p.f16x = xmode != 0;
+        p.ovf = xmode == 2 ? m.d_ovf : nullptr;
         VTF_CHECK(C == L.cin, VTF_E_ARG, "candidate net channel mismatch");
         launch_conv(p, false, m.st);
         H = p.OH;
@@ -324,6 +333,15 @@ static void run_candidates(Mtcnn& m, bool onet, const float* x0, int64_t n, floa
         }
     }
     VTF_CHECK(H == 1 && W == 1, VTF_E_ARG, "candidate net shape walk mismatch");
+    if (xmode == 2) {  // guarded split-fp16: an out-of-range operand -> the whole net again in fp32
+        int ovf = 0;
+        VTF_HIP(hipMemcpyAsync(&ovf, m.d_ovf, 4, hipMemcpyDeviceToHost, m.st));
+        VTF_HIP(hipStreamSynchronize(m.st));
+        if (ovf) {
+            run_candidates(m, onet, x0, n, reg, lm, prob, first, 1);
+            return;
+        }
+    }
     if (onet)
         launch_heads(cur, n, C, m.oh1w, m.oh1b, m.oh2w, m.oh2b, m.oh3w, m.oh3b, prob, reg, lm, m.st);
     else
