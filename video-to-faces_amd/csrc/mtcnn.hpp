@@ -21,6 +21,10 @@ struct PNetW {
     const uint16_t* c3h;
     const uint16_t* c2h;  // conv2 likewise: [2][16][160], k = tap * 16 + ci (ci >= 10 zero)
     const uint16_t* c1h;  // conv1: [2][16][64], k = ky * 16 + kx * 4 + c (c = 3, kx = 3, ky = 3, co >= 10 zero)
+    // both 1x1 heads as fp16 split planes [2][16 rows][32 k] (rows 0,1 conv4_1, 2..5 conv4_2);
+    // k = 8g + j holds channel 4g + j (j < 4) or 16 + 4g + j - 4: exactly the conv3 accumulator
+    // values lane group g owns, so the heads need no lane movement.  null -> fp32 heads
+    const uint16_t* hh;
 };
 struct PNetOut {
     // sparse (candidate) mode

@@ -284,6 +284,7 @@ __global__ __launch_bounds__(256, PNET_GROUPS_PER_CU) void k_pnet(const uint8_t*
     const __amdgpu_buffer_rsrc_t rw3h = __builtin_amdgcn_make_buffer_rsrc((void*)wg.c3h, 0, 2 * 32 * 160 * 2, 0x00020000);
     const __amdgpu_buffer_rsrc_t rw2h = __builtin_amdgcn_make_buffer_rsrc((void*)wg.c2h, 0, 2 * 16 * 160 * 2, 0x00020000);
     const __amdgpu_buffer_rsrc_t rw1h = __builtin_amdgcn_make_buffer_rsrc((void*)wg.c1h, 0, 2 * 16 * 64 * 2, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rhh = __builtin_amdgcn_make_buffer_rsrc((void*)wg.hh, 0, 2 * 16 * 32 * 2, 0x00020000);
     const bool split3 = wg.c3h != nullptr;  // conv3 on fp16 matrix cores (mtcnn_runtime: range bound)
     __shared__ float sA[P_A];     // level tile, later conv2 output
     __shared__ float sP[P_POOL];  // frame patch (u8) during the fill, then pooled conv1
@@ -400,7 +401,47 @@ __global__ __launch_bounds__(256, PNET_GROUPS_PER_CU) void k_pnet(const uint8_t*
                     if (i0 + j * 256 < PL_H * PL_W) store_level(sA, split3, i0 + j * 256, v[j][0], v[j][1], v[j][2]);
             }
         }
-        for (int i = tid; i < ((o.dbg & 1) || P.pre ? 0 : PL_H * PL_W); i += 256) {
+        // separable fill: the bin sums are exact integers in any order (see sat_box), so row sums
+        // over each level column's bin (pass H, int16 in LDS after the patch) then column sums
+        // over each level row's bin (pass V) give the reference's fp32 bin sums bit for bit, with
+        // each frame byte read ~once instead of once per covering level pixel
+        const int nrows = fy1 - fy0;
+        const int hs_off = (nrows * pw3 + 3) & ~3;
+        const bool sep = staged && !(o.dbg & 1) && hs_off + nrows * PL_W * 6 <= PATCH_BYTES && W < 128 * P.lw;
+        if (sep) {
+            int16_t* hs = (int16_t*)(patch + hs_off);
+            for (int i = tid; i < nrows * PL_W; i += 256) {
+                const int r = i / PL_W, q = i - r * PL_W;
+                const int xs = xbin[q].x, n = xbin[q].y - xs;
+                const uint8_t* row = patch + r * pw3 + (xs - fx0) * 3;
+                int a0 = 0, a1 = 0, a2 = 0;
+                for (int x = 0; x < n; x++) {
+                    a0 += row[3 * x + 2];
+                    a1 += row[3 * x + 1];
+                    a2 += row[3 * x];
+                }
+                hs[3 * i] = (int16_t)(2 * a0 - 255 * n);
+                hs[3 * i + 1] = (int16_t)(2 * a1 - 255 * n);
+                hs[3 * i + 2] = (int16_t)(2 * a2 - 255 * n);
+            }
+            __syncthreads();
+            for (int i = tid; i < PL_H * PL_W; i += 256) {
+                const int r = i / PL_W, q = i - r * PL_W;
+                const int ys = ybin[r].x, kh = ybin[r].y - ys, kw = xbin[q].y - xbin[q].x;
+                const int16_t* h = hs + ((ys - fy0) * PL_W + q) * 3;
+                int s0 = 0, s1 = 0, s2 = 0;
+                for (int y = 0; y < kh; y++) {
+                    s0 += h[y * PL_W * 3];
+                    s1 += h[y * PL_W * 3 + 1];
+                    s2 += h[y * PL_W * 3 + 2];
+                }
+                const bool in = kh > 0 && kw > 0;
+                store_level(sA, split3, i, in ? div_bin(div_bin((float)s0 * 0.00390625f, kh), kw) : 0.f,
+                            in ? div_bin(div_bin((float)s1 * 0.00390625f, kh), kw) : 0.f,
+                            in ? div_bin(div_bin((float)s2 * 0.00390625f, kh), kw) : 0.f);
+            }
+        }
+        for (int i = tid; i < ((o.dbg & 1) || P.pre || sep ? 0 : PL_H * PL_W); i += 256) {
             int r = i / PL_W, q = i - r * PL_W;
             const int2 yb = make_int2(ybin[r].x, ybin[r].y), xb = make_int2(xbin[q].x, xbin[q].y);
             float s0 = 0.f, s1 = 0.f, s2 = 0.f;
@@ -786,6 +827,13 @@ __global__ __launch_bounds__(256, PNET_GROUPS_PER_CU) void k_pnet(const uint8_t*
                     const float hv = lrx < 2 ? wc.c41w[hrow] : wc.c42w[hrow];
                     hwA[mf][i] = lrx < 6 ? hv : 0.f;
                 }
+            const bool splith = wg.hh != nullptr;
+            f16x8 hw0 = {}, hw1 = {};
+            if (splith) {
+                const int hoff = (lrx * 32 + 8 * lkx) * 2;
+                hw0 = __builtin_bit_cast(f16x8, __builtin_amdgcn_raw_buffer_load_b128(rhh, hoff, 0, 0));
+                hw1 = __builtin_bit_cast(f16x8, __builtin_amdgcn_raw_buffer_load_b128(rhh, hoff, 16 * 32 * 2, 0));
+            }
             const float hb0 = wc.c41b[0], hb1 = wc.c41b[1], hb2 = wc.c42b[0], hb3 = wc.c42b[1];
             const float hb4 = wc.c42b[2], hb5 = wc.c42b[3];
 #pragma unroll 1
@@ -873,12 +921,32 @@ __global__ __launch_bounds__(256, PNET_GROUPS_PER_CU) void k_pnet(const uint8_t*
                 for (int j = 0; j < ((o.dbg & 32) ? 0 : FH); j++) {
                     const int cell = (wave * FPW + hh * FH + j) * 16 + lrx;
                     f32x4 hacc = {0.f, 0.f, 0.f, 0.f};
+                    if (splith) {
+                        // the lane's 8 activations are k = 8 * lkx .. +7 of one 16x16x32 step:
+                        // cross terms first, scaled by 2^-11 into the main product's accumulator
+                        f16x8 x0, x1;
     #pragma unroll
-                    for (int i = 0; i < 4; i++) {
-                        const float fa = prelu(acc[j][0][i] + cb3[0][i], ca3[0][i]);
-                        const float fb = prelu(acc[j][1][i] + cb3[1][i], ca3[1][i]);
-                        hacc = __builtin_amdgcn_mfma_f32_16x16x4f32(hwA[0][i], fa, hacc, 0, 0, 0);
-                        hacc = __builtin_amdgcn_mfma_f32_16x16x4f32(hwA[1][i], fb, hacc, 0, 0, 0);
+                        for (int i = 0; i < 4; i++) {
+                            _Float16 p0, p1;
+                            split_f16(prelu(acc[j][0][i] + cb3[0][i], ca3[0][i]), p0, p1);
+                            x0[i] = p0;
+                            x1[i] = p1;
+                            split_f16(prelu(acc[j][1][i] + cb3[1][i], ca3[1][i]), p0, p1);
+                            x0[4 + i] = p0;
+                            x1[4 + i] = p1;
+                        }
+                        hacc = __builtin_amdgcn_mfma_f32_16x16x32_f16(hw0, x1, hacc, 0, 0, 0);
+                        hacc = __builtin_amdgcn_mfma_f32_16x16x32_f16(hw1, x0, hacc, 0, 0, 0);
+                        hacc = hacc * 0.00048828125f;
+                        hacc = __builtin_amdgcn_mfma_f32_16x16x32_f16(hw0, x0, hacc, 0, 0, 0);
+                    } else {
+    #pragma unroll
+                        for (int i = 0; i < 4; i++) {
+                            const float fa = prelu(acc[j][0][i] + cb3[0][i], ca3[0][i]);
+                            const float fb = prelu(acc[j][1][i] + cb3[1][i], ca3[1][i]);
+                            hacc = __builtin_amdgcn_mfma_f32_16x16x4f32(hwA[0][i], fa, hacc, 0, 0, 0);
+                            hacc = __builtin_amdgcn_mfma_f32_16x16x4f32(hwA[1][i], fb, hacc, 0, 0, 0);
+                        }
                     }
                     // hacc: lane (cell lrx, heads 4*lkx + i): group 0 = (a0, a1, r0, r1), group 1 = (r2, r3, -, -)
                     const float r2 = __shfl_down(hacc[0], 16), r3 = __shfl_down(hacc[1], 16);

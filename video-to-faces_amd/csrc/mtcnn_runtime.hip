@@ -131,7 +131,7 @@ static void build_weights(Mtcnn& m, const float* params, int64_t n_params) {
         const float* b = m.d_w;
         int i = 0;
         auto nx = [&]() { return b + off[i++]; };
-        m.pw = PNetW{nx(), nx(), nx(), nx(), nx(), nx(), nx(), nx(), nx(), nx(), nx(), nx(), nx(), nullptr, nullptr, nullptr};
+        m.pw = PNetW{nx(), nx(), nx(), nx(), nx(), nx(), nx(), nx(), nx(), nx(), nx(), nx(), nx(), nullptr, nullptr, nullptr, nullptr};
     }
     // raw (reference layout) tensors by spec index
     std::vector<const float*> raw(NP);
@@ -263,6 +263,24 @@ static void build_weights(Mtcnn& m, const float* params, int64_t n_params) {
             }
             m.pw.c2h = split(raw[3], 16, 10);
             m.pw.c3h = split(raw[6], 32, 16);
+            if (bound(6, 32, 144, b2) < 16384.0) {  // conv3 activations feed the split heads
+                std::vector<uint16_t> h(2 * 16 * 32, 0);
+                for (int r = 0; r < 6; r++)
+                    for (int g = 0; g < 4; g++)
+                        for (int j = 0; j < 8; j++) {
+                            const int ch = j < 4 ? 4 * g + j : 16 + 4 * g + (j - 4);
+                            const float w = r < 2 ? raw[9][r * 32 + ch] : raw[11][(r - 2) * 32 + ch];
+                            const _Float16 w0 = (_Float16)w;
+                            const _Float16 w1 = (_Float16)((w - (float)w0) * 2048.f);
+                            std::memcpy(&h[(size_t)r * 32 + 8 * g + j], &w0, 2);
+                            std::memcpy(&h[(size_t)(16 + r) * 32 + 8 * g + j], &w1, 2);
+                        }
+                uint16_t* d = nullptr;
+                VTF_HIP(hipMalloc((void**)&d, h.size() * 2));
+                VTF_HIP(hipMemcpy(d, h.data(), h.size() * 2, hipMemcpyHostToDevice));
+                m.allocs.push_back((void*)d);
+                m.pw.hh = d;
+            }
         }
     }
     auto dev = [&](int i) { return m.d_w + off[i]; };
