@@ -1,12 +1,12 @@
 """Per-launch timeline of the FaceNet forwards in a rocprofv3 results db: span/busy of every
-forward (k_blob ... k_facenet_head) and the per-kernel listing of the largest one."""
+forward (k_blob ... k_l2_normalize) and the per-kernel listing of the largest one."""
 import glob, re, sqlite3, sys
 p = sys.argv[1]
 if not p.endswith('.db'):
     p = glob.glob(p + '/**/*results.db', recursive=True)[0]
 rows = sqlite3.connect(p).execute(
     "select name,start,end,duration,grid_x,grid_y,grid_z,workgroup_x,stream_id from kernels order by start").fetchall()
-heads = [i for i, r in enumerate(rows) if 'k_facenet_head' in r[0]]
+heads = [i for i, r in enumerate(rows) if 'k_l2_normalize' in r[0] or 'k_facenet_head' in r[0]]
 fw = []
 for h in heads:
     s = h

@@ -46,28 +46,33 @@ __device__ inline float from_f<float>(float v) { return v; }
 template <>
 __device__ inline __bf16 from_f<__bf16>(float v) { return (__bf16)v; }
 
-// fused epilogue of one output element (bias / BN / scale / residual / activation / layout)
+// residual element index of output (m, c): same layout as the output, or the half-resolution
+// map of the FPN top-down add (res_up2)
+__device__ inline int64_t res_index(const ConvParams& p, int64_t m, int c) {
+    if (!p.res_up2) return m * p.res_cstride + c;
+    const int ow = (int)(m % p.OW);
+    const int64_t t = m / p.OW;
+    const int oh = (int)(t % p.OH);
+    const int64_t n = t / p.OH;
+    return ((n * (p.OH >> 1) + (oh >> 1)) * (p.OW >> 1) + (ow >> 1)) * p.res_cstride + c;
+}
+
+// fused epilogue of one output element (bias / BN / scale / residual / activation / layout);
+// rv = the residual element (loaded by the caller: a workgroup's residual loads are issued
+// together, not one round trip per output behind the previous store)
 template <typename T>
-__device__ inline void conv_epilogue(const ConvParams& p, int64_t m, int c, float v, float bias, float al, float be) {
+__device__ inline void conv_epilogue(const ConvParams& p, int64_t m, int c, float v, float bias, float al, float be,
+                                     float pr, float rv) {
     T* __restrict__ out = (T*)p.out;
-    const T* __restrict__ res = (const T*)p.res;
     if (p.bias) v = v + bias;
     if (p.alpha) v = fmaf(v, al, be);
     if (p.scale != 1.f) v = v * p.scale;
-    int64_t ridx = m * p.res_cstride + c;
-    if (p.res_up2) {
-        int ow = (int)(m % p.OW);
-        int64_t t = m / p.OW;
-        int oh = (int)(t % p.OH);
-        int64_t n = t / p.OH;
-        ridx = ((n * (p.OH >> 1) + (oh >> 1)) * (p.OW >> 1) + (ow >> 1)) * p.res_cstride + c;
-    }
-    if (res && !p.res_post) v = v + to_f(res[ridx]);
+    if (p.res && !p.res_post) v = v + rv;
     if (p.relu) v = fmaxf(v, 0.f);
     if (p.leaky) v = v > 0.f ? v : v * p.slope;
-    if (p.prelu) v = v > 0.f ? v : p.prelu[c] * v;
+    if (p.prelu) v = v > 0.f ? v : pr * v;
     if (p.gelu) v = 0.5f * v * (1.0f + erff(v * 0.70710678118654752f));
-    if (res && p.res_post) v = v + to_f(res[ridx]);
+    if (p.res && p.res_post) v = v + rv;
     if (p.up2) {
         int ow = (int)(m % p.OW);
         int64_t t = m / p.OW;
@@ -297,24 +302,47 @@ __global__ __launch_bounds__(256) void k_conv(ConvParams p) {
 #pragma unroll
             for (int j = 0; j < FN; j++) acc[i][j] = acc[i][j] + accx[i][j] * 0.00048828125f;
     }
-    // epilogue: C layout col = lane & 15, row = 4 * (lane >> 4) + i
+    // epilogue: C layout col = lane & 15, row = 4 * (lane >> 4) + i.  Per 16-column fragment,
+    // the residual elements are loaded first (one batch of loads in flight, not one round trip
+    // per output behind the previous store), then the outputs are finished and stored.
 #pragma unroll
     for (int j = 0; j < FN; j++) {
-        int c = n0 + wn * WN + j * 16 + (lane & 15);
-        if (c >= p.Cout) continue;
-        const float bias = !SPLIT && p.bias ? p.bias[c] : 0.f;
-        const float al = !SPLIT && p.alpha ? p.alpha[c] : 1.f;
-        const float be = !SPLIT && p.alpha ? p.beta[c] : 0.f;
+        const int c = n0 + wn * WN + j * 16 + (lane & 15);
+        if constexpr (SPLIT) {
+            if (c < p.Cout) {
 #pragma unroll
-        for (int i = 0; i < FM; i++) {
+                for (int i = 0; i < FM; i++)
 #pragma unroll
-            for (int q = 0; q < 4; q++) {
-                int64_t m = m0 + wm * WM + i * 16 + 4 * (lane >> 4) + q;
-                if (m >= p.M) continue;
-                if constexpr (SPLIT)
-                    p.ws[((int64_t)blockIdx.z * p.M + m) * p.Cout + c] = acc[i][j][q];
-                else
-                    conv_epilogue<T>(p, m, c, acc[i][j][q], bias, al, be);
+                    for (int q = 0; q < 4; q++) {
+                        const int64_t m = m0 + wm * WM + i * 16 + 4 * (lane >> 4) + q;
+                        if (m < p.M) p.ws[((int64_t)blockIdx.z * p.M + m) * p.Cout + c] = acc[i][j][q];
+                    }
+            }
+        } else {
+            float rv[FM][4];
+            if (p.res) {
+                const T* __restrict__ res = (const T*)p.res;
+                const int cc = min(c, p.Cout - 1);
+#pragma unroll
+                for (int i = 0; i < FM; i++)
+#pragma unroll
+                    for (int q = 0; q < 4; q++) {
+                        const int64_t m = min(m0 + wm * WM + i * 16 + 4 * (lane >> 4) + q, p.M - 1);
+                        rv[i][q] = to_f(res[res_index(p, m, cc)]);
+                    }
+            }
+            if (c < p.Cout) {
+                const float bias = p.bias ? p.bias[c] : 0.f;
+                const float al = p.alpha ? p.alpha[c] : 1.f;
+                const float be = p.alpha ? p.beta[c] : 0.f;
+                const float pr = p.prelu ? p.prelu[c] : 0.f;
+#pragma unroll
+                for (int i = 0; i < FM; i++)
+#pragma unroll
+                    for (int q = 0; q < 4; q++) {
+                        const int64_t m = m0 + wm * WM + i * 16 + 4 * (lane >> 4) + q;
+                        if (m < p.M) conv_epilogue<T>(p, m, c, acc[i][j][q], bias, al, be, pr, p.res ? rv[i][q] : 0.f);
+                    }
             }
         }
     }
@@ -329,7 +357,9 @@ __global__ void k_conv_splitk_epi(ConvParams p) {
     const int64_t m = i / p.Cout;
     float v = 0.f;
     for (int z = 0; z < p.split; z++) v += p.ws[((int64_t)z * p.M + m) * p.Cout + c];
-    conv_epilogue<T>(p, m, c, v, p.bias ? p.bias[c] : 0.f, p.alpha ? p.alpha[c] : 1.f, p.alpha ? p.beta[c] : 0.f);
+    const float rv = p.res ? to_f(((const T*)p.res)[res_index(p, m, c)]) : 0.f;
+    conv_epilogue<T>(p, m, c, v, p.bias ? p.bias[c] : 0.f, p.alpha ? p.alpha[c] : 1.f, p.alpha ? p.beta[c] : 0.f,
+                     p.prelu ? p.prelu[c] : 0.f, rv);
 }
 
 // per-stream split-K workspace (lanes run concurrently on their own streams); grows x1.5, never
