@@ -92,6 +92,55 @@ __device__ inline void conv_epilogue(const ConvParams& p, int64_t m, int c, floa
     }
 }
 
+// 8 consecutive output channels c0..c0+7 of row m (c0 % 8 == 0, channel strides / offsets
+// multiples of 8): the same element math as conv_epilogue with 16/32-byte loads and stores
+template <typename T>
+__device__ inline void conv_epilogue8(const ConvParams& p, int64_t m, int c0, float (&v)[8], const float (&b8)[8],
+                                      const float (&al8)[8], const float (&be8)[8], const float (&pr8)[8]) {
+    typedef __attribute__((ext_vector_type(8))) T t8;
+    float rv[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    if (p.res) {
+        const t8 r = *(const t8*)((const T*)p.res + res_index(p, m, c0));
+#pragma unroll
+        for (int e = 0; e < 8; e++) rv[e] = to_f(r[e]);
+    }
+    t8 o;
+#pragma unroll
+    for (int e = 0; e < 8; e++) {
+        float x = v[e];
+        if (p.bias) x = x + b8[e];
+        if (p.alpha) x = fmaf(x, al8[e], be8[e]);
+        if (p.scale != 1.f) x = x * p.scale;
+        if (p.res && !p.res_post) x = x + rv[e];
+        if (p.relu) x = fmaxf(x, 0.f);
+        if (p.leaky) x = x > 0.f ? x : x * p.slope;
+        if (p.prelu) x = x > 0.f ? x : pr8[e] * x;
+        if (p.gelu) x = 0.5f * x * (1.0f + erff(x * 0.70710678118654752f));
+        if (p.res && p.res_post) x = x + rv[e];
+        v[e] = x;
+        o[e] = from_f<T>(x);
+    }
+    if (p.up2) {
+        const int ow = (int)(m % p.OW);
+        const int64_t t = m / p.OW;
+        const int oh = (int)(t % p.OH);
+        const int64_t n = t / p.OH;
+        T* out = (T*)p.out;
+        const int64_t a = ((n * 2 * p.OH + 2 * oh) * 2 * p.OW + 2 * ow) * p.out_cstride + p.out_coff + c0;
+        const int64_t rs = (int64_t)2 * p.OW * p.out_cstride;
+        *(t8*)(out + a) = o;
+        *(t8*)(out + a + p.out_cstride) = o;
+        *(t8*)(out + a + rs) = o;
+        *(t8*)(out + a + rs + p.out_cstride) = o;
+    } else if (p.out_f32) {
+        float* out = (float*)p.out + m * p.out_cstride + p.out_coff + c0;
+        *(f32x4*)out = f32x4{v[0], v[1], v[2], v[3]};
+        *(f32x4*)(out + 4) = f32x4{v[4], v[5], v[6], v[7]};
+    } else {
+        *(t8*)((T*)p.out + m * p.out_cstride + p.out_coff + c0) = o;
+    }
+}
+
 template <typename T, int BM, int BN, int BK, bool SPLIT, bool X = false>
 __global__ __launch_bounds__(256) void k_conv(ConvParams p) {
     using vec = typename VecT<T>::type;
@@ -108,8 +157,13 @@ __global__ __launch_bounds__(256) void k_conv(ConvParams p) {
     constexpr int LDH = BK + 8;
     constexpr int A_BYTES = X ? 2 * BM * LDH * 2 : BM * LDA * (int)sizeof(T);
     constexpr int B_BYTES = X ? 2 * BN * LDH * 2 : BN * LDA * (int)sizeof(T);
-    __shared__ __attribute__((aligned(16))) char As_raw[A_BYTES];
-    __shared__ __attribute__((aligned(16))) char Bs_raw[B_BYTES];
+    // the operand tiles, reused after the K loop as the fp32 output tile of the staged epilogue
+    constexpr int LDE = BN + 4;
+    constexpr int E_BYTES = SPLIT ? 0 : BM * LDE * 4;
+    constexpr int SM_BYTES = A_BYTES + B_BYTES > E_BYTES ? A_BYTES + B_BYTES : E_BYTES;
+    __shared__ __attribute__((aligned(16))) char smem[SM_BYTES];
+    char* As_raw = smem;
+    char* Bs_raw = smem + A_BYTES;
     T* As = (T*)As_raw;
     T* Bs = (T*)Bs_raw;
 
@@ -301,6 +355,46 @@ __global__ __launch_bounds__(256) void k_conv(ConvParams p) {
         for (int i = 0; i < FM; i++)
 #pragma unroll
             for (int j = 0; j < FN; j++) acc[i][j] = acc[i][j] + accx[i][j] * 0.00048828125f;
+    }
+    // staged epilogue: the accumulator tile goes through LDS so every thread finishes 8
+    // consecutive channels of a row -- 16-byte residual loads and output stores instead of
+    // 2-byte accesses scattered over 4 rows per instruction
+    if constexpr (!SPLIT) {
+        const bool vec_ok = (p.Cout % 8 == 0) && (p.out_cstride % 8 == 0) && (p.out_coff % 8 == 0) &&
+                            (!p.res || p.res_cstride % 8 == 0);
+        if (vec_ok) {
+            __syncthreads();  // every wave is done with the operand tiles
+            float* E = (float*)smem;
+#pragma unroll
+            for (int j = 0; j < FN; j++)
+#pragma unroll
+                for (int i = 0; i < FM; i++)
+#pragma unroll
+                    for (int q = 0; q < 4; q++)
+                        E[(wm * WM + i * 16 + 4 * (lane >> 4) + q) * LDE + wn * WN + j * 16 + (lane & 15)] = acc[i][j][q];
+            __syncthreads();
+            constexpr int G = BN / 8;  // 8-channel groups per row
+            static_assert(256 % G == 0, "epilogue groups");
+            const int g = tid % G, c0 = n0 + 8 * g;
+            if (c0 < p.Cout) {
+                float b8[8], al8[8], be8[8], pr8[8];
+#pragma unroll
+                for (int e = 0; e < 8; e++) {
+                    b8[e] = p.bias ? p.bias[c0 + e] : 0.f;
+                    al8[e] = p.alpha ? p.alpha[c0 + e] : 1.f;
+                    be8[e] = p.alpha ? p.beta[c0 + e] : 0.f;
+                    pr8[e] = p.prelu ? p.prelu[c0 + e] : 0.f;
+                }
+                for (int r = tid / G; r < BM; r += 256 / G) {
+                    const int64_t m = m0 + r;
+                    if (m >= p.M) break;
+                    const f32x4 lo = *(const f32x4*)(E + r * LDE + 8 * g), hi = *(const f32x4*)(E + r * LDE + 8 * g + 4);
+                    float v[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+                    conv_epilogue8<T>(p, m, c0, v, b8, al8, be8, pr8);
+                }
+            }
+            return;
+        }
     }
     // epilogue: C layout col = lane & 15, row = 4 * (lane >> 4) + i.  Per 16-column fragment,
     // the residual elements are loaded first (one batch of loads in flight, not one round trip
