@@ -47,7 +47,7 @@ def parse():
     ap.add_argument('--enc-precision', default='bf16', choices=['bf16', 'fp32'])
     ap.add_argument('--min-face-size', type=float, default=5.0)
     ap.add_argument('--pool', type=int, default=32, help='distinct synthetic frames per rank (cycled)')
-    ap.add_argument('--lanes', type=int, default=3, help='concurrent det-batch pipelines (threads + HIP streams) per GPU')
+    ap.add_argument('--lanes', type=int, default=2, help='concurrent det-batch pipelines (threads + HIP streams) per GPU')
     ap.add_argument('--cpu-frames', type=int, default=None,
                     help='frames in the bounded CPU-baseline sample (default 12 mtcnn / 32 yolo, ~10 s of CPU work)')
     ap.add_argument('--no-cpu-baseline', action='store_true')

@@ -1019,7 +1019,14 @@ void launch_pnet(bool dense, const uint8_t* frames, int64_t frame_stride, int64_
     int dev = 0, cus = 256;
     VTF_HIP(hipGetDevice(&dev));
     VTF_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
-    int64_t grid = std::min<int64_t>(total_tiles, (int64_t)cus * PNET_GROUPS_PER_CU);
+    // persistent workgroups per CU: PNET_GROUPS_PER_CU fills every CU; a smaller count leaves
+    // room for concurrently running lanes' kernels (env VTF_PNET_WG_PER_CU, experiments)
+    static const int wg_per_cu = [] {
+        const char* e = std::getenv("VTF_PNET_WG_PER_CU");
+        const int v = e ? std::atoi(e) : 0;
+        return v >= 1 && v <= PNET_GROUPS_PER_CU ? v : PNET_GROUPS_PER_CU;
+    }();
+    int64_t grid = std::min<int64_t>(total_tiles, (int64_t)cus * wg_per_cu);
     if (dense)
         k_pnet<true><<<(unsigned)grid, 256, 0, st>>>(frames, frame_stride, row_stride, H, W, d_levels, n_levels,
                                                       total_tiles, d_tile_ctr, w, o);
