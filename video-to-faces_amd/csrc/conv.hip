@@ -233,7 +233,8 @@ __global__ __launch_bounds__(256) void k_conv(ConvParams p) {
                     x1[e] = (_Float16)((to_f(v[e]) - (float)x0[e]) * 2048.f);
                     mx = fmaxf(mx, fabsf(to_f(v[e])));
                 }
-                if (p.ovf && !(mx < 16384.f)) atomicOr(p.ovf, 1);  // also catches NaN
+                // also catches NaN; one atomic per wave, not per lane
+                if (p.ovf && __ballot(!(mx < 16384.f)) && __lane_id() == 0) atomicOr(p.ovf, 1);
                 _Float16* h = (_Float16*)base;
                 *(h4*)(h + row * LDH + kv * 4) = x0;
                 *(h4*)(h + rows * LDH + row * LDH + kv * 4) = x1;
