@@ -2,7 +2,7 @@
 
 Workload (BASELINE.json configs[1]): MTCNN (min_face_size=5, RealMTCNN default) + FaceNet,
 det-batch 16, enc-batch 128, frames resident in HBM.  One step = one det-batch per GPU:
-  MTCNN detect (fp32 parity mode; pyramid + P/R/O-Net + NMS on device)
+  MTCNN detect (fp32-grade: split-fp16 matrix-core convs; pyramid + P/R/O-Net + NMS on device)
   -> reference box post-processing (filter_boxes / adjust_boxes, detection.py:174-262, host)
   -> crop + INTER_LINEAR resize + FaceNet on device (bf16 by default; --enc-precision fp32).
 --det-model yolo runs configs[2] instead: YOLOv3 (letterbox + Darknet53 + decode + NMS on
