@@ -44,15 +44,16 @@ __global__ void k_call_max(const float4* __restrict__ boxes, const int64_t* __re
     if (threadIdx.x == 0) call_max[c] = red[0];
 }
 
-// key = [call:12][seg image:20] [desc score:32]; element order is position order.
+// key = [call][seg image: sbits] [desc score:32], only as many high bits as the call / image
+// counts need (the radix sort runs end_bit / 8 passes); element order is position order.
 __global__ void k_seg_keys(const float* __restrict__ scores, const int32_t* __restrict__ img,
                            const int32_t* __restrict__ elem_call, const uint8_t* __restrict__ call_vanilla,
-                           int64_t N, int with_seg, uint64_t* __restrict__ keys, int32_t* __restrict__ vals) {
+                           int64_t N, int with_seg, int sbits, uint64_t* __restrict__ keys, int32_t* __restrict__ vals) {
     int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (e >= N) return;
     uint32_t c = (uint32_t)elem_call[e];
     uint32_t s = (with_seg && call_vanilla[c]) ? (uint32_t)img[e] : 0u;
-    keys[e] = ((uint64_t)((c << 20) | s) << 32) | desc_key(scores[e]);
+    keys[e] = ((uint64_t)((c << sbits) | s) << 32) | desc_key(scores[e]);
     vals[e] = (int32_t)e;
 }
 
@@ -321,10 +322,14 @@ void nms_multi(Arena& ar, const float* d_boxes, const float* d_scores, const int
 
     // small host->device tables, packed into one transfer (each hipMemcpyAsync from pageable
     // memory is a staged copy + blit kernel: ~4.5 us apiece on the lane's stream)
+    int sbits = 0, cbits = 0;
+    while ((1 << sbits) < n_img) sbits++;
+    while ((1 << cbits) < C) cbits++;
+    const int end_bit = 32 + sbits + cbits;
     std::vector<uint32_t> seg_hi(S), call_hi(C);
     for (int c = 0; c < C; c++) {
-        call_hi[c] = (uint32_t)c << 20;
-        for (int s2 = seg_base[c]; s2 < seg_base[c + 1]; s2++) seg_hi[s2] = ((uint32_t)c << 20) | (uint32_t)(s2 - seg_base[c]);
+        call_hi[c] = (uint32_t)c << sbits;
+        for (int s2 = seg_base[c]; s2 < seg_base[c + 1]; s2++) seg_hi[s2] = ((uint32_t)c << sbits) | (uint32_t)(s2 - seg_base[c]);
     }
     HostPack pk;
     const size_t o_cbeg = pk.add(call_beg.data(), C * 8), o_cn = pk.add(call_n.data(), C * 8);
@@ -355,8 +360,8 @@ void nms_multi(Arena& ar, const float* d_boxes, const float* d_scores, const int
     uint64_t* k1 = ar.get<uint64_t>(47, N);
     int32_t* v0 = ar.get<int32_t>(48, N);
     int32_t* ord = ar.get<int32_t>(49, N);
-    k_seg_keys<<<cdiv(N, 256), 256, 0, st>>>(d_scores, d_img, d_elem_call, d_van, N, 1, k0, v0);
-    sort_u64_pairs(ar, 50, k0, k1, v0, ord, N, 64, st);
+    k_seg_keys<<<cdiv(N, 256), 256, 0, st>>>(d_scores, d_img, d_elem_call, d_van, N, 1, sbits, k0, v0);
+    sort_u64_pairs(ar, 50, k0, k1, v0, ord, N, end_bit, st);
     // segment bounds by binary search on the sorted keys
     k_seg_bounds<<<cdiv(S + 1, 256), 256, 0, st>>>(k1, N, d_seghi, S, d_sstart);
     std::vector<uint8_t> r1((size_t)(S + 1) * 8 + (size_t)C * 4);
@@ -409,8 +414,8 @@ void nms_multi(Arena& ar, const float* d_boxes, const float* d_scores, const int
     k_scatter_flags<<<cdiv(N, 256), 256, 0, st>>>(ord, keep_sorted, N, keep_elem);
 
     // sort 2: (call, score desc), stable over position order -> output order
-    k_seg_keys<<<cdiv(N, 256), 256, 0, st>>>(d_scores, d_img, d_elem_call, d_van, N, 0, k0, v0);
-    sort_u64_pairs(ar, 50, k0, k1, v0, ord, N, 64, st);
+    k_seg_keys<<<cdiv(N, 256), 256, 0, st>>>(d_scores, d_img, d_elem_call, d_van, N, 0, sbits, k0, v0);
+    sort_u64_pairs(ar, 50, k0, k1, v0, ord, N, end_bit, st);
     int32_t* flag = (int32_t*)k0;  // reuse
     int32_t* incl = ((int32_t*)k0) + N;
     k_flag_in_order<<<cdiv(N, 256), 256, 0, st>>>(ord, keep_elem, N, flag);
