@@ -1163,9 +1163,9 @@ void launch_cand_front(bool onet, const int4* sat, int H, int W, const float4* b
                        const float* w1, const float* b1, const float* a1, float* out, int32_t* err, hipStream_t st) {
     if (n <= 0) return;
     if (onet)
-        k_cand_front<48, 3, 512><<<(unsigned)n, 512, 0, st>>>(sat, H, W, boxes, img, w1, b1, a1, out, err);
+        k_cand_front<48, 1, 512><<<(unsigned)n, 512, 0, st>>>(sat, H, W, boxes, img, w1, b1, a1, out, err);
     else
-        k_cand_front<24, 6, 256><<<(unsigned)n, 256, 0, st>>>(sat, H, W, boxes, img, w1, b1, a1, out, err);
+        k_cand_front<24, 3, 256><<<(unsigned)n, 256, 0, st>>>(sat, H, W, boxes, img, w1, b1, a1, out, err);
 }
 
 // heads: x [n, D] -> softmax(x W1^T + b1)[:, 1], x W2^T + b2 (4), optional x W3^T + b3 (10).
