@@ -514,10 +514,10 @@ static void launch_tile(const ConvParams& p0, hipStream_t st) {
 template <typename T>
 static void launch_t(const ConvParams& p, hipStream_t st) {
     const int bn = p.Cout <= 32 ? 32 : 64;
-    // bf16: grids of 128-row tiles that cannot fill the chip take 64-row tiles first (twice the
+    // bf16: grids of < 1.5 128-row tiles per CU take 64-row tiles first (twice the
     // workgroups from one launch; split-K with its second launch only if still short).  The
     // per-output k order is the same for every tile shape, so results do not change.
-    const bool small = sizeof(T) == 2 && (int64_t)cdiv(p.M, 128) * cdiv(p.Cout, bn) < 192;
+    const bool small = sizeof(T) == 2 && (int64_t)cdiv(p.M, 128) * cdiv(p.Cout, bn) < 384;
     if (p.Cout <= 32) {
         if constexpr (sizeof(T) == 2) {
             if (small)
