@@ -1312,28 +1312,52 @@ __global__ void k_landmarks(const float4* __restrict__ boxes, const float* __res
 
 // _nms_vectorized(method='Min', chain_suppression=True) (mtcnn.py:273-309) on score-sorted
 // rows: drop row k if any earlier row of the same image overlaps it with IoM > thr.
-__global__ void k_iom_chain(const float4* __restrict__ boxes, const int32_t* __restrict__ img,
-                            const int32_t* __restrict__ order, int64_t n, float thr, int32_t* __restrict__ keep) {
-    int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (k >= n) return;
-    int32_t j = order[k];
-    float4 b2 = boxes[j];
-    int32_t ij = img[j];
-    int drop = 0;
-    for (int64_t q = 0; q < k && !drop; q++) {
-        int32_t i = order[q];
-        if (img[i] != ij) continue;
-        float4 b1 = boxes[i];
-        float iw = (fminf(b1.z, b2.z) - fmaxf(b1.x, b2.x)) + 1.0f;
-        float ih = (fminf(b1.w, b2.w) - fmaxf(b1.y, b2.y)) + 1.0f;
-        if (!(iw > 0.f && ih > 0.f)) continue;
-        float inter = iw * ih;
-        float a1 = ((b1.z - b1.x) + 1.0f) * ((b1.w - b1.y) + 1.0f);
-        float a2 = ((b2.z - b2.x) + 1.0f) * ((b2.w - b2.y) + 1.0f);
-        float iom = __fdiv_rn(inter, fminf(a1, a2));
-        if (iom > thr) drop = 1;
+// earlier boxes (in `order`) staged through LDS in tiles of IOM_TILE; each row is scanned by
+// IOM_SUB adjacent lanes (interleaved predecessors), their drop flags OR-ed at the end
+constexpr int IOM_TILE = 1024, IOM_SUB = 4, IOM_ROWS = 256 / IOM_SUB;
+__global__ __launch_bounds__(256) void k_iom_chain(const float4* __restrict__ boxes, const int32_t* __restrict__ img,
+                                                   const int32_t* __restrict__ order, int64_t n, float thr,
+                                                   int32_t* __restrict__ keep) {
+    __shared__ float4 sb[IOM_TILE];
+    __shared__ int32_t si[IOM_TILE];
+    const int sub = threadIdx.x % IOM_SUB;
+    const int64_t k = (int64_t)blockIdx.x * IOM_ROWS + threadIdx.x / IOM_SUB;
+    const bool valid = k < n;
+    float4 b2 = make_float4(0.f, 0.f, 0.f, 0.f);
+    int32_t ij = -1;
+    if (valid) {
+        const int32_t j = order[k];
+        b2 = boxes[j];
+        ij = img[j];
     }
-    keep[k] = !drop;
+    const float a2 = ((b2.z - b2.x) + 1.0f) * ((b2.w - b2.y) + 1.0f);
+    int drop = 0;
+    const int64_t last = min(n, ((int64_t)blockIdx.x + 1) * IOM_ROWS);  // this block's rows are < last
+    for (int64_t q0 = 0; q0 < last - 1; q0 += IOM_TILE) {
+        __syncthreads();
+        for (int t = threadIdx.x; t < IOM_TILE; t += blockDim.x)
+            if (q0 + t < n) {
+                const int32_t i = order[q0 + t];
+                sb[t] = boxes[i];
+                si[t] = img[i];
+            }
+        __syncthreads();
+        const int64_t qe = valid ? min((int64_t)IOM_TILE, k - q0) : 0;
+        for (int t = sub; t < qe && !drop; t += IOM_SUB) {
+            if (si[t] != ij) continue;
+            const float4 b1 = sb[t];
+            const float iw = (fminf(b1.z, b2.z) - fmaxf(b1.x, b2.x)) + 1.0f;
+            const float ih = (fminf(b1.w, b2.w) - fmaxf(b1.y, b2.y)) + 1.0f;
+            if (!(iw > 0.f && ih > 0.f)) continue;
+            const float inter = iw * ih;
+            const float a1 = ((b1.z - b1.x) + 1.0f) * ((b1.w - b1.y) + 1.0f);
+            const float iom = __fdiv_rn(inter, fminf(a1, a2));
+            if (iom > thr) drop = 1;
+        }
+    }
+    drop |= __shfl_xor(drop, 1);
+    drop |= __shfl_xor(drop, 2);
+    if (valid && sub == 0) keep[k] = !drop;
 }
 
 void launch_decode_stage1(const uint64_t* key_sorted, const int32_t* slot_sorted, const float* score,
@@ -1361,7 +1385,7 @@ void launch_landmarks(const float4* boxes, const float* lm, int64_t n, float* ou
 }
 void launch_iom_chain(const float4* boxes, const int32_t* img, const int32_t* order, int64_t n, float thr,
                       int32_t* keep, hipStream_t st) {
-    if (n > 0) k_iom_chain<<<cdiv(n, 128), 128, 0, st>>>(boxes, img, order, n, thr, keep);
+    if (n > 0) k_iom_chain<<<cdiv(n, IOM_ROWS), 256, 0, st>>>(boxes, img, order, n, thr, keep);
 }
 
 }  // namespace vtf
