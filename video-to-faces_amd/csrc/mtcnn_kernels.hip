@@ -1,22 +1,24 @@
-// MTCNN kernels for gfx950 (fp32; parity with the reference PyTorch-CPU path).
+// MTCNN kernels for gfx950 (fp32-grade; parity with the reference PyTorch-CPU path).
 //
 // Reference: src/videotofaces/detectors/mtcnn.py
 //   _preprocess 133-139, _resample 150-151, PNet 12-38, stage-1 candidates 183-194,
 //   _get_cropped_candidates 153-163, RNet 41-76, ONet 79-121.
 //
 // MI355X design:
-//   * k_pnet: ONE launch per det-batch covers every pyramid level of every frame.  Each
-//     256-thread workgroup owns a PNET_TH x PNET_TW (24x16) tile of PNet output cells.  The
-//     level pixels it needs ((2TH+10)x(2TW+10)x3) are computed on the fly from the uint8 BGR frame (preprocess +
-//     adaptive_avg_pool2d, bit-exact: exact (u-127.5)/128, row-major fp32 bin sum, /kh, /kw)
-//     straight into LDS, so the 10.7 Mpx/frame pyramid never exists in HBM (large-bin
-//     downsampled levels come from the frame's summed-area table, k_resample_sat).  conv1+PReLU+
-//     maxpool(ceil), conv2+PReLU, conv3+PReLU and both 1x1 heads + softmax run from LDS with
-//     weights streamed through the scalar cache (wave-uniform, transposed to [ci][ky][kx][co]
-//     on the host so one s_load_dwordx16 feeds 16 v_fma).  Cells with p >= 0.6 are appended
-//     with one wave-aggregated atomic -- the dense prob/reg maps are never written.
-//   * k_rnet / k_onet: one workgroup per candidate box; the crop + adaptive pool to 24x24 /
-//     48x48 (replacing the reference's per-box Python loop) feeds the whole network in LDS.
+//   * k_pnet: ONE persistent launch per det-batch covers every pyramid level of every frame.
+//     Each 256-thread workgroup (3 per CU) takes PNET_TH x PNET_TW (16x16) tiles of PNet output
+//     cells from a chunked atomic counter.  The level pixels a tile needs ((2TH+10)^2 x 3) are
+//     computed on the fly from the uint8 BGR frame (preprocess + adaptive_avg_pool2d,
+//     bit-exact: the bin sums are exact integers) straight into LDS, so the 10.7 Mpx/frame
+//     pyramid never exists in HBM (large-bin downsampled levels come from the frame's
+//     summed-area table, k_resample_sat).  conv1 + PReLU + maxpool(ceil), conv2 + PReLU,
+//     conv3 + PReLU and both 1x1 heads run on the fp16 matrix cores with split operands
+//     (x = x0 + x1 * 2^-11, fp32-grade products), with fp32 MFMA / VALU fallbacks
+//     when the host cannot bound the activations to the fp16 range.  Cells with p >= 0.6 are
+//     appended with one wave-aggregated atomic -- the dense prob/reg maps are never written.
+//   * k_cand_front: one workgroup per candidate box; the crop + adaptive pool to 24x24 / 48x48
+//     from the SAT (replacing the reference's per-box Python loop) feeds conv1 + PReLU + the
+//     ceil max-pool in LDS; the rest of RNet / ONet runs on the conv kernel (conv.hip).
 // Build with -ffp-contract=off: only explicit fmaf() fuses.
 #include <algorithm>
 #include <cstdlib>
