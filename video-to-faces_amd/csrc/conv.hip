@@ -7,11 +7,16 @@
 //   A = im2col gathered on the fly from NHWC input (16-B vectors along ci),
 //   B = weights [Cout][K] (host re-layout), C -> fused epilogue -> NHWC output slice
 //   (channel offset + stride, so Inception concats are free).
-// Two precisions from one template:
+// Three operand modes from one template:
 //   fp32: v_mfma_f32_16x16x4_f32  (exact fp32 products, parity mode, 1e-4 vs the reference)
+//   f16x: fp32 operands split at LDS staging into x0 + x1 * 2^-11 fp16 planes, three
+//         v_mfma_f32_16x16x32_f16 per 32-deep step (fp32-grade products; callers guarantee or
+//         guard the fp16 range -- ConvParams::f16x / ovf)
 //   bf16: v_mfma_f32_16x16x32_bf16 (bf16 operands/activations, fp32 accumulate; perf mode)
 // Tile: BM x BN per 256-thread workgroup (2x2 waves, each (BM/2)x(BN/2) = 16x16 fragments),
-// BK-deep K steps, global->register prefetch of step k+1 while step k runs on MFMA from LDS.
+// BK-deep K steps, global->register prefetch of step k+1 while step k runs on MFMA from LDS;
+// split-K over blockIdx.z for grids that cannot fill the chip.  Epilogue staged through LDS:
+// each thread finishes 8 consecutive channels of a row (16/32-byte residual loads / stores).
 #include <algorithm>
 #include <mutex>
 #include <unordered_map>
