@@ -80,7 +80,9 @@ __device__ inline PNetWC to_const(const PNetW& w) {
 
 // ----------------------------------------------------------------------------------- resample
 
-// row pass: block per frame row, thread-contiguous chunks, block scan of the chunk totals
+// row pass: block per frame row, thread-contiguous chunks (read once into registers), block
+// scan of the chunk totals
+constexpr int SAT_ROW_PX = 8;  // pixels per thread (rows up to 2048 px in one pass)
 __global__ __launch_bounds__(256) void k_sat_rows(const uint8_t* __restrict__ frames, int64_t frame_stride,
                                                   int64_t row_stride, int H, int W, int4* __restrict__ sat) {
     const int y = blockIdx.x % H, b = blockIdx.x / H;
@@ -89,45 +91,59 @@ __global__ __launch_bounds__(256) void k_sat_rows(const uint8_t* __restrict__ fr
     int4* out = sat + ((int64_t)b * (H + 1) + y + 1) * W1;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int per = (W + 255) / 256, xs = tid * per;
-    int r = 0, g = 0, bl = 0;
-    for (int i = 0; i < per; i++) {
-        const int x = xs + i;
-        if (x < W) {
-            r += 2 * row[3 * x + 2] - 255;
-            g += 2 * row[3 * x + 1] - 255;
-            bl += 2 * row[3 * x] - 255;
-        }
-    }
-    // inclusive wave scan, then wave offsets
-    int ir = r, ig = g, ib = bl;
-    for (int off = 1; off < 64; off <<= 1) {
-        const int tr = __shfl_up(ir, off), tg = __shfl_up(ig, off), tb = __shfl_up(ib, off);
-        if (lane >= off) {
-            ir += tr;
-            ig += tg;
-            ib += tb;
-        }
-    }
     __shared__ int3 wt[4];
-    if (lane == 63) wt[wave] = make_int3(ir, ig, ib);
-    __syncthreads();
-    int3 base = make_int3(0, 0, 0);
-    for (int w = 0; w < wave; w++) {
-        base.x += wt[w].x;
-        base.y += wt[w].y;
-        base.z += wt[w].z;
-    }
-    r = base.x + ir - r;  // exclusive prefix of this thread's chunk
-    g = base.y + ig - g;
-    bl = base.z + ib - bl;
-    for (int i = 0; i < per; i++) {
-        const int x = xs + i;
-        if (x < W) {
-            r += 2 * row[3 * x + 2] - 255;
-            g += 2 * row[3 * x + 1] - 255;
-            bl += 2 * row[3 * x] - 255;
-            out[x + 1] = make_int4(r, g, bl, 0);
+    int3 carry = make_int3(0, 0, 0);
+    // chunks of SAT_ROW_PX pixels per thread per pass (one pass for rows up to 2048 px)
+    for (int base = 0; base < per; base += SAT_ROW_PX) {
+        int v[SAT_ROW_PX][3];
+        int r = 0, g = 0, bl = 0;
+#pragma unroll
+        for (int i = 0; i < SAT_ROW_PX; i++) {
+            const int x = xs + base + i;
+            const bool in = base + i < per && x < W;
+            v[i][0] = in ? 2 * row[3 * x + 2] - 255 : 0;
+            v[i][1] = in ? 2 * row[3 * x + 1] - 255 : 0;
+            v[i][2] = in ? 2 * row[3 * x] - 255 : 0;
+            r += v[i][0];
+            g += v[i][1];
+            bl += v[i][2];
         }
+        // inclusive wave scan, then wave offsets
+        int ir = r, ig = g, ib = bl;
+        for (int off = 1; off < 64; off <<= 1) {
+            const int tr = __shfl_up(ir, off), tg = __shfl_up(ig, off), tb = __shfl_up(ib, off);
+            if (lane >= off) {
+                ir += tr;
+                ig += tg;
+                ib += tb;
+            }
+        }
+        __syncthreads();
+        if (lane == 63) wt[wave] = make_int3(ir, ig, ib);
+        __syncthreads();
+        int3 wb = carry, tot = carry;
+        for (int w = 0; w < 4; w++) {
+            if (w < wave) {
+                wb.x += wt[w].x;
+                wb.y += wt[w].y;
+                wb.z += wt[w].z;
+            }
+            tot.x += wt[w].x;
+            tot.y += wt[w].y;
+            tot.z += wt[w].z;
+        }
+        r = wb.x + ir - r;  // exclusive prefix of this thread's chunk
+        g = wb.y + ig - g;
+        bl = wb.z + ib - bl;
+#pragma unroll
+        for (int i = 0; i < SAT_ROW_PX; i++) {
+            const int x = xs + base + i;
+            r += v[i][0];
+            g += v[i][1];
+            bl += v[i][2];
+            if (base + i < per && x < W) out[x + 1] = make_int4(r, g, bl, 0);
+        }
+        carry = tot;
     }
     if (tid == 0) {
         out[0] = make_int4(0, 0, 0, 0);
@@ -138,17 +154,18 @@ __global__ __launch_bounds__(256) void k_sat_rows(const uint8_t* __restrict__ fr
     }
 }
 
-// column pass, in place: block = 64 columns x 4 row groups (group totals combined in LDS)
+// column pass, in place: block = 16 columns x 16 row groups (group totals combined in LDS)
+constexpr int SAT_COLS = 16, SAT_GROUPS = 16;
 __global__ __launch_bounds__(256) void k_sat_cols(int H, int W, int4* __restrict__ sat) {
     const int W1 = W + 1;
-    const int ncb = (W1 + 63) / 64;
+    const int ncb = (W1 + SAT_COLS - 1) / SAT_COLS;
     const int b = blockIdx.x / ncb, cb = blockIdx.x % ncb;
-    const int lane = threadIdx.x & 63, g = threadIdx.x >> 6;
-    const int x = cb * 64 + lane;
-    const int per = (H + 3) / 4;
+    const int c = threadIdx.x % SAT_COLS, g = threadIdx.x / SAT_COLS;
+    const int x = cb * SAT_COLS + c;
+    const int per = (H + SAT_GROUPS - 1) / SAT_GROUPS;
     const int ys = 1 + g * per, ye = min(H + 1, ys + per);
     int4* col = sat + (int64_t)b * (H + 1) * W1 + x;
-    __shared__ int4 tot[4][64];
+    __shared__ int4 tot[SAT_GROUPS][SAT_COLS];
     int4 acc = make_int4(0, 0, 0, 0);
     if (x < W1)
         for (int y = ys; y < ye; y++) {
@@ -157,13 +174,13 @@ __global__ __launch_bounds__(256) void k_sat_cols(int H, int W, int4* __restrict
             acc.y += v.y;
             acc.z += v.z;
         }
-    tot[g][lane] = acc;
+    tot[g][c] = acc;
     __syncthreads();
     int4 off = make_int4(0, 0, 0, 0);
     for (int k = 0; k < g; k++) {
-        off.x += tot[k][lane].x;
-        off.y += tot[k][lane].y;
-        off.z += tot[k][lane].z;
+        off.x += tot[k][c].x;
+        off.y += tot[k][c].y;
+        off.z += tot[k][c].z;
     }
     if (x < W1)
         for (int y = ys; y < ye; y++) {
@@ -178,7 +195,7 @@ __global__ __launch_bounds__(256) void k_sat_cols(int H, int W, int4* __restrict
 void launch_sat(const uint8_t* frames, int64_t frame_stride, int64_t row_stride, int B, int H, int W, int4* sat,
                 hipStream_t st) {
     k_sat_rows<<<(unsigned)((int64_t)B * H), 256, 0, st>>>(frames, frame_stride, row_stride, H, W, sat);
-    k_sat_cols<<<(unsigned)(B * ((W + 64) / 64)), 256, 0, st>>>(H, W, sat);
+    k_sat_cols<<<(unsigned)(B * ((W + SAT_COLS) / SAT_COLS)), 256, 0, st>>>(H, W, sat);
 }
 
 // MTCNN._resample of the preprocessed frames (mtcnn.py:133-139, 150-151) from the SAT:
