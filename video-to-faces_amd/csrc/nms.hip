@@ -14,6 +14,7 @@
 // registers (readlane) and ORs kept rows into an LDS "removed" bitset -- no barriers.
 // Build with -ffp-contract=off: every IoU op is rounded exactly like the CPU kernel.
 #include <cstring>
+#include <rocprim/device/device_merge_sort.hpp>
 #include <rocprim/device/device_radix_sort.hpp>
 #include <rocprim/device/device_scan.hpp>
 
@@ -282,6 +283,17 @@ static void radix_pairs(Arena& ar, int slot, const K* kin, K* kout, const V* vin
     VTF_HIP(rocprim::radix_sort_pairs(t, tmp, kin, kout, vin, vout, (size_t)n, 0, end_bit, st));
 }
 
+// stable merge sort (block sort + independent merge passes): no decoupled look-back, so it does
+// not stall when another lane's persistent kernel holds the CUs (the radix sort's look-back
+// blocks waited up to ~0.2 ms per call under 2 lanes); used for nms_multi's two sorts
+static void merge_pairs_u64(Arena& ar, int slot, const uint64_t* kin, uint64_t* kout, const int32_t* vin,
+                            int32_t* vout, int64_t n, hipStream_t st) {
+    size_t tmp = 0;
+    VTF_HIP(rocprim::merge_sort(nullptr, tmp, kin, kout, vin, vout, (size_t)n, rocprim::less<uint64_t>(), st));
+    void* t = ar.get(slot, tmp);
+    VTF_HIP(rocprim::merge_sort(t, tmp, kin, kout, vin, vout, (size_t)n, rocprim::less<uint64_t>(), st));
+}
+
 void sort_u64_pairs(Arena& ar, int slot, const uint64_t* kin, uint64_t* kout, const int32_t* vin, int32_t* vout,
                     int64_t n, int end_bit, hipStream_t st) {
     radix_pairs(ar, slot, kin, kout, vin, vout, n, end_bit, st);
@@ -361,7 +373,8 @@ void nms_multi(Arena& ar, const float* d_boxes, const float* d_scores, const int
     int32_t* v0 = ar.get<int32_t>(48, N);
     int32_t* ord = ar.get<int32_t>(49, N);
     k_seg_keys<<<cdiv(N, 256), 256, 0, st>>>(d_scores, d_img, d_elem_call, d_van, N, 1, sbits, k0, v0);
-    sort_u64_pairs(ar, 50, k0, k1, v0, ord, N, end_bit, st);
+    merge_pairs_u64(ar, 50, k0, k1, v0, ord, N, st);
+    (void)end_bit;
     // segment bounds by binary search on the sorted keys
     k_seg_bounds<<<cdiv(S + 1, 256), 256, 0, st>>>(k1, N, d_seghi, S, d_sstart);
     std::vector<uint8_t> r1((size_t)(S + 1) * 8 + (size_t)C * 4);
@@ -415,7 +428,7 @@ void nms_multi(Arena& ar, const float* d_boxes, const float* d_scores, const int
 
     // sort 2: (call, score desc), stable over position order -> output order
     k_seg_keys<<<cdiv(N, 256), 256, 0, st>>>(d_scores, d_img, d_elem_call, d_van, N, 0, sbits, k0, v0);
-    sort_u64_pairs(ar, 50, k0, k1, v0, ord, N, end_bit, st);
+    merge_pairs_u64(ar, 50, k0, k1, v0, ord, N, st);
     int32_t* flag = (int32_t*)k0;  // reuse
     int32_t* incl = ((int32_t*)k0) + N;
     k_flag_in_order<<<cdiv(N, 256), 256, 0, st>>>(ord, keep_elem, N, flag);
