@@ -286,7 +286,7 @@ static void radix_pairs(Arena& ar, int slot, const K* kin, K* kout, const V* vin
 // stable merge sort (block sort + independent merge passes): no decoupled look-back, so it does
 // not stall when another lane's persistent kernel holds the CUs (the radix sort's look-back
 // blocks waited up to ~0.2 ms per call under 2 lanes); used for nms_multi's two sorts
-static void merge_pairs_u64(Arena& ar, int slot, const uint64_t* kin, uint64_t* kout, const int32_t* vin,
+void merge_pairs_u64(Arena& ar, int slot, const uint64_t* kin, uint64_t* kout, const int32_t* vin,
                             int32_t* vout, int64_t n, hipStream_t st) {
     size_t tmp = 0;
     VTF_HIP(rocprim::merge_sort(nullptr, tmp, kin, kout, vin, vout, (size_t)n, rocprim::less<uint64_t>(), st));
