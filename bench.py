@@ -32,6 +32,8 @@ BF16_PEAK_TFLOPS = 2500.0  # MI355X dense bf16 MFMA (no sparsity), MI355X_MICROA
 # k_pnet's convs run on the fp16 matrix cores with split operands (x0 w0 + 2^-11 (x0 w1 + x1 w0):
 # three fp16 products per fp32-grade product), so its fp32-equivalent ceiling is fp16 dense / 3
 F16X_PEAK_TFLOPS = round(BF16_PEAK_TFLOPS / 3, 1)
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E (MI355X_MICROARCH.md)
+LBL_BYTES_PER_FLOP = 2075e6 / 38.66e9  # PNet layer-by-layer fp32 bytes per FLOP
 H, W = 720, 1280
 
 
@@ -270,6 +272,15 @@ def main():
                          'frac': round(achieved / peak, 4), 'traffic': traffic,
                          'avg_launch_ms': round(avg_ms, 4), 'flops_per_launch': flops_per_launch,
                          'launches': k_launches, 'concurrent_lanes': L},
+            # north-star's "memory-bound HBM roofline on the detector conv path": the layer-by-layer
+            # PNet bytes of SURVEY.md §8d (2,075 MB fp32 per 720p frame at 38.66 GFLOP, AI 18.6) over
+            # the same launch time -- an equivalent rate (the fused kernel moves `traffic` bytes)
+            'hbm_equiv': None if yolo else {
+                'bytes_per_launch': round(flops_per_launch * LBL_BYTES_PER_FLOP),
+                'achieved': round(flops_per_launch * LBL_BYTES_PER_FLOP / (avg_ms / 1e3) / 1e9, 1) if avg_ms > 0 else 0.0,
+                'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
+                'frac': round(flops_per_launch * LBL_BYTES_PER_FLOP / (avg_ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4)
+                if avg_ms > 0 else 0.0},
             'cpu_baseline': None,
         }
         if world == 1 and not args.no_cpu_baseline:

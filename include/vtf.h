@@ -113,10 +113,13 @@ int vtf_blob_from_crops(const uint8_t* d_frames, int H, int W, int64_t frame_str
 /* ---------------------------------------------------------------- ViT encoder
  * Replaces ViT / AnimeVIT (src/videotofaces/encoders/vit.py:80-146), called by grouping.py:37.
  * dim 768 / depth 12 (B16) or 1024 / 24 (L16); params in the reference state_dict order
- * (specs.py vit_spec).  fp32. */
+ * (specs.py vit_spec).  fp32 or guarded split-fp16 (vtf_vit_set_precision). */
 int vtf_vit_create(const float* params, int64_t n_params, int dim, int depth, int device, vtf_vit_t* out);
 int vtf_vit_destroy(vtf_vit_t h);
 int vtf_vit_set_stream(vtf_vit_t h, void* hip_stream);
+/* GEMM operand mode: 0 = fp32 MFMA (default); 2 = fp32 operands split into two fp16 parts on the
+ * fp16 matrix cores (fp32-grade products), guarded: an operand >= 2^14 re-runs the forward in fp32. */
+int vtf_vit_set_precision(vtf_vit_t h, int mode);
 /* d_x [N,3,128,128] fp32 blob (blobFromImages(1/127.5, 128x128, 127.5, swapRB)) -> d_emb [N,dim]
  * (LayerNorm of the CLS token, not L2-normalised). */
 int vtf_vit_forward(vtf_vit_t h, const float* d_x, int64_t N, float* d_emb);

@@ -1,4 +1,4 @@
-// ViT-B/16 and ViT-L/16 encoders on gfx950 (fp32 parity mode).
+// ViT-B/16 and ViT-L/16 encoders on gfx950 (fp32 MFMA, or fp32-grade split-fp16 MFMA, guarded).
 //
 // Replaces ViT / AnimeVIT (src/videotofaces/encoders/vit.py:9-146):
 //   patch conv 16x16/16 -> [N,64,D]; CLS + pos -> [N,65,D]; depth x pre-LN blocks
@@ -117,6 +117,10 @@ struct Lin {
 
 struct Vit {
     int device = 0, D = 768, depth = 12, heads = 12;
+    // GEMM operand mode: 0 fp32 MFMA; 2 split-fp16 (fp32-grade products on the fp16 matrix
+    // cores, conv.hip f16x) guarded by the device overflow flag -> the forward re-runs in fp32
+    int xmode = 0, cur_x = 0;
+    int* d_ovf = nullptr;
     hipStream_t st = 0;
     const float *cls = nullptr, *pos = nullptr, *pw = nullptr, *pb = nullptr;  // patch conv [D][16][16][8]
     struct Block {
@@ -129,6 +133,7 @@ struct Vit {
     Arena ar;
     ~Vit() {
         for (void* p : allocs) (void)hipFree(p);
+        if (d_ovf) (void)hipFree(d_ovf);
     }
     const float* up(const std::vector<float>& v) {
         void* p = nullptr;
@@ -205,6 +210,8 @@ static void linear(Vit& V, const Lin& L, const float* x, int64_t M, float* y, co
     p.K = L.in;
     p.M = M;
     p.out_cstride = L.out;
+    p.f16x = V.cur_x != 0;
+    p.ovf = V.cur_x ? V.d_ovf : nullptr;
     launch_conv(p, false, V.st);
 }
 
@@ -234,6 +241,8 @@ static void vit_forward(Vit& V, const float* x_nhwc8, int64_t N, float* emb) {
     p.K = 16 * 16 * 8;
     p.M = N * 64;
     p.out_cstride = D;
+    p.f16x = V.cur_x != 0;
+    p.ovf = V.cur_x ? V.d_ovf : nullptr;
     launch_conv(p, false, V.st);
     k_vit_tokens<<<cdiv(M * D, 256), 256, 0, V.st>>>(patches, V.cls, V.pos, N, D, X);
     for (const auto& B : V.blocks) {
@@ -249,6 +258,24 @@ static void vit_forward(Vit& V, const float* x_nhwc8, int64_t N, float* emb) {
     }
     // LayerNorm of the CLS rows (vit.py:100-101)
     k_layernorm<<<(unsigned)N, 256, 0, V.st>>>(X, N, D, (int64_t)VT * D, V.nw, V.nb, 1e-12f, emb, D);
+}
+
+// forward in the handle's operand mode; guarded split-fp16: an operand >= 2^14 (or NaN) anywhere
+// raises the flag and the whole forward runs again on fp32 MFMA (same contract as MTCNN's ONet)
+static void vit_run(Vit& V, const float* x_nhwc8, int64_t N, float* emb) {
+    V.cur_x = V.xmode;
+    if (V.cur_x) {
+        if (!V.d_ovf) VTF_HIP(hipMalloc((void**)&V.d_ovf, 4));
+        VTF_HIP(hipMemsetAsync(V.d_ovf, 0, 4, V.st));
+    }
+    vit_forward(V, x_nhwc8, N, emb);
+    if (V.cur_x) {
+        int ovf = 0;
+        VTF_HIP(hipMemcpyAsync(&ovf, V.d_ovf, 4, hipMemcpyDeviceToHost, V.st));
+        VTF_HIP(hipStreamSynchronize(V.st));
+        V.cur_x = 0;
+        if (ovf) vit_forward(V, x_nhwc8, N, emb);
+    }
 }
 
 }  // namespace vtf
@@ -290,6 +317,13 @@ int vtf_vit_destroy(vtf_vit_t h) {
     return guarded([&] { delete h; });
 }
 
+int vtf_vit_set_precision(vtf_vit_t h, int mode) {
+    return guarded([&] {
+        VTF_CHECK(h && (mode == 0 || mode == 2), VTF_E_ARG, "vit precision: 0 (fp32) or 2 (guarded split-fp16)");
+        h->v.xmode = mode;
+    });
+}
+
 int vtf_vit_set_stream(vtf_vit_t h, void* stream) {
     return guarded([&] {
         VTF_CHECK(h, VTF_E_ARG, "null handle");
@@ -304,7 +338,7 @@ int vtf_vit_forward(vtf_vit_t h, const float* d_x, int64_t N, float* d_emb) {
         VTF_CHECK(d_x && d_emb, VTF_E_ARG, "null argument");
         float* x8 = h->v.ar.get<float>(6, N * 128 * 128 * 8);
         launch_nchw_to_nhwc(d_x, (int)N, 3, 128, 128, 8, x8, false, h->v.st);
-        vit_forward(h->v, x8, N, d_emb);
+        vit_run(h->v, x8, N, d_emb);
         VTF_HIP(hipGetLastError());
     });
 }
@@ -321,7 +355,7 @@ int vtf_vit_encode_crops(vtf_vit_t h, const uint8_t* d_frames, int H, int W, int
         // blobFromImages(images, 1/127.5, (128,128), (127.5,)*3, swapRB=True) (vit.py:141)
         launch_blob(d_frames, H, W, frame_stride, row_stride, dc, N, 128, 127.5f, (float)(1.0 / 127.5), 1, 8, false,
                     x8, h->v.st);
-        vit_forward(h->v, x8, N, d_emb);
+        vit_run(h->v, x8, N, d_emb);
         VTF_HIP(hipGetLastError());
     });
 }

@@ -46,6 +46,7 @@ SIGNATURES = {
     'vtf_vit_create': [_p, _i64, _i32, _i32, _i32, _p],
     'vtf_vit_destroy': [_p],
     'vtf_vit_set_stream': [_p, _p],
+    'vtf_vit_set_precision': [_p, _i32],
     'vtf_vit_forward': [_p, _p, _i64, _p],
     'vtf_vit_encode_crops': [_p, _p, _i32, _i32, _i64, _i64, _p, _i64, _p],
     'vtf_blob_from_crops': [_p, _i32, _i32, _i64, _i64, _p, _i64, _i32, _f32, _f32, _p, _p],

@@ -3,7 +3,8 @@
 ``AnimeVIT(device, isL=False)`` keeps the reference constructor and ``__call__`` contract
 (vit.py:105-146): ``list[np.ndarray uint8 (h,w,3) BGR]`` -> ``np.ndarray f32 [N,768|1024]``
 (LayerNorm of the CLS token, not L2-normalised).  Blob (128x128, (x-127.5)/127.5, RGB) and
-the whole ViT-B/16 or ViT-L/16 run in libvtf_hip.so (fp32).
+the whole ViT-B/16 or ViT-L/16 run in libvtf_hip.so: fp32 operands, GEMMs on the fp16 matrix
+cores with split operands (fp32-grade products; guarded, fp32 MFMA fallback) or on fp32 MFMA.
 """
 import ctypes
 import os
@@ -19,7 +20,11 @@ from .facenet import blob_from_images
 class ViT:
     """Handle around vtf_vit_* (the reference's nn.Module ViT, vit.py:80-102)."""
 
-    def __init__(self, device=None, params=None, isL=False):
+    def __init__(self, device=None, params=None, isL=False, precision='f16x'):
+        """precision: 'fp32' (fp32 MFMA) or 'f16x' (fp32-grade split-fp16 MFMA products, guarded:
+        an out-of-range operand re-runs the forward in fp32)."""
+        if precision not in ('fp32', 'f16x'):
+            raise ValueError("precision must be 'fp32' or 'f16x'")
         self.device = nat.require_gpu(device)
         self.name = 'vit_l' if isL else 'vit_b'
         self.dim, depth = (1024, 24) if isL else (768, 12)
@@ -30,6 +35,8 @@ class ViT:
         nat.check(nat.lib().vtf_vit_create(flat.ctypes.data, flat.size, self.dim, depth, self.device.index or 0,
                                            ctypes.byref(h)))
         self._h = h
+        self.precision = precision
+        nat.check(nat.lib().vtf_vit_set_precision(h, 2 if precision == 'f16x' else 0))
 
     def __del__(self):
         h = getattr(self, '_h', None)
