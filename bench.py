@@ -49,7 +49,7 @@ def parse():
     ap.add_argument('--enc-precision', default='bf16', choices=['bf16', 'fp32'])
     ap.add_argument('--min-face-size', type=float, default=5.0)
     ap.add_argument('--pool', type=int, default=32, help='distinct synthetic frames per rank (cycled)')
-    ap.add_argument('--lanes', type=int, default=2, help='concurrent det-batch pipelines (threads + HIP streams) per GPU')
+    ap.add_argument('--lanes', type=int, default=3, help='concurrent det-batch pipelines (threads + HIP streams) per GPU')
     ap.add_argument('--cpu-frames', type=int, default=None,
                     help='frames in the bounded CPU-baseline sample (default 12 mtcnn / 32 yolo, ~10 s of CPU work)')
     ap.add_argument('--no-cpu-baseline', action='store_true')
@@ -218,6 +218,14 @@ def main():
     for d in dets:
         a, b_, c, e = d.profile(False)
         k_ms, k_launches, k_flops, k_frames = k_ms + a, k_launches + b_, k_flops + c, k_frames + e
+    # the same kernel with the chip to itself (outside the timed region): one lane, 3 det-batches.
+    # Under concurrent lanes the events above also span co-running kernels of the other lanes.
+    dets[0].profile(True)
+    with torch.cuda.stream(streams[0]):
+        for i in range(3):
+            detect_step(0, i)
+    streams[0].synchronize()
+    s_ms, s_launches, s_flops, _ = dets[0].profile(False)
     dets = dets_n
     tot = torch.tensor([faces, dets, k_frames], dtype=torch.float64, device=dev)
     el = torch.tensor([elapsed], dtype=torch.float64, device=dev)
@@ -231,6 +239,8 @@ def main():
         flops_per_launch = k_flops / max(1, k_launches)
         achieved = flops_per_launch / (avg_ms / 1e3) / 1e12 if avg_ms > 0 else 0.0
         traffic = None
+        s_avg = s_ms / max(1, s_launches)
+        s_ach = s_flops / max(1, s_launches) / (s_avg / 1e3) / 1e12 if s_avg > 0 else 0.0
         tf = os.path.join(ROOT, 'profiles', ('yolo' if yolo else 'pnet') + '_traffic.json')
         if os.path.exists(tf):
             traffic = json.load(open(tf)).get('hbm_bytes_per_launch')
@@ -271,7 +281,9 @@ def main():
                          'achieved': round(achieved, 3), 'peak': peak, 'unit': 'TFLOP/s',
                          'frac': round(achieved / peak, 4), 'traffic': traffic,
                          'avg_launch_ms': round(avg_ms, 4), 'flops_per_launch': flops_per_launch,
-                         'launches': k_launches, 'concurrent_lanes': L},
+                         'launches': k_launches, 'concurrent_lanes': L,
+                         'solo': {'avg_launch_ms': round(s_avg, 4), 'achieved': round(s_ach, 3),
+                                  'frac': round(s_ach / peak, 4), 'launches': s_launches}},
             # north-star's "memory-bound HBM roofline on the detector conv path": the layer-by-layer
             # PNet bytes of SURVEY.md §8d (2,075 MB fp32 per 720p frame at 38.66 GFLOP, AI 18.6) over
             # the same launch time -- an equivalent rate (the fused kernel moves `traffic` bytes)
@@ -280,7 +292,9 @@ def main():
                 'achieved': round(flops_per_launch * LBL_BYTES_PER_FLOP / (avg_ms / 1e3) / 1e9, 1) if avg_ms > 0 else 0.0,
                 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
                 'frac': round(flops_per_launch * LBL_BYTES_PER_FLOP / (avg_ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4)
-                if avg_ms > 0 else 0.0},
+                if avg_ms > 0 else 0.0,
+                'solo_frac': round(s_flops / max(1, s_launches) * LBL_BYTES_PER_FLOP / (s_avg / 1e3) / 1e9
+                                   / HBM_PEAK_GBS, 4) if s_avg > 0 else 0.0},
             'cpu_baseline': None,
         }
         if world == 1 and not args.no_cpu_baseline:
