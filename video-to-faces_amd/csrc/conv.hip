@@ -150,7 +150,10 @@ template <typename T, int BM, int BN, int BK, bool SPLIT, bool X = false>
 __global__ __launch_bounds__(256) void k_conv(ConvParams p) {
     using vec = typename VecT<T>::type;
     constexpr int V = VecT<T>::V;
-    constexpr int PAD = V;
+    // row pads chosen for conflict-free ds_read_b128 fragment reads (16-lane groups
+    // {0-3,12-15,20-27}, ...; bank = dword mod 64): a 144-B bf16 row / 80-B split row put two
+    // lanes of a group on one bank (2 LDS cycles per read), 160 B / 96 B do not
+    constexpr int PAD = sizeof(T) == 2 ? 16 : V;
     constexpr int LDA = BK + PAD;
     constexpr int KV = BK / V;                // vectors per tile row
     constexpr int RA = BM * KV / 256;         // A vectors per thread
@@ -158,8 +161,8 @@ __global__ __launch_bounds__(256) void k_conv(ConvParams p) {
     static_assert(RA >= 1 && RB >= 1 && (256 % KV) == 0, "tile config");
     static_assert(!X || (sizeof(T) == 4 && BK == 32), "split-fp16 mode: fp32 operands, one 32-deep step");
     constexpr int WM = BM / 2, WN = BN / 2, FM = WM / 16, FN = WN / 16;
-    // X: fp16 split planes [2][rows][LDH] (row stride 80 B keeps 16-B fragment reads aligned)
-    constexpr int LDH = BK + 8;
+    // X: fp16 split planes [2][rows][LDH] (row stride 96 B: 16-B aligned, conflict-free reads)
+    constexpr int LDH = BK + 16;
     constexpr int A_BYTES = X ? 2 * BM * LDH * 2 : BM * LDA * (int)sizeof(T);
     constexpr int B_BYTES = X ? 2 * BN * LDH * 2 : BN * LDA * (int)sizeof(T);
     // the operand tiles, reused after the K loop as the fp32 output tile of the staged epilogue
