@@ -62,7 +62,8 @@ __global__ __launch_bounds__(256) void k_layernorm(const float* __restrict__ x, 
 // qkv [N,65,3D] (q | k | v, head-major inside each) -> out [N,65,D]; one workgroup per (n, head)
 __global__ __launch_bounds__(256) void k_vit_attention(const float* __restrict__ qkv, int64_t N, int D, int heads,
                                                        float* __restrict__ out) {
-    __shared__ float Q[VT * (VHD + 1)], K[VT * (VHD + 1)], V[VT * VHD], S[VT * 68];
+    __shared__ __attribute__((aligned(16))) float V[VT * VHD];  // 16-B rows: float4 reads in P V
+    __shared__ float Q[VT * (VHD + 1)], K[VT * (VHD + 1)], S[VT * 68];
     const int64_t n = blockIdx.x / heads;
     const int h = blockIdx.x % heads;
     const int tid = threadIdx.x;
@@ -75,13 +76,32 @@ __global__ __launch_bounds__(256) void k_vit_attention(const float* __restrict__
         V[t * VHD + d] = row[2 * D];
     }
     __syncthreads();
-    // scores = q k^T / sqrt(64)  (vit.py:24; division by 8 is exact as * 0.125)
-    for (int i = tid; i < VT * VT; i += 256) {
-        int a = i / VT, c = i % VT;
-        float s = 0.f;
-#pragma unroll 16
-        for (int d = 0; d < VHD; d++) s = fmaf(Q[a * (VHD + 1) + d], K[c * (VHD + 1) + d], s);
-        S[a * 68 + c] = s * 0.125f;
+    // scores = q k^T / sqrt(64)  (vit.py:24; division by 8 is exact as * 0.125).  65 = 13 x 5:
+    // each of 169 threads keeps a 5 x 5 block of scores in registers (10 LDS reads per 25 FMAs
+    // instead of 2 per FMA); every score still accumulates d = 0..63 in order (same bits)
+    if (tid < 169) {
+        const int a0 = 5 * (tid / 13), c0 = 5 * (tid % 13);
+        float acc[5][5];
+#pragma unroll
+        for (int i = 0; i < 5; i++)
+#pragma unroll
+            for (int j = 0; j < 5; j++) acc[i][j] = 0.f;
+#pragma unroll 4
+        for (int d = 0; d < VHD; d++) {
+            float q[5], k[5];
+#pragma unroll
+            for (int i = 0; i < 5; i++) q[i] = Q[(a0 + i) * (VHD + 1) + d];
+#pragma unroll
+            for (int j = 0; j < 5; j++) k[j] = K[(c0 + j) * (VHD + 1) + d];
+#pragma unroll
+            for (int i = 0; i < 5; i++)
+#pragma unroll
+                for (int j = 0; j < 5; j++) acc[i][j] = fmaf(q[i], k[j], acc[i][j]);
+        }
+#pragma unroll
+        for (int i = 0; i < 5; i++)
+#pragma unroll
+            for (int j = 0; j < 5; j++) S[(a0 + i) * 68 + c0 + j] = acc[i][j] * 0.125f;
     }
     __syncthreads();
     // row softmax: one wave per row (65 entries -> lanes 0..63 + lane 0 takes the 65th)
@@ -99,14 +119,31 @@ __global__ __launch_bounds__(256) void k_vit_attention(const float* __restrict__
         if (lane == 0) S[a * 68 + 64] = e1 * inv;
     }
     __syncthreads();
-    // out = scores @ v, written back head-major: [N,65,D] feature h*64 + d
+    // out = scores @ v, written back head-major: [N,65,D] feature h*64 + d.  208 threads, each a
+    // 5-row x 4-feature block (S broadcast reads, one 16-B V read per c); c = 0..64 in order
     float* ob = out + n * VT * D + h * VHD;
-    for (int i = tid; i < VT * VHD; i += 256) {
-        int a = i / VHD, d = i % VHD;
-        float s = 0.f;
-#pragma unroll 13
-        for (int c = 0; c < VT; c++) s = fmaf(S[a * 68 + c], V[c * VHD + d], s);
-        ob[(int64_t)a * D + d] = s;
+    if (tid < 208) {
+        const int a0 = 5 * (tid / 16), d0 = 4 * (tid % 16);
+        float acc[5][4];
+#pragma unroll
+        for (int i = 0; i < 5; i++)
+#pragma unroll
+            for (int j = 0; j < 4; j++) acc[i][j] = 0.f;
+#pragma unroll 5
+        for (int c = 0; c < VT; c++) {
+            const float4 v = *(const float4*)(V + c * VHD + d0);
+#pragma unroll
+            for (int i = 0; i < 5; i++) {
+                const float sc = S[(a0 + i) * 68 + c];
+                acc[i][0] = fmaf(sc, v.x, acc[i][0]);
+                acc[i][1] = fmaf(sc, v.y, acc[i][1]);
+                acc[i][2] = fmaf(sc, v.z, acc[i][2]);
+                acc[i][3] = fmaf(sc, v.w, acc[i][3]);
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < 5; i++)
+            *(float4*)(ob + (int64_t)(a0 + i) * D + d0) = make_float4(acc[i][0], acc[i][1], acc[i][2], acc[i][3]);
     }
 }
 
