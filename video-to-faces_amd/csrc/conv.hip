@@ -150,10 +150,12 @@ template <typename T, int BM, int BN, int BK, bool SPLIT, bool X = false>
 __global__ __launch_bounds__(256) void k_conv(ConvParams p) {
     using vec = typename VecT<T>::type;
     constexpr int V = VecT<T>::V;
-    // row pads chosen for conflict-free ds_read_b128 fragment reads (16-lane groups
-    // {0-3,12-15,20-27}, ...; bank = dword mod 64): a 144-B bf16 row / 80-B split row put two
-    // lanes of a group on one bank (2 LDS cycles per read), 160 B / 96 B do not
-    constexpr int PAD = sizeof(T) == 2 ? 16 : V;
+    // row pads chosen for conflict-free fragment reads.  ds_read_b128 (bf16, split) serves
+    // 16-lane groups {0-3,12-15,20-27}, ... with bank = dword mod 64: a 144-B bf16 row / 80-B
+    // split row put two lanes of a group on one bank (2 LDS cycles per read), 160 B / 96 B do
+    // not.  ds_read_b32 (fp32: rows lane&15, k = lane>>4) serves lanes 0-31 with bank = dword
+    // mod 32: a 36-float row maps rows r and r+8 to one bank, a 34-float row (2r + k) does not
+    constexpr int PAD = sizeof(T) == 2 ? 16 : 2;
     constexpr int LDA = BK + PAD;
     constexpr int KV = BK / V;                // vectors per tile row
     constexpr int RA = BM * KV / 256;         // A vectors per thread
@@ -252,16 +254,20 @@ __global__ __launch_bounds__(256) void k_conv(ConvParams p) {
 #pragma unroll
             for (int r = 0; r < RB; r++) put(Bs_raw, BN, (tid + 256 * r) / KV, rb[r]);
         } else {
+            // fp32 rows of 34 floats are 8-B aligned only: two 8-byte stores per vector
+            auto st = [&](T* dst, const vec& v) {
+                if constexpr (LDA % V == 0) {
+                    *(vec*)dst = v;
+                } else {
+                    typedef __attribute__((ext_vector_type(2))) float f32x2;
+                    *(f32x2*)dst = f32x2{to_f(v[0]), to_f(v[1])};
+                    *(f32x2*)(dst + 2) = f32x2{to_f(v[2]), to_f(v[3])};
+                }
+            };
 #pragma unroll
-            for (int r = 0; r < RA; r++) {
-                int row = (tid + 256 * r) / KV;
-                *(vec*)(As + row * LDA + kv * V) = ra[r];
-            }
+            for (int r = 0; r < RA; r++) st(As + ((tid + 256 * r) / KV) * LDA + kv * V, ra[r]);
 #pragma unroll
-            for (int r = 0; r < RB; r++) {
-                int row = (tid + 256 * r) / KV;
-                *(vec*)(Bs + row * LDA + kv * V) = rb[r];
-            }
+            for (int r = 0; r < RB; r++) st(Bs + ((tid + 256 * r) / KV) * LDA + kv * V, rb[r]);
         }
     };
     auto advance = [&]() {
