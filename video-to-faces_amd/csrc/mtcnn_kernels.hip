@@ -1063,7 +1063,8 @@ void launch_pnet(bool dense, const uint8_t* frames, int64_t frame_stride, int64_
 // workgroup.  The S x S crop is adaptive-pooled from the uint8 frame straight into LDS
 // (bit-exact bins), conv1 runs on fp32 MFMA with the true K = 27 (im2col order (c, ky, kx),
 // no channel padding), and the pool reads the conv1 band from LDS: only the pooled
-// [n, P, P, 32] map reaches HBM (P = 11 / 23).  Conv rows are produced in bands of 2*PB+1.
+// [n, P, P, 32] map reaches HBM (P = 11 / 23).  Conv rows are produced 2*PB per band into a
+// ring of 2*PB+1 rows (the pool window's shared row is kept, not recomputed).
 // w1: [28][32] (k, co; row 27 and channels >= Cout zero); b1, a1: [32].
 template <int S, int PB, int NT>
 __global__ __launch_bounds__(NT) void k_cand_front(const int4* __restrict__ sat, int H, int W,
@@ -1128,14 +1129,17 @@ __global__ __launch_bounds__(NT) void k_cand_front(const int4* __restrict__ sat,
     }
     const float bb0 = b1[lr], bb1 = b1[16 + lr], aa0 = a1[lr], aa1 = a1[16 + lr];
     __syncthreads();
+    // conv rows live in a ring of BR rows (slot = row % BR): a band's first row (2*pr0) is the
+    // previous band's last, so each band computes only its 2*PB new rows
     for (int pr0 = 0; pr0 < P; pr0 += PB) {
         const int cr0 = 2 * pr0;
-        const int ncr = min(BR, O - cr0);
-        const int npos = ncr * O;
-        const int nf = (npos + 15) / 16;
+        const int r_lo = pr0 == 0 ? 0 : cr0 + 1;
+        const int r_hi = min(cr0 + 2 * PB, O - 1);
+        const int npos = (r_hi - r_lo + 1) * O;
+        const int nf = npos > 0 ? (npos + 15) / 16 : 0;
         for (int f = wave; f < nf; f += NW) {
             const int p = min(f * 16 + lr, npos - 1);
-            const int y = cr0 + p / O, x = p % O;
+            const int y = r_lo + p / O, x = p % O;
             f32x4 c0 = {0.f, 0.f, 0.f, 0.f}, c1 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
             for (int s = 0; s < 7; s++) {
@@ -1150,8 +1154,10 @@ __global__ __launch_bounds__(NT) void k_cand_front(const int4* __restrict__ sat,
             for (int i = 0; i < 4; i++) {
                 const int q = f * 16 + 4 * lk + i;
                 if (q < npos) {
-                    cv[lr * BR * O + q] = prelu(c0[i] + bb0, aa0);
-                    cv[(16 + lr) * BR * O + q] = prelu(c1[i] + bb1, aa1);
+                    const int yq = r_lo + q / O;
+                    const int slot = (yq % BR) * O + (q - (yq - r_lo) * O);
+                    cv[lr * BR * O + slot] = prelu(c0[i] + bb0, aa0);
+                    cv[(16 + lr) * BR * O + slot] = prelu(c1[i] + bb1, aa1);
                 }
             }
         }
@@ -1167,7 +1173,7 @@ __global__ __launch_bounds__(NT) void k_cand_front(const int4* __restrict__ sat,
                 for (int dx = 0; dx < 3; dx++) {
                     const int xx = 2 * px + dx;
                     if (xx >= O) break;
-                    m = fmaxf(m, cv[c * BR * O + (yy - cr0) * O + xx]);
+                    m = fmaxf(m, cv[c * BR * O + (yy % BR) * O + xx]);
                 }
             }
             o[((pr0 + pyl) * P + px) * 32 + c] = m;
