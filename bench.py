@@ -34,7 +34,8 @@ BF16_PEAK_TFLOPS = 2500.0  # MI355X dense bf16 MFMA (no sparsity), MI355X_MICROA
 F16X_PEAK_TFLOPS = round(BF16_PEAK_TFLOPS / 3, 1)
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E (MI355X_MICROARCH.md)
 LBL_BYTES_PER_FLOP = 2075e6 / 38.66e9  # PNet layer-by-layer fp32 bytes per FLOP
-H, W = 720, 1280
+H, W = 720, 1280  # --frame 1080p: 1080, 1920
+ENC_NAMES = {'facenet': 'FaceNet', 'vit_b': 'ViT-B/16', 'vit_l': 'ViT-L/16'}
 
 
 def parse():
@@ -58,7 +59,13 @@ def parse():
     ap.add_argument('--det-min-score', type=float, default=0.4)
     ap.add_argument('--det-min-size', type=int, default=None, help='default 0 (mtcnn) / 50 (yolo)')
     ap.add_argument('--det-min-border', type=int, default=5)
+    ap.add_argument('--enc-model', default='facenet', choices=['facenet', 'vit_b', 'vit_l'],
+                    help='vit_*: ViT-B/L-16 encoder (BASELINE config 5 pairs YOLO with ViT-L); '
+                         'its GEMMs run split-fp16 unless --enc-precision fp32')
+    ap.add_argument('--frame', default='720p', choices=['720p', '1080p'])
     a = ap.parse_args()
+    global H, W
+    H, W = (1080, 1920) if a.frame == '1080p' else (720, 1280)
     yolo = a.det_model == 'yolo'
     if a.det_batch is None:
         a.det_batch = 32 if yolo else 16
@@ -80,6 +87,7 @@ def cpu_baseline(frames, args):
     from oracle import mtcnn as om
     from oracle import yolo as oy
     from oracle.facenet import inception_resnet_v1, resize_linear_u8
+    from oracle.vit import vit
     from videotofaces import synth
     from videotofaces.detection import boxes_to_crops
     cores = len(os.sched_getaffinity(0))
@@ -88,7 +96,8 @@ def cpu_baseline(frames, args):
         cores = min(cores, int(env))
     torch.set_num_threads(cores)
     yolo = args.det_model == 'yolo'
-    pm, pf = synth.make_params(args.det_model), synth.make_params('facenet')
+    pm, pf = synth.make_params(args.det_model), synth.make_params(args.enc_model)
+    vit_dims = {'vit_b': (768, 12), 'vit_l': (1024, 24)}.get(args.enc_model)
     n = min(args.cpu_frames, frames.shape[0])
     sample = frames[:n]
     t0 = time.time()
@@ -101,14 +110,22 @@ def cpu_baseline(frames, args):
     for i in range(0, crops.shape[0], args.enc_batch):
         blobs = []
         for f, x1, y1, x2, y2 in crops[i:i + args.enc_batch]:
-            r = resize_linear_u8(sample[f, y1:y2, x1:x2], 160)[:, :, ::-1].transpose(2, 0, 1)
-            blobs.append((torch.from_numpy(np.ascontiguousarray(r)).float() - 127.5) * (1 / 128))
-        inception_resnet_v1(pf, torch.stack(blobs))
+            if vit_dims:  # blobFromImages(1/127.5, 128x128, 127.5, swapRB) (vit.py:141)
+                r = resize_linear_u8(sample[f, y1:y2, x1:x2], 128)[:, :, ::-1].transpose(2, 0, 1)
+                blobs.append((torch.from_numpy(np.ascontiguousarray(r)).float() - 127.5) * (1 / 127.5))
+            else:
+                r = resize_linear_u8(sample[f, y1:y2, x1:x2], 160)[:, :, ::-1].transpose(2, 0, 1)
+                blobs.append((torch.from_numpy(np.ascontiguousarray(r)).float() - 127.5) * (1 / 128))
+        if vit_dims:
+            vit(pf, torch.stack(blobs), *vit_dims)
+        else:
+            inception_resnet_v1(pf, torch.stack(blobs))
         faces += len(blobs)
     dt = time.time() - t0
     return {'value': round(faces / dt, 3), 'unit': 'faces/s', 'cores': cores, 'kind': 'port',
-            'sample': '%d synthetic 720p frames (%d faces), oracle %s+FaceNet fp32 on CPU, %.1f s'
-                      % (n, faces, 'YOLOv3' if yolo else 'MTCNN(min_face_size=%g)' % args.min_face_size, dt)}
+            'sample': '%d synthetic %s frames (%d faces), oracle %s+%s fp32 on CPU, %.1f s'
+                      % (n, args.frame, faces, 'YOLOv3' if yolo else 'MTCNN(min_face_size=%g)' % args.min_face_size,
+                         ENC_NAMES[args.enc_model], dt)}
 
 
 def main():
@@ -138,7 +155,15 @@ def main():
     # independent, so per-batch results are exactly the single-lane results.
     L = max(1, args.lanes)
     dets = [YOLOv3(dev, precision=args.det_precision) if yolo else MTCNN(dev) for _ in range(L)]
-    encs = [InceptionResnetV1(dev, precision=args.enc_precision) for _ in range(L)]
+    if args.enc_model == 'facenet':
+        encs = [InceptionResnetV1(dev, precision=args.enc_precision) for _ in range(L)]
+        D = 512
+    else:
+        from videotofaces.encoders.vit import ViT
+        vp = synth.make_params(args.enc_model)
+        encs = [ViT(dev, vp, isL=args.enc_model == 'vit_l',
+                    precision='fp32' if args.enc_precision == 'fp32' else 'f16x') for _ in range(L)]
+        D = encs[0].dim
     streams = [torch.cuda.Stream(dev) for _ in range(L)]
     torch.cuda.synchronize(dev)
 
@@ -185,7 +210,7 @@ def main():
             s.synchronize()
         # lane streams -> global (step, face) order
         parts, offs = [], [0] * L
-        flat = [torch.cat(e) if e else torch.zeros((0, 512), device=dev) for e in lane_embs]
+        flat = [torch.cat(e) if e else torch.zeros((0, D), device=dev) for e in lane_embs]
         for k in range(n):
             lane, nf = k % L, stats[k][0]
             parts.append(flat[lane][offs[lane]:offs[lane] + nf])
@@ -203,7 +228,7 @@ def main():
     stats, embs = run(args.warmup, args.steps)
     faces = sum(s_[0] for s_ in stats)
     dets_n = sum(s_[1] for s_ in stats)
-    local_emb = torch.cat(embs) if embs else torch.zeros((0, 512), device=dev)
+    local_emb = torch.cat(embs) if embs else torch.zeros((0, D), device=dev)
     if world > 1:
         from videotofaces.parallel import all_gather_rows
         gathered = all_gather_rows(local_emb)
@@ -247,14 +272,14 @@ def main():
         if yolo:
             peak = BF16_PEAK_TFLOPS if args.det_precision == 'bf16' else FP32_PEAK_TFLOPS
             kname = 'k_conv (YOLOv3 Darknet53+neck+head, 75 implicit-GEMM launches per det-batch, %s)' % args.det_precision
-            wl = 'YOLOv3(%s)+FaceNet' % args.det_precision
+            wl = 'YOLOv3(%s)+%s' % (args.det_precision, ENC_NAMES[args.enc_model])
         else:
             peak = F16X_PEAK_TFLOPS
             kname = ('k_pnet (fused pyramid resample + PNet; convs on fp16 matrix cores with split operands, '
                      'fp32-grade; peak = fp16 dense / 3 products)')
-            wl = 'MTCNN(min_face_size=%g)+FaceNet' % args.min_face_size
+            wl = 'MTCNN(min_face_size=%g)+%s' % (args.min_face_size, ENC_NAMES[args.enc_model])
         out = {
-            'metric': 'faces/sec end-to-end (detect+encode) on 1280x720 synthetic frames',
+            'metric': 'faces/sec end-to-end (detect+encode) on %dx%d synthetic frames' % (W, H),
             'value': round(faces_all / elapsed, 2),
             'unit': 'faces/s',
             'n_gpus': world,
@@ -264,12 +289,14 @@ def main():
             'higher_is_better': True,
             'scaling': 'weak',
             'vs_baseline': None,
-            'dtype': '%s det / %s enc' % (args.det_precision if yolo else 'fp32 (split-fp16 MFMA)', args.enc_precision),
-            'data': 'synthetic (seeded 720p value-noise frames with face blobs; hash-seeded synthetic weights, '
-                    'detector heads calibrated to a few faces/frame)',
-            'config': {'workload': '%s, det-batch %d, enc-batch %d, 720p, frames in HBM, '
+            'dtype': '%s det / %s enc' % (args.det_precision if yolo else 'fp32 (split-fp16 MFMA)',
+                                          args.enc_precision if args.enc_model == 'facenet' or args.enc_precision == 'fp32'
+                                          else 'fp32 (split-fp16 MFMA)'),
+            'data': 'synthetic (seeded %s value-noise frames with face blobs; hash-seeded synthetic weights, '
+                    'detector heads calibrated to a few faces/frame)' % args.frame,
+            'config': {'workload': '%s, det-batch %d, enc-batch %d, %s, frames in HBM, '
                                    'box filter min_score %g min_size %d min_border %d, det_scale (1.5,1.5,2.2,1.2), square'
-                                   % (wl, B, args.enc_batch, args.det_min_score, args.det_min_size,
+                                   % (wl, B, args.enc_batch, args.frame, args.det_min_score, args.det_min_size,
                                       args.det_min_border),
                        'det_batch': B, 'enc_batch': args.enc_batch, 'frames_per_step_per_gpu': B,
                        'lanes': L,
