@@ -31,32 +31,55 @@ __global__ void k_vit_tokens(const float* __restrict__ patches, const float* __r
     x[i] = v + pos[t * D + d];
 }
 
-// LayerNorm over the last dim (eps), rows of length D with row stride `ld`; one workgroup per row.
+// LayerNorm over the last dim (eps), rows of length D (D % 256 == 0, D <= 1024) with row stride
+// `ld`: one wave per row, 4 rows per workgroup; the row is read once into registers (16-B
+// loads), mean and variance are wave reductions over it, then the normalised row is written
+constexpr int LN_ROWS = 4;
+constexpr int LN_MAXV = 4;  // float4 per lane: D <= 1024
 __global__ __launch_bounds__(256) void k_layernorm(const float* __restrict__ x, int64_t rows, int D, int64_t ld,
                                                    const float* __restrict__ g, const float* __restrict__ b, float eps,
                                                    float* __restrict__ y, int64_t ldy) {
-    const int64_t r = blockIdx.x;
-    const float* xr = x + r * ld;
-    __shared__ float red[8];
+    const int lane = threadIdx.x & 63;
+    const int64_t r = (int64_t)blockIdx.x * LN_ROWS + (threadIdx.x >> 6);
+    if (r >= rows) return;
+    const int nv = D / 256;  // float4 per lane
+    const float4* xr = (const float4*)(x + r * ld);
+    float4 v[LN_MAXV];
     float s = 0.f;
-    for (int d = threadIdx.x; d < D; d += 256) s += xr[d];
+#pragma unroll
+    for (int j = 0; j < LN_MAXV; j++)
+        if (j < nv) {
+            v[j] = xr[lane + 64 * j];
+            s += (v[j].x + v[j].y) + (v[j].z + v[j].w);
+        }
     for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off);
-    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
-    __syncthreads();
-    const float mean = (red[0] + red[1] + red[2] + red[3]) / (float)D;
-    __syncthreads();
+    const float mean = s / (float)D;
     float q = 0.f;
-    for (int d = threadIdx.x; d < D; d += 256) {
-        float t = xr[d] - mean;
-        q = fmaf(t, t, q);
-    }
+#pragma unroll
+    for (int j = 0; j < LN_MAXV; j++)
+        if (j < nv) {
+            v[j].x -= mean;
+            v[j].y -= mean;
+            v[j].z -= mean;
+            v[j].w -= mean;
+            q = fmaf(v[j].x, v[j].x, q);
+            q = fmaf(v[j].y, v[j].y, q);
+            q = fmaf(v[j].z, v[j].z, q);
+            q = fmaf(v[j].w, v[j].w, q);
+        }
     for (int off = 32; off > 0; off >>= 1) q += __shfl_xor(q, off);
-    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = q;
-    __syncthreads();
-    const float var = (red[0] + red[1] + red[2] + red[3]) / (float)D;
-    const float rstd = 1.0f / sqrtf(var + eps);
-    float* yr = y + r * ldy;
-    for (int d = threadIdx.x; d < D; d += 256) yr[d] = fmaf((xr[d] - mean) * rstd, g[d], b[d]);
+    const float rstd = 1.0f / sqrtf(q / (float)D + eps);
+    float4* yr = (float4*)(y + r * ldy);
+    const float4* g4 = (const float4*)g;
+    const float4* b4 = (const float4*)b;
+#pragma unroll
+    for (int j = 0; j < LN_MAXV; j++)
+        if (j < nv) {
+            const int c = lane + 64 * j;
+            const float4 gg = g4[c], bb = b4[c];
+            yr[c] = make_float4(fmaf(v[j].x * rstd, gg.x, bb.x), fmaf(v[j].y * rstd, gg.y, bb.y),
+                                fmaf(v[j].z * rstd, gg.z, bb.z), fmaf(v[j].w * rstd, gg.w, bb.w));
+        }
 }
 
 // qkv [N,65,3D] (q | k | v, head-major inside each) -> out [N,65,D]; one workgroup per (n, head)
@@ -283,18 +306,18 @@ static void vit_forward(Vit& V, const float* x_nhwc8, int64_t N, float* emb) {
     launch_conv(p, false, V.st);
     k_vit_tokens<<<cdiv(M * D, 256), 256, 0, V.st>>>(patches, V.cls, V.pos, N, D, X);
     for (const auto& B : V.blocks) {
-        k_layernorm<<<(unsigned)M, 256, 0, V.st>>>(X, M, D, D, B.n1w, B.n1b, 1e-12f, Hn, D);
+        k_layernorm<<<(unsigned)cdiv(M, LN_ROWS), 256, 0, V.st>>>(X, M, D, D, B.n1w, B.n1b, 1e-12f, Hn, D);
         linear(V, B.qkv, Hn, M, QKV, nullptr, false);
         k_vit_attention<<<(unsigned)(N * V.heads), 256, 0, V.st>>>(QKV, N, D, V.heads, A);
         linear(V, B.proj, A, M, Hn, X, false);  // x + proj(attn)
         std::swap(X, Hn);
-        k_layernorm<<<(unsigned)M, 256, 0, V.st>>>(X, M, D, D, B.n2w, B.n2b, 1e-12f, A, D);
+        k_layernorm<<<(unsigned)cdiv(M, LN_ROWS), 256, 0, V.st>>>(X, M, D, D, B.n2w, B.n2b, 1e-12f, A, D);
         linear(V, B.fc1, A, M, F, nullptr, true);
         linear(V, B.fc2, F, M, Hn, X, false);   // x + fc2(gelu(fc1(...)))
         std::swap(X, Hn);
     }
     // LayerNorm of the CLS rows (vit.py:100-101)
-    k_layernorm<<<(unsigned)N, 256, 0, V.st>>>(X, N, D, (int64_t)VT * D, V.nw, V.nb, 1e-12f, emb, D);
+    k_layernorm<<<(unsigned)cdiv(N, LN_ROWS), 256, 0, V.st>>>(X, N, D, (int64_t)VT * D, V.nw, V.nb, 1e-12f, emb, D);
 }
 
 // forward in the handle's operand mode; guarded split-fp16: an operand >= 2^14 (or NaN) anywhere
@@ -333,7 +356,9 @@ extern "C" {
 
 int vtf_vit_create(const float* params, int64_t n_params, int dim, int depth, int device, vtf_vit_t* out) {
     return guarded([&] {
-        VTF_CHECK(params && out && dim % 64 == 0 && depth > 0, VTF_E_ARG, "bad argument");
+        // dim: 64-wide heads, and k_layernorm's float4-per-lane rows (dim % 256 == 0, <= 1024)
+        VTF_CHECK(params && out && dim % 256 == 0 && dim <= 256 * LN_MAXV && depth > 0, VTF_E_ARG,
+                  "bad argument (dim must be a multiple of 256, at most 1024)");
         VTF_HIP(hipSetDevice(device));
         auto* h = new vtf_vit_s();
         h->v.device = device;
