@@ -91,12 +91,17 @@ __global__ __launch_bounds__(256) void k_vit_attention(const float* __restrict__
     const int h = blockIdx.x % heads;
     const int tid = threadIdx.x;
     const float* base = qkv + n * VT * 3 * D + h * VHD;
-    for (int i = tid; i < VT * VHD; i += 256) {
-        int t = i / VHD, d = i % VHD;
+    // 16-B loads (16 per 64-wide head row); Q/K rows are padded to 65 floats in LDS, so their
+    // four lanes are stored one by one
+    for (int i = tid; i < VT * VHD / 4; i += 256) {
+        const int t = i / (VHD / 4), d = 4 * (i % (VHD / 4));
         const float* row = base + (int64_t)t * 3 * D + d;
-        Q[t * (VHD + 1) + d] = row[0];
-        K[t * (VHD + 1) + d] = row[D];
-        V[t * VHD + d] = row[2 * D];
+        const float4 q = *(const float4*)row, k = *(const float4*)(row + D), v = *(const float4*)(row + 2 * D);
+        float* qd = Q + t * (VHD + 1) + d;
+        float* kd = K + t * (VHD + 1) + d;
+        qd[0] = q.x, qd[1] = q.y, qd[2] = q.z, qd[3] = q.w;
+        kd[0] = k.x, kd[1] = k.y, kd[2] = k.z, kd[3] = k.w;
+        *(float4*)(V + t * VHD + d) = v;
     }
     __syncthreads();
     // scores = q k^T / sqrt(64)  (vit.py:24; division by 8 is exact as * 0.125).  65 = 13 x 5:
