@@ -36,6 +36,17 @@ typedef struct vtf_yolo_s* vtf_yolo_t;
 typedef struct vtf_group_s* vtf_group_t;
 typedef struct vtf_rcnn_s* vtf_rcnn_t;
 
+/* Box post-processing parameters (video_to_faces det_min_score, det_min_size, det_min_border,
+ * det_scale, det_square; main.py:50-51), see vtf_boxes_to_crops. */
+typedef struct vtf_box_params {
+    float min_score;   /* compared in fp32 (numpy float32 vs Python float, NEP 50) */
+    double min_size;   /* width or height below -> rejected */
+    double min_border; /* 0 = no border check */
+    double scale[4];   /* sx1, sx2, sy1, sy2 */
+    int32_t square;
+    int32_t adjust;    /* 1: adjust_boxes after filter_boxes (the pipeline); 0: filter_boxes only */
+} vtf_box_params;
+
 /* ---------------------------------------------------------------- MTCNN detector
  * Replaces RealMTCNN / MTCNN.forward (src/videotofaces/detectors/mtcnn.py:167-252,
  * 312-326), called by detection.py:131 `detout = model(frames)`.
@@ -55,6 +66,14 @@ int vtf_mtcnn_detect(vtf_mtcnn_t h, const uint8_t* frames, int frames_on_device,
                      int64_t frame_stride, int64_t row_stride, double min_face_size,
                      float* out_boxes, float* out_landmarks, int32_t* out_counts, int64_t cap,
                      int64_t* out_total);
+
+/* detect + box post-processing with nothing on the host but the counts: the detector's rows
+ * stay in HBM and go through vtf_boxes_to_crops (detection.py:131-145).  frames as above;
+ * d_crops / out_frame_counts / cap / out_n as in vtf_boxes_to_crops. */
+int vtf_mtcnn_detect_crops(vtf_mtcnn_t h, const uint8_t* frames, int frames_on_device, int B, int H, int W,
+                           int64_t frame_stride, int64_t row_stride, double min_face_size,
+                           const vtf_box_params* params, int32_t frame_offset, int32_t* d_crops,
+                           int32_t* out_frame_counts, int64_t cap, int64_t* out_n);
 
 /* Per-stage counters of the last detect call: [0] levels, [1] stage-1 candidates (all
  * levels), [2] after per-level NMS, [3] after cross-level NMS (= stage-2 proposals),
@@ -81,6 +100,22 @@ int vtf_mtcnn_resample(vtf_mtcnn_t h, const uint8_t* d_frames, int B, int H, int
 int vtf_mtcnn_rnet(vtf_mtcnn_t h, const float* d_in, int64_t n, float* d_reg, float* d_prob);
 int vtf_mtcnn_onet(vtf_mtcnn_t h, const float* d_in, int64_t n, float* d_reg, float* d_lm, float* d_prob);
 
+/* ---------------------------------------------------------------- box post-processing
+ * process_frames_batch steps 2-5 (src/videotofaces/detection.py:133-145) on device:
+ * filter_boxes (detection.py:174-217, with check_box 165-171), adjust_boxes (220-262) and the
+ * (frame, face) flatten of get_crops (161-162).  Parameters as video_to_faces passes them
+ * (main.py:50-51): det_min_score, det_min_size, det_min_border, det_scale (sx1, sx2, sy1, sy2),
+ * det_square. */
+
+/* d_rows: device fp32 [n,5] (x1,y1,x2,y2,score) grouped by frame, counts: host int32 [B] rows per
+ * frame (negative = frame absent from the detector output: no crops).  Writes device int32
+ * d_crops [m,5] (frame_offset + frame, x1, y1, x2, y2) in row order, d_src [m] (source row, may be
+ * NULL), host out_frame_counts [B] (may be NULL) and *out_n = m.  VTF_E_CAPACITY when the rows
+ * exceed cap (then *out_n = rows, nothing written). */
+int vtf_boxes_to_crops(const float* d_rows, const int32_t* counts, int B, int H, int W, const vtf_box_params* params,
+                       int32_t frame_offset, int32_t* d_crops, int32_t* d_src, int32_t* out_frame_counts,
+                       int64_t cap, int64_t* out_n, void* hip_stream);
+
 /* ---------------------------------------------------------------- box ops
  * torchvision.ops.batched_nms as called at mtcnn.py:196,205,219 and
  * detectors/operations/post.py:8: d_boxes [n,4] fp32, d_scores [n], d_idxs [n] int64.
@@ -100,13 +135,17 @@ int vtf_facenet_set_stream(vtf_facenet_t h, void* hip_stream);
 int vtf_facenet_forward(vtf_facenet_t h, const float* d_x, int64_t N, float* d_emb);
 /* Crop + resize + normalise faces straight from device frames (blobFromImages(1/128,
  * 160x160, 127.5, swapRB) on each crop, INTER_LINEAR uint8), then encode.
- * d_frames as in vtf_mtcnn_detect; crops: host int32 [N,5] (frame index, x1, y1, x2, y2)
- * in frame pixels (detection.py:161-162 get_crops slices). */
-int vtf_facenet_encode_crops(vtf_facenet_t h, const uint8_t* d_frames, int H, int W, int64_t frame_stride,
-                             int64_t row_stride, const int32_t* crops, int64_t N, float* d_emb);
+ * d_frames: F device frames as in vtf_mtcnn_detect; crops int32 [N,5] (frame index, x1, y1,
+ * x2, y2) in frame pixels (detection.py:161-162 get_crops slices), a host array (validated:
+ * 0 <= frame < F, non-empty slice inside the frame, else VTF_E_ARG) or, with crops_on_device,
+ * a device array such as vtf_*_detect_crops writes (read by the kernel; an invalid rectangle
+ * encodes a zero image instead of reading outside the frames). */
+int vtf_facenet_encode_crops(vtf_facenet_t h, const uint8_t* d_frames, int F, int H, int W, int64_t frame_stride,
+                             int64_t row_stride, const int32_t* crops, int crops_on_device, int64_t N,
+                             float* d_emb);
 /* Blob of uint8 BGR crops (cv2.dnn.blobFromImages, INTER_LINEAR, swapRB): d_out [N,3,S,S].
- * out = (resized_u8 - mean) * scale. */
-int vtf_blob_from_crops(const uint8_t* d_frames, int H, int W, int64_t frame_stride, int64_t row_stride,
+ * out = (resized_u8 - mean) * scale.  d_crops: device int32 [N,5] into F frames. */
+int vtf_blob_from_crops(const uint8_t* d_frames, int F, int H, int W, int64_t frame_stride, int64_t row_stride,
                         const int32_t* d_crops, int64_t N, int S, float mean, float scale, float* d_out,
                         void* hip_stream);
 
@@ -124,8 +163,8 @@ int vtf_vit_set_precision(vtf_vit_t h, int mode);
  * (LayerNorm of the CLS token, not L2-normalised). */
 int vtf_vit_forward(vtf_vit_t h, const float* d_x, int64_t N, float* d_emb);
 /* crops as in vtf_facenet_encode_crops, resized to 128x128 (vit.py:141). */
-int vtf_vit_encode_crops(vtf_vit_t h, const uint8_t* d_frames, int H, int W, int64_t frame_stride,
-                         int64_t row_stride, const int32_t* crops, int64_t N, float* d_emb);
+int vtf_vit_encode_crops(vtf_vit_t h, const uint8_t* d_frames, int F, int H, int W, int64_t frame_stride,
+                         int64_t row_stride, const int32_t* crops, int crops_on_device, int64_t N, float* d_emb);
 
 /* ---------------------------------------------------------------- grouping
  * remove_dupes_overall 'enc' branch (dupes.py:51-68 with sklearn cosine_distances):
@@ -138,10 +177,11 @@ int vtf_cosine_classify(const float* d_X, int64_t N, const float* d_R, int64_t C
 
 /* ---------------------------------------------------------------- hash dedupe
  * dupes.ahash (dupes.py:11-15) of N face crops of device frames (frames as in
- * vtf_mtcnn_detect, crops host int32 [N,5] = frame, x1, y1, x2, y2 as get_crops slices them,
+ * vtf_mtcnn_detect (F frames), crops host int32 [N,5] = frame, x1, y1, x2, y2 as get_crops slices them
+ * (validated as in vtf_facenet_encode_crops),
  * detection.py:161-162): out_hashes host uint64 [N], bit k = 8x8 thumbnail pixel k (row-major)
  * > mean.  cvtColor(BGR2GRAY) + resize INTER_LINEAR restated from OpenCV's fixed point. */
-int vtf_ahash_crops(const uint8_t* d_frames, int H, int W, int64_t frame_stride, int64_t row_stride,
+int vtf_ahash_crops(const uint8_t* d_frames, int F, int H, int W, int64_t frame_stride, int64_t row_stride,
                     const int32_t* crops, int64_t N, uint64_t* out_hashes, void* hip_stream);
 /* remove_dupes_overall('hash') distances (dupes.py:55-64): for row i, min and first argmin over
  * j < i of popcount(h_i ^ h_j); row 0 -> 10000, 0.  d_hashes uint64 [N] -> d_min int32 [N],
@@ -162,6 +202,11 @@ int vtf_yolo_set_stream(vtf_yolo_t h, void* hip_stream);
 int vtf_yolo_detect(vtf_yolo_t h, const uint8_t* frames, int frames_on_device, int B, int H, int W,
                     int64_t frame_stride, int64_t row_stride, float* out_boxes, float* out_scores,
                     int32_t* out_counts, int64_t cap, int64_t* out_total);
+/* detect + box post-processing on device, as vtf_mtcnn_detect_crops. */
+int vtf_yolo_detect_crops(vtf_yolo_t h, const uint8_t* frames, int frames_on_device, int B, int H, int W,
+                          int64_t frame_stride, int64_t row_stride, const vtf_box_params* params,
+                          int32_t frame_offset, int32_t* d_crops, int32_t* out_frame_counts, int64_t cap,
+                          int64_t* out_n);
 /* resize_cv2 keep-ratio size (prep.py:71-73) and the x32 padded net input: {h, w, Hp, Wp}. */
 int vtf_yolo_input_size(int H, int W, int* out4);
 /* Parity entries.  letterbox: preprocess (prep.py:12-92) -> d_out NHWC fp32 [B,Hp,Wp,8]
@@ -196,6 +241,12 @@ int vtf_rcnn_set_stream(vtf_rcnn_t h, void* hip_stream);
 int vtf_rcnn_detect(vtf_rcnn_t h, const uint8_t* frames, int frames_on_device, int B, int H, int W,
                     int64_t frame_stride, int64_t row_stride, float* out_boxes, float* out_scores,
                     int32_t* out_counts, int64_t cap, int64_t* out_total);
+/* detect + box post-processing on device, as vtf_mtcnn_detect_crops (frames past the last
+ * proposal image produce no crops, as the reference's shorter detout list does). */
+int vtf_rcnn_detect_crops(vtf_rcnn_t h, const uint8_t* frames, int frames_on_device, int B, int H, int W,
+                          int64_t frame_stride, int64_t row_stride, const vtf_box_params* params,
+                          int32_t frame_offset, int32_t* d_crops, int32_t* out_frame_counts, int64_t cap,
+                          int64_t* out_n);
 /* resize_cv2 keep-ratio size for resize=(800, 1333) (prep.py:71-74) and the x32 padded net
  * input: {h, w, Hp, Wp}. */
 int vtf_rcnn_input_size(int H, int W, int* out4);

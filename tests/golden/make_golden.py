@@ -435,7 +435,61 @@ def gen_dupes():
     print('dupes', N, 'kept', len(goods))
 
 
+# (H, W), mscore, msize, mborder, scale, square: the API / CLI / bench settings plus frames
+# smaller than the scaled boxes (square overflow, side > other frame dimension, both
+# orientations) and thresholds whose float32 rounding falls below the Python float (0.7)
+BOX_CASES = [
+    ((720, 1280), 0.4, 50, 5, (1.5, 1.5, 2.2, 1.2), True),
+    ((720, 1280), 0.4, 0, 5, (1.5, 1.5, 2.2, 1.2), True),
+    ((1080, 1920), 0.4, 50, 5, (1.5, 1.5, 2.2, 1.2), False),
+    ((60, 100), 0.7, 0, 0, (2.0, 2.0, 3.0, 3.0), True),
+    ((300, 120), 0.1, 3, 2, (1.25, 2.5, 1.75, 1.1), True),
+    ((96, 96), 0.5, 1, 7.5, 2, True),
+    ((200, 640), 0.0, 0, 0, (1, 1, 1, 1), True),
+]
+
+
+def box_rows(rng, H, W, n):
+    """random detector rows (x1,y1,x2,y2,score) f32 over and around a HxW frame, with exact
+    threshold scores, integer-valued corners, zero-size and out-of-frame boxes"""
+    x1 = rng.uniform(-0.2 * W, 1.1 * W, n)
+    y1 = rng.uniform(-0.2 * H, 1.1 * H, n)
+    w = rng.uniform(0, 1.2 * max(H, W), n) * rng.choice([0.05, 0.3, 1.0], n)
+    h = w * rng.uniform(0.3, 3.0, n)
+    r = np.stack([x1, y1, x1 + w, y1 + h, rng.uniform(0, 1, n)], 1).astype(np.float32)
+    k = n // 8
+    r[:k, :4] = np.round(r[:k, :4])
+    r[k:2 * k, 2] = r[k:2 * k, 0]
+    r[2 * k:3 * k, 4] = rng.choice(np.array([0.4, 0.7, 0.5, 0.1, 0.0], np.float32), k)
+    r[3 * k:4 * k, 4] = np.nextafter(rng.choice(np.array([0.4, 0.7], np.float32), k), np.float32(0))
+    return r
+
+
+def gen_boxes():
+    """filter_boxes + adjust_boxes (detection.py:174-262) of the reference on random and
+    edge-case boxes: inputs, and per case the kept (row, x1, y1, x2, y2)."""
+    load_ref()
+    det = importlib.import_module('ref_vtf.detection')
+    rng = np.random.default_rng(23)
+    out = {}
+    save_params = ('', '', None, False, False, False)
+    for ci, (sz, ms, mz, mb, sc, sq) in enumerate(BOX_CASES):
+        rows = box_rows(rng, sz[0], sz[1], 1500)
+        kept = det.filter_boxes(rows, sz, ms, mz, mb, save_params, None, 0)
+        # filter_boxes returns rounded boxes; recover each one's row by its position among the
+        # rows that pass (the reference keeps their order)
+        adj = det.adjust_boxes(kept, sz, sc, sq)
+        out['rows%d' % ci] = rows
+        out['filtered%d' % ci] = np.array([b[:4] for b in kept], np.int64).reshape(-1, 4)
+        out['filtered_score%d' % ci] = np.array([b[4] for b in kept], np.float32)
+        out['adjusted%d' % ci] = np.array([b[:4] for b in adj], np.int64).reshape(-1, 4)
+        print('boxes case', ci, sz, 'kept', len(kept), 'of', len(rows))
+    import json
+    out['cases_json'] = np.array(json.dumps(BOX_CASES))
+    np.savez_compressed(os.path.join(HERE, 'boxes.npz'), **out)
+
+
 if __name__ == '__main__':
-    which = sys.argv[1:] or ['mtcnn', 'facenet', 'vit', 'grouping', 'yolo', 'kmeans', 'rcnn', 'dupes']
+    which = sys.argv[1:] or ['mtcnn', 'facenet', 'vit', 'grouping', 'yolo', 'kmeans', 'rcnn', 'dupes', 'boxes']
     for w in which:
         globals()['gen_' + w]()

@@ -26,7 +26,7 @@ __device__ inline __bf16 cvt_out<__bf16>(float v) { return (__bf16)v; }
 
 // layout 0: NCHW [N,3,S,S]; layout 1: NHWC [N,S,S,Cp] (channels >= 3 zero)
 template <typename T, int LAYOUT>
-__global__ void k_blob(const uint8_t* __restrict__ frames, int H, int W, int64_t fstride, int64_t rstride,
+__global__ void k_blob(const uint8_t* __restrict__ frames, int F, int H, int W, int64_t fstride, int64_t rstride,
                        const int32_t* __restrict__ crops, int64_t N, int S, float mean, float scale, int Cp,
                        T* __restrict__ out) {
     int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -36,13 +36,16 @@ __global__ void k_blob(const uint8_t* __restrict__ frames, int H, int W, int64_t
     int64_t n = i / ((int64_t)S * S);
     const int32_t* c = crops + n * 5;
     int f = c[0], x1 = c[1], y1 = c[2], x2 = c[3], y2 = c[4];
-    // numpy slice semantics of img[y1:y2, x1:x2] for in-frame boxes (adjust_boxes clamps)
+    // numpy slice semantics of img[y1:y2, x1:x2] for in-frame boxes (adjust_boxes clamps); a
+    // frame index outside [0, F) (only possible for device-side crop lists, host lists are
+    // validated) encodes a zero image instead of reading outside the frames
     x1 = max(0, min(x1, W));
     x2 = max(x1, min(x2, W));
     y1 = max(0, min(y1, H));
     y2 = max(y1, min(y2, H));
     int w = x2 - x1, h = y2 - y1;
-    const uint8_t* base = frames + (int64_t)f * fstride + (int64_t)y1 * rstride + (int64_t)x1 * 3;
+    if (f < 0 || f >= F) w = h = 0;
+    const uint8_t* base = frames + (int64_t)(w > 0 && h > 0 ? f : 0) * fstride + (int64_t)y1 * rstride + (int64_t)x1 * 3;
     int v[3];
     if (w <= 0 || h <= 0) {
         v[0] = v[1] = v[2] = 0;
@@ -80,18 +83,18 @@ __global__ void k_blob(const uint8_t* __restrict__ frames, int H, int W, int64_t
         for (int oc = 3; oc < Cp; oc++) out[((n * S + dy) * S + dx) * Cp + oc] = cvt_out<T>(0.f);
 }
 
-void launch_blob(const uint8_t* frames, int H, int W, int64_t fstride, int64_t rstride, const int32_t* d_crops,
+void launch_blob(const uint8_t* frames, int F, int H, int W, int64_t fstride, int64_t rstride, const int32_t* d_crops,
                  int64_t N, int S, float mean, float scale, int layout, int Cp, bool bf16, void* out, hipStream_t st) {
     int64_t tot = N * S * S;
     if (tot <= 0) return;
     if (layout == 0)
-        k_blob<float, 0><<<cdiv(tot, 256), 256, 0, st>>>(frames, H, W, fstride, rstride, d_crops, N, S, mean, scale, 3,
+        k_blob<float, 0><<<cdiv(tot, 256), 256, 0, st>>>(frames, F, H, W, fstride, rstride, d_crops, N, S, mean, scale, 3,
                                                           (float*)out);
     else if (bf16)
-        k_blob<__bf16, 1><<<cdiv(tot, 256), 256, 0, st>>>(frames, H, W, fstride, rstride, d_crops, N, S, mean, scale,
+        k_blob<__bf16, 1><<<cdiv(tot, 256), 256, 0, st>>>(frames, F, H, W, fstride, rstride, d_crops, N, S, mean, scale,
                                                            Cp, (__bf16*)out);
     else
-        k_blob<float, 1><<<cdiv(tot, 256), 256, 0, st>>>(frames, H, W, fstride, rstride, d_crops, N, S, mean, scale, Cp,
+        k_blob<float, 1><<<cdiv(tot, 256), 256, 0, st>>>(frames, F, H, W, fstride, rstride, d_crops, N, S, mean, scale, Cp,
                                                           (float*)out);
 }
 
@@ -99,14 +102,14 @@ void launch_blob(const uint8_t* frames, int H, int W, int64_t fstride, int64_t r
 
 using namespace vtf;
 
-extern "C" int vtf_blob_from_crops(const uint8_t* d_frames, int H, int W, int64_t frame_stride, int64_t row_stride,
+extern "C" int vtf_blob_from_crops(const uint8_t* d_frames, int F, int H, int W, int64_t frame_stride, int64_t row_stride,
                                    const int32_t* d_crops, int64_t N, int S, float mean, float scale, float* d_out,
                                    void* hip_stream) {
-    return guarded([&] {
+    return guarded_on(stream_device((hipStream_t)hip_stream), [&] {
         VTF_CHECK(N >= 0 && S > 0, VTF_E_ARG, "bad argument");
         if (N == 0) return;
         VTF_CHECK(d_frames && d_crops && d_out, VTF_E_ARG, "null argument");
-        launch_blob(d_frames, H, W, frame_stride, row_stride, d_crops, N, S, mean, scale, 0, 3, false, d_out,
+        launch_blob(d_frames, F, H, W, frame_stride, row_stride, d_crops, N, S, mean, scale, 0, 3, false, d_out,
                     (hipStream_t)hip_stream);
         VTF_HIP(hipGetLastError());
     });

@@ -1,4 +1,6 @@
 // C-ABI glue: error state, version, standalone box ops (include/vtf.h).
+#include <map>
+#include <memory>
 #include <mutex>
 #include <string>
 
@@ -19,11 +21,33 @@ __global__ void k_i32_to_i64(const int32_t* in, int64_t n, int64_t* out) {
     if (i < n) out[i] = (int64_t)in[i];
 }
 
-static Arena& standalone_arena() {
-    static Arena a;
-    return a;
+int stream_device(hipStream_t st) {
+    int dev = 0;
+    if (st) {
+        VTF_HIP(hipStreamGetDevice(st, &dev));
+    } else {
+        VTF_HIP(hipGetDevice(&dev));
+    }
+    return dev;
 }
-static std::mutex g_standalone_mu;
+
+StreamScratch stream_scratch(hipStream_t st) {
+    struct Slot {
+        std::mutex mu;
+        Arena ar;
+    };
+    static std::mutex g_mu;
+    static std::map<std::pair<int, hipStream_t>, std::unique_ptr<Slot>> g_slots;
+    const int dev = stream_device(st);
+    Slot* s;
+    {
+        std::lock_guard<std::mutex> lk(g_mu);
+        auto& p = g_slots[{dev, st}];
+        if (!p) p.reset(new Slot());
+        s = p.get();
+    }
+    return StreamScratch{&s->ar, std::unique_lock<std::mutex>(s->mu)};
+}
 
 }  // namespace vtf
 
@@ -37,14 +61,14 @@ int vtf_version(void) { return 1; }
 
 int vtf_batched_nms(const float* d_boxes, const float* d_scores, const int64_t* d_idxs, int64_t n,
                     double iou_threshold, int64_t* d_keep, int64_t* out_nkeep, void* hip_stream) {
-    return guarded([&] {
+    return guarded_on(stream_device((hipStream_t)hip_stream), [&] {
         VTF_CHECK(out_nkeep && n >= 0, VTF_E_ARG, "bad argument");
         *out_nkeep = 0;
         if (n == 0) return;
         VTF_CHECK(d_boxes && d_scores && d_idxs && d_keep, VTF_E_ARG, "null argument");
-        std::lock_guard<std::mutex> lk(g_standalone_mu);
         hipStream_t st = (hipStream_t)hip_stream;
-        Arena& ar = standalone_arena();
+        StreamScratch sc = stream_scratch(st);
+        Arena& ar = *sc.ar;
         int32_t* img = ar.get<int32_t>(0, n);
         int32_t* call = ar.get<int32_t>(1, n);
         int32_t* keep = ar.get<int32_t>(2, n);

@@ -6,6 +6,7 @@
 
 #include <cstdint>
 #include <cstdio>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -81,6 +82,41 @@ struct Arena {
         return reinterpret_cast<T*>(get(slot, n * sizeof(T)));
     }
 };
+
+// Makes `device` the calling thread's current HIP device for the scope of one entry point
+// (allocations and launches of a handle bound to cuda:1 must not land on cuda:0 when the
+// caller's current device differs) and restores the caller's device afterwards.
+struct DeviceGuard {
+    int prev = -1, dev = -1;
+    explicit DeviceGuard(int d) : dev(d) {
+        if (d < 0) return;
+        if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+        if (prev != d) VTF_HIP(hipSetDevice(d));
+    }
+    ~DeviceGuard() {
+        if (dev >= 0 && prev >= 0 && prev != dev) (void)hipSetDevice(prev);
+    }
+};
+
+// guarded() with the handle's device current for the call
+template <class F>
+int guarded_on(int device, F&& f) {
+    return guarded([&] {
+        DeviceGuard g(device);
+        f();
+    });
+}
+
+// Scratch of the stateless entry points (NMS, cosine dedupe / classify, blob): one arena per
+// (device, stream), held under its own lock for the call.  A process-global arena would hand
+// one device's buffer to a launch on another device, or one lane's buffer to a concurrent lane.
+struct StreamScratch {
+    Arena* ar;
+    std::unique_lock<std::mutex> lock;
+};
+StreamScratch stream_scratch(hipStream_t st);
+// the device a stream belongs to (the current device for the null stream)
+int stream_device(hipStream_t st);
 
 inline int cdiv(int64_t a, int64_t b) { return (int)((a + b - 1) / b); }
 

@@ -18,6 +18,7 @@
 // split-K over blockIdx.z for grids that cannot fill the chip.  Epilogue staged through LDS:
 // each thread finishes 8 consecutive channels of a row (16/32-byte residual loads / stores).
 #include <algorithm>
+#include <map>
 #include <mutex>
 #include <unordered_map>
 
@@ -476,10 +477,12 @@ __global__ void k_conv_splitk_epi(ConvParams p) {
 // and queued kernels may still use it) -- bounded by the geometric growth, process lifetime
 static float* splitk_workspace(hipStream_t st, size_t bytes) {
     static std::mutex mu;
-    static std::unordered_map<hipStream_t, std::pair<float*, size_t>> ws;
+    // keyed by (device, stream): the null stream of two devices is two different queues
+    static std::map<std::pair<int, hipStream_t>, std::pair<float*, size_t>> ws;
     static std::vector<float*> retired;
+    const int dev = stream_device(st);
     std::lock_guard<std::mutex> g(mu);
-    auto& e = ws[st];
+    auto& e = ws[{dev, st}];
     if (e.second < bytes) {
         if (e.first) retired.push_back(e.first);
         e.first = nullptr;

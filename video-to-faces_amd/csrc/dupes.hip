@@ -16,6 +16,7 @@
 #include <vector>
 
 #include "blob.hpp"
+#include "boxes.hpp"
 #include "common.hpp"
 
 namespace vtf {
@@ -105,12 +106,13 @@ using namespace vtf;
 
 extern "C" {
 
-int vtf_ahash_crops(const uint8_t* d_frames, int H, int W, int64_t frame_stride, int64_t row_stride,
+int vtf_ahash_crops(const uint8_t* d_frames, int F, int H, int W, int64_t frame_stride, int64_t row_stride,
                     const int32_t* crops, int64_t N, uint64_t* out_hashes, void* hip_stream) {
-    return guarded([&] {
+    return guarded_on(stream_device((hipStream_t)hip_stream), [&] {
         VTF_CHECK(N >= 0 && H > 0 && W > 0, VTF_E_ARG, "bad argument");
         if (N == 0) return;
         VTF_CHECK(d_frames && crops && out_hashes, VTF_E_ARG, "null argument");
+        check_crops_host(crops, N, F, H, W);
         hipStream_t st = (hipStream_t)hip_stream;
         int32_t* dc = nullptr;
         uint64_t* dh = nullptr;
@@ -126,7 +128,7 @@ int vtf_ahash_crops(const uint8_t* d_frames, int H, int W, int64_t frame_stride,
 }
 
 int vtf_hamming_dedupe(const uint64_t* d_hashes, int64_t N, int32_t* d_min, int64_t* d_arg, void* hip_stream) {
-    return guarded([&] {
+    return guarded_on(stream_device((hipStream_t)hip_stream), [&] {
         VTF_CHECK(N >= 0, VTF_E_ARG, "bad argument");
         if (N == 0) return;
         VTF_CHECK(d_hashes && d_min && d_arg, VTF_E_ARG, "null argument");

@@ -7,6 +7,7 @@
 #include <vector>
 
 #include "blob.hpp"
+#include "boxes.hpp"
 #include "common.hpp"
 #include "conv.hpp"
 
@@ -321,7 +322,7 @@ extern "C" {
 int vtf_facenet_create(const float* params, int64_t n_params, int device, int precision, vtf_facenet_t* out) {
     return guarded([&] {
         VTF_CHECK(params && out && (precision == 0 || precision == 1), VTF_E_ARG, "bad argument");
-        VTF_HIP(hipSetDevice(device));
+        DeviceGuard dg(device);
         auto* h = new vtf_facenet_s();
         h->f.device = device;
         h->f.bf16 = precision == 1;
@@ -336,18 +337,18 @@ int vtf_facenet_create(const float* params, int64_t n_params, int device, int pr
 }
 
 int vtf_facenet_destroy(vtf_facenet_t h) {
-    return guarded([&] { delete h; });
+    return guarded_on(h ? h->f.device : -1, [&] { delete h; });
 }
 
 int vtf_facenet_set_stream(vtf_facenet_t h, void* stream) {
-    return guarded([&] {
+    return guarded_on(h ? h->f.device : -1, [&] {
         VTF_CHECK(h, VTF_E_ARG, "null handle");
         h->f.st = (hipStream_t)stream;
     });
 }
 
 int vtf_facenet_forward(vtf_facenet_t h, const float* d_x, int64_t N, float* d_emb) {
-    return guarded([&] {
+    return guarded_on(h ? h->f.device : -1, [&] {
         VTF_CHECK(h && N >= 0, VTF_E_ARG, "bad argument");
         if (N == 0) return;
         VTF_CHECK(d_x && d_emb, VTF_E_ARG, "null argument");
@@ -359,18 +360,24 @@ int vtf_facenet_forward(vtf_facenet_t h, const float* d_x, int64_t N, float* d_e
     });
 }
 
-int vtf_facenet_encode_crops(vtf_facenet_t h, const uint8_t* d_frames, int H, int W, int64_t frame_stride,
-                             int64_t row_stride, const int32_t* crops, int64_t N, float* d_emb) {
-    return guarded([&] {
-        VTF_CHECK(h && N >= 0, VTF_E_ARG, "bad argument");
+int vtf_facenet_encode_crops(vtf_facenet_t h, const uint8_t* d_frames, int n_frames, int H, int W,
+                             int64_t frame_stride, int64_t row_stride, const int32_t* crops, int crops_on_device,
+                             int64_t N, float* d_emb) {
+    return guarded_on(h ? h->f.device : -1, [&] {
+        VTF_CHECK(h && N >= 0 && n_frames > 0 && H > 0 && W > 0, VTF_E_ARG, "bad argument");
         if (N == 0) return;
         VTF_CHECK(d_frames && crops && d_emb, VTF_E_ARG, "null argument");
         Facenet& F = h->f;
-        int32_t* dc = F.ar.get<int32_t>(6, N * 5);
-        VTF_HIP(hipMemcpyAsync(dc, crops, N * 5 * 4, hipMemcpyHostToDevice, F.st));
+        const int32_t* dc = crops;
+        if (!crops_on_device) {
+            check_crops_host(crops, N, n_frames, H, W);
+            int32_t* d = F.ar.get<int32_t>(6, N * 5);
+            VTF_HIP(hipMemcpyAsync(d, crops, N * 5 * 4, hipMemcpyHostToDevice, F.st));
+            dc = d;
+        }
         void* xin = F.ar.get(5, (size_t)N * 160 * 160 * 8 * (F.bf16 ? 2 : 4));
         // blobFromImages(images, 1/128, (160,160), (127.5,)*3, swapRB=True) (facenet.py:179)
-        launch_blob(d_frames, H, W, frame_stride, row_stride, dc, N, 160, 127.5f, 0.0078125f, 1, 8, F.bf16, xin, F.st);
+        launch_blob(d_frames, n_frames, H, W, frame_stride, row_stride, dc, N, 160, 127.5f, 0.0078125f, 1, 8, F.bf16, xin, F.st);
         forward(F, xin, (int)N, d_emb);
         VTF_HIP(hipGetLastError());
     });

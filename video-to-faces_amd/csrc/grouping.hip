@@ -152,10 +152,6 @@ __global__ void k_classify(const float* __restrict__ Xn, const float* __restrict
     arg[i] = bk;
 }
 
-static Arena& grouping_arena() {
-    static Arena a;
-    return a;
-}
 
 }  // namespace vtf
 
@@ -164,12 +160,13 @@ using namespace vtf;
 extern "C" {
 
 int vtf_cosine_dedupe(const float* d_X, int64_t N, int64_t D, float* d_min, int64_t* d_arg, void* hip_stream) {
-    return guarded([&] {
+    return guarded_on(stream_device((hipStream_t)hip_stream), [&] {
         VTF_CHECK(N >= 0 && D > 0, VTF_E_ARG, "bad argument");
         if (N == 0) return;
         VTF_CHECK(d_X && d_min && d_arg && N < (int64_t)1 << 31, VTF_E_ARG, "bad argument");
         hipStream_t st = (hipStream_t)hip_stream;
-        Arena& ar = grouping_arena();
+        StreamScratch sc = stream_scratch(st);
+        Arena& ar = *sc.ar;
         int Dp = (int)((D + CK - 1) / CK * CK);
         float* Xn = ar.get<float>(0, N * Dp);
         uint64_t* key = ar.get<uint64_t>(1, N);
@@ -186,12 +183,13 @@ int vtf_cosine_dedupe(const float* d_X, int64_t N, int64_t D, float* d_min, int6
 
 int vtf_cosine_classify(const float* d_X, int64_t N, const float* d_R, int64_t C, int64_t D, float* d_min,
                         int64_t* d_arg, void* hip_stream) {
-    return guarded([&] {
+    return guarded_on(stream_device((hipStream_t)hip_stream), [&] {
         VTF_CHECK(N >= 0 && C > 0 && D > 0, VTF_E_ARG, "bad argument");
         if (N == 0) return;
         VTF_CHECK(d_X && d_R && d_min && d_arg, VTF_E_ARG, "null argument");
         hipStream_t st = (hipStream_t)hip_stream;
-        Arena& ar = grouping_arena();
+        StreamScratch sc = stream_scratch(st);
+        Arena& ar = *sc.ar;
         int Dp = (int)((D + CK - 1) / CK * CK);
         float* Xn = ar.get<float>(2, N * Dp);
         float* Rn = ar.get<float>(3, C * Dp);

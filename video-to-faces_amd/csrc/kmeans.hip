@@ -413,7 +413,7 @@ extern "C" {
 int vtf_group_create(int device, vtf_group_t* out) {
     return guarded([&] {
         VTF_CHECK(out, VTF_E_ARG, "null argument");
-        VTF_HIP(hipSetDevice(device));
+        DeviceGuard dg(device);
         auto* h = new vtf_group_s();
         h->g.device = device;
         *out = h;
@@ -421,18 +421,18 @@ int vtf_group_create(int device, vtf_group_t* out) {
 }
 
 int vtf_group_destroy(vtf_group_t h) {
-    return guarded([&] { delete h; });
+    return guarded_on(h ? h->g.device : -1, [&] { delete h; });
 }
 
 int vtf_group_set_stream(vtf_group_t h, void* stream) {
-    return guarded([&] {
+    return guarded_on(h ? h->g.device : -1, [&] {
         VTF_CHECK(h, VTF_E_ARG, "null handle");
         h->g.st = (hipStream_t)stream;
     });
 }
 
 int vtf_colstats(vtf_group_t h, const float* d_X, int64_t N, int64_t D, float* d_Xc, float* d_mean, float* d_var) {
-    return guarded([&] {
+    return guarded_on(h ? h->g.device : -1, [&] {
         VTF_CHECK(h && d_X && d_mean && d_var && N > 0 && D > 0 && D < (1 << 20), VTF_E_ARG, "bad argument");
         k_colstats<<<cdiv(D, 64), 64, 0, h->g.st>>>(d_X, N, (int)D, d_Xc, d_mean, d_var);
         VTF_HIP(hipGetLastError());
@@ -440,7 +440,7 @@ int vtf_colstats(vtf_group_t h, const float* d_X, int64_t N, int64_t D, float* d
 }
 
 int vtf_sqdist_rows(vtf_group_t h, const float* d_X, int64_t N, int64_t D, const int64_t* rows, int T, float* d_out) {
-    return guarded([&] {
+    return guarded_on(h ? h->g.device : -1, [&] {
         VTF_CHECK(h && d_X && rows && d_out && N > 0 && D > 0 && T > 0 && T <= 16, VTF_E_ARG, "bad argument");
         VTF_CHECK((size_t)T * D * 4 <= 64 * 1024, VTF_E_LIMIT, "sqdist_rows: T*D too large");
         for (int t = 0; t < T; t++) VTF_CHECK(rows[t] >= 0 && rows[t] < N, VTF_E_ARG, "row index out of range");
@@ -459,7 +459,7 @@ int vtf_sqdist_rows(vtf_group_t h, const float* d_X, int64_t N, int64_t D, const
 // E-step (+ M-step sums when d_sums != NULL).  d_labels in/out; *out_changed = labels changed.
 int vtf_kmeans_step(vtf_group_t h, const float* d_X, int64_t N, int64_t D, const float* d_centers, int k,
                     int32_t* d_labels, float* d_sums, float* d_weights, int64_t* out_changed) {
-    return guarded([&] {
+    return guarded_on(h ? h->g.device : -1, [&] {
         VTF_CHECK(h && d_X && d_centers && d_labels && N > 0 && D > 0 && k > 0 && k <= 256, VTF_E_ARG,
                   "bad argument");
         VTF_CHECK((size_t)k * D * 4 <= 128 * 1024, VTF_E_LIMIT, "kmeans: k*D too large for LDS");
@@ -490,7 +490,7 @@ int vtf_kmeans_step(vtf_group_t h, const float* d_X, int64_t N, int64_t D, const
 
 int vtf_kmeans_average(vtf_group_t h, float* d_sums, const float* d_weights, const float* d_centers_old, int k,
                        int64_t D, float* d_shift) {
-    return guarded([&] {
+    return guarded_on(h ? h->g.device : -1, [&] {
         VTF_CHECK(h && d_sums && d_weights && d_centers_old && d_shift && k > 0 && D > 0, VTF_E_ARG, "bad argument");
         k_average<<<1, 256, 0, h->g.st>>>(d_sums, d_weights, d_centers_old, k, (int)D, d_shift);
         VTF_HIP(hipGetLastError());
@@ -499,7 +499,7 @@ int vtf_kmeans_average(vtf_group_t h, float* d_sums, const float* d_weights, con
 
 int vtf_center_dist(vtf_group_t h, const float* d_X, int64_t N, int64_t D, const float* d_centers,
                     const int32_t* d_labels, float* d_out) {
-    return guarded([&] {
+    return guarded_on(h ? h->g.device : -1, [&] {
         VTF_CHECK(h && d_X && d_centers && d_labels && d_out && N > 0 && D > 0, VTF_E_ARG, "bad argument");
         k_center_dist<<<cdiv(N, 256), 256, 0, h->g.st>>>(d_X, N, (int)D, d_centers, d_labels, d_out);
         VTF_HIP(hipGetLastError());
@@ -507,7 +507,7 @@ int vtf_center_dist(vtf_group_t h, const float* d_X, int64_t N, int64_t D, const
 }
 
 int vtf_pairwise_euclidean(vtf_group_t h, const float* d_X, int64_t N, int64_t D, float* d_out) {
-    return guarded([&] {
+    return guarded_on(h ? h->g.device : -1, [&] {
         VTF_CHECK(h && d_X && d_out && N > 0 && D > 0, VTF_E_ARG, "bad argument");
         VTF_CHECK(N <= (1 << 20), VTF_E_LIMIT, "pairwise: N too large");
         double* nrm = h->g.ar.get<double>(5, N);
@@ -520,7 +520,7 @@ int vtf_pairwise_euclidean(vtf_group_t h, const float* d_X, int64_t N, int64_t D
 
 int vtf_silhouette_samples(vtf_group_t h, const float* d_D, int64_t N, const int32_t* d_labels, int k,
                            const int64_t* d_freq, float* d_sil) {
-    return guarded([&] {
+    return guarded_on(h ? h->g.device : -1, [&] {
         VTF_CHECK(h && d_D && d_labels && d_freq && d_sil && N > 1 && k >= 2, VTF_E_ARG, "bad argument");
         VTF_CHECK(k <= 64, VTF_E_LIMIT, "silhouette: more than 64 labels");
         hipStream_t st = h->g.st;
@@ -539,7 +539,7 @@ int vtf_silhouette_samples(vtf_group_t h, const float* d_D, int64_t N, const int
 
 int vtf_cluster_sums(vtf_group_t h, const float* d_X, int64_t N, int64_t D, const int32_t* d_labels, int k,
                      double* d_sums, double* d_sqnorm, int64_t* d_counts) {
-    return guarded([&] {
+    return guarded_on(h ? h->g.device : -1, [&] {
         VTF_CHECK(h && d_X && d_labels && d_sums && d_sqnorm && d_counts && N > 0 && D > 0 && k > 0, VTF_E_ARG,
                   "bad argument");
         hipStream_t st = h->g.st;
@@ -554,7 +554,7 @@ int vtf_cluster_sums(vtf_group_t h, const float* d_X, int64_t N, int64_t D, cons
 
 int vtf_cluster_dist(vtf_group_t h, const float* d_X, int64_t N, int64_t D, const int32_t* d_labels, int k,
                      const double* d_centroids, double* d_dsum) {
-    return guarded([&] {
+    return guarded_on(h ? h->g.device : -1, [&] {
         VTF_CHECK(h && d_X && d_labels && d_centroids && d_dsum && N > 0 && D > 0 && k > 0, VTF_E_ARG,
                   "bad argument");
         VTF_HIP(hipMemsetAsync(d_dsum, 0, (size_t)k * 8, h->g.st));

@@ -7,6 +7,7 @@
 #include <numeric>
 #include <vector>
 
+#include "boxes.hpp"
 #include "common.hpp"
 #include "conv.hpp"
 #include "mtcnn.hpp"
@@ -22,6 +23,61 @@ __global__ void k_desc_keys(const float* s, int64_t n, uint64_t* k) {
     int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i < n) k[i] = desc_key(s[i]);
 }
+// Final rows grouped by image, keeping the IoM keep order inside each image (the reference
+// splits the kept boxes per image with boolean masks, mtcnn.py:244-249): row k of the keep list
+// is element order[pos[k]].  One workgroup: a stable counting sort by image (per-image counts,
+// their exclusive scan, then each 1024-row chunk ranks its rows among equal images).
+__global__ __launch_bounds__(1024) void k_mtcnn_rows(const int32_t* __restrict__ order, const int32_t* __restrict__ pos,
+                                                     int nf, const int32_t* __restrict__ img,
+                                                     const float4* __restrict__ box, const float* __restrict__ score,
+                                                     const float* __restrict__ lm, int B, float* __restrict__ rows,
+                                                     float* __restrict__ lmo, int32_t* __restrict__ counts) {
+    __shared__ int s_cnt[4096];
+    __shared__ int s_base[4096];
+    __shared__ int s_img[1024];
+    const int tid = threadIdx.x;
+    for (int b = tid; b < B; b += 1024) s_cnt[b] = 0;
+    __syncthreads();
+    for (int k = tid; k < nf; k += 1024) atomicAdd(&s_cnt[img[order[pos[k]]]], 1);
+    __syncthreads();
+    if (tid == 0) {
+        int acc = 0;
+        for (int b = 0; b < B; b++) {
+            s_base[b] = acc;
+            counts[b] = s_cnt[b];
+            acc += s_cnt[b];
+            s_cnt[b] = 0;
+        }
+    }
+    __syncthreads();
+    for (int c0 = 0; c0 < nf; c0 += 1024) {
+        const int k = c0 + tid;
+        int e = -1, b = -1;
+        if (k < nf) {
+            e = order[pos[k]];
+            b = img[e];
+        }
+        s_img[tid] = b;
+        __syncthreads();
+        if (k < nf) {
+            int rank = 0;
+            for (int j = 0; j < tid; j++) rank += s_img[j] == b;
+            const int dst = s_base[b] + s_cnt[b] + rank;
+            const float4 bx = box[e];
+            float* o = rows + (int64_t)dst * 5;
+            o[0] = bx.x;
+            o[1] = bx.y;
+            o[2] = bx.z;
+            o[3] = bx.w;
+            o[4] = score[e];
+            for (int j = 0; j < 10; j++) lmo[(int64_t)dst * 10 + j] = lm[(int64_t)e * 10 + j];
+        }
+        __syncthreads();
+        if (k < nf) atomicAdd(&s_cnt[b], 1);
+        __syncthreads();
+    }
+}
+
 __global__ void k_gather_rows(const int32_t* idx, int64_t n, const float* in, int row, float* out) {
     int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n * row) return;
@@ -290,7 +346,7 @@ static void build_weights(Mtcnn& m, const float* params, int64_t n_params) {
 
 // RNet / ONet on NHWC fp32 crops x0 [n,S,S,8] (mtcnn.py:58-76 / 101-121), layer by layer on
 // the MFMA conv kernel; pools are torch MaxPool2d(ceil_mode=True).
-enum RSlot { S_RA = 70, S_RB = 71 };  // nms_multi owns slots 40-61
+enum RSlot { S_RA = 70, S_RB = 71, S_BOXPOST = 72 };  // nms_multi owns slots 40-61
 // first = 1: x0 is the fused front end's pooled conv1 map [n,P,P,32] (k_cand_front)
 static void run_candidates(Mtcnn& m, bool onet, const float* x0, int64_t n, float4* reg, float* lm, float* prob,
                            int first = 0, int force_fp32 = 0) {
@@ -425,10 +481,13 @@ static int64_t threshold_compact(Mtcnn& m, const float* d_s, int64_t n, float th
     return cnt;
 }
 
+// final detections in HBM: rows [n,5] (x1,y1,x2,y2,score) and landmarks [n,10] grouped by image
+// in the reference's order; counts per image (host)
 struct DetectOut {
-    std::vector<float> boxes;  // [n,5]
-    std::vector<float> lms;    // [n,10] as [5][2]
-    std::vector<int32_t> img;
+    const float* rows = nullptr;
+    const float* lms = nullptr;
+    int64_t n = 0;
+    std::vector<int32_t> counts;
 };
 
 static void detect(Mtcnn& m, const uint8_t* frames, int on_dev, int B, int H, int W, int64_t fstride,
@@ -436,9 +495,9 @@ static void detect(Mtcnn& m, const uint8_t* frames, int on_dev, int B, int H, in
     VTF_CHECK(B > 0 && H > 0 && W > 0 && minsize > 0, VTF_E_ARG, "mtcnn: bad shape");
     hipStream_t st = m.st;
     std::memset(m.stats, 0, sizeof(m.stats));
-    out.boxes.clear();
-    out.lms.clear();
-    out.img.clear();
+    out.rows = out.lms = nullptr;
+    out.n = 0;
+    out.counts.assign(B, 0);
     const uint8_t* fr = frames;
     if (!on_dev) {
         uint8_t* d = m.ar.get<uint8_t>(S_FRAMES, (size_t)B * H * W * 3);
@@ -457,6 +516,7 @@ static void detect(Mtcnn& m, const uint8_t* frames, int on_dev, int B, int H, in
     m.stats[0] = NL;
     if (NL == 0) return;
     VTF_CHECK(NL < 4096 && cells < (int64_t)1 << 31, VTF_E_LIMIT, "mtcnn: pyramid too large for one call");
+    VTF_CHECK(B <= 4096, VTF_E_LIMIT, "mtcnn: at most 4096 frames per call");
     // downsampled levels whose adaptive-pool bins exceed 2 frame pixels are resampled by a
     // separate fully parallel kernel (one thread per level value) into HBM; inside the fused
     // tile kernel their long serial bin sums would leave a few workgroups as a long tail.
@@ -610,32 +670,15 @@ static void detect(Mtcnn& m, const uint8_t* frames, int on_dev, int B, int H, in
     d2h_sync(&nf, incl + n3 - 1, 4, st);
     m.stats[7] = nf;
     if (nf == 0) return;
-    // final rows in IoM keep order: element = order[pos[k]]
-    std::vector<int32_t> h_order(n3), h_pos(nf), h_img(n3);
-    std::vector<float4> h_box(n3);
-    std::vector<float> h_s(n3), h_lm(n3 * 10);
-    VTF_HIP(hipMemcpyAsync(h_order.data(), order, n3 * 4, hipMemcpyDeviceToHost, st));
-    VTF_HIP(hipMemcpyAsync(h_pos.data(), pos, nf * 4, hipMemcpyDeviceToHost, st));
-    VTF_HIP(hipMemcpyAsync(h_img.data(), i2, n3 * 4, hipMemcpyDeviceToHost, st));
-    VTF_HIP(hipMemcpyAsync(h_box.data(), b3, n3 * 16, hipMemcpyDeviceToHost, st));
-    VTF_HIP(hipMemcpyAsync(h_s.data(), s2, n3 * 4, hipMemcpyDeviceToHost, st));
-    VTF_HIP(hipMemcpyAsync(h_lm.data(), lmk, n3 * 40, hipMemcpyDeviceToHost, st));
-    VTF_HIP(hipStreamSynchronize(st));
-    out.boxes.resize(nf * 5);
-    out.lms.resize(nf * 10);
-    out.img.resize(nf);
-    for (int k = 0; k < nf; k++) {
-        int e = h_order[h_pos[k]];
-        float4 bx = h_box[e];
-        float* o = &out.boxes[k * 5];
-        o[0] = bx.x;
-        o[1] = bx.y;
-        o[2] = bx.z;
-        o[3] = bx.w;
-        o[4] = h_s[e];
-        std::memcpy(&out.lms[k * 10], &h_lm[e * 10], 40);
-        out.img[k] = h_img[e];
-    }
+    // final rows grouped by image in IoM keep order (element of keep row k = order[pos[k]])
+    float* rows = m.ar.get<float>(S_OUTB, (size_t)nf * 5);
+    float* lmo = m.ar.get<float>(S_OUTS, (size_t)nf * 10);
+    int32_t* dcnt = m.ar.get<int32_t>(S_OUTI, B);
+    k_mtcnn_rows<<<1, 1024, 0, st>>>(order, pos, nf, i2, b3, s2, lmk, B, rows, lmo, dcnt);
+    d2h_sync(out.counts.data(), dcnt, (size_t)B * 4, st);
+    out.rows = rows;
+    out.lms = lmo;
+    out.n = nf;
 }
 
 }  // namespace vtf
@@ -651,7 +694,7 @@ extern "C" {
 int vtf_mtcnn_create(const float* params, int64_t n_params, int device, vtf_mtcnn_t* out) {
     return guarded([&] {
         VTF_CHECK(params && out, VTF_E_ARG, "null argument");
-        VTF_HIP(hipSetDevice(device));
+        DeviceGuard dg(device);
         auto* h = new vtf_mtcnn_s();
         h->m.device = device;
         try {
@@ -665,18 +708,18 @@ int vtf_mtcnn_create(const float* params, int64_t n_params, int device, vtf_mtcn
 }
 
 int vtf_mtcnn_destroy(vtf_mtcnn_t h) {
-    return guarded([&] { delete h; });
+    return guarded_on(h ? h->m.device : -1, [&] { delete h; });
 }
 
 int vtf_mtcnn_set_stream(vtf_mtcnn_t h, void* stream) {
-    return guarded([&] {
+    return guarded_on(h ? h->m.device : -1, [&] {
         VTF_CHECK(h, VTF_E_ARG, "null handle");
         h->m.st = (hipStream_t)stream;
     });
 }
 
 int vtf_mtcnn_stats(vtf_mtcnn_t h, int64_t* out8) {
-    return guarded([&] {
+    return guarded_on(h ? h->m.device : -1, [&] {
         VTF_CHECK(h && out8, VTF_E_ARG, "null argument");
         std::memcpy(out8, h->m.stats, sizeof(h->m.stats));
     });
@@ -684,7 +727,7 @@ int vtf_mtcnn_stats(vtf_mtcnn_t h, int64_t* out8) {
 
 int vtf_mtcnn_profile(vtf_mtcnn_t h, int enable, double* out_ms, int64_t* out_launches, double* out_flops,
                       int64_t* out_frames) {
-    return guarded([&] {
+    return guarded_on(h ? h->m.device : -1, [&] {
         VTF_CHECK(h, VTF_E_ARG, "null handle");
         Mtcnn& m = h->m;
         if (out_ms) *out_ms = m.prof_ms;
@@ -704,30 +747,37 @@ int vtf_mtcnn_profile(vtf_mtcnn_t h, int enable, double* out_ms, int64_t* out_la
 int vtf_mtcnn_detect(vtf_mtcnn_t h, const uint8_t* frames, int frames_on_device, int B, int H, int W,
                      int64_t frame_stride, int64_t row_stride, double min_face_size, float* out_boxes,
                      float* out_landmarks, int32_t* out_counts, int64_t cap, int64_t* out_total) {
-    return guarded([&] {
+    return guarded_on(h ? h->m.device : -1, [&] {
         VTF_CHECK(h && frames && out_counts, VTF_E_ARG, "null argument");
-        VTF_HIP(hipSetDevice(h->m.device));
         DetectOut r;
         detect(h->m, frames, frames_on_device, B, H, W, frame_stride, row_stride, min_face_size, r);
-        int64_t n = (int64_t)r.img.size();
-        if (out_total) *out_total = n;
-        VTF_CHECK(n <= cap, VTF_E_CAPACITY, "output capacity too small");
-        for (int b = 0; b < B; b++) out_counts[b] = 0;
-        int64_t k = 0;
-        for (int b = 0; b < B; b++)
-            for (int64_t e = 0; e < n; e++)
-                if (r.img[e] == b) {
-                    if (out_boxes) std::memcpy(out_boxes + k * 5, &r.boxes[e * 5], 20);
-                    if (out_landmarks) std::memcpy(out_landmarks + k * 10, &r.lms[e * 10], 40);
-                    out_counts[b]++;
-                    k++;
-                }
+        if (out_total) *out_total = r.n;
+        VTF_CHECK(r.n <= cap, VTF_E_CAPACITY, "output capacity too small");
+        std::copy(r.counts.begin(), r.counts.end(), out_counts);
+        if (r.n == 0) return;
+        if (out_boxes) VTF_HIP(hipMemcpyAsync(out_boxes, r.rows, r.n * 20, hipMemcpyDeviceToHost, h->m.st));
+        if (out_landmarks) VTF_HIP(hipMemcpyAsync(out_landmarks, r.lms, r.n * 40, hipMemcpyDeviceToHost, h->m.st));
+        VTF_HIP(hipStreamSynchronize(h->m.st));
+    });
+}
+
+int vtf_mtcnn_detect_crops(vtf_mtcnn_t h, const uint8_t* frames, int frames_on_device, int B, int H, int W,
+                           int64_t frame_stride, int64_t row_stride, double min_face_size,
+                           const vtf_box_params* params, int32_t frame_offset, int32_t* d_crops,
+                           int32_t* out_frame_counts, int64_t cap, int64_t* out_n) {
+    return guarded_on(h ? h->m.device : -1, [&] {
+        VTF_CHECK(h && frames && params && out_n, VTF_E_ARG, "null argument");
+        DetectOut r;
+        detect(h->m, frames, frames_on_device, B, H, W, frame_stride, row_stride, min_face_size, r);
+        VTF_CHECK(r.n == 0 || d_crops, VTF_E_ARG, "null argument");
+        rows_to_crops(h->m.ar, S_BOXPOST, r.rows, r.counts, H, W, *params, frame_offset, d_crops, nullptr,
+                      out_frame_counts, cap, out_n, h->m.st);
     });
 }
 
 int vtf_mtcnn_pnet_level(vtf_mtcnn_t h, const uint8_t* d_frames, int B, int H, int W, int64_t frame_stride,
                          int64_t row_stride, int lh, int lw, float* d_prob, float* d_reg) {
-    return guarded([&] {
+    return guarded_on(h ? h->m.device : -1, [&] {
         VTF_CHECK(h && d_frames && d_prob && d_reg && lh >= 12 && lw >= 12, VTF_E_ARG, "bad argument");
         PNetLevel L{};
         L.lh = lh;
@@ -760,7 +810,7 @@ int vtf_mtcnn_pnet_level(vtf_mtcnn_t h, const uint8_t* d_frames, int B, int H, i
 
 int vtf_mtcnn_resample(vtf_mtcnn_t h, const uint8_t* d_frames, int B, int H, int W, int64_t frame_stride,
                        int64_t row_stride, int lh, int lw, float* d_out) {
-    return guarded([&] {
+    return guarded_on(h ? h->m.device : -1, [&] {
         VTF_CHECK(h && d_frames && d_out, VTF_E_ARG, "null argument");
         int4* sat = h->m.ar.get<int4>(S_SAT, (size_t)B * (H + 1) * (W + 1));
         launch_sat(d_frames, frame_stride, row_stride, B, H, W, sat, h->m.st);
@@ -770,7 +820,7 @@ int vtf_mtcnn_resample(vtf_mtcnn_t h, const uint8_t* d_frames, int B, int H, int
 }
 
 int vtf_mtcnn_rnet(vtf_mtcnn_t h, const float* d_in, int64_t n, float* d_reg, float* d_prob) {
-    return guarded([&] {
+    return guarded_on(h ? h->m.device : -1, [&] {
         VTF_CHECK(h && d_in && d_reg && d_prob, VTF_E_ARG, "null argument");
         float* x0 = h->m.ar.get<float>(S_CROP, (size_t)n * 24 * 24 * 8);
         launch_nchw_to_nhwc(d_in, (int)n, 3, 24, 24, 8, x0, false, h->m.st);
@@ -780,7 +830,7 @@ int vtf_mtcnn_rnet(vtf_mtcnn_t h, const float* d_in, int64_t n, float* d_reg, fl
 }
 
 int vtf_mtcnn_onet(vtf_mtcnn_t h, const float* d_in, int64_t n, float* d_reg, float* d_lm, float* d_prob) {
-    return guarded([&] {
+    return guarded_on(h ? h->m.device : -1, [&] {
         VTF_CHECK(h && d_in && d_reg && d_lm && d_prob, VTF_E_ARG, "null argument");
         float* x0 = h->m.ar.get<float>(S_CROP, (size_t)n * 48 * 48 * 8);
         launch_nchw_to_nhwc(d_in, (int)n, 3, 48, 48, 8, x0, false, h->m.st);

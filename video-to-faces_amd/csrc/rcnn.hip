@@ -25,6 +25,7 @@
 #include <vector>
 
 #include "blob.hpp"
+#include "boxes.hpp"
 #include "common.hpp"
 #include "conv.hpp"
 #include "nms.hpp"
@@ -780,14 +781,19 @@ __global__ void k_rcnn_final(const int32_t* __restrict__ keep, const int64_t* __
 }
 
 struct ROut {
-    std::vector<float> rows;     // [n,5] x1,y1,x2,y2,score
+    std::vector<float> rows;     // [n,5] x1,y1,x2,y2,score (host copy, when requested)
     std::vector<int32_t> counts;  // per image; -1 past the last image holding a proposal
+    const float* d_rows = nullptr;  // the same rows in HBM
+    int64_t n = 0;
+    bool host = true;
 };
 
 static void roi_stage(Rcnn& R, const RMap P[R_LEVELS], const float4* d_props, const int32_t* d_pimg, int64_t np, int B,
                       int H, int W, int hu, int wu, ROut& out) {
     hipStream_t st = R.st;
     out.rows.clear();
+    out.d_rows = nullptr;
+    out.n = 0;
     out.counts.assign(B, 0);
     // n = max(imidx) + 1 (rcnn.py:111): later images are absent from the reference's lists
     int nimg = 0;
@@ -853,6 +859,9 @@ static void roi_stage(Rcnn& R, const RMap P[R_LEVELS], const float4* d_props, co
     // scale_boxes: torch.tensor(sz_orig) / torch.tensor(sz_used) in fp32, flipped to (x, y)
     const float sx = (float)W / (float)wu, sy = (float)H / (float)hu;
     k_rcnn_final<<<B, 128, 0, st>>>(keep, doffs, cb, cs, sx, sy, R_FINAL, drows);
+    out.d_rows = drows;
+    out.n = ob;
+    if (!out.host) return;
     out.rows.resize((size_t)ob * 5);
     if (ob) VTF_HIP(hipMemcpyAsync(out.rows.data(), drows, ob * 20, hipMemcpyDeviceToHost, st));
     VTF_HIP(hipStreamSynchronize(st));
@@ -910,7 +919,7 @@ extern "C" {
 int vtf_rcnn_create(const float* params, int64_t n_params, int device, int precision, vtf_rcnn_t* out) {
     return guarded([&] {
         VTF_CHECK(params && out && (precision == 0 || precision == 1), VTF_E_ARG, "bad argument");
-        VTF_HIP(hipSetDevice(device));
+        DeviceGuard dg(device);
         auto* h = new vtf_rcnn_s();
         h->r.device = device;
         h->r.bf16 = precision == 1;
@@ -925,13 +934,28 @@ int vtf_rcnn_create(const float* params, int64_t n_params, int device, int preci
 }
 
 int vtf_rcnn_destroy(vtf_rcnn_t h) {
-    return guarded([&] { delete h; });
+    return guarded_on(h ? h->r.device : -1, [&] { delete h; });
 }
 
 int vtf_rcnn_set_stream(vtf_rcnn_t h, void* stream) {
-    return guarded([&] {
+    return guarded_on(h ? h->r.device : -1, [&] {
         VTF_CHECK(h, VTF_E_ARG, "null handle");
         h->r.st = (hipStream_t)stream;
+    });
+}
+
+int vtf_rcnn_detect_crops(vtf_rcnn_t h, const uint8_t* frames, int frames_on_device, int B, int H, int W,
+                          int64_t frame_stride, int64_t row_stride, const vtf_box_params* params,
+                          int32_t frame_offset, int32_t* d_crops, int32_t* out_frame_counts, int64_t cap,
+                          int64_t* out_n) {
+    return guarded_on(h ? h->r.device : -1, [&] {
+        VTF_CHECK(h && frames && params && out_n, VTF_E_ARG, "null argument");
+        ROut r;
+        r.host = false;
+        detect(h->r, frames, frames_on_device, B, H, W, frame_stride, row_stride, r);
+        VTF_CHECK(r.n == 0 || d_crops, VTF_E_ARG, "null argument");
+        rows_to_crops(h->r.ar, 300, r.d_rows, r.counts, H, W, *params, frame_offset, d_crops, nullptr,
+                      out_frame_counts, cap, out_n, h->r.st);
     });
 }
 
@@ -950,9 +974,8 @@ int vtf_rcnn_input_size(int H, int W, int* out4) {
 int vtf_rcnn_detect(vtf_rcnn_t h, const uint8_t* frames, int frames_on_device, int B, int H, int W,
                     int64_t frame_stride, int64_t row_stride, float* out_boxes, float* out_scores, int32_t* out_counts,
                     int64_t cap, int64_t* out_total) {
-    return guarded([&] {
+    return guarded_on(h ? h->r.device : -1, [&] {
         VTF_CHECK(h && frames && out_counts, VTF_E_ARG, "null argument");
-        VTF_HIP(hipSetDevice(h->r.device));
         ROut r;
         detect(h->r, frames, frames_on_device, B, H, W, frame_stride, row_stride, r);
         int64_t n = (int64_t)r.rows.size() / 5;
@@ -968,7 +991,7 @@ int vtf_rcnn_detect(vtf_rcnn_t h, const uint8_t* frames, int frames_on_device, i
 
 int vtf_rcnn_preprocess(vtf_rcnn_t h, const uint8_t* d_frames, int B, int H, int W, int64_t frame_stride,
                         int64_t row_stride, float* d_out) {
-    return guarded([&] {
+    return guarded_on(h ? h->r.device : -1, [&] {
         VTF_CHECK(h && d_frames && d_out && B > 0, VTF_E_ARG, "bad argument");
         int hu, wu;
         used_size(H, W, hu, wu);
@@ -980,7 +1003,7 @@ int vtf_rcnn_preprocess(vtf_rcnn_t h, const uint8_t* d_frames, int B, int H, int
 
 int vtf_rcnn_rpn_heads(vtf_rcnn_t h, const float* d_x, int B, int Hp, int Wp, float* d_head0, float* d_head1,
                        float* d_head2, float* d_head3, float* d_head4) {
-    return guarded([&] {
+    return guarded_on(h ? h->r.device : -1, [&] {
         VTF_CHECK(h && d_x && d_head0 && d_head1 && d_head2 && d_head3 && d_head4 && B > 0, VTF_E_ARG, "bad argument");
         Rcnn& R = h->r;
         void* x0 = R.ar.get(291, (size_t)B * Hp * Wp * 8 * (R.bf16 ? 2 : 4));
@@ -993,7 +1016,7 @@ int vtf_rcnn_rpn_heads(vtf_rcnn_t h, const float* d_x, int B, int Hp, int Wp, fl
 }
 
 int vtf_rcnn_proposals(vtf_rcnn_t h, float* out, int64_t cap, int64_t* out_n) {
-    return guarded([&] {
+    return guarded_on(h ? h->r.device : -1, [&] {
         VTF_CHECK(h && out_n, VTF_E_ARG, "null argument");
         int64_t n = (int64_t)h->r.last_props.size() / 5;
         *out_n = n;
@@ -1039,7 +1062,7 @@ int vtf_roi_align(const float* d_fmap, int N, int H, int W, int C, const float* 
 
 int vtf_rcnn_profile(vtf_rcnn_t h, int enable, double* out_ms, int64_t* out_launches, double* out_flops,
                      int64_t* out_frames) {
-    return guarded([&] {
+    return guarded_on(h ? h->r.device : -1, [&] {
         VTF_CHECK(h, VTF_E_ARG, "null handle");
         Rcnn& R = h->r;
         if (out_ms) *out_ms = R.prof_ms;

@@ -11,6 +11,8 @@
 #include <cmath>
 #include <vector>
 
+#include "blob.hpp"
+#include "boxes.hpp"
 #include "common.hpp"
 #include "conv.hpp"
 
@@ -345,11 +347,6 @@ static void vit_run(Vit& V, const float* x_nhwc8, int64_t N, float* emb) {
 
 }  // namespace vtf
 
-// blob / layout helpers from other units
-namespace vtf {
-void launch_blob(const uint8_t* frames, int H, int W, int64_t fstride, int64_t rstride, const int32_t* d_crops,
-                 int64_t N, int S, float mean, float scale, int layout, int Cp, bool bf16, void* out, hipStream_t st);
-}
 
 using namespace vtf;
 
@@ -364,7 +361,7 @@ int vtf_vit_create(const float* params, int64_t n_params, int dim, int depth, in
         // dim: 64-wide heads, and k_layernorm's float4-per-lane rows (dim % 256 == 0, <= 1024)
         VTF_CHECK(params && out && dim % 256 == 0 && dim <= 256 * LN_MAXV && depth > 0, VTF_E_ARG,
                   "bad argument (dim must be a multiple of 256, at most 1024)");
-        VTF_HIP(hipSetDevice(device));
+        DeviceGuard dg(device);
         auto* h = new vtf_vit_s();
         h->v.device = device;
         h->v.D = dim;
@@ -381,25 +378,25 @@ int vtf_vit_create(const float* params, int64_t n_params, int dim, int depth, in
 }
 
 int vtf_vit_destroy(vtf_vit_t h) {
-    return guarded([&] { delete h; });
+    return guarded_on(h ? h->v.device : -1, [&] { delete h; });
 }
 
 int vtf_vit_set_precision(vtf_vit_t h, int mode) {
-    return guarded([&] {
+    return guarded_on(h ? h->v.device : -1, [&] {
         VTF_CHECK(h && (mode == 0 || mode == 2), VTF_E_ARG, "vit precision: 0 (fp32) or 2 (guarded split-fp16)");
         h->v.xmode = mode;
     });
 }
 
 int vtf_vit_set_stream(vtf_vit_t h, void* stream) {
-    return guarded([&] {
+    return guarded_on(h ? h->v.device : -1, [&] {
         VTF_CHECK(h, VTF_E_ARG, "null handle");
         h->v.st = (hipStream_t)stream;
     });
 }
 
 int vtf_vit_forward(vtf_vit_t h, const float* d_x, int64_t N, float* d_emb) {
-    return guarded([&] {
+    return guarded_on(h ? h->v.device : -1, [&] {
         VTF_CHECK(h && N >= 0, VTF_E_ARG, "bad argument");
         if (N == 0) return;
         VTF_CHECK(d_x && d_emb, VTF_E_ARG, "null argument");
@@ -410,17 +407,22 @@ int vtf_vit_forward(vtf_vit_t h, const float* d_x, int64_t N, float* d_emb) {
     });
 }
 
-int vtf_vit_encode_crops(vtf_vit_t h, const uint8_t* d_frames, int H, int W, int64_t frame_stride,
-                         int64_t row_stride, const int32_t* crops, int64_t N, float* d_emb) {
-    return guarded([&] {
-        VTF_CHECK(h && N >= 0, VTF_E_ARG, "bad argument");
+int vtf_vit_encode_crops(vtf_vit_t h, const uint8_t* d_frames, int n_frames, int H, int W, int64_t frame_stride,
+                         int64_t row_stride, const int32_t* crops, int crops_on_device, int64_t N, float* d_emb) {
+    return guarded_on(h ? h->v.device : -1, [&] {
+        VTF_CHECK(h && N >= 0 && n_frames > 0 && H > 0 && W > 0, VTF_E_ARG, "bad argument");
         if (N == 0) return;
         VTF_CHECK(d_frames && crops && d_emb, VTF_E_ARG, "null argument");
-        int32_t* dc = h->v.ar.get<int32_t>(7, N * 5);
-        VTF_HIP(hipMemcpyAsync(dc, crops, N * 5 * 4, hipMemcpyHostToDevice, h->v.st));
+        const int32_t* dc = crops;
+        if (!crops_on_device) {
+            check_crops_host(crops, N, n_frames, H, W);
+            int32_t* d = h->v.ar.get<int32_t>(7, N * 5);
+            VTF_HIP(hipMemcpyAsync(d, crops, N * 5 * 4, hipMemcpyHostToDevice, h->v.st));
+            dc = d;
+        }
         float* x8 = h->v.ar.get<float>(6, N * 128 * 128 * 8);
         // blobFromImages(images, 1/127.5, (128,128), (127.5,)*3, swapRB=True) (vit.py:141)
-        launch_blob(d_frames, H, W, frame_stride, row_stride, dc, N, 128, 127.5f, (float)(1.0 / 127.5), 1, 8, false,
+        launch_blob(d_frames, n_frames, H, W, frame_stride, row_stride, dc, N, 128, 127.5f, (float)(1.0 / 127.5), 1, 8, false,
                     x8, h->v.st);
         vit_run(h->v, x8, N, d_emb);
         VTF_HIP(hipGetLastError());

@@ -23,6 +23,7 @@
 #include <vector>
 
 #include "blob.hpp"
+#include "boxes.hpp"
 #include "common.hpp"
 #include "conv.hpp"
 #include "nms.hpp"
@@ -456,8 +457,11 @@ __global__ void k_yolo_final(const int32_t* __restrict__ keep, const int64_t* __
 }
 
 struct YOut {
-    std::vector<float> rows;  // [n,5] x1,y1,x2,y2,score
+    std::vector<float> rows;  // [n,5] x1,y1,x2,y2,score (host copy, when requested)
     std::vector<int32_t> counts;
+    const float* d_rows = nullptr;  // the same rows in HBM
+    int64_t n = 0;
+    bool host = true;
 };
 
 static void postprocess(Yolo& Y, float* const maps[3], int B, int Hp, int Wp, int H, int W, YOut& out) {
@@ -479,6 +483,8 @@ static void postprocess(Yolo& Y, float* const maps[3], int B, int Hp, int Wp, in
     for (int b = 0; b < B; b++) n += calls[b] = cnt[b];
     out.counts.assign(B, 0);
     out.rows.clear();
+    out.d_rows = nullptr;
+    out.n = 0;
     if (n == 0) return;
     float4* boxes = Y.ar.get<float4>(94, n);
     float* score = Y.ar.get<float>(95, n);
@@ -507,6 +513,9 @@ static void postprocess(Yolo& Y, float* const maps[3], int B, int Hp, int Wp, in
     // scale_boxes: torch.tensor(szo) / torch.tensor(szu) in fp32, flipped to (x, y)
     float sx = (float)W / (float)w, sy = (float)H / (float)h;
     k_yolo_final<<<B, 128, 0, st>>>(keep, doffs, boxes, score, sx, sy, top, drows);
+    out.d_rows = drows;
+    out.n = ob;
+    if (!out.host) return;
     out.rows.resize((size_t)ob * 5);
     VTF_HIP(hipMemcpyAsync(out.rows.data(), drows, ob * 20, hipMemcpyDeviceToHost, st));
     VTF_HIP(hipStreamSynchronize(st));
@@ -567,7 +576,7 @@ extern "C" {
 int vtf_yolo_create(const float* params, int64_t n_params, int device, int precision, vtf_yolo_t* out) {
     return guarded([&] {
         VTF_CHECK(params && out && (precision == 0 || precision == 1), VTF_E_ARG, "bad argument");
-        VTF_HIP(hipSetDevice(device));
+        DeviceGuard dg(device);
         auto* h = new vtf_yolo_s();
         h->y.device = device;
         h->y.bf16 = precision == 1;
@@ -582,11 +591,11 @@ int vtf_yolo_create(const float* params, int64_t n_params, int device, int preci
 }
 
 int vtf_yolo_destroy(vtf_yolo_t h) {
-    return guarded([&] { delete h; });
+    return guarded_on(h ? h->y.device : -1, [&] { delete h; });
 }
 
 int vtf_yolo_set_stream(vtf_yolo_t h, void* stream) {
-    return guarded([&] {
+    return guarded_on(h ? h->y.device : -1, [&] {
         VTF_CHECK(h, VTF_E_ARG, "null handle");
         h->y.st = (hipStream_t)stream;
     });
@@ -595,12 +604,26 @@ int vtf_yolo_set_stream(vtf_yolo_t h, void* stream) {
 int vtf_yolo_detect(vtf_yolo_t h, const uint8_t* frames, int frames_on_device, int B, int H, int W,
                     int64_t frame_stride, int64_t row_stride, float* out_boxes, float* out_scores, int32_t* out_counts,
                     int64_t cap, int64_t* out_total) {
-    return guarded([&] {
+    return guarded_on(h ? h->y.device : -1, [&] {
         VTF_CHECK(h && frames && out_counts, VTF_E_ARG, "null argument");
-        VTF_HIP(hipSetDevice(h->y.device));
         YOut r;
         detect(h->y, frames, frames_on_device, B, H, W, frame_stride, row_stride, r);
         write_out(r, B, out_boxes, out_scores, out_counts, cap, out_total);
+    });
+}
+
+int vtf_yolo_detect_crops(vtf_yolo_t h, const uint8_t* frames, int frames_on_device, int B, int H, int W,
+                          int64_t frame_stride, int64_t row_stride, const vtf_box_params* params,
+                          int32_t frame_offset, int32_t* d_crops, int32_t* out_frame_counts, int64_t cap,
+                          int64_t* out_n) {
+    return guarded_on(h ? h->y.device : -1, [&] {
+        VTF_CHECK(h && frames && params && out_n, VTF_E_ARG, "null argument");
+        YOut r;
+        r.host = false;
+        detect(h->y, frames, frames_on_device, B, H, W, frame_stride, row_stride, r);
+        VTF_CHECK(r.n == 0 || d_crops, VTF_E_ARG, "null argument");
+        rows_to_crops(h->y.ar, 110, r.d_rows, r.counts, H, W, *params, frame_offset, d_crops, nullptr,
+                      out_frame_counts, cap, out_n, h->y.st);
     });
 }
 
@@ -618,7 +641,7 @@ int vtf_yolo_input_size(int H, int W, int* out4) {
 
 int vtf_yolo_letterbox(vtf_yolo_t h, const uint8_t* d_frames, int B, int H, int W, int64_t frame_stride,
                        int64_t row_stride, float* d_out) {
-    return guarded([&] {
+    return guarded_on(h ? h->y.device : -1, [&] {
         VTF_CHECK(h && d_frames && d_out && B > 0, VTF_E_ARG, "bad argument");
         int hh, ww;
         used_size(H, W, hh, ww);
@@ -629,7 +652,7 @@ int vtf_yolo_letterbox(vtf_yolo_t h, const uint8_t* d_frames, int B, int H, int 
 }
 
 int vtf_yolo_net(vtf_yolo_t h, const float* d_x, int B, int Hp, int Wp, float* d_map0, float* d_map1, float* d_map2) {
-    return guarded([&] {
+    return guarded_on(h ? h->y.device : -1, [&] {
         VTF_CHECK(h && d_x && d_map0 && d_map1 && d_map2 && B > 0, VTF_E_ARG, "bad argument");
         Yolo& Y = h->y;
         void* x0 = Y.ar.get(105, (size_t)B * Hp * Wp * 8 * (Y.bf16 ? 2 : 4));
@@ -643,7 +666,7 @@ int vtf_yolo_net(vtf_yolo_t h, const float* d_x, int B, int Hp, int Wp, float* d
 int vtf_yolo_postprocess(vtf_yolo_t h, const float* d_map0, const float* d_map1, const float* d_map2, int B, int H,
                          int W, float* out_boxes, float* out_scores, int32_t* out_counts, int64_t cap,
                          int64_t* out_total) {
-    return guarded([&] {
+    return guarded_on(h ? h->y.device : -1, [&] {
         VTF_CHECK(h && d_map0 && d_map1 && d_map2 && out_counts && B > 0, VTF_E_ARG, "bad argument");
         int hh, ww;
         used_size(H, W, hh, ww);
@@ -656,7 +679,7 @@ int vtf_yolo_postprocess(vtf_yolo_t h, const float* d_map0, const float* d_map1,
 
 int vtf_yolo_profile(vtf_yolo_t h, int enable, double* out_ms, int64_t* out_launches, double* out_flops,
                      int64_t* out_frames) {
-    return guarded([&] {
+    return guarded_on(h ? h->y.device : -1, [&] {
         VTF_CHECK(h, VTF_E_ARG, "null handle");
         Yolo& Y = h->y;
         if (out_ms) *out_ms = Y.prof_ms;

@@ -42,14 +42,14 @@ SIGNATURES = {
     'vtf_facenet_destroy': [_p],
     'vtf_facenet_set_stream': [_p, _p],
     'vtf_facenet_forward': [_p, _p, _i64, _p],
-    'vtf_facenet_encode_crops': [_p, _p, _i32, _i32, _i64, _i64, _p, _i64, _p],
+    'vtf_facenet_encode_crops': [_p, _p, _i32, _i32, _i32, _i64, _i64, _p, _i32, _i64, _p],
     'vtf_vit_create': [_p, _i64, _i32, _i32, _i32, _p],
     'vtf_vit_destroy': [_p],
     'vtf_vit_set_stream': [_p, _p],
     'vtf_vit_set_precision': [_p, _i32],
     'vtf_vit_forward': [_p, _p, _i64, _p],
-    'vtf_vit_encode_crops': [_p, _p, _i32, _i32, _i64, _i64, _p, _i64, _p],
-    'vtf_blob_from_crops': [_p, _i32, _i32, _i64, _i64, _p, _i64, _i32, _f32, _f32, _p, _p],
+    'vtf_vit_encode_crops': [_p, _p, _i32, _i32, _i32, _i64, _i64, _p, _i32, _i64, _p],
+    'vtf_blob_from_crops': [_p, _i32, _i32, _i32, _i64, _i64, _p, _i64, _i32, _f32, _f32, _p, _p],
     'vtf_cosine_dedupe': [_p, _i64, _i64, _p, _p, _p],
     'vtf_group_create': [_i32, _p],
     'vtf_group_destroy': [_p],
@@ -73,7 +73,11 @@ SIGNATURES = {
     'vtf_yolo_postprocess': [_p, _p, _p, _p, _i32, _i32, _i32, _p, _p, _p, _i64, _p],
     'vtf_yolo_profile': [_p, _i32, _p, _p, _p, _p],
     'vtf_cosine_classify': [_p, _i64, _p, _i64, _i64, _p, _p, _p],
-    'vtf_ahash_crops': [_p, _i32, _i32, _i64, _i64, _p, _i64, _p, _p],
+    'vtf_ahash_crops': [_p, _i32, _i32, _i32, _i64, _i64, _p, _i64, _p, _p],
+    'vtf_boxes_to_crops': [_p, _p, _i32, _i32, _i32, _p, _i32, _p, _p, _p, _i64, _p, _p],
+    'vtf_mtcnn_detect_crops': [_p, _p, _i32, _i32, _i32, _i32, _i64, _i64, _f64, _p, _i32, _p, _p, _i64, _p],
+    'vtf_yolo_detect_crops': [_p, _p, _i32, _i32, _i32, _i32, _i64, _i64, _p, _i32, _p, _p, _i64, _p],
+    'vtf_rcnn_detect_crops': [_p, _p, _i32, _i32, _i32, _i32, _i64, _i64, _p, _i32, _p, _p, _i64, _p],
     'vtf_hamming_dedupe': [_p, _i64, _p, _p, _p],
     'vtf_rcnn_create': [_p, _i64, _i32, _i32, _p],
     'vtf_rcnn_destroy': [_p],
@@ -89,6 +93,20 @@ SIGNATURES = {
 _RESTYPE = {'vtf_last_error': _c.c_char_p}
 
 _LIB = None
+
+
+class BoxParams(ctypes.Structure):
+    """vtf_box_params (include/vtf.h): the box filter / adjust settings of video_to_faces
+    (det_min_score, det_min_size, det_min_border, det_scale, det_square; main.py:50-51)."""
+    _fields_ = [('min_score', _c.c_float), ('min_size', _c.c_double), ('min_border', _c.c_double),
+                ('scale', _c.c_double * 4), ('square', _c.c_int32), ('adjust', _c.c_int32)]
+
+    @classmethod
+    def make(cls, mscore=0.4, msize=50, mborder=5, scale=(1.5, 1.5, 2.2, 1.2), square=True, adjust=True):
+        if isinstance(scale, int):  # adjust_boxes accepts one int for all four (detection.py:221-222)
+            scale = (scale,) * 4
+        return cls(float(mscore), float(msize), float(mborder or 0), (_c.c_double * 4)(*[float(v) for v in scale]),
+                   1 if square else 0, 1 if adjust else 0)
 
 
 def lib():
@@ -139,9 +157,38 @@ def stream_ptr(device):
     return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
 
 
-def frames_view(imgs):
+def device_of(model, default=None):
+    """torch.device a model wrapper (RealMTCNN/RealYOLO/AnimeFRCNN/FaceNet/AnimeVIT or their
+    handles) runs on."""
+    for obj in (model, getattr(model, 'model', None)):
+        d = getattr(obj, 'device', None)
+        if d is not None:
+            return torch.device(d)
+    return require_gpu(default)
+
+
+def run_detect_crops(call, device, B, cap):
+    """Drive a vtf_*_detect_crops entry point: call(d_crops, frame_counts, cap, byref(n)) -> rc.
+    Returns (device int32 crops [n,5], host int32 per-frame crop counts [B]).  The capacity bound
+    is the detector's row count; on VTF_E_CAPACITY the call is repeated with the reported size."""
+    import numpy as np
+    counts = np.zeros(B, np.int32)
+    n = _c.c_int64(0)
+    while True:
+        crops = torch.empty((max(int(cap), 1), 5), dtype=torch.int32, device=device)
+        rc = call(ptr(crops), counts.ctypes.data, int(cap), _c.byref(n))
+        if rc == VTF_E_CAPACITY:
+            cap = int(n.value)
+            continue
+        check(rc)
+        return crops[:n.value], counts
+
+
+def frames_view(imgs, device=None):
     """Frames argument of the detectors: np.ndarray uint8 [B,H,W,3] (any non-negative
-    strides with packed pixels), a list of frames, or a uint8 CUDA tensor in HBM.
+    strides with packed pixels), a list of frames, or a uint8 CUDA tensor in HBM.  A CUDA
+    tensor must live on `device` (the handle's GPU): a kernel on one GPU cannot read another's
+    HBM through a raw pointer.
     Returns (base pointer, on_device, B, H, W, frame_stride, row_stride, owner)."""
     import numpy as np
     import torch
@@ -149,6 +196,8 @@ def frames_view(imgs):
         t = imgs
         if t.dtype != torch.uint8 or t.dim() != 4 or t.shape[3] != 3:
             raise ValueError('frames tensor must be uint8 [B,H,W,3]')
+        if t.is_cuda and device is not None and t.device != torch.device(device):
+            raise ValueError('frames tensor is on %s, the model runs on %s' % (t.device, device))
         if t.stride(3) != 1 or t.stride(2) != 3:
             t = t.contiguous()
         B, H, W = t.shape[:3]

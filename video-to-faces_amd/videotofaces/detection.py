@@ -3,11 +3,13 @@
 get_detector_model keeps the reference's style coupling (detection.py:22-29); detect_faces /
 process_frames_batch mirror the detection stage (detection.py:32-158) with the frames of a
 det-batch uploaded to HBM once (detector, average hashes of the crops).  The box
-post-processing (filter_boxes 174-217, adjust_boxes 220-262, get_crops 161-162) is the
-reference's integer logic, kept on the host (a few boxes per frame); frames may stay in HBM:
-``detect_and_crop`` returns crop rectangles that the encoder consumes on device
-(vtf_facenet_encode_crops), replacing the reference's JPEG write/read hand-off.
+post-processing (filter_boxes 174-217, adjust_boxes 220-262, get_crops 161-162) runs on the
+device (vtf_boxes_to_crops, csrc/boxes.hip) straight on the detector's rows in HBM:
+``detect_crops`` returns device crop rectangles that the encoders consume on device
+(vtf_*_encode_crops), replacing the reference's JPEG write/read hand-off.
 """
+import ctypes
+
 import numpy as np
 
 
@@ -24,67 +26,60 @@ def get_detector_model(style, det_model, device):
     return 0
 
 
-def check_box(box, img_size, mscore, msize, mborder):
-    """detection.py:165-171"""
-    x1, y1, x2, y2, score = box
-    H, W = img_size
-    c1 = score < mscore
-    c2 = x2 - x1 < msize or y2 - y1 < msize
-    c3 = mborder and (x1 < mborder or y1 < mborder or x2 > W - mborder or y2 > H - mborder)
-    return (c1, c2, c3)
+def _rows_to_crops(rows, img_size, params, frame_offset=0, device=None):
+    """Host detector rows (list of [n_i,5] fp32 arrays, one per frame) through the device box
+    kernel (vtf_boxes_to_crops) -> (crops int32 [N,5], source row per crop, per-frame counts)."""
+    import torch
+    from . import _native as nat
+    dev = nat.require_gpu(device)
+    B = len(rows)
+    counts = np.array([len(r) for r in rows], np.int32)
+    flat = np.concatenate([np.asarray(r, np.float32).reshape(-1, 5) for r in rows]) if B else np.zeros((0, 5), np.float32)
+    n = flat.shape[0]
+    if B == 0:
+        return np.zeros((0, 5), np.int32), np.zeros(0, np.int32), counts
+    d_rows = torch.from_numpy(np.ascontiguousarray(flat)).to(dev)
+    d_crops = torch.empty((max(n, 1), 5), dtype=torch.int32, device=dev)
+    d_src = torch.empty(max(n, 1), dtype=torch.int32, device=dev)
+    fc = np.zeros(B, np.int32)
+    m = ctypes.c_int64(0)
+    H, W = int(img_size[0]), int(img_size[1])
+    with torch.cuda.device(dev):
+        nat.check(nat.lib().vtf_boxes_to_crops(nat.ptr(d_rows), counts.ctypes.data, B, H, W, ctypes.byref(params),
+                                               int(frame_offset), nat.ptr(d_crops), nat.ptr(d_src), fc.ctypes.data,
+                                               max(n, 1), ctypes.byref(m), nat.stream_ptr(dev)))
+    k = m.value
+    return d_crops[:k].cpu().numpy(), d_src[:k].cpu().numpy(), fc
 
 
-def filter_boxes(boxes, img_size, mscore, msize, mborder):
-    """detection.py:174-180 (the rejects / frames saving side effects are IO, not here)."""
-    boxes = [(int(np.floor(x1)), int(np.floor(y1)), int(np.ceil(x2)), int(np.ceil(y2)), score)
-             for (x1, y1, x2, y2, score) in boxes]
-    return [b for b in boxes if not any(check_box(b, img_size, mscore, msize, mborder))]
+def filter_boxes(boxes, img_size, mscore, msize, mborder, *debug_io, device=None):
+    """filter_boxes (detection.py:174-217) on the device box kernel: integer-rounded boxes that
+    pass check_box (score, size, border), as (x1, y1, x2, y2, score) tuples.  The reference's
+    save_frames / save_rejects debug IO (its trailing arguments) is not mirrored."""
+    from . import _native as nat
+    b = np.asarray(boxes, np.float32).reshape(-1, 5)
+    cr, src, _ = _rows_to_crops([b], img_size, nat.BoxParams.make(mscore, msize, mborder, adjust=False),
+                                device=device)
+    return [(int(c[1]), int(c[2]), int(c[3]), int(c[4]), b[i, 4]) for c, i in zip(cr, src)]
 
 
-def adjust_boxes(boxes, img_size, scale, square):
-    """detection.py:220-262"""
-    if isinstance(scale, int):
-        scale = (scale, scale, scale, scale)
-    (sx1, sx2, sy1, sy2) = scale
-    H, W = img_size
-    adjusted = []
-    for (x1, y1, x2, y2, score) in boxes:
-        w, h = x2 - x1, y2 - y1
-        xc, yc = x1 + w / 2, y1 + h / 2
-        x1 = int(np.floor(max(0, xc - sx1 * w / 2)))
-        x2 = int(np.ceil(min(W, xc + sx2 * w / 2)))
-        y1 = int(np.floor(max(0, yc - sy1 * h / 2)))
-        y2 = int(np.ceil(min(H, yc + sy2 * h / 2)))
-        w, h = x2 - x1, y2 - y1
-        if square:
-            if h > w:
-                d = h - w
-                x1 -= d // 2
-                x2 += d - d // 2
-                if x1 < 0: x2 += abs(x1); x1 = 0; x2 = min(W, x2)  # noqa: E701,E702
-                if x2 > W: x1 -= x2 - W; x2 = W; x1 = max(0, x1)  # noqa: E701,E702
-            elif w > h:
-                d = w - h
-                y1 -= d // 2
-                y2 += d - d // 2
-                if y1 < 0: y2 += abs(y1); y1 = 0; y2 = min(H, y2)  # noqa: E701,E702
-                if y2 > H: y1 -= y2 - H; y2 = H; y1 = max(0, y1)  # noqa: E701,E702
-            w, h = x2 - x1, y2 - y1
-            if w > H:
-                d = w - H
-                x1 += d // 2
-                x2 -= d - d // 2
-            elif h > W:
-                d = h - W
-                y1 += d // 2
-                y2 -= d - d // 2
-        adjusted.append((x1, y1, x2, y2, score))
-    return adjusted
+def adjust_boxes(boxes, img_size, scale, square, device=None):
+    """adjust_boxes (detection.py:220-262) on the device box kernel; boxes are filter_boxes
+    output (integer corners, score)."""
+    from . import _native as nat
+    b = np.asarray([tuple(x) for x in boxes], np.float32).reshape(-1, 5)
+    keep_all = nat.BoxParams.make(float('-inf'), float('-inf'), 0, scale, square)
+    cr, src, _ = _rows_to_crops([b], img_size, keep_all, device=device)
+    return [(int(c[1]), int(c[2]), int(c[3]), int(c[4]), boxes[i][4]) for c, i in zip(cr, src)]
 
 
 def get_crops(img, boxes):
-    """detection.py:161-162"""
-    return [img[y1: y2, x1: x2] for (x1, y1, x2, y2, _) in boxes]
+    """detection.py:161-162: the frame slice of every (x1, y1, x2, y2, score) box."""
+    out = []
+    for b in boxes:
+        x1, y1, x2, y2 = b[:4]
+        out.append(img[y1:y2, x1:x2])
+    return out
 
 
 DEFAULT_DET_PARAMS = dict(mscore=0.4, msize=50, mborder=5, scale=(1.5, 1.5, 2.2, 1.2), square=True)
@@ -99,14 +94,24 @@ def normalize_detout(detout):
 
 
 def boxes_to_crops(detout, img_size, frame_offset=0, mscore=0.4, msize=50, mborder=5,
-                   scale=(1.5, 1.5, 2.2, 1.2), square=True):
-    """process_frames_batch steps 2-5 (detection.py:133-152): filter, adjust, flatten in
-    (frame, face) order -> int32 [N,5] (frame index, x1, y1, x2, y2)."""
-    out = []
-    for i, b in enumerate(normalize_detout(detout)):
-        bx = adjust_boxes(filter_boxes(b, img_size, mscore, msize, mborder), img_size, scale, square)
-        out.extend((frame_offset + i, x1, y1, x2, y2) for (x1, y1, x2, y2, _) in bx)
-    return np.array(out, np.int32).reshape(-1, 5)
+                   scale=(1.5, 1.5, 2.2, 1.2), square=True, device=None):
+    """process_frames_batch steps 2-5 (detection.py:133-152) for host detector output, on the
+    device box kernel -> int32 [N,5] (frame_offset + frame, x1, y1, x2, y2) in (frame, face)
+    order."""
+    from . import _native as nat
+    rows = normalize_detout(detout)
+    cr, _, _ = _rows_to_crops(rows, img_size, nat.BoxParams.make(mscore, msize, mborder, scale, square),
+                              frame_offset, device)
+    return cr
+
+
+def detect_crops(model, frames_dev, frame_offset=0, mscore=0.4, msize=50, mborder=5,
+                 scale=(1.5, 1.5, 2.2, 1.2), square=True):
+    """model(frames) + process_frames_batch steps 2-5 with nothing on the host but counts:
+    -> (device int32 crops [N,5], host per-frame counts).  model: RealMTCNN / RealYOLO /
+    AnimeFRCNN or their handles (their detect_crops)."""
+    from . import _native as nat
+    return model.detect_crops(frames_dev, nat.BoxParams.make(mscore, msize, mborder, scale, square), frame_offset)
 
 
 # ------------------------------------------------------------------ detection stage (detection.py:32-158)
@@ -147,32 +152,35 @@ def frame_source(path, video_reader='opencv'):
 
 
 def process_frames_batch(frames, indices, model, det_params, save_params, hash_thr, hashes):
-    """detection.py:126-158 with the frames uploaded to HBM once: detect, filter/adjust on the
-    host (integer box logic), average hashes of the crops on device, nearest-5 hash dedupe,
-    JPEG save.  Returns (file names, updated `hashes` list)."""
+    """detection.py:126-158 with the frames uploaded to HBM once: detect and filter/adjust the
+    boxes on device (detect_crops), average hashes of the crops on device, nearest-5 hash
+    dedupe, JPEG save.  Returns (file names, updated `hashes` list)."""
     import os.path as osp
     import numpy as np
     import torch
     from .dupes import ahash_crops, ahash, nearest_dupes
     from .utils import resize_keep_ratio, imwrite
+    from . import _native as nat
     _, mscore, msize, mborder, scale, square = det_params
     out_dir, out_prefix, resize_to, _, _, _ = save_params
-    imsize = frames.shape[1:3]
-    fr_dev = torch.from_numpy(np.ascontiguousarray(frames)).cuda()
-    boxes = normalize_detout(model(fr_dev))
-    faces, rects = [], []
-    for b, fi, fidx in zip(boxes, range(len(frames)), indices):
-        bx = adjust_boxes(filter_boxes(b, imsize, mscore, msize, mborder), imsize, scale, square)
-        for j, (x1, y1, x2, y2, _) in enumerate(bx):
-            faces.append((frames[fi][y1:y2, x1:x2], out_prefix + '%06d_%u.jpg' % (fidx, j)))
-            rects.append((fi, x1, y1, x2, y2))
+    fr_dev = torch.from_numpy(np.ascontiguousarray(frames)).to(nat.device_of(model))
+    # detector + box post-processing on device; only the crop rectangles come back for the
+    # JPEG slices and file names
+    with torch.inference_mode():
+        d_crops, _ = detect_crops(model, fr_dev, 0, mscore, msize, mborder, scale, square)
+    rects = d_crops.cpu().numpy()
+    faces, seen = [], {}
+    for fi, x1, y1, x2, y2 in rects.tolist():
+        j = seen.get(fi, 0)
+        seen[fi] = j + 1
+        faces.append((frames[fi][y1:y2, x1:x2], out_prefix + '%06d_%u.jpg' % (indices[fi], j)))
     if resize_to:
         faces = [(resize_keep_ratio(img, resize_to), fn) for (img, fn) in faces]
     if hash_thr and hash_thr != -1 and faces:
         if resize_to:  # the reference hashes the resized face (detection.py:149-153)
-            hs = [int(sum(int(v) << k for k, v in enumerate(ahash(img)))) for img, _ in faces]
+            hs = [int(sum(int(v) << k for k, v in enumerate(ahash(img, fr_dev.device)))) for img, _ in faces]
         else:
-            hs = ahash_crops(fr_dev, np.array(rects))
+            hs = ahash_crops(fr_dev, rects)
         flags, _ = nearest_dupes(list(zip(hs, [fn for _, fn in faces])), hashes, hash_thr)
         faces = [f for f, d in zip(faces, flags) if not d]
     for img, fn in faces:

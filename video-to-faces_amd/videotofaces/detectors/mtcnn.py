@@ -42,7 +42,7 @@ class MTCNN:
     def forward(self, imgs, minsize=20, return_landmarks=False):
         L = nat.lib()
         self._bind_stream()
-        base, on_dev, B, H, W, fstride, rstride, keep_alive = nat.frames_view(imgs)
+        base, on_dev, B, H, W, fstride, rstride, keep_alive = nat.frames_view(imgs, self.device)
         cap = max(64, 256 * B)
         while True:
             boxes = np.empty((cap, 5), np.float32)
@@ -72,6 +72,23 @@ class MTCNN:
         return res
 
     __call__ = forward
+
+    def detect_crops(self, imgs, minsize, box_params, frame_offset=0):
+        """forward + box post-processing on device (detection.py:131-145 without the host):
+        -> (device int32 crops [N,5] = frame_offset + frame, x1, y1, x2, y2; host per-frame counts).
+        box_params: _native.BoxParams."""
+        L = nat.lib()
+        self._bind_stream()
+        base, on_dev, B, H, W, fstride, rstride, keep_alive = nat.frames_view(imgs, self.device)
+        out = nat.run_detect_crops(
+            lambda d, c, cap, n: L.vtf_mtcnn_detect_crops(self._h, base, on_dev, B, H, W, fstride, rstride,
+                                                          float(minsize), ctypes.byref(box_params), int(frame_offset),
+                                                          d, c, cap, n), self.device, B, 64 * B)
+        del keep_alive
+        st = np.zeros(8, np.int64)
+        nat.check(L.vtf_mtcnn_stats(self._h, st.ctypes.data))
+        self.last_stats = st
+        return out
 
     def profile(self, enable):
         """Start (enable=True, resets) or stop kernel timing of the fused pyramid+PNet kernel;
@@ -136,6 +153,9 @@ class RealMTCNN():
         with torch.inference_mode():
             boxes = self.model(frames, self.minsize)
         return boxes
+
+    def detect_crops(self, frames, box_params, frame_offset=0):
+        return self.model.detect_crops(frames, self.minsize, box_params, frame_offset)
 
 
 def batched_nms(boxes, scores, idxs, iou_threshold):

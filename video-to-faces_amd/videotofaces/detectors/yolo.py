@@ -75,12 +75,25 @@ class YOLOv3:
     def forward(self, imgs):
         L = nat.lib()
         self._bind_stream()
-        base, on_dev, B, H, W, fs, rs, keep_alive = nat.frames_view(imgs)
+        base, on_dev, B, H, W, fs, rs, keep_alive = nat.frames_view(imgs, self.device)
         out = self._run(lambda *o: L.vtf_yolo_detect(self._h, base, on_dev, B, H, W, fs, rs, *o), B)
         del keep_alive
         return out
 
     __call__ = forward
+
+    def detect_crops(self, imgs, box_params, frame_offset=0):
+        """forward + box post-processing on device -> (device int32 crops [N,5], host per-frame
+        counts), as MTCNN.detect_crops."""
+        L = nat.lib()
+        self._bind_stream()
+        base, on_dev, B, H, W, fs, rs, keep_alive = nat.frames_view(imgs, self.device)
+        out = nat.run_detect_crops(
+            lambda d, c, cap, n: L.vtf_yolo_detect_crops(self._h, base, on_dev, B, H, W, fs, rs,
+                                                         ctypes.byref(box_params), int(frame_offset), d, c, cap, n),
+            self.device, B, 100 * B)
+        del keep_alive
+        return out
 
     def profile(self, enable):
         """Start (enable=True, resets) or stop timing of the conv stack (75 conv launches
@@ -133,3 +146,6 @@ class RealYOLO():
     def __call__(self, imgs):
         with torch.inference_mode():
             return self.model(imgs)
+
+    def detect_crops(self, frames, box_params, frame_offset=0):
+        return self.model.detect_crops(frames, box_params, frame_offset)

@@ -51,26 +51,26 @@ def ahash_crops(frames_dev, crops):
     if c.shape[0] == 0:
         return out
     B, H, W = frames_dev.shape[:3]
-    nat.check(nat.lib().vtf_ahash_crops(nat.ptr(frames_dev), H, W, frames_dev.stride(0), frames_dev.stride(1),
+    nat.check(nat.lib().vtf_ahash_crops(nat.ptr(frames_dev), B, H, W, frames_dev.stride(0), frames_dev.stride(1),
                                         c.ctypes.data, c.shape[0], out.ctypes.data, nat.stream_ptr(frames_dev.device)))
     return out
 
 
-def ahash(img):
+def ahash(img, device=None):
     """dupes.ahash (dupes.py:11-15) of one uint8 BGR image -> 64-element 0/1 array."""
-    t = torch.from_numpy(np.ascontiguousarray(img)[None]).cuda()
+    t = torch.from_numpy(np.ascontiguousarray(img)[None]).to(nat.require_gpu(device))
     h, w = img.shape[:2]
     return unpack_hash(ahash_crops(t, [[0, 0, 0, w, h]])[0])
 
 
-def hamming_lower(H):
+def hamming_lower(H, device=None):
     """hash branch distances (dupes.py:55-64) on the GPU: min / first argmin over j < i of the
     Hamming distance of the 64-bit average hashes; row 0 -> (10000, 0)."""
     h = pack_hashes(H)
     n = h.shape[0]
     if n == 0:
         return np.zeros(0, np.int32), np.zeros(0, np.int64)
-    dev = torch.device('cuda:0')
+    dev = nat.require_gpu(device)
     d = torch.from_numpy(h.view(np.int64)).to(dev)
     mins = torch.empty(n, dtype=torch.int32, device=dev)
     inds = torch.empty(n, dtype=torch.int64, device=dev)
@@ -100,12 +100,13 @@ def nearest_dupes(hashes, prev, hash_thr):
     return flags, log
 
 
-def remove_dupes_overall(X, filenames, dup_params):
+def remove_dupes_overall(X, filenames, dup_params, device=None):
+    """dupes.py:51-93; `device` (an addition) picks the GPU, default cuda:0."""
     measure_type, threshold, save_dupes, out_dir = dup_params
     if measure_type == 'hash':
-        mins, inds = hamming_lower(X)
+        mins, inds = hamming_lower(X, device)
     else:
-        dev = torch.device('cuda:0')
+        dev = nat.require_gpu(device)
         mins, inds = cosine_dedupe_device(torch.from_numpy(np.ascontiguousarray(X, np.float32)).to(dev))
     idx = (mins <= threshold).nonzero()[0]
     sidx = set(idx.tolist())

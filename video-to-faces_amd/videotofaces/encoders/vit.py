@@ -58,15 +58,27 @@ class ViT:
     __call__ = forward
 
     def encode_crops(self, frames_dev, crops):
-        c = np.ascontiguousarray(crops, dtype=np.int32).reshape(-1, 5)
+        """frames_dev: CUDA uint8 [F,H,W,3]; crops int [N,5] (frame, x1, y1, x2, y2): a host array
+        (validated against the frames) or a CUDA int32 tensor on this device (e.g. from
+        detect_crops) -> [N,D] embeddings on device."""
+        if isinstance(crops, torch.Tensor) and crops.is_cuda:
+            if crops.device != self.device:
+                raise ValueError('crops are on %s, the encoder runs on %s' % (crops.device, self.device))
+            c = crops.to(torch.int32).contiguous().reshape(-1, 5)
+            on_dev, cptr = 1, nat.ptr(c)
+        else:
+            c = np.ascontiguousarray(crops, dtype=np.int32).reshape(-1, 5)
+            on_dev, cptr = 0, c.ctypes.data
         n = c.shape[0]
         out = torch.empty((n, self.dim), dtype=torch.float32, device=self.device)
         if n == 0:
             return out
-        B, H, W = frames_dev.shape[:3]
+        if frames_dev.device != self.device:
+            raise ValueError('frames are on %s, the encoder runs on %s' % (frames_dev.device, self.device))
+        F, H, W = frames_dev.shape[:3]
         self._bind()
-        nat.check(nat.lib().vtf_vit_encode_crops(self._h, nat.ptr(frames_dev), H, W, frames_dev.stride(0),
-                                                 frames_dev.stride(1), c.ctypes.data, n, nat.ptr(out)))
+        nat.check(nat.lib().vtf_vit_encode_crops(self._h, nat.ptr(frames_dev), F, H, W, frames_dev.stride(0),
+                                    frames_dev.stride(1), cptr, on_dev, n, nat.ptr(out)))
         return out
 
 
