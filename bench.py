@@ -1,335 +1,666 @@
-"""Benchmark: faces/sec end-to-end (detect + encode) on synthetic 1280x720 frames.
+"""Benchmark: faces/sec end-to-end (detect + encode) on synthetic frames, 1..8 GPUs of one node.
 
-Workload (BASELINE.json configs[1]): MTCNN (min_face_size=5, RealMTCNN default) + FaceNet,
-det-batch 16, enc-batch 128, frames resident in HBM.  One step = one det-batch per GPU:
-  MTCNN detect (fp32-grade: split-fp16 matrix-core convs; pyramid + P/R/O-Net + NMS on device)
-  -> reference box post-processing (filter_boxes / adjust_boxes, detection.py:174-262, host)
-  -> crop + INTER_LINEAR resize + FaceNet on device (bf16 by default; --enc-precision fp32).
---det-model yolo runs configs[2] instead: YOLOv3 (letterbox + Darknet53 + decode + NMS on
-device, fp32 or --det-precision bf16) + FaceNet, det-batch 32.
-The timed region ends with the RCCL all-gather-v of every rank's embeddings (the exchange
-step before grouping).  value = faces encoded by all ranks / max-over-ranks wall time.
+Workloads (BASELINE.json configs; --config picks the preset, single flags override it):
+  c2 (default)  MTCNN (min_face_size=5, RealMTCNN default) + FaceNet bf16, det-batch 16,
+                enc-batch 128, 720p frames resident in HBM.  One step = one det-batch per GPU:
+                MTCNN (fp32-grade split-fp16 matrix-core convs; pyramid + P/R/O-Net + NMS on device)
+                -> box post-processing on device (filter_boxes / adjust_boxes, detection.py:174-262)
+                -> crop + INTER_LINEAR resize + FaceNet on device, fed in batches of exactly
+                enc-batch (encode_faces, grouping.py:29-40).
+  c3            YOLOv3 (fp32, letterbox + Darknet53 + decode + NMS on device) + FaceNet, det-batch 32.
+  c4            ViT-L/16 encoder only, enc-batch 128 over pre-cropped 224x224 faces in HBM; one step
+                = one enc-batch per GPU.
+  c5            YOLOv3 + ViT-L/16 on 1080p frames; after the timed detect+encode region, the
+                gathered embeddings go through the cosine dedupe and the K-means k=2..16 sweep
+                sharded by k across ranks (timed separately: `grouping`).
+The timed region ends with the RCCL all-gather-v of every rank's embeddings (the exchange step
+before grouping).  value = faces encoded by all ranks / max-over-ranks wall time.
 
-  python bench.py [--gpus N --steps K --warmup W]
-  torchrun --nproc-per-node N bench.py --gpus N ...   (one process per GPU, RCCL)
+  python bench.py [--gpus N --steps K --warmup W] [--config c2|c3|c4|c5]
+With --gpus N > 1 and no torchrun environment the script starts
+`torch.distributed.run --nproc-per-node N` itself (before touching a GPU) and exits with its code;
+under torchrun WORLD_SIZE must equal --gpus.
 """
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import threading
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
-sys.path[:0] = [ROOT, os.path.join(ROOT, 'video-to-faces_amd')]
+for _p in (ROOT, os.path.join(ROOT, 'video-to-faces_amd')):
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
 
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
-FP32_PEAK_TFLOPS = 157.3  # MI355X dense fp32 (vector = f32 MFMA), MI355X_MICROARCH.md
+FP32_PEAK_TFLOPS = 157.3  # MI355X dense fp32 (f32 MFMA), MI355X_MICROARCH.md
 BF16_PEAK_TFLOPS = 2500.0  # MI355X dense bf16 MFMA (no sparsity), MI355X_MICROARCH.md
-# k_pnet's convs run on the fp16 matrix cores with split operands (x0 w0 + 2^-11 (x0 w1 + x1 w0):
-# three fp16 products per fp32-grade product), so its fp32-equivalent ceiling is fp16 dense / 3
+# split-fp16 operands (x0 w0 + 2^-11 (x0 w1 + x1 w0)): three fp16 products per fp32-grade product
 F16X_PEAK_TFLOPS = round(BF16_PEAK_TFLOPS / 3, 1)
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E (MI355X_MICROARCH.md)
 LBL_BYTES_PER_FLOP = 2075e6 / 38.66e9  # PNet layer-by-layer fp32 bytes per FLOP
-H, W = 720, 1280  # --frame 1080p: 1080, 1920
+VIT_GFLOP = {'vit_b': 11.27, 'vit_l': 39.78}  # per face at 128x128
 ENC_NAMES = {'facenet': 'FaceNet', 'vit_b': 'ViT-B/16', 'vit_l': 'ViT-L/16'}
+CONFIGS = {
+    'c2': dict(det_model='mtcnn', enc_model='facenet', enc_precision='bf16', frame='720p', det_batch=16),
+    'c3': dict(det_model='yolo', enc_model='facenet', enc_precision='bf16', frame='720p', det_batch=32),
+    'c4': dict(det_model='none', enc_model='vit_l', enc_precision='f16x', frame='224'),
+    'c5': dict(det_model='yolo', enc_model='vit_l', enc_precision='f16x', frame='1080p', det_batch=32,
+               grouping=True),
+}
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument('--gpus', type=int, default=1)
     ap.add_argument('--steps', type=int, default=20)
     ap.add_argument('--warmup', type=int, default=3)
-    ap.add_argument('--det-model', default='mtcnn', choices=['mtcnn', 'yolo'])
+    ap.add_argument('--config', default='c2', choices=sorted(CONFIGS))
+    ap.add_argument('--det-model', choices=['mtcnn', 'yolo', 'none'])
     ap.add_argument('--det-precision', default='fp32', choices=['fp32', 'bf16'], help='YOLO conv precision')
-    ap.add_argument('--det-batch', type=int, default=None, help='default 16 (mtcnn) / 32 (yolo)')
+    ap.add_argument('--det-batch', type=int)
+    ap.add_argument('--enc-model', choices=['facenet', 'vit_b', 'vit_l'])
     ap.add_argument('--enc-batch', type=int, default=128)
-    ap.add_argument('--enc-precision', default='bf16', choices=['bf16', 'fp32'])
+    ap.add_argument('--enc-precision', choices=['bf16', 'fp32', 'f16x'],
+                    help='FaceNet: bf16 | fp32; ViT: f16x (guarded split-fp16) | fp32')
+    ap.add_argument('--frame', choices=['720p', '1080p', '224'])
     ap.add_argument('--min-face-size', type=float, default=5.0)
     ap.add_argument('--pool', type=int, default=32, help='distinct synthetic frames per rank (cycled)')
     ap.add_argument('--lanes', type=int, default=3, help='concurrent det-batch pipelines (threads + HIP streams) per GPU')
+    ap.add_argument('--sustain-frames', type=int, default=10000,
+                    help='frames of the sustained leg (BASELINE config 2: 10k frames), 0 = skip')
     ap.add_argument('--cpu-frames', type=int, default=None,
-                    help='frames in the bounded CPU-baseline sample (default 12 mtcnn / 32 yolo, ~10 s of CPU work)')
+                    help='frames in the bounded CPU-baseline sample (default 12 mtcnn / 24 yolo, ~10-20 s of CPU work)')
     ap.add_argument('--no-cpu-baseline', action='store_true')
+    ap.add_argument('--no-extras', action='store_true', help='skip the solo / sustained / host-frame / drift legs')
     # box post-processing (detection.py:174-262): reference defaults except det_min_size,
     # because synthetic-weight detections are mostly < 50 px and would never reach the encoder
     ap.add_argument('--det-min-score', type=float, default=0.4)
     ap.add_argument('--det-min-size', type=int, default=None, help='default 0 (mtcnn) / 50 (yolo)')
     ap.add_argument('--det-min-border', type=int, default=5)
-    ap.add_argument('--enc-model', default='facenet', choices=['facenet', 'vit_b', 'vit_l'],
-                    help='vit_*: ViT-B/L-16 encoder (BASELINE config 5 pairs YOLO with ViT-L); '
-                         'its GEMMs run split-fp16 unless --enc-precision fp32')
-    ap.add_argument('--frame', default='720p', choices=['720p', '1080p'])
-    a = ap.parse_args()
-    global H, W
-    H, W = (1080, 1920) if a.frame == '1080p' else (720, 1280)
+    a = ap.parse_args(argv)
+    preset = CONFIGS[a.config]
+    for k in ('det_model', 'enc_model', 'enc_precision', 'frame', 'det_batch'):
+        if getattr(a, k) is None:
+            setattr(a, k, preset.get(k))
+    a.grouping = preset.get('grouping', False)
+    if a.enc_model == 'facenet' and a.enc_precision == 'f16x':
+        a.enc_precision = 'bf16'
+    if a.enc_model != 'facenet' and a.enc_precision == 'bf16':
+        a.enc_precision = 'f16x'
     yolo = a.det_model == 'yolo'
     if a.det_batch is None:
         a.det_batch = 32 if yolo else 16
     if a.det_min_size is None:
         a.det_min_size = 50 if yolo else 0
     if a.cpu_frames is None:
-        a.cpu_frames = 32 if yolo else 12
+        a.cpu_frames = 24 if yolo else 12
+    a.H, a.W = {'720p': (720, 1280), '1080p': (1080, 1920), '224': (224, 224)}[a.frame]
     return a
 
 
-def det_params(args):
-    return dict(mscore=args.det_min_score, msize=args.det_min_size, mborder=args.det_min_border,
-                scale=(1.5, 1.5, 2.2, 1.2), square=True)
+# ------------------------------------------------------------------ launch
+def spawn_command(args_gpus, argv, port):
+    """torchrun command line that re-runs this script with one process per GPU."""
+    return [sys.executable, '-m', 'torch.distributed.run', '--nnodes=1', '--nproc-per-node', str(args_gpus),
+            '--master-addr', '127.0.0.1', '--master-port', str(port), os.path.abspath(__file__)] + list(argv)
 
 
-def cpu_baseline(frames, args):
-    """The oracle (CPU restatement of the reference path, torch-CPU + C NMS) on a bounded
-    sample of the same workload, rank 0 only."""
-    from oracle import mtcnn as om
-    from oracle import yolo as oy
-    from oracle.facenet import inception_resnet_v1, resize_linear_u8
-    from oracle.vit import vit
-    from videotofaces import synth
-    from videotofaces.detection import boxes_to_crops
-    cores = len(os.sched_getaffinity(0))
-    env = os.environ.get('OMP_NUM_THREADS')
-    if env and env.isdigit():
-        cores = min(cores, int(env))
-    torch.set_num_threads(cores)
-    yolo = args.det_model == 'yolo'
-    pm, pf = synth.make_params(args.det_model), synth.make_params(args.enc_model)
-    vit_dims = {'vit_b': (768, 12), 'vit_l': (1024, 24)}.get(args.enc_model)
-    n = min(args.cpu_frames, frames.shape[0])
-    sample = frames[:n]
-    t0 = time.time()
-    if yolo:
-        res = oy.forward(pm, list(sample))
-    else:
-        res = om.forward(pm, list(sample), minsize=args.min_face_size)
-    crops = boxes_to_crops(res, (H, W), **det_params(args))
-    faces = 0
-    for i in range(0, crops.shape[0], args.enc_batch):
-        blobs = []
-        for f, x1, y1, x2, y2 in crops[i:i + args.enc_batch]:
-            if vit_dims:  # blobFromImages(1/127.5, 128x128, 127.5, swapRB) (vit.py:141)
-                r = resize_linear_u8(sample[f, y1:y2, x1:x2], 128)[:, :, ::-1].transpose(2, 0, 1)
-                blobs.append((torch.from_numpy(np.ascontiguousarray(r)).float() - 127.5) * (1 / 127.5))
+def _free_port():
+    s = socket.socket()
+    s.bind(('127.0.0.1', 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def maybe_spawn(args, argv):
+    """Called before anything touches a GPU.  Returns an exit code when this process only
+    launches (or refuses), None when it should run the benchmark itself."""
+    world = os.environ.get('WORLD_SIZE')
+    if world is None:
+        if args.gpus > 1:
+            return subprocess.call(spawn_command(args.gpus, argv, _free_port()))
+        return None
+    if int(world) != args.gpus:
+        print('bench.py: --gpus %d but WORLD_SIZE=%s; launch one process per GPU with '
+              'torch.distributed.run --nproc-per-node %d' % (args.gpus, world, args.gpus), file=sys.stderr)
+        return 2
+    return None
+
+
+class Ctx:
+    """Rank context: process group over RCCL (GPU) or gloo (CPU tests)."""
+
+    def __init__(self, backend='nccl', device=None):
+        self.world = int(os.environ.get('WORLD_SIZE', '1'))
+        self.rank = int(os.environ.get('RANK', '0'))
+        self.local = int(os.environ.get('LOCAL_RANK', '0'))
+        self.device = device if device is not None else torch.device('cuda', self.local)
+        self.gpu = self.device.type == 'cuda'
+        if self.gpu:
+            torch.cuda.set_device(self.device)
+        if self.world > 1 and not dist.is_initialized():
+            if backend == 'nccl':
+                dist.init_process_group('nccl', device_id=self.device)
             else:
-                r = resize_linear_u8(sample[f, y1:y2, x1:x2], 160)[:, :, ::-1].transpose(2, 0, 1)
-                blobs.append((torch.from_numpy(np.ascontiguousarray(r)).float() - 127.5) * (1 / 128))
-        if vit_dims:
-            vit(pf, torch.stack(blobs), *vit_dims)
-        else:
-            inception_resnet_v1(pf, torch.stack(blobs))
-        faces += len(blobs)
-    dt = time.time() - t0
-    return {'value': round(faces / dt, 3), 'unit': 'faces/s', 'cores': cores, 'kind': 'port',
-            'sample': '%d synthetic %s frames (%d faces), oracle %s+%s fp32 on CPU, %.1f s'
-                      % (n, args.frame, faces, 'YOLOv3' if yolo else 'MTCNN(min_face_size=%g)' % args.min_face_size,
-                         ENC_NAMES[args.enc_model], dt)}
+                dist.init_process_group(backend)
+
+    def sync(self):
+        if self.gpu:
+            torch.cuda.synchronize(self.device)
+
+    def barrier(self):
+        if self.world > 1:
+            dist.barrier()
+
+    def reduce(self, values, op):
+        t = torch.tensor(values, dtype=torch.float64, device=self.device)
+        if self.world > 1:
+            dist.all_reduce(t, op=op)
+        return [float(v) for v in t.tolist()]
+
+    def gather_rows(self, local):
+        if self.world == 1:
+            return local
+        from videotofaces.parallel import all_gather_rows
+        return all_gather_rows(local)
+
+    def close(self):
+        if self.world > 1 and dist.is_initialized():
+            dist.barrier()
+            dist.destroy_process_group()
 
 
-def main():
-    args = parse()
-    world = int(os.environ.get('WORLD_SIZE', '1'))
-    rank = int(os.environ.get('RANK', '0'))
-    local = int(os.environ.get('LOCAL_RANK', '0'))
-    if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group('nccl', device_id=torch.device('cuda', local))
-    dev = torch.device('cuda', local)
+def measure(pipe, steps, warmup, ctx):
+    """Warm-up steps untimed, then exactly `steps` steps bracketed by barrier + device sync on
+    both sides, ending with the rank-ordered all-gather of the embeddings.  Returns
+    (faces on all ranks, max-over-ranks seconds, gathered embeddings [N,D], per-step faces)."""
+    pipe.run(0, warmup)
+    ctx.sync()
+    ctx.barrier()
+    ctx.sync()
+    t0 = time.perf_counter()
+    stats, parts = pipe.run(warmup, steps)
+    local = torch.cat(parts) if parts else torch.zeros((0, pipe.D), device=ctx.device)
+    gathered = ctx.gather_rows(local)
+    ctx.sync()
+    ctx.barrier()
+    ctx.sync()
+    elapsed = time.perf_counter() - t0
+    faces, = ctx.reduce([sum(stats)], dist.ReduceOp.SUM)
+    el, = ctx.reduce([elapsed], dist.ReduceOp.MAX)
+    return faces, el, gathered, stats
+
+
+# ------------------------------------------------------------------ GPU pipelines
+def _box_params(args):
+    from videotofaces import _native as nat
+    return nat.BoxParams.make(args.det_min_score, args.det_min_size, args.det_min_border, (1.5, 1.5, 2.2, 1.2), True)
+
+
+def _make_encoder(args, dev):
     from videotofaces import synth
-    from videotofaces.detectors.mtcnn import MTCNN
-    from videotofaces.detectors.yolo import YOLOv3
-    from videotofaces.detection import normalize_detout
-    from videotofaces.encoders.facenet import InceptionResnetV1
-    from videotofaces.detection import boxes_to_crops
-
-    B = args.det_batch
-    pool_n = max(B, args.pool // B * B)
-    frames_np = synth.make_frames(pool_n, H, W, seed=1000 + rank)
-    frames = torch.from_numpy(frames_np).to(dev)
-    yolo = args.det_model == 'yolo'
-    # `lanes` independent (detector, encoder, HIP stream) sets work on alternate det-batches
-    # from host threads (the ctypes calls release the GIL): one lane's host syncs and small
-    # stage-2/3 kernels overlap the other lane's pyramid kernel.  Batches stay whole and
-    # independent, so per-batch results are exactly the single-lane results.
-    L = max(1, args.lanes)
-    dets = [YOLOv3(dev, precision=args.det_precision) if yolo else MTCNN(dev) for _ in range(L)]
     if args.enc_model == 'facenet':
-        encs = [InceptionResnetV1(dev, precision=args.enc_precision) for _ in range(L)]
-        D = 512
-    else:
-        from videotofaces.encoders.vit import ViT
-        vp = synth.make_params(args.enc_model)
-        encs = [ViT(dev, vp, isL=args.enc_model == 'vit_l',
-                    precision='fp32' if args.enc_precision == 'fp32' else 'f16x') for _ in range(L)]
-        D = encs[0].dim
-    streams = [torch.cuda.Stream(dev) for _ in range(L)]
-    torch.cuda.synchronize(dev)
+        from videotofaces.encoders.facenet import InceptionResnetV1
+        return InceptionResnetV1(dev, precision='bf16' if args.enc_precision == 'bf16' else 'fp32')
+    from videotofaces.encoders.vit import ViT
+    return ViT(dev, synth.make_params(args.enc_model), isL=args.enc_model == 'vit_l',
+               precision='fp32' if args.enc_precision == 'fp32' else 'f16x')
 
-    def detect_step(lane, i):
-        """one det-batch: detect + box post-processing -> crops with frame indices into the
-        resident frame pool (so faces of consecutive det-batches can share encoder batches)."""
-        j = (i * B) % pool_n
-        fb = frames[j:j + B]
-        res = normalize_detout(dets[lane](fb)) if yolo else dets[lane](fb, args.min_face_size)
-        return boxes_to_crops(res, (H, W), frame_offset=j, **det_params(args)), sum(r.shape[0] for r in res)
 
-    def run(first, n):
-        """steps first..first+n-1, step i on lane i % L.  Each lane feeds its face stream to its
-        encoder in batches of exactly enc_batch (encode_faces, grouping.py:29-40), flushing the
-        remainder at the end.  Returns per-step (n faces, n detections) and the embeddings in
-        global (step, face) order."""
-        stats = [None] * n
-        lane_embs = [[] for _ in range(L)]
+def _make_detector(args, dev, fp32=False):
+    if args.det_model == 'yolo':
+        from videotofaces.detectors.yolo import YOLOv3
+        return YOLOv3(dev, precision='fp32' if fp32 else args.det_precision)
+    from videotofaces.detectors.mtcnn import MTCNN
+    if not fp32:
+        return MTCNN(dev)
+    old = os.environ.get('VTF_MTCNN_FP32')
+    os.environ['VTF_MTCNN_FP32'] = '1'  # read once when the handle is built: all-fp32 MFMA paths
+    try:
+        return MTCNN(dev)
+    finally:
+        if old is None:
+            del os.environ['VTF_MTCNN_FP32']
+        else:
+            os.environ['VTF_MTCNN_FP32'] = old
+
+
+class DetEncPipeline:
+    """L lanes of (detector, encoder, HIP stream) on alternate det-batches from host threads (the
+    ctypes calls release the GIL): one lane's host syncs and small stage-2/3 kernels overlap
+    another lane's pyramid kernel.  Batches stay whole and independent, so per-batch results are
+    exactly the single-lane results.  Detector rows never leave HBM: detect_crops returns device
+    crop rectangles that the lane's encoder consumes in batches of exactly enc_batch."""
+
+    def __init__(self, args, dev, frames_np):
+        self.args, self.dev = args, dev
+        self.B = args.det_batch
+        self.frames_np = frames_np
+        self.pool_n = frames_np.shape[0]
+        self.frames = torch.from_numpy(frames_np).to(dev)
+        self.L = max(1, args.lanes)
+        self.dets = [_make_detector(args, dev) for _ in range(self.L)]
+        self.encs = [_make_encoder(args, dev) for _ in range(self.L)]
+        self.D = 512 if args.enc_model == 'facenet' else self.encs[0].dim
+        self.streams = [torch.cuda.Stream(dev) for _ in range(self.L)]
+        self.bp = _box_params(args)
+        self.host = None  # host-frame leg: (pinned frames, device ring per lane, slots per lane)
+        self.minsize = args.min_face_size
+
+    def detect_step(self, lane, i, det=None):
+        j = (i * self.B) % self.pool_n
+        det = det or self.dets[lane]
+        if self.host is None:
+            src, off = self.frames[j:j + self.B], j
+        else:  # frames from pinned host memory: async H2D on the lane stream into a ring slot
+            pinned, ring, R = self.host
+            slot = lane * R + (i // self.L) % R
+            off = slot * self.B
+            ring[off:off + self.B].copy_(pinned[j:j + self.B], non_blocking=True)
+            src = ring[off:off + self.B]
+        if self.args.det_model == 'yolo':
+            crops, _ = det.detect_crops(src, self.bp, off)
+        else:
+            crops, _ = det.detect_crops(src, self.minsize, self.bp, off)
+        return crops
+
+    def run(self, first, n):
+        """steps first..first+n-1, step i on lane i % L -> (faces per step, embeddings per step)."""
+        stats = [0] * n
+        lane_embs = [[] for _ in range(self.L)]
         errs = []
+        eb = self.args.enc_batch
+        frames_of = (lambda: self.host[1]) if self.host is not None else (lambda: self.frames)
 
         def lane_fn(lane):
             try:
-                with torch.cuda.stream(streams[lane]):
-                    pend = []
-                    for k in range(lane, n, L):
-                        crops, nd = detect_step(lane, first + k)
-                        stats[k] = (crops.shape[0], nd)
-                        pend.extend(crops.tolist())
-                        while len(pend) >= args.enc_batch:
-                            lane_embs[lane].append(encs[lane].encode_crops(frames, pend[:args.enc_batch]))
-                            pend = pend[args.enc_batch:]
-                    if pend:
-                        lane_embs[lane].append(encs[lane].encode_crops(frames, pend))
+                enc = self.encs[lane]
+                with torch.cuda.stream(self.streams[lane]):
+                    pend, npend, slots = [], 0, []
+                    for k in range(lane, n, self.L):
+                        if self.host is not None and npend:
+                            # the ring slot this step overwrites still holds pending faces: flush
+                            R = self.host[2]
+                            slot = lane * R + ((first + k) // self.L) % R
+                            if slot in slots:
+                                lane_embs[lane].append(enc.encode_crops(frames_of(), torch.cat(pend)))
+                                pend, npend, slots = [], 0, []
+                        crops = self.detect_step(lane, first + k)
+                        stats[k] = int(crops.shape[0])
+                        if stats[k]:
+                            pend.append(crops)
+                            npend += stats[k]
+                            if self.host is not None:
+                                slots.append(lane * self.host[2] + ((first + k) // self.L) % self.host[2])
+                        while npend >= eb:
+                            allc = torch.cat(pend)
+                            lane_embs[lane].append(enc.encode_crops(frames_of(), allc[:eb]))
+                            pend = [allc[eb:]] if allc.shape[0] > eb else []
+                            npend -= eb
+                            if not npend:
+                                slots = []
+                    if npend:
+                        lane_embs[lane].append(enc.encode_crops(frames_of(), torch.cat(pend)))
             except BaseException as e:  # surfaced after join
                 errs.append(e)
-        ths = [threading.Thread(target=lane_fn, args=(l,)) for l in range(L)]
+        ths = [threading.Thread(target=lane_fn, args=(lane,)) for lane in range(self.L)]
         for t in ths:
             t.start()
         for t in ths:
             t.join()
         if errs:
             raise errs[0]
-        for s in streams:
+        for s in self.streams:
             s.synchronize()
         # lane streams -> global (step, face) order
-        parts, offs = [], [0] * L
-        flat = [torch.cat(e) if e else torch.zeros((0, D), device=dev) for e in lane_embs]
+        parts, offs = [], [0] * self.L
+        flat = [torch.cat(e) if e else torch.zeros((0, self.D), device=self.dev) for e in lane_embs]
         for k in range(n):
-            lane, nf = k % L, stats[k][0]
+            lane, nf = k % self.L, stats[k]
             parts.append(flat[lane][offs[lane]:offs[lane] + nf])
             offs[lane] += nf
         return stats, parts
 
-    run(0, max(args.warmup, L))
-    torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    for d in dets:
+    # ---- extras
+    def solo(self, steps=4):
+        """The detector's dominant kernel with the chip to itself: one lane, `steps` det-batches,
+        HIP events on the lane stream (vtf_*_profile)."""
+        d = self.dets[0]
         d.profile(True)
-    t0 = time.perf_counter()
-    stats, embs = run(args.warmup, args.steps)
-    faces = sum(s_[0] for s_ in stats)
-    dets_n = sum(s_[1] for s_ in stats)
-    local_emb = torch.cat(embs) if embs else torch.zeros((0, D), device=dev)
-    if world > 1:
-        from videotofaces.parallel import all_gather_rows
-        gathered = all_gather_rows(local_emb)
-    else:
-        gathered = local_emb
-    torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    elapsed = time.perf_counter() - t0
-    k_ms = k_launches = k_flops = k_frames = 0
-    for d in dets:
-        a, b_, c, e = d.profile(False)
-        k_ms, k_launches, k_flops, k_frames = k_ms + a, k_launches + b_, k_flops + c, k_frames + e
-    # the same kernel with the chip to itself (outside the timed region): one lane, 3 det-batches.
-    # Under concurrent lanes the events above also span co-running kernels of the other lanes.
-    dets[0].profile(True)
-    with torch.cuda.stream(streams[0]):
-        for i in range(3):
-            detect_step(0, i)
-    streams[0].synchronize()
-    s_ms, s_launches, s_flops, _ = dets[0].profile(False)
-    dets = dets_n
-    tot = torch.tensor([faces, dets, k_frames], dtype=torch.float64, device=dev)
-    el = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-    if world > 1:
-        dist.all_reduce(tot, op=dist.ReduceOp.SUM)
-        dist.all_reduce(el, op=dist.ReduceOp.MAX)
-    faces_all, dets_all, frames_all = [float(x) for x in tot.tolist()]
-    elapsed = float(el.item())
-    if rank == 0:
-        avg_ms = k_ms / max(1, k_launches)
-        flops_per_launch = k_flops / max(1, k_launches)
-        achieved = flops_per_launch / (avg_ms / 1e3) / 1e12 if avg_ms > 0 else 0.0
-        traffic = None
-        s_avg = s_ms / max(1, s_launches)
-        s_ach = s_flops / max(1, s_launches) / (s_avg / 1e3) / 1e12 if s_avg > 0 else 0.0
-        tf = os.path.join(ROOT, 'profiles', ('yolo' if yolo else 'pnet') + '_traffic.json')
-        if os.path.exists(tf):
-            traffic = json.load(open(tf)).get('hbm_bytes_per_launch')
-        if yolo:
-            peak = BF16_PEAK_TFLOPS if args.det_precision == 'bf16' else FP32_PEAK_TFLOPS
-            kname = 'k_conv (YOLOv3 Darknet53+neck+head, 75 implicit-GEMM launches per det-batch, %s)' % args.det_precision
-            wl = 'YOLOv3(%s)+%s' % (args.det_precision, ENC_NAMES[args.enc_model])
+        with torch.cuda.stream(self.streams[0]):
+            for i in range(steps):
+                self.detect_step(0, i)
+        self.streams[0].synchronize()
+        return d.profile(False)
+
+    def host_frames(self, ring_slots=4):
+        """Switch to frames in pinned host memory (None restores HBM-resident frames)."""
+        if ring_slots is None:
+            self.host = None
+            return
+        pinned = torch.from_numpy(self.frames_np).pin_memory()
+        ring = torch.empty((self.L * ring_slots * self.B,) + tuple(self.frames_np.shape[1:]), dtype=torch.uint8,
+                           device=self.dev)
+        self.host = (pinned, ring, ring_slots)
+
+    def drift(self, steps=2):
+        """bf16 / split-fp16 perf modes vs the fp32 parity modes on the same det-batches: detector
+        boxes (fp32 MFMA detector) and embeddings (fp32 encoder on the same crops)."""
+        det32 = _make_detector(self.args, self.dev, fp32=True)
+        a = dict(vars(self.args))
+        a['enc_precision'] = 'fp32'
+        enc32 = _make_encoder(argparse.Namespace(**a), self.dev)
+        ious, n_match, n_a, n_b, cos = [], 0, 0, 0, []
+        for i in range(steps):
+            ca = self.detect_step(0, i).cpu().numpy()
+            cb = self.detect_step(0, i, det32).cpu().numpy()
+            n_a += len(ca)
+            n_b += len(cb)
+            for f in np.unique(np.concatenate([ca[:, 0], cb[:, 0]])):
+                ra, rb = ca[ca[:, 0] == f, 1:], cb[cb[:, 0] == f, 1:]
+                for r in ra:
+                    if len(rb):
+                        ix = np.clip(np.minimum(r[2], rb[:, 2]) - np.maximum(r[0], rb[:, 0]), 0, None)
+                        iy = np.clip(np.minimum(r[3], rb[:, 3]) - np.maximum(r[1], rb[:, 1]), 0, None)
+                        inter = ix * iy
+                        uni = (r[2] - r[0]) * (r[3] - r[1]) + (rb[:, 2] - rb[:, 0]) * (rb[:, 3] - rb[:, 1]) - inter
+                        best = float((inter / np.maximum(uni, 1)).max())
+                        ious.append(best)
+                        n_match += best == 1.0
+            if len(ca):
+                dc = torch.from_numpy(ca).to(self.dev)
+                e16 = self.encs[0].encode_crops(self.frames, dc)
+                e32 = enc32.encode_crops(self.frames, dc)
+                cos.append(torch.nn.functional.cosine_similarity(e16, e32, dim=1).cpu().numpy())
+        cos = np.concatenate(cos) if cos else np.zeros(0)
+        return {'det_batches': steps, 'faces_perf_mode': n_a, 'faces_fp32_mode': n_b,
+                'crop_rect_identical_frac': round(n_match / max(1, n_a), 4),
+                'crop_iou_mean': round(float(np.mean(ious)), 6) if ious else None,
+                'crop_iou_min': round(float(np.min(ious)), 6) if ious else None,
+                'embedding_cos_mean': round(float(cos.mean()), 6) if len(cos) else None,
+                'embedding_cos_min': round(float(cos.min()), 6) if len(cos) else None,
+                'enc_modes': '%s vs fp32' % self.args.enc_precision,
+                'det_modes': ('split-fp16 vs fp32 MFMA' if self.args.det_model == 'mtcnn'
+                              else '%s vs fp32' % self.args.det_precision)}
+
+
+class EncodePipeline:
+    """BASELINE config 4: pre-cropped 224x224 faces resident in HBM, one enc-batch per step
+    (blob 224 -> 128 + ViT forward, one stream)."""
+
+    def __init__(self, args, dev, rank):
+        from videotofaces import synth
+        self.args, self.dev, self.B = args, dev, args.enc_batch
+        self.pool_n = max(self.B, 4 * self.B)
+        self.crops_u8 = torch.from_numpy(synth.make_crops(self.pool_n, 224, seed=1 + rank)).to(dev)
+        self.boxes = torch.tensor([[i, 0, 0, 224, 224] for i in range(self.pool_n)], dtype=torch.int32, device=dev)
+        self.enc = _make_encoder(args, dev)
+        self.D = self.enc.dim
+
+    def run(self, first, n):
+        stats, parts = [], []
+        for i in range(first, first + n):
+            j = (i * self.B) % self.pool_n
+            parts.append(self.enc.encode_crops(self.crops_u8, self.boxes[j:j + self.B]))
+            stats.append(self.B)
+        return stats, parts
+
+
+# ------------------------------------------------------------------ CPU baseline (oracle)
+def _cores():
+    n = len(os.sched_getaffinity(0))
+    env = os.environ.get('OMP_NUM_THREADS')
+    return min(n, int(env)) if env and env.isdigit() else n
+
+
+def cpu_baseline(args, frames_np):
+    """The oracle (CPU restatement of the reference path: torch-CPU nets, C NMS, numpy box logic)
+    on a bounded sample of the same workload, rank 0 only.  Detection runs at det-batch 1, the
+    BASELINE config-1 shape (the reference CPU path)."""
+    from oracle.boxes import rows_to_crops
+    from oracle.facenet import inception_resnet_v1, resize_linear_u8
+    from oracle.vit import vit
+    from videotofaces import synth
+    cores = _cores()
+    torch.set_num_threads(cores)
+    pf = synth.make_params(args.enc_model)
+    vit_dims = {'vit_b': (768, 12), 'vit_l': (1024, 24)}.get(args.enc_model)
+
+    def encode(imgs):
+        blobs = []
+        for im in imgs:
+            if vit_dims:  # blobFromImages(1/127.5, 128x128, 127.5, swapRB) (vit.py:141)
+                r = resize_linear_u8(im, 128)[:, :, ::-1].transpose(2, 0, 1)
+                blobs.append((torch.from_numpy(np.ascontiguousarray(r)).float() - 127.5) * (1 / 127.5))
+            else:  # blobFromImages(1/128, 160x160, 127.5, swapRB) (facenet.py:179)
+                r = resize_linear_u8(im, 160)[:, :, ::-1].transpose(2, 0, 1)
+                blobs.append((torch.from_numpy(np.ascontiguousarray(r)).float() - 127.5) * (1 / 128))
+        for i in range(0, len(blobs), args.enc_batch):
+            x = torch.stack(blobs[i:i + args.enc_batch])
+            vit(pf, x, *vit_dims) if vit_dims else inception_resnet_v1(pf, x)
+
+    if args.det_model == 'none':
+        n = 16
+        crops = synth.make_crops(n, 224, seed=2)
+        t0 = time.time()
+        encode(list(crops))
+        dt = time.time() - t0
+        return {'value': round(n / dt, 3), 'unit': 'faces/s', 'cores': cores, 'kind': 'port',
+                'sample': '%d synthetic 224x224 crops, oracle %s fp32 on CPU, %.1f s' % (n, ENC_NAMES[args.enc_model], dt)}
+    from oracle import mtcnn as om
+    from oracle import yolo as oy
+    pm = synth.make_params(args.det_model)
+    n = min(args.cpu_frames, frames_np.shape[0])
+    t0 = time.time()
+    faces = 0
+    imgs = []
+    for f in range(n):  # det-batch 1 (config 1)
+        fr = frames_np[f:f + 1]
+        if args.det_model == 'yolo':
+            b, s, _ = oy.forward(pm, list(fr))
+            res = [np.concatenate([b[0], s[0][:, None]], 1)]
         else:
-            peak = F16X_PEAK_TFLOPS
-            kname = ('k_pnet (fused pyramid resample + PNet; convs on fp16 matrix cores with split operands, '
-                     'fp32-grade; peak = fp16 dense / 3 products)')
-            wl = 'MTCNN(min_face_size=%g)+%s' % (args.min_face_size, ENC_NAMES[args.enc_model])
-        out = {
-            'metric': 'faces/sec end-to-end (detect+encode) on %dx%d synthetic frames' % (W, H),
-            'value': round(faces_all / elapsed, 2),
-            'unit': 'faces/s',
-            'n_gpus': world,
-            'steps': args.steps,
-            'warmup': args.warmup,
-            'ms_per_step': round(elapsed * 1e3 / args.steps, 3),
-            'higher_is_better': True,
-            'scaling': 'weak',
-            'vs_baseline': None,
-            'dtype': '%s det / %s enc' % (args.det_precision if yolo else 'fp32 (split-fp16 MFMA)',
-                                          args.enc_precision if args.enc_model == 'facenet' or args.enc_precision == 'fp32'
-                                          else 'fp32 (split-fp16 MFMA)'),
-            'data': 'synthetic (seeded %s value-noise frames with face blobs; hash-seeded synthetic weights, '
-                    'detector heads calibrated to a few faces/frame)' % args.frame,
-            'config': {'workload': '%s, det-batch %d, enc-batch %d, %s, frames in HBM, '
-                                   'box filter min_score %g min_size %d min_border %d, det_scale (1.5,1.5,2.2,1.2), square'
-                                   % (wl, B, args.enc_batch, args.frame, args.det_min_score, args.det_min_size,
-                                      args.det_min_border),
-                       'det_batch': B, 'enc_batch': args.enc_batch, 'frames_per_step_per_gpu': B,
-                       'lanes': L,
-                       'parallelism': 'dp%d (frame-sharded, RCCL all-gather of embeddings)' % world},
-            'frames_per_s': round(world * args.steps * B / elapsed, 2),
-            'faces_per_frame': round(faces_all / max(1.0, world * args.steps * B), 3),
-            'detections_per_frame': round(dets_all / max(1.0, world * args.steps * B), 3),
-            'roofline': {'kernel': kname, 'bound': 'mfma',
-                         'achieved': round(achieved, 3), 'peak': peak, 'unit': 'TFLOP/s',
-                         'frac': round(achieved / peak, 4), 'traffic': traffic,
-                         'avg_launch_ms': round(avg_ms, 4), 'flops_per_launch': flops_per_launch,
-                         'launches': k_launches, 'concurrent_lanes': L,
-                         'solo': {'avg_launch_ms': round(s_avg, 4), 'achieved': round(s_ach, 3),
-                                  'frac': round(s_ach / peak, 4), 'launches': s_launches}},
-            # north-star's "memory-bound HBM roofline on the detector conv path": the layer-by-layer
-            # PNet bytes of SURVEY.md §8d (2,075 MB fp32 per 720p frame at 38.66 GFLOP, AI 18.6) over
-            # the same launch time -- an equivalent rate (the fused kernel moves `traffic` bytes)
-            'hbm_equiv': None if yolo else {
-                'bytes_per_launch': round(flops_per_launch * LBL_BYTES_PER_FLOP),
-                'achieved': round(flops_per_launch * LBL_BYTES_PER_FLOP / (avg_ms / 1e3) / 1e9, 1) if avg_ms > 0 else 0.0,
-                'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
-                'frac': round(flops_per_launch * LBL_BYTES_PER_FLOP / (avg_ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4)
-                if avg_ms > 0 else 0.0,
-                'solo_frac': round(s_flops / max(1, s_launches) * LBL_BYTES_PER_FLOP / (s_avg / 1e3) / 1e9
-                                   / HBM_PEAK_GBS, 4) if s_avg > 0 else 0.0},
-            'cpu_baseline': None,
+            res = om.forward(pm, list(fr), minsize=args.min_face_size)
+        crops, _ = rows_to_crops(res, (args.H, args.W), args.det_min_score, args.det_min_size, args.det_min_border,
+                                 (1.5, 1.5, 2.2, 1.2), True)
+        imgs.extend(fr[0, y1:y2, x1:x2] for _, x1, y1, x2, y2 in crops)
+    encode(imgs)
+    faces = len(imgs)
+    dt = time.time() - t0
+    det = 'YOLOv3' if args.det_model == 'yolo' else 'MTCNN(min_face_size=%g)' % args.min_face_size
+    return {'value': round(faces / dt, 3), 'unit': 'faces/s', 'cores': cores, 'kind': 'port',
+            'sample': '%d synthetic %s frames at det-batch 1 (%d faces), oracle %s + box logic + %s fp32 on CPU, %.1f s'
+                      % (n, args.frame, faces, det, ENC_NAMES[args.enc_model], dt)}
+
+
+# ------------------------------------------------------------------ roofline
+def roofline_det(args, pipe, shared, solo):
+    """Dominant detector kernel: k_pnet (MTCNN) or the YOLO conv stack.  `avg_launch_ms` is the
+    kernel's own duration with the chip to itself (solo leg, one lane; it matches a one-lane
+    rocprofv3 trace); the concurrent-lane figure (events spanning co-running kernels of the
+    other lanes) is kept under `shared`."""
+    yolo = args.det_model == 'yolo'
+    s_ms, s_n, s_fl, _ = solo
+    c_ms, c_n, c_fl, _ = shared
+    s_avg, c_avg = s_ms / max(1, s_n), c_ms / max(1, c_n)
+    fl = s_fl / max(1, s_n)
+    if yolo:
+        peak = BF16_PEAK_TFLOPS if args.det_precision == 'bf16' else FP32_PEAK_TFLOPS
+        kname = 'k_conv (YOLOv3 Darknet53+neck+head, 75 implicit-GEMM launches per det-batch, %s)' % args.det_precision
+    else:
+        peak = F16X_PEAK_TFLOPS
+        kname = ('k_pnet (fused pyramid resample + PNet; convs on fp16 matrix cores with split operands, '
+                 'fp32-grade; peak = fp16 dense / 3 products)')
+    ach = fl / (s_avg / 1e3) / 1e12 if s_avg > 0 else 0.0
+    c_ach = (c_fl / max(1, c_n)) / (c_avg / 1e3) / 1e12 if c_avg > 0 else 0.0
+    traffic = None
+    tf = os.path.join(ROOT, 'profiles', ('yolo' if yolo else 'pnet') + '_traffic.json')
+    if os.path.exists(tf):
+        traffic = json.load(open(tf)).get('hbm_bytes_per_launch')
+    r = {'kernel': kname, 'bound': 'mfma', 'achieved': round(ach, 3), 'peak': peak, 'unit': 'TFLOP/s',
+         'frac': round(ach / peak, 4), 'traffic': traffic, 'avg_launch_ms': round(s_avg, 4),
+         'flops_per_launch': fl, 'launches': s_n, 'timing': 'solo leg: one lane, HIP events on its stream',
+         'shared': {'avg_launch_ms': round(c_avg, 4), 'achieved': round(c_ach, 3), 'frac': round(c_ach / peak, 4),
+                    'launches': c_n, 'concurrent_lanes': pipe.L}}
+    hbm = None
+    if not yolo:
+        # north-star "memory-bound HBM roofline on the detector conv path": SURVEY.md §8d's
+        # layer-by-layer PNet bytes over the same launch time (an equivalent rate; the fused
+        # kernel moves `traffic` bytes)
+        b = fl * LBL_BYTES_PER_FLOP
+        hbm = {'bytes_per_launch': round(b), 'achieved': round(b / (s_avg / 1e3) / 1e9, 1) if s_avg else 0.0,
+               'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
+               'frac': round(b / (s_avg / 1e3) / 1e9 / HBM_PEAK_GBS, 4) if s_avg else 0.0,
+               'shared_frac': round(c_fl / max(1, c_n) * LBL_BYTES_PER_FLOP / (c_avg / 1e3) / 1e9 / HBM_PEAK_GBS, 4)
+               if c_avg else 0.0}
+    return r, hbm
+
+
+def roofline_enc(args, ms_per_step):
+    peak = FP32_PEAK_TFLOPS if args.enc_precision == 'fp32' else F16X_PEAK_TFLOPS
+    ach = VIT_GFLOP[args.enc_model] * args.enc_batch / ms_per_step
+    return {'kernel': 'whole ViT encoder step (blob + k_conv split-fp16 GEMMs + attention + LayerNorm)',
+            'bound': 'mfma', 'achieved': round(ach, 3), 'peak': peak, 'unit': 'TFLOP/s', 'frac': round(ach / peak, 4),
+            'traffic': None, 'avg_launch_ms': round(ms_per_step, 4),
+            'flops_per_launch': VIT_GFLOP[args.enc_model] * 1e9 * args.enc_batch,
+            'timing': 'one enc-batch per step, wall clock of the timed region'}
+
+
+# ------------------------------------------------------------------ main
+def run_gpu(args):
+    ctx = Ctx('nccl')
+    dev = ctx.device
+    from videotofaces import synth
+    if args.det_model == 'none':
+        pipe = EncodePipeline(args, dev, ctx.rank)
+    else:
+        B = args.det_batch
+        pool_n = max(B, args.pool // B * B)
+        frames_np = synth.make_frames(pool_n, args.H, args.W, seed=1000 + ctx.rank)
+        pipe = DetEncPipeline(args, dev, frames_np)
+    ctx.sync()
+    faces, elapsed, gathered, _ = measure(pipe, args.steps, max(args.warmup, getattr(pipe, 'L', 1)), ctx)
+    det = args.det_model != 'none'
+    shared = None
+    if det:
+        for d in pipe.dets:
+            d.profile(True)
+        pipe.run(0, len(pipe.dets))  # one det-batch per lane with timing on (events, concurrent lanes)
+        shared = [0, 0, 0, 0]
+        for d in pipe.dets:
+            shared = [a + b for a, b in zip(shared, d.profile(False))]
+    out = {}
+    extras = not args.no_extras
+    if det and extras:
+        solo = pipe.solo(4)
+        # sustained leg: BASELINE config 2's 10k frames (per rank) through the same pipeline
+        if args.sustain_frames > 0:
+            n_sus = max(1, -(-args.sustain_frames // args.det_batch))
+            f_sus, t_sus, _, _ = measure(pipe, n_sus, 0, ctx)
+            out['sustained'] = {'frames_per_rank': n_sus * args.det_batch, 'steps': n_sus,
+                                'value': round(f_sus / t_sus, 2), 'seconds': round(t_sus, 3),
+                                'ms_per_step': round(t_sus * 1e3 / n_sus, 3)}
+        # PCIe-inclusive variant: frames from pinned host memory, async H2D on each lane's stream
+        pipe.host_frames(4)
+        f_h, t_h, _, _ = measure(pipe, args.steps, pipe.L, ctx)
+        pipe.host_frames(None)
+        out['host_frames'] = {'value': round(f_h / t_h, 2), 'ms_per_step': round(t_h * 1e3 / args.steps, 3),
+                              'note': 'frames start in pinned host memory; H2D (%.1f MB per det-batch) inside the '
+                                      'timed region' % (args.det_batch * args.H * args.W * 3 / 1e6)}
+        if ctx.rank == 0:
+            out['bf16_drift'] = pipe.drift(2)
+    elif det:
+        solo = pipe.solo(2)
+    grouping = None
+    if args.grouping:
+        from videotofaces import dupes
+        from videotofaces.grouping import cluster_sweep
+        X = gathered.contiguous()
+        ctx.sync()
+        ctx.barrier()
+        t0 = time.perf_counter()
+        mins, _ = dupes.cosine_dedupe_device(X)
+        ctx.sync()
+        t_dd = time.perf_counter() - t0
+        # BASELINE config 5 clusters the gathered embeddings; the dedupe (main.py:72-74) is timed
+        # and reported beside it but not applied: with hash-seeded synthetic ViT weights nearly
+        # every embedding lies within the 0.25 cosine threshold of an earlier one
+        Xh = X.cpu().numpy()
+        ks = [k for k in range(2, 17) if k <= Xh.shape[0]]
+        t1 = time.perf_counter()
+        labels, scores = cluster_sweep(Xh, ks, 0, device=dev)
+        ctx.sync()
+        t_sw = time.perf_counter() - t1
+        ctx.barrier()
+        tg, t_dd, t_sw = ctx.reduce([time.perf_counter() - t0, t_dd, t_sw], dist.ReduceOp.MAX)
+        best = max(scores, key=lambda s: s[1])[0] if scores else None
+        grouping = {'faces': int(X.shape[0]), 'dupes_at_0.25': int((mins <= 0.25).sum()),
+                    'k': [ks[0], ks[-1]] if ks else [], 'seconds': round(tg, 4), 'dedupe_s': round(t_dd, 4),
+                    'sweep_s': round(t_sw, 4), 'best_k_silhouette': best,
+                    'note': 'fused cosine dedupe, then KMeans + silhouette/CH/DB for each k on the gathered '
+                            'embeddings, k sharded across ranks (max over ranks)'}
+    if ctx.rank == 0:
+        steps = args.steps
+        frames_all = ctx.world * steps * (args.det_batch if det else 0)
+        dtype_enc = args.enc_precision if args.enc_precision != 'f16x' else 'fp32 (split-fp16 MFMA)'
+        if det:
+            roof, hbm = roofline_det(args, pipe, shared, solo)
+            wl = ('YOLOv3(%s)' % args.det_precision if args.det_model == 'yolo'
+                  else 'MTCNN(min_face_size=%g)' % args.min_face_size) + '+' + ENC_NAMES[args.enc_model]
+            dtype = '%s det / %s enc' % (args.det_precision if args.det_model == 'yolo' else 'fp32 (split-fp16 MFMA)',
+                                         dtype_enc)
+            workload = ('%s, det-batch %d, enc-batch %d, %s, frames in HBM, box filter min_score %g min_size %d '
+                        'min_border %d, det_scale (1.5,1.5,2.2,1.2), square' % (
+                            wl, args.det_batch, args.enc_batch, args.frame, args.det_min_score, args.det_min_size,
+                            args.det_min_border))
+            metric = 'faces/sec end-to-end (detect+encode) on %dx%d synthetic frames' % (args.W, args.H)
+        else:
+            roof, hbm = roofline_enc(args, elapsed * 1e3 / steps), None
+            dtype = dtype_enc
+            workload = '%s encoder only, enc-batch %d, pre-cropped 224x224 uint8 faces in HBM' % (
+                ENC_NAMES[args.enc_model], args.enc_batch)
+            metric = 'faces/sec, %s encoder on pre-cropped 224x224 faces' % ENC_NAMES[args.enc_model]
+        res = {
+            'metric': metric, 'value': round(faces / elapsed, 2), 'unit': 'faces/s', 'n_gpus': ctx.world,
+            'steps': steps, 'warmup': args.warmup, 'ms_per_step': round(elapsed * 1e3 / steps, 3),
+            'higher_is_better': True, 'scaling': 'weak', 'vs_baseline': None, 'dtype': dtype,
+            'data': 'synthetic (seeded %s frames/crops; hash-seeded synthetic weights, detector heads calibrated '
+                    'to a few faces/frame)' % args.frame,
+            'config': {'workload': workload, 'baseline_config': args.config, 'det_batch': args.det_batch if det else None,
+                       'enc_batch': args.enc_batch, 'frames_per_step_per_gpu': args.det_batch if det else 0,
+                       'lanes': getattr(pipe, 'L', 1),
+                       'parallelism': 'dp%d (frame-sharded, RCCL all-gather of embeddings)' % ctx.world},
+            'faces_per_frame': round(faces / max(1, frames_all), 3) if det else None,
+            'frames_per_s': round(frames_all / elapsed, 2) if det else None,
+            'embeddings_gathered': int(gathered.shape[0]),
+            'roofline': roof, 'cpu_baseline': None,
         }
-        if world == 1 and not args.no_cpu_baseline:
-            out['cpu_baseline'] = cpu_baseline(frames_np, args)
-        print(json.dumps(out), flush=True)
-    if world > 1:
-        dist.barrier()
-        dist.destroy_process_group()
+        if hbm:
+            res['hbm_equiv'] = hbm
+        res.update(out)
+        if grouping:
+            res['grouping'] = grouping
+        if ctx.world == 1 and not args.no_cpu_baseline:
+            res['cpu_baseline'] = cpu_baseline(args, getattr(pipe, 'frames_np', None))
+        print(json.dumps(res), flush=True)
+    ctx.close()
+
+
+def main(argv=None):
+    argv = sys.argv[1:] if argv is None else argv
+    args = parse(argv)
+    rc = maybe_spawn(args, argv)
+    if rc is not None:
+        sys.exit(rc)
+    run_gpu(args)
 
 
 if __name__ == '__main__':

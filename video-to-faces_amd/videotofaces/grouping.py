@@ -53,8 +53,10 @@ def encode_faces(paths, model, bs, area):
     return np.concatenate(x)
 
 
-def cosine_classify_device(X, R):
-    dev = torch.device('cuda:0')
+def cosine_classify_device(X, R, device=None):
+    """classify's distances (grouping.py:51-53): min / argmin over the reference rows of the
+    cosine distance, on `device` (default cuda:0)."""
+    dev = nat.require_gpu(device)
     Xd = torch.from_numpy(np.ascontiguousarray(X, np.float32)).to(dev)
     Rd = torch.from_numpy(np.ascontiguousarray(R, np.float32)).to(dev)
     n, d = Xd.shape
@@ -65,14 +67,15 @@ def cosine_classify_device(X, R):
     return mins.cpu().numpy(), inds.cpu().numpy()
 
 
-def classify(X, R, classes, thr, log, paths, out_dir):
-    mins, inds = cosine_classify_device(X, R)
+def classify(X, R, classes, thr, log, paths, out_dir, device=None):
+    mins, inds = cosine_classify_device(X, R, device)
     if thr and thr != -1:
         inds[mins >= thr] = len(classes)
         classes.append('other')
     if log:
-        import sklearn.metrics
-        dist = sklearn.metrics.pairwise.cosine_distances(X, R)
+        # the per-class distances of the CSV: the same device kernel against one class at a time
+        R = np.asarray(R, np.float32)
+        dist = np.stack([cosine_classify_device(X, R[c:c + 1], device)[0] for c in range(R.shape[0])], 1)
         fnames = [osp.basename(p) for p in paths]
         with open(osp.join(out_dir, 'faces', 'log_classification.csv'), 'w') as f:
             extra = '(other_threshold=%s)' % str(thr) if thr else ''
@@ -90,7 +93,7 @@ def sweep_scores(X, k, random_state, grouper, prep=None):
                 grouper.davies_bouldin_score(X, lb))
 
 
-def cluster_sweep(X, clusters, random_state, compute=None):
+def cluster_sweep(X, clusters, random_state, compute=None, device=None):
     """KMeans + scores for every k in `clusters`, in order.  With torch.distributed
     initialised, rank r computes the k at positions i % world == r (each rank holds the
     replicated X) and the results are all-gathered -- the parity-preserving sharding of
@@ -98,7 +101,7 @@ def cluster_sweep(X, clusters, random_state, compute=None):
     import torch.distributed as dist
     if compute is None:
         from .kmeans import Grouper
-        g = Grouper()
+        g = Grouper(device)
         prep = g.prepare(X)
         compute = lambda k: sweep_scores(X, k, random_state, g, prep)  # noqa: E731
     world = dist.get_world_size() if dist.is_available() and dist.is_initialized() else 1
@@ -114,12 +117,13 @@ def cluster_sweep(X, clusters, random_state, compute=None):
     return labels, scores
 
 
-def cluster_faces(paths, X, cluster_params):
-    """grouping.py:92-137 with the KMeans / score sweep on the GPU (cluster_sweep)."""
+def cluster_faces(paths, X, cluster_params, device=None):
+    """grouping.py:92-137 with the KMeans / score sweep on the GPU (cluster_sweep); `device`
+    (an addition) picks the GPU."""
     clusters, save_all, rstate, log, out_dir = cluster_params
     clusters = [c for c in clusters if c <= len(paths)]
     print('Clustering images into %s groups' % ', '.join([str(cl) for cl in clusters]))
-    labels, scores = cluster_sweep(X, clusters, rstate)
+    labels, scores = cluster_sweep(X, clusters, rstate, device=device)
     if log:
         with open(osp.join(out_dir, 'faces', 'log_clustering.csv'), 'w') as f:
             f.write('n_clusters,silhouette_score,calinski_harabasz_score,davies_bouldin_score\n')
@@ -152,7 +156,7 @@ def encode_refs(refs, model):
     return model([_imread(ps[0]) for (_, ps) in refs])
 
 
-def classify_faces(paths, X, model, classif_params):
+def classify_faces(paths, X, model, classif_params, device=None):
     """grouping.py:69-89: classify against reference images, move files into class folders."""
     refs, thr, log, out_dir = classif_params
     classes = [c for (c, _) in refs]
@@ -160,7 +164,7 @@ def classify_faces(paths, X, model, classif_params):
     print('Extracting features from reference images')
     R = encode_refs(refs, model)
     print('Classifying images')
-    inds, classes = classify(X, R, classes, thr, log, paths, out_dir)
+    inds, classes = classify(X, R, classes, thr, log, paths, out_dir, device or nat.device_of(model))
     img_dir = osp.dirname(osp.abspath(paths[0]))
     for c in classes:
         os.makedirs(osp.join(img_dir, c), exist_ok=True)

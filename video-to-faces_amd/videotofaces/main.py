@@ -8,7 +8,11 @@ and every all-pairs / K-means pass runs in libvtf_hip.so.  Additions, all opt-in
     decode needs OpenCV, which this image lacks (SURVEY.md §8f: decode is a later row);
   * decoupled=True lifts the style <-> model coupling (prep.py:39-44), e.g. det_model='yolo'
     with enc_model='vit_l' (BASELINE config 5);
-  * det_precision / enc_precision 'bf16' select the bf16 perf mode (default fp32 = parity).
+  * det_precision / enc_precision select the operand mode of YOLO / R-CNN and FaceNet / ViT:
+    'fp32' (default, fp32 MFMA: the parity mode), 'bf16' (bf16 operands; FaceNet, YOLO, R-CNN)
+    or 'f16x' (fp32 operands split into two fp16 parts, fp32-grade products; ViT).  The
+    reference-default paths (det_model / enc_model 'default') keep the reference classes'
+    defaults.
 """
 import os.path as osp
 
@@ -37,7 +41,7 @@ def get_encoder(style, enc_model, device, precision='fp32'):
         return get_encoder_model(style, enc_model, device)
     if enc_model.startswith('vit'):
         from .encoders.vit import AnimeVIT
-        return AnimeVIT(device, enc_model[-1] == 'l')
+        return AnimeVIT(device, enc_model[-1] == 'l', precision=precision)
     from .encoders.facenet import FaceNet
     return FaceNet(device, enc_model.split('_')[1] == 'casia', precision=precision)
 
@@ -102,9 +106,11 @@ def video_to_faces(input_path=None, input_ext=None,
         encoder = get_encoder(style, enc_model, device, enc_precision)
         features = encode_faces(imgpaths, encoder, enc_batch_size, enc_area)
         if enc_dup_thr and enc_dup_thr != -1:
-            features, imgpaths = remove_dupes_overall(features, imgpaths, ('enc', enc_dup_thr, save_dupes, out_dir))
+            features, imgpaths = remove_dupes_overall(features, imgpaths, ('enc', enc_dup_thr, save_dupes, out_dir),
+                                                      device=device)
         if group_mode == 'clustering':
-            cluster_faces(imgpaths, features, (clusters, clusters_save_all, random_state, group_log, out_dir))
+            cluster_faces(imgpaths, features, (clusters, clusters_save_all, random_state, group_log, out_dir),
+                          device=device)
         if group_mode == 'classification':
-            classify_faces(imgpaths, features, encoder, (refs, enc_oth_thr, group_log, out_dir))
+            classify_faces(imgpaths, features, encoder, (refs, enc_oth_thr, group_log, out_dir), device=device)
     print('Done')
