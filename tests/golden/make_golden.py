@@ -435,6 +435,152 @@ def gen_dupes():
     print('dupes', N, 'kept', len(goods))
 
 
+def _u8(seed, shape):
+    """seeded uint8 test images (numpy PCG64: identical on the GPU box)"""
+    return np.random.default_rng(seed).integers(0, 256, shape, dtype=np.uint8)
+
+
+def _yolo_input(frames):
+    """the reference's letterbox input from the build's INTER_LINEAR restatement (cv2 absent)"""
+    sys.path.insert(0, ROOT)
+    from oracle import yolo as oy
+    prep = importlib.import_module('ref_vtf.detectors.operations.prep')
+    resized, szo, szu = [], [], []
+    for f in frames:
+        sz = f.shape[:2]
+        scl = min(608 / min(sz), 608 / max(sz))
+        n = int(sz[0] * scl + 0.5), int(sz[1] * scl + 0.5)
+        resized.append(oy.resize_linear_u8_hw(f, n))
+        szo.append(sz)
+        szu.append(n)
+    ts = prep.to_tensors(resized, 'cpu', None, 255, True)
+    return prep.pad_and_batch(ts, 32), szo, szu, resized
+
+
+def _yolo_ref(net, y, frames):
+    with torch.inference_mode():
+        x, szo, szu, resized = _yolo_input(frames)
+        xs = net.head(net.neck(net.backbone(x)))
+        pri = y.get_priors(x.shape[-2:], y.YOLOv3.bases, 'cpu', 'center')
+        b, s, _ = net.postprocess(xs, pri, num_classes=1)
+        b = y.scale_boxes(b, szo, szu)
+    return [t.numpy() for t in b], [t.numpy() for t in s], resized
+
+
+def gen_shapes():
+    """Golden vectors at the benchmarked shapes (BASELINE configs 2-5), from the reference's own
+    modules: MTCNN 720p det-batch 16 at min_face_size 5 and det-batch 4 at 20 (main.py:18
+    default batch), YOLO 1080p det-batch 4, FaceNet fp32 batch 128, ViT-L batch 8 and 128.
+    Inputs are regenerated from seeds on the GPU box (synth.make_frames, numpy PCG64)."""
+    import hashlib
+    load_ref()
+    out = {}
+    m = importlib.import_module('ref_vtf.detectors.mtcnn')
+    net = _load(m.MTCNN('cpu'), synth.make_params('mtcnn'))
+    for name, n, seed, ms in (('mtcnn_b16_ms5', 16, 100, 5), ('mtcnn_b4_ms20', 4, 101, 20)):
+        frames = synth.make_frames(n, seed=seed)
+        with torch.inference_mode():
+            res = net(list(frames), ms)
+        out[name + '_counts'] = np.array([r.shape[0] for r in res], np.int64)
+        out[name + '_boxes'] = np.concatenate(res).astype(np.float32)
+        print(name, out[name + '_counts'])
+    y = importlib.import_module('ref_vtf.detectors.yolo')
+    ynet = _load(y.YOLOv3('cpu'), synth.make_params('yolo'))
+    frames = synth.make_frames(4, 1080, 1920, seed=102)
+    b, sc, resized = _yolo_ref(ynet, y, frames)
+    out['yolo_1080_b4_counts'] = np.array([len(t) for t in sc], np.int64)
+    out['yolo_1080_b4_boxes'] = np.concatenate(b)
+    out['yolo_1080_b4_scores'] = np.concatenate(sc)
+    out['yolo_1080_b4_resized_sha256'] = np.frombuffer(hashlib.sha256(np.stack(resized).tobytes()).digest(), np.uint8)
+    print('yolo 1080p', out['yolo_1080_b4_counts'])
+    f = importlib.import_module('ref_vtf.encoders.facenet')
+    fnet = _load(f.InceptionResnetV1('cpu'), synth.make_params('facenet'))
+    u8 = torch.from_numpy(_u8(103, (128, 3, 160, 160)))
+    with torch.inference_mode():
+        out['facenet_b128'] = fnet((u8.float() - 127.5) * (1 / 128)).numpy()
+    v = importlib.import_module('ref_vtf.encoders.vit')
+    vnet = _load(v.ViT('cpu', 128, 16, 1024, 24), synth.make_params('vit_l'))
+    u8 = torch.from_numpy(_u8(104, (128, 3, 128, 128)))
+    x = (u8.float() - 127.5) * np.float32(1 / 127.5)
+    with torch.inference_mode():
+        out['vit_l_b8'] = vnet(x[:8]).numpy()
+        out['vit_l_b128'] = vnet(x).numpy()
+    np.savez_compressed(os.path.join(HERE, 'shapes.npz'), **out)
+    print('shapes', {k: v.shape for k, v in out.items()})
+
+
+# BASELINE config 5 chain: YOLO on 1080p frames -> box filter/adjust -> ViT-L on the crops ->
+# cosine dedupe -> KMeans k=2..16 + scores; bench settings of the box filter
+CHAIN = dict(frames=16, det_batch=8, seed=109, mscore=0.4, msize=50, mborder=5, scale=(1.5, 1.5, 2.2, 1.2),
+             square=True)
+
+
+def gen_chain():
+    """Config-5 chain with the reference's own modules end to end (detector, detection.py box
+    logic, ViT, dupes.remove_dupes_overall, sklearn KMeans/scores as cluster_faces calls them);
+    cv2's resizes are the build's INTER_LINEAR restatement (parity-unpinned step)."""
+    import json
+    import sklearn.cluster
+    import sklearn.metrics
+    load_ref()
+    sys.path.insert(0, ROOT)
+    from oracle.facenet import resize_linear_u8
+    c = CHAIN
+    y = importlib.import_module('ref_vtf.detectors.yolo')
+    det = importlib.import_module('ref_vtf.detection')
+    dupes = importlib.import_module('ref_vtf.dupes')
+    v = importlib.import_module('ref_vtf.encoders.vit')
+    ynet = _load(y.YOLOv3('cpu'), synth.make_params('yolo'))
+    vnet = _load(v.ViT('cpu', 128, 16, 1024, 24), synth.make_params('vit_l'))
+    frames = synth.make_frames(c['frames'], 1080, 1920, seed=c['seed'])
+    rects, margins, raw = [], [], []
+    sp = ('', '', None, False, False, False)
+    for j in range(0, c['frames'], c['det_batch']):
+        fb = frames[j:j + c['det_batch']]
+        b, sc, _ = _yolo_ref(ynet, y, fb)
+        for i, (bi, si) in enumerate(zip(b, sc)):
+            rows = np.concatenate([bi, si[:, None]], 1)
+            raw.append(rows)
+            kept = det.filter_boxes(rows, (1080, 1920), c['mscore'], c['msize'], c['mborder'], sp, None, 0)
+            adj = det.adjust_boxes(kept, (1080, 1920), c['scale'], c['square'])
+            rects.extend((j + i, x1, y1, x2, y2) for (x1, y1, x2, y2, _) in adj)
+            # fp32 re-association on the GPU can flip a floor/ceil only for a coordinate within a
+            # few ulp of an integer, and the score gate only for a score within noise of
+            # min_score: record both margins over the boxes the score gate could pass
+            live = si >= c['mscore'] - 1e-3
+            if live.any():
+                margins.append(min(np.abs(bi[live] - np.round(bi[live])).min(), np.abs(si - c['mscore']).min()))
+    rects = np.array(rects, np.int32)
+    blobs = []
+    for f, x1, y1, x2, y2 in rects:
+        r = resize_linear_u8(frames[f, y1:y2, x1:x2], 128)[:, :, ::-1].transpose(2, 0, 1)
+        blobs.append((torch.from_numpy(np.ascontiguousarray(r)).float() - 127.5) * np.float32(1 / 127.5))
+    with torch.inference_mode():
+        X = vnet(torch.stack(blobs)).numpy()
+    names = ['f%05d.jpg' % i for i in range(len(X))]
+    with tempfile.TemporaryDirectory() as td:
+        os.makedirs(os.path.join(td, 'faces'))
+        for n in names:
+            open(os.path.join(td, 'faces', n), 'w').close()
+        _, goods = dupes.remove_dupes_overall(X.copy(), names, ('enc', 0.25, False, td))
+    Dm = sklearn.metrics.pairwise.cosine_distances(X)
+    Dm += (1 - np.tri(len(X), k=-1).astype(Dm.dtype)) * 10000
+    ks = [k for k in range(2, 17) if k <= len(X)]
+    labels, scores = [], []
+    for k in ks:  # grouping.py:97-107 on the gathered embeddings (BASELINE config 5)
+        lb = sklearn.cluster.KMeans(n_clusters=k, random_state=0, n_init='auto').fit(X).labels_
+        labels.append(lb)
+        scores.append((sklearn.metrics.silhouette_score(X, lb), sklearn.metrics.calinski_harabasz_score(X, lb),
+                       sklearn.metrics.davies_bouldin_score(X, lb)))
+    out = dict(params_json=np.array(json.dumps(c)), rects=rects, X=X,
+               dedupe_keep=np.array([int(n[1:6]) for n in goods], np.int64), dedupe_mins=Dm.min(1),
+               dedupe_inds=Dm.argmin(1), k=np.array(ks), labels=np.stack(labels).astype(np.int32),
+               scores=np.array(scores, np.float64), min_int_margin=np.array(min(margins)))
+    np.savez_compressed(os.path.join(HERE, 'chain.npz'), **out)
+    print('chain faces', len(X), 'kept after dedupe', len(goods), 'min |coord - round| %.4g' % min(margins),
+          'best k', ks[int(np.argmax([s[0] for s in scores]))])
+
+
 # (H, W), mscore, msize, mborder, scale, square: the API / CLI / bench settings plus frames
 # smaller than the scaled boxes (square overflow, side > other frame dimension, both
 # orientations) and thresholds whose float32 rounding falls below the Python float (0.7)
@@ -490,6 +636,6 @@ def gen_boxes():
 
 
 if __name__ == '__main__':
-    which = sys.argv[1:] or ['mtcnn', 'facenet', 'vit', 'grouping', 'yolo', 'kmeans', 'rcnn', 'dupes', 'boxes']
+    which = sys.argv[1:] or ['mtcnn', 'facenet', 'vit', 'grouping', 'yolo', 'kmeans', 'rcnn', 'dupes', 'boxes', 'shapes', 'chain']
     for w in which:
         globals()['gen_' + w]()

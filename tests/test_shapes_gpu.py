@@ -1,0 +1,167 @@
+"""GPU parity at the BENCHMARKED shapes (BASELINE configs 2-5), against golden vectors made by
+the reference's own modules (tests/golden/make_golden.py gen_shapes / gen_chain):
+
+* MTCNN 720p, det-batch 16 at min_face_size 5 (config 2) and det-batch 4 at 20 (main.py:18's
+  default batch): batched_nms offsets depend on the batch composition (mtcnn.py:196,205,219);
+* YOLOv3 on 1080p frames, det-batch 4 (configs 3/5 detector at the config-5 frame size);
+* FaceNet fp32 at batch 128 and ViT-L at batch 8 and 128 (the multi-tile / split-K GEMM paths
+  that run at enc-batch 128);
+* the config-5 chain end to end: YOLO 1080p -> device box post-processing -> ViT-L on the device
+  crops -> fused cosine dedupe -> KMeans k=2..16 + scores.
+
+Tolerances: counts / crop rectangles / dedupe argmin and keep sets / KMeans labels exact;
+detector boxes as the per-model tests (MTCNN 2e-3 px, YOLO 1e-2 px, scores 1e-4); embeddings
+1e-4 (fp32 and split-fp16 operand modes); cosine minima 1e-5; scores rtol 1e-5.
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import GOLDEN
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope='module')
+def g():
+    return np.load(os.path.join(GOLDEN, 'shapes.npz'))
+
+
+@pytest.fixture(scope='module')
+def chain():
+    return np.load(os.path.join(GOLDEN, 'chain.npz'))
+
+
+def _u8(seed, shape):
+    return np.random.default_rng(seed).integers(0, 256, shape, dtype=np.uint8)
+
+
+@pytest.mark.parametrize('name,n,seed,ms', [('mtcnn_b16_ms5', 16, 100, 5), ('mtcnn_b4_ms20', 4, 101, 20)])
+def test_mtcnn_benchmark_batches(g, name, n, seed, ms):
+    from videotofaces import synth
+    from videotofaces.detectors.mtcnn import MTCNN
+    frames = synth.make_frames(n, seed=seed)
+    res = MTCNN('cuda:0')(torch.from_numpy(frames).cuda(), ms)
+    np.testing.assert_array_equal([r.shape[0] for r in res], g[name + '_counts'])
+    np.testing.assert_allclose(np.concatenate(res), g[name + '_boxes'], rtol=1e-5, atol=2e-3)
+
+
+def test_mtcnn_b16_device_crops(g):
+    """config 2's hand-off: detect_crops on det-batch 16 == the reference's boxes through the
+    reference box logic (oracle/boxes.py, pinned by tests/golden/boxes.npz).  A crop may differ
+    only where a golden coordinate lies within 2e-3 px of an integer (floor/ceil of a value inside
+    the box tolerance); the test reports how many rows that rule covers."""
+    from oracle.boxes import rows_to_crops
+    from videotofaces import synth, _native as nat
+    from videotofaces.detectors.mtcnn import MTCNN
+    frames = synth.make_frames(16, seed=100)
+    rows = np.split(g['mtcnn_b16_ms5_boxes'], np.cumsum(g['mtcnn_b16_ms5_counts'])[:-1])
+    ref, src = rows_to_crops(rows, (720, 1280), 0.4, 0, 5, (1.5, 1.5, 2.2, 1.2), True)
+    d, counts = MTCNN('cuda:0').detect_crops(torch.from_numpy(frames).cuda(), 5,
+                                             nat.BoxParams.make(0.4, 0, 5, (1.5, 1.5, 2.2, 1.2), True))
+    got = d.cpu().numpy()
+    assert got.shape == ref.shape
+    flat = np.concatenate(rows)
+    start = np.concatenate([[0], np.cumsum(g['mtcnn_b16_ms5_counts'])[:-1]])
+    gidx = start[ref[:, 0]] + src
+    near = (np.abs(flat[gidx, :4] - np.round(flat[gidx, :4])) < 2e-3).any(1)
+    diff = (got != ref).any(1)
+    print('crops', len(ref), 'near-integer rows', int(near.sum()), 'differing', int(diff.sum()))
+    assert not (diff & ~near).any()
+
+
+def test_yolo_1080p_b4(g):
+    from videotofaces import synth
+    from videotofaces.detectors.yolo import YOLOv3
+    frames = synth.make_frames(4, 1080, 1920, seed=102)
+    b, s, c = YOLOv3('cuda:0', precision='fp32')(torch.from_numpy(frames).cuda())
+    np.testing.assert_array_equal([len(t) for t in s], g['yolo_1080_b4_counts'])
+    np.testing.assert_allclose(np.concatenate(b), g['yolo_1080_b4_boxes'], rtol=1e-6, atol=1e-2)
+    np.testing.assert_allclose(np.concatenate(s), g['yolo_1080_b4_scores'], rtol=1e-6, atol=1e-4)
+
+
+def test_facenet_fp32_batch128(g):
+    from videotofaces.encoders.facenet import InceptionResnetV1
+    x = (torch.from_numpy(_u8(103, (128, 3, 160, 160))).float() - 127.5) * (1 / 128)
+    emb = InceptionResnetV1('cuda:0', precision='fp32')(x).cpu().numpy()
+    np.testing.assert_allclose(emb, g['facenet_b128'], rtol=0, atol=1e-4)
+    bf = InceptionResnetV1('cuda:0', precision='bf16')(x).cpu().numpy()
+    cos = (bf * g['facenet_b128']).sum(1) / np.linalg.norm(bf, axis=1)
+    print('facenet bf16 batch 128: cos min %.6f mean %.6f' % (cos.min(), cos.mean()))
+    assert cos.min() > 0.999
+
+
+@pytest.mark.parametrize('precision', ['fp32', 'f16x'])
+def test_vit_l_batches(g, precision):
+    from videotofaces import synth
+    from videotofaces.encoders.vit import ViT
+    m = ViT('cuda:0', synth.make_params('vit_l'), isL=True, precision=precision)
+    x = (torch.from_numpy(_u8(104, (128, 3, 128, 128))).float() - 127.5) * np.float32(1 / 127.5)
+    np.testing.assert_allclose(m(x[:8]).cpu().numpy(), g['vit_l_b8'], rtol=0, atol=1e-4)
+    np.testing.assert_allclose(m(x).cpu().numpy(), g['vit_l_b128'], rtol=0, atol=1e-4)
+
+
+@pytest.mark.parametrize('precision', ['fp32', 'f16x'])
+def test_config5_chain(chain, precision):
+    from videotofaces import synth, dupes
+    from videotofaces.detection import detect_crops
+    from videotofaces.detectors.yolo import YOLOv3
+    from videotofaces.encoders.vit import ViT
+    from videotofaces.grouping import cluster_sweep
+    c = json.loads(str(chain['params_json']))
+    frames = torch.from_numpy(synth.make_frames(c['frames'], 1080, 1920, seed=c['seed'])).cuda()
+    det = YOLOv3('cuda:0', precision='fp32')
+    parts = []
+    for j in range(0, c['frames'], c['det_batch']):
+        d, _ = detect_crops(det, frames[j:j + c['det_batch']], j, c['mscore'], c['msize'], c['mborder'],
+                            tuple(c['scale']), c['square'])
+        parts.append(d)
+    crops = torch.cat(parts)
+    np.testing.assert_array_equal(crops.cpu().numpy(), chain['rects'])
+    enc = ViT('cuda:0', synth.make_params('vit_l'), isL=True, precision=precision)
+    X = enc.encode_crops(frames, crops)
+    np.testing.assert_allclose(X.cpu().numpy(), chain['X'], rtol=0, atol=1e-4)
+    mins, inds = dupes.cosine_dedupe_device(X)
+    np.testing.assert_allclose(mins, chain['dedupe_mins'], rtol=0, atol=1e-5)
+    np.testing.assert_array_equal(inds, chain['dedupe_inds'])
+    np.testing.assert_array_equal(np.nonzero(~(mins <= 0.25))[0], chain['dedupe_keep'])
+    ks = [int(k) for k in chain['k']]
+    labels, scores = cluster_sweep(X.cpu().numpy(), ks, 0)
+    for i, k in enumerate(ks):
+        np.testing.assert_array_equal(labels[i], chain['labels'][i], err_msg='k=%d' % k)
+    np.testing.assert_allclose(np.array([s[1:] for s in scores]), chain['scores'], rtol=1e-5)
+
+
+def test_cosine_dedupe_keep_set_10k():
+    """remove_dupes_overall('enc') at N = 10k (configs 4/5 scale): keep set exact vs the
+    reference's formula (sklearn cosine_distances + strict lower triangle); argmin exact wherever
+    the best earlier face beats the runner-up by more than fp32 GEMM noise (1e-5)."""
+    from oracle import grouping as og
+    from videotofaces import dupes
+    rng = np.random.default_rng(31)
+    N, D = 10000, 512
+    X = rng.normal(0, 1, (N, D)).astype(np.float32)
+    # near-duplicates of earlier rows at cosine distances spread over 0.02 .. 0.5 (both sides of
+    # the 0.25 threshold), away from the threshold by more than the noise
+    src = rng.integers(0, N // 2, 600)
+    dst = rng.choice(np.arange(N // 2, N), 600, replace=False)
+    for s_, d_ in zip(src, dst):
+        t = rng.uniform(0.02, 0.5)
+        noise = rng.normal(0, 1, D).astype(np.float32)
+        X[d_] = X[s_] + noise * np.float32(np.sqrt(2 * t / (1 - t)) * 0.999)  # ~ distance t
+    mins, inds = dupes.cosine_dedupe_device(torch.from_numpy(X).cuda())
+    Dm = og.cosine_lower(X)
+    rm, ri = Dm.min(1), Dm.argmin(1)
+    np.testing.assert_allclose(mins, rm, rtol=0, atol=1e-5)
+    # the keep decision (mins <= 0.25) is exact for every row whose reference minimum is not
+    # within the 1e-5 distance noise of the threshold (the test reports how many are)
+    far = np.abs(rm - 0.25) > 1e-5
+    np.testing.assert_array_equal((mins <= 0.25)[far], (rm <= 0.25)[far])
+    print('rows within 1e-5 of the threshold:', int((~far).sum()))
+    part = np.partition(Dm, 1, axis=1)
+    clear = (part[:, 1] - part[:, 0]) > 1e-5
+    np.testing.assert_array_equal(inds[clear], ri[clear])
+    print('dupes', int((rm <= 0.25).sum()), 'rows with a clear argmin', int(clear.sum()), 'of', N)
