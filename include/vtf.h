@@ -123,6 +123,15 @@ int vtf_boxes_to_crops(const float* d_rows, const int32_t* counts, int B, int H,
 int vtf_batched_nms(const float* d_boxes, const float* d_scores, const int64_t* d_idxs, int64_t n,
                     double iou_threshold, int64_t* d_keep, int64_t* out_nkeep, void* hip_stream);
 
+/* MTCNN._nms_vectorized(boxes, scores, classes, thr, 'Min') with chain suppression
+ * (mtcnn.py:273-309, called at 242): rows sorted by descending score (ties in index order:
+ * the reference's argsort is unstable there), a row is dropped when ANY earlier row of the same
+ * class overlaps it with intersection-over-minimum (+1 pixel widths) > thr (fp32).
+ * d_boxes [n,4] fp32, d_scores [n], d_classes [n] int32 -> d_keep int64 (kept rows in that
+ * order), *out_nkeep. */
+int vtf_iom_nms(const float* d_boxes, const float* d_scores, const int32_t* d_classes, int64_t n, float thr,
+                int64_t* d_keep, int64_t* out_nkeep, void* hip_stream);
+
 /* ---------------------------------------------------------------- FaceNet encoder
  * Replaces FaceNet / InceptionResnetV1 (src/videotofaces/encoders/facenet.py:123-183),
  * called by grouping.py:37 `xk = model(images)`.
@@ -260,6 +269,14 @@ int vtf_rcnn_rpn_heads(vtf_rcnn_t h, const float* d_x, int B, int Hp, int Wp, fl
                        float* d_head2, float* d_head3, float* d_head4);
 /* RPN proposals of the last detect call (rcnn.py:82): host [n,5] (image, x1, y1, x2, y2). */
 int vtf_rcnn_proposals(vtf_rcnn_t h, float* out, int64_t cap, int64_t* out_n);
+/* RegionProposalNetwork.forward after the heads (rcnn.py:49-82: per-level top-1000, decode,
+ * clamp, remove_small, batched_nms(0.7) by (image, level), top-1000 per image) on given head maps
+ * (NHWC fp32 as vtf_rcnn_rpn_heads writes them) of a B x Hp x Wp input whose images are
+ * h_used x w_used: host out [n,5] (image, x1, y1, x2, y2).  The integer path (top-k, NMS keep
+ * sets) can so be checked on identical inputs. */
+int vtf_rcnn_rpn_proposals(vtf_rcnn_t h, const float* d_head0, const float* d_head1, const float* d_head2,
+                           const float* d_head3, const float* d_head4, int B, int Hp, int Wp, int h_used, int w_used,
+                           float* out, int64_t cap, int64_t* out_n);
 /* torchvision.ops.roi_align(fmap, rois, (7,7), spatial_scale, sampling_ratio=0, aligned=True)
  * as roi.py:31 calls it: d_fmap NHWC fp32 [N,H,W,C], d_rois fp32 [R,5] (image, x1, y1, x2, y2)
  * -> d_out NHWC fp32 [R,7,7,C]. */

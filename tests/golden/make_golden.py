@@ -581,6 +581,43 @@ def gen_chain():
           'best k', ks[int(np.argmax([s[0] for s in scores]))])
 
 
+def gen_iom():
+    """MTCNN._nms_vectorized(..., 0.7, 'Min') (mtcnn.py:273-309) of the reference on crafted edge
+    cases -- overlap chains (A~B~C with A, C apart: both B and C go), boxes touching on one pixel
+    row (+1 widths make that an overlap), IoM exactly at the threshold, nested boxes, several
+    classes -- and on random clustered boxes; distinct scores (the reference's argsort is
+    unstable among ties)."""
+    load_ref()
+    m = importlib.import_module('ref_vtf.detectors.mtcnn')
+    net = m.MTCNN('cpu')
+    rng = np.random.default_rng(29)
+    cases = {}
+    crafted = np.array([
+        [0, 0, 9, 9], [6, 0, 15, 9], [12, 0, 21, 9],            # chain: 0~1 (IoM 0.4?), 1~2
+        [30, 30, 39, 39], [39, 30, 48, 39],                     # touch on one column (+1 -> inter 1x10)
+        [50, 50, 59, 59], [50, 50, 59, 59],                     # identical
+        [70, 70, 99, 99], [75, 75, 84, 84],                     # nested: IoM 1
+        [100, 100, 109, 109], [103, 100, 112, 109],             # IoM = 7*10/100 = 0.7 exactly -> kept
+        [120, 120, 129, 129], [122, 120, 131, 129],             # IoM 0.8
+        [0, 0, 9, 9], [6, 0, 15, 9]], np.float32)               # same geometry, other class
+    cls = np.array([0] * 13 + [1, 1], np.int64)
+    sc = rng.permutation(len(crafted)).astype(np.float32) / len(crafted) + 0.01
+    cases['crafted'] = (crafted, sc, cls)
+    for name, n, spread in (('dense', 300, 60.0), ('sparse', 500, 600.0)):
+        ctr = rng.uniform(0, spread, (n, 2)).astype(np.float32)
+        wh = rng.uniform(4, 40, (n, 2)).astype(np.float32)
+        b = np.concatenate([ctr, ctr + wh], 1)
+        cases[name] = (b, rng.permutation(n).astype(np.float32) / n + 0.001, rng.integers(0, 3, n))
+    out = {}
+    for name, (b, sc, cls) in cases.items():
+        with torch.inference_mode():
+            keep = net._nms_vectorized(torch.from_numpy(b), torch.from_numpy(sc), torch.from_numpy(cls), 0.7, 'Min')
+        out[name + '_boxes'], out[name + '_scores'], out[name + '_classes'] = b, sc, cls
+        out[name + '_keep'] = keep.numpy()
+        print('iom', name, len(b), '->', len(keep))
+    np.savez_compressed(os.path.join(HERE, 'iom.npz'), **out)
+
+
 # (H, W), mscore, msize, mborder, scale, square: the API / CLI / bench settings plus frames
 # smaller than the scaled boxes (square overflow, side > other frame dimension, both
 # orientations) and thresholds whose float32 rounding falls below the Python float (0.7)
@@ -636,6 +673,6 @@ def gen_boxes():
 
 
 if __name__ == '__main__':
-    which = sys.argv[1:] or ['mtcnn', 'facenet', 'vit', 'grouping', 'yolo', 'kmeans', 'rcnn', 'dupes', 'boxes', 'shapes', 'chain']
+    which = sys.argv[1:] or ['mtcnn', 'facenet', 'vit', 'grouping', 'yolo', 'kmeans', 'rcnn', 'dupes', 'boxes', 'shapes', 'chain', 'iom']
     for w in which:
         globals()['gen_' + w]()

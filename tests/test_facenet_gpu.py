@@ -62,3 +62,35 @@ def test_encode_crops_vs_oracle(fp32):
         blobs.append((torch.from_numpy(np.ascontiguousarray(r)).float() - 127.5) * (1 / 128))
     ref = inception_resnet_v1(synth.make_params('facenet'), torch.stack(blobs)).numpy()
     np.testing.assert_allclose(emb, ref, atol=1e-4)
+
+
+@pytest.mark.parametrize('area', [None, (0.1, 0.05, 0.9, 0.8)])
+def test_encode_faces_order_vs_oracle(tmp_path, area):
+    """A-E5: grouping.encode_faces (grouping.py:29-40) over face files in batches of 3: the
+    concatenated [N,512] rows are in path order and equal the oracle on the same images (PNG, so
+    the file round trip is lossless), with and without enc_area (utils/image.py:17-22)."""
+    from PIL import Image
+    from videotofaces import synth
+    from videotofaces.encoders.facenet import FaceNet
+    from videotofaces.grouping import encode_faces
+    from oracle.facenet import resize_linear_u8, inception_resnet_v1
+    fr = synth.make_frames(1, 300, 400, seed=12)[0]
+    rects = [(0, 0, 120, 150), (50, 40, 90, 70), (200, 100, 399, 299), (10, 200, 70, 300), (300, 0, 400, 64),
+             (120, 120, 280, 280), (5, 5, 37, 29)]
+    paths = []
+    for i, (x1, y1, x2, y2) in enumerate(rects):
+        p = str(tmp_path / ('face_%02d.png' % i))
+        Image.fromarray(np.ascontiguousarray(fr[y1:y2, x1:x2, ::-1])).save(p)  # BGR frame -> RGB file
+        paths.append(p)
+    X = encode_faces(paths, FaceNet('cuda:0'), 3, area)
+    blobs = []
+    for x1, y1, x2, y2 in rects:
+        im = fr[y1:y2, x1:x2]
+        if area:
+            h, w = im.shape[:2]
+            im = im[int(area[1] * h):int(area[3] * h + 1), int(area[0] * w):int(area[2] * w + 1)]
+        r = resize_linear_u8(im, 160)[:, :, ::-1].transpose(2, 0, 1)
+        blobs.append((torch.from_numpy(np.ascontiguousarray(r)).float() - 127.5) * (1 / 128))
+    ref = inception_resnet_v1(synth.make_params('facenet'), torch.stack(blobs)).numpy()
+    assert X.shape == (len(rects), 512)
+    np.testing.assert_allclose(X, ref, rtol=0, atol=1e-4)

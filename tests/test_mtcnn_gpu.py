@@ -153,3 +153,15 @@ def test_detect_device_frames_and_strided_view(model):
     for x, y, z in zip(a, b, c):
         np.testing.assert_array_equal(x, y)
         np.testing.assert_array_equal(x, z)
+
+
+@pytest.mark.parametrize('case', ['crafted', 'dense', 'sparse'])
+def test_iom_chain_nms_vs_reference(case):
+    """A-M12 edge cases: MTCNN._nms_vectorized(..., 0.7, 'Min') of the reference (chains, one-pixel
+    touches counted by the +1 widths, IoM exactly 0.7 kept, identical and nested boxes, several
+    classes) -- the device kernel (vtf_iom_nms) keeps exactly the same rows in the same order."""
+    from videotofaces.detectors.mtcnn import nms_iom
+    gi = np.load(os.path.join(GOLDEN, 'iom.npz'))
+    b, s, c = (torch.from_numpy(gi[case + k]).cuda() for k in ('_boxes', '_scores', '_classes'))
+    keep = nms_iom(b, s, c, 0.7).cpu().numpy()
+    np.testing.assert_array_equal(keep, gi[case + '_keep'])

@@ -253,3 +253,14 @@ def test_pack_hashes_roundtrip():
     assert P.dtype == np.uint64
     for h, p in zip(H, P):
         np.testing.assert_array_equal(unpack_hash(p), h)
+
+
+@pytest.mark.parametrize('case', ['crafted', 'dense', 'sparse'])
+def test_oracle_iom_chain_vs_reference(case):
+    """oracle.mtcnn.nms_iom_chain (mtcnn.py:273-309 restated) vs the reference's own
+    _nms_vectorized on edge cases (tests/golden/iom.npz)."""
+    from oracle import mtcnn as om
+    gi = np.load(os.path.join(GOLDEN, 'iom.npz'))
+    keep = om.nms_iom_chain(torch.from_numpy(gi[case + '_boxes']), torch.from_numpy(gi[case + '_scores']),
+                            torch.from_numpy(gi[case + '_classes']), 0.7)
+    np.testing.assert_array_equal(np.asarray(keep), gi[case + '_keep'])

@@ -77,19 +77,59 @@ def _match_rows(a, b, atol):
     return float((d.min(1) <= atol).mean())
 
 
+def test_rpn_selection_exact_on_same_heads(det):
+    """A-R2's integer path on identical inputs: the device RPN selection (per-level top-1000,
+    decode, clamp, remove_small, batched_nms(0.7) by (image, level), top-1000 per image;
+    rcnn.py:49-82) and the oracle's restatement (pinned to the reference's own RPN by
+    tests/golden/rcnn.npz) fed the SAME head maps of two 720p frames keep the same proposal set
+    per image (boxes within 1e-3 px: exp() ulps in the decode).  The rule that permits a
+    difference in ORDER: the objectness is sigmoid(logit) = 1 / (1 + exp(-logit)) in fp32 and
+    torch's CPU exp (SLEEF, vectorised) and the device expf may differ in the last ulp, so two
+    proposals whose scores coincide in one and not the other trade places (stable sort by score).
+    The set is asserted exact; the displaced rows are counted and bounded."""
+    from videotofaces import synth
+    from videotofaces.detectors.rcnn import input_size
+    from oracle import rcnn as orc
+    fr = torch.from_numpy(synth.make_frames(2, seed=0)).cuda()
+    hu, wu, Hp, Wp = input_size(720, 1280)
+    x = det.preprocess(fr)[..., :3].permute(0, 3, 1, 2).contiguous()
+    heads = det.rpn_heads(x, raw=True)
+    pb, pi = det.rpn_proposals(heads, Hp, Wp, hu, wu)
+    regs, logs = [], []
+    for t in heads:
+        t = t.cpu().reshape(2, -1, 15)
+        logs.append(t[..., :3].reshape(2, -1, 1))
+        regs.append(t[..., 3:].reshape(2, -1, 4))
+    with torch.inference_mode():
+        rb, ri = orc.rpn_select(regs, logs, orc.priors((Hp, Wp)), [(hu, wu)] * 2)
+    rb, ri = rb.numpy(), ri.numpy()
+    np.testing.assert_array_equal(pi, ri)
+    moved = 0
+    for i in range(2):
+        a, b = pb[pi == i], rb[ri == i]
+        oa, ob = np.lexsort(a.T[::-1]), np.lexsort(b.T[::-1])
+        np.testing.assert_allclose(a[oa], b[ob], rtol=0, atol=1e-3)
+        moved += int((np.abs(a - b).max(1) > 1e-3).sum())
+    print('proposals', len(pb), 'at a different position', moved)
+    assert moved <= 0.05 * len(pb)
+
+
 def test_detect_e2e_vs_golden(det, g):
     from videotofaces import synth
     fr = synth.make_frames(2, seed=0)
     b, s, c = det(fr)
     props, pimg = det.proposals()
-    # RPN: same per-image proposal counts; >= 99% of proposals shared (boundary swaps of the
-    # per-level top-1000 when two logits differ by less than the fp32 summation noise)
+    # RPN from frames: same per-image proposal counts and the same proposal set (order-free, boxes
+    # within 1e-2 px).  The head convs' fp32 summation order differs from oneDNN's, so in general
+    # two logits closer than that noise at a per-level top-1000 boundary (193,536 anchors at level
+    # 0) could trade places; on this fixture none do, and the selection itself is exact on
+    # identical heads (test_rpn_selection_exact_on_same_heads)
     for i in range(2):
         pa, pb = props[pimg == i], g['proposals'][g['prop_imidx'] == i]
         assert len(pa) == len(pb)
         frac = _match_rows(pa, pb, 1e-2)
         print('image %d proposals matched %.4f' % (i, frac))
-        assert frac >= 0.99
+        assert frac == 1.0
     assert [len(t) for t in s] == list(g['counts'])
     np.testing.assert_allclose(np.concatenate(b), g['boxes'], rtol=1e-6, atol=1e-2)
     np.testing.assert_allclose(np.concatenate(s), g['scores'], rtol=1e-6, atol=1e-4)

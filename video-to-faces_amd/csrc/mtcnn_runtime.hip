@@ -78,6 +78,10 @@ __global__ __launch_bounds__(1024) void k_mtcnn_rows(const int32_t* __restrict__
     }
 }
 
+__global__ void k_gather_order(const int32_t* order, const int32_t* pos, int64_t n, int64_t* out) {
+    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) out[i] = order[pos[i]];
+}
 __global__ void k_gather_rows(const int32_t* idx, int64_t n, const float* in, int row, float* out) {
     int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n * row) return;
@@ -772,6 +776,37 @@ int vtf_mtcnn_detect_crops(vtf_mtcnn_t h, const uint8_t* frames, int frames_on_d
         VTF_CHECK(r.n == 0 || d_crops, VTF_E_ARG, "null argument");
         rows_to_crops(h->m.ar, S_BOXPOST, r.rows, r.counts, H, W, *params, frame_offset, d_crops, nullptr,
                       out_frame_counts, cap, out_n, h->m.st);
+    });
+}
+
+int vtf_iom_nms(const float* d_boxes, const float* d_scores, const int32_t* d_classes, int64_t n, float thr,
+                int64_t* d_keep, int64_t* out_nkeep, void* hip_stream) {
+    return guarded_on(stream_device((hipStream_t)hip_stream), [&] {
+        VTF_CHECK(out_nkeep && n >= 0 && n < ((int64_t)1 << 31), VTF_E_ARG, "bad argument");
+        *out_nkeep = 0;
+        if (n == 0) return;
+        VTF_CHECK(d_boxes && d_scores && d_classes && d_keep, VTF_E_ARG, "null argument");
+        hipStream_t st = (hipStream_t)hip_stream;
+        StreamScratch sc = stream_scratch(st);
+        Arena& ar = *sc.ar;
+        uint64_t* kk = ar.get<uint64_t>(80, n);
+        uint64_t* kk2 = ar.get<uint64_t>(81, n);
+        int32_t* io = ar.get<int32_t>(82, n);
+        int32_t* order = ar.get<int32_t>(83, n);
+        int32_t* flag = ar.get<int32_t>(84, n);
+        int32_t* incl = ar.get<int32_t>(85, n);
+        int32_t* pos = ar.get<int32_t>(86, n);
+        k_desc_keys<<<cdiv(n, 256), 256, 0, st>>>(d_scores, n, kk);
+        k_iota<<<cdiv(n, 256), 256, 0, st>>>(io, n);
+        sort_u64_pairs(ar, 87, kk, kk2, io, order, n, 32, st);
+        launch_iom_chain((const float4*)d_boxes, d_classes, order, n, thr, flag, st);
+        inclusive_scan_i32(ar, 88, flag, incl, n, st);
+        launch_flag_compact(flag, incl, n, pos, st);
+        int32_t nf = 0;
+        d2h_sync(&nf, incl + n - 1, 4, st);
+        k_gather_order<<<cdiv(std::max(nf, 1), 256), 256, 0, st>>>(order, pos, nf, d_keep);
+        VTF_HIP(hipStreamSynchronize(st));
+        *out_nkeep = nf;
     });
 }
 

@@ -1025,6 +1025,33 @@ int vtf_rcnn_proposals(vtf_rcnn_t h, float* out, int64_t cap, int64_t* out_n) {
     });
 }
 
+int vtf_rcnn_rpn_proposals(vtf_rcnn_t h, const float* d_head0, const float* d_head1, const float* d_head2,
+                           const float* d_head3, const float* d_head4, int B, int Hp, int Wp, int h_used, int w_used,
+                           float* out, int64_t cap, int64_t* out_n) {
+    return guarded_on(h ? h->r.device : -1, [&] {
+        VTF_CHECK(h && d_head0 && d_head1 && d_head2 && d_head3 && d_head4 && out_n && B > 0, VTF_E_ARG,
+                  "bad argument");
+        VTF_CHECK(Hp % 32 == 0 && Wp % 32 == 0 && h_used > 0 && w_used > 0 && h_used <= Hp && w_used <= Wp,
+                  VTF_E_ARG, "rcnn: bad input size");
+        float* heads[R_LEVELS] = {(float*)d_head0, (float*)d_head1, (float*)d_head2, (float*)d_head3,
+                                  (float*)d_head4};
+        RMap P[R_LEVELS];
+        int hh = Hp / 4, ww = Wp / 4;
+        for (int l = 0; l < R_LEVELS; l++) {
+            P[l] = RMap{nullptr, hh, ww};
+            hh = (hh - 1) / 2 + 1;
+            ww = (ww - 1) / 2 + 1;
+        }
+        float4* props = nullptr;
+        int32_t* pimg = nullptr;
+        rpn_proposals(h->r, heads, P, B, h_used, w_used, &props, &pimg);
+        int64_t n = (int64_t)h->r.last_props.size() / 5;
+        *out_n = n;
+        VTF_CHECK(n <= cap, VTF_E_CAPACITY, "output capacity too small");
+        if (n) std::memcpy(out, h->r.last_props.data(), n * 20);
+    });
+}
+
 int vtf_roi_align(const float* d_fmap, int N, int H, int W, int C, const float* d_rois, int64_t R, float spatial_scale,
                   float* d_out, void* hip_stream) {
     return guarded([&] {

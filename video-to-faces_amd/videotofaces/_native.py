@@ -74,6 +74,7 @@ SIGNATURES = {
     'vtf_yolo_profile': [_p, _i32, _p, _p, _p, _p],
     'vtf_cosine_classify': [_p, _i64, _p, _i64, _i64, _p, _p, _p],
     'vtf_ahash_crops': [_p, _i32, _i32, _i32, _i64, _i64, _p, _i64, _p, _p],
+    'vtf_iom_nms': [_p, _p, _p, _i64, _f32, _p, _p, _p],
     'vtf_boxes_to_crops': [_p, _p, _i32, _i32, _i32, _p, _i32, _p, _p, _p, _i64, _p, _p],
     'vtf_mtcnn_detect_crops': [_p, _p, _i32, _i32, _i32, _i32, _i64, _i64, _f64, _p, _i32, _p, _p, _i64, _p],
     'vtf_yolo_detect_crops': [_p, _p, _i32, _i32, _i32, _i32, _i64, _i64, _p, _i32, _p, _p, _i64, _p],
@@ -88,6 +89,7 @@ SIGNATURES = {
     'vtf_rcnn_rpn_heads': [_p, _p, _i32, _i32, _i32, _p, _p, _p, _p, _p],
     'vtf_rcnn_proposals': [_p, _p, _i64, _p],
     'vtf_roi_align': [_p, _i32, _i32, _i32, _i32, _p, _i64, _f32, _p, _p],
+    'vtf_rcnn_rpn_proposals': [_p, _p, _p, _p, _p, _p, _i32, _i32, _i32, _i32, _i32, _p, _i64, _p],
     'vtf_rcnn_profile': [_p, _i32, _p, _p, _p, _p],
 }
 _RESTYPE = {'vtf_last_error': _c.c_char_p}

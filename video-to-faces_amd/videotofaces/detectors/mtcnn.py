@@ -158,6 +158,21 @@ class RealMTCNN():
         return self.model.detect_crops(frames, self.minsize, box_params, frame_offset)
 
 
+def nms_iom(boxes, scores, classes, thresh):
+    """MTCNN._nms_vectorized(boxes, scores, classes, thresh, 'Min') (mtcnn.py:273-309, chain
+    suppression) on device tensors, via vtf_iom_nms -> int64 keep indices."""
+    dev = boxes.device
+    b = boxes[:, :4].to(torch.float32).contiguous()
+    s = scores.to(torch.float32).contiguous()
+    c = classes.to(torch.int32).contiguous()
+    n = b.shape[0]
+    keep = torch.empty(max(n, 1), dtype=torch.int64, device=dev)
+    nk = ctypes.c_int64(0)
+    nat.check(nat.lib().vtf_iom_nms(nat.ptr(b), nat.ptr(s), nat.ptr(c), n, float(thresh), nat.ptr(keep),
+                                    ctypes.byref(nk), nat.stream_ptr(dev)))
+    return keep[:nk.value]
+
+
 def batched_nms(boxes, scores, idxs, iou_threshold):
     """torchvision.ops.batched_nms on device tensors, via vtf_batched_nms."""
     dev = boxes.device

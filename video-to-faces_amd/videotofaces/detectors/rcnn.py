@@ -110,9 +110,9 @@ class FasterRCNN:
                                                 frames_dev.stride(1), nat.ptr(out)))
         return out
 
-    def rpn_heads(self, x):
+    def rpn_heads(self, x, raw=False):
         """x: NCHW fp32 [B,3,Hp,Wp] -> per level (reg [B,h*w*3,4], log [B,h*w*3,1]) like
-        RegionProposalNetwork.head (rcnn.py:42-47)."""
+        RegionProposalNetwork.head (rcnn.py:42-47); raw=True: the NHWC [B,h,w,15] head maps."""
         x = x.to(self.device, torch.float32).contiguous()
         B, _, Hp, Wp = x.shape
         h, w, heads = Hp // 4, Wp // 4, []
@@ -121,6 +121,8 @@ class FasterRCNN:
             h, w = (h - 1) // 2 + 1, (w - 1) // 2 + 1
         self._bind_stream()
         nat.check(nat.lib().vtf_rcnn_rpn_heads(self._h, nat.ptr(x), B, Hp, Wp, *[nat.ptr(t) for t in heads]))
+        if raw:
+            return heads
         out = []
         for t in heads:
             t = t.reshape(B, -1, 15)
@@ -128,6 +130,21 @@ class FasterRCNN:
             reg = t[..., 3:].reshape(B, -1, 4)
             out.append((reg, log))
         return out
+
+    def rpn_proposals(self, heads_nhwc, Hp, Wp, h_used, w_used):
+        """RPN selection (rcnn.py:49-82) from given head maps (NHWC [B,h,w,15] device tensors, as
+        rpn_heads computes them) -> (boxes f32 [n,4], image index int64 [n])."""
+        hs = [t.to(self.device, torch.float32).contiguous() for t in heads_nhwc]
+        B = hs[0].shape[0]
+        L = nat.lib()
+        cap = 1000 * B
+        n = ctypes.c_int64(0)
+        buf = np.empty((cap, 5), np.float32)
+        self._bind_stream()
+        nat.check(L.vtf_rcnn_rpn_proposals(self._h, *[nat.ptr(t) for t in hs], B, Hp, Wp, h_used, w_used,
+                                           buf.ctypes.data, cap, ctypes.byref(n)))
+        buf = buf[:n.value]
+        return buf[:, 1:].copy(), buf[:, 0].astype(np.int64)
 
     def proposals(self):
         """RPN proposals of the last call: (boxes f32 [n,4], image index int64 [n])."""
