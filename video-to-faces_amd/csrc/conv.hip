@@ -18,6 +18,7 @@
 // split-K over blockIdx.z for grids that cannot fill the chip.  Epilogue staged through LDS:
 // each thread finishes 8 consecutive channels of a row (16/32-byte residual loads / stores).
 #include <algorithm>
+#include <cstdlib>
 #include <map>
 #include <mutex>
 #include <unordered_map>
@@ -180,9 +181,25 @@ __global__ __launch_bounds__(256) void k_conv(ConvParams p) {
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int wm = wave >> 1, wn = wave & 1;
-    // XCD-friendly order is irrelevant here (weights are L2/MALL resident); plain mapping
-    const int64_t m0 = (int64_t)blockIdx.x * BM;
-    const int n0 = blockIdx.y * BN;
+    // XCD-aware tile order: workgroups are dealt to the 8 XCDs round-robin in dispatch order
+    // (linear id % 8), each XCD with its own L2.  Re-number so that every XCD owns one
+    // contiguous run of tiles and walks it in groups of group_m M-tiles x all N-tiles: the A
+    // row-blocks and B column-blocks its resident workgroups share stay in its L2.  (Placement
+    // only affects speed; any bijection is correct.)
+    int tile_m = blockIdx.x, tile_n = blockIdx.y;
+    if (p.group_m > 0) {
+        const int gx = gridDim.x, gy = gridDim.y;
+        const int lin = blockIdx.x + gx * blockIdx.y, total = gx * gy;
+        const int xcd = lin & 7, loc = lin >> 3, per = total >> 3, rem = total & 7;
+        const int L = xcd < rem ? xcd * (per + 1) + loc : rem * (per + 1) + (xcd - rem) * per + loc;
+        const int span = p.group_m * gy;
+        const int first = (L / span) * p.group_m;
+        const int gsz = min(gx - first, p.group_m);
+        tile_m = first + (L % span) % gsz;
+        tile_n = (L % span) / gsz;
+    }
+    const int64_t m0 = (int64_t)tile_m * BM;
+    const int n0 = tile_n * BN;
     const T* __restrict__ in = (const T*)p.in;
     const T* __restrict__ wt = (const T*)p.w;
     const int ics = p.in_cstride ? p.in_cstride : p.Cin;
@@ -494,6 +511,15 @@ static float* splitk_workspace(hipStream_t st, size_t bytes) {
     return e.first;
 }
 
+// M-tile group height of the XCD-aware tile order (VTF_CONV_GROUP_M overrides; 0 = plain)
+static int conv_group_m() {
+    static int g = [] {
+        const char* e = std::getenv("VTF_CONV_GROUP_M");
+        return e ? std::atoi(e) : 8;
+    }();
+    return g;
+}
+
 // split factor: grids far below the CU count (FaceNet Block17/Block8, YOLO/R-CNN deep stages at
 // small batch) are split along K into up to 8 slices so ~2 workgroups land on every CU. bf16
 // (perf) mode only: the fp32 parity mode keeps the single-pass summation order.
@@ -512,6 +538,7 @@ static void launch_tile(const ConvParams& p0, hipStream_t st) {
     p.split = pick_split(gx * gy, KT, sizeof(T) == 2 || (p.split_fp32 && !p.f16x));
     p.ws = nullptr;
     if (p.split > 1) p.ws = splitk_workspace(st, (size_t)p.split * p.M * p.Cout * sizeof(float));
+    p.group_m = conv_group_m();
     dim3 g((unsigned)gx, (unsigned)gy, (unsigned)p.split);
     if (p.split > 1) {
         k_conv<T, BM, BN, BK, true><<<g, 256, 0, st>>>(p);

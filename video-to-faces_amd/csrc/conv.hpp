@@ -31,6 +31,7 @@ struct ConvParams {
     int split_fp32;      // allow split-K in fp32 mode too (slice-order reduction: deterministic, but the
                          // summation order differs from the single pass; used where parity is a tolerance)
     int split;           // split-K factor (set by launch_conv; > 1: raw partial sums to ws)
+    int group_m;         // XCD-aware tile order: M-tile group height (0 = plain blockIdx mapping; set by launch_conv)
     float* ws;           // fp32 [split][M][Cout] partial sums (split-K only)
     int64_t M;           // N*OH*OW
     int N, H, W, Cin, OH, OW, Cout, KH, KW, sh, sw, ph, pw, K;
