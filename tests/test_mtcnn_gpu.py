@@ -165,3 +165,19 @@ def test_iom_chain_nms_vs_reference(case):
     b, s, c = (torch.from_numpy(gi[case + k]).cuda() for k in ('_boxes', '_scores', '_classes'))
     keep = nms_iom(b, s, c, 0.7).cpu().numpy()
     np.testing.assert_array_equal(keep, gi[case + '_keep'])
+
+
+@pytest.mark.parametrize('ms', [5, 20])
+def test_fused_candidate_nets_match_layer_path(ms, monkeypatch):
+    """The fused RNet/ONet front half (crop .. conv2 + pool2 in LDS, mtcnn_cand.hip; opt-in with
+    VTF_MTCNN_FUSED=1) against the default layer-by-layer path on the same 720p frames: same
+    detections, boxes and scores within the fp32-grade tolerance of the e2e golden test."""
+    from videotofaces import synth
+    from videotofaces.detectors.mtcnn import MTCNN
+    fr = torch.from_numpy(synth.make_frames(4, seed=21)).cuda()
+    b = MTCNN('cuda:0')(fr, ms)
+    monkeypatch.setenv('VTF_MTCNN_FUSED', '1')
+    a = MTCNN('cuda:0')(fr, ms)
+    assert [x.shape for x in a] == [y.shape for y in b]
+    for x, y in zip(a, b):
+        np.testing.assert_allclose(x, y, rtol=1e-5, atol=2e-3)

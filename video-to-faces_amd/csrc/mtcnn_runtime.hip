@@ -117,7 +117,10 @@ struct Mtcnn {
     // weights; 2 split-fp16 guarded: a device flag reports an operand >= 2^14 and the net re-runs
     // in fp32
     int cand_x[2] = {0, 0};
-    int* d_ovf = nullptr;
+    int* d_ovf = nullptr;  // [0] conv-layer guard, [1] fused front-half guard
+    // fused RNet / ONet front half (mtcnn_cand.hip); used when the split mode is allowed
+    CandFusedW cf[2]{};
+    bool fused = false;
     ~Mtcnn() {
         for (void* p : allocs) (void)hipFree(p);
         if (ev0) (void)hipEventDestroy(ev0);
@@ -278,7 +281,46 @@ static void build_weights(Mtcnn& m, const float* params, int64_t n_params) {
         const double o1 = bound(29, 32, 27, 1.0), o2 = bound(32, 64, 32 * 9, o1), o3 = bound(35, 64, 64 * 9, o2),
                      o4 = bound(38, 128, 64 * 4, o3);
         m.cand_x[1] = !allow_x ? 0 : (o1 < 16384.0 && o2 < 16384.0 && o3 < 16384.0 && o4 < 16384.0 ? 1 : 2);
-        VTF_HIP(hipMalloc((void**)&m.d_ovf, 4));
+        VTF_HIP(hipMalloc((void**)&m.d_ovf, 8));
+        // the fused front half is opt-in (VTF_MTCNN_FUSED=1): correct (tests/test_mtcnn_gpu.py) but
+        // measured slower than the layer path on MI355X (ONet 347 vs ~300 ns per candidate chip-wide,
+        // RNet 93 vs ~80; profiles/r02b_probe_cand.txt): at 137 KB of LDS one workgroup per CU
+        // cannot hide its own barrier / LDS latency
+        const char* fz = std::getenv("VTF_MTCNN_FUSED");
+        m.fused = fz && fz[0] == '1';
+        // split fp16 planes of conv1 ([2][32][64], k = ky*16 + kx*4 + c) and conv2 ([2][C2][288],
+        // k = tap*32 + ci) for the fused front half
+        auto split_to = [&](std::vector<uint16_t>& h, size_t i0, size_t i1, float w) {
+            const _Float16 w0 = (_Float16)w;
+            const _Float16 w1 = (_Float16)((w - (float)w0) * 2048.f);
+            std::memcpy(&h[i0], &w0, 2);
+            std::memcpy(&h[i1], &w1, 2);
+        };
+        auto upload = [&](const std::vector<uint16_t>& h) {
+            uint16_t* d = nullptr;
+            VTF_HIP(hipMalloc((void**)&d, h.size() * 2));
+            VTF_HIP(hipMemcpy(d, h.data(), h.size() * 2, hipMemcpyHostToDevice));
+            m.allocs.push_back((void*)d);
+            return (const _Float16*)d;
+        };
+        for (int net = 0; net < 2; net++) {
+            const int wc1 = net ? 29 : 13, wc2 = net ? 32 : 16;
+            const int co1 = net ? 32 : 28, ci2 = co1, co2 = net ? 64 : 48;
+            std::vector<uint16_t> h1((size_t)2 * 32 * 64, 0), h2((size_t)2 * co2 * 288, 0);
+            for (int co = 0; co < co1; co++)
+                for (int c = 0; c < 3; c++)
+                    for (int ky = 0; ky < 3; ky++)
+                        for (int kx = 0; kx < 3; kx++)
+                            split_to(h1, (size_t)co * 64 + ky * 16 + kx * 4 + c, (size_t)(32 + co) * 64 + ky * 16 + kx * 4 + c,
+                                     raw[wc1][((co * 3 + c) * 3 + ky) * 3 + kx]);
+            for (int co = 0; co < co2; co++)
+                for (int ci = 0; ci < ci2; ci++)
+                    for (int t = 0; t < 9; t++)
+                        split_to(h2, (size_t)co * 288 + t * 32 + ci, (size_t)(co2 + co) * 288 + t * 32 + ci,
+                                 raw[wc2][((size_t)co * ci2 + ci) * 9 + t]);
+            const auto& L = net ? m.ol : m.rl;
+            m.cf[net] = CandFusedW{upload(h1), L[0].b, L[0].a, upload(h2), L[1].b, L[1].a};
+        }
     }
     {
         const double b1 = bound(0, 10, 27, 1.0), b2 = bound(3, 16, 90, b1);
@@ -357,6 +399,7 @@ static void run_candidates(Mtcnn& m, bool onet, const float* x0, int64_t n, floa
     if (n <= 0) return;
     const int xmode = force_fp32 ? 0 : m.cand_x[onet ? 1 : 0];
     if (xmode == 2) VTF_HIP(hipMemsetAsync(m.d_ovf, 0, 4, m.st));
+    const int npool_done = first == 2 ? 2 : 0;  // the fused front half ends with pool2
     const int S = onet ? 48 : 24;
     const auto& Ls = onet ? m.ol : m.rl;
     // pools after each conv except the last two of RNet / last two of ONet
@@ -370,6 +413,9 @@ static void run_candidates(Mtcnn& m, bool onet, const float* x0, int64_t n, floa
     if (first == 1) {
         H = W = cand_front_side(onet);
         C = 32;
+    } else if (first == 2) {
+        H = W = cand_fused_side(onet);
+        C = onet ? 64 : 48;
     }
     for (size_t li = first; li < Ls.size(); li++) {
         const auto& L = Ls[li];
@@ -401,7 +447,7 @@ static void run_candidates(Mtcnn& m, bool onet, const float* x0, int64_t n, floa
         W = p.OW;
         C = L.cout;
         cur = out;
-        if ((int)li < npool) {
+        if ((int)li < npool && (int)li >= npool_done) {
             float* pout = (out == X) ? Y : X;
             int OH, OW;
             launch_maxpool_ks(out, (int)n, H, W, C, pk[li], 2, true, pout, OH, OW, m.st);
@@ -424,6 +470,34 @@ static void run_candidates(Mtcnn& m, bool onet, const float* x0, int64_t n, floa
         launch_heads(cur, n, C, m.oh1w, m.oh1b, m.oh2w, m.oh2b, m.oh3w, m.oh3b, prob, reg, lm, m.st);
     else
         launch_heads(cur, n, C, m.rh1w, m.rh1b, m.rh2w, m.rh2b, nullptr, nullptr, prob, reg, nullptr, m.st);
+}
+
+// stage 2 / 3 nets on the stage's candidates (mtcnn.py:213-216 / 228-230): the fused front half
+// (crop .. pool2 in LDS, split fp16) + the remaining layers batched; on a fused-guard trip
+// (an operand beyond the fp16 range) or without the split mode, the layer-by-layer path.
+static void cand_nets(Mtcnn& m, bool onet, const int4* sat, int H, int W, const float4* boxes, const int32_t* img,
+                      int64_t n, float4* reg, float* lm, float* prob, int32_t* err) {
+    if (n <= 0) return;
+    hipStream_t st = m.st;
+    const int net = onet ? 1 : 0;
+    if (m.fused && m.cand_x[net] != 0) {
+        const int P2 = cand_fused_side(onet), C2 = onet ? 64 : 48;
+        float* x2 = m.ar.get<float>(S_CROP, (size_t)n * P2 * P2 * C2);
+        VTF_HIP(hipMemsetAsync(m.d_ovf + 1, 0, 4, st));
+        launch_cand_fused(onet, sat, H, W, boxes, img, n, m.cf[net], x2, err, m.d_ovf + 1, st);
+        run_candidates(m, onet, x2, n, reg, lm, prob, 2);
+        int f_ovf = 0;
+        VTF_HIP(hipMemcpyAsync(&f_ovf, m.d_ovf + 1, 4, hipMemcpyDeviceToHost, st));
+        VTF_HIP(hipStreamSynchronize(st));
+        if (!f_ovf) return;
+        VTF_HIP(hipMemsetAsync(err, 0, 4, st));
+    }
+    const int P = cand_front_side(onet);
+    float* x0 = m.ar.get<float>(S_CROP, (size_t)n * P * P * 32);
+    const int rl = net;
+    launch_cand_front(onet, sat, H, W, boxes, img, n, m.fw[rl], onet ? m.ol[0].b : m.rl[0].b,
+                      onet ? m.ol[0].a : m.rl[0].a, x0, err, st);
+    run_candidates(m, onet, x0, n, reg, lm, prob, 1, m.fused && m.cand_x[net] != 0 ? 1 : 0);
 }
 
 // MTCNN._scale_pyramid (mtcnn.py:141-148): Python double math, int() truncation
@@ -609,12 +683,7 @@ static void detect(Mtcnn& m, const uint8_t* frames, int on_dev, int B, int H, in
     float4* reg = m.ar.get<float4>(S_REG, k2);
     int32_t* err = m.ar.get<int32_t>(S_ERR, 1);
     VTF_HIP(hipMemsetAsync(err, 0, 4, st));
-    {
-        const int P = cand_front_side(false);
-        float* x0 = m.ar.get<float>(S_CROP, (size_t)k2 * P * P * 32);
-        launch_cand_front(false, sat, H, W, b1, i1, k2, m.fw[0], m.rl[0].b, m.rl[0].a, x0, err, st);
-        run_candidates(m, false, x0, k2, reg, nullptr, prob, 1);
-    }
+    cand_nets(m, false, sat, H, W, b1, i1, k2, reg, nullptr, prob, err);
     int32_t nerr = 0;
     d2h_sync(&nerr, err, 4, st);
     VTF_CHECK(nerr == 0, VTF_E_DEGENERATE,
@@ -635,12 +704,7 @@ static void detect(Mtcnn& m, const uint8_t* frames, int on_dev, int B, int H, in
     reg = m.ar.get<float4>(S_REG, k3);
     float* lm = m.ar.get<float>(S_LM, k3 * 10);
     VTF_HIP(hipMemsetAsync(err, 0, 4, st));
-    {
-        const int P = cand_front_side(true);
-        float* x0 = m.ar.get<float>(S_CROP, (size_t)k3 * P * P * 32);
-        launch_cand_front(true, sat, H, W, b1, i1, k3, m.fw[1], m.ol[0].b, m.ol[0].a, x0, err, st);
-        run_candidates(m, true, x0, k3, reg, lm, prob, 1);
-    }
+    cand_nets(m, true, sat, H, W, b1, i1, k3, reg, lm, prob, err);
     d2h_sync(&nerr, err, 4, st);
     VTF_CHECK(nerr == 0, VTF_E_DEGENERATE,
               "stage 3: a candidate box lies outside the frame; the reference skips it in "
