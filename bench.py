@@ -403,7 +403,7 @@ class EncodePipeline:
         self.crops_u8 = torch.from_numpy(synth.make_crops(self.pool_n, 224, seed=1 + rank)).to(dev)
         self.boxes = torch.tensor([[i, 0, 0, 224, 224] for i in range(self.pool_n)], dtype=torch.int32, device=dev)
         self.enc = _make_encoder(args, dev)
-        self.D = self.enc.dim
+        self.D = 512 if args.enc_model == 'facenet' else self.enc.dim
 
     def run(self, first, n):
         stats, parts = [], []
@@ -525,6 +525,13 @@ def roofline_det(args, pipe, shared, solo):
 
 
 def roofline_enc(args, ms_per_step):
+    if args.enc_model == 'facenet':
+        peak = BF16_PEAK_TFLOPS if args.enc_precision == 'bf16' else FP32_PEAK_TFLOPS
+        ach = 2.835 * args.enc_batch / ms_per_step  # 2.835 GFLOP per face
+        return {'kernel': 'whole FaceNet encoder step (blob + k_conv %s + pools + head)' % args.enc_precision,
+                'bound': 'mfma', 'achieved': round(ach, 3), 'peak': peak, 'unit': 'TFLOP/s',
+                'frac': round(ach / peak, 4), 'traffic': None, 'avg_launch_ms': round(ms_per_step, 4),
+                'flops_per_launch': 2.835e9 * args.enc_batch, 'timing': 'one enc-batch per step'}
     peak = FP32_PEAK_TFLOPS if args.enc_precision == 'fp32' else F16X_PEAK_TFLOPS
     ach = VIT_GFLOP[args.enc_model] * args.enc_batch / ms_per_step
     return {'kernel': 'whole ViT encoder step (blob + k_conv split-fp16 GEMMs + attention + LayerNorm)',

@@ -511,6 +511,25 @@ static float* splitk_workspace(hipStream_t st, size_t bytes) {
     return e.first;
 }
 
+// bf16 grids of 64-row tiles below this many workgroups per CU use 32-row tiles instead: each
+// workgroup's K loop is load-latency bound (one register stage), so more resident workgroups per
+// CU is what hides it (VTF_CONV_BF16_SMALL = the threshold in workgroups per CU; 0 disables)
+static int conv_small_wg_per_cu() {
+    static int v = [] {
+        const char* e = std::getenv("VTF_CONV_BF16_SMALL");
+        return e ? std::atoi(e) : 3;
+    }();
+    return v;
+}
+static int device_cus() {
+    static int cus = [] {
+        int dev = 0, n = 256;
+        if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev);
+        return n;
+    }();
+    return cus;
+}
+
 // M-tile group height of the XCD-aware tile order (VTF_CONV_GROUP_M overrides; 0 = plain)
 static int conv_group_m() {
     static int g = [] {
@@ -561,6 +580,17 @@ static void launch_t(const ConvParams& p, hipStream_t st) {
     // 128-row tiles hide more load latency than the larger tiles save in operand traffic
     // (forward 2.82 -> 2.67 ms); the per-output k order does not depend on the tile shape.
     // fp32 (parity) keeps 128-row tiles.
+    if constexpr (sizeof(T) == 2) {
+        const int BN = p.Cout <= 32 ? 32 : 64;
+        const int64_t wg64 = (int64_t)cdiv(p.M, 64) * cdiv(p.Cout, BN);
+        if (wg64 < (int64_t)conv_small_wg_per_cu() * device_cus()) {
+            if (BN == 32)
+                launch_tile<T, 32, 32, 64>(p, st);
+            else
+                launch_tile<T, 32, 64, 64>(p, st);
+            return;
+        }
+    }
     if (p.Cout <= 32) {
         if constexpr (sizeof(T) == 2)
             launch_tile<T, 64, 32, 64>(p, st);
