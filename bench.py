@@ -14,7 +14,10 @@ Workloads (BASELINE.json configs; --config picks the preset, single flags overri
                 gathered embeddings go through the cosine dedupe and the K-means k=2..16 sweep
                 sharded by k across ranks (timed separately: `grouping`).
 The timed region ends with the RCCL all-gather-v of every rank's embeddings (the exchange step
-before grouping).  value = faces encoded by all ranks / max-over-ranks wall time.
+before grouping).  value = faces encoded by all ranks / max-over-ranks wall time.  Without
+--steps the detector configs time BASELINE's 10k frames per GPU (625 det-batches of 16): the
+per-lane encoder flush at the end of a run (a partial enc-batch per lane) is then amortised as in
+a real video, instead of weighing on a 10-20 step sample.
 
   python bench.py [--gpus N --steps K --warmup W] [--config c2|c3|c4|c5]
 With --gpus N > 1 and no torchrun environment the script starts
@@ -59,7 +62,9 @@ CONFIGS = {
 def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument('--gpus', type=int, default=1)
-    ap.add_argument('--steps', type=int, default=20)
+    ap.add_argument('--steps', type=int, default=None,
+                    help='timed steps (det-batches or enc-batches); default: the BASELINE frame count '
+                         '(--sustain-frames, 10k frames) for detector configs, 20 enc-batches otherwise')
     ap.add_argument('--warmup', type=int, default=3)
     ap.add_argument('--config', default='c2', choices=sorted(CONFIGS))
     ap.add_argument('--det-model', choices=['mtcnn', 'yolo', 'none'])
@@ -99,6 +104,8 @@ def parse(argv=None):
         a.det_batch = 32 if yolo else 16
     if a.det_min_size is None:
         a.det_min_size = 50 if yolo else 0
+    if a.steps is None:
+        a.steps = max(1, -(-a.sustain_frames // a.det_batch)) if a.det_model != 'none' and a.sustain_frames > 0 else 20
     if a.cpu_frames is None:
         a.cpu_frames = 24 if yolo else 12
     a.H, a.W = {'720p': (720, 1280), '1080p': (1080, 1920), '224': (224, 224)}[a.frame]
@@ -569,8 +576,8 @@ def run_gpu(args):
     if det and extras:
         solo = pipe.solo(4)
         # sustained leg: BASELINE config 2's 10k frames (per rank) through the same pipeline
-        if args.sustain_frames > 0:
-            n_sus = max(1, -(-args.sustain_frames // args.det_batch))
+        n_sus = max(1, -(-args.sustain_frames // args.det_batch)) if args.sustain_frames > 0 else 0
+        if n_sus > args.steps:  # (the default timed region already covers the BASELINE frame count)
             f_sus, t_sus, _, _ = measure(pipe, n_sus, 0, ctx)
             out['sustained'] = {'frames_per_rank': n_sus * args.det_batch, 'steps': n_sus,
                                 'value': round(f_sus / t_sus, 2), 'seconds': round(t_sus, 3),

@@ -21,7 +21,7 @@ if len(sys.argv) > 1 and sys.argv[1] == 'child':
     ms, n, fl, f = m.profile(False)
     print(json.dumps({'mask': os.environ.get('VTF_PNET_DEBUG', '0'), 'ms': ms / max(n, 1), 'tflops': fl / max(n, 1) / (ms / max(n, 1) / 1e3) / 1e12}))
 else:
-    for mask in ['0', '16', '17', '18', '20', '24', '48', '31', '127']:
+    for mask in sys.argv[1:] or ['0', '16', '17', '18', '20', '24', '48', '31', '127']:
         env = dict(os.environ, VTF_PNET_DEBUG=mask)
         out = subprocess.run([sys.executable, __file__, 'child'], env=env, capture_output=True, text=True, timeout=300)
         print(out.stdout.strip().splitlines()[-1] if out.stdout.strip() else out.stderr[-500:], flush=True)

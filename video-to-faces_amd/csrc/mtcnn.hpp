@@ -19,7 +19,7 @@ struct PNetW {
     // conv3 as fp16 split planes [2][32][160] (w = w0 + w1 * 2^-11, k = tap * 16 + ci, zero
     // padded 144 -> 160) for the fp16 matrix-core path; null -> fp32 MFMA path (see k_pnet)
     const uint16_t* c3h;
-    const uint16_t* c2h;  // conv2 likewise: [2][16][160], k = tap * 16 + ci (ci >= 10 zero)
+    const uint16_t* c2h;  // conv2: [2][16][96], the 90 (tap, ci) products packed in 3 k-steps (mtcnn_runtime)
     const uint16_t* c1h;  // conv1: [2][16][64], k = ky * 16 + kx * 4 + c (c = 3, kx = 3, ky = 3, co >= 10 zero)
     // both 1x1 heads as fp16 split planes [2][16 rows][32 k] (rows 0,1 conv4_1, 2..5 conv4_2);
     // k = 8g + j holds channel 4g + j (j < 4) or 16 + 4g + j - 4: exactly the conv3 accumulator

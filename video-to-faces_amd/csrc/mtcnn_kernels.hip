@@ -22,6 +22,7 @@
 // Build with -ffp-contract=off: only explicit fmaf() fuses.
 #include <algorithm>
 #include <cstdlib>
+#include <type_traits>
 
 #include "common.hpp"
 #include "mtcnn.hpp"
@@ -203,11 +204,11 @@ void launch_resample_sat(const int4* sat, int B, int H, int W, int lh, int lw, f
 
 constexpr int PT_H = PNET_TH, PT_W = PNET_TW;         // output cells per tile (mtcnn.hpp)
 static_assert(PT_W % 16 == 0 && (PT_H * PT_W) % 64 == 0, "conv3 fragments are 16-cell row runs, 4 waves");
-constexpr int PL_H = 2 * PT_H + 10, PL_W = 2 * PT_W + 10;  // level tile 42 x 74
-constexpr int PP_H = PT_H + 4, PP_W = PT_W + 4;       // pooled 20 x 36
-constexpr int PC_H = PT_H + 2, PC_W = PT_W + 2;       // conv2 out 18 x 34
-constexpr int P_LVL = 3 * PL_H * PL_W;                // 9324
-constexpr int P_C2 = 16 * PC_H * PC_W;                // 9792
+constexpr int PL_H = 2 * PT_H + 10, PL_W = 2 * PT_W + 10;  // level tile 42 x 42
+constexpr int PP_H = PT_H + 4, PP_W = PT_W + 4;       // pooled 20 x 20
+constexpr int PC_H = PT_H + 2, PC_W = PT_W + 2;       // conv2 out 18 x 18
+constexpr int P_LVL = 3 * PL_H * PL_W;                // 5292
+constexpr int P_C2 = 16 * PC_H * PC_W;                // 5184
 // pooled conv1: fp32 [10][cells], or fp16 split planes [2][cells][12] (ch 10, 11 zero; conv2 reads
 // 8 halves from channel 8 into the next cell, against zero weights) + 4 halves of end padding
 constexpr int PQ_C = 12;
@@ -234,10 +235,13 @@ __device__ inline void split_f16(float v, _Float16& x0, _Float16& x1) {
     x1 = (_Float16)((v - (float)x0) * 2048.f);
 }
 
-// 8 halves from an 8-byte aligned LDS address (two ds_read_b64)
+// 8 halves from an 8-byte aligned LDS address as two ds_read_b64 (2 LDS cycles each, 32-lane
+// bank groups over 64 banks).  The accesses are volatile so they are not merged into one
+// ds_read2_b64, which costs 8 cycles (half the bandwidth) and banks over 32 dwords per 16 lanes.
 typedef __attribute__((ext_vector_type(4))) _Float16 f16x4;
+typedef const volatile __attribute__((address_space(3))) f16x4 lds_f16x4;
 __device__ inline f16x8 ld_h8(const _Float16* p) {
-    const f16x4 lo = *(const f16x4*)p, hi = *(const f16x4*)(p + 4);
+    const f16x4 lo = *(lds_f16x4*)p, hi = *(lds_f16x4*)(p + 4);
     return f16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
 }
 
@@ -278,7 +282,7 @@ __global__ __launch_bounds__(256, PNET_GROUPS_PER_CU) void k_pnet(const uint8_t*
     const __amdgpu_buffer_rsrc_t rw2 = __builtin_amdgcn_make_buffer_rsrc((void*)wg.c2w, 0, 90 * 16 * 4, 0x00020000);
     const __amdgpu_buffer_rsrc_t rw3 = __builtin_amdgcn_make_buffer_rsrc((void*)wg.c3w, 0, 144 * 32 * 4, 0x00020000);
     const __amdgpu_buffer_rsrc_t rw3h = __builtin_amdgcn_make_buffer_rsrc((void*)wg.c3h, 0, 2 * 32 * 160 * 2, 0x00020000);
-    const __amdgpu_buffer_rsrc_t rw2h = __builtin_amdgcn_make_buffer_rsrc((void*)wg.c2h, 0, 2 * 16 * 160 * 2, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rw2h = __builtin_amdgcn_make_buffer_rsrc((void*)wg.c2h, 0, 2 * 16 * 96 * 2, 0x00020000);
     const __amdgpu_buffer_rsrc_t rw1h = __builtin_amdgcn_make_buffer_rsrc((void*)wg.c1h, 0, 2 * 16 * 64 * 2, 0x00020000);
     const __amdgpu_buffer_rsrc_t rhh = __builtin_amdgcn_make_buffer_rsrc((void*)wg.hh, 0, 2 * 16 * 32 * 2, 0x00020000);
     const bool split3 = wg.c3h != nullptr;  // conv3 on fp16 matrix cores (mtcnn_runtime: range bound)
@@ -496,7 +500,13 @@ __global__ __launch_bounds__(256, PNET_GROUPS_PER_CU) void k_pnet(const uint8_t*
             // the tile's conv1 window lies inside the level: no per-corner bounds checks
             const bool interior = 2 * (oy0 + PP_H - 1) + 1 < L1h && 2 * (ox0 + PP_W - 1) + 1 < L1w;
             const bool mono = a1 >= 0.f;
+            // upsampled levels (lh >= H, lw >= W: every bin 1 or 2 frame pixels per side) hold
+            // s / 2^(8..10) with |s| <= 1020, exact in fp16: the residual plane is zero there, so
+            // its MFMA and its operand reads are skipped (the products it would add are all zero)
+            const bool exact = P.lh >= H && P.lw >= W;
             constexpr int NU = 2;  // fragments per iteration
+            auto conv1_frags = [&](auto exact_t) {
+            constexpr bool EX = decltype(exact_t)::value;
             for (int f0 = wave; f0 < NF1; f0 += 4 * NU) {
                 int ab[NU];
 #pragma unroll
@@ -514,7 +524,7 @@ __global__ __launch_bounds__(256, PNET_GROUPS_PER_CU) void k_pnet(const uint8_t*
 #pragma unroll
                     for (int u = 0; u < NU; u++) {
                         xa[s2][u] = ld_h8(sL + ab[u] * 4 + xo);
-                        xb[s2][u] = ld_h8(sL + PLN + ab[u] * 4 + xo);
+                        if (!EX) xb[s2][u] = ld_h8(sL + PLN + ab[u] * 4 + xo);
                     }
                 }
                 // cross terms first, scaled by 2^-11 (exact) into the main chain's accumulator:
@@ -526,7 +536,7 @@ __global__ __launch_bounds__(256, PNET_GROUPS_PER_CU) void k_pnet(const uint8_t*
 #pragma unroll
                     for (int s2 = 0; s2 < 2; s2++) {
                         cd = __builtin_amdgcn_mfma_f32_16x16x32_f16(xa[s2][u], w1[s2], cd, 0, 0, 0);
-                        cd = __builtin_amdgcn_mfma_f32_16x16x32_f16(xb[s2][u], w0[s2], cd, 0, 0, 0);
+                        if (!EX) cd = __builtin_amdgcn_mfma_f32_16x16x32_f16(xb[s2][u], w0[s2], cd, 0, 0, 0);
                     }
                     cm[u] = cd * 0.00048828125f;
                 }
@@ -571,6 +581,11 @@ __global__ __launch_bounds__(256, PNET_GROUPS_PER_CU) void k_pnet(const uint8_t*
                     }
                 }
             }
+            };
+            if (exact)
+                conv1_frags(std::true_type{});
+            else
+                conv1_frags(std::false_type{});
         }
         {
             constexpr int NPP = PP_H * PP_W;        // pooled cells
@@ -637,60 +652,92 @@ __global__ __launch_bounds__(256, PNET_GROUPS_PER_CU) void k_pnet(const uint8_t*
         }
         __syncthreads();
 
-        // ---- 3. conv2 (10->16, 3x3) + PReLU on MFMA: M = 18*34 positions (39 frags), N = 16,
-        //         K = 90 (+2 zero) in 23 steps; A gathered from the pooled map.
+        // ---- 3. conv2 (10->16, 3x3) + PReLU on MFMA: 18 x 18 positions (21 frags of 16), 16
+        //         output channels, K = 90; operands gathered from the pooled map.
         {
-            constexpr int NPOS = PC_H * PC_W;      // 612
-            constexpr int NF = (NPOS + 15) / 16;   // 39
+            constexpr int NPOS = PC_H * PC_W;      // 324
+            constexpr int NF = (NPOS + 15) / 16;   // 21
             if (split3 && !(o.dbg & 4)) {
-                // fp16 matrix cores on split operands (as conv3): K = 9 taps x 16 ch (10 real) in 5
-                // steps of 32; rows = conv2 positions, lane group lkx reads 8 channels of tap
-                // 2s + (lkx >> 1) of both planes (16 B each); main and 2^11-scaled cross products
-                // in separate accumulators
+                // fp16 matrix cores on split operands (as conv3), computed TRANSPOSED (rows = the 16
+                // output channels, A = weights; columns = 16 conv2 positions, B = the pooled map), K =
+                // 90 packed into 3 steps of 32: step 0 / 1 = channels 0-7 of taps g / 4 + g for lane
+                // group g (one 16-byte read per plane); step 2 = 4 dwords per lane: group 0 channels
+                // 0-7 of tap 8, groups 1 / 2 channels 8, 9 of taps 0-3 / 4-7, group 3 channels 8, 9
+                // of tap 8 (+ 3 zero-weight slots).  Each lane ends with 4 consecutive output channels
+                // of one position: one 8-byte store per plane.  Main and 2^11-scaled cross products
+                // in separate accumulators.
                 constexpr int NPP = PP_H * PP_W;
                 const _Float16* sH = (const _Float16*)sP;
-                f16x8 w0[5], w1[5];
-                const int woff = (lrx * 160 + 8 * lkx) * 2;
+                typedef const volatile __attribute__((address_space(3))) uint32_t lds_u32;
+                f16x8 w0[3], w1[3];
+                const int woff = (lrx * 96 + 8 * lkx) * 2;
 #pragma unroll
-                for (int s5 = 0; s5 < 5; s5++) {
-                    w0[s5] = __builtin_bit_cast(f16x8, __builtin_amdgcn_raw_buffer_load_b128(rw2h, woff, 64 * s5, 0));
-                    w1[s5] = __builtin_bit_cast(f16x8,
-                                                __builtin_amdgcn_raw_buffer_load_b128(rw2h, woff, 16 * 160 * 2 + 64 * s5, 0));
+                for (int s3 = 0; s3 < 3; s3++) {
+                    w0[s3] = __builtin_bit_cast(f16x8, __builtin_amdgcn_raw_buffer_load_b128(rw2h, woff, 64 * s3, 0));
+                    w1[s3] = __builtin_bit_cast(f16x8,
+                                                __builtin_amdgcn_raw_buffer_load_b128(rw2h, woff, 16 * 96 * 2 + 64 * s3, 0));
+                }
+                // operand offsets (halves) relative to the position's pooled cell
+                auto tapoff = [](int t) { return ((t / 3) * PP_W + t % 3) * PQ_C; };
+                const int o0 = tapoff(lkx), o1 = tapoff(4 + lkx);
+                int o2[4];
+#pragma unroll
+                for (int jj = 0; jj < 4; jj++)
+                    o2[jj] = lkx == 0 ? tapoff(8) + 2 * jj : lkx == 3 ? tapoff(8) + 8 : tapoff(4 * (lkx - 1) + jj) + 8;
+                float bb[4], aa[4];
+#pragma unroll
+                for (int i = 0; i < 4; i++) {
+                    bb[i] = wc.c2b[4 * lkx + i];
+                    aa[i] = wc.p2[4 * lkx + i];
                 }
                 _Float16* sO = (_Float16*)sA;
                 for (int f0 = wave; f0 < NF; f0 += 8) {
                     const int f1 = f0 + 4;
                     const bool two = f1 < NF;
                     const int p0 = min(f0 * 16 + lrx, NPOS - 1), p1 = min((two ? f1 : f0) * 16 + lrx, NPOS - 1);
-                    const int ab0 = (p0 / PC_W) * PP_W + (p0 % PC_W), ab1 = (p1 / PC_W) * PP_W + (p1 % PC_W);
+                    const int ab0 = ((p0 / PC_W) * PP_W + (p0 % PC_W)) * PQ_C, ab1 = ((p1 / PC_W) * PP_W + (p1 % PC_W)) * PQ_C;
+                    f16x8 x[3][2][2];  // [step][fragment][plane]
+#pragma unroll
+                    for (int pl = 0; pl < 2; pl++) {
+                        const _Float16* base = sH + pl * NPP * PQ_C;
+                        x[0][0][pl] = ld_h8(base + ab0 + o0);
+                        x[0][1][pl] = ld_h8(base + ab1 + o0);
+                        x[1][0][pl] = ld_h8(base + ab0 + o1);
+                        x[1][1][pl] = ld_h8(base + ab1 + o1);
+                        uint32_t u0[4], u1[4];
+#pragma unroll
+                        for (int jj = 0; jj < 4; jj++) {
+                            u0[jj] = *(lds_u32*)(base + ab0 + o2[jj]);
+                            u1[jj] = *(lds_u32*)(base + ab1 + o2[jj]);
+                        }
+                        x[2][0][pl] = __builtin_bit_cast(f16x8, u0);
+                        x[2][1][pl] = __builtin_bit_cast(f16x8, u1);
+                    }
                     f32x4 c0 = {0.f, 0.f, 0.f, 0.f}, c1 = c0, d0 = c0, d1 = c0;
 #pragma unroll
-                    for (int s5 = 0; s5 < 5; s5++) {
-                        const int tap = min(2 * s5 + (lkx >> 1), 8);
-                        const int xo = ((tap / 3) * PP_W + (tap % 3)) * PQ_C + 8 * (lkx & 1);
-                        const f16x8 a00 = ld_h8(sH + ab0 * PQ_C + xo);
-                        const f16x8 a01 = ld_h8(sH + NPP * PQ_C + ab0 * PQ_C + xo);
-                        const f16x8 a10 = ld_h8(sH + ab1 * PQ_C + xo);
-                        const f16x8 a11 = ld_h8(sH + NPP * PQ_C + ab1 * PQ_C + xo);
-                        c0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a00, w0[s5], c0, 0, 0, 0);
-                        d0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a00, w1[s5], d0, 0, 0, 0);
-                        d0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a01, w0[s5], d0, 0, 0, 0);
-                        c1 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a10, w0[s5], c1, 0, 0, 0);
-                        d1 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a10, w1[s5], d1, 0, 0, 0);
-                        d1 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a11, w0[s5], d1, 0, 0, 0);
+                    for (int s3 = 0; s3 < 3; s3++) {
+                        c0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(w0[s3], x[s3][0][0], c0, 0, 0, 0);
+                        d0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(w1[s3], x[s3][0][0], d0, 0, 0, 0);
+                        d0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(w0[s3], x[s3][0][1], d0, 0, 0, 0);
+                        c1 = __builtin_amdgcn_mfma_f32_16x16x32_f16(w0[s3], x[s3][1][0], c1, 0, 0, 0);
+                        d1 = __builtin_amdgcn_mfma_f32_16x16x32_f16(w1[s3], x[s3][1][0], d1, 0, 0, 0);
+                        d1 = __builtin_amdgcn_mfma_f32_16x16x32_f16(w0[s3], x[s3][1][1], d1, 0, 0, 0);
                     }
 #pragma unroll
-                    for (int i = 0; i < 4; i++) {
+                    for (int h = 0; h < 2; h++) {
+                        const int q = (h ? f1 : f0) * 16 + lrx;
+                        if (q < NPOS && (h == 0 || two)) {
+                            f16x4 v0, v1;
 #pragma unroll
-                        for (int h = 0; h < 2; h++) {
-                            const int q = (h ? f1 : f0) * 16 + 4 * lkx + i;
-                            if (q < NPOS && (h == 0 || two)) {
+                            for (int i = 0; i < 4; i++) {
                                 const float acc2 = h ? c1[i] + d1[i] * 0.00048828125f : c0[i] + d0[i] * 0.00048828125f;
-                                const float v = prelu(acc2 + b2, a2);
+                                const float v = prelu(acc2 + bb[i], aa[i]);
                                 const _Float16 x0 = (_Float16)v;
-                                sO[q * 16 + lrx] = x0;
-                                sO[NPOS * 16 + q * 16 + lrx] = (_Float16)((v - (float)x0) * 2048.f);
+                                v0[i] = x0;
+                                v1[i] = (_Float16)((v - (float)x0) * 2048.f);
                             }
+                            *(f16x4*)(sO + q * 16 + 4 * lkx) = v0;
+                            *(f16x4*)(sO + NPOS * 16 + q * 16 + 4 * lkx) = v1;
                         }
                     }
                 }

@@ -363,7 +363,33 @@ static void build_weights(Mtcnn& m, const float* params, int64_t n_params) {
                 m.allocs.push_back((void*)d);
                 m.pw.c1h = d;
             }
-            m.pw.c2h = split(raw[3], 16, 10);
+            {
+                // conv2 [2][16][96]: k = 32 s + 8 g + j packs the 90 (tap, ci) products in 3 steps
+                // (k_pnet conv2): s < 2 -> tap 4 s + g, ci j; s = 2 -> g 0: tap 8, ci j; g 1 / 2:
+                // tap 4 (g - 1) + j / 2, ci 8 + j % 2; g 3: tap 8, ci 8 + j (j < 2), else zero
+                std::vector<uint16_t> h((size_t)2 * 16 * 96, 0);
+                const float* W = raw[3];  // [16][10][3][3]
+                for (int co = 0; co < 16; co++)
+                    for (int k = 0; k < 96; k++) {
+                        const int st = k / 32, g = (k % 32) / 8, j = k % 8;
+                        int tap = -1, ci = -1;
+                        if (st < 2) tap = 4 * st + g, ci = j;
+                        else if (g == 0) tap = 8, ci = j;
+                        else if (g < 3) tap = 4 * (g - 1) + j / 2, ci = 8 + j % 2;
+                        else if (j < 2) tap = 8, ci = 8 + j;
+                        if (tap < 0) continue;
+                        const float w = W[((size_t)co * 10 + ci) * 9 + tap];
+                        const _Float16 w0 = (_Float16)w;
+                        const _Float16 w1 = (_Float16)((w - (float)w0) * 2048.f);
+                        std::memcpy(&h[(size_t)co * 96 + k], &w0, 2);
+                        std::memcpy(&h[(size_t)(16 + co) * 96 + k], &w1, 2);
+                    }
+                uint16_t* d = nullptr;
+                VTF_HIP(hipMalloc((void**)&d, h.size() * 2));
+                VTF_HIP(hipMemcpy(d, h.data(), h.size() * 2, hipMemcpyHostToDevice));
+                m.allocs.push_back((void*)d);
+                m.pw.c2h = d;
+            }
             m.pw.c3h = split(raw[6], 32, 16);
             if (bound(6, 32, 144, b2) < 16384.0) {  // conv3 activations feed the split heads
                 std::vector<uint16_t> h(2 * 16 * 32, 0);
