@@ -16,8 +16,8 @@ struct PNetLevel {
 // All conv weights transposed to [ci][ky][kx][co]; dense weights to [k][out] where noted.
 struct PNetW {
     const float *c1w, *c1b, *p1, *c2w, *c2b, *p2, *c3w, *c3b, *p3, *c41w, *c41b, *c42w, *c42b;
-    // conv3 as fp16 split planes [2][32][160] (w = w0 + w1 * 2^-11, k = tap * 16 + ci, zero
-    // padded 144 -> 160) for the fp16 matrix-core path; null -> fp32 MFMA path (see k_pnet)
+    // conv3 as fp16 split planes [2][32][144] (w = w0 + w1 * 2^-11, k = tap * 16 + ci) for the
+    // fp16 matrix-core path (copied to LDS per tile); null -> fp32 MFMA path (see k_pnet)
     const uint16_t* c3h;
     const uint16_t* c2h;  // conv2: [2][16][96], the 90 (tap, ci) products packed in 3 k-steps (mtcnn_runtime)
     const uint16_t* c1h;  // conv1: [2][16][64], k = ky * 16 + kx * 4 + c (c = 3, kx = 3, ky = 3, co >= 10 zero)
@@ -38,7 +38,8 @@ struct PNetOut {
     float* prob;
     float* reg;
     int dbg;  // phase-skip mask for profiling (env VTF_PNET_DEBUG): 1 fill, 2 conv1, 4 conv2, 8 conv3,
-              // 16 no candidate output, 32 no heads, 64 no frame-patch staging
+              // 16 no candidate output, 32 no heads, 64 no frame-patch staging; 256 = phase clocks
+    unsigned long long* clk;  // [8] summed shader clocks per phase over workgroups (null: off)
 };
 
 void launch_sat(const uint8_t* frames, int64_t frame_stride, int64_t row_stride, int B, int H, int W, int4* sat,

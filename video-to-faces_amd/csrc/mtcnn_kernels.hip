@@ -212,7 +212,12 @@ constexpr int P_C2 = 16 * PC_H * PC_W;                // 5184
 // pooled conv1: fp32 [10][cells], or fp16 split planes [2][cells][12] (ch 10, 11 zero; conv2 reads
 // 8 halves from channel 8 into the next cell, against zero weights) + 4 halves of end padding
 constexpr int PQ_C = 12;
-constexpr int P_POOL = (10 * PP_H * PP_W > PQ_C * PP_H * PP_W + 4) ? 10 * PP_H * PP_W : PQ_C * PP_H * PP_W + 4;
+constexpr int P_POOL0 = (10 * PP_H * PP_W > PQ_C * PP_H * PP_W) ? 10 * PP_H * PP_W : PQ_C * PP_H * PP_W;
+// during conv3 the pooled buffer holds the next tile's first 2 KB of frame patch (floats 0..511)
+// and conv3's split weights [2][32][144] halves (floats 512..5119, rows of 72 dwords: conflict-free
+// for the 16-byte A-operand reads), so conv3 issues no global loads
+constexpr int P_W3 = 512, W3_ROW = 144;
+constexpr int P_POOL = P_POOL0 > P_W3 + 2 * 32 * W3_ROW / 2 ? P_POOL0 : P_W3 + 2 * 32 * W3_ROW / 2;
 constexpr int P_LVLH = PL_H * PL_W * 4;                // level as fp16 split planes [2][y][x][4] (in floats)
 constexpr int P_A0 = P_C2 > P_LVL ? P_C2 : P_LVL;
 // + 4 floats of zero padding after the split level planes: conv1's 16-byte operand reads run one
@@ -264,6 +269,15 @@ __device__ inline void store_level(float* sA, bool split, int i, float r, float 
     }
 }
 
+// a level descriptor from the constant address space (scalar loads; the generic copy
+// constructor does not take an address-space-qualified source)
+__device__ inline PNetLevel load_level(const VTF_CONST PNetLevel* p) {
+    PNetLevel r;
+    r.lh = p->lh, r.lw = p->lw, r.ph = p->ph, r.pw = p->pw, r.scale = p->scale;
+    r.tiles_x = p->tiles_x, r.tiles_y = p->tiles_y, r.pad = p->pad, r.tile_beg = p->tile_beg, r.pre = p->pre;
+    return r;
+}
+
 constexpr int PNET_TILE_CHUNK = 4;
 constexpr int PNET_GROUPS_PER_CU = (160 * 1024) / ((PNET_LDS + 511) / 512 * 512);  // LDS granule: 512 B
 static_assert(PNET_GROUPS_PER_CU >= 2, "k_pnet tile too large for 2 workgroups per CU");
@@ -281,17 +295,29 @@ __global__ __launch_bounds__(256, PNET_GROUPS_PER_CU) void k_pnet(const uint8_t*
     // (k rows 90, 91 of conv2 are zeroed explicitly: soffset is outside the range check)
     const __amdgpu_buffer_rsrc_t rw2 = __builtin_amdgcn_make_buffer_rsrc((void*)wg.c2w, 0, 90 * 16 * 4, 0x00020000);
     const __amdgpu_buffer_rsrc_t rw3 = __builtin_amdgcn_make_buffer_rsrc((void*)wg.c3w, 0, 144 * 32 * 4, 0x00020000);
-    const __amdgpu_buffer_rsrc_t rw3h = __builtin_amdgcn_make_buffer_rsrc((void*)wg.c3h, 0, 2 * 32 * 160 * 2, 0x00020000);
     const __amdgpu_buffer_rsrc_t rw2h = __builtin_amdgcn_make_buffer_rsrc((void*)wg.c2h, 0, 2 * 16 * 96 * 2, 0x00020000);
     const __amdgpu_buffer_rsrc_t rw1h = __builtin_amdgcn_make_buffer_rsrc((void*)wg.c1h, 0, 2 * 16 * 64 * 2, 0x00020000);
     const __amdgpu_buffer_rsrc_t rhh = __builtin_amdgcn_make_buffer_rsrc((void*)wg.hh, 0, 2 * 16 * 32 * 2, 0x00020000);
     const bool split3 = wg.c3h != nullptr;  // conv3 on fp16 matrix cores (mtcnn_runtime: range bound)
-    __shared__ float sA[P_A];     // level tile, later conv2 output
-    __shared__ float sP[P_POOL];  // frame patch (u8) during the fill, then pooled conv1
+    __shared__ __attribute__((aligned(16))) float sA[P_A];     // level tile, later conv2 output
+    __shared__ __attribute__((aligned(16))) float sP[P_POOL];  // frame patch (u8) during the fill, then pooled conv1
     __shared__ ushort2 ybin[PL_H], xbin[PL_W];  // frame bin [start, end) of each level row / column
     __shared__ int s_tile, s_next, s_cend;
+    __shared__ unsigned long long s_clk[8];  // phase clocks (VTF_PNET_DEBUG & 256)
     const int tid = threadIdx.x;
     bool pf_done = false;  // the first 2 KB of this tile's frame patch were staged by the previous tile
+    int L_prev = 0;
+    // phase timing (debug): thread 0 reads the shader clock after each phase's closing barrier
+    const bool clk_on = o.clk != nullptr;
+    unsigned long long t_last = clk_on ? clock64() : 0;
+    auto mark = [&](int k) {
+        if (clk_on && tid == 0) {
+            const unsigned long long t = clock64();
+            s_clk[k] += t - t_last;
+            t_last = t;
+        }
+    };
+    if (tid < 8) s_clk[tid] = 0;
     const int lane = tid & 63, wave = tid >> 6;
     const int lr = lane & 15, lk = lane >> 4;
 
@@ -300,9 +326,9 @@ __global__ __launch_bounds__(256, PNET_GROUPS_PER_CU) void k_pnet(const uint8_t*
     // ---- tiles come from an atomic counter (dynamic: pyramid tiles differ in cost); the next
     //      index is requested as soon as the current one is known, so the atomic's round trip
     //      overlaps the tile's work instead of opening it
-    // zero pads read (against zero weights) past the split level planes and the pooled planes
+    // zero pad after the split level planes: read by conv1 (against zero weights) one pixel past
+    // the last level pixel, and conv3's zero weight slots (k >= 144) point at it
     if (tid < 4) sA[P_A - 4 + tid] = 0.f;
-    else if (tid < 8) sP[P_POOL - 8 + tid] = 0.f;
     // tiles are handed out in chunks of PNET_TILE_CHUNK: one same-address atomic per chunk (a
     // single counter hit once per tile serialises ~166k atomics per launch at the L2)
     if (tid == 0) {
@@ -311,7 +337,9 @@ __global__ __launch_bounds__(256, PNET_GROUPS_PER_CU) void k_pnet(const uint8_t*
     }
     for (;;) {
         __syncthreads();
-        const int64_t blk = s_tile;
+        mark(0);  // 0: end-of-tile prefetch store + loop barrier
+        // (wave-uniform: the level table and tile geometry below become scalar loads)
+        const int64_t blk = __builtin_amdgcn_readfirstlane(s_tile);
         if (blk >= total_tiles) break;
         uint32_t next_tile = 0, next_cend = 0;
         if (tid == 0) {
@@ -325,9 +353,12 @@ __global__ __launch_bounds__(256, PNET_GROUPS_PER_CU) void k_pnet(const uint8_t*
             }
             s_next = (int)next_tile;  // read at conv3 (several barriers later) for the prefetch
         }
-        int L = 0;
-        while (L + 1 < n_levels && blk >= lv[L + 1].tile_beg) L++;
-        const PNetLevel P = lv[L];
+        // a workgroup's tiles come in increasing order, so its level only moves forward
+        int L = L_prev;
+        const VTF_CONST PNetLevel* lvc = cptr(lv);  // constant address space: scalar loads
+        while (L + 1 < n_levels && blk >= lvc[L + 1].tile_beg) L++;
+        const PNetLevel P = load_level(lvc + L);
+        L_prev = L;
         const int64_t t = blk - P.tile_beg;
         const int tiles_per_img = P.tiles_x * P.tiles_y;
         const int b = (int)(t / tiles_per_img);
@@ -350,6 +381,7 @@ __global__ __launch_bounds__(256, PNET_GROUPS_PER_CU) void k_pnet(const uint8_t*
             xbin[q] = lx < P.lw ? make_ushort2((lx * W) / P.lw, ((lx + 1) * W + P.lw - 1) / P.lw) : make_ushort2(0, 0);
         }
         __syncthreads();
+        mark(1);  // 1: tile index, level lookup, bins
         // frame patch covering every bin of the tile; staged to LDS with coalesced loads when it fits
         int fy0 = ybin[0].x, fx0 = xbin[0].x, fy1 = fy0, fx1 = fx0;
         {
@@ -377,6 +409,7 @@ __global__ __launch_bounds__(256, PNET_GROUPS_PER_CU) void k_pnet(const uint8_t*
             }
         }
         __syncthreads();
+        mark(2);  // 2: frame patch staging
         if (P.pre) {
             // large-bin level precomputed by k_resample_sat (bit-identical values)
             const float* pre = P.pre + (int64_t)b * 3 * P.lh * P.lw;
@@ -406,9 +439,49 @@ __global__ __launch_bounds__(256, PNET_GROUPS_PER_CU) void k_pnet(const uint8_t*
         // over each level row's bin (pass V) give the reference's fp32 bin sums bit for bit, with
         // each frame byte read ~once instead of once per covering level pixel
         const int nrows = fy1 - fy0;
-        const int hs_off = (nrows * pw3 + 3) & ~3;
-        const bool sep = staged && !(o.dbg & 1) && hs_off + nrows * PL_W * 6 <= PATCH_BYTES && W < 128 * P.lw;
-        if (sep) {
+        const int hs_off = (nrows * pw3 + 7) & ~7;
+        // upsampled levels on the split path: bins of 1 or 2 frame pixels per side, every level
+        // value s * 2^-(8..10) exact in fp16 (conv1 skips the residual plane there)
+        const bool exact_fill = split3 && P.lh >= H && P.lw >= W;
+        const bool sep = staged && !(o.dbg & 1) && hs_off + nrows * PL_W * (exact_fill ? 8 : 6) <= PATCH_BYTES &&
+                         W < 128 * P.lw;
+        if (sep && exact_fill) {
+            // bins of n in {0, 1, 2} pixels: branch-free sums, 8-byte row-sum entries, one store
+            // per level pixel (plane 0 only; the value is its own fp16 split: x1 = 0)
+            typedef __attribute__((ext_vector_type(4))) short s16x4;
+            s16x4* hs = (s16x4*)(patch + hs_off);
+            for (int i = tid; i < nrows * PL_W; i += 256) {
+                const int r = i / PL_W, q = i - r * PL_W;
+                const ushort2 xb = xbin[q];
+                const int n = xb.y - xb.x;
+                const uint8_t* row = patch + r * pw3 + (n ? (xb.x - fx0) * 3 : 0);
+                const uint8_t* row2 = n > 1 ? row + 3 : row;
+                const int m = n > 1 ? 1 : 0;
+                const int a0 = row[2] + m * row2[2], a1 = row[1] + m * row2[1], a2 = row[0] + m * row2[0];
+                hs[i] = s16x4{(short)(2 * a0 - 255 * n), (short)(2 * a1 - 255 * n), (short)(2 * a2 - 255 * n), 0};
+            }
+            __syncthreads();
+            typedef __attribute__((ext_vector_type(4))) _Float16 h4;
+            h4* lvl = (h4*)sA;
+            // conv1's operand reads run one pixel past plane 0 (against zero weights) into plane
+            // 1, which this path leaves stale: that pixel must be finite
+            if (tid == 0) lvl[PL_H * PL_W] = h4{(_Float16)0.f, (_Float16)0.f, (_Float16)0.f, (_Float16)0.f};
+            for (int i = tid; i < PL_H * PL_W; i += 256) {
+                const int r = i / PL_W, q = i - r * PL_W;
+                const ushort2 yb = ybin[r], xb = xbin[q];
+                const int kh = yb.y - yb.x, kw = xb.y - xb.x;
+                const s16x4* h = hs + (kh ? yb.x - fy0 : 0) * PL_W + q;
+                const s16x4 v0 = h[0], v1 = h[kh > 1 ? PL_W : 0];
+                const int m = kh > 1 ? 1 : 0;
+                // s / kh / kw with kh, kw in {1, 2}: a power-of-two scale, exact
+                const float sc = 0.00390625f * (kh > 1 ? 0.5f : 1.f) * (kw > 1 ? 0.5f : 1.f);
+                const bool in = kh > 0 && kw > 0;
+                const float r0 = in ? (float)(v0[0] + m * v1[0]) * sc : 0.f;
+                const float g0 = in ? (float)(v0[1] + m * v1[1]) * sc : 0.f;
+                const float b0 = in ? (float)(v0[2] + m * v1[2]) * sc : 0.f;
+                lvl[i] = h4{(_Float16)r0, (_Float16)g0, (_Float16)b0, (_Float16)0.f};
+            }
+        } else if (sep) {
             int16_t* hs = (int16_t*)(patch + hs_off);
             for (int i = tid; i < nrows * PL_W; i += 256) {
                 const int r = i / PL_W, q = i - r * PL_W;
@@ -471,6 +544,7 @@ __global__ __launch_bounds__(256, PNET_GROUPS_PER_CU) void k_pnet(const uint8_t*
                         in ? div_bin(div_bin(s2, kh), kw) : 0.f);
         }
         __syncthreads();
+        mark(3);  // 3: level tile fill
 
         // ---- 2. conv1 (3->10, 3x3) + PReLU + maxpool 2x2 ceil.  Default: fp16 matrix cores on
         //         split operands (below).  fp32 fallback: the VALU -- with N = 10 output channels
@@ -504,9 +578,11 @@ __global__ __launch_bounds__(256, PNET_GROUPS_PER_CU) void k_pnet(const uint8_t*
             // s / 2^(8..10) with |s| <= 1020, exact in fp16: the residual plane is zero there, so
             // its MFMA and its operand reads are skipped (the products it would add are all zero)
             const bool exact = P.lh >= H && P.lw >= W;
-            constexpr int NU = 2;  // fragments per iteration
             auto conv1_frags = [&](auto exact_t) {
             constexpr bool EX = decltype(exact_t)::value;
+            // fragments per iteration: the exact path holds one operand plane, so twice the
+            // fragments fit the same registers (more independent MFMA chains per wave)
+            constexpr int NU = EX ? 4 : 2;
             for (int f0 = wave; f0 < NF1; f0 += 4 * NU) {
                 int ab[NU];
 #pragma unroll
@@ -527,25 +603,43 @@ __global__ __launch_bounds__(256, PNET_GROUPS_PER_CU) void k_pnet(const uint8_t*
                         if (!EX) xb[s2][u] = ld_h8(sL + PLN + ab[u] * 4 + xo);
                     }
                 }
-                // cross terms first, scaled by 2^-11 (exact) into the main chain's accumulator:
-                // one accumulator per fragment, no combine step
                 f32x4 cm[NU];
+                if (EX) {
+                    // main and cross (x0 w1) chains independent, combined once: c + d * 2^-11 (the
+                    // scaling is exact, so the fma rounds once like the add)
+                    f32x4 cd[NU];
 #pragma unroll
-                for (int u = 0; u < NU; u++) {
-                    f32x4 cd = {0.f, 0.f, 0.f, 0.f};
+                    for (int u = 0; u < NU; u++) cm[u] = cd[u] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-                    for (int s2 = 0; s2 < 2; s2++) {
-                        cd = __builtin_amdgcn_mfma_f32_16x16x32_f16(xa[s2][u], w1[s2], cd, 0, 0, 0);
-                        if (!EX) cd = __builtin_amdgcn_mfma_f32_16x16x32_f16(xb[s2][u], w0[s2], cd, 0, 0, 0);
-                    }
-                    cm[u] = cd * 0.00048828125f;
-                }
+                    for (int s2 = 0; s2 < 2; s2++)
 #pragma unroll
-                for (int s2 = 0; s2 < 2; s2++)
+                        for (int u = 0; u < NU; u++) {
+                            cm[u] = __builtin_amdgcn_mfma_f32_16x16x32_f16(xa[s2][u], w0[s2], cm[u], 0, 0, 0);
+                            cd[u] = __builtin_amdgcn_mfma_f32_16x16x32_f16(xa[s2][u], w1[s2], cd[u], 0, 0, 0);
+                        }
 #pragma unroll
                     for (int u = 0; u < NU; u++)
-                        cm[u] = __builtin_amdgcn_mfma_f32_16x16x32_f16(xa[s2][u], w0[s2], cm[u], 0, 0, 0);
 #pragma unroll
+                        for (int i = 0; i < 4; i++) cm[u][i] = __builtin_fmaf(cd[u][i], 0.00048828125f, cm[u][i]);
+                } else {
+                    // cross terms first, scaled by 2^-11 (exact) into the main chain's accumulator:
+                    // one accumulator per fragment, no combine step
+#pragma unroll
+                    for (int u = 0; u < NU; u++) {
+                        f32x4 cd = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                        for (int s2 = 0; s2 < 2; s2++) {
+                            cd = __builtin_amdgcn_mfma_f32_16x16x32_f16(xa[s2][u], w1[s2], cd, 0, 0, 0);
+                            cd = __builtin_amdgcn_mfma_f32_16x16x32_f16(xb[s2][u], w0[s2], cd, 0, 0, 0);
+                        }
+                        cm[u] = cd * 0.00048828125f;
+                    }
+#pragma unroll
+                    for (int s2 = 0; s2 < 2; s2++)
+#pragma unroll
+                        for (int u = 0; u < NU; u++)
+                            cm[u] = __builtin_amdgcn_mfma_f32_16x16x32_f16(xa[s2][u], w0[s2], cm[u], 0, 0, 0);
+                }
                 for (int u = 0; u < NU; u++) {
                     const int f = f0 + 4 * u;
                     if (f >= NF1) break;
@@ -651,6 +745,7 @@ __global__ __launch_bounds__(256, PNET_GROUPS_PER_CU) void k_pnet(const uint8_t*
             }
         }
         __syncthreads();
+        mark(4);  // 4: conv1 + pool
 
         // ---- 3. conv2 (10->16, 3x3) + PReLU on MFMA: 18 x 18 positions (21 frags of 16), 16
         //         output channels, K = 90; operands gathered from the pooled map.
@@ -803,6 +898,18 @@ __global__ __launch_bounds__(256, PNET_GROUPS_PER_CU) void k_pnet(const uint8_t*
             }
         }
         __syncthreads();
+        if (split3) {
+            // conv3's split weights [2][32][144] halves (18 KB, L2-resident) -> the pooled buffer,
+            // now free: 18 lane-linear 1 KB LDS-DMA pieces, waited for by the barrier
+            constexpr int W3_PIECES = 2 * 32 * W3_ROW * 2 / 1024;
+            static_assert(2 * 32 * W3_ROW * 2 % 1024 == 0, "whole 1 KB pieces");
+            const char* src = (const char*)wg.c3h;
+            for (int c = wave; c < W3_PIECES; c += 4)
+                __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)(src + c * 1024 + lane * 16),
+                                                 (void __attribute__((address_space(3)))*)(sP + P_W3 + c * 256), 16, 0, 0);
+            __syncthreads();
+        }
+        mark(5);  // 5: conv2
 
         // ---- 4. conv3 (16->32, 3x3) + PReLU on MFMA, computed TRANSPOSED (C = W3^T x im2col:
         //         rows = 32 channels in 2 frags, cols = 16 cells per frag, K = 144 in 36 steps) so
@@ -816,40 +923,12 @@ __global__ __launch_bounds__(256, PNET_GROUPS_PER_CU) void k_pnet(const uint8_t*
         //         time).  Fallback (conv2 activations could leave the fp16 range, host bound):
         //         fp32 MFMA with the weights streamed in 4 chunks of 9 k-steps.
         // ---- next tile's frame patch: the first 8 bytes per thread (2 KB, the whole patch of the
-        //      upsampled levels that dominate the tile count) are loaded here, in flight during
-        //      conv3, and stored to the (now free) patch buffer after it -- the next tile's
-        //      staging latency hides behind this tile's matrix work
+        //      upsampled levels that dominate the tile count) are loaded at conv3's start, in
+        //      flight during conv3 (which reads its weights from LDS: no later global load waits
+        //      on them), and stored to the patch buffer after it -- the next tile's staging
+        //      latency hides behind this tile's matrix work
         uint8_t pfv[8];
         int pf_n = 0;
-        {
-            const int64_t nt = s_next;
-            if (nt < total_tiles && !(o.dbg & 64)) {
-                int L2 = 0;
-                while (L2 + 1 < n_levels && nt >= lv[L2 + 1].tile_beg) L2++;
-                const PNetLevel Q = lv[L2];
-                if (!Q.pre) {
-                    const int64_t t2 = nt - Q.tile_beg;
-                    const int tpi = Q.tiles_x * Q.tiles_y;
-                    const int b2i = (int)(t2 / tpi), tt2 = (int)(t2 % tpi);
-                    const int oy2 = (tt2 / Q.tiles_x) * PT_H, ox2 = (tt2 % Q.tiles_x) * PT_W;
-                    const int ry = min(PL_H - 1, Q.lh - 1 - 2 * oy2), rx = min(PL_W - 1, Q.lw - 1 - 2 * ox2);
-                    const int gy0 = (2 * oy2 * H) / Q.lh, gy1 = ((2 * oy2 + ry + 1) * H + Q.lh - 1) / Q.lh;
-                    const int gx0 = (2 * ox2 * W) / Q.lw, gx1 = ((2 * ox2 + rx + 1) * W + Q.lw - 1) / Q.lw;
-                    const int qw3 = (gx1 - gx0) * 3;
-                    const int nb2 = (gy1 - gy0) * qw3;
-                    if ((int64_t)(gy1 - gy0) * qw3 <= PATCH_BYTES && nb2 > 0) {
-                        const uint8_t* fr2 = frames + (int64_t)b2i * frame_stride;
-#pragma unroll
-                        for (int j = 0; j < 8; j++) {
-                            const int i = min(tid + j * 256, nb2 - 1);
-                            const int r = i / qw3, q = i - r * qw3;
-                            pfv[j] = fr2[(int64_t)(gy0 + r) * row_stride + gx0 * 3 + q];
-                        }
-                        pf_n = nb2;
-                    }
-                }
-            }
-        }
         {
             constexpr int FPW = PT_H * PT_W / 64;  // 16-cell fragments per wave
             // two passes of FPW/2 fragments each: conv3 + heads per pass keeps the accumulators
@@ -877,6 +956,45 @@ __global__ __launch_bounds__(256, PNET_GROUPS_PER_CU) void k_pnet(const uint8_t*
                 hw0 = __builtin_bit_cast(f16x8, __builtin_amdgcn_raw_buffer_load_b128(rhh, hoff, 0, 0));
                 hw1 = __builtin_bit_cast(f16x8, __builtin_amdgcn_raw_buffer_load_b128(rhh, hoff, 16 * 32 * 2, 0));
             }
+            // (issued after the head weights: loads complete in order, and the frame bytes are
+            //  the slow ones; the scheduling barrier keeps the order)
+            __builtin_amdgcn_sched_barrier(0);
+            {
+                // the loads are issued on every tile (a dummy read of the first frame byte when
+                // there is nothing to prefetch), so both paths leave the same count of loads in
+                // flight and the waits for the head weights above stay partial
+                const uint8_t* pf_src = frames;
+                int qw3 = 1, nb2 = 1, pf_rows = 0;
+                const int64_t nt = __builtin_amdgcn_readfirstlane(s_next);
+                if (nt < total_tiles && !(o.dbg & 64)) {
+                    int L2 = L;  // nt > blk
+                    while (L2 + 1 < n_levels && nt >= lvc[L2 + 1].tile_beg) L2++;
+                    const PNetLevel Q = load_level(lvc + L2);
+                    if (!Q.pre) {
+                        const int t2 = (int)(nt - Q.tile_beg);
+                        const int tpi = Q.tiles_x * Q.tiles_y;
+                        const int b2i = t2 / tpi, tt2 = t2 % tpi;
+                        const int oy2 = (tt2 / Q.tiles_x) * PT_H, ox2 = (tt2 % Q.tiles_x) * PT_W;
+                        const int ry = min(PL_H - 1, Q.lh - 1 - 2 * oy2), rx = min(PL_W - 1, Q.lw - 1 - 2 * ox2);
+                        const int gy0 = (2 * oy2 * H) / Q.lh, gy1 = ((2 * oy2 + ry + 1) * H + Q.lh - 1) / Q.lh;
+                        const int gx0 = (2 * ox2 * W) / Q.lw, gx1 = ((2 * ox2 + rx + 1) * W + Q.lw - 1) / Q.lw;
+                        const int w3 = (gx1 - gx0) * 3, nb = (gy1 - gy0) * w3;
+                        if ((int64_t)(gy1 - gy0) * w3 <= PATCH_BYTES && nb > 0) {
+                            pf_src = frames + (int64_t)b2i * frame_stride + (int64_t)gy0 * row_stride + gx0 * 3;
+                            qw3 = w3;
+                            nb2 = nb;
+                            pf_rows = 1;
+                        }
+                    }
+                }
+#pragma unroll
+                for (int j = 0; j < 8; j++) {
+                    const int i = min(tid + j * 256, nb2 - 1);
+                    const int r = i / qw3, q = i - r * qw3;
+                    pfv[j] = pf_src[(int64_t)r * row_stride + q];
+                }
+                pf_n = pf_rows ? nb2 : 0;
+            }
             const float hb0 = wc.c41b[0], hb1 = wc.c41b[1], hb2 = wc.c42b[0], hb3 = wc.c42b[1];
             const float hb4 = wc.c42b[2], hb5 = wc.c42b[3];
 #pragma unroll 1
@@ -901,16 +1019,18 @@ __global__ __launch_bounds__(256, PNET_GROUPS_PER_CU) void k_pnet(const uint8_t*
                     f32x4 accc[FH][2];
     #pragma unroll
                     for (int j = 0; j < FH; j++) accc[j][0] = accc[j][1] = f32x4{0.f, 0.f, 0.f, 0.f};
-                    const int woff = (lrx * 160 + 8 * lkx) * 2;
+                    // weights from the pooled buffer (rows of W3_ROW halves); k slots >= 144 (step 4,
+                    // lane groups 2, 3) are zero: those lanes read the zero pad after the level planes
+                    const _Float16* sWh = (const _Float16*)(sP + P_W3) + lrx * W3_ROW + 8 * lkx;
+                    const _Float16* zpad = (const _Float16*)(sA + P_A - 4);
     #pragma unroll
                     for (int s5 = 0; s5 < 5; s5++) {
                         f16x8 w0[2], w1[2];
+                        const bool zw = s5 == 4 && lkx >= 2;
     #pragma unroll
                         for (int mf = 0; mf < 2; mf++) {
-                            w0[mf] = __builtin_bit_cast(
-                                f16x8, __builtin_amdgcn_raw_buffer_load_b128(rw3h, woff, (mf * 16 * 160 + 32 * s5) * 2, 0));
-                            w1[mf] = __builtin_bit_cast(
-                                f16x8, __builtin_amdgcn_raw_buffer_load_b128(rw3h, woff, ((32 + mf * 16) * 160 + 32 * s5) * 2, 0));
+                            w0[mf] = *(const f16x8*)(zw ? zpad : sWh + (mf * 16) * W3_ROW + 32 * s5);
+                            w1[mf] = *(const f16x8*)(zw ? zpad : sWh + (32 + mf * 16) * W3_ROW + 32 * s5);
                         }
                         const int tap = min(2 * s5 + (lkx >> 1), 8);
                         const int xo = ((tap / 3) * PC_W + (tap % 3)) * 16 + 8 * (lkx & 1);
@@ -1050,7 +1170,9 @@ __global__ __launch_bounds__(256, PNET_GROUPS_PER_CU) void k_pnet(const uint8_t*
             s_cend = (int)next_cend;
         }
         __syncthreads();  // sA/sP are rewritten by the next tile
+        mark(6);  // 6: prefetch issue, conv3, heads, gate
     }
+    if (clk_on && tid < 8) atomicAdd(&o.clk[tid], s_clk[tid]);
 }
 
 void launch_pnet(bool dense, const uint8_t* frames, int64_t frame_stride, int64_t row_stride, int H, int W,

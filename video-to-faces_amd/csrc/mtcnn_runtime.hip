@@ -325,17 +325,17 @@ static void build_weights(Mtcnn& m, const float* params, int64_t n_params) {
     {
         const double b1 = bound(0, 10, 27, 1.0), b2 = bound(3, 16, 90, b1);
         if (b1 < 16384.0 && b2 < 16384.0 && allow_x) {
-            // [2][co][160] split planes of a [co][ci][3][3] conv, k = tap * 16 + ci
+            // [2][co][144] split planes of a [co][ci][3][3] conv, k = tap * 16 + ci
             auto split = [&](const float* W, int co_n, int ci_n) {
-                std::vector<uint16_t> h((size_t)2 * co_n * 160, 0);
+                std::vector<uint16_t> h((size_t)2 * co_n * 144, 0);
                 for (int co = 0; co < co_n; co++)
                     for (int tap = 0; tap < 9; tap++)
                         for (int ci = 0; ci < ci_n; ci++) {
                             const float w = W[((size_t)co * ci_n + ci) * 9 + tap];
                             const _Float16 w0 = (_Float16)w;
                             const _Float16 w1 = (_Float16)((w - (float)w0) * 2048.f);
-                            std::memcpy(&h[(size_t)co * 160 + tap * 16 + ci], &w0, 2);
-                            std::memcpy(&h[(size_t)(co_n + co) * 160 + tap * 16 + ci], &w1, 2);
+                            std::memcpy(&h[(size_t)co * 144 + tap * 16 + ci], &w0, 2);
+                            std::memcpy(&h[(size_t)(co_n + co) * 144 + tap * 16 + ci], &w1, 2);
                         }
                 uint16_t* d = nullptr;
                 VTF_HIP(hipMalloc((void**)&d, h.size() * 2));
@@ -418,7 +418,7 @@ static void build_weights(Mtcnn& m, const float* params, int64_t n_params) {
 
 // RNet / ONet on NHWC fp32 crops x0 [n,S,S,8] (mtcnn.py:58-76 / 101-121), layer by layer on
 // the MFMA conv kernel; pools are torch MaxPool2d(ceil_mode=True).
-enum RSlot { S_RA = 70, S_RB = 71, S_BOXPOST = 72 };  // nms_multi owns slots 40-61
+enum RSlot { S_RA = 70, S_RB = 71, S_BOXPOST = 72, S_CLK = 73 };  // nms_multi owns slots 40-61
 // first = 1: x0 is the fused front end's pooled conv1 map [n,P,P,32] (k_cand_front)
 static void run_candidates(Mtcnn& m, bool onet, const float* x0, int64_t n, float4* reg, float* lm, float* prob,
                            int first = 0, int force_fp32 = 0) {
@@ -654,11 +654,21 @@ static void detect(Mtcnn& m, const uint8_t* frames, int on_dev, int B, int H, in
     po.score = m.ar.get<float>(S_SCORE, cells);
     po.regv = m.ar.get<float4>(S_REGV, cells);
     if (const char* e = getenv("VTF_PNET_DEBUG")) po.dbg = atoi(e);
+    if (po.dbg & 256) po.clk = m.ar.get<unsigned long long>(S_CLK, 8);
+    if (po.clk) VTF_HIP(hipMemsetAsync(po.clk, 0, 64, st));
     if (m.prof) VTF_HIP(hipEventRecord(m.ev0, st));
     launch_pnet(false, fr, fstride, rstride, H, W, d_lv, NL, tiles, m.pw, po, d_cnt + NL + 1, st);
     if (m.prof) VTF_HIP(hipEventRecord(m.ev1, st));
     std::vector<uint32_t> cnt(NL + 1);
     d2h_sync(cnt.data(), d_cnt, (NL + 1) * 4, st);
+    if (po.clk) {  // debug: average workgroup clocks per tile and phase (k_pnet mark() points)
+        unsigned long long c[8];
+        d2h_sync(c, po.clk, 64, st);
+        static const char* nm[7] = {"tail", "head", "stage", "fill", "conv1", "conv2", "conv3+heads"};
+        fprintf(stderr, "k_pnet phase clocks per tile (%lld tiles):", (long long)tiles);
+        for (int k = 0; k < 7; k++) fprintf(stderr, " %s %.0f", nm[k], (double)c[k] / (double)tiles);
+        fprintf(stderr, "\n");
+    }
     if (m.prof) {
         float ms = 0.f;
         VTF_HIP(hipEventElapsedTime(&ms, m.ev0, m.ev1));
