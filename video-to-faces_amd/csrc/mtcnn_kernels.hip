@@ -573,22 +573,35 @@ __global__ __launch_bounds__(256, PNET_GROUPS_PER_CU) void k_pnet(const uint8_t*
             const int corner = lrx & 3, dy = corner >> 1, dx = corner & 1;
             // the tile's conv1 window lies inside the level: no per-corner bounds checks
             const bool interior = 2 * (oy0 + PP_H - 1) + 1 < L1h && 2 * (ox0 + PP_W - 1) + 1 < L1w;
-            const bool mono = a1 >= 0.f;
+            // pool-then-activate is exact when every channel's slope is >= 0 (PReLU and rounding
+            // monotone); with slopes in [0, 1] PReLU is max(v, a v) (two instructions)
+            const uint64_t all = ~0ull;
+            const bool mono = __ballot(a1 >= 0.f) == all;
+            const bool unit_slope = __ballot(a1 >= 0.f && a1 <= 1.f) == all;
+            const bool fastpool = interior && mono;
             // upsampled levels (lh >= H, lw >= W: every bin 1 or 2 frame pixels per side) hold
             // s / 2^(8..10) with |s| <= 1020, exact in fp16: the residual plane is zero there, so
             // its MFMA and its operand reads are skipped (the products it would add are all zero)
             const bool exact = P.lh >= H && P.lw >= W;
+            // fragment f = pooled cells 4f .. 4f+3 of one pooled row (PP_W % 4 == 0): a lane's
+            // operand pixel is its per-lane offset plus a wave-uniform fragment offset
+            static_assert(PP_W % 4 == 0, "a fragment's 4 pooled cells share a row");
+            const int wv = __builtin_amdgcn_readfirstlane(wave);
+            const int lpix = dy * PL_W + dx + 2 * (lrx >> 2);
+            // pooled-map slot of the lane's output: channel lrx of cell 4f + lkx (lanes 12..15 repeat
+            // channels 10, 11, which conv2 never reads)
+            const int qlane = lkx * PQ_C + (lrx < 12 ? lrx : 10 + (lrx & 1));
             auto conv1_frags = [&](auto exact_t) {
             constexpr bool EX = decltype(exact_t)::value;
             // fragments per iteration: the exact path holds one operand plane, so twice the
             // fragments fit the same registers (more independent MFMA chains per wave)
             constexpr int NU = EX ? 4 : 2;
-            for (int f0 = wave; f0 < NF1; f0 += 4 * NU) {
+            for (int f0 = wv; f0 < NF1; f0 += 4 * NU) {
                 int ab[NU];
 #pragma unroll
                 for (int u = 0; u < NU; u++) {
-                    const int pp = min(f0 + 4 * u, NF1 - 1) * 4 + (lrx >> 2);
-                    ab[u] = (2 * (pp / PP_W) + dy) * PL_W + 2 * (pp % PP_W) + dx;
+                    const int f = min(f0 + 4 * u, NF1 - 1);
+                    ab[u] = lpix + 2 * ((4 * f) / PP_W) * PL_W + 2 * ((4 * f) % PP_W);
                 }
                 // slots 8*(lkx&1) .. +7 of row ky = pixels x + 2*(lkx&1), +1 (4 halves each); row 3
                 // (s2 = 1, lkx >= 2) has zero weights: read row 2 instead
@@ -617,10 +630,14 @@ __global__ __launch_bounds__(256, PNET_GROUPS_PER_CU) void k_pnet(const uint8_t*
                             cm[u] = __builtin_amdgcn_mfma_f32_16x16x32_f16(xa[s2][u], w0[s2], cm[u], 0, 0, 0);
                             cd[u] = __builtin_amdgcn_mfma_f32_16x16x32_f16(xa[s2][u], w1[s2], cd[u], 0, 0, 0);
                         }
+                    typedef __attribute__((ext_vector_type(2))) float f32x2;
+                    const f32x2 k11 = {0.00048828125f, 0.00048828125f};
 #pragma unroll
-                    for (int u = 0; u < NU; u++)
-#pragma unroll
-                        for (int i = 0; i < 4; i++) cm[u][i] = __builtin_fmaf(cd[u][i], 0.00048828125f, cm[u][i]);
+                    for (int u = 0; u < NU; u++) {
+                        const f32x2 lo = __builtin_elementwise_fma(f32x2{cd[u][0], cd[u][1]}, k11, f32x2{cm[u][0], cm[u][1]});
+                        const f32x2 hi = __builtin_elementwise_fma(f32x2{cd[u][2], cd[u][3]}, k11, f32x2{cm[u][2], cm[u][3]});
+                        cm[u] = f32x4{lo[0], lo[1], hi[0], hi[1]};
+                    }
                 } else {
                     // cross terms first, scaled by 2^-11 (exact) into the main chain's accumulator:
                     // one accumulator per fragment, no combine step
@@ -640,39 +657,37 @@ __global__ __launch_bounds__(256, PNET_GROUPS_PER_CU) void k_pnet(const uint8_t*
                         for (int u = 0; u < NU; u++)
                             cm[u] = __builtin_amdgcn_mfma_f32_16x16x32_f16(xa[s2][u], w0[s2], cm[u], 0, 0, 0);
                 }
+#pragma unroll
                 for (int u = 0; u < NU; u++) {
                     const int f = f0 + 4 * u;
                     if (f >= NF1) break;
                     const f32x4 cc = cm[u];
-                    const int pp = f * 4 + lkx;
-                    float out = 0.f;  // channels 10, 11 of the padded planes: zero
-                    if (lrx < 10) {
-                        if (interior && mono) {
-                            // PReLU with a non-negative slope is monotone: pool, then activate
-                            out = prelu(fmaxf(fmaxf(cc[0], cc[1]), fmaxf(cc[2], cc[3])) + b1, a1);
-                        } else {
-                            const int py = pp / PP_W, px = pp % PP_W;
-                            const int gy = 2 * (oy0 + py), gx = 2 * (ox0 + px);
-                            float m = -3.402823466e38f;
-                            bool any = false;
+                    float out;
+                    if (fastpool) {
+                        const float v = fmaxf(fmaxf(cc[0], cc[1]), fmaxf(cc[2], cc[3])) + b1;
+                        out = unit_slope ? fmaxf(v, a1 * v) : prelu(v, a1);
+                    } else {
+                        const int pp = f * 4 + lkx;
+                        const int py = pp / PP_W, px = pp % PP_W;
+                        const int gy = 2 * (oy0 + py), gx = 2 * (ox0 + px);
+                        float m = -3.402823466e38f;
+                        bool any = false;
 #pragma unroll
-                            for (int i = 0; i < 4; i++) {
-                                const bool ok = (gy + (i >> 1) < L1h) && (gx + (i & 1) < L1w);
-                                const float v = prelu(cc[i] + b1, a1);
-                                if (ok) {
-                                    m = fmaxf(m, v);
-                                    any = true;
-                                }
+                        for (int i = 0; i < 4; i++) {
+                            const bool ok = (gy + (i >> 1) < L1h) && (gx + (i & 1) < L1w);
+                            const float v = prelu(cc[i] + b1, a1);
+                            if (ok) {
+                                m = fmaxf(m, v);
+                                any = true;
                             }
-                            out = any ? m : 0.f;  // outside the valid pooled map: keep finite
                         }
+                        out = any ? m : 0.f;  // outside the valid pooled map: keep finite
                     }
-                    if (lrx < PQ_C) {
-                        _Float16 x0, x1;
-                        split_f16(out, x0, x1);
-                        sQ[pp * PQ_C + lrx] = x0;
-                        sQ[NPP * PQ_C + pp * PQ_C + lrx] = x1;
-                    }
+                    _Float16 x0, x1;
+                    split_f16(out, x0, x1);
+                    _Float16* q = sQ + f * 4 * PQ_C + qlane;
+                    q[0] = x0;
+                    q[NPP * PQ_C] = x1;
                 }
             }
             };
