@@ -1232,14 +1232,17 @@ __global__ __launch_bounds__(NT) void k_cand_front(const int4* __restrict__ sat,
                                                    const float4* __restrict__ boxes, const int32_t* __restrict__ img,
                                                    const float* __restrict__ w1, const float* __restrict__ b1,
                                                    const float* __restrict__ a1, float* __restrict__ out,
-                                                   int32_t* __restrict__ err) {
+                                                   int32_t* __restrict__ err, int dbg) {
     constexpr int O = S - 2;                // conv1 output side
     constexpr int P = (O - 3 + 1) / 2 + 1;  // ceil-mode pool output side
     constexpr int BR = 2 * PB + 1;          // conv rows per band
     constexpr int NW = NT / 64;
     constexpr int PIX = (S * S + NT - 1) / NT;  // crop pixels per thread
+    // conv ring [32 ch][CS]: an odd channel stride puts the 32 channels a pool read spans on
+    // 32 distinct banks
+    constexpr int CS = (BR * O) | 1;
     __shared__ float crop[3 * S * S];
-    __shared__ float cv[32 * BR * O];
+    __shared__ float cv[32 * CS];
     const int64_t k = blockIdx.x;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, lr = lane & 15, lk = lane >> 4;
     float* o = out + k * (P * P * 32);
@@ -1253,7 +1256,7 @@ __global__ __launch_bounds__(NT) void k_cand_front(const int4* __restrict__ sat,
     // crop bins from the SAT: every thread issues all of its corner loads before using any
     // (the gathers are latency-bound; PIX * 4 loads in flight per thread)
     const int4* sk = sat + (int64_t)img[k] * (H + 1) * (W + 1);
-    {
+    if (!(dbg & 1)) {
         int4 cn[PIX][4];
         int kh[PIX], kw[PIX];
 #pragma unroll
@@ -1297,7 +1300,7 @@ __global__ __launch_bounds__(NT) void k_cand_front(const int4* __restrict__ sat,
         const int r_lo = pr0 == 0 ? 0 : cr0 + 1;
         const int r_hi = min(cr0 + 2 * PB, O - 1);
         const int npos = (r_hi - r_lo + 1) * O;
-        const int nf = npos > 0 ? (npos + 15) / 16 : 0;
+        const int nf = npos > 0 && !(dbg & 2) ? (npos + 15) / 16 : 0;
         for (int f = wave; f < nf; f += NW) {
             const int p = min(f * 16 + lr, npos - 1);
             const int y = r_lo + p / O, x = p % O;
@@ -1317,26 +1320,32 @@ __global__ __launch_bounds__(NT) void k_cand_front(const int4* __restrict__ sat,
                 if (q < npos) {
                     const int yq = r_lo + q / O;
                     const int slot = (yq % BR) * O + (q - (yq - r_lo) * O);
-                    cv[lr * BR * O + slot] = prelu(c0[i] + bb0, aa0);
-                    cv[(16 + lr) * BR * O + slot] = prelu(c1[i] + bb1, aa1);
+                    cv[lr * CS + slot] = prelu(c0[i] + bb0, aa0);
+                    cv[(16 + lr) * CS + slot] = prelu(c1[i] + bb1, aa1);
                 }
             }
         }
         __syncthreads();
         const int npr = min(PB, P - pr0);
-        for (int i = tid; i < npr * P * 32; i += NT) {
+        for (int i = tid; i < ((dbg & 4) ? 0 : npr * P * 32); i += NT) {
             const int c = i & 31, t = i >> 5;
             const int px = t % P, pyl = t / P;
-            float m = -3.402823466e38f;
-            for (int dy = 0; dy < 3; dy++) {
-                const int yy = 2 * (pr0 + pyl) + dy;
-                if (yy >= O) break;
-                for (int dx = 0; dx < 3; dx++) {
-                    const int xx = 2 * px + dx;
-                    if (xx >= O) break;
-                    m = fmaxf(m, cv[c * BR * O + (yy % BR) * O + xx]);
-                }
+            // ceil-mode windows clipped at the map edge: a clipped index is clamped onto the
+            // window's last valid row / column instead (max is idempotent), so every lane runs
+            // the same 9 reads
+            const float* cr = cv + c * CS;
+            int xo[3], yo[3];
+#pragma unroll
+            for (int d = 0; d < 3; d++) {
+                xo[d] = min(2 * px + d, O - 1);
+                yo[d] = (min(2 * (pr0 + pyl) + d, O - 1) % BR) * O;
             }
+            float m = cr[yo[0] + xo[0]];
+#pragma unroll
+            for (int dy = 0; dy < 3; dy++)
+#pragma unroll
+                for (int dx = 0; dx < 3; dx++)
+                    if (dy | dx) m = fmaxf(m, cr[yo[dy] + xo[dx]]);
             o[((pr0 + pyl) * P + px) * 32 + c] = m;
         }
         __syncthreads();
@@ -1348,10 +1357,14 @@ int cand_front_side(bool onet) { return onet ? 23 : 11; }
 void launch_cand_front(bool onet, const int4* sat, int H, int W, const float4* boxes, const int32_t* img, int64_t n,
                        const float* w1, const float* b1, const float* a1, float* out, int32_t* err, hipStream_t st) {
     if (n <= 0) return;
+    static const int dbg = [] {  // phase-skip mask for profiling (VTF_FRONT_DEBUG): 1 crop, 2 conv1, 4 pool
+        const char* e = std::getenv("VTF_FRONT_DEBUG");
+        return e ? std::atoi(e) : 0;
+    }();
     if (onet)
-        k_cand_front<48, 1, 512><<<(unsigned)n, 512, 0, st>>>(sat, H, W, boxes, img, w1, b1, a1, out, err);
+        k_cand_front<48, 1, 512><<<(unsigned)n, 512, 0, st>>>(sat, H, W, boxes, img, w1, b1, a1, out, err, dbg);
     else
-        k_cand_front<24, 3, 256><<<(unsigned)n, 256, 0, st>>>(sat, H, W, boxes, img, w1, b1, a1, out, err);
+        k_cand_front<24, 3, 256><<<(unsigned)n, 256, 0, st>>>(sat, H, W, boxes, img, w1, b1, a1, out, err, dbg);
 }
 
 // heads: x [n, D] -> softmax(x W1^T + b1)[:, 1], x W2^T + b2 (4), optional x W3^T + b3 (10).
