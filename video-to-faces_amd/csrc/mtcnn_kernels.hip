@@ -1227,12 +1227,12 @@ void launch_pnet(bool dense, const uint8_t* frames, int64_t frame_stride, int64_
 // [n, P, P, 32] map reaches HBM (P = 11 / 23).  Conv rows are produced 2*PB per band into a
 // ring of 2*PB+1 rows (the pool window's shared row is kept, not recomputed).
 // w1: [28][32] (k, co; row 27 and channels >= Cout zero); b1, a1: [32].
-template <int S, int PB, int NT>
+template <int S, int PB, int NT, bool XS>
 __global__ __launch_bounds__(NT) void k_cand_front(const int4* __restrict__ sat, int H, int W,
                                                    const float4* __restrict__ boxes, const int32_t* __restrict__ img,
-                                                   const float* __restrict__ w1, const float* __restrict__ b1,
-                                                   const float* __restrict__ a1, float* __restrict__ out,
-                                                   int32_t* __restrict__ err, int dbg) {
+                                                   const float* __restrict__ w1, const _Float16* __restrict__ w1h,
+                                                   const float* __restrict__ b1, const float* __restrict__ a1,
+                                                   float* __restrict__ out, int32_t* __restrict__ err, int dbg) {
     constexpr int O = S - 2;                // conv1 output side
     constexpr int P = (O - 3 + 1) / 2 + 1;  // ceil-mode pool output side
     constexpr int BR = 2 * PB + 1;          // conv rows per band
@@ -1241,7 +1241,11 @@ __global__ __launch_bounds__(NT) void k_cand_front(const int4* __restrict__ sat,
     // conv ring [32 ch][CS]: an odd channel stride puts the 32 channels a pool read spans on
     // 32 distinct banks
     constexpr int CS = (BR * O) | 1;
-    __shared__ float crop[3 * S * S];
+    // crop: fp32 channel planes [3][S*S], or (XS) fp16 split planes [2][S*S + 1][4] (R, G, B, 0;
+    // one zero pixel after each plane: the conv operand reads run one pixel past the last one,
+    // against zero weights)
+    constexpr int CROP_F = XS ? 4 * (S * S + 1) : 3 * S * S;
+    __shared__ __attribute__((aligned(16))) float crop[CROP_F];
     __shared__ float cv[32 * CS];
     const int64_t k = blockIdx.x;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, lr = lane & 15, lk = lane >> 4;
@@ -1252,6 +1256,17 @@ __global__ __launch_bounds__(NT) void k_cand_front(const int4* __restrict__ sat,
         if (tid == 0) atomicAdd(err, 1);
         for (int i = tid; i < P * P * 32; i += NT) o[i] = 0.f;
         return;
+    }
+    // upsampled crops (box within S x S): bins of 1 or 2 pixels per side, every value s / 2^(8..10)
+    // with |s| <= 1020 -- exact in fp16, so the residual plane is zero and skipped
+    const bool exact = XS && hc <= S && wc <= S;
+    typedef __attribute__((ext_vector_type(4))) _Float16 h4;
+    h4* cp0 = (h4*)crop;
+    h4* cp1 = cp0 + (S * S + 1);
+    if (XS && tid == 0) {
+        const h4 z = {(_Float16)0.f, (_Float16)0.f, (_Float16)0.f, (_Float16)0.f};
+        cp0[S * S] = z;
+        cp1[S * S] = z;
     }
     // crop bins from the SAT: every thread issues all of its corner loads before using any
     // (the gathers are latency-bound; PIX * 4 loads in flight per thread)
@@ -1279,17 +1294,43 @@ __global__ __launch_bounds__(NT) void k_cand_front(const int4* __restrict__ sat,
             const int i = tid + j * NT;
             if (i < S * S) {
                 const int4 &a = cn[j][0], &b = cn[j][1], &c = cn[j][2], &d = cn[j][3];
-                crop[i] = bin_avg(d.x - b.x - c.x + a.x, kh[j], kw[j]);
-                crop[S * S + i] = bin_avg(d.y - b.y - c.y + a.y, kh[j], kw[j]);
-                crop[2 * S * S + i] = bin_avg(d.z - b.z - c.z + a.z, kh[j], kw[j]);
+                const float r = bin_avg(d.x - b.x - c.x + a.x, kh[j], kw[j]);
+                const float g = bin_avg(d.y - b.y - c.y + a.y, kh[j], kw[j]);
+                const float bl = bin_avg(d.z - b.z - c.z + a.z, kh[j], kw[j]);
+                if (XS) {
+                    _Float16 r0, r1, g0, g1, b0, b1_;
+                    split_f16(r, r0, r1);
+                    split_f16(g, g0, g1);
+                    split_f16(bl, b0, b1_);
+                    cp0[i] = h4{r0, g0, b0, (_Float16)0.f};
+                    if (!exact) cp1[i] = h4{r1, g1, b1_, (_Float16)0.f};
+                } else {
+                    crop[i] = r;
+                    crop[S * S + i] = g;
+                    crop[2 * S * S + i] = bl;
+                }
             }
         }
     }
-    float wb[7][2];
+    // conv1 weights: fp32 [28][32] (k, co) for the fp32 MFMA path, or the split planes [2][32][64]
+    // (k = ky*16 + kx*4 + c) as the B operand of 16x16x32 fp16 MFMAs, channel block nb = co / 16
+    float wb[XS ? 1 : 7][2];
+    f16x8 wh0[XS ? 2 : 1][2], wh1[XS ? 2 : 1][2];
+    if (XS) {
 #pragma unroll
-    for (int s = 0; s < 7; s++) {
-        wb[s][0] = w1[(4 * s + lk) * 32 + lr];
-        wb[s][1] = w1[(4 * s + lk) * 32 + 16 + lr];
+        for (int s2 = 0; s2 < 2; s2++)
+#pragma unroll
+            for (int nb = 0; nb < 2; nb++) {
+                const _Float16* src = w1h + (16 * nb + lr) * 64 + 32 * s2 + 8 * lk;
+                wh0[s2][nb] = *(const f16x8*)src;
+                wh1[s2][nb] = *(const f16x8*)(src + 32 * 64);
+            }
+    } else {
+#pragma unroll
+        for (int s = 0; s < 7; s++) {
+            wb[s][0] = w1[(4 * s + lk) * 32 + lr];
+            wb[s][1] = w1[(4 * s + lk) * 32 + 16 + lr];
+        }
     }
     const float bb0 = b1[lr], bb1 = b1[16 + lr], aa0 = a1[lr], aa1 = a1[16 + lr];
     __syncthreads();
@@ -1305,14 +1346,41 @@ __global__ __launch_bounds__(NT) void k_cand_front(const int4* __restrict__ sat,
             const int p = min(f * 16 + lr, npos - 1);
             const int y = r_lo + p / O, x = p % O;
             f32x4 c0 = {0.f, 0.f, 0.f, 0.f}, c1 = {0.f, 0.f, 0.f, 0.f};
+            if (XS) {
+                // split operands (k_pnet conv1's K layout): slots 8*(lk&1) .. +7 of row ky are
+                // pixels x + 2*(lk&1), +1; row 3 (s2 = 1, lk >= 2) has zero weights
+                const _Float16* c0p = (const _Float16*)cp0;
+                f32x4 d0 = c0, d1 = c0;
 #pragma unroll
-            for (int s = 0; s < 7; s++) {
-                const int kk = 4 * s + lk;
-                const int kc = min(kk, 26);
-                const int c = kc / 9, r = kc - 9 * c;
-                const float av = kk < 27 ? crop[c * S * S + (y + r / 3) * S + x + r % 3] : 0.f;
-                c0 = __builtin_amdgcn_mfma_f32_16x16x4f32(av, wb[s][0], c0, 0, 0, 0);
-                c1 = __builtin_amdgcn_mfma_f32_16x16x4f32(av, wb[s][1], c1, 0, 0, 0);
+                for (int s2 = 0; s2 < 2; s2++) {
+                    const int ky = min(2 * s2 + (lk >> 1), 2);
+                    const int pix = (y + ky) * S + x + 2 * (lk & 1);
+                    const f16x8 xa = ld_h8(c0p + pix * 4);
+                    c0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(xa, wh0[s2][0], c0, 0, 0, 0);
+                    c1 = __builtin_amdgcn_mfma_f32_16x16x32_f16(xa, wh0[s2][1], c1, 0, 0, 0);
+                    d0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(xa, wh1[s2][0], d0, 0, 0, 0);
+                    d1 = __builtin_amdgcn_mfma_f32_16x16x32_f16(xa, wh1[s2][1], d1, 0, 0, 0);
+                    if (!exact) {
+                        const f16x8 xb = ld_h8(c0p + (S * S + 1) * 4 + pix * 4);
+                        d0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(xb, wh0[s2][0], d0, 0, 0, 0);
+                        d1 = __builtin_amdgcn_mfma_f32_16x16x32_f16(xb, wh0[s2][1], d1, 0, 0, 0);
+                    }
+                }
+#pragma unroll
+                for (int i = 0; i < 4; i++) {
+                    c0[i] = __builtin_fmaf(d0[i], 0.00048828125f, c0[i]);
+                    c1[i] = __builtin_fmaf(d1[i], 0.00048828125f, c1[i]);
+                }
+            } else {
+#pragma unroll
+                for (int s = 0; s < 7; s++) {
+                    const int kk = 4 * s + lk;
+                    const int kc = min(kk, 26);
+                    const int c = kc / 9, r = kc - 9 * c;
+                    const float av = kk < 27 ? crop[c * S * S + (y + r / 3) * S + x + r % 3] : 0.f;
+                    c0 = __builtin_amdgcn_mfma_f32_16x16x4f32(av, wb[s][0], c0, 0, 0, 0);
+                    c1 = __builtin_amdgcn_mfma_f32_16x16x4f32(av, wb[s][1], c1, 0, 0, 0);
+                }
             }
 #pragma unroll
             for (int i = 0; i < 4; i++) {
@@ -1355,16 +1423,22 @@ __global__ __launch_bounds__(NT) void k_cand_front(const int4* __restrict__ sat,
 int cand_front_side(bool onet) { return onet ? 23 : 11; }
 
 void launch_cand_front(bool onet, const int4* sat, int H, int W, const float4* boxes, const int32_t* img, int64_t n,
-                       const float* w1, const float* b1, const float* a1, float* out, int32_t* err, hipStream_t st) {
+                       const float* w1, const _Float16* w1h, const float* b1, const float* a1, float* out, int32_t* err,
+                       hipStream_t st) {
     if (n <= 0) return;
     static const int dbg = [] {  // phase-skip mask for profiling (VTF_FRONT_DEBUG): 1 crop, 2 conv1, 4 pool
         const char* e = std::getenv("VTF_FRONT_DEBUG");
         return e ? std::atoi(e) : 0;
     }();
-    if (onet)
-        k_cand_front<48, 1, 512><<<(unsigned)n, 512, 0, st>>>(sat, H, W, boxes, img, w1, b1, a1, out, err, dbg);
+    // w1h (split conv1 planes) selects conv1 on fp16 matrix cores; null keeps the fp32 MFMA path
+    if (onet && w1h)
+        k_cand_front<48, 1, 512, true><<<(unsigned)n, 512, 0, st>>>(sat, H, W, boxes, img, w1, w1h, b1, a1, out, err, dbg);
+    else if (onet)
+        k_cand_front<48, 1, 512, false><<<(unsigned)n, 512, 0, st>>>(sat, H, W, boxes, img, w1, w1h, b1, a1, out, err, dbg);
+    else if (w1h)
+        k_cand_front<24, 3, 256, true><<<(unsigned)n, 256, 0, st>>>(sat, H, W, boxes, img, w1, w1h, b1, a1, out, err, dbg);
     else
-        k_cand_front<24, 3, 256><<<(unsigned)n, 256, 0, st>>>(sat, H, W, boxes, img, w1, b1, a1, out, err, dbg);
+        k_cand_front<24, 3, 256, false><<<(unsigned)n, 256, 0, st>>>(sat, H, W, boxes, img, w1, w1h, b1, a1, out, err, dbg);
 }
 
 // heads: x [n, D] -> softmax(x W1^T + b1)[:, 1], x W2^T + b2 (4), optional x W3^T + b3 (10).

@@ -521,8 +521,10 @@ static void cand_nets(Mtcnn& m, bool onet, const int4* sat, int H, int W, const 
     const int P = cand_front_side(onet);
     float* x0 = m.ar.get<float>(S_CROP, (size_t)n * P * P * 32);
     const int rl = net;
-    launch_cand_front(onet, sat, H, W, boxes, img, n, m.fw[rl], onet ? m.ol[0].b : m.rl[0].b,
-                      onet ? m.ol[0].a : m.rl[0].a, x0, err, st);
+    // conv1 on split fp16 unless the fp32 paths are forced (crop values lie in [-1, 1]: no range
+    // guard needed)
+    launch_cand_front(onet, sat, H, W, boxes, img, n, m.fw[rl], m.cand_x[net] != 0 ? m.cf[net].w1h : nullptr,
+                      onet ? m.ol[0].b : m.rl[0].b, onet ? m.ol[0].a : m.rl[0].a, x0, err, st);
     run_candidates(m, onet, x0, n, reg, lm, prob, 1, m.fused && m.cand_x[net] != 0 ? 1 : 0);
 }
 
