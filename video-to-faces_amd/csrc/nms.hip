@@ -185,13 +185,29 @@ __global__ __launch_bounds__(64 * SCAN_WAVES) void k_nms_scan(const uint64_t* __
     const uint64_t* msk = mask + seg_mask_off[s];
     const int64_t beg = seg_beg[s];
     for (int w = threadIdx.x; w < nb; w += 64 * SCAN_WAVES) removed[w] = 0;
+    // the words a row block needs (its diagonal word and the first round of later column
+    // words) are loaded one block ahead, unconditionally: the global-load round trip overlaps the
+    // previous block's scan instead of following it (the kept mask is applied after the load)
+    constexpr int G = 8;
+    auto load_block = [&](int cb, uint64_t& dg, uint64_t (&v)[G]) {
+        const uint64_t* blk = msk + (int64_t)cb * nb * 64 + lane;
+        dg = (wave == 0 && cb * 64 + lane < m) ? blk[(int64_t)cb * 64] : 0ull;
+#pragma unroll
+        for (int g = 0; g < G; g++) v[g] = blk[(int64_t)min(cb + 1 + wave * G + g, nb - 1) * 64];
+    };
+    uint64_t dg_n, v_n[G];
+    load_block(0, dg_n, v_n);
     __syncthreads();
     for (int cb = 0; cb < nb; cb++) {
         const uint64_t* blk = msk + (int64_t)cb * nb * 64 + lane;
+        const uint64_t diag = dg_n;
+        uint64_t v[G];
+#pragma unroll
+        for (int g = 0; g < G; g++) v[g] = v_n[g];
+        if (cb + 1 < nb) load_block(cb + 1, dg_n, v_n);
         if (wave == 0) {
             const int row = cb * 64 + lane;
             const int nrow = min(64, m - cb * 64);
-            const uint64_t diag = (row < m) ? blk[(int64_t)cb * 64] : 0ull;
             const uint64_t valid = nrow == 64 ? ~0ull : ((1ull << nrow) - 1ull);
             uint64_t rem = removed[cb];
             uint64_t kept = 0;
@@ -212,18 +228,15 @@ __global__ __launch_bounds__(64 * SCAN_WAVES) void k_nms_scan(const uint64_t* __
         __syncthreads();
         const uint64_t kept = s_kept;
         if (kept != 0) {
-            const bool mine = (kept >> lane) & 1ull;
-            constexpr int G = 8;
+            const uint64_t mine = ((kept >> lane) & 1ull) ? ~0ull : 0ull;
             for (int w0 = cb + 1 + wave * G; w0 < nb; w0 += SCAN_WAVES * G) {
-                uint64_t v[G];
+                if (w0 != cb + 1 + wave * G) {  // rounds past the first: loaded here
 #pragma unroll
-                for (int g = 0; g < G; g++) {
-                    const int w = min(w0 + g, nb - 1);
-                    v[g] = mine ? blk[(int64_t)w * 64] : 0ull;
+                    for (int g = 0; g < G; g++) v[g] = blk[(int64_t)min(w0 + g, nb - 1) * 64];
                 }
 #pragma unroll
                 for (int g = 0; g < G; g++) {
-                    const uint64_t r = wave_or(v[g]);
+                    const uint64_t r = wave_or(v[g] & mine);
                     if (lane == 0 && w0 + g < nb) removed[w0 + g] |= r;
                 }
             }
