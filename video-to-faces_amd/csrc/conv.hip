@@ -232,6 +232,13 @@ __global__ __launch_bounds__(256) void k_conv(ConvParams p) {
 
     vec ra[RA], rb[RB];
     auto load_tile = [&](int kcur, int ci_, int kw0, int kh0) {
+        if (X && (p.xdbg & 2)) {
+#pragma unroll
+            for (int r = 0; r < RA; r++) ra[r] = vec{};
+#pragma unroll
+            for (int r = 0; r < RB; r++) rb[r] = vec{};
+            return;
+        }
 #pragma unroll
         for (int r = 0; r < RA; r++) {
             vec v = {};
@@ -255,11 +262,16 @@ __global__ __launch_bounds__(256) void k_conv(ConvParams p) {
             auto put = [&](char* base, int rows, int row, const vec& v) {
                 h4 x0, x1;
                 float mx = 0.f;
+                if (p.xdbg & 1) {
 #pragma unroll
-                for (int e = 0; e < 4; e++) {
-                    x0[e] = (_Float16)to_f(v[e]);
-                    x1[e] = (_Float16)((to_f(v[e]) - (float)x0[e]) * 2048.f);
-                    mx = fmaxf(mx, fabsf(to_f(v[e])));
+                    for (int e = 0; e < 4; e++) x0[e] = x1[e] = (_Float16)to_f(v[e]);
+                } else {
+#pragma unroll
+                    for (int e = 0; e < 4; e++) {
+                        x0[e] = (_Float16)to_f(v[e]);
+                        x1[e] = (_Float16)((to_f(v[e]) - (float)x0[e]) * 2048.f);
+                        mx = fmaxf(mx, fabsf(to_f(v[e])));
+                    }
                 }
                 // also catches NaN; one atomic per wave, not per lane
                 if (p.ovf && __ballot(!(mx < 16384.f)) && __lane_id() == 0) atomicOr(p.ovf, 1);
@@ -558,6 +570,11 @@ static void launch_tile(const ConvParams& p0, hipStream_t st) {
     p.ws = nullptr;
     if (p.split > 1) p.ws = splitk_workspace(st, (size_t)p.split * p.M * p.Cout * sizeof(float));
     p.group_m = conv_group_m();
+    static const int xdbg = [] {
+        const char* e = std::getenv("VTF_CONV_XDBG");
+        return e ? std::atoi(e) : 0;
+    }();
+    p.xdbg = p.f16x ? xdbg : 0;
     dim3 g((unsigned)gx, (unsigned)gy, (unsigned)p.split);
     if (p.split > 1) {
         k_conv<T, BM, BN, BK, true><<<g, 256, 0, st>>>(p);

@@ -278,6 +278,27 @@ __device__ inline PNetLevel load_level(const VTF_CONST PNetLevel* p) {
     return r;
 }
 
+// (row, column) of a linear byte index in a w-wide frame patch, stepped by one workgroup pass
+// (256): one division per thread instead of one per byte
+struct PatchIdx {
+    int r, q, w, dr, dq;
+    __device__ void init(int i, int w_) {
+        w = w_;
+        r = i / w;
+        q = i - r * w;
+        dr = 256 / w;
+        dq = 256 - dr * w;
+    }
+    __device__ void step() {
+        q += dq;
+        r += dr;
+        if (q >= w) {
+            q -= w;
+            r++;
+        }
+    }
+};
+
 constexpr int PNET_TILE_CHUNK = 4;
 constexpr int PNET_GROUPS_PER_CU = (160 * 1024) / ((PNET_LDS + 511) / 512 * 512);  // LDS granule: 512 B
 static_assert(PNET_GROUPS_PER_CU >= 2, "k_pnet tile too large for 2 workgroups per CU");
@@ -395,13 +416,16 @@ __global__ __launch_bounds__(256, PNET_GROUPS_PER_CU) void k_pnet(const uint8_t*
         // (gathers below issue 8 loads per thread before the first use: latency-bound otherwise)
         if (staged && !(o.dbg & 64)) {
             const int nbytes = (fy1 - fy0) * pw3;
+            const uint8_t* src = fr + (int64_t)fy0 * row_stride + fx0 * 3;
+            const int64_t last = (int64_t)(fy1 - fy0 - 1) * row_stride + pw3 - 1;
+            PatchIdx ix;
+            ix.init(tid + (pf_done ? 256 * 8 : 0), pw3);
             for (int i0 = tid + (pf_done ? 256 * 8 : 0); i0 < nbytes; i0 += 256 * 8) {
                 uint8_t v[8];
 #pragma unroll
                 for (int j = 0; j < 8; j++) {
-                    const int i = min(i0 + j * 256, nbytes - 1);
-                    const int r = i / pw3, q = i - r * pw3;
-                    v[j] = fr[(int64_t)(fy0 + r) * row_stride + fx0 * 3 + q];
+                    v[j] = src[min((int64_t)ix.r * row_stride + ix.q, last)];
+                    ix.step();
                 }
 #pragma unroll
                 for (int j = 0; j < 8; j++)
@@ -1002,11 +1026,13 @@ __global__ __launch_bounds__(256, PNET_GROUPS_PER_CU) void k_pnet(const uint8_t*
                         }
                     }
                 }
+                const int64_t last = pf_rows ? (int64_t)(nb2 / qw3 - 1) * row_stride + qw3 - 1 : 0;
+                PatchIdx ix;
+                ix.init(tid, qw3);
 #pragma unroll
                 for (int j = 0; j < 8; j++) {
-                    const int i = min(tid + j * 256, nb2 - 1);
-                    const int r = i / qw3, q = i - r * qw3;
-                    pfv[j] = pf_src[(int64_t)r * row_stride + q];
+                    pfv[j] = pf_src[min((int64_t)ix.r * row_stride + ix.q, last)];
+                    ix.step();
                 }
                 pf_n = pf_rows ? nb2 : 0;
             }
