@@ -94,6 +94,8 @@ __device__ inline void conv_epilogue(const ConvParams& p, int64_t m, int c, floa
         out[o + rs + p.out_cstride] = tv;
     } else if (p.out_f32) {
         ((float*)p.out)[m * p.out_cstride + p.out_coff + c] = v;
+    } else if (p.n_split && c >= p.n_split) {
+        ((T*)p.out2)[m * p.out2_cstride + p.out2_coff + (c - p.n_split)] = from_f<T>(v);
     } else {
         out[m * p.out_cstride + p.out_coff + c] = from_f<T>(v);
     }
@@ -143,6 +145,8 @@ __device__ inline void conv_epilogue8(const ConvParams& p, int64_t m, int c0, fl
         float* out = (float*)p.out + m * p.out_cstride + p.out_coff + c0;
         *(f32x4*)out = f32x4{v[0], v[1], v[2], v[3]};
         *(f32x4*)(out + 4) = f32x4{v[4], v[5], v[6], v[7]};
+    } else if (p.n_split && c0 >= p.n_split) {
+        *(t8*)((T*)p.out2 + m * p.out2_cstride + p.out2_coff + (c0 - p.n_split)) = o;
     } else {
         *(t8*)((T*)p.out + m * p.out_cstride + p.out_coff + c0) = o;
     }
@@ -406,7 +410,8 @@ __global__ __launch_bounds__(256) void k_conv(ConvParams p) {
     // 2-byte accesses scattered over 4 rows per instruction
     if constexpr (!SPLIT) {
         const bool vec_ok = (p.Cout % 8 == 0) && (p.out_cstride % 8 == 0) && (p.out_coff % 8 == 0) &&
-                            (!p.res || p.res_cstride % 8 == 0);
+                            (!p.res || p.res_cstride % 8 == 0) &&
+                            (!p.n_split || (p.n_split % 8 == 0 && p.out2_cstride % 8 == 0 && p.out2_coff % 8 == 0));
         if (vec_ok) {
             __syncthreads();  // every wave is done with the operand tiles
             float* E = (float*)smem;
@@ -627,6 +632,8 @@ void launch_conv(const ConvParams& p, bool bf16, hipStream_t st) {
     VTF_CHECK(p.in_cstride == 0 || (p.in_cstride >= p.Cin && p.in_cstride % 8 == 0), VTF_E_ARG,
               "conv: bad input channel stride");
     VTF_CHECK(!p.res_up2 || (p.OH % 2 == 0 && p.OW % 2 == 0), VTF_E_ARG, "conv: half-resolution residual needs even OH/OW");
+    VTF_CHECK(!p.n_split || (p.out2 && p.n_split > 0 && p.n_split < p.Cout && !p.up2 && !p.out_f32), VTF_E_ARG,
+              "conv: output split needs out2, 0 < n_split < Cout, plain layout");
     if (bf16)
         launch_t<__bf16>(p, st);
     else

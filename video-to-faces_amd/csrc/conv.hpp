@@ -38,6 +38,12 @@ struct ConvParams {
     int64_t M;           // N*OH*OW
     int N, H, W, Cin, OH, OW, Cout, KH, KW, sh, sw, ph, pw, K;
     int out_cstride, out_coff, res_cstride;
+    // output channels >= n_split (n_split % 8 == 0; 0 = off) go to out2 [.., out2_cstride] at
+    // channel out2_coff + (c - n_split): sibling 1x1 convs of one input run as one launch
+    // (FaceNet branches) while each part lands in its own buffer
+    int n_split;
+    void* out2;
+    int out2_cstride, out2_coff;
 };
 
 void launch_conv(const ConvParams& p, bool bf16, hipStream_t st);

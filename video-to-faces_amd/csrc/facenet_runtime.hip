@@ -1,7 +1,9 @@
 // FaceNet (InceptionResnetV1) runtime: layer table, buffer plan, forward.
 // Mirrors src/videotofaces/encoders/facenet.py:10-183 layer for layer; every conv is one
 // launch of the implicit-GEMM kernel (conv.hip) with its BN/bias/residual/ReLU epilogue
-// fused; concatenations are written in place as channel slices.
+// fused; concatenations are written in place as channel slices.  Sibling 1x1 convs that read the
+// same input (the first conv of every Inception branch) run as one merged launch whose output
+// channels are split between the concat buffer and the branch temporaries.
 #include <cmath>
 #include <cstring>
 #include <vector>
@@ -28,6 +30,8 @@ struct Facenet {
     bool bf16 = false;
     hipStream_t st = 0;
     std::vector<Layer> L;
+    // merged sibling 1x1 convs, keyed by their first member's layer index
+    std::vector<std::pair<int, Layer>> LM;
     float* head_w = nullptr;  // [512][1792] fp32
     float* head_alpha = nullptr;
     float* head_beta = nullptr;
@@ -113,6 +117,8 @@ static void build(Facenet& F, const float* params, int64_t n_params) {
         src += n;
         return p;
     };
+    std::vector<std::vector<float>> host_w;  // per layer [cout][K] fp32 (merged-layer source)
+    std::vector<std::vector<float>> host_a, host_b;
     for (const G& g : geo) {
         Layer l{};
         l.cin = g.cin;
@@ -141,6 +147,7 @@ static void build(Facenet& F, const float* params, int64_t n_params) {
         } else {
             l.w = F.upload(wt);
         }
+        host_w.push_back(std::move(wt));
         if (g.bias) {
             const float* b = take(g.cout);
             l.b = F.upload(std::vector<float>(b, b + g.cout));
@@ -153,9 +160,42 @@ static void build(Facenet& F, const float* params, int64_t n_params) {
             bn_fold(bw, bb, bm, bv, g.cout, 1e-3f, a, be);  // conv_unit BN eps 1e-3 (facenet.py:11)
             l.alpha = F.upload(a);
             l.beta = F.upload(be);
+            host_a.resize(F.L.size() + 1);
+            host_b.resize(F.L.size() + 1);
+            host_a[F.L.size()] = a;
+            host_b[F.L.size()] = be;
         }
         F.L.push_back(l);
     }
+    // merged sibling 1x1 convs (same input, BN + ReLU units): weights / BN rows concatenated, so
+    // every output channel's dot product and epilogue are those of its own conv
+    auto merge = [&](std::vector<int> ids) {
+        Layer m = F.L[ids[0]];
+        std::vector<float> w, a, be;
+        m.cout = 0;
+        for (int i : ids) {
+            VTF_CHECK(F.L[i].kh == 1 && F.L[i].kw == 1 && F.L[i].cin == m.cin && !F.L[i].bias, VTF_E_ARG,
+                      "facenet: merged convs must be sibling 1x1 units");
+            w.insert(w.end(), host_w[i].begin(), host_w[i].end());
+            a.insert(a.end(), host_a[i].begin(), host_a[i].end());
+            be.insert(be.end(), host_b[i].begin(), host_b[i].end());
+            m.cout += F.L[i].cout;
+        }
+        if (F.bf16) {
+            std::vector<uint16_t> wb(w.size());
+            for (size_t i = 0; i < w.size(); i++) wb[i] = f2bf(w[i]);
+            m.w = F.upload(wb);
+        } else {
+            m.w = F.upload(w);
+        }
+        m.alpha = F.upload(a);
+        m.beta = F.upload(be);
+        F.LM.push_back({ids[0], m});
+    };
+    for (int k = 0; k < 5; k++) merge({6 + 7 * k, 7 + 7 * k, 9 + 7 * k});  // Block35 branches 0, 1, 2
+    for (int k = 0; k < 10; k++) merge({45 + 5 * k, 46 + 5 * k});         // Block17 branches 0, 1
+    merge({95, 97, 99});                                                   // Mixed_7a branches 0, 1, 2
+    for (int k = 0; k < 6; k++) merge({102 + 5 * k, 103 + 5 * k});        // Block8 branches 0, 1
     const float* hw = take(512 * 1792);
     F.head_w = F.upload(std::vector<float>(hw, hw + 512 * 1792));
     const float* bw = take(512);
@@ -174,12 +214,16 @@ struct Act {
     int H, W, C;
 };
 
+// in_cstride / in_coff: read channels [in_coff, in_coff + in.C) of a buffer with in_cstride
+// channels per pixel (0: the input is dense)
 static void conv(Facenet& F, int li, const Act& in, int N, void* out, int out_cstride, int out_coff,
-                 const void* res = nullptr, float scale = 1.f, bool relu = true, Act* out_act = nullptr) {
+                 const void* res = nullptr, float scale = 1.f, bool relu = true, Act* out_act = nullptr,
+                 int in_cstride = 0, int in_coff = 0) {
     const Layer& l = F.L[li];
     VTF_CHECK(in.C == l.cin_pad, VTF_E_ARG, "facenet: channel mismatch");
     ConvParams p{};
-    p.in = in.p;
+    p.in = (const char*)in.p + (size_t)in_coff * (F.bf16 ? 2 : 4);
+    p.in_cstride = in_cstride;
     p.w = l.w;
     p.out = out;
     p.N = N;
@@ -215,6 +259,41 @@ static void conv(Facenet& F, int li, const Act& in, int N, void* out, int out_cs
     if (out_act) *out_act = Act{out, p.OH, p.OW, out_cstride};
 }
 
+// merged sibling 1x1 convs whose first member is layer li: output channels [0, n_split) to
+// out (out_cstride, out_coff), the rest to out2 (out2_cstride, out2_coff)
+static void conv_merged(Facenet& F, int li, const Act& in, int N, void* out, int out_cstride, int out_coff,
+                        int n_split, void* out2, int out2_cstride, int out2_coff) {
+    const Layer* l = nullptr;
+    for (auto& e : F.LM)
+        if (e.first == li) l = &e.second;
+    VTF_CHECK(l && in.C == l->cin_pad, VTF_E_ARG, "facenet: no merged conv at this layer");
+    ConvParams p{};
+    p.in = in.p;
+    p.w = l->w;
+    p.out = out;
+    p.N = N;
+    p.H = in.H;
+    p.W = in.W;
+    p.Cin = l->cin_pad;
+    p.KH = p.KW = p.sh = p.sw = 1;
+    p.OH = in.H;
+    p.OW = in.W;
+    p.Cout = l->cout;
+    p.K = l->cin_pad;
+    p.M = (int64_t)N * p.OH * p.OW;
+    p.out_cstride = out_cstride;
+    p.out_coff = out_coff;
+    p.alpha = l->alpha;
+    p.beta = l->beta;
+    p.scale = 1.f;
+    p.relu = 1;
+    p.n_split = n_split;
+    p.out2 = out2;
+    p.out2_cstride = out2_cstride;
+    p.out2_coff = out2_coff;
+    launch_conv(p, F.bf16, F.st);
+}
+
 // x: NHWC [N,160,160,8] (precision dtype) -> emb [N,512] fp32
 static void forward(Facenet& F, const void* x, int N, float* emb) {
     const size_t es = F.bf16 ? 2 : 4;
@@ -248,11 +327,12 @@ static void forward(Facenet& F, const void* x, int N, float* emb) {
     Act t1{}, t2{};
     // 5 x Block35 (facenet.py:14-33), scale 0.17
     for (int k = 0; k < 5; k++) {
-        conv(F, li++, X, N, CAT, 96, 0);
-        conv(F, li++, X, N, T1, 32, 0, nullptr, 1.f, true, &t1);
-        conv(F, li++, t1, N, CAT, 96, 32);
-        conv(F, li++, X, N, T1, 32, 0, nullptr, 1.f, true, &t1);
-        conv(F, li++, t1, N, T2, 32, 0, nullptr, 1.f, true, &t2);
+        // branch 0 -> CAT[0:32]; branch 1 / 2 heads -> T1[0:32] / T1[32:64]
+        conv_merged(F, li, X, N, CAT, 96, 0, 32, T1, 64, 0);
+        li += 2;
+        conv(F, li++, Act{T1, X.H, X.W, 32}, N, CAT, 96, 32, nullptr, 1.f, true, nullptr, 64, 0);
+        li++;
+        conv(F, li++, Act{T1, X.H, X.W, 32}, N, T2, 32, 0, nullptr, 1.f, true, &t2, 64, 32);
         conv(F, li++, t2, N, CAT, 96, 64);
         conv(F, li++, Act{CAT, X.H, X.W, 96}, N, Y, 256, 0, X.p, 0.17f, true);
         swap(256);
@@ -271,8 +351,9 @@ static void forward(Facenet& F, const void* x, int N, float* emb) {
     }
     // 10 x Block17 (facenet.py:36-56), scale 0.10
     for (int k = 0; k < 10; k++) {
-        conv(F, li++, X, N, CAT, 256, 0);
-        conv(F, li++, X, N, T1, 128, 0, nullptr, 1.f, true, &t1);
+        conv_merged(F, li, X, N, CAT, 256, 0, 128, T1, 128, 0);
+        li += 2;
+        t1 = Act{T1, X.H, X.W, 128};
         conv(F, li++, t1, N, T2, 128, 0, nullptr, 1.f, true, &t2);
         conv(F, li++, t2, N, CAT, 256, 128);
         conv(F, li++, Act{CAT, X.H, X.W, 256}, N, Y, 896, 0, X.p, 0.10f, true);
@@ -281,12 +362,15 @@ static void forward(Facenet& F, const void* x, int N, float* emb) {
     // Mixed_7a (facenet.py:104-120)
     {
         Act o{};
-        conv(F, li++, X, N, T1, 256, 0, nullptr, 1.f, true, &t1);
-        conv(F, li++, t1, N, Y, 1792, 0, nullptr, 1.f, true, &o);
-        conv(F, li++, X, N, T1, 256, 0, nullptr, 1.f, true, &t1);
-        conv(F, li++, t1, N, Y, 1792, 384);
-        conv(F, li++, X, N, T1, 256, 0, nullptr, 1.f, true, &t1);
-        conv(F, li++, t1, N, T2, 256, 0, nullptr, 1.f, true, &t2);
+        // the three branch heads (1x1, 896 -> 256 each) as one launch into T1 [.., 768]
+        conv_merged(F, li, X, N, T1, 768, 0, 0, nullptr, 0, 0);
+        const Act h{T1, X.H, X.W, 256};
+        li++;
+        conv(F, li++, h, N, Y, 1792, 0, nullptr, 1.f, true, &o, 768, 0);
+        li++;
+        conv(F, li++, h, N, Y, 1792, 384, nullptr, 1.f, true, nullptr, 768, 256);
+        li++;
+        conv(F, li++, h, N, T2, 256, 0, nullptr, 1.f, true, &t2, 768, 512);
         conv(F, li++, t2, N, Y, 1792, 640);
         launch_maxpool(X.p, N, X.H, X.W, 896, Y, 1792, 896, F.bf16, F.st);
         X.H = o.H;
@@ -296,8 +380,9 @@ static void forward(Facenet& F, const void* x, int N, float* emb) {
     // 5 x Block8 (scale 0.20) + Block8(scale 1.0, relu=False) (facenet.py:59-81,142-143)
     for (int k = 0; k < 6; k++) {
         bool last = k == 5;
-        conv(F, li++, X, N, CAT, 384, 0);
-        conv(F, li++, X, N, T1, 192, 0, nullptr, 1.f, true, &t1);
+        conv_merged(F, li, X, N, CAT, 384, 0, 192, T1, 192, 0);
+        li += 2;
+        t1 = Act{T1, X.H, X.W, 192};
         conv(F, li++, t1, N, T2, 192, 0, nullptr, 1.f, true, &t2);
         conv(F, li++, t2, N, CAT, 384, 192);
         conv(F, li++, Act{CAT, X.H, X.W, 384}, N, Y, 1792, 0, X.p, last ? 1.0f : 0.20f, !last);
