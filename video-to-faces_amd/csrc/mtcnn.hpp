@@ -45,6 +45,14 @@ struct PNetOut {
 void launch_sat(const uint8_t* frames, int64_t frame_stride, int64_t row_stride, int B, int H, int W, int4* sat,
                 hipStream_t st);
 void launch_resample_sat(const int4* sat, int B, int H, int W, int lh, int lw, float* out, hipStream_t st);
+struct ResampleLevels {  // precomputed pyramid levels of one det-batch (k_resample_sat_multi)
+    static constexpr int MAXL = 32;
+    int n;
+    int lh[MAXL], lw[MAXL];
+    int64_t beg[MAXL + 1];  // first output element (b, y, x) of each level in the flattened grid
+    float* out[MAXL];       // [B][3][lh][lw]
+};
+void launch_resample_sat_multi(const int4* sat, int B, int H, int W, const ResampleLevels& lv, hipStream_t st);
 void launch_pnet(bool dense, const uint8_t* frames, int64_t frame_stride, int64_t row_stride, int H, int W,
                  const PNetLevel* d_levels, int n_levels, int64_t total_tiles, const PNetW& w, const PNetOut& o,
                  uint32_t* d_tile_ctr, hipStream_t st);

@@ -200,6 +200,33 @@ void launch_resample_sat(const int4* sat, int B, int H, int W, int lh, int lw, f
     k_resample_sat<<<cdiv(n, 256), 256, 0, st>>>(sat, B, H, W, lh, lw, out);
 }
 
+// every precomputed level of a det-batch in one launch (the small levels alone are launch-bound)
+__global__ void k_resample_sat_multi(const int4* __restrict__ sat, int B, int H, int W, ResampleLevels lv) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= lv.beg[lv.n]) return;
+    int l = 0;
+    while (l + 1 < lv.n && i >= lv.beg[l + 1]) l++;
+    const int lh = lv.lh[l], lw = lv.lw[l];
+    const int64_t j = i - lv.beg[l];
+    const int lx = (int)(j % lw);
+    const int ly = (int)((j / lw) % lh);
+    const int b = (int)(j / ((int64_t)lw * lh));
+    const int y0 = (int)(((int64_t)ly * H) / lh), y1 = (int)(((int64_t)(ly + 1) * H + lh - 1) / lh);
+    const int x0 = (int)(((int64_t)lx * W) / lw), x1 = (int)(((int64_t)(lx + 1) * W + lw - 1) / lw);
+    const int4 s = sat_box(sat + (int64_t)b * (H + 1) * (W + 1), W + 1, y0, y1, x0, x1);
+    const int64_t plane = (int64_t)lh * lw, o = (int64_t)b * 3 * plane + (int64_t)ly * lw + lx;
+    float* out = lv.out[l];
+    out[o] = bin_avg(s.x, y1 - y0, x1 - x0);
+    out[o + plane] = bin_avg(s.y, y1 - y0, x1 - x0);
+    out[o + 2 * plane] = bin_avg(s.z, y1 - y0, x1 - x0);
+}
+
+void launch_resample_sat_multi(const int4* sat, int B, int H, int W, const ResampleLevels& lv, hipStream_t st) {
+    VTF_CHECK(lv.n >= 0 && lv.n <= ResampleLevels::MAXL, VTF_E_LIMIT, "mtcnn: too many precomputed levels");
+    if (lv.n == 0 || lv.beg[lv.n] == 0) return;
+    k_resample_sat_multi<<<cdiv(lv.beg[lv.n], 256), 256, 0, st>>>(sat, B, H, W, lv);
+}
+
 // ----------------------------------------------------------------------------------- PNet
 
 constexpr int PT_H = PNET_TH, PT_W = PNET_TW;         // output cells per tile (mtcnn.hpp)

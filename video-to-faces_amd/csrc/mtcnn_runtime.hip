@@ -635,14 +635,21 @@ static void detect(Mtcnn& m, const uint8_t* frames, int on_dev, int B, int H, in
         for (auto& L : lv)
             if ((int64_t)H > 2 * (int64_t)L.lh) pre_elems += (int64_t)B * 3 * L.lh * L.lw;
         float* pre = pre_elems ? m.ar.get<float>(S_PRE, pre_elems) : nullptr;
+        ResampleLevels rl{};
         for (auto& L : lv) {
             L.pre = nullptr;
             if ((int64_t)H > 2 * (int64_t)L.lh) {
+                VTF_CHECK(rl.n < ResampleLevels::MAXL, VTF_E_LIMIT, "mtcnn: too many precomputed levels");
                 L.pre = pre;
-                launch_resample_sat(sat, B, H, W, L.lh, L.lw, pre, st);
+                rl.lh[rl.n] = L.lh;
+                rl.lw[rl.n] = L.lw;
+                rl.out[rl.n] = pre;
+                rl.beg[rl.n + 1] = rl.beg[rl.n] + (int64_t)B * L.lh * L.lw;
+                rl.n++;
                 pre += (int64_t)B * 3 * L.lh * L.lw;
             }
         }
+        launch_resample_sat_multi(sat, B, H, W, rl, st);
     }
     PNetLevel* d_lv = m.ar.get<PNetLevel>(S_LEVELS, NL);
     VTF_HIP(hipMemcpyAsync(d_lv, lv.data(), NL * sizeof(PNetLevel), hipMemcpyHostToDevice, st));
