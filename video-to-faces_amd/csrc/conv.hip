@@ -559,8 +559,11 @@ static int conv_group_m() {
 // split factor: grids far below the CU count (FaceNet Block17/Block8, YOLO/R-CNN deep stages at
 // small batch) are split along K into up to 8 slices so ~2 workgroups land on every CU. bf16
 // (perf) mode only: the fp32 parity mode keeps the single-pass summation order.
-static int pick_split(int64_t tiles, int KT, bool bf16) {
-    if (!bf16 || tiles >= 192 || KT < 8) return 1;
+static int pick_split(int64_t tiles, int KT, bool bf16, bool fp32_split) {
+    // bf16: grids below 192 tiles; fp32 callers that accept a slice-order reduction
+    // (split_fp32: ONet's dense layer, 120 tiles of K = 1152: 72 -> 51 us with the epilogue
+    // kernel; RNet's 196 tiles of K = 576 measured slower split) below 160
+    if (!(bf16 || fp32_split) || tiles >= (bf16 ? 192 : 160) || KT < 8) return 1;
     int s = (int)std::min<int64_t>(8, (512 + tiles - 1) / tiles);
     s = std::min(s, KT / 4);
     return s < 2 ? 1 : s;
@@ -571,7 +574,7 @@ static void launch_tile(const ConvParams& p0, hipStream_t st) {
     ConvParams p = p0;
     const int64_t gx = cdiv(p.M, BM), gy = cdiv(p.Cout, BN);
     const int KT = (p.K + BK - 1) / BK;
-    p.split = pick_split(gx * gy, KT, sizeof(T) == 2 || (p.split_fp32 && !p.f16x));
+    p.split = pick_split(gx * gy, KT, sizeof(T) == 2, sizeof(T) == 4 && p.split_fp32);
     p.ws = nullptr;
     if (p.split > 1) p.ws = splitk_workspace(st, (size_t)p.split * p.M * p.Cout * sizeof(float));
     p.group_m = conv_group_m();
@@ -582,7 +585,14 @@ static void launch_tile(const ConvParams& p0, hipStream_t st) {
     p.xdbg = p.f16x ? xdbg : 0;
     dim3 g((unsigned)gx, (unsigned)gy, (unsigned)p.split);
     if (p.split > 1) {
-        k_conv<T, BM, BN, BK, true><<<g, 256, 0, st>>>(p);
+        if constexpr (sizeof(T) == 4) {
+            if (p.f16x)
+                k_conv<T, BM, BN, BK, true, true><<<g, 256, 0, st>>>(p);
+            else
+                k_conv<T, BM, BN, BK, true><<<g, 256, 0, st>>>(p);
+        } else {
+            k_conv<T, BM, BN, BK, true><<<g, 256, 0, st>>>(p);
+        }
         const int64_t n = p.M * p.Cout;
         k_conv_splitk_epi<T><<<(unsigned)cdiv(n, 256), 256, 0, st>>>(p);
         return;

@@ -467,6 +467,9 @@ static void run_candidates(Mtcnn& m, bool onet, const float* x0, int64_t n, floa
         p.out_cstride = L.cout;
         p.f16x = xmode != 0;
         p.ovf = xmode == 2 ? m.d_ovf : nullptr;
+        // the dense layers run on 120-200 tiles of long K: split-K (slice-order reduction;
+        // parity is a tolerance here)
+        p.split_fp32 = 1;
         VTF_CHECK(C == L.cin, VTF_E_ARG, "candidate net channel mismatch");
         launch_conv(p, false, m.st);
         H = p.OH;
