@@ -58,100 +58,90 @@ __device__ inline PNetWC to_const(const PNetW& w) {
 
 // ----------------------------------------------------------------------------------- resample
 
-// row pass: block per frame row, thread-contiguous chunks (read once into registers), block
-// scan of the chunk totals
-constexpr int SAT_ROW_PX = 8;  // pixels per thread (rows up to 2048 px in one pass)
+// row pass: block per frame row
 __global__ __launch_bounds__(256) void k_sat_rows(const uint8_t* __restrict__ frames, int64_t frame_stride,
                                                   int64_t row_stride, int H, int W, int4* __restrict__ sat) {
+    // row prefix sums in passes of 256 consecutive pixels (one per thread: coalesced byte loads
+    // and 4 KB contiguous int4 stores), a block scan per pass with the carry in registers
     const int y = blockIdx.x % H, b = blockIdx.x / H;
     const int W1 = W + 1;
     const uint8_t* row = frames + (int64_t)b * frame_stride + (int64_t)y * row_stride;
     int4* out = sat + ((int64_t)b * (H + 1) + y + 1) * W1;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int per = (W + 255) / 256, xs = tid * per;
-    __shared__ int3 wt[4];
+    __shared__ int3 wt[2][4];
     int3 carry = make_int3(0, 0, 0);
-    // chunks of SAT_ROW_PX pixels per thread per pass (one pass for rows up to 2048 px)
-    for (int base = 0; base < per; base += SAT_ROW_PX) {
-        int v[SAT_ROW_PX][3];
-        int r = 0, g = 0, bl = 0;
-#pragma unroll
-        for (int i = 0; i < SAT_ROW_PX; i++) {
-            const int x = xs + base + i;
-            const bool in = base + i < per && x < W;
-            v[i][0] = in ? 2 * row[3 * x + 2] - 255 : 0;
-            v[i][1] = in ? 2 * row[3 * x + 1] - 255 : 0;
-            v[i][2] = in ? 2 * row[3 * x] - 255 : 0;
-            r += v[i][0];
-            g += v[i][1];
-            bl += v[i][2];
-        }
-        // inclusive wave scan, then wave offsets
-        int ir = r, ig = g, ib = bl;
-        for (int off = 1; off < 64; off <<= 1) {
-            const int tr = __shfl_up(ir, off), tg = __shfl_up(ig, off), tb = __shfl_up(ib, off);
-            if (lane >= off) {
-                ir += tr;
-                ig += tg;
-                ib += tb;
-            }
-        }
-        __syncthreads();
-        if (lane == 63) wt[wave] = make_int3(ir, ig, ib);
-        __syncthreads();
-        int3 wb = carry, tot = carry;
-        for (int w = 0; w < 4; w++) {
-            if (w < wave) {
-                wb.x += wt[w].x;
-                wb.y += wt[w].y;
-                wb.z += wt[w].z;
-            }
-            tot.x += wt[w].x;
-            tot.y += wt[w].y;
-            tot.z += wt[w].z;
-        }
-        r = wb.x + ir - r;  // exclusive prefix of this thread's chunk
-        g = wb.y + ig - g;
-        bl = wb.z + ib - bl;
-#pragma unroll
-        for (int i = 0; i < SAT_ROW_PX; i++) {
-            const int x = xs + base + i;
-            r += v[i][0];
-            g += v[i][1];
-            bl += v[i][2];
-            if (base + i < per && x < W) out[x + 1] = make_int4(r, g, bl, 0);
-        }
-        carry = tot;
+    // bytes of the next pass loaded before the current one is scanned
+    int nr = 0, ng = 0, nb = 0;
+    if (tid < W) {
+        nr = 2 * row[3 * tid + 2] - 255;
+        ng = 2 * row[3 * tid + 1] - 255;
+        nb = 2 * row[3 * tid] - 255;
     }
-    if (tid == 0) {
-        out[0] = make_int4(0, 0, 0, 0);
-        if (y == 0) {
-            int4* r0 = sat + (int64_t)b * (H + 1) * W1;
-            for (int x = 0; x < W1; x++) r0[x] = make_int4(0, 0, 0, 0);
+    for (int x0 = 0, it = 0; x0 < W; x0 += 256, it++) {
+        int r = nr, g = ng, bl = nb;
+        const int xn = x0 + 256 + tid;
+        nr = ng = nb = 0;
+        if (xn < W) {
+            nr = 2 * row[3 * xn + 2] - 255;
+            ng = 2 * row[3 * xn + 1] - 255;
+            nb = 2 * row[3 * xn] - 255;
         }
+        for (int off = 1; off < 64; off <<= 1) {  // inclusive wave scan
+            const int tr = __shfl_up(r, off), tg = __shfl_up(g, off), tb = __shfl_up(bl, off);
+            if (lane >= off) {
+                r += tr;
+                g += tg;
+                bl += tb;
+            }
+        }
+        if (lane == 63) wt[it & 1][wave] = make_int3(r, g, bl);  // double-buffered: one barrier per pass
+        __syncthreads();
+        int3 wb = carry;
+        for (int w = 0; w < 4; w++) {
+            const int3 t = wt[it & 1][w];
+            if (w < wave) {
+                wb.x += t.x;
+                wb.y += t.y;
+                wb.z += t.z;
+            }
+            carry.x += t.x;
+            carry.y += t.y;
+            carry.z += t.z;
+        }
+        const int x = x0 + tid;
+        if (x < W) out[x + 1] = make_int4(wb.x + r, wb.y + g, wb.z + bl, 0);
+    }
+    if (tid == 0) out[0] = make_int4(0, 0, 0, 0);
+    if (y == 0) {
+        int4* r0 = sat + (int64_t)b * (H + 1) * W1;
+        for (int x = tid; x < W1; x += 256) r0[x] = make_int4(0, 0, 0, 0);
     }
 }
 
-// column pass, in place: block = 16 columns x 16 row groups (group totals combined in LDS)
-constexpr int SAT_COLS = 16, SAT_GROUPS = 16;
-__global__ __launch_bounds__(256) void k_sat_cols(int H, int W, int4* __restrict__ sat) {
+// column pass, in place: block = 16 columns x G row groups of up to SAT_PER rows; each thread
+// keeps its rows in registers (the SAT is read once and written once), group totals combined
+// in LDS
+constexpr int SAT_COLS = 16, SAT_PER = 24, SAT_MAXG = 64;
+__global__ __launch_bounds__(SAT_COLS * SAT_MAXG) void k_sat_cols(int H, int W, int4* __restrict__ sat) {
     const int W1 = W + 1;
+    const int G = blockDim.x / SAT_COLS;
     const int ncb = (W1 + SAT_COLS - 1) / SAT_COLS;
     const int b = blockIdx.x / ncb, cb = blockIdx.x % ncb;
     const int c = threadIdx.x % SAT_COLS, g = threadIdx.x / SAT_COLS;
     const int x = cb * SAT_COLS + c;
-    const int per = (H + SAT_GROUPS - 1) / SAT_GROUPS;
+    const int per = (H + G - 1) / G;
     const int ys = 1 + g * per, ye = min(H + 1, ys + per);
-    int4* col = sat + (int64_t)b * (H + 1) * W1 + x;
-    __shared__ int4 tot[SAT_GROUPS][SAT_COLS];
+    int4* col = sat + (int64_t)b * (H + 1) * W1 + min(x, W1 - 1);
+    __shared__ int4 tot[SAT_MAXG][SAT_COLS];
+    int4 v[SAT_PER];
     int4 acc = make_int4(0, 0, 0, 0);
-    if (x < W1)
-        for (int y = ys; y < ye; y++) {
-            const int4 v = col[(int64_t)y * W1];
-            acc.x += v.x;
-            acc.y += v.y;
-            acc.z += v.z;
-        }
+#pragma unroll
+    for (int i = 0; i < SAT_PER; i++) {
+        v[i] = (x < W1 && ys + i < ye) ? col[(int64_t)(ys + i) * W1] : make_int4(0, 0, 0, 0);
+        acc.x += v[i].x;
+        acc.y += v[i].y;
+        acc.z += v[i].z;
+    }
     tot[g][c] = acc;
     __syncthreads();
     int4 off = make_int4(0, 0, 0, 0);
@@ -160,20 +150,21 @@ __global__ __launch_bounds__(256) void k_sat_cols(int H, int W, int4* __restrict
         off.y += tot[k][c].y;
         off.z += tot[k][c].z;
     }
-    if (x < W1)
-        for (int y = ys; y < ye; y++) {
-            const int4 v = col[(int64_t)y * W1];
-            off.x += v.x;
-            off.y += v.y;
-            off.z += v.z;
-            col[(int64_t)y * W1] = off;
-        }
+#pragma unroll
+    for (int i = 0; i < SAT_PER; i++) {
+        off.x += v[i].x;
+        off.y += v[i].y;
+        off.z += v[i].z;
+        if (x < W1 && ys + i < ye) col[(int64_t)(ys + i) * W1] = off;
+    }
 }
 
 void launch_sat(const uint8_t* frames, int64_t frame_stride, int64_t row_stride, int B, int H, int W, int4* sat,
                 hipStream_t st) {
     k_sat_rows<<<(unsigned)((int64_t)B * H), 256, 0, st>>>(frames, frame_stride, row_stride, H, W, sat);
-    k_sat_cols<<<(unsigned)(B * ((W + SAT_COLS) / SAT_COLS)), 256, 0, st>>>(H, W, sat);
+    const int G = (H + SAT_PER - 1) / SAT_PER;
+    VTF_CHECK(G <= SAT_MAXG, VTF_E_LIMIT, "mtcnn: frames taller than 1536 rows");
+    k_sat_cols<<<(unsigned)(B * ((W + SAT_COLS) / SAT_COLS)), SAT_COLS * G, 0, st>>>(H, W, sat);
 }
 
 // MTCNN._resample of the preprocessed frames (mtcnn.py:133-139, 150-151) from the SAT:
