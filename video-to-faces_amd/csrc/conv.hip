@@ -26,6 +26,11 @@
 #include "common.hpp"
 #include "conv.hpp"
 
+// timing-only staging switches (scripts/ab_xdbg.sh): build with -DVTF_CONV_XDBG=1
+#ifndef VTF_CONV_XDBG
+#define VTF_CONV_XDBG 0
+#endif
+
 namespace vtf {
 
 typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
@@ -236,6 +241,7 @@ __global__ __launch_bounds__(256) void k_conv(ConvParams p) {
 
     vec ra[RA], rb[RB];
     auto load_tile = [&](int kcur, int ci_, int kw0, int kh0) {
+#if VTF_CONV_XDBG
         if (X && (p.xdbg & 2)) {
 #pragma unroll
             for (int r = 0; r < RA; r++) ra[r] = vec{};
@@ -243,6 +249,7 @@ __global__ __launch_bounds__(256) void k_conv(ConvParams p) {
             for (int r = 0; r < RB; r++) rb[r] = vec{};
             return;
         }
+#endif
 #pragma unroll
         for (int r = 0; r < RA; r++) {
             vec v = {};
@@ -266,10 +273,13 @@ __global__ __launch_bounds__(256) void k_conv(ConvParams p) {
             auto put = [&](char* base, int rows, int row, const vec& v) {
                 h4 x0, x1;
                 float mx = 0.f;
+#if VTF_CONV_XDBG
                 if (p.xdbg & 1) {
 #pragma unroll
                     for (int e = 0; e < 4; e++) x0[e] = x1[e] = (_Float16)to_f(v[e]);
-                } else {
+                } else
+#endif
+                {
 #pragma unroll
                     for (int e = 0; e < 4; e++) {
                         x0[e] = (_Float16)to_f(v[e]);
@@ -578,11 +588,13 @@ static void launch_tile(const ConvParams& p0, hipStream_t st) {
     p.ws = nullptr;
     if (p.split > 1) p.ws = splitk_workspace(st, (size_t)p.split * p.M * p.Cout * sizeof(float));
     p.group_m = conv_group_m();
+#if VTF_CONV_XDBG
     static const int xdbg = [] {
         const char* e = std::getenv("VTF_CONV_XDBG");
         return e ? std::atoi(e) : 0;
     }();
     p.xdbg = p.f16x ? xdbg : 0;
+#endif
     dim3 g((unsigned)gx, (unsigned)gy, (unsigned)p.split);
     if (p.split > 1) {
         if constexpr (sizeof(T) == 4) {

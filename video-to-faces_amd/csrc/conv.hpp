@@ -32,8 +32,9 @@ struct ConvParams {
                          // summation order differs from the single pass; used where parity is a tolerance)
     int split;           // split-K factor (set by launch_conv; > 1: raw partial sums to ws)
     int group_m;         // XCD-aware tile order: M-tile group height (0 = plain blockIdx mapping; set by launch_conv)
-    int xdbg;            // experiments only (env VTF_CONV_XDBG, f16x mode): 1 = staging without the split
-                         // arithmetic / range check, 2 = no operand loads (wrong results; timing only)
+    int xdbg;            // experiments only (built with -DVTF_CONV_XDBG=1, env VTF_CONV_XDBG, f16x mode):
+                         // 1 = staging without the split arithmetic / range check, 2 = no operand loads
+                         // (wrong results; timing only)
     float* ws;           // fp32 [split][M][Cout] partial sums (split-K only)
     int64_t M;           // N*OH*OW
     int N, H, W, Cin, OH, OW, Cout, KH, KW, sh, sw, ph, pw, K;
