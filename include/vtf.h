@@ -175,6 +175,13 @@ int vtf_vit_forward(vtf_vit_t h, const float* d_x, int64_t N, float* d_emb);
 int vtf_vit_encode_crops(vtf_vit_t h, const uint8_t* d_frames, int F, int H, int W, int64_t frame_stride,
                          int64_t row_stride, const int32_t* crops, int crops_on_device, int64_t N, float* d_emb);
 
+/* fp32-grade GEMM on the fp16 matrix cores (the split-fp16 ViT Linear layers, vit.py:29-37):
+ * out[M,N] = a[M,K] b[N,K]^T (+ bias[N]); device fp32 row-major operands, split on device into
+ * x0 + x1 * 2^-11 fp16 pairs (|x| < 2^14 required: VTF_E_ARG otherwise).  K % 32 == 0, N % 8 == 0.
+ * Stream-ordered; returns after the stream is synchronised. */
+int vtf_gemm_split(const float* d_a, const float* d_b, int64_t M, int N, int K, const float* d_bias, float* d_out,
+                   void* hip_stream);
+
 /* ---------------------------------------------------------------- grouping
  * remove_dupes_overall 'enc' branch (dupes.py:51-68 with sklearn cosine_distances):
  * for each row i, min and argmin over j < i of clip(1 - cos(X_i, X_j), 0, 2); row 0 gets

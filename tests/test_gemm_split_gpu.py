@@ -1,0 +1,62 @@
+"""GPU: the pre-split fp32-grade GEMM (gemm_x3.hip, the split-fp16 ViT Linear layers of
+encoders/vit.py:29-37) against float64 products, and the ViT forward on it against k_conv's
+staging-split mode (same chains and order: bit-identical)."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _gemm(a, b, bias=None):
+    from videotofaces import _native as nat
+    M, K = a.shape
+    N = b.shape[0]
+    da, db = torch.from_numpy(a).cuda(), torch.from_numpy(b).cuda()
+    dbias = torch.from_numpy(bias).cuda() if bias is not None else None
+    out = torch.empty((M, N), dtype=torch.float32, device='cuda')
+    st = torch.cuda.current_stream().cuda_stream
+    rc = nat.lib().vtf_gemm_split(da.data_ptr(), db.data_ptr(), M, N, K,
+                                  dbias.data_ptr() if dbias is not None else None, out.data_ptr(), st)
+    return rc, out.cpu().numpy()
+
+
+@pytest.mark.parametrize('M,N,K', [(1, 8, 32), (65, 24, 64), (300, 136, 96), (8320, 1024, 1024), (1000, 256, 4096)])
+def test_gemm_split_vs_float64(M, N, K):
+    """Tails in M (rows past M are loaded clamped, never stored) and in N (N % 128 != 0); the
+    error bound of the split products is ~2^-22 of sum |a||b| plus fp32 accumulation."""
+    rng = np.random.default_rng(M + N + K)
+    a = rng.standard_normal((M, K)).astype(np.float32)
+    b = (rng.standard_normal((N, K)) * 0.05).astype(np.float32)
+    bias = rng.standard_normal(N).astype(np.float32)
+    rc, got = _gemm(a, b, bias)
+    assert rc == 0
+    ref = a.astype(np.float64) @ b.astype(np.float64).T + bias
+    scale = np.abs(a).astype(np.float64) @ np.abs(b).astype(np.float64).T + np.abs(bias)
+    err = np.abs(got - ref) / scale
+    print('max rel-to-|a||b| err', err.max())
+    assert err.max() < 2e-6
+
+
+def test_gemm_split_refuses_out_of_range():
+    a = np.ones((16, 32), np.float32)
+    a[3, 5] = 20000.0
+    b = np.ones((8, 32), np.float32)
+    rc, _ = _gemm(a, b)
+    assert rc != 0
+
+
+def test_vit_l_sp_gemm_matches_conv_split_bitwise():
+    """ViT-L split mode on pre-split operands vs k_conv's staging-split mode at batch 8 (M = 520
+    token rows: 5 M-tiles, the last partial): identical bits."""
+    from videotofaces.encoders.vit import ViT
+    x = (torch.rand((8, 3, 128, 128), generator=torch.Generator().manual_seed(3)) * 2 - 1).float()
+    new = ViT('cuda:0', isL=True, precision='f16x')(x).cpu().numpy()
+    os.environ['VTF_VIT_GEMM'] = 'conv'
+    try:
+        old = ViT('cuda:0', isL=True, precision='f16x')(x).cpu().numpy()
+    finally:
+        del os.environ['VTF_VIT_GEMM']
+    np.testing.assert_array_equal(new, old)

@@ -1,0 +1,291 @@
+// fp32-grade GEMM on the fp16 matrix cores with pre-split operands (gfx950).
+//
+// Replaces the nn.Linear layers of the ViT blocks (src/videotofaces/encoders/vit.py:29-37:
+// q|k|v, proj, fc1, fc2) in the split-fp16 mode.  k_conv's split mode (conv.hip) split every
+// fp32 operand element at LDS staging: per 32-deep step each thread loaded fp32 vectors into
+// registers, converted them to two fp16 planes with VALU and stored them with ds_write_b64 --
+// the staging (load latency, split VALU, LDS writes) bounded it at ~0.18 of the split peak.
+// Here the operands arrive split ("SP" layout, gemm_x3.hpp): the producers (LayerNorm, attention,
+// the fc1 epilogue) write x0/x1 once, the weights are split once on the host, and the tiles
+// go HBM -> LDS by LDS-DMA (global_load_lds_dwordx4): no staging VGPRs, no staging VALU.
+//
+// Tile 128 x 128 per 256-thread workgroup (2 x 2 waves of 64 x 64 = 4 x 4 fragments), 32-deep
+// k-steps, two LDS stages (64 KB; two workgroups per CU): the DMA of step k+1 is in flight while
+// step k runs on the MFMA; one barrier per step.  Per step and fragment pair three
+// v_mfma_f32_16x16x32_f16: x0 w0 into acc, x0 w1 + x1 w0 into accx (the same chains and order
+// as k_conv's split mode, so the results are bit-identical to it), combined once at the end.
+//
+// LDS image of a stage: rows of 128 B (the 32-deep k-step of one row: 4 chunks x 2 planes of
+// 16 B), 16-B slot s of row r holds (plane, chunk) = s ^ ((r >> 1) & 7) split as (s' >> 2, s' & 3).
+// One DMA wave-instruction writes 1 KB = 8 whole rows lane-linearly, so the swizzle is applied
+// on the global source address; the fragment reads (ds_read_b128, rows lane & 15, chunk
+// lane >> 4) then hit 16 distinct slots per 16-lane bank group: conflict-free.
+#include <algorithm>
+#include <cstdlib>
+#include <cmath>
+#include <cstring>
+
+#include "common.hpp"
+#include "gemm_x3.hpp"
+
+namespace vtf {
+
+namespace {
+
+typedef __attribute__((ext_vector_type(8))) _Float16 h8;
+typedef __attribute__((ext_vector_type(4))) float f4;
+
+template <int BM, int BN>
+__global__ __launch_bounds__(256, 2) void k_gemm_x3(GemmX3Params p) {
+    constexpr int RB = 128;  // LDS bytes per row and k-step
+    constexpr int A_ST = BM * RB, ST = (BM + BN) * RB;
+    constexpr int LDE = BN + 4;
+    constexpr int SM = 2 * ST > BM * LDE * 4 ? 2 * ST : BM * LDE * 4;
+    constexpr int WM = BM / 2, WN = BN / 2, FM = WM / 16, FN = WN / 16;
+    constexpr int PA = BM / 32, PB = BN / 32;  // 1-KB DMA pieces per wave and stage
+    static_assert(BM % 32 == 0 && BN % 32 == 0, "tile");
+    __shared__ __attribute__((aligned(16))) char smem[SM];
+
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wm = wave >> 1, wn = wave & 1;
+    // XCD-aware tile order (as k_conv): every XCD walks one contiguous run of tiles in groups of
+    // group_m M-tiles x all N-tiles
+    int tile_m = blockIdx.x, tile_n = blockIdx.y;
+    if (p.group_m > 0) {
+        const int gx = gridDim.x, gy = gridDim.y;
+        const int lin = blockIdx.x + gx * blockIdx.y, total = gx * gy;
+        const int xcd = lin & 7, loc = lin >> 3, per = total >> 3, rem = total & 7;
+        const int L = xcd < rem ? xcd * (per + 1) + loc : rem * (per + 1) + (xcd - rem) * per + loc;
+        const int span = p.group_m * gy;
+        const int first = (L / span) * p.group_m;
+        const int gsz = min(gx - first, p.group_m);
+        tile_m = first + (L % span) % gsz;
+        tile_n = (L % span) / gsz;
+    }
+    const int64_t m0 = (int64_t)tile_m * BM;
+    const int n0 = tile_n * BN;
+
+    // DMA sources: piece j of this wave = rows 32 j + 8 wave .. +7; the lane's LDS slot lane & 7
+    // of row 32 j + 8 wave + (lane >> 3) takes source slot (lane & 7) ^ h, h = (row >> 1) & 7
+    const int src = (lane & 7) ^ (((lane >> 4) + 4 * (wave & 1)) & 7);
+    const int soff = (src & 3) * 32 + (src >> 2) * 16;
+    const int64_t rowb = (int64_t)p.K * 4;
+    const char* ga[PA];
+    const char* gb[PB];
+#pragma unroll
+    for (int j = 0; j < PA; j++) {
+        const int64_t m = min(m0 + 32 * j + 8 * wave + (lane >> 3), p.M - 1);
+        ga[j] = (const char*)p.a + m * rowb + soff;
+    }
+#pragma unroll
+    for (int j = 0; j < PB; j++) {
+        const int64_t n = min(n0 + 32 * j + 8 * wave + (lane >> 3), p.N - 1);
+        gb[j] = (const char*)p.b + n * rowb + soff;
+    }
+    auto issue = [&](int kt, int s) {
+        const int64_t kb = (int64_t)kt * RB;
+        char* base = smem + s * ST;
+#pragma unroll
+        for (int j = 0; j < PA; j++)
+            __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)(ga[j] + kb),
+                                             (void __attribute__((address_space(3)))*)(base + (wave + 4 * j) * 1024), 16,
+                                             0, 0);
+#pragma unroll
+        for (int j = 0; j < PB; j++)
+            __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)(gb[j] + kb),
+                                             (void __attribute__((address_space(3)))*)(base + A_ST + (wave + 4 * j) * 1024),
+                                             16, 0, 0);
+    };
+
+    f4 acc[FM][FN], accx[FM][FN];
+#pragma unroll
+    for (int i = 0; i < FM; i++)
+#pragma unroll
+        for (int j = 0; j < FN; j++) {
+            acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
+            accx[i][j] = f4{0.f, 0.f, 0.f, 0.f};
+        }
+    // fragment read offsets: row (lane & 15) of a 16-row block, chunk lane >> 4, plane pl
+    const int hsw = (lane & 15) >> 1;
+    const int o0 = (lane & 15) * RB + (((lane >> 4) ^ hsw) << 4);      // plane 0
+    const int o1 = (lane & 15) * RB + (((4 + (lane >> 4)) ^ hsw) << 4);  // plane 1
+
+    const int KT = p.K / 32;
+    issue(0, 0);
+    for (int kt = 0; kt < KT; kt++) {
+        // this wave's pieces of step kt have landed; after the barrier every wave's have, and
+        // every wave is done reading the other stage (its MFMAs consumed those reads)
+        asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+        if (kt + 1 < KT) issue(kt + 1, (kt + 1) & 1);
+        const char* As = smem + (kt & 1) * ST + wm * WM * RB;
+        const char* Bs = smem + (kt & 1) * ST + A_ST + wn * WN * RB;
+        h8 b0[FN], b1[FN];
+#pragma unroll
+        for (int j = 0; j < FN; j++) {
+            b0[j] = *(const h8*)(Bs + j * 16 * RB + o0);
+            b1[j] = *(const h8*)(Bs + j * 16 * RB + o1);
+        }
+#pragma unroll
+        for (int i = 0; i < FM; i++) {
+            const h8 a0 = *(const h8*)(As + i * 16 * RB + o0);
+            const h8 a1 = *(const h8*)(As + i * 16 * RB + o1);
+#pragma unroll
+            for (int j = 0; j < FN; j++) {
+                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a0, b0[j], acc[i][j], 0, 0, 0);
+                accx[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a0, b1[j], accx[i][j], 0, 0, 0);
+                accx[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a1, b0[j], accx[i][j], 0, 0, 0);
+            }
+        }
+    }
+    __syncthreads();  // no DMA outstanding; every wave is done with the stages
+    float* E = (float*)smem;
+#pragma unroll
+    for (int j = 0; j < FN; j++)
+#pragma unroll
+        for (int i = 0; i < FM; i++) {
+            const f4 v = acc[i][j] + accx[i][j] * 0.00048828125f;
+#pragma unroll
+            for (int q = 0; q < 4; q++)
+                E[(wm * WM + i * 16 + 4 * (lane >> 4) + q) * LDE + wn * WN + j * 16 + (lane & 15)] = v[q];
+        }
+    __syncthreads();
+    constexpr int G = BN / 8;
+    static_assert(256 % G == 0, "epilogue groups");
+    const int g = tid % G, c0 = n0 + 8 * g;
+    if (c0 >= p.N) return;
+    float b8[8];
+#pragma unroll
+    for (int e = 0; e < 8; e++) b8[e] = p.bias ? p.bias[c0 + e] : 0.f;
+    bool bad = false;
+    for (int r = tid / G; r < BM; r += 256 / G) {
+        const int64_t m = m0 + r;
+        if (m >= p.M) break;
+        const f4 lo = *(const f4*)(E + r * LDE + 8 * g), hi = *(const f4*)(E + r * LDE + 8 * g + 4);
+        float v[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        float rv[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+        if (p.res) {
+            const f4 r0 = *(const f4*)(p.res + m * p.ldr + c0), r1 = *(const f4*)(p.res + m * p.ldr + c0 + 4);
+            rv[0] = r0[0], rv[1] = r0[1], rv[2] = r0[2], rv[3] = r0[3];
+            rv[4] = r1[0], rv[5] = r1[1], rv[6] = r1[2], rv[7] = r1[3];
+        }
+#pragma unroll
+        for (int e = 0; e < 8; e++) {
+            float x = v[e];
+            if (p.bias) x = x + b8[e];
+            if (p.res) x = x + rv[e];
+            if (p.gelu) x = 0.5f * x * (1.0f + erff(x * 0.70710678118654752f));
+            v[e] = x;
+        }
+        if (p.out_sp) {
+            char* row = (char*)p.out + m * (int64_t)p.N * 4;
+            sp_store4(row, c0, v[0], v[1], v[2], v[3], bad);
+            sp_store4(row, c0 + 4, v[4], v[5], v[6], v[7], bad);
+        } else {
+            float* o = (float*)p.out + m * p.ldo + c0;
+            *(f4*)o = f4{v[0], v[1], v[2], v[3]};
+            *(f4*)(o + 4) = f4{v[4], v[5], v[6], v[7]};
+        }
+    }
+    if (p.ovf && __ballot(bad) && lane == 0) atomicOr(p.ovf, 1);
+}
+
+// one thread per 8-element chunk
+__global__ void k_split_rows(const float* __restrict__ x, int64_t rows, int K, int64_t ld, char* __restrict__ out,
+                             int* __restrict__ ovf) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int KC = K / 8;
+    bool bad = false;
+    if (i < rows * KC) {
+        const int64_t r = i / KC;
+        const int c = (int)(i % KC);
+        const f4 lo = *(const f4*)(x + r * ld + 8 * c), hi = *(const f4*)(x + r * ld + 8 * c + 4);
+        char* row = out + r * (int64_t)K * 4;
+        sp_store4(row, 8 * c, lo[0], lo[1], lo[2], lo[3], bad);
+        sp_store4(row, 8 * c + 4, hi[0], hi[1], hi[2], hi[3], bad);
+    }
+    if (ovf && __ballot(bad) && (threadIdx.x & 63) == 0) atomicOr(ovf, 1);
+}
+
+int gemm_group_m() {
+    static int g = [] {
+        const char* e = std::getenv("VTF_CONV_GROUP_M");
+        return e ? std::atoi(e) : 8;
+    }();
+    return g;
+}
+
+}  // namespace
+
+void launch_gemm_x3(const GemmX3Params& p0, hipStream_t st) {
+    if (p0.M <= 0) return;
+    VTF_CHECK(p0.K > 0 && p0.K % 32 == 0 && p0.N > 0 && p0.N % 8 == 0, VTF_E_ARG, "gemm_x3: K % 32, N % 8");
+    VTF_CHECK(p0.out_sp || p0.ldo >= p0.N, VTF_E_ARG, "gemm_x3: output stride");
+    VTF_CHECK(!p0.res || (p0.ldr >= p0.N && p0.ldr % 4 == 0), VTF_E_ARG, "gemm_x3: residual stride");
+    GemmX3Params p = p0;
+    p.group_m = gemm_group_m();
+    constexpr int BM = 128, BN = 128;
+    dim3 g((unsigned)cdiv(p.M, BM), (unsigned)cdiv(p.N, BN));
+    k_gemm_x3<BM, BN><<<g, 256, 0, st>>>(p);
+}
+
+void launch_split_rows(const float* x, int64_t rows, int K, int64_t ld, void* out, int* ovf, hipStream_t st) {
+    const int64_t n = rows * (K / 8);
+    if (n <= 0) return;
+    k_split_rows<<<(unsigned)cdiv(n, 256), 256, 0, st>>>(x, rows, K, ld, (char*)out, ovf);
+}
+
+bool split_rows_host(const float* x, int64_t rows, int K, uint16_t* out) {
+    bool ok = true;
+    for (int64_t r = 0; r < rows; r++)
+        for (int k = 0; k < K; k++) {
+            const float v = x[r * K + k];
+            ok &= std::fabs(v) < 16384.f;
+            const _Float16 h0 = (_Float16)v;
+            const _Float16 h1 = (_Float16)((v - (float)h0) * 2048.f);
+            uint16_t* c = out + r * (int64_t)K * 2 + (k >> 3) * 16;
+            std::memcpy(c + (k & 7), &h0, 2);
+            std::memcpy(c + 8 + (k & 7), &h1, 2);
+        }
+    return ok;
+}
+
+}  // namespace vtf
+
+using namespace vtf;
+
+extern "C" int vtf_gemm_split(const float* d_a, const float* d_b, int64_t M, int N, int K, const float* d_bias,
+                              float* d_out, void* hip_stream) {
+    return guarded_on(stream_device((hipStream_t)hip_stream), [&] {
+        VTF_CHECK(M >= 0 && N > 0 && K > 0 && K % 32 == 0 && N % 8 == 0, VTF_E_ARG,
+                  "gemm_split: K % 32 == 0, N % 8 == 0");
+        if (M == 0) return;
+        VTF_CHECK(d_a && d_b && d_out, VTF_E_ARG, "null argument");
+        hipStream_t st = (hipStream_t)hip_stream;
+        char *sa = nullptr, *sb = nullptr;
+        int* ovf = nullptr;
+        VTF_HIP(hipMallocAsync((void**)&sa, (size_t)M * K * 4, st));
+        VTF_HIP(hipMallocAsync((void**)&sb, (size_t)N * K * 4, st));
+        VTF_HIP(hipMallocAsync((void**)&ovf, 4, st));
+        VTF_HIP(hipMemsetAsync(ovf, 0, 4, st));
+        launch_split_rows(d_a, M, K, K, sa, ovf, st);
+        launch_split_rows(d_b, N, K, K, sb, ovf, st);
+        GemmX3Params p{};
+        p.a = sa;
+        p.b = sb;
+        p.out = d_out;
+        p.bias = d_bias;
+        p.M = M;
+        p.N = N;
+        p.K = K;
+        p.ldo = N;
+        launch_gemm_x3(p, st);
+        int h_ovf = 0;
+        VTF_HIP(hipMemcpyAsync(&h_ovf, ovf, 4, hipMemcpyDeviceToHost, st));
+        VTF_HIP(hipFreeAsync(sa, st));
+        VTF_HIP(hipFreeAsync(sb, st));
+        VTF_HIP(hipFreeAsync(ovf, st));
+        VTF_HIP(hipStreamSynchronize(st));
+        VTF_CHECK(!h_ovf, VTF_E_ARG, "gemm_split: an operand is outside the fp16 range (|x| >= 2^14 or NaN)");
+        VTF_HIP(hipGetLastError());
+    });
+}

@@ -9,12 +9,15 @@
 // residual / GELU fused in the epilogue.  Attention: one workgroup per (image, head) keeps
 // Q, K, V (65 x 64 each) and the 65 x 65 scores in LDS; row softmax by wave reductions.
 #include <cmath>
+#include <cstdlib>
+#include <string>
 #include <vector>
 
 #include "blob.hpp"
 #include "boxes.hpp"
 #include "common.hpp"
 #include "conv.hpp"
+#include "gemm_x3.hpp"
 
 namespace vtf {
 
@@ -38,9 +41,12 @@ __global__ void k_vit_tokens(const float* __restrict__ patches, const float* __r
 // loads), mean and variance are wave reductions over it, then the normalised row is written
 constexpr int LN_ROWS = 4;
 constexpr int LN_MAXV = 4;  // float4 per lane: D <= 1024
+// SP: the normalised rows go out in the split-pair layout of the split-fp16 GEMM (gemm_x3.hpp,
+// row stride D * 4 bytes) and an element beyond the fp16 range raises *ovf
+template <bool SP = false>
 __global__ __launch_bounds__(256) void k_layernorm(const float* __restrict__ x, int64_t rows, int D, int64_t ld,
                                                    const float* __restrict__ g, const float* __restrict__ b, float eps,
-                                                   float* __restrict__ y, int64_t ldy) {
+                                                   float* __restrict__ y, int64_t ldy, int* __restrict__ ovf = nullptr) {
     const int lane = threadIdx.x & 63;
     const int64_t r = (int64_t)blockIdx.x * LN_ROWS + (threadIdx.x >> 6);
     if (r >= rows) return;
@@ -74,19 +80,28 @@ __global__ __launch_bounds__(256) void k_layernorm(const float* __restrict__ x, 
     float4* yr = (float4*)(y + r * ldy);
     const float4* g4 = (const float4*)g;
     const float4* b4 = (const float4*)b;
+    bool bad = false;
 #pragma unroll
     for (int j = 0; j < LN_MAXV; j++)
         if (j < nv) {
             const int c = lane + 64 * j;
             const float4 gg = g4[c], bb = b4[c];
-            yr[c] = make_float4(fmaf(v[j].x * rstd, gg.x, bb.x), fmaf(v[j].y * rstd, gg.y, bb.y),
-                                fmaf(v[j].z * rstd, gg.z, bb.z), fmaf(v[j].w * rstd, gg.w, bb.w));
+            const float4 o = make_float4(fmaf(v[j].x * rstd, gg.x, bb.x), fmaf(v[j].y * rstd, gg.y, bb.y),
+                                         fmaf(v[j].z * rstd, gg.z, bb.z), fmaf(v[j].w * rstd, gg.w, bb.w));
+            if constexpr (SP)
+                sp_store4((char*)y + r * (int64_t)D * 4, 4 * c, o.x, o.y, o.z, o.w, bad);
+            else
+                yr[c] = o;
         }
+    if constexpr (SP)
+        if (__ballot(bad) && lane == 0) atomicOr(ovf, 1);
 }
 
-// qkv [N,65,3D] (q | k | v, head-major inside each) -> out [N,65,D]; one workgroup per (n, head)
+// qkv [N,65,3D] (q | k | v, head-major inside each) -> out [N,65,D]; one workgroup per (n, head).
+// SP: out in the split-pair layout of the split-fp16 GEMM (proj's operand), range flag *ovf
+template <bool SP = false>
 __global__ __launch_bounds__(256) void k_vit_attention(const float* __restrict__ qkv, int64_t N, int D, int heads,
-                                                       float* __restrict__ out) {
+                                                       float* __restrict__ out, int* __restrict__ ovf = nullptr) {
     __shared__ __attribute__((aligned(16))) float V[VT * VHD];  // 16-B rows: float4 reads in P V
     __shared__ float Q[VT * (VHD + 1)], K[VT * (VHD + 1)], S[VT * 68];
     const int64_t n = blockIdx.x / heads;
@@ -171,15 +186,24 @@ __global__ __launch_bounds__(256) void k_vit_attention(const float* __restrict__
                 acc[i][3] = fmaf(sc, v.w, acc[i][3]);
             }
         }
+        bool bad = false;
 #pragma unroll
-        for (int i = 0; i < 5; i++)
-            *(float4*)(ob + (int64_t)(a0 + i) * D + d0) = make_float4(acc[i][0], acc[i][1], acc[i][2], acc[i][3]);
+        for (int i = 0; i < 5; i++) {
+            if constexpr (SP)
+                sp_store4((char*)out + (n * VT + a0 + i) * (int64_t)D * 4, h * VHD + d0, acc[i][0], acc[i][1], acc[i][2],
+                          acc[i][3], bad);
+            else
+                *(float4*)(ob + (int64_t)(a0 + i) * D + d0) = make_float4(acc[i][0], acc[i][1], acc[i][2], acc[i][3]);
+        }
+        if constexpr (SP)
+            if (__ballot(bad) && (tid & 63) == 0) atomicOr(ovf, 1);
     }
 }
 
 struct Lin {
     const float *w, *b;  // [out][in], [out]
     int in, out;
+    const void* sp;      // the weights split once into the SP layout (split-fp16 GEMM), or null
 };
 
 struct Vit {
@@ -187,6 +211,9 @@ struct Vit {
     // GEMM operand mode: 0 fp32 MFMA; 2 split-fp16 (fp32-grade products on the fp16 matrix
     // cores, conv.hip f16x) guarded by the device overflow flag -> the forward re-runs in fp32
     int xmode = 0, cur_x = 0;
+    // split mode on pre-split operands (gemm_x3.hip) when every weight is inside the fp16 range;
+    // VTF_VIT_GEMM=conv keeps k_conv's staging-split mode (A/B timing, bit-identical results)
+    bool sp_ok = false;
     int* d_ovf = nullptr;
     hipStream_t st = 0;
     const float *cls = nullptr, *pos = nullptr, *pw = nullptr, *pb = nullptr;  // patch conv [D][16][16][8]
@@ -201,6 +228,15 @@ struct Vit {
     ~Vit() {
         for (void* p : allocs) (void)hipFree(p);
         if (d_ovf) (void)hipFree(d_ovf);
+    }
+    const void* up_sp(const std::vector<float>& v, int rows, int K) {
+        std::vector<uint16_t> h((size_t)rows * K * 2);
+        if (!split_rows_host(v.data(), rows, K, h.data())) return nullptr;
+        void* p = nullptr;
+        VTF_HIP(hipMalloc(&p, h.size() * 2));
+        VTF_HIP(hipMemcpy(p, h.data(), h.size() * 2, hipMemcpyHostToDevice));
+        allocs.push_back(p);
+        return p;
     }
     const float* up(const std::vector<float>& v) {
         void* p = nullptr;
@@ -244,14 +280,17 @@ static void vit_build(Vit& V, const float* params, int64_t n_params) {
         std::vector<float> b(qb);
         b.insert(b.end(), kb.begin(), kb.end());
         b.insert(b.end(), vb.begin(), vb.end());
-        B.qkv = Lin{V.up(w), V.up(b), D, 3 * D};
-        { auto pw = take((int64_t)D * D); auto pb = take(D); B.proj = Lin{V.up(pw), V.up(pb), D, D}; }
+        B.qkv = Lin{V.up(w), V.up(b), D, 3 * D, V.up_sp(w, 3 * D, D)};
+        { auto pw = take((int64_t)D * D); auto pb = take(D); B.proj = Lin{V.up(pw), V.up(pb), D, D, V.up_sp(pw, D, D)}; }
         B.n2w = V.up(take(D));
         B.n2b = V.up(take(D));
-        { auto w1 = take((int64_t)4 * D * D); auto b1 = take(4 * D); B.fc1 = Lin{V.up(w1), V.up(b1), D, 4 * D}; }
-        { auto w2 = take((int64_t)4 * D * D); auto b2 = take(D); B.fc2 = Lin{V.up(w2), V.up(b2), 4 * D, D}; }
+        { auto w1 = take((int64_t)4 * D * D); auto b1 = take(4 * D); B.fc1 = Lin{V.up(w1), V.up(b1), D, 4 * D, V.up_sp(w1, 4 * D, D)}; }
+        { auto w2 = take((int64_t)4 * D * D); auto b2 = take(D); B.fc2 = Lin{V.up(w2), V.up(b2), 4 * D, D, V.up_sp(w2, D, 4 * D)}; }
         V.blocks.push_back(B);
     }
+    const char* ge = std::getenv("VTF_VIT_GEMM");
+    V.sp_ok = !(ge && std::string(ge) == "conv");
+    for (const auto& B : V.blocks) V.sp_ok = V.sp_ok && B.qkv.sp && B.proj.sp && B.fc1.sp && B.fc2.sp;
     V.nw = V.up(take(D));
     V.nb = V.up(take(D));
     VTF_CHECK(src == n_params, VTF_E_ARG, "vit: parameter count mismatch");
@@ -280,6 +319,25 @@ static void linear(Vit& V, const Lin& L, const float* x, int64_t M, float* y, co
     p.f16x = V.cur_x != 0;
     p.ovf = V.cur_x ? V.d_ovf : nullptr;
     launch_conv(p, false, V.st);
+}
+
+// y[M,out] = x W^T + b (+ res) (+ GELU) on pre-split operands: x SP [M][in] -> y fp32 or SP
+static void linear_sp(Vit& V, const Lin& L, const void* x, int64_t M, void* y, bool y_sp, const float* res, bool gelu) {
+    GemmX3Params p{};
+    p.a = x;
+    p.b = L.sp;
+    p.out = y;
+    p.bias = L.b;
+    p.res = res;
+    p.ldr = L.out;
+    p.ovf = V.d_ovf;
+    p.M = M;
+    p.N = L.out;
+    p.K = L.in;
+    p.ldo = L.out;
+    p.gelu = gelu;
+    p.out_sp = y_sp;
+    launch_gemm_x3(p, V.st);
 }
 
 static void vit_forward(Vit& V, const float* x_nhwc8, int64_t N, float* emb) {
@@ -312,6 +370,24 @@ static void vit_forward(Vit& V, const float* x_nhwc8, int64_t N, float* emb) {
     p.ovf = V.cur_x ? V.d_ovf : nullptr;
     launch_conv(p, false, V.st);
     k_vit_tokens<<<cdiv(M * D, 256), 256, 0, V.st>>>(patches, V.cls, V.pos, N, D, X);
+    if (V.cur_x && V.sp_ok) {
+        // split mode on pre-split operands: LayerNorm, attention and fc1 write the GEMM operands
+        // split (SP), the residual stream X and q|k|v stay fp32; same bits as the k_conv split mode
+        const unsigned lg = (unsigned)cdiv(M, LN_ROWS);
+        for (const auto& B : V.blocks) {
+            k_layernorm<true><<<lg, 256, 0, V.st>>>(X, M, D, D, B.n1w, B.n1b, 1e-12f, Hn, D, V.d_ovf);
+            linear_sp(V, B.qkv, Hn, M, QKV, false, nullptr, false);
+            k_vit_attention<true><<<(unsigned)(N * V.heads), 256, 0, V.st>>>(QKV, N, D, V.heads, A, V.d_ovf);
+            linear_sp(V, B.proj, A, M, Hn, false, X, false);  // x + proj(attn)
+            std::swap(X, Hn);
+            k_layernorm<true><<<lg, 256, 0, V.st>>>(X, M, D, D, B.n2w, B.n2b, 1e-12f, A, D, V.d_ovf);
+            linear_sp(V, B.fc1, A, M, F, true, nullptr, true);
+            linear_sp(V, B.fc2, F, M, Hn, false, X, false);  // x + fc2(gelu(fc1(...)))
+            std::swap(X, Hn);
+        }
+        k_layernorm<<<(unsigned)cdiv(N, LN_ROWS), 256, 0, V.st>>>(X, N, D, (int64_t)VT * D, V.nw, V.nb, 1e-12f, emb, D);
+        return;
+    }
     for (const auto& B : V.blocks) {
         k_layernorm<<<(unsigned)cdiv(M, LN_ROWS), 256, 0, V.st>>>(X, M, D, D, B.n1w, B.n1b, 1e-12f, Hn, D);
         linear(V, B.qkv, Hn, M, QKV, nullptr, false);

@@ -50,6 +50,7 @@ SIGNATURES = {
     'vtf_vit_forward': [_p, _p, _i64, _p],
     'vtf_vit_encode_crops': [_p, _p, _i32, _i32, _i32, _i64, _i64, _p, _i32, _i64, _p],
     'vtf_blob_from_crops': [_p, _i32, _i32, _i32, _i64, _i64, _p, _i64, _i32, _f32, _f32, _p, _p],
+    'vtf_gemm_split': [_p, _p, _i64, _i32, _i32, _p, _p, _p],
     'vtf_cosine_dedupe': [_p, _i64, _i64, _p, _p, _p],
     'vtf_group_create': [_i32, _p],
     'vtf_group_destroy': [_p],
