@@ -23,10 +23,13 @@ def _gemm(a, b, bias=None):
     return rc, out.cpu().numpy()
 
 
-@pytest.mark.parametrize('M,N,K', [(1, 8, 32), (65, 24, 64), (300, 136, 96), (8320, 1024, 1024), (1000, 256, 4096)])
+@pytest.mark.parametrize('M,N,K', [(1, 8, 32), (65, 24, 64), (300, 136, 96), (8320, 1024, 1024), (1000, 256, 4096),
+                                   (8320, 1032, 256)])
 def test_gemm_split_vs_float64(M, N, K):
-    """Tails in M (rows past M are loaded clamped, never stored) and in N (N % 128 != 0); the
-    error bound of the split products is ~2^-22 of sum |a||b| plus fp32 accumulation."""
+    """Tails in M (rows past M are loaded clamped, never stored) and in N (N % 128 != 0); grids
+    just past a whole round of workgroup slots (520 / 585 tiles on 2 x 256) run their last tiles
+    as in-launch split-K slices.  The error bound of the split products is ~2^-22 of
+    sum |a||b| plus fp32 accumulation."""
     rng = np.random.default_rng(M + N + K)
     a = rng.standard_normal((M, K)).astype(np.float32)
     b = (rng.standard_normal((N, K)) * 0.05).astype(np.float32)
@@ -38,6 +41,10 @@ def test_gemm_split_vs_float64(M, N, K):
     err = np.abs(got - ref) / scale
     print('max rel-to-|a||b| err', err.max())
     assert err.max() < 2e-6
+    # deterministic (fixed slice order) and the tail arrival counters are reset for the next launch
+    rc2, again = _gemm(a, b, bias)
+    assert rc2 == 0
+    np.testing.assert_array_equal(got, again)
 
 
 def test_gemm_split_refuses_out_of_range():

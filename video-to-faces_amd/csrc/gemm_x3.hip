@@ -24,6 +24,9 @@
 #include <cstdlib>
 #include <cmath>
 #include <cstring>
+#include <map>
+#include <mutex>
+#include <vector>
 
 #include "common.hpp"
 #include "gemm_x3.hpp"
@@ -34,6 +37,52 @@ namespace {
 
 typedef __attribute__((ext_vector_type(8))) _Float16 h8;
 typedef __attribute__((ext_vector_type(4))) float f4;
+
+// fused epilogue of one tile from its fp32 LDS image E [BM][BN + 4]: each thread finishes 8
+// consecutive channels of a row (bias, residual, GELU; fp32 or SP stores, 16-byte accesses)
+template <int BM, int BN>
+__device__ inline void tile_epilogue(const GemmX3Params& p, const float* E, int64_t m0, int n0) {
+    constexpr int LDE = BN + 4;
+    const int tid = threadIdx.x, lane = tid & 63;
+    constexpr int G = BN / 8;
+    static_assert(256 % G == 0, "epilogue groups");
+    const int g = tid % G, c0 = n0 + 8 * g;
+    if (c0 >= p.N) return;
+    float b8[8];
+#pragma unroll
+    for (int e = 0; e < 8; e++) b8[e] = p.bias ? p.bias[c0 + e] : 0.f;
+    bool bad = false;
+    for (int r = tid / G; r < BM; r += 256 / G) {
+        const int64_t m = m0 + r;
+        if (m >= p.M) break;
+        const f4 lo = *(const f4*)(E + r * LDE + 8 * g), hi = *(const f4*)(E + r * LDE + 8 * g + 4);
+        float v[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        float rv[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+        if (p.res) {
+            const f4 r0 = *(const f4*)(p.res + m * p.ldr + c0), r1 = *(const f4*)(p.res + m * p.ldr + c0 + 4);
+            rv[0] = r0[0], rv[1] = r0[1], rv[2] = r0[2], rv[3] = r0[3];
+            rv[4] = r1[0], rv[5] = r1[1], rv[6] = r1[2], rv[7] = r1[3];
+        }
+#pragma unroll
+        for (int e = 0; e < 8; e++) {
+            float x = v[e];
+            if (p.bias) x = x + b8[e];
+            if (p.res) x = x + rv[e];
+            if (p.gelu) x = 0.5f * x * (1.0f + erff(x * 0.70710678118654752f));
+            v[e] = x;
+        }
+        if (p.out_sp) {
+            char* row = (char*)p.out + m * (int64_t)p.N * 4;
+            sp_store4(row, c0, v[0], v[1], v[2], v[3], bad);
+            sp_store4(row, c0 + 4, v[4], v[5], v[6], v[7], bad);
+        } else {
+            float* o = (float*)p.out + m * p.ldo + c0;
+            *(f4*)o = f4{v[0], v[1], v[2], v[3]};
+            *(f4*)(o + 4) = f4{v[4], v[5], v[6], v[7]};
+        }
+    }
+    if (p.ovf && __ballot(bad) && lane == 0) atomicOr(p.ovf, 1);
+}
 
 template <int BM, int BN>
 __global__ __launch_bounds__(256, 2) void k_gemm_x3(GemmX3Params p) {
@@ -48,20 +97,25 @@ __global__ __launch_bounds__(256, 2) void k_gemm_x3(GemmX3Params p) {
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int wm = wave >> 1, wn = wave & 1;
-    // XCD-aware tile order (as k_conv): every XCD walks one contiguous run of tiles in groups of
-    // group_m M-tiles x all N-tiles
-    int tile_m = blockIdx.x, tile_n = blockIdx.y;
-    if (p.group_m > 0) {
-        const int gx = gridDim.x, gy = gridDim.y;
-        const int lin = blockIdx.x + gx * blockIdx.y, total = gx * gy;
-        const int xcd = lin & 7, loc = lin >> 3, per = total >> 3, rem = total & 7;
-        const int L = xcd < rem ? xcd * (per + 1) + loc : rem * (per + 1) + (xcd - rem) * per + loc;
-        const int span = p.group_m * gy;
-        const int first = (L / span) * p.group_m;
-        const int gsz = min(gx - first, p.group_m);
-        tile_m = first + (L % span) % gsz;
-        tile_n = (L % span) / gsz;
+    // Work item: blockIdx.x < dp_tiles = one whole tile (data-parallel rounds); the rest are the
+    // tail tiles' K slices (split-K over tail_split slices, reduced in-launch by the last
+    // arriving slice).  Whole tiles are dealt XCD-aware: every XCD owns one contiguous run of
+    // tile ids (workgroups go to XCDs round-robin by id); tile ids walk groups of group_m
+    // M-tiles x all N-tiles, so the A row-blocks and B column-blocks an XCD's resident
+    // workgroups share stay in its L2.  (Placement only affects speed; any bijection is correct.)
+    const int bid = blockIdx.x;
+    const bool tail = bid >= p.dp_tiles;
+    int t, slice = 0;
+    if (!tail) {
+        const int xcd = bid & 7, loc = bid >> 3, per = p.dp_tiles >> 3, rem = p.dp_tiles & 7;
+        t = xcd < rem ? xcd * (per + 1) + loc : rem * (per + 1) + (xcd - rem) * per + loc;
+    } else {
+        t = p.dp_tiles + (bid - p.dp_tiles) / p.tail_split;
+        slice = (bid - p.dp_tiles) % p.tail_split;
     }
+    const int gm = p.group_m > 0 ? p.group_m : p.gx;
+    const int span = gm * p.gy, first = (t / span) * gm, gsz = min(p.gx - first, gm);
+    const int tile_m = first + (t % span) % gsz, tile_n = (t % span) / gsz;
     const int64_t m0 = (int64_t)tile_m * BM;
     const int n0 = tile_n * BN;
 
@@ -111,14 +165,17 @@ __global__ __launch_bounds__(256, 2) void k_gemm_x3(GemmX3Params p) {
     const int o1 = (lane & 15) * RB + (((4 + (lane >> 4)) ^ hsw) << 4);  // plane 1
 
     const int KT = p.K / 32;
-    issue(0, 0);
-    for (int kt = 0; kt < KT; kt++) {
+    const int kt0 = tail ? (int)((int64_t)slice * KT / p.tail_split) : 0;
+    const int kt1 = tail ? (int)((int64_t)(slice + 1) * KT / p.tail_split) : KT;
+    issue(kt0, 0);
+    for (int kt = kt0; kt < kt1; kt++) {
         // this wave's pieces of step kt have landed; after the barrier every wave's have, and
         // every wave is done reading the other stage (its MFMAs consumed those reads)
         asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
-        if (kt + 1 < KT) issue(kt + 1, (kt + 1) & 1);
-        const char* As = smem + (kt & 1) * ST + wm * WM * RB;
-        const char* Bs = smem + (kt & 1) * ST + A_ST + wn * WN * RB;
+        const int sb = (kt - kt0) & 1;
+        if (kt + 1 < kt1) issue(kt + 1, sb ^ 1);
+        const char* As = smem + sb * ST + wm * WM * RB;
+        const char* Bs = smem + sb * ST + A_ST + wn * WN * RB;
         h8 b0[FN], b1[FN];
 #pragma unroll
         for (int j = 0; j < FN; j++) {
@@ -138,6 +195,19 @@ __global__ __launch_bounds__(256, 2) void k_gemm_x3(GemmX3Params p) {
         }
     }
     __syncthreads();  // no DMA outstanding; every wave is done with the stages
+    if (tail) {
+        // K slice of a tail tile: the fp32 partial (fragment order: 16-B stores, coalesced) to the
+        // workspace; k_gemm_x3_tail sums the slices in order and runs the epilogue.  (An in-launch
+        // last-arriver reduction needs agent-scope release/acquire fences, which write back and
+        // invalidate the XCD's L2 under the whole-tile workgroups still streaming from it:
+        // measured 20% slower on ViT-L.)
+        f4* slab = (f4*)(p.ws + ((int64_t)(t - p.dp_tiles) * p.tail_split + slice) * (BM * BN));
+#pragma unroll
+        for (int i = 0; i < FM; i++)
+#pragma unroll
+            for (int j = 0; j < FN; j++) slab[((wave * FM + i) * FN + j) * 64 + lane] = acc[i][j] + accx[i][j] * 0.00048828125f;
+        return;
+    }
     float* E = (float*)smem;
 #pragma unroll
     for (int j = 0; j < FN; j++)
@@ -149,44 +219,36 @@ __global__ __launch_bounds__(256, 2) void k_gemm_x3(GemmX3Params p) {
                 E[(wm * WM + i * 16 + 4 * (lane >> 4) + q) * LDE + wn * WN + j * 16 + (lane & 15)] = v[q];
         }
     __syncthreads();
-    constexpr int G = BN / 8;
-    static_assert(256 % G == 0, "epilogue groups");
-    const int g = tid % G, c0 = n0 + 8 * g;
-    if (c0 >= p.N) return;
-    float b8[8];
+    tile_epilogue<BM, BN>(p, E, m0, n0);
+}
+
+// tail tiles: 8 workgroups per tile, each sums the K slices of one 16-row block (the 8 fragments
+// with that wm, i: 2 f4 per thread) in slice order (deterministic) into an LDS image of the
+// block, then the shared epilogue over those 16 rows
+template <int BM, int BN>
+__global__ __launch_bounds__(256) void k_gemm_x3_tail(GemmX3Params p) {
+    constexpr int LDE = BN + 4, WM = BM / 2, WN = BN / 2, FM = WM / 16, FN = WN / 16;
+    static_assert(BM == 128 && BN == 128, "tail reduce layout: 16-row blocks of 2 waves x 4 fragments");
+    __shared__ __attribute__((aligned(16))) float E[16 * LDE];
+    const int tid = threadIdx.x;
+    const int tt = blockIdx.x >> 3, part = blockIdx.x & 7, wm = part >> 2, i = part & 3;
+    const int t = p.dp_tiles + tt;
+    const int gm = p.group_m > 0 ? p.group_m : p.gx;
+    const int span = gm * p.gy, first = (t / span) * gm, gsz = min(p.gx - first, gm);
+    const int tile_m = first + (t % span) % gsz, tile_n = (t % span) / gsz;
+    const f4* s0 = (const f4*)(p.ws + (int64_t)tt * p.tail_split * (BM * BN));
 #pragma unroll
-    for (int e = 0; e < 8; e++) b8[e] = p.bias ? p.bias[c0 + e] : 0.f;
-    bool bad = false;
-    for (int r = tid / G; r < BM; r += 256 / G) {
-        const int64_t m = m0 + r;
-        if (m >= p.M) break;
-        const f4 lo = *(const f4*)(E + r * LDE + 8 * g), hi = *(const f4*)(E + r * LDE + 8 * g + 4);
-        float v[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-        float rv[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-        if (p.res) {
-            const f4 r0 = *(const f4*)(p.res + m * p.ldr + c0), r1 = *(const f4*)(p.res + m * p.ldr + c0 + 4);
-            rv[0] = r0[0], rv[1] = r0[1], rv[2] = r0[2], rv[3] = r0[3];
-            rv[4] = r1[0], rv[5] = r1[1], rv[6] = r1[2], rv[7] = r1[3];
-        }
+    for (int h = 0; h < 2; h++) {
+        const int f = tid + 256 * h;  // 512 f4: wn (1 bit) | j (2 bits) | lane (6 bits)
+        const int wn = f >> 8, j = (f >> 6) & 3, lane = f & 63;
+        const int idx = (((2 * wm + wn) * FM + i) * FN + j) * 64 + lane;
+        f4 v = s0[idx];
+        for (int z = 1; z < p.tail_split; z++) v = v + s0[(int64_t)z * (BM * BN / 4) + idx];
 #pragma unroll
-        for (int e = 0; e < 8; e++) {
-            float x = v[e];
-            if (p.bias) x = x + b8[e];
-            if (p.res) x = x + rv[e];
-            if (p.gelu) x = 0.5f * x * (1.0f + erff(x * 0.70710678118654752f));
-            v[e] = x;
-        }
-        if (p.out_sp) {
-            char* row = (char*)p.out + m * (int64_t)p.N * 4;
-            sp_store4(row, c0, v[0], v[1], v[2], v[3], bad);
-            sp_store4(row, c0 + 4, v[4], v[5], v[6], v[7], bad);
-        } else {
-            float* o = (float*)p.out + m * p.ldo + c0;
-            *(f4*)o = f4{v[0], v[1], v[2], v[3]};
-            *(f4*)(o + 4) = f4{v[4], v[5], v[6], v[7]};
-        }
+        for (int q = 0; q < 4; q++) E[(4 * (lane >> 4) + q) * LDE + wn * WN + j * 16 + (lane & 15)] = v[q];
     }
-    if (p.ovf && __ballot(bad) && lane == 0) atomicOr(p.ovf, 1);
+    __syncthreads();
+    tile_epilogue<16, BN>(p, E, (int64_t)tile_m * BM + wm * WM + i * 16, tile_n * BN);
 }
 
 // one thread per 8-element chunk
@@ -214,6 +276,43 @@ int gemm_group_m() {
     return g;
 }
 
+// tail split-K (VTF_GEMM_TAIL=0 disables: every tile whole)
+bool gemm_tail_on() {
+    static bool on = [] {
+        const char* e = std::getenv("VTF_GEMM_TAIL");
+        return !(e && std::atoi(e) == 0);
+    }();
+    return on;
+}
+
+// per-(device, stream) tail workspace (fp32 slabs): grows x1.5; an outgrown buffer is retired,
+// not freed (hipFree synchronises the device while other lanes' kernels may still use it)
+float* tail_ws(hipStream_t st, size_t bytes) {
+    static std::mutex mu;
+    static std::map<std::pair<int, hipStream_t>, std::pair<float*, size_t>> m;
+    static std::vector<void*> retired;
+    std::lock_guard<std::mutex> g(mu);
+    auto& w = m[{stream_device(st), st}];
+    if (w.second < bytes) {
+        if (w.first) retired.push_back(w.first);
+        w.first = nullptr;
+        w.second = 0;
+        const size_t b = bytes + bytes / 2;
+        VTF_HIP(hipMalloc((void**)&w.first, b));
+        w.second = b;
+    }
+    return w.first;
+}
+
+int device_cu_count() {
+    static int cus = [] {
+        int dev = 0, n = 256;
+        if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev);
+        return n;
+    }();
+    return cus;
+}
+
 }  // namespace
 
 void launch_gemm_x3(const GemmX3Params& p0, hipStream_t st) {
@@ -224,8 +323,28 @@ void launch_gemm_x3(const GemmX3Params& p0, hipStream_t st) {
     GemmX3Params p = p0;
     p.group_m = gemm_group_m();
     constexpr int BM = 128, BN = 128;
-    dim3 g((unsigned)cdiv(p.M, BM), (unsigned)cdiv(p.N, BN));
-    k_gemm_x3<BM, BN><<<g, 256, 0, st>>>(p);
+    p.gx = (int)cdiv(p.M, BM);
+    p.gy = (int)cdiv(p.N, BN);
+    const int T = p.gx * p.gy, KT = p.K / 32;
+    // Rounds of whole tiles fill the chip's 2 x CUs workgroup slots; a last round holding only a
+    // few tiles (M = 8320 token rows x N = 1024: 520 tiles on 512 slots) would run them on an
+    // otherwise idle chip, so those tiles are split along K instead (>= 4 k-steps per slice)
+    // and spread over the free slots.
+    const int slots = 2 * device_cu_count();
+    p.dp_tiles = T;
+    p.tail_split = 1;
+    if (gemm_tail_on() && T > slots) {
+        const int R = T % slots;
+        const int S = R > 0 ? std::min(slots / R, KT / 4) : 0;
+        if (R > 0 && R <= slots / 2 && S >= 2) {
+            p.dp_tiles = T - R;
+            p.tail_split = S;
+            p.ws = tail_ws(st, (size_t)R * S * BM * BN * 4);
+        }
+    }
+    const int64_t grid = (int64_t)p.dp_tiles + (int64_t)(T - p.dp_tiles) * p.tail_split;
+    k_gemm_x3<BM, BN><<<(unsigned)grid, 256, 0, st>>>(p);
+    if (p.dp_tiles < T) k_gemm_x3_tail<BM, BN><<<(unsigned)(T - p.dp_tiles) * 8, 256, 0, st>>>(p);
 }
 
 void launch_split_rows(const float* x, int64_t rows, int K, int64_t ld, void* out, int* ovf, hipStream_t st) {

@@ -19,7 +19,11 @@ struct GemmX3Params {
     int N, K, ldo, ldr;
     int gelu;            // exact erf GELU after bias / residual (ViT MLP, vit.py:37)
     int out_sp;
-    int group_m;         // XCD-aware tile order (set by launch_gemm_x3)
+    // set by launch_gemm_x3: tile grid, XCD-aware order, whole tiles vs split-K tail tiles
+    int gx, gy, group_m;
+    int dp_tiles;        // work items < dp_tiles are whole tiles
+    int tail_split;      // the remaining tiles run as tail_split K slices each
+    float* ws;           // tail partial sums [tail tiles][tail_split][BM * BN] (k_gemm_x3_tail reduces)
 };
 
 // C = A B^T (+ bias) (+ res) (GELU): K % 32 == 0, N % 8 == 0
