@@ -18,7 +18,7 @@ print('forwards:', ' '.join('%.0f' % (b / 1e3) for b, _ in fw), 'us busy')
 busy, seq = max(fw, key=lambda t: t[0])
 agg = {}
 for r in seq:
-    n = re.sub(r'\(.*', '', r[0]).replace('_ZN3vtf6k_convIDF16bLi', 'conv').replace('EEEvNS_10ConvParamsE', '')[:44]
+    n = re.sub(r'\(anonymous namespace\)::', '', r[0]); n = re.sub(r'\(.*', '', n).replace('_ZN3vtf6k_convIDF16bLi', 'conv').replace('EEEvNS_10ConvParamsE', '')[:44]
     if len(sys.argv) > 2:
         print('%-44s %8.1f us  grid %6d x %4d x %2d' % (n, r[3] / 1e3, r[4] // r[7], r[5], r[6]))
     a = agg.setdefault(n, [0, 0.0])

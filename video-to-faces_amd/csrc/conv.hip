@@ -25,6 +25,7 @@
 
 #include "common.hpp"
 #include "conv.hpp"
+#include "conv_dev.hpp"
 
 // timing-only staging switches (scripts/ab_xdbg.sh): build with -DVTF_CONV_XDBG=1
 #ifndef VTF_CONV_XDBG
@@ -32,130 +33,6 @@
 #endif
 
 namespace vtf {
-
-typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
-typedef __attribute__((ext_vector_type(4))) float f32x4;
-
-template <typename T>
-struct VecT;
-template <>
-struct VecT<float> {
-    typedef f32x4 type;
-    static constexpr int V = 4;
-};
-template <>
-struct VecT<__bf16> {
-    typedef bf16x8 type;
-    static constexpr int V = 8;
-};
-
-__device__ inline float to_f(float v) { return v; }
-__device__ inline float to_f(__bf16 v) { return (float)v; }
-template <typename T>
-__device__ inline T from_f(float v);
-template <>
-__device__ inline float from_f<float>(float v) { return v; }
-template <>
-__device__ inline __bf16 from_f<__bf16>(float v) { return (__bf16)v; }
-
-// residual element index of output (m, c): same layout as the output, or the half-resolution
-// map of the FPN top-down add (res_up2)
-__device__ inline int64_t res_index(const ConvParams& p, int64_t m, int c) {
-    if (!p.res_up2) return m * p.res_cstride + c;
-    const int ow = (int)(m % p.OW);
-    const int64_t t = m / p.OW;
-    const int oh = (int)(t % p.OH);
-    const int64_t n = t / p.OH;
-    return ((n * (p.OH >> 1) + (oh >> 1)) * (p.OW >> 1) + (ow >> 1)) * p.res_cstride + c;
-}
-
-// fused epilogue of one output element (bias / BN / scale / residual / activation / layout);
-// rv = the residual element (loaded by the caller: a workgroup's residual loads are issued
-// together, not one round trip per output behind the previous store)
-template <typename T>
-__device__ inline void conv_epilogue(const ConvParams& p, int64_t m, int c, float v, float bias, float al, float be,
-                                     float pr, float rv) {
-    T* __restrict__ out = (T*)p.out;
-    if (p.bias) v = v + bias;
-    if (p.alpha) v = fmaf(v, al, be);
-    if (p.scale != 1.f) v = v * p.scale;
-    if (p.res && !p.res_post) v = v + rv;
-    if (p.relu) v = fmaxf(v, 0.f);
-    if (p.leaky) v = v > 0.f ? v : v * p.slope;
-    if (p.prelu) v = v > 0.f ? v : pr * v;
-    if (p.gelu) v = 0.5f * v * (1.0f + erff(v * 0.70710678118654752f));
-    if (p.res && p.res_post) v = v + rv;
-    if (p.up2) {
-        int ow = (int)(m % p.OW);
-        int64_t t = m / p.OW;
-        int oh = (int)(t % p.OH);
-        int64_t n = t / p.OH;
-        int64_t o = ((n * 2 * p.OH + 2 * oh) * 2 * p.OW + 2 * ow) * p.out_cstride + p.out_coff + c;
-        int64_t rs = (int64_t)2 * p.OW * p.out_cstride;
-        T tv = from_f<T>(v);
-        out[o] = tv;
-        out[o + p.out_cstride] = tv;
-        out[o + rs] = tv;
-        out[o + rs + p.out_cstride] = tv;
-    } else if (p.out_f32) {
-        ((float*)p.out)[m * p.out_cstride + p.out_coff + c] = v;
-    } else if (p.n_split && c >= p.n_split) {
-        ((T*)p.out2)[m * p.out2_cstride + p.out2_coff + (c - p.n_split)] = from_f<T>(v);
-    } else {
-        out[m * p.out_cstride + p.out_coff + c] = from_f<T>(v);
-    }
-}
-
-// 8 consecutive output channels c0..c0+7 of row m (c0 % 8 == 0, channel strides / offsets
-// multiples of 8): the same element math as conv_epilogue with 16/32-byte loads and stores
-template <typename T>
-__device__ inline void conv_epilogue8(const ConvParams& p, int64_t m, int c0, float (&v)[8], const float (&b8)[8],
-                                      const float (&al8)[8], const float (&be8)[8], const float (&pr8)[8]) {
-    typedef __attribute__((ext_vector_type(8))) T t8;
-    float rv[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    if (p.res) {
-        const t8 r = *(const t8*)((const T*)p.res + res_index(p, m, c0));
-#pragma unroll
-        for (int e = 0; e < 8; e++) rv[e] = to_f(r[e]);
-    }
-    t8 o;
-#pragma unroll
-    for (int e = 0; e < 8; e++) {
-        float x = v[e];
-        if (p.bias) x = x + b8[e];
-        if (p.alpha) x = fmaf(x, al8[e], be8[e]);
-        if (p.scale != 1.f) x = x * p.scale;
-        if (p.res && !p.res_post) x = x + rv[e];
-        if (p.relu) x = fmaxf(x, 0.f);
-        if (p.leaky) x = x > 0.f ? x : x * p.slope;
-        if (p.prelu) x = x > 0.f ? x : pr8[e] * x;
-        if (p.gelu) x = 0.5f * x * (1.0f + erff(x * 0.70710678118654752f));
-        if (p.res && p.res_post) x = x + rv[e];
-        v[e] = x;
-        o[e] = from_f<T>(x);
-    }
-    if (p.up2) {
-        const int ow = (int)(m % p.OW);
-        const int64_t t = m / p.OW;
-        const int oh = (int)(t % p.OH);
-        const int64_t n = t / p.OH;
-        T* out = (T*)p.out;
-        const int64_t a = ((n * 2 * p.OH + 2 * oh) * 2 * p.OW + 2 * ow) * p.out_cstride + p.out_coff + c0;
-        const int64_t rs = (int64_t)2 * p.OW * p.out_cstride;
-        *(t8*)(out + a) = o;
-        *(t8*)(out + a + p.out_cstride) = o;
-        *(t8*)(out + a + rs) = o;
-        *(t8*)(out + a + rs + p.out_cstride) = o;
-    } else if (p.out_f32) {
-        float* out = (float*)p.out + m * p.out_cstride + p.out_coff + c0;
-        *(f32x4*)out = f32x4{v[0], v[1], v[2], v[3]};
-        *(f32x4*)(out + 4) = f32x4{v[4], v[5], v[6], v[7]};
-    } else if (p.n_split && c0 >= p.n_split) {
-        *(t8*)((T*)p.out2 + m * p.out2_cstride + p.out2_coff + (c0 - p.n_split)) = o;
-    } else {
-        *(t8*)((T*)p.out + m * p.out_cstride + p.out_coff + c0) = o;
-    }
-}
 
 template <typename T, int BM, int BN, int BK, bool SPLIT, bool X = false>
 __global__ __launch_bounds__(256) void k_conv(ConvParams p) {
@@ -656,6 +533,16 @@ void launch_conv(const ConvParams& p, bool bf16, hipStream_t st) {
     VTF_CHECK(!p.res_up2 || (p.OH % 2 == 0 && p.OW % 2 == 0), VTF_E_ARG, "conv: half-resolution residual needs even OH/OW");
     VTF_CHECK(!p.n_split || (p.out2 && p.n_split > 0 && p.n_split < p.Cout && !p.up2 && !p.out_f32), VTF_E_ARG,
               "conv: output split needs out2, 0 < n_split < Cout, plain layout");
+    // bf16 convs go to the LDS-DMA kernel (conv_dma.hip) when their channel counts allow it
+    // (VTF_CONV_DMA=0 keeps k_conv: A/B timing)
+    static const bool dma = [] {
+        const char* e = std::getenv("VTF_CONV_DMA");
+        return !(e && std::atoi(e) == 0);
+    }();
+    if (bf16 && dma && conv_dma_prefer_bf16(p)) {
+        launch_conv_dma(p, true, st);
+        return;
+    }
     if (bf16)
         launch_t<__bf16>(p, st);
     else
@@ -732,6 +619,51 @@ static int pool_out(int L, int k, int s, bool ceil_mode) {
     if (ceil_mode && (o - 1) * s >= L) o--;
     return o;
 }
+
+// the same pool writing the split-pair layout (gemm_x3.hpp) for a split-mode conv; a value beyond
+// the fp16 range raises *ovf
+__global__ void k_maxpool_ks_sp(const float* __restrict__ in, int N, int H, int W, int C, int k, int s, int OH, int OW,
+                                char* __restrict__ out, int* __restrict__ ovf) {
+    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int C4 = C >> 2;
+    int64_t tot = (int64_t)N * OH * OW * C4;
+    bool bad = false;
+    if (i < tot) {
+        int c4 = (int)(i % C4);
+        int64_t t = i / C4;
+        int ow = (int)(t % OW);
+        t /= OW;
+        int oh = (int)(t % OH);
+        int n = (int)(t / OH);
+        f32x4 m = {-3.402823466e38f, -3.402823466e38f, -3.402823466e38f, -3.402823466e38f};
+        const f32x4* src = (const f32x4*)in + (int64_t)n * H * W * C4 + c4;
+        for (int dy = 0; dy < k; dy++) {
+            int y = oh * s + dy;
+            if (y >= H) break;
+            for (int dx = 0; dx < k; dx++) {
+                int x = ow * s + dx;
+                if (x >= W) break;
+                f32x4 v = src[((int64_t)y * W + x) * C4];
+                m.x = fmaxf(m.x, v.x);
+                m.y = fmaxf(m.y, v.y);
+                m.z = fmaxf(m.z, v.z);
+                m.w = fmaxf(m.w, v.w);
+            }
+        }
+        sp_store4(out + (i / C4) * (int64_t)C * 4, 4 * c4, m.x, m.y, m.z, m.w, bad);
+    }
+    if (__ballot(bad) && (threadIdx.x & 63) == 0) atomicOr(ovf, 1);
+}
+
+void launch_maxpool_ks_sp(const float* in, int N, int H, int W, int C, int k, int s, bool ceil_mode, void* out, int& OH,
+                          int& OW, int* ovf, hipStream_t st) {
+    OH = pool_out(H, k, s, ceil_mode);
+    OW = pool_out(W, k, s, ceil_mode);
+    VTF_CHECK(C % 8 == 0, VTF_E_ARG, "maxpool (split pairs): C must be a multiple of 8");
+    int64_t tot = (int64_t)N * OH * OW * (C / 4);
+    if (tot > 0) k_maxpool_ks_sp<<<cdiv(tot, 256), 256, 0, st>>>(in, N, H, W, C, k, s, OH, OW, (char*)out, ovf);
+}
+
 
 void launch_maxpool_ks(const float* in, int N, int H, int W, int C, int k, int s, bool ceil_mode, float* out,
                        int& OH, int& OW, hipStream_t st) {

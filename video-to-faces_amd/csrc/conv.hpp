@@ -36,6 +36,11 @@ struct ConvParams {
                          // 1 = staging without the split arithmetic / range check, 2 = no operand loads
                          // (wrong results; timing only)
     float* ws;           // fp32 [split][M][Cout] partial sums (split-K only)
+    int out_sp;          // output in the split-pair layout (gemm_x3.hpp; fp32 operand modes): the next
+                         // layer's operand for conv_dma's split mode; a value beyond 2^14 sets *ovf
+    int in_sp;           // input (and weights) in the split-pair layout: conv_dma split mode
+    const void* zero;    // conv_dma: 16 zero bytes (the DMA source of padding / K-tail pieces; set by the launcher)
+    int dp_tiles, tail_split, gx, gy;  // conv_dma work items (set by the launcher)
     int64_t M;           // N*OH*OW
     int N, H, W, Cin, OH, OW, Cout, KH, KW, sh, sw, ph, pw, K;
     int out_cstride, out_coff, res_cstride;
@@ -48,11 +53,18 @@ struct ConvParams {
 };
 
 void launch_conv(const ConvParams& p, bool bf16, hipStream_t st);
+// LDS-DMA implicit-GEMM conv (conv_dma.hip): bf16 operands, or split-pair operands (in_sp, fp32-grade)
+bool conv_dma_ok(const ConvParams& p);
+bool conv_dma_prefer_bf16(const ConvParams& p);  // bf16 shapes where conv_dma beats k_conv
+void launch_conv_dma(const ConvParams& p, bool bf16, hipStream_t st);
 void launch_maxpool(const void* in, int N, int H, int W, int C, void* out, int out_cstride, int out_coff, bool bf16,
                     hipStream_t st);
 // torch MaxPool2d(k, s, ceil_mode) without padding, NHWC fp32; returns (OH, OW)
 void launch_maxpool_ks(const float* in, int N, int H, int W, int C, int k, int s, bool ceil_mode, float* out,
                        int& OH, int& OW, hipStream_t st);
+// the same pool with a split-pair output (gemm_x3.hpp; C % 8 == 0), range flag *ovf
+void launch_maxpool_ks_sp(const float* in, int N, int H, int W, int C, int k, int s, bool ceil_mode, void* out, int& OH,
+                          int& OW, int* ovf, hipStream_t st);
 void launch_nchw_to_nhwc(const float* in, int N, int C, int H, int W, int Cp, void* out, bool bf16, hipStream_t st);
 // scratch: N * (C + D) floats
 void launch_facenet_head(const void* x, int N, int HW, int C, const float* w, const float* alpha, const float* beta,

@@ -1,0 +1,449 @@
+// Implicit-GEMM convolution with LDS-DMA operand staging (gfx950): k_conv's successor for the
+// bf16 (perf) mode and for the fp32-grade split-fp16 mode on pre-split operands.
+//
+// Same GEMM view and epilogue as k_conv (conv.hip): M = N*OH*OW output pixels, N = Cout,
+// K = KH*KW*Cin with k = (kh, kw, ci); A is gathered from the NHWC input on the fly, B is the
+// weight matrix [Cout][K].  What changes is the staging: every operand piece is 16 bytes =
+// 8 consecutive channels of one input pixel (Cin % 8 == 0), and goes HBM -> LDS by one lane of
+// a global_load_lds_dwordx4 -- no staging registers, no VALU conversion, no ds_write.  A piece
+// that lies in the zero padding, past K or past M is read from a 16-byte zero page instead
+// (the per-lane source address makes the im2col gather free).
+//
+//   MODE 0 (bf16): a k-step is 64 deep; LDS row = 8 chunks of 8 bf16; per fragment pair two
+//                  v_mfma_f32_16x16x32_bf16 (k 0..31, 32..63: k_conv's bf16 order, same bits)
+//   MODE 1 (split): operands in the split-pair layout (gemm_x3.hpp: x = x0 + x1 2^-11, fp16
+//                  pairs), a k-step is 32 deep; LDS row = 4 chunks x 2 planes; per fragment pair
+//                  three v_mfma_f32_16x16x32_f16 (x0 w0 | x0 w1 + x1 w0: k_conv's split chains,
+//                  same bits when the K loop is not split)
+//
+// LDS image (both modes): rows of 128 B, 16-B slot s of row r holds source slot s ^ ((r >> 1) & 7),
+// written lane-linearly by the DMA (1 KB = 8 rows per wave-instruction; the swizzle is applied
+// to the source address), read conflict-free by ds_read_b128 fragment loads.  Two stages (the
+// DMA of step k+1 in flight during step k), one barrier per step, two workgroups per CU.
+// Grids past a whole round of workgroup slots split their last tiles along K, grids below one
+// round split every tile (bf16, or callers that accept a slice-order reduction: split_fp32);
+// k_conv_dma_tail sums the slices in order and runs the epilogue.
+#include <algorithm>
+#include <cstdlib>
+#include <map>
+#include <mutex>
+#include <type_traits>
+#include <vector>
+
+#include "common.hpp"
+#include "conv.hpp"
+#include "conv_dev.hpp"
+
+namespace vtf {
+
+namespace {
+
+typedef __attribute__((ext_vector_type(8))) _Float16 h8;
+typedef __attribute__((ext_vector_type(4))) float f4;
+
+template <int MODE, int BM, int BN, int WGM, int OCC = 2>
+struct DCfg {
+    static constexpr int WGN = 4 / WGM, WM = BM / WGM, WN = BN / WGN, FM = WM / 16, FN = WN / 16;
+    static constexpr int RB = 128, A_ST = BM * RB, ST = (BM + BN) * RB, LDE = BN + 4;
+    static constexpr int SM = 2 * ST > BM * LDE * 4 ? 2 * ST : BM * LDE * 4;
+    static constexpr int PA = BM / 32, PB = BN / 32;  // 1-KB DMA pieces per wave and stage
+    static constexpr int CPS = MODE == 1 ? 4 : 8;     // 8-element chunks per k-step
+    static constexpr int EB = MODE == 1 ? 4 : 2;      // global bytes per element
+    static constexpr int CB = 8 * EB;                 // global bytes per chunk
+    static constexpr int KS = 8 * CPS;                // k per step
+    static_assert(FM >= 1 && FN >= 1 && BM % 32 == 0 && BN % 32 == 0 && SM * OCC <= 160 * 1024, "tile config");
+};
+
+// the tile of work item bid: whole tiles dealt XCD-aware (each XCD owns a contiguous run of
+// tile ids; ids walk groups of group_m M-tiles x all N-tiles), then the K slices of the tail tiles
+__device__ inline void work_item(const ConvParams& p, int bid, int& t, int& slice, bool& tail) {
+    tail = bid >= p.dp_tiles;
+    slice = 0;
+    if (!tail) {
+        const int xcd = bid & 7, loc = bid >> 3, per = p.dp_tiles >> 3, rem = p.dp_tiles & 7;
+        t = xcd < rem ? xcd * (per + 1) + loc : rem * (per + 1) + (xcd - rem) * per + loc;
+    } else {
+        t = p.dp_tiles + (bid - p.dp_tiles) / p.tail_split;
+        slice = (bid - p.dp_tiles) % p.tail_split;
+    }
+}
+__device__ inline void tile_of(const ConvParams& p, int t, int& tile_m, int& tile_n) {
+    const int gm = p.group_m > 0 ? p.group_m : p.gx;
+    const int span = gm * p.gy, first = (t / span) * gm, gsz = min(p.gx - first, gm);
+    tile_m = first + (t % span) % gsz;
+    tile_n = (t % span) / gsz;
+}
+
+// epilogue of `rows` rows of the LDS tile image E [rows][BN + 4] starting at output row m0
+template <typename T, int BN>
+__device__ inline void dma_epilogue(const ConvParams& p, const float* E, int rows, int64_t m0, int n0) {
+    constexpr int LDE = BN + 4, G = BN / 8;
+    static_assert(256 % G == 0, "epilogue groups");
+    const int tid = threadIdx.x, g = tid % G, c0 = n0 + 8 * g;
+    bool bad = false;
+    if (c0 < p.Cout) {
+        float b8[8], al8[8], be8[8], pr8[8];
+#pragma unroll
+        for (int e = 0; e < 8; e++) {
+            b8[e] = p.bias ? p.bias[c0 + e] : 0.f;
+            al8[e] = p.alpha ? p.alpha[c0 + e] : 1.f;
+            be8[e] = p.alpha ? p.beta[c0 + e] : 0.f;
+            pr8[e] = p.prelu ? p.prelu[c0 + e] : 0.f;
+        }
+        for (int r = tid / G; r < rows; r += 256 / G) {
+            const int64_t m = m0 + r;
+            if (m >= p.M) break;
+            const f4 lo = *(const f4*)(E + r * LDE + 8 * g), hi = *(const f4*)(E + r * LDE + 8 * g + 4);
+            float v[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+            conv_epilogue8<T>(p, m, c0, v, b8, al8, be8, pr8, &bad);
+        }
+    }
+    if (p.out_sp && p.ovf && __ballot(bad) && (threadIdx.x & 63) == 0) atomicOr(p.ovf, 1);
+}
+
+template <int MODE, int BM, int BN, int WGM, int OCC>
+__global__ __launch_bounds__(256, OCC) void k_conv_dma(ConvParams p) {
+    using C = DCfg<MODE, BM, BN, WGM, OCC>;
+    using T = typename std::conditional<MODE == 0, __bf16, float>::type;
+    constexpr int PA = C::PA, PB = C::PB, FM = C::FM, FN = C::FN, RB = C::RB;
+    __shared__ __attribute__((aligned(16))) char smem[C::SM];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wm = wave / C::WGN, wn = wave % C::WGN;
+    int t, slice, tile_m, tile_n;
+    bool tail;
+    work_item(p, blockIdx.x, t, slice, tail);
+    tile_of(p, t, tile_m, tile_n);
+    const int64_t m0 = (int64_t)tile_m * BM;
+    const int n0 = tile_n * BN;
+
+    // this lane's DMA slot: row 32 j + 8 wave + (lane >> 3) of piece j, LDS slot lane & 7 holding
+    // source slot src (chunk kc of the step, plane offset pl for the split mode)
+    const int src = (lane & 7) ^ (((lane >> 4) + 4 * (wave & 1)) & 7);
+    const int kc = MODE == 1 ? (src & 3) : src;
+    const int pl = MODE == 1 ? (src >> 2) * 16 : 0;
+    const int ics = p.in_cstride ? p.in_cstride : p.Cin;
+    const int64_t pixb = (int64_t)ics * C::EB;
+    const int Cin8 = p.Cin >> 3, K8 = p.K >> 3;
+    const char* in = (const char*)p.in;
+    const char* wt = (const char*)p.w;
+    const char* zero = (const char*)p.zero;
+    // A rows: window origin (ih0, iw0) and its pixel address (outside the input for padded
+    // rows: only dereferenced for in-bounds taps); rows past M never pass the bounds test
+    int64_t abase[PA];
+    int aih[PA], aiw[PA];
+#pragma unroll
+    for (int j = 0; j < PA; j++) {
+        const int64_t m = m0 + 32 * j + 8 * wave + (lane >> 3);
+        if (m < p.M) {
+            const int ow = (int)(m % p.OW);
+            const int64_t q = m / p.OW;
+            const int oh = (int)(q % p.OH);
+            const int64_t n = q / p.OH;
+            aih[j] = oh * p.sh - p.ph;
+            aiw[j] = ow * p.sw - p.pw;
+            abase[j] = ((n * p.H + aih[j]) * p.W + aiw[j]) * pixb + pl;
+        } else {
+            aih[j] = -(1 << 29);
+            aiw[j] = 0;
+            abase[j] = 0;
+        }
+    }
+    int64_t bbase[PB];
+#pragma unroll
+    for (int j = 0; j < PB; j++) {
+        const int n = min(n0 + 32 * j + 8 * wave + (lane >> 3), p.Cout - 1);
+        bbase[j] = (int64_t)n * p.K * C::EB + pl;
+    }
+    const int KT = (p.K + C::KS - 1) / C::KS;
+    const int kt0 = tail ? (int)((int64_t)slice * KT / p.tail_split) : 0;
+    const int kt1 = tail ? (int)((int64_t)(slice + 1) * KT / p.tail_split) : KT;
+    // the lane's chunk c = (kh, kw, cc): k = 8 c = (kh * KW + kw) * Cin + 8 cc
+    int c = kt0 * C::CPS + kc;
+    int tap = c / Cin8, cc = c - tap * Cin8;
+    int kh = tap / p.KW, kw = tap - kh * p.KW;
+    const bool chk = p.ph | p.pw;  // padded windows: bounds-test every tap
+    auto issue = [&](int s) {
+        char* base = smem + s * C::ST;
+        const bool kv = c < K8;
+        const int64_t toff = ((int64_t)kh * p.W + kw) * pixb + cc * C::CB;
+#pragma unroll
+        for (int j = 0; j < PA; j++) {
+            bool ok = kv && aih[j] + kh >= 0;
+            if (chk) ok = ok && aih[j] + kh < p.H && (unsigned)(aiw[j] + kw) < (unsigned)p.W;
+            const char* g = ok ? in + abase[j] + toff : zero;
+            __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)g,
+                                             (void __attribute__((address_space(3)))*)(base + (wave + 4 * j) * 1024), 16,
+                                             0, 0);
+        }
+#pragma unroll
+        for (int j = 0; j < PB; j++) {
+            const char* g = kv ? wt + bbase[j] + (int64_t)c * C::CB : zero;
+            __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)g,
+                                             (void __attribute__((address_space(3)))*)(base + C::A_ST + (wave + 4 * j) * 1024),
+                                             16, 0, 0);
+        }
+    };
+    auto advance = [&]() {
+        c += C::CPS;
+        cc += C::CPS;
+        while (cc >= Cin8) {
+            cc -= Cin8;
+            if (++kw == p.KW) {
+                kw = 0;
+                kh++;
+            }
+        }
+    };
+
+    f4 acc[FM][FN], accx[MODE == 1 ? FM : 1][MODE == 1 ? FN : 1];
+#pragma unroll
+    for (int i = 0; i < FM; i++)
+#pragma unroll
+        for (int j = 0; j < FN; j++) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
+    if constexpr (MODE == 1) {
+#pragma unroll
+        for (int i = 0; i < FM; i++)
+#pragma unroll
+            for (int j = 0; j < FN; j++) accx[i][j] = f4{0.f, 0.f, 0.f, 0.f};
+    }
+    // fragment reads: row lane & 15 of a 16-row block, slot (lane >> 4) (plane 0 / k 0..31) and
+    // 4 + (lane >> 4) (plane 1 / k 32..63), swizzled by (row >> 1) & 7
+    const int hsw = (lane & 15) >> 1;
+    const int o0 = (lane & 15) * RB + (((lane >> 4) ^ hsw) << 4);
+    const int o1 = (lane & 15) * RB + (((4 + (lane >> 4)) ^ hsw) << 4);
+
+    issue(0);
+    for (int kt = kt0; kt < kt1; kt++) {
+        // this wave's pieces of step kt have landed; after the barrier every wave's have, and every
+        // wave is done reading the other stage
+        asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+        const int sb = (kt - kt0) & 1;
+        if (kt + 1 < kt1) {
+            advance();
+            issue(sb ^ 1);
+        }
+        const char* As = smem + sb * C::ST + wm * C::WM * RB;
+        const char* Bs = smem + sb * C::ST + C::A_ST + wn * C::WN * RB;
+        if constexpr (MODE == 1) {
+            h8 b0[FN], b1[FN];
+#pragma unroll
+            for (int j = 0; j < FN; j++) {
+                b0[j] = *(const h8*)(Bs + j * 16 * RB + o0);
+                b1[j] = *(const h8*)(Bs + j * 16 * RB + o1);
+            }
+#pragma unroll
+            for (int i = 0; i < FM; i++) {
+                const h8 a0 = *(const h8*)(As + i * 16 * RB + o0);
+                const h8 a1 = *(const h8*)(As + i * 16 * RB + o1);
+#pragma unroll
+                for (int j = 0; j < FN; j++) {
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a0, b0[j], acc[i][j], 0, 0, 0);
+                    accx[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a0, b1[j], accx[i][j], 0, 0, 0);
+                    accx[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a1, b0[j], accx[i][j], 0, 0, 0);
+                }
+            }
+        } else {
+            bf16x8 b0[FN], b1[FN];
+#pragma unroll
+            for (int j = 0; j < FN; j++) {
+                b0[j] = *(const bf16x8*)(Bs + j * 16 * RB + o0);
+                b1[j] = *(const bf16x8*)(Bs + j * 16 * RB + o1);
+            }
+#pragma unroll
+            for (int i = 0; i < FM; i++) {
+                const bf16x8 a0 = *(const bf16x8*)(As + i * 16 * RB + o0);
+                const bf16x8 a1 = *(const bf16x8*)(As + i * 16 * RB + o1);
+#pragma unroll
+                for (int j = 0; j < FN; j++) {
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, b0[j], acc[i][j], 0, 0, 0);
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1, b1[j], acc[i][j], 0, 0, 0);
+                }
+            }
+        }
+    }
+    if constexpr (MODE == 1) {
+#pragma unroll
+        for (int i = 0; i < FM; i++)
+#pragma unroll
+            for (int j = 0; j < FN; j++) acc[i][j] = acc[i][j] + accx[i][j] * 0.00048828125f;
+    }
+    __syncthreads();  // no DMA outstanding; every wave is done with the stages
+    if (tail) {
+        // K slice of a tail tile: fp32 partial in fragment order (coalesced 16-B stores)
+        f4* slab = (f4*)(p.ws + ((int64_t)(t - p.dp_tiles) * p.tail_split + slice) * (BM * BN));
+#pragma unroll
+        for (int i = 0; i < FM; i++)
+#pragma unroll
+            for (int j = 0; j < FN; j++) slab[((wave * FM + i) * FN + j) * 64 + lane] = acc[i][j];
+        return;
+    }
+    float* E = (float*)smem;
+#pragma unroll
+    for (int j = 0; j < FN; j++)
+#pragma unroll
+        for (int i = 0; i < FM; i++)
+#pragma unroll
+            for (int q = 0; q < 4; q++)
+                E[(wm * C::WM + i * 16 + 4 * (lane >> 4) + q) * C::LDE + wn * C::WN + j * 16 + (lane & 15)] = acc[i][j][q];
+    __syncthreads();
+    dma_epilogue<T, BN>(p, E, BM, m0, n0);
+}
+
+// tail tiles: one workgroup per (tile, 16-row block) sums the block's K slices in slice order
+// (deterministic) into an LDS image, then the epilogue of those 16 rows
+template <int MODE, int BM, int BN, int WGM, int OCC>
+__global__ __launch_bounds__(256) void k_conv_dma_tail(ConvParams p) {
+    using C = DCfg<MODE, BM, BN, WGM, OCC>;
+    using T = typename std::conditional<MODE == 0, __bf16, float>::type;
+    constexpr int NB = BM / 16, FM = C::FM, FN = C::FN, LDE = C::LDE;
+    __shared__ __attribute__((aligned(16))) float E[16 * LDE];
+    const int tid = threadIdx.x;
+    const int tt = blockIdx.x / NB, rb = blockIdx.x % NB, wm = rb / FM, i = rb % FM;
+    int tile_m, tile_n;
+    tile_of(p, p.dp_tiles + tt, tile_m, tile_n);
+    const f4* s0 = (const f4*)(p.ws + (int64_t)tt * p.tail_split * (BM * BN));
+    for (int f = tid; f < BN * 4; f += 256) {  // fragments (wn, j) x 64 lanes of this 16-row block
+        const int wn = f / (FN * 64), j = (f / 64) % FN, lane = f & 63;
+        const int idx = (((wm * C::WGN + wn) * FM + i) * FN + j) * 64 + lane;
+        f4 v = s0[idx];
+        for (int z = 1; z < p.tail_split; z++) v = v + s0[(int64_t)z * (BM * BN / 4) + idx];
+#pragma unroll
+        for (int q = 0; q < 4; q++) E[(4 * (lane >> 4) + q) * LDE + wn * C::WN + j * 16 + (lane & 15)] = v[q];
+    }
+    __syncthreads();
+    dma_epilogue<T, BN>(p, E, 16, (int64_t)tile_m * BM + wm * C::WM + i * 16, tile_n * BN);
+}
+
+// per-(device, stream) tail workspace: grows x1.5, outgrown buffers retired (hipFree would
+// synchronise the device while other streams' kernels may still use them)
+float* dma_ws(hipStream_t st, size_t bytes) {
+    static std::mutex mu;
+    static std::map<std::pair<int, hipStream_t>, std::pair<float*, size_t>> m;
+    static std::vector<void*> retired;
+    std::lock_guard<std::mutex> g(mu);
+    auto& w = m[{stream_device(st), st}];
+    if (w.second < bytes) {
+        if (w.first) retired.push_back(w.first);
+        w.first = nullptr;
+        w.second = 0;
+        const size_t b = bytes + bytes / 2;
+        VTF_HIP(hipMalloc((void**)&w.first, b));
+        w.second = b;
+    }
+    return w.first;
+}
+
+// 16 zero bytes per device (the DMA source of padding, K-tail and M-tail pieces)
+const void* zero_page(int dev) {
+    static std::mutex mu;
+    static std::map<int, void*> m;
+    std::lock_guard<std::mutex> g(mu);
+    void*& z = m[dev];
+    if (!z) {
+        VTF_HIP(hipMalloc(&z, 256));
+        VTF_HIP(hipMemset(z, 0, 256));
+    }
+    return z;
+}
+
+int cu_count() {
+    static int cus = [] {
+        int dev = 0, n = 256;
+        if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev);
+        return n;
+    }();
+    return cus;
+}
+
+int dma_group_m() {
+    static int g = [] {
+        const char* e = std::getenv("VTF_CONV_GROUP_M");
+        return e ? std::atoi(e) : 8;
+    }();
+    return g;
+}
+
+template <int MODE, int BM, int BN, int WGM, int OCC = 2>
+void launch_dma_t(ConvParams p, hipStream_t st) {
+    using C = DCfg<MODE, BM, BN, WGM, OCC>;
+    p.gx = (int)cdiv(p.M, BM);
+    p.gy = (int)cdiv(p.Cout, BN);
+    p.group_m = dma_group_m();
+    p.zero = zero_page(stream_device(st));
+    const int T = p.gx * p.gy, KT = (p.K + C::KS - 1) / C::KS;
+    const int slots = OCC * cu_count();
+    p.dp_tiles = T;
+    p.tail_split = 1;
+    p.split = 1;
+    if (MODE == 0 || p.split_fp32) {
+        if (T > slots) {
+            // a last round of only a few tiles: split those along K over the free slots
+            const int R = T % slots;
+            const int S = R > 0 ? std::min(slots / R, KT / 4) : 0;
+            if (R > 0 && R <= slots / 2 && S >= 2) {
+                p.dp_tiles = T - R;
+                p.tail_split = S;
+            }
+        } else {
+            // less than one round: split every tile (>= 4 k-steps per slice)
+            const int S = std::min(std::min(slots / T, KT / 4), 16);
+            if (S >= 2) {
+                p.dp_tiles = 0;
+                p.tail_split = S;
+            }
+        }
+    }
+    const int nt = T - p.dp_tiles;
+    p.ws = nt ? dma_ws(st, (size_t)nt * p.tail_split * BM * BN * 4) : nullptr;
+    k_conv_dma<MODE, BM, BN, WGM, OCC><<<(unsigned)(p.dp_tiles + nt * p.tail_split), 256, 0, st>>>(p);
+    if (nt) k_conv_dma_tail<MODE, BM, BN, WGM, OCC><<<(unsigned)(nt * (BM / 16)), 256, 0, st>>>(p);
+}
+
+}  // namespace
+
+bool conv_dma_ok(const ConvParams& p) {
+    // the 16-B pieces need 8-channel granules; the staged epilogue 8-channel groups
+    return p.Cin % 8 == 0 && (p.in_cstride == 0 || p.in_cstride % 8 == 0) && p.Cout % 8 == 0 && p.out_cstride % 8 == 0 &&
+           p.out_coff % 8 == 0 && (!p.res || p.res_cstride % 8 == 0) &&
+           (!p.n_split || (p.n_split % 8 == 0 && p.out2_cstride % 8 == 0 && p.out2_coff % 8 == 0));
+}
+
+bool conv_dma_prefer_bf16(const ConvParams& p) {
+    // measured on FaceNet (batch 128, profiles/r02n_*): the DMA kernel wins on grids of at least
+    // one whole round of 64+-channel tiles (stem 3x3 convs, Mixed_6a), k_conv's small tiles win on
+    // the small Block35/17/8 grids and on 32-channel outputs
+    if (!conv_dma_ok(p) || p.Cout <= 32) return false;
+    const int bm = p.Cout <= 64 ? 256 : 128, bn = p.Cout <= 64 ? 64 : 128;
+    return cdiv(p.M, bm) * cdiv(p.Cout, bn) >= 2 * cu_count();
+}
+
+void launch_conv_dma(const ConvParams& p, bool bf16, hipStream_t st) {
+    if (p.M <= 0) return;
+    VTF_CHECK(conv_dma_ok(p), VTF_E_ARG, "conv_dma: channel counts / strides must be multiples of 8");
+    VTF_CHECK(bf16 || p.in_sp, VTF_E_ARG, "conv_dma: bf16 or split-pair operands");
+    VTF_CHECK(!p.out_sp || !bf16, VTF_E_ARG, "conv_dma: split-pair output is an fp32-mode output");
+    if (bf16) {
+        if (p.Cout <= 32)
+            launch_dma_t<0, 256, 32, 4>(p, st);
+        else if (p.Cout <= 64)
+            launch_dma_t<0, 256, 64, 4>(p, st);
+        else
+            launch_dma_t<0, 128, 128, 2>(p, st);
+    } else {
+        // split mode, <= 64 channels (MTCNN RNet / ONet convs, K = 192..576: 6-18 k-steps, so the
+        // per-tile prologue / epilogue latency weighs): 128 x 64 tiles at 3 workgroups per CU hide
+        // more of it than 256 x 64 tiles at 2 (VTF_DMA_SPLIT64=256 for the latter)
+        static const int big = [] {
+            const char* e = std::getenv("VTF_DMA_SPLIT64");
+            return e ? std::atoi(e) : 128;
+        }();
+        if (p.Cout <= 64 && big == 256)
+            launch_dma_t<1, 256, 64, 4>(p, st);
+        else if (p.Cout <= 64)
+            launch_dma_t<1, 128, 64, 2, 3>(p, st);
+        else
+            launch_dma_t<1, 128, 128, 2>(p, st);
+    }
+}
+
+}  // namespace vtf

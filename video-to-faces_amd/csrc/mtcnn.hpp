@@ -59,7 +59,7 @@ void launch_pnet(bool dense, const uint8_t* frames, int64_t frame_stride, int64_
 int cand_front_side(bool onet);
 void launch_cand_front(bool onet, const int4* sat, int H, int W, const float4* boxes, const int32_t* img, int64_t n,
                        const float* w1, const _Float16* w1h, const float* b1, const float* a1, float* out, int32_t* err,
-                       hipStream_t st);
+                       hipStream_t st, int* ovf = nullptr);
 // Fused RNet / ONet front half (mtcnn_cand.hip): crop + conv1 + PReLU + pool + conv2 + PReLU +
 // pool on split-fp16 matrix cores -> pool2 map [n, P2, P2, 48 | 64] fp32 (P2 = 4 | 10).
 // w1h: conv1 split planes [2][32][64] (k = ky*16 + kx*4 + c), w2h: conv2 [2][C2][288]

@@ -1276,7 +1276,8 @@ __global__ __launch_bounds__(NT) void k_cand_front(const int4* __restrict__ sat,
                                                    const float4* __restrict__ boxes, const int32_t* __restrict__ img,
                                                    const float* __restrict__ w1, const _Float16* __restrict__ w1h,
                                                    const float* __restrict__ b1, const float* __restrict__ a1,
-                                                   float* __restrict__ out, int32_t* __restrict__ err, int dbg) {
+                                                   float* __restrict__ out, int32_t* __restrict__ err, int dbg,
+                                                   int* __restrict__ ovf) {
     constexpr int O = S - 2;                // conv1 output side
     constexpr int P = (O - 3 + 1) / 2 + 1;  // ceil-mode pool output side
     constexpr int BR = 2 * PB + 1;          // conv rows per band
@@ -1439,6 +1440,7 @@ __global__ __launch_bounds__(NT) void k_cand_front(const int4* __restrict__ sat,
         }
         __syncthreads();
         const int npr = min(PB, P - pr0);
+        bool bad = false;
         for (int i = tid; i < ((dbg & 4) ? 0 : npr * P * 32); i += NT) {
             const int c = i & 31, t = i >> 5;
             const int px = t % P, pyl = t / P;
@@ -1458,8 +1460,19 @@ __global__ __launch_bounds__(NT) void k_cand_front(const int4* __restrict__ sat,
 #pragma unroll
                 for (int dx = 0; dx < 3; dx++)
                     if (dy | dx) m = fmaxf(m, cr[yo[dy] + xo[dx]]);
-            o[((pr0 + pyl) * P + px) * 32 + c] = m;
+            if (ovf) {
+                // split-pair layout (gemm_x3.hpp) for the split-mode conv2: 32-B chunks of 8 channels
+                // [x0 x 8 | x1 x 8]; a value beyond the fp16 range raises *ovf
+                const _Float16 h0 = (_Float16)m, h1 = (_Float16)((m - (float)h0) * 2048.f);
+                _Float16* ch = (_Float16*)(o + ((pr0 + pyl) * P + px) * 32 + (c & ~7));
+                ch[c & 7] = h0;
+                ch[8 + (c & 7)] = h1;
+                bad |= !(fabsf(m) < 16384.f);
+            } else {
+                o[((pr0 + pyl) * P + px) * 32 + c] = m;
+            }
         }
+        if (ovf && __ballot(bad) && lane == 0) atomicOr(ovf, 1);
         __syncthreads();
     }
 }
@@ -1468,7 +1481,7 @@ int cand_front_side(bool onet) { return onet ? 23 : 11; }
 
 void launch_cand_front(bool onet, const int4* sat, int H, int W, const float4* boxes, const int32_t* img, int64_t n,
                        const float* w1, const _Float16* w1h, const float* b1, const float* a1, float* out, int32_t* err,
-                       hipStream_t st) {
+                       hipStream_t st, int* ovf) {
     if (n <= 0) return;
     static const int dbg = [] {  // phase-skip mask for profiling (VTF_FRONT_DEBUG): 1 crop, 2 conv1, 4 pool
         const char* e = std::getenv("VTF_FRONT_DEBUG");
@@ -1476,13 +1489,13 @@ void launch_cand_front(bool onet, const int4* sat, int H, int W, const float4* b
     }();
     // w1h (split conv1 planes) selects conv1 on fp16 matrix cores; null keeps the fp32 MFMA path
     if (onet && w1h)
-        k_cand_front<48, 1, 512, true><<<(unsigned)n, 512, 0, st>>>(sat, H, W, boxes, img, w1, w1h, b1, a1, out, err, dbg);
+        k_cand_front<48, 1, 512, true><<<(unsigned)n, 512, 0, st>>>(sat, H, W, boxes, img, w1, w1h, b1, a1, out, err, dbg, ovf);
     else if (onet)
-        k_cand_front<48, 1, 512, false><<<(unsigned)n, 512, 0, st>>>(sat, H, W, boxes, img, w1, w1h, b1, a1, out, err, dbg);
+        k_cand_front<48, 1, 512, false><<<(unsigned)n, 512, 0, st>>>(sat, H, W, boxes, img, w1, w1h, b1, a1, out, err, dbg, ovf);
     else if (w1h)
-        k_cand_front<24, 3, 256, true><<<(unsigned)n, 256, 0, st>>>(sat, H, W, boxes, img, w1, w1h, b1, a1, out, err, dbg);
+        k_cand_front<24, 3, 256, true><<<(unsigned)n, 256, 0, st>>>(sat, H, W, boxes, img, w1, w1h, b1, a1, out, err, dbg, ovf);
     else
-        k_cand_front<24, 3, 256, false><<<(unsigned)n, 256, 0, st>>>(sat, H, W, boxes, img, w1, w1h, b1, a1, out, err, dbg);
+        k_cand_front<24, 3, 256, false><<<(unsigned)n, 256, 0, st>>>(sat, H, W, boxes, img, w1, w1h, b1, a1, out, err, dbg, ovf);
 }
 
 // heads: x [n, D] -> softmax(x W1^T + b1)[:, 1], x W2^T + b2 (4), optional x W3^T + b3 (10).

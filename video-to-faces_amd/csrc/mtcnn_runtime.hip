@@ -10,6 +10,7 @@
 #include "boxes.hpp"
 #include "common.hpp"
 #include "conv.hpp"
+#include "gemm_x3.hpp"
 #include "mtcnn.hpp"
 #include "nms.hpp"
 
@@ -99,6 +100,7 @@ struct Mtcnn {
     struct CL {
         int cin, cout, k;
         const float *w, *b, *a;
+        const void* sp;  // the weights in the split-pair layout (conv_dma split mode), or null
     };
     std::vector<CL> rl, ol;
     const float* fw[2] = {nullptr, nullptr};  // conv1 of RNet / ONet for k_cand_front: [28][32]
@@ -121,6 +123,9 @@ struct Mtcnn {
     // fused RNet / ONet front half (mtcnn_cand.hip); used when the split mode is allowed
     CandFusedW cf[2]{};
     bool fused = false;
+    // RNet / ONet on the LDS-DMA conv kernel's split mode with split-pair activations
+    // (VTF_MTCNN_SP=0: k_conv's staging-split mode)
+    bool sp = true;
     ~Mtcnn() {
         for (void* p : allocs) (void)hipFree(p);
         if (ev0) (void)hipEventDestroy(ev0);
@@ -225,7 +230,17 @@ static void build_weights(Mtcnn& m, const float* params, int64_t n_params) {
             b[co] = raw[wi + 1][co];
             a[co] = raw[wi + 2][co];
         }
-        Mtcnn::CL L{cin_p, cout_p, k, nullptr, nullptr, nullptr};
+        Mtcnn::CL L{cin_p, cout_p, k, nullptr, nullptr, nullptr, nullptr};
+        if (k * k * cin_p % 8 == 0) {
+            std::vector<uint16_t> h((size_t)cout_p * k * k * cin_p * 2);
+            if (split_rows_host(w.data(), cout_p, k * k * cin_p, h.data())) {
+                void* d = nullptr;
+                VTF_HIP(hipMalloc(&d, h.size() * 2));
+                VTF_HIP(hipMemcpy(d, h.data(), h.size() * 2, hipMemcpyHostToDevice));
+                m.allocs.push_back(d);
+                L.sp = d;
+            }
+        }
         float* d = nullptr;
         VTF_HIP(hipMalloc(&d, (w.size() + b.size() + a.size()) * 4));
         VTF_HIP(hipMemcpy(d, w.data(), w.size() * 4, hipMemcpyHostToDevice));
@@ -288,6 +303,8 @@ static void build_weights(Mtcnn& m, const float* params, int64_t n_params) {
         // cannot hide its own barrier / LDS latency
         const char* fz = std::getenv("VTF_MTCNN_FUSED");
         m.fused = fz && fz[0] == '1';
+        const char* spe = std::getenv("VTF_MTCNN_SP");
+        m.sp = !(spe && spe[0] == '0');
         // split fp16 planes of conv1 ([2][32][64], k = ky*16 + kx*4 + c) and conv2 ([2][C2][288],
         // k = tap*32 + ci) for the fused front half
         auto split_to = [&](std::vector<uint16_t>& h, size_t i0, size_t i1, float w) {
@@ -501,6 +518,73 @@ static void run_candidates(Mtcnn& m, bool onet, const float* x0, int64_t n, floa
         launch_heads(cur, n, C, m.rh1w, m.rh1b, m.rh2w, m.rh2b, nullptr, nullptr, prob, reg, nullptr, m.st);
 }
 
+// RNet / ONet after the candidate front end on the LDS-DMA conv kernel's split mode
+// (conv_dma.hip): x0 = k_cand_front's pooled conv1 map [n,P,P,32] in the split-pair layout.  A
+// layer feeding a conv writes split pairs from its epilogue, a layer feeding a pool writes fp32
+// and the pool writes split pairs; every split-pair producer raises d_ovf[0] on an operand
+// beyond the fp16 range (the caller then re-runs the net in fp32).  Same k order and MFMA chains
+// as k_conv's split mode.
+static void run_candidates_sp(Mtcnn& m, bool onet, const void* x0, int64_t n, float4* reg, float* lm, float* prob) {
+    const auto& Ls = onet ? m.ol : m.rl;
+    const int pk[5] = {3, 3, onet ? 2 : 0, 0, 0};
+    const int npool = onet ? 3 : 2;
+    const int S = onet ? 48 : 24;
+    size_t big = (size_t)n * (S - 2) * (S - 2) * 32;
+    float* X = m.ar.get<float>(S_RA, big);
+    float* Y = m.ar.get<float>(S_RB, big);
+    const void* cur = x0;
+    int H = cand_front_side(onet), W = H, C = 32;
+    for (size_t li = 1; li < Ls.size(); li++) {
+        const auto& L = Ls[li];
+        float* out = (cur == (const void*)X) ? Y : X;
+        const bool pool = (int)li < npool;
+        const bool last = li + 1 == Ls.size();
+        ConvParams p{};
+        p.in = cur;
+        p.in_sp = 1;
+        p.w = L.sp;
+        p.out = out;
+        p.bias = L.b;
+        p.prelu = L.a;
+        p.scale = 1.f;
+        p.N = (int)n;
+        p.H = H;
+        p.W = W;
+        p.Cin = C;
+        p.KH = p.KW = L.k;
+        p.sh = p.sw = 1;
+        p.OH = H - L.k + 1;
+        p.OW = W - L.k + 1;
+        p.Cout = L.cout;
+        p.K = L.k * L.k * C;
+        p.M = (int64_t)n * p.OH * p.OW;
+        p.out_cstride = L.cout;
+        p.out_sp = !pool && !last;
+        p.ovf = m.d_ovf;
+        p.split_fp32 = 1;  // slice-order reduction of small grids (parity is a tolerance here)
+        VTF_CHECK(C == L.cin && L.sp, VTF_E_ARG, "candidate net channel mismatch");
+        launch_conv_dma(p, false, m.st);
+        H = p.OH;
+        W = p.OW;
+        C = L.cout;
+        cur = out;
+        if (pool) {
+            float* pout = (out == X) ? Y : X;
+            int OH, OW;
+            launch_maxpool_ks_sp(out, (int)n, H, W, C, pk[li], 2, true, pout, OH, OW, m.d_ovf, m.st);
+            H = OH;
+            W = OW;
+            cur = pout;
+        }
+    }
+    VTF_CHECK(H == 1 && W == 1, VTF_E_ARG, "candidate net shape walk mismatch");
+    const float* f = (const float*)cur;
+    if (onet)
+        launch_heads(f, n, C, m.oh1w, m.oh1b, m.oh2w, m.oh2b, m.oh3w, m.oh3b, prob, reg, lm, m.st);
+    else
+        launch_heads(f, n, C, m.rh1w, m.rh1b, m.rh2w, m.rh2b, nullptr, nullptr, prob, reg, nullptr, m.st);
+}
+
 // stage 2 / 3 nets on the stage's candidates (mtcnn.py:213-216 / 228-230): the fused front half
 // (crop .. pool2 in LDS, split fp16) + the remaining layers batched; on a fused-guard trip
 // (an operand beyond the fp16 range) or without the split mode, the layer-by-layer path.
@@ -524,6 +608,25 @@ static void cand_nets(Mtcnn& m, bool onet, const int4* sat, int H, int W, const 
     const int P = cand_front_side(onet);
     float* x0 = m.ar.get<float>(S_CROP, (size_t)n * P * P * 32);
     const int rl = net;
+    bool sp_ok = m.sp && m.cand_x[net] != 0 && !m.fused;
+    for (size_t li = 1; li < (onet ? m.ol : m.rl).size(); li++) sp_ok = sp_ok && (onet ? m.ol : m.rl)[li].sp;
+    if (sp_ok) {
+        // split-pair path: front end writes split pairs, layers on the LDS-DMA conv kernel
+        VTF_HIP(hipMemsetAsync(m.d_ovf, 0, 4, st));
+        launch_cand_front(onet, sat, H, W, boxes, img, n, m.fw[rl], m.cf[net].w1h, onet ? m.ol[0].b : m.rl[0].b,
+                          onet ? m.ol[0].a : m.rl[0].a, x0, err, st, m.d_ovf);
+        run_candidates_sp(m, onet, x0, n, reg, lm, prob);
+        if (m.cand_x[net] == 1) return;  // operand range proven from the weights
+        int ovf = 0;
+        VTF_HIP(hipMemcpyAsync(&ovf, m.d_ovf, 4, hipMemcpyDeviceToHost, st));
+        VTF_HIP(hipStreamSynchronize(st));
+        if (!ovf) return;
+        VTF_HIP(hipMemsetAsync(err, 0, 4, st));  // the fp32 re-run counts invalid boxes again
+        launch_cand_front(onet, sat, H, W, boxes, img, n, m.fw[rl], nullptr, onet ? m.ol[0].b : m.rl[0].b,
+                          onet ? m.ol[0].a : m.rl[0].a, x0, err, st);
+        run_candidates(m, onet, x0, n, reg, lm, prob, 1, 1);
+        return;
+    }
     // conv1 on split fp16 unless the fp32 paths are forced (crop values lie in [-1, 1]: no range
     // guard needed)
     launch_cand_front(onet, sat, H, W, boxes, img, n, m.fw[rl], m.cand_x[net] != 0 ? m.cf[net].w1h : nullptr,
