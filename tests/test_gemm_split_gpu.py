@@ -57,13 +57,18 @@ def test_gemm_split_refuses_out_of_range():
 
 def test_vit_l_sp_gemm_matches_conv_split_bitwise():
     """ViT-L split mode on pre-split operands vs k_conv's staging-split mode at batch 8 (M = 520
-    token rows: 5 M-tiles, the last partial): identical bits."""
+    token rows: 5 M-tiles, the last partial): identical bits with the same (VALU) attention; the
+    fp32-MFMA attention of the split mode stays within 1e-5 of it."""
     from videotofaces.encoders.vit import ViT
     x = (torch.rand((8, 3, 128, 128), generator=torch.Generator().manual_seed(3)) * 2 - 1).float()
-    new = ViT('cuda:0', isL=True, precision='f16x')(x).cpu().numpy()
-    os.environ['VTF_VIT_GEMM'] = 'conv'
+    mfma = ViT('cuda:0', isL=True, precision='f16x')(x).cpu().numpy()
+    os.environ['VTF_VIT_ATTN'] = 'valu'
     try:
+        new = ViT('cuda:0', isL=True, precision='f16x')(x).cpu().numpy()
+        os.environ['VTF_VIT_GEMM'] = 'conv'
         old = ViT('cuda:0', isL=True, precision='f16x')(x).cpu().numpy()
     finally:
-        del os.environ['VTF_VIT_GEMM']
+        os.environ.pop('VTF_VIT_GEMM', None)
+        del os.environ['VTF_VIT_ATTN']
     np.testing.assert_array_equal(new, old)
+    np.testing.assert_allclose(mfma, new, atol=1e-5, rtol=0)

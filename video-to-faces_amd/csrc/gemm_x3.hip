@@ -40,19 +40,19 @@ typedef __attribute__((ext_vector_type(4))) float f4;
 
 // fused epilogue of one tile from its fp32 LDS image E [BM][BN + 4]: each thread finishes 8
 // consecutive channels of a row (bias, residual, GELU; fp32 or SP stores, 16-byte accesses)
-template <int BM, int BN>
+template <int BM, int BN, int NT = 256>
 __device__ inline void tile_epilogue(const GemmX3Params& p, const float* E, int64_t m0, int n0) {
     constexpr int LDE = BN + 4;
     const int tid = threadIdx.x, lane = tid & 63;
     constexpr int G = BN / 8;
-    static_assert(256 % G == 0, "epilogue groups");
+    static_assert(NT % G == 0, "epilogue groups");
     const int g = tid % G, c0 = n0 + 8 * g;
     if (c0 >= p.N) return;
     float b8[8];
 #pragma unroll
     for (int e = 0; e < 8; e++) b8[e] = p.bias ? p.bias[c0 + e] : 0.f;
     bool bad = false;
-    for (int r = tid / G; r < BM; r += 256 / G) {
+    for (int r = tid / G; r < BM; r += NT / G) {
         const int64_t m = m0 + r;
         if (m >= p.M) break;
         const f4 lo = *(const f4*)(E + r * LDE + 8 * g), hi = *(const f4*)(E + r * LDE + 8 * g + 4);
@@ -84,15 +84,19 @@ __device__ inline void tile_epilogue(const GemmX3Params& p, const float* E, int6
     if (p.ovf && __ballot(bad) && lane == 0) atomicOr(p.ovf, 1);
 }
 
-template <int BM, int BN>
-__global__ __launch_bounds__(256, 2) void k_gemm_x3(GemmX3Params p) {
+// NW waves as (NW / 2) x 2, each a 64 x 64 output block (4 x 4 fragments); the epilogue stages
+// 128 rows at a time through the stage memory
+template <int BM, int BN, int NW>
+__global__ __launch_bounds__(64 * NW, 8 / NW) void k_gemm_x3(GemmX3Params p) {
+    constexpr int NT = 64 * NW;
     constexpr int RB = 128;  // LDS bytes per row and k-step
     constexpr int A_ST = BM * RB, ST = (BM + BN) * RB;
     constexpr int LDE = BN + 4;
-    constexpr int SM = 2 * ST > BM * LDE * 4 ? 2 * ST : BM * LDE * 4;
-    constexpr int WM = BM / 2, WN = BN / 2, FM = WM / 16, FN = WN / 16;
-    constexpr int PA = BM / 32, PB = BN / 32;  // 1-KB DMA pieces per wave and stage
-    static_assert(BM % 32 == 0 && BN % 32 == 0, "tile");
+    constexpr int ER = 128;  // epilogue rows per pass
+    constexpr int SM = 2 * ST > ER * LDE * 4 ? 2 * ST : ER * LDE * 4;
+    constexpr int WM = BM / (NW / 2), WN = BN / 2, FM = WM / 16, FN = WN / 16;
+    constexpr int PA = BM / (8 * NW), PB = BN / (8 * NW);  // 1-KB DMA pieces per wave and stage
+    static_assert(BM % (8 * NW) == 0 && BN % (8 * NW) == 0 && WM == 64 && WN == 64 && BM % ER == 0, "tile");
     __shared__ __attribute__((aligned(16))) char smem[SM];
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -119,8 +123,8 @@ __global__ __launch_bounds__(256, 2) void k_gemm_x3(GemmX3Params p) {
     const int64_t m0 = (int64_t)tile_m * BM;
     const int n0 = tile_n * BN;
 
-    // DMA sources: piece j of this wave = rows 32 j + 8 wave .. +7; the lane's LDS slot lane & 7
-    // of row 32 j + 8 wave + (lane >> 3) takes source slot (lane & 7) ^ h, h = (row >> 1) & 7
+    // DMA sources: piece j of this wave = rows 8 (wave + NW j) .. +7; the lane's LDS slot lane & 7
+    // of row 8 (wave + NW j) + (lane >> 3) takes source slot (lane & 7) ^ h, h = (row >> 1) & 7
     const int src = (lane & 7) ^ (((lane >> 4) + 4 * (wave & 1)) & 7);
     const int soff = (src & 3) * 32 + (src >> 2) * 16;
     const int64_t rowb = (int64_t)p.K * 4;
@@ -128,12 +132,12 @@ __global__ __launch_bounds__(256, 2) void k_gemm_x3(GemmX3Params p) {
     const char* gb[PB];
 #pragma unroll
     for (int j = 0; j < PA; j++) {
-        const int64_t m = min(m0 + 32 * j + 8 * wave + (lane >> 3), p.M - 1);
+        const int64_t m = min(m0 + 8 * (wave + NW * j) + (lane >> 3), p.M - 1);
         ga[j] = (const char*)p.a + m * rowb + soff;
     }
 #pragma unroll
     for (int j = 0; j < PB; j++) {
-        const int64_t n = min(n0 + 32 * j + 8 * wave + (lane >> 3), p.N - 1);
+        const int64_t n = min(n0 + 8 * (wave + NW * j) + (lane >> 3), p.N - 1);
         gb[j] = (const char*)p.b + n * rowb + soff;
     }
     auto issue = [&](int kt, int s) {
@@ -142,12 +146,12 @@ __global__ __launch_bounds__(256, 2) void k_gemm_x3(GemmX3Params p) {
 #pragma unroll
         for (int j = 0; j < PA; j++)
             __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)(ga[j] + kb),
-                                             (void __attribute__((address_space(3)))*)(base + (wave + 4 * j) * 1024), 16,
+                                             (void __attribute__((address_space(3)))*)(base + (wave + NW * j) * 1024), 16,
                                              0, 0);
 #pragma unroll
         for (int j = 0; j < PB; j++)
             __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)(gb[j] + kb),
-                                             (void __attribute__((address_space(3)))*)(base + A_ST + (wave + 4 * j) * 1024),
+                                             (void __attribute__((address_space(3)))*)(base + A_ST + (wave + NW * j) * 1024),
                                              16, 0, 0);
     };
 
@@ -210,28 +214,34 @@ __global__ __launch_bounds__(256, 2) void k_gemm_x3(GemmX3Params p) {
     }
     float* E = (float*)smem;
 #pragma unroll
-    for (int j = 0; j < FN; j++)
+    for (int ph = 0; ph < BM / ER; ph++) {
+        if (ph) __syncthreads();  // the previous pass's rows are finished
+        if (wm * WM / ER == ph) {
 #pragma unroll
-        for (int i = 0; i < FM; i++) {
-            const f4 v = acc[i][j] + accx[i][j] * 0.00048828125f;
+            for (int j = 0; j < FN; j++)
 #pragma unroll
-            for (int q = 0; q < 4; q++)
-                E[(wm * WM + i * 16 + 4 * (lane >> 4) + q) * LDE + wn * WN + j * 16 + (lane & 15)] = v[q];
+                for (int i = 0; i < FM; i++) {
+                    const f4 v = acc[i][j] + accx[i][j] * 0.00048828125f;
+#pragma unroll
+                    for (int q = 0; q < 4; q++)
+                        E[(wm * WM - ph * ER + i * 16 + 4 * (lane >> 4) + q) * LDE + wn * WN + j * 16 + (lane & 15)] = v[q];
+                }
         }
-    __syncthreads();
-    tile_epilogue<BM, BN>(p, E, m0, n0);
+        __syncthreads();
+        tile_epilogue<ER, BN, NT>(p, E, m0 + ph * ER, n0);
+    }
 }
 
 // tail tiles: 8 workgroups per tile, each sums the K slices of one 16-row block (the 8 fragments
 // with that wm, i: 2 f4 per thread) in slice order (deterministic) into an LDS image of the
 // block, then the shared epilogue over those 16 rows
-template <int BM, int BN>
+template <int BM, int BN, int NW>
 __global__ __launch_bounds__(256) void k_gemm_x3_tail(GemmX3Params p) {
-    constexpr int LDE = BN + 4, WM = BM / 2, WN = BN / 2, FM = WM / 16, FN = WN / 16;
-    static_assert(BM == 128 && BN == 128, "tail reduce layout: 16-row blocks of 2 waves x 4 fragments");
+    constexpr int LDE = BN + 4, WM = 64, WN = BN / 2, FM = WM / 16, FN = WN / 16, NB = BM / 16;
+    static_assert(BN == 128, "tail reduce layout: 16-row blocks of 2 waves x 4 fragments");
     __shared__ __attribute__((aligned(16))) float E[16 * LDE];
     const int tid = threadIdx.x;
-    const int tt = blockIdx.x >> 3, part = blockIdx.x & 7, wm = part >> 2, i = part & 3;
+    const int tt = blockIdx.x / NB, part = blockIdx.x % NB, wm = part / FM, i = part % FM;
     const int t = p.dp_tiles + tt;
     const int gm = p.group_m > 0 ? p.group_m : p.gx;
     const int span = gm * p.gy, first = (t / span) * gm, gsz = min(p.gx - first, gm);
@@ -315,6 +325,20 @@ int device_cu_count() {
 
 }  // namespace
 
+template <int BM, int BN, int NW>
+void launch_t(GemmX3Params p, hipStream_t st);
+
+// 256 x 128 tiles of 8 waves for large M: a third less operand traffic per FLOP than 128 x 128,
+// but one workgroup per CU whose 8 waves share every barrier -- measured slower on ViT-L c4
+// (6.3-6.5k vs 6.8k faces/s, profiles/r02o_*), so opt-in (VTF_GEMM_BIG=1)
+static bool big_tiles() {
+    static bool on = [] {
+        const char* e = std::getenv("VTF_GEMM_BIG");
+        return e && std::atoi(e) == 1;
+    }();
+    return on;
+}
+
 void launch_gemm_x3(const GemmX3Params& p0, hipStream_t st) {
     if (p0.M <= 0) return;
     VTF_CHECK(p0.K > 0 && p0.K % 32 == 0 && p0.N > 0 && p0.N % 8 == 0, VTF_E_ARG, "gemm_x3: K % 32, N % 8");
@@ -322,7 +346,12 @@ void launch_gemm_x3(const GemmX3Params& p0, hipStream_t st) {
     VTF_CHECK(!p0.res || (p0.ldr >= p0.N && p0.ldr % 4 == 0), VTF_E_ARG, "gemm_x3: residual stride");
     GemmX3Params p = p0;
     p.group_m = gemm_group_m();
-    constexpr int BM = 128, BN = 128;
+    if (p.M >= 4096 && big_tiles()) launch_t<256, 128, 8>(p, st);
+    else launch_t<128, 128, 4>(p, st);
+}
+
+template <int BM, int BN, int NW>
+void launch_t(GemmX3Params p, hipStream_t st) {
     p.gx = (int)cdiv(p.M, BM);
     p.gy = (int)cdiv(p.N, BN);
     const int T = p.gx * p.gy, KT = p.K / 32;
@@ -330,7 +359,7 @@ void launch_gemm_x3(const GemmX3Params& p0, hipStream_t st) {
     // few tiles (M = 8320 token rows x N = 1024: 520 tiles on 512 slots) would run them on an
     // otherwise idle chip, so those tiles are split along K instead (>= 4 k-steps per slice)
     // and spread over the free slots.
-    const int slots = 2 * device_cu_count();
+    const int slots = (8 / NW) * device_cu_count();
     p.dp_tiles = T;
     p.tail_split = 1;
     if (gemm_tail_on() && T > slots) {
@@ -343,8 +372,8 @@ void launch_gemm_x3(const GemmX3Params& p0, hipStream_t st) {
         }
     }
     const int64_t grid = (int64_t)p.dp_tiles + (int64_t)(T - p.dp_tiles) * p.tail_split;
-    k_gemm_x3<BM, BN><<<(unsigned)grid, 256, 0, st>>>(p);
-    if (p.dp_tiles < T) k_gemm_x3_tail<BM, BN><<<(unsigned)(T - p.dp_tiles) * 8, 256, 0, st>>>(p);
+    k_gemm_x3<BM, BN, NW><<<(unsigned)grid, 64 * NW, 0, st>>>(p);
+    if (p.dp_tiles < T) k_gemm_x3_tail<BM, BN, NW><<<(unsigned)(T - p.dp_tiles) * (BM / 16), 256, 0, st>>>(p);
 }
 
 void launch_split_rows(const float* x, int64_t rows, int K, int64_t ld, void* out, int* ovf, hipStream_t st) {

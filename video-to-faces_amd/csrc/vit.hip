@@ -200,6 +200,111 @@ __global__ __launch_bounds__(256) void k_vit_attention(const float* __restrict__
     }
 }
 
+// The same attention on the fp32 matrix cores (v_mfma_f32_16x16x4_f32: exact fp32 products,
+// fp32 accumulation in the MFMA's order), used by the split-fp16 mode: q k^T as 5 x 5 blocks
+// of 16 x 16 over d = 0..63 (rows 65..79 zero), the row softmax exactly as k_vit_attention, and
+// P V as 5 x 4 blocks over c = 0..79 (P columns 65..79 zeroed).  LDS: Q | K (reused for the
+// scores, then for the output tile) and V: 65 KB, two workgroups per CU.
+constexpr int AP = 80;        // tokens padded to 5 x 16
+constexpr int AQ = VHD + 4;   // Q / K / V / O row stride (floats)
+constexpr int AS = AP + 4;    // score row stride
+template <bool SP>
+__global__ __launch_bounds__(256, 2) void k_vit_attention_mfma(const float* __restrict__ qkv, int64_t N, int D, int heads,
+                                                               float* __restrict__ out, int* __restrict__ ovf) {
+    typedef __attribute__((ext_vector_type(4))) float f4;
+    __shared__ __attribute__((aligned(16))) float sm[2 * AP * AQ + AP * AQ];
+    float* Q = sm;
+    float* K = sm + AP * AQ;
+    float* V = sm + 2 * AP * AQ;
+    float* S = sm;  // scores / probabilities [AP][AS] over Q | K once q k^T is in registers
+    const int64_t n = blockIdx.x / heads;
+    const int h = blockIdx.x % heads;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, lr = lane & 15, lk = lane >> 4;
+    const float* base = qkv + n * VT * 3 * D + h * VHD;
+    for (int i = tid; i < AP * VHD / 4; i += 256) {
+        const int t = i / (VHD / 4), d = 4 * (i % (VHD / 4));
+        f4 q = {0.f, 0.f, 0.f, 0.f}, k = q, v = q;
+        if (t < VT) {
+            const float* row = base + (int64_t)t * 3 * D + d;
+            q = *(const f4*)row;
+            k = *(const f4*)(row + D);
+            v = *(const f4*)(row + 2 * D);
+        }
+        *(f4*)(Q + t * AQ + d) = q;
+        *(f4*)(K + t * AQ + d) = k;
+        *(f4*)(V + t * AQ + d) = v;
+    }
+    __syncthreads();
+    // scores: 25 blocks, wave w takes blocks w, w + 4, ...
+    f4 sc[7];
+#pragma unroll
+    for (int u = 0; u < 7; u++) {
+        const int b = wave + 4 * u;
+        sc[u] = f4{0.f, 0.f, 0.f, 0.f};
+        if (b < 25) {
+            const float* qa = Q + ((b / 5) * 16 + lr) * AQ + lk;
+            const float* kb = K + ((b % 5) * 16 + lr) * AQ + lk;
+#pragma unroll
+            for (int ks = 0; ks < VHD; ks += 4) sc[u] = __builtin_amdgcn_mfma_f32_16x16x4f32(qa[ks], kb[ks], sc[u], 0, 0, 0);
+        }
+    }
+    __syncthreads();  // Q and K are dead: the scores go over them
+#pragma unroll
+    for (int u = 0; u < 7; u++) {
+        const int b = wave + 4 * u;
+        if (b < 25)
+#pragma unroll
+            for (int i = 0; i < 4; i++) S[((b / 5) * 16 + 4 * lk + i) * AS + (b % 5) * 16 + lr] = sc[u][i] * 0.125f;
+    }
+    __syncthreads();
+    // row softmax over the 65 scores (as k_vit_attention); P columns 65..79 zeroed
+    for (int a = wave; a < VT; a += 4) {
+        float v0 = S[a * AS + lane];
+        float v1 = lane == 0 ? S[a * AS + 64] : -INFINITY;
+        float m = fmaxf(v0, v1);
+        for (int off = 32; off > 0; off >>= 1) m = fmaxf(m, __shfl_xor(m, off));
+        float e0 = expf(v0 - m), e1 = lane == 0 ? expf(v1 - m) : 0.f;
+        float s = e0 + e1;
+        for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off);
+        float inv = 1.0f / s;
+        S[a * AS + lane] = e0 * inv;
+        if (lane == 0) S[a * AS + 64] = e1 * inv;
+        if (lane < AP - VT) S[a * AS + VT + lane] = 0.f;
+    }
+    __syncthreads();
+    // out = P V: 20 blocks (5 row x 4 feature blocks), wave w takes blocks w, w + 4, ...
+    f4 oc[5];
+#pragma unroll
+    for (int u = 0; u < 5; u++) {
+        const int b = wave + 4 * u;
+        oc[u] = f4{0.f, 0.f, 0.f, 0.f};
+        const float* pa = S + ((b >> 2) * 16 + lr) * AS + lk;
+        const float* vb = V + lk * AQ + (b & 3) * 16 + lr;
+#pragma unroll
+        for (int ks = 0; ks < AP; ks += 4) oc[u] = __builtin_amdgcn_mfma_f32_16x16x4f32(pa[ks], vb[ks * AQ], oc[u], 0, 0, 0);
+    }
+    __syncthreads();  // P is dead: the output tile goes over it
+    float* O = sm;
+#pragma unroll
+    for (int u = 0; u < 5; u++) {
+        const int b = wave + 4 * u;
+#pragma unroll
+        for (int i = 0; i < 4; i++) O[((b >> 2) * 16 + 4 * lk + i) * AQ + (b & 3) * 16 + lr] = oc[u][i];
+    }
+    __syncthreads();
+    bool bad = false;
+    for (int i = tid; i < VT * VHD / 4; i += 256) {
+        const int t = i / (VHD / 4), d = 4 * (i % (VHD / 4));
+        const f4 o = *(const f4*)(O + t * AQ + d);
+        if constexpr (SP)
+            sp_store4((char*)out + (n * VT + t) * (int64_t)D * 4, h * VHD + d, o[0], o[1], o[2], o[3], bad);
+        else
+            *(f4*)(out + (n * VT + t) * (int64_t)D + h * VHD + d) = o;
+    }
+    if constexpr (SP)
+        if (__ballot(bad) && lane == 0) atomicOr(ovf, 1);
+}
+
 struct Lin {
     const float *w, *b;  // [out][in], [out]
     int in, out;
@@ -214,6 +319,8 @@ struct Vit {
     // split mode on pre-split operands (gemm_x3.hip) when every weight is inside the fp16 range;
     // VTF_VIT_GEMM=conv keeps k_conv's staging-split mode (A/B timing, bit-identical results)
     bool sp_ok = false;
+    // split mode: attention on the fp32 matrix cores (VTF_VIT_ATTN=valu: the VALU kernel)
+    bool attn_mfma = true;
     int* d_ovf = nullptr;
     hipStream_t st = 0;
     const float *cls = nullptr, *pos = nullptr, *pw = nullptr, *pb = nullptr;  // patch conv [D][16][16][8]
@@ -288,6 +395,8 @@ static void vit_build(Vit& V, const float* params, int64_t n_params) {
         { auto w2 = take((int64_t)4 * D * D); auto b2 = take(D); B.fc2 = Lin{V.up(w2), V.up(b2), 4 * D, D, V.up_sp(w2, D, 4 * D)}; }
         V.blocks.push_back(B);
     }
+    const char* ae = std::getenv("VTF_VIT_ATTN");
+    V.attn_mfma = !(ae && std::string(ae) == "valu");
     const char* ge = std::getenv("VTF_VIT_GEMM");
     V.sp_ok = !(ge && std::string(ge) == "conv");
     for (const auto& B : V.blocks) V.sp_ok = V.sp_ok && B.qkv.sp && B.proj.sp && B.fc1.sp && B.fc2.sp;
@@ -377,7 +486,10 @@ static void vit_forward(Vit& V, const float* x_nhwc8, int64_t N, float* emb) {
         for (const auto& B : V.blocks) {
             k_layernorm<true><<<lg, 256, 0, V.st>>>(X, M, D, D, B.n1w, B.n1b, 1e-12f, Hn, D, V.d_ovf);
             linear_sp(V, B.qkv, Hn, M, QKV, false, nullptr, false);
-            k_vit_attention<true><<<(unsigned)(N * V.heads), 256, 0, V.st>>>(QKV, N, D, V.heads, A, V.d_ovf);
+            if (V.attn_mfma)
+                k_vit_attention_mfma<true><<<(unsigned)(N * V.heads), 256, 0, V.st>>>(QKV, N, D, V.heads, A, V.d_ovf);
+            else
+                k_vit_attention<true><<<(unsigned)(N * V.heads), 256, 0, V.st>>>(QKV, N, D, V.heads, A, V.d_ovf);
             linear_sp(V, B.proj, A, M, Hn, false, X, false);  // x + proj(attn)
             std::swap(X, Hn);
             k_layernorm<true><<<lg, 256, 0, V.st>>>(X, M, D, D, B.n2w, B.n2b, 1e-12f, A, D, V.d_ovf);
