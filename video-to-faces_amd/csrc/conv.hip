@@ -539,7 +539,7 @@ void launch_conv(const ConvParams& p, bool bf16, hipStream_t st) {
         const char* e = std::getenv("VTF_CONV_DMA");
         return !(e && std::atoi(e) == 0);
     }();
-    if (bf16 && dma && conv_dma_prefer_bf16(p)) {
+    if (bf16 && dma && conv_dma_choice_bf16(p) != 0) {
         launch_conv_dma(p, true, st);
         return;
     }

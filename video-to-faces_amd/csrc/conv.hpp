@@ -55,7 +55,8 @@ struct ConvParams {
 void launch_conv(const ConvParams& p, bool bf16, hipStream_t st);
 // LDS-DMA implicit-GEMM conv (conv_dma.hip): bf16 operands, or split-pair operands (in_sp, fp32-grade)
 bool conv_dma_ok(const ConvParams& p);
-bool conv_dma_prefer_bf16(const ConvParams& p);  // bf16 shapes where conv_dma beats k_conv
+// bf16 layer -> 0 k_conv, 1 conv_dma large tiles, 2 conv_dma 64 x 64 3-stage tiles (measured per shape)
+int conv_dma_choice_bf16(const ConvParams& p);
 void launch_conv_dma(const ConvParams& p, bool bf16, hipStream_t st);
 void launch_maxpool(const void* in, int N, int H, int W, int C, void* out, int out_cstride, int out_coff, bool bf16,
                     hipStream_t st);

@@ -41,11 +41,12 @@ namespace {
 typedef __attribute__((ext_vector_type(8))) _Float16 h8;
 typedef __attribute__((ext_vector_type(4))) float f4;
 
-template <int MODE, int BM, int BN, int WGM, int OCC = 2>
+template <int MODE, int BM, int BN, int WGM, int OCC = 2, int NSTG = 2>
 struct DCfg {
+    static constexpr int NS = NSTG;  // LDS stages: NS - 1 k-steps in flight ahead of the MFMAs
     static constexpr int WGN = 4 / WGM, WM = BM / WGM, WN = BN / WGN, FM = WM / 16, FN = WN / 16;
     static constexpr int RB = 128, A_ST = BM * RB, ST = (BM + BN) * RB, LDE = BN + 4;
-    static constexpr int SM = 2 * ST > BM * LDE * 4 ? 2 * ST : BM * LDE * 4;
+    static constexpr int SM = NS * ST > BM * LDE * 4 ? NS * ST : BM * LDE * 4;
     static constexpr int PA = BM / 32, PB = BN / 32;  // 1-KB DMA pieces per wave and stage
     static constexpr int CPS = MODE == 1 ? 4 : 8;     // 8-element chunks per k-step
     static constexpr int EB = MODE == 1 ? 4 : 2;      // global bytes per element
@@ -101,9 +102,15 @@ __device__ inline void dma_epilogue(const ConvParams& p, const float* E, int row
     if (p.out_sp && p.ovf && __ballot(bad) && (threadIdx.x & 63) == 0) atomicOr(p.ovf, 1);
 }
 
-template <int MODE, int BM, int BN, int WGM, int OCC>
+// s_waitcnt vmcnt(N) then the workgroup barrier (LDS reads stay after it)
+template <int N>
+__device__ inline void wait_vm_barrier() {
+    asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(N) : "memory");
+}
+
+template <int MODE, int BM, int BN, int WGM, int OCC, int NSTG>
 __global__ __launch_bounds__(256, OCC) void k_conv_dma(ConvParams p) {
-    using C = DCfg<MODE, BM, BN, WGM, OCC>;
+    using C = DCfg<MODE, BM, BN, WGM, OCC, NSTG>;
     using T = typename std::conditional<MODE == 0, __bf16, float>::type;
     constexpr int PA = C::PA, PB = C::PB, FM = C::FM, FN = C::FN, RB = C::RB;
     __shared__ __attribute__((aligned(16))) char smem[C::SM];
@@ -212,15 +219,33 @@ __global__ __launch_bounds__(256, OCC) void k_conv_dma(ConvParams p) {
     const int o0 = (lane & 15) * RB + (((lane >> 4) ^ hsw) << 4);
     const int o1 = (lane & 15) * RB + (((4 + (lane >> 4)) ^ hsw) << 4);
 
-    issue(0);
+    constexpr int NS = C::NS, PPS = PA + PB;  // DMA instructions per wave and stage
+    static_assert(NS >= 2 && NS <= 4, "stages");
+    // prologue: steps kt0 .. kt0 + NS - 2 in flight
+    int issued = kt0;
+#pragma unroll
+    for (int s = 0; s < NS - 1; s++)
+        if (issued < kt1) {
+            if (s) advance();
+            issue(s);
+            issued++;
+        }
     for (int kt = kt0; kt < kt1; kt++) {
-        // this wave's pieces of step kt have landed; after the barrier every wave's have, and every
-        // wave is done reading the other stage
-        asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
-        const int sb = (kt - kt0) & 1;
-        if (kt + 1 < kt1) {
+        // this wave's pieces of step kt have landed (the steps issued after it may still be in
+        // flight: counted vmcnt); after the barrier every wave's have, and every wave is done
+        // reading the stage the next DMA overwrites (step kt - 1's)
+        const int ahead = issued - kt - 1;
+        if (NS >= 4 && ahead >= 2)
+            wait_vm_barrier<(NS >= 4 ? 2 * PPS : 0)>();
+        else if (NS >= 3 && ahead >= 1)
+            wait_vm_barrier<(NS >= 3 ? PPS : 0)>();
+        else
+            wait_vm_barrier<0>();
+        const int sb = (kt - kt0) % NS;
+        if (issued < kt1) {
             advance();
-            issue(sb ^ 1);
+            issue((issued - kt0) % NS);
+            issued++;
         }
         const char* As = smem + sb * C::ST + wm * C::WM * RB;
         const char* Bs = smem + sb * C::ST + C::A_ST + wn * C::WN * RB;
@@ -291,9 +316,9 @@ __global__ __launch_bounds__(256, OCC) void k_conv_dma(ConvParams p) {
 
 // tail tiles: one workgroup per (tile, 16-row block) sums the block's K slices in slice order
 // (deterministic) into an LDS image, then the epilogue of those 16 rows
-template <int MODE, int BM, int BN, int WGM, int OCC>
+template <int MODE, int BM, int BN, int WGM, int OCC, int NSTG>
 __global__ __launch_bounds__(256) void k_conv_dma_tail(ConvParams p) {
-    using C = DCfg<MODE, BM, BN, WGM, OCC>;
+    using C = DCfg<MODE, BM, BN, WGM, OCC, NSTG>;
     using T = typename std::conditional<MODE == 0, __bf16, float>::type;
     constexpr int NB = BM / 16, FM = C::FM, FN = C::FN, LDE = C::LDE;
     __shared__ __attribute__((aligned(16))) float E[16 * LDE];
@@ -363,9 +388,9 @@ int dma_group_m() {
     return g;
 }
 
-template <int MODE, int BM, int BN, int WGM, int OCC = 2>
+template <int MODE, int BM, int BN, int WGM, int OCC = 2, int NSTG = 2>
 void launch_dma_t(ConvParams p, hipStream_t st) {
-    using C = DCfg<MODE, BM, BN, WGM, OCC>;
+    using C = DCfg<MODE, BM, BN, WGM, OCC, NSTG>;
     p.gx = (int)cdiv(p.M, BM);
     p.gy = (int)cdiv(p.Cout, BN);
     p.group_m = dma_group_m();
@@ -395,8 +420,8 @@ void launch_dma_t(ConvParams p, hipStream_t st) {
     }
     const int nt = T - p.dp_tiles;
     p.ws = nt ? dma_ws(st, (size_t)nt * p.tail_split * BM * BN * 4) : nullptr;
-    k_conv_dma<MODE, BM, BN, WGM, OCC><<<(unsigned)(p.dp_tiles + nt * p.tail_split), 256, 0, st>>>(p);
-    if (nt) k_conv_dma_tail<MODE, BM, BN, WGM, OCC><<<(unsigned)(nt * (BM / 16)), 256, 0, st>>>(p);
+    k_conv_dma<MODE, BM, BN, WGM, OCC, NSTG><<<(unsigned)(p.dp_tiles + nt * p.tail_split), 256, 0, st>>>(p);
+    if (nt) k_conv_dma_tail<MODE, BM, BN, WGM, OCC, NSTG><<<(unsigned)(nt * (BM / 16)), 256, 0, st>>>(p);
 }
 
 }  // namespace
@@ -408,13 +433,23 @@ bool conv_dma_ok(const ConvParams& p) {
            (!p.n_split || (p.n_split % 8 == 0 && p.out2_cstride % 8 == 0 && p.out2_coff % 8 == 0));
 }
 
-bool conv_dma_prefer_bf16(const ConvParams& p) {
-    // measured on FaceNet (batch 128, profiles/r02n_*): the DMA kernel wins on grids of at least
-    // one whole round of 64+-channel tiles (stem 3x3 convs, Mixed_6a), k_conv's small tiles win on
-    // the small Block35/17/8 grids and on 32-channel outputs
-    if (!conv_dma_ok(p) || p.Cout <= 32) return false;
+int conv_dma_choice_bf16(const ConvParams& p) {
+    // per-layer A/B on FaceNet (batch 128, profiles/r02o_facenet_layers_*): k_conv's small
+    // register-staged tiles win on 32-channel outputs and on K < 256 (1-4 k-steps); the 2-stage
+    // 128 x 128 / 256 x 64 DMA tiles on grids of at least one whole round; the 3-stage 64 x 64 DMA
+    // tiles on 1x1 and strided convs and on the 3x3-spatial Block8 maps (M <= 2048); k_conv keeps
+    // the padded 1x7 / 7x1 / 3x3 convs of the small maps
+    static const int force = [] {
+        const char* e = std::getenv("VTF_DMA_BF16");  // -1 auto, 0 k_conv, 1 large tiles, 2 small tiles
+        return e ? std::atoi(e) : -1;
+    }();
+    if (!conv_dma_ok(p)) return 0;
+    if (force >= 0) return force;
+    if (p.Cout <= 32 || p.K < 256) return 0;
     const int bm = p.Cout <= 64 ? 256 : 128, bn = p.Cout <= 64 ? 64 : 128;
-    return cdiv(p.M, bm) * cdiv(p.Cout, bn) >= 2 * cu_count();
+    if (cdiv(p.M, bm) * cdiv(p.Cout, bn) >= 2 * cu_count()) return 1;
+    if (p.KH * p.KW == 1 || p.M <= 2048 || p.sh > 1 || p.sw > 1) return 2;
+    return 0;
 }
 
 void launch_conv_dma(const ConvParams& p, bool bf16, hipStream_t st) {
@@ -423,6 +458,12 @@ void launch_conv_dma(const ConvParams& p, bool bf16, hipStream_t st) {
     VTF_CHECK(bf16 || p.in_sp, VTF_E_ARG, "conv_dma: bf16 or split-pair operands");
     VTF_CHECK(!p.out_sp || !bf16, VTF_E_ARG, "conv_dma: split-pair output is an fp32-mode output");
     if (bf16) {
+        // grids below a whole round of large tiles (FaceNet Block35 / 17 / 8): 64 x 64 tiles, three
+        // stages (two k-steps in flight) at 3 workgroups per CU
+        if (conv_dma_choice_bf16(p) == 2) {
+            launch_dma_t<0, 64, 64, 2, 3, 3>(p, st);
+            return;
+        }
         if (p.Cout <= 32)
             launch_dma_t<0, 256, 32, 4>(p, st);
         else if (p.Cout <= 64)
