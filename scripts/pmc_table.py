@@ -24,7 +24,8 @@ def load(d):
     acc = defaultdict(lambda: defaultdict(float))
     calls = defaultdict(set)
     for r in csv.DictReader(open(f[0])):
-        name = re.sub(r'\(.*', '', r['Kernel_Name'])
+        name = re.sub(r'\(anonymous namespace\)::', '', r['Kernel_Name'])
+        name = re.sub(r'\(.*', '', name)
         name = re.sub(r'^void ', '', name)
         acc[name][r['Counter_Name']] += float(r['Counter_Value'])
         calls[name].add(r.get('Dispatch_Id') or r.get('Correlation_Id'))
@@ -39,7 +40,7 @@ def durations(d):
     c = sqlite3.connect(f[0])
     out = {}
     for n, k, s in c.execute('select name, count(*), sum(duration) from kernels group by name'):
-        n = re.sub(r'^void ', '', re.sub(r'\(.*', '', n))
+        n = re.sub(r'^void ', '', re.sub(r'\(.*', '', re.sub(r'\(anonymous namespace\)::', '', n)))
         out[n] = (k, s / 1e3)
     return out
 

@@ -480,6 +480,10 @@ void launch_conv_dma(const ConvParams& p, bool bf16, hipStream_t st) {
         }();
         if (p.Cout <= 64 && big == 256)
             launch_dma_t<1, 256, 64, 4>(p, st);
+        else if (p.Cout <= 64 && big == 64)
+            launch_dma_t<1, 64, 64, 2, 3, 3>(p, st);
+        else if (p.Cout <= 64 && big == 129)
+            launch_dma_t<1, 128, 64, 2, 2, 3>(p, st);
         else if (p.Cout <= 64)
             launch_dma_t<1, 128, 64, 2, 3>(p, st);
         else

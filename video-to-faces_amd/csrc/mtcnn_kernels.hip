@@ -132,7 +132,11 @@ __global__ __launch_bounds__(SAT_COLS * SAT_MAXG) void k_sat_cols(int H, int W, 
     const int per = (H + G - 1) / G;
     const int ys = 1 + g * per, ye = min(H + 1, ys + per);
     int4* col = sat + (int64_t)b * (H + 1) * W1 + min(x, W1 - 1);
-    __shared__ int4 tot[SAT_MAXG][SAT_COLS];
+    // [G][SAT_COLS] group totals, sized by the launch (7.7 KB at 720p): small enough to co-reside
+    // with another lane's persistent k_pnet (3 x 49 KB of the CU's 160 KB), so a det-batch's SAT
+    // does not wait for the other lanes' pyramid kernels to drain
+    extern __shared__ int4 tot_s[];
+    int4 (*tot)[SAT_COLS] = (int4 (*)[SAT_COLS])tot_s;
     int4 v[SAT_PER];
     int4 acc = make_int4(0, 0, 0, 0);
 #pragma unroll
@@ -164,7 +168,7 @@ void launch_sat(const uint8_t* frames, int64_t frame_stride, int64_t row_stride,
     k_sat_rows<<<(unsigned)((int64_t)B * H), 256, 0, st>>>(frames, frame_stride, row_stride, H, W, sat);
     const int G = (H + SAT_PER - 1) / SAT_PER;
     VTF_CHECK(G <= SAT_MAXG, VTF_E_LIMIT, "mtcnn: frames taller than 1536 rows");
-    k_sat_cols<<<(unsigned)(B * ((W + SAT_COLS) / SAT_COLS)), SAT_COLS * G, 0, st>>>(H, W, sat);
+    k_sat_cols<<<(unsigned)(B * ((W + SAT_COLS) / SAT_COLS)), SAT_COLS * G, (size_t)G * SAT_COLS * sizeof(int4), st>>>(H, W, sat);
 }
 
 // MTCNN._resample of the preprocessed frames (mtcnn.py:133-139, 150-151) from the SAT:
