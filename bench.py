@@ -46,16 +46,19 @@ FP32_PEAK_TFLOPS = 157.3  # MI355X dense fp32 (f32 MFMA), MI355X_MICROARCH.md
 BF16_PEAK_TFLOPS = 2500.0  # MI355X dense bf16 MFMA (no sparsity), MI355X_MICROARCH.md
 # split-fp16 operands (x0 w0 + 2^-11 (x0 w1 + x1 w0)): three fp16 products per fp32-grade product
 F16X_PEAK_TFLOPS = round(BF16_PEAK_TFLOPS / 3, 1)
+# bf16x3 operands (three bf16 terms each): six bf16 products per fp32-grade product
+X3_PEAK_TFLOPS = round(BF16_PEAK_TFLOPS / 6, 1)
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E (MI355X_MICROARCH.md)
 LBL_BYTES_PER_FLOP = 2075e6 / 38.66e9  # PNet layer-by-layer fp32 bytes per FLOP
 VIT_GFLOP = {'vit_b': 11.27, 'vit_l': 39.78}  # per face at 128x128
 ENC_NAMES = {'facenet': 'FaceNet', 'vit_b': 'ViT-B/16', 'vit_l': 'ViT-L/16'}
 CONFIGS = {
     'c2': dict(det_model='mtcnn', enc_model='facenet', enc_precision='bf16', frame='720p', det_batch=16),
-    'c3': dict(det_model='yolo', enc_model='facenet', enc_precision='bf16', frame='720p', det_batch=32),
+    'c3': dict(det_model='yolo', det_precision='x3', enc_model='facenet', enc_precision='bf16', frame='720p',
+               det_batch=32),
     'c4': dict(det_model='none', enc_model='vit_l', enc_precision='f16x', frame='224'),
-    'c5': dict(det_model='yolo', enc_model='vit_l', enc_precision='f16x', frame='1080p', det_batch=32,
-               grouping=True),
+    'c5': dict(det_model='yolo', det_precision='x3', enc_model='vit_l', enc_precision='f16x', frame='1080p',
+               det_batch=32, grouping=True),
 }
 
 
@@ -68,7 +71,8 @@ def parse(argv=None):
     ap.add_argument('--warmup', type=int, default=3)
     ap.add_argument('--config', default='c2', choices=sorted(CONFIGS))
     ap.add_argument('--det-model', choices=['mtcnn', 'yolo', 'none'])
-    ap.add_argument('--det-precision', default='fp32', choices=['fp32', 'bf16'], help='YOLO conv precision')
+    ap.add_argument('--det-precision', default=None, choices=['fp32', 'x3', 'bf16'],
+                    help='YOLO conv precision (default: the config\'s; x3 = fp32-grade bf16x3 products)')
     ap.add_argument('--det-batch', type=int)
     ap.add_argument('--enc-model', choices=['facenet', 'vit_b', 'vit_l'])
     ap.add_argument('--enc-batch', type=int, default=128)
@@ -91,9 +95,11 @@ def parse(argv=None):
     ap.add_argument('--det-min-border', type=int, default=5)
     a = ap.parse_args(argv)
     preset = CONFIGS[a.config]
-    for k in ('det_model', 'enc_model', 'enc_precision', 'frame', 'det_batch'):
+    for k in ('det_model', 'det_precision', 'enc_model', 'enc_precision', 'frame', 'det_batch'):
         if getattr(a, k) is None:
             setattr(a, k, preset.get(k))
+    if a.det_precision is None:
+        a.det_precision = 'fp32'
     a.grouping = preset.get('grouping', False)
     if a.enc_model == 'facenet' and a.enc_precision == 'f16x':
         a.enc_precision = 'bf16'
@@ -500,8 +506,10 @@ def roofline_det(args, pipe, shared, solo):
     s_avg, c_avg = s_ms / max(1, s_n), c_ms / max(1, c_n)
     fl = s_fl / max(1, s_n)
     if yolo:
-        peak = BF16_PEAK_TFLOPS if args.det_precision == 'bf16' else FP32_PEAK_TFLOPS
-        kname = 'k_conv (YOLOv3 Darknet53+neck+head, 75 implicit-GEMM launches per det-batch, %s)' % args.det_precision
+        peak = {'bf16': BF16_PEAK_TFLOPS, 'x3': X3_PEAK_TFLOPS}.get(args.det_precision, FP32_PEAK_TFLOPS)
+        kname = ('k_conv_dma3 (YOLOv3 Darknet53+neck+head, 75 implicit-GEMM launches per det-batch, bf16x3 operands: '
+                 'fp32-grade; peak = bf16 dense / 6 products)' if args.det_precision == 'x3' else
+                 'k_conv (YOLOv3 Darknet53+neck+head, 75 implicit-GEMM launches per det-batch, %s)' % args.det_precision)
     else:
         peak = F16X_PEAK_TFLOPS
         kname = ('k_pnet (fused pyramid resample + PNet; convs on fp16 matrix cores with split operands, '
@@ -510,7 +518,7 @@ def roofline_det(args, pipe, shared, solo):
     c_ach = (c_fl / max(1, c_n)) / (c_avg / 1e3) / 1e12 if c_avg > 0 else 0.0
     traffic = None
     tf = os.path.join(ROOT, 'profiles', ('yolo' if yolo else 'pnet') + '_traffic.json')
-    if os.path.exists(tf):
+    if os.path.exists(tf) and not (yolo and args.det_precision != 'fp32'):  # measured for the fp32 YOLO / k_pnet
         traffic = json.load(open(tf)).get('hbm_bytes_per_launch')
     r = {'kernel': kname, 'bound': 'mfma', 'achieved': round(ach, 3), 'peak': peak, 'unit': 'TFLOP/s',
          'frac': round(ach / peak, 4), 'traffic': traffic, 'avg_launch_ms': round(s_avg, 4),

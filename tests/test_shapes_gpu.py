@@ -73,11 +73,12 @@ def test_mtcnn_b16_device_crops(g):
     assert not (diff & ~near).any()
 
 
-def test_yolo_1080p_b4(g):
+@pytest.mark.parametrize('precision', ['fp32', 'x3'])
+def test_yolo_1080p_b4(g, precision):
     from videotofaces import synth
     from videotofaces.detectors.yolo import YOLOv3
     frames = synth.make_frames(4, 1080, 1920, seed=102)
-    b, s, c = YOLOv3('cuda:0', precision='fp32')(torch.from_numpy(frames).cuda())
+    b, s, c = YOLOv3('cuda:0', precision=precision)(torch.from_numpy(frames).cuda())
     np.testing.assert_array_equal([len(t) for t in s], g['yolo_1080_b4_counts'])
     np.testing.assert_allclose(np.concatenate(b), g['yolo_1080_b4_boxes'], rtol=1e-6, atol=1e-2)
     np.testing.assert_allclose(np.concatenate(s), g['yolo_1080_b4_scores'], rtol=1e-6, atol=1e-4)

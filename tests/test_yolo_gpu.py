@@ -23,10 +23,12 @@ def g():
     return np.load(os.path.join(GOLDEN, 'yolo.npz'))
 
 
-@pytest.fixture(scope='module')
-def det():
+@pytest.fixture(scope='module', params=['fp32', 'x3'])
+def det(request):
+    """fp32 MFMA (parity mode) and the bf16x3 mode (fp32-grade products: three bf16 terms per
+    operand), both at the fp32 tolerances of this file."""
     from videotofaces.detectors.yolo import YOLOv3
-    return YOLOv3('cuda:0', precision='fp32')
+    return YOLOv3('cuda:0', precision=request.param)
 
 
 def _ref_input(g):

@@ -39,6 +39,8 @@ struct ConvParams {
     int out_sp;          // output in the split-pair layout (gemm_x3.hpp; fp32 operand modes): the next
                          // layer's operand for conv_dma's split mode; a value beyond 2^14 sets *ovf
     int in_sp;           // input (and weights) in the split-pair layout: conv_dma split mode
+    int s3;              // bf16x3 mode (conv_dma MODE 2): input, weights, residual and output (unless
+                         // out_f32) in the split-triple layout (conv_dev.hpp)
     const void* zero;    // conv_dma: 16 zero bytes (the DMA source of padding / K-tail pieces; set by the launcher)
     int dp_tiles, tail_split, gx, gy;  // conv_dma work items (set by the launcher)
     int64_t M;           // N*OH*OW

@@ -80,6 +80,33 @@ __device__ inline void conv_epilogue(const ConvParams& p, int64_t m, int c, floa
     }
 }
 
+// "Split-triple" (S3) layout of the bf16x3 mode (conv_dma MODE 2): a row of C fp32 values
+// (C % 8 == 0) is stored as C/8 chunks of 48 bytes, chunk j = [b0 | b1 | b2] of elements
+// 8j..8j+7 (8 bf16 each) with b0 = bf16(x), b1 = bf16(x - b0), b2 = x - b0 - b1 (exact in bf16:
+// x has 24 significant bits, b0 and b1 take 8 each).  x = (b0 + b1) + b2 exactly, so one S3
+// tensor is both the next conv's operand and an exact fp32 residual; the bf16 exponent range is
+// fp32's (no range guard, unlike the fp16 split pairs).
+__device__ inline void s3_store8(char* q, const float (&v)[8]) {
+    bf16x8 h0, h1, h2;
+#pragma unroll
+    for (int e = 0; e < 8; e++) {
+        const __bf16 a = (__bf16)v[e];
+        const float r1 = v[e] - (float)a;
+        const __bf16 b = (__bf16)r1;
+        h0[e] = a;
+        h1[e] = b;
+        h2[e] = (__bf16)(r1 - (float)b);
+    }
+    *(bf16x8*)q = h0;
+    *(bf16x8*)(q + 16) = h1;
+    *(bf16x8*)(q + 32) = h2;
+}
+__device__ inline void s3_load8(const char* q, float (&v)[8]) {
+    const bf16x8 h0 = *(const bf16x8*)q, h1 = *(const bf16x8*)(q + 16), h2 = *(const bf16x8*)(q + 32);
+#pragma unroll
+    for (int e = 0; e < 8; e++) v[e] = ((float)h0[e] + (float)h1[e]) + (float)h2[e];
+}
+
 // 8 consecutive output channels c0..c0+7 of row m (c0 % 8 == 0, channel strides / offsets
 // multiples of 8): the same element math as conv_epilogue with 16/32-byte loads and stores
 template <typename T>
@@ -88,7 +115,9 @@ __device__ inline void conv_epilogue8(const ConvParams& p, int64_t m, int c0, fl
                                       bool* bad = nullptr) {
     typedef __attribute__((ext_vector_type(8))) T t8;
     float rv[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    if (p.res) {
+    if (p.res && p.s3) {
+        s3_load8((const char*)p.res + (res_index(p, m, c0) >> 3) * 48, rv);
+    } else if (p.res) {
         const t8 r = *(const t8*)((const T*)p.res + res_index(p, m, c0));
 #pragma unroll
         for (int e = 0; e < 8; e++) rv[e] = to_f(r[e]);
@@ -109,7 +138,19 @@ __device__ inline void conv_epilogue8(const ConvParams& p, int64_t m, int c0, fl
         v[e] = x;
         o[e] = from_f<T>(x);
     }
-    if (p.up2) {
+    if (p.up2 && p.s3 && !p.out_f32) {
+        const int ow = (int)(m % p.OW);
+        const int64_t t = m / p.OW;
+        const int oh = (int)(t % p.OH);
+        const int64_t n = t / p.OH;
+        const int64_t a = ((n * 2 * p.OH + 2 * oh) * 2 * p.OW + 2 * ow) * p.out_cstride + p.out_coff + c0;
+        const int64_t rs = (int64_t)2 * p.OW * p.out_cstride;
+        char* out = (char*)p.out;
+        s3_store8(out + (a >> 3) * 48, v);
+        s3_store8(out + ((a + p.out_cstride) >> 3) * 48, v);
+        s3_store8(out + ((a + rs) >> 3) * 48, v);
+        s3_store8(out + ((a + rs + p.out_cstride) >> 3) * 48, v);
+    } else if (p.up2) {
         const int ow = (int)(m % p.OW);
         const int64_t t = m / p.OW;
         const int oh = (int)(t % p.OH);
@@ -132,6 +173,8 @@ __device__ inline void conv_epilogue8(const ConvParams& p, int64_t m, int c0, fl
         float* out = (float*)p.out + m * p.out_cstride + p.out_coff + c0;
         *(f32x4*)out = f32x4{v[0], v[1], v[2], v[3]};
         *(f32x4*)(out + 4) = f32x4{v[4], v[5], v[6], v[7]};
+    } else if (p.s3) {
+        s3_store8((char*)p.out + ((m * p.out_cstride + p.out_coff + c0) >> 3) * 48, v);
     } else if (p.n_split && c0 >= p.n_split) {
         *(t8*)((T*)p.out2 + m * p.out2_cstride + p.out2_coff + (c0 - p.n_split)) = o;
     } else {

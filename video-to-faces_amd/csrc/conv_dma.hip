@@ -314,6 +314,184 @@ __global__ __launch_bounds__(256, OCC) void k_conv_dma(ConvParams p) {
     dma_epilogue<T, BN>(p, E, BM, m0, n0);
 }
 
+// ---------------------------------------------------------------- MODE 2: bf16x3 (fp32-grade)
+// Operands in the split-triple layout (conv_dev.hpp: x = b0 + b1 + b2, three bf16 terms of 8
+// significant bits each), so every fp32 product is x w = b0 w0 + [b0 w1 + b1 w0 + b0 w2 + b1 w1 +
+// b2 w0] up to terms of 2^-24 relative: six v_mfma_f32_16x16x32_bf16 per 32-deep step and
+// fragment pair (96 cycles) instead of eight v_mfma_f32_16x16x4_f32 (256), with fp32's exponent
+// range (YOLO's Darknet activations reach 1.5e5 with the synthetic weights: beyond the fp16 split).
+// LDS image per stage: three planes of A rows then three planes of B rows, 64-B rows (one
+// 32-deep step of one plane: 4 chunks), 16-B slot s of row r holding chunk s ^ f((r >> 2) & 3) with
+// f(x) = (4 - x) & 3 -- conflict-free for the ds_read_b128 fragment reads (rows lane & 15, chunk
+// lane >> 4); a DMA wave-instruction writes one plane's 16-row block (1 KB) lane-linearly.
+template <int BM, int BN, int WGM>
+struct D3Cfg {
+    static constexpr int WGN = 4 / WGM, WM = BM / WGM, WN = BN / WGN, FM = WM / 16, FN = WN / 16;
+    static constexpr int RB = 64, PLA = BM * RB, PLB = BN * RB, A_ST = 3 * PLA, ST = 3 * (PLA + PLB), LDE = BN + 4;
+    static constexpr int SM = 2 * ST > BM * LDE * 4 ? 2 * ST : BM * LDE * 4;
+    static constexpr int RA = BM / 64, RBN = BN / 64;  // 16-row blocks per wave (A, B)
+    static_assert(BM % 64 == 0 && BN % 64 == 0 && FM >= 1 && FN >= 1 && SM * 2 <= 160 * 1024, "bf16x3 tile");
+};
+
+__device__ inline int s3_swz(int r) { return (4 - ((r >> 2) & 3)) & 3; }
+
+template <int BM, int BN, int WGM>
+__global__ __launch_bounds__(256, 2) void k_conv_dma3(ConvParams p) {
+    using C = D3Cfg<BM, BN, WGM>;
+    constexpr int FM = C::FM, FN = C::FN, RB = C::RB, RA = C::RA, RBN = C::RBN;
+    __shared__ __attribute__((aligned(16))) char smem[C::SM];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wm = wave / C::WGN, wn = wave % C::WGN;
+    int t, slice, tile_m, tile_n;
+    bool tail;
+    work_item(p, blockIdx.x, t, slice, tail);
+    tile_of(p, t, tile_m, tile_n);
+    const int64_t m0 = (int64_t)tile_m * BM;
+    const int n0 = tile_n * BN;
+    // DMA: lane L of a 16-row block writes row L >> 2, slot L & 3, which holds chunk
+    // kc = (L & 3) ^ f((L >> 4) & 3) of the step (the same for every block of the lane)
+    const int kc = (lane & 3) ^ s3_swz(lane >> 2);
+    const int ics = p.in_cstride ? p.in_cstride : p.Cin;
+    const int64_t pixb = (int64_t)ics * 6;
+    const int Cin8 = p.Cin >> 3, K8 = p.K >> 3;
+    const char* in = (const char*)p.in;
+    const char* wt = (const char*)p.w;
+    const char* zero = (const char*)p.zero;
+    int64_t abase[RA];
+    int aih[RA], aiw[RA];
+#pragma unroll
+    for (int j = 0; j < RA; j++) {
+        const int64_t m = m0 + 16 * (wave + 4 * j) + (lane >> 2);
+        if (m < p.M) {
+            const int ow = (int)(m % p.OW);
+            const int64_t q = m / p.OW;
+            const int oh = (int)(q % p.OH);
+            const int64_t n = q / p.OH;
+            aih[j] = oh * p.sh - p.ph;
+            aiw[j] = ow * p.sw - p.pw;
+            abase[j] = ((n * p.H + aih[j]) * p.W + aiw[j]) * pixb;
+        } else {
+            aih[j] = -(1 << 29);
+            aiw[j] = 0;
+            abase[j] = 0;
+        }
+    }
+    int64_t bbase[RBN];
+#pragma unroll
+    for (int j = 0; j < RBN; j++) {
+        const int n = min(n0 + 16 * (wave + 4 * j) + (lane >> 2), p.Cout - 1);
+        bbase[j] = (int64_t)n * K8 * 48;
+    }
+    const int KT = (p.K + 31) / 32;
+    const int kt0 = tail ? (int)((int64_t)slice * KT / p.tail_split) : 0;
+    const int kt1 = tail ? (int)((int64_t)(slice + 1) * KT / p.tail_split) : KT;
+    int c = kt0 * 4 + kc;
+    int tap = c / Cin8, cc = c - tap * Cin8;
+    int kh = tap / p.KW, kw = tap - kh * p.KW;
+    const bool chk = p.ph | p.pw;
+    auto issue = [&](int s) {
+        char* base = smem + s * C::ST;
+        const bool kv = c < K8;
+        const int64_t toff = ((int64_t)kh * p.W + kw) * pixb + cc * 48;
+#pragma unroll
+        for (int j = 0; j < RA; j++) {
+            bool ok = kv && aih[j] + kh >= 0;
+            if (chk) ok = ok && aih[j] + kh < p.H && (unsigned)(aiw[j] + kw) < (unsigned)p.W;
+            const char* g = ok ? in + abase[j] + toff : zero;
+#pragma unroll
+            for (int pl = 0; pl < 3; pl++)
+                __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)(ok ? g + 16 * pl : zero),
+                                                 (void __attribute__((address_space(3)))*)(base + pl * C::PLA +
+                                                                                           (wave + 4 * j) * 1024),
+                                                 16, 0, 0);
+        }
+#pragma unroll
+        for (int j = 0; j < RBN; j++) {
+            const char* g = wt + bbase[j] + (int64_t)c * 48;
+#pragma unroll
+            for (int pl = 0; pl < 3; pl++)
+                __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)(kv ? g + 16 * pl : zero),
+                                                 (void __attribute__((address_space(3)))*)(base + C::A_ST + pl * C::PLB +
+                                                                                           (wave + 4 * j) * 1024),
+                                                 16, 0, 0);
+        }
+    };
+    auto advance = [&]() {
+        c += 4;
+        cc += 4;
+        while (cc >= Cin8) {
+            cc -= Cin8;
+            if (++kw == p.KW) {
+                kw = 0;
+                kh++;
+            }
+        }
+    };
+    f4 acc[FM][FN], accx[FM][FN];
+#pragma unroll
+    for (int i = 0; i < FM; i++)
+#pragma unroll
+        for (int j = 0; j < FN; j++) {
+            acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
+            accx[i][j] = f4{0.f, 0.f, 0.f, 0.f};
+        }
+    const int of = (lane & 15) * RB + (((lane >> 4) ^ s3_swz(lane & 15)) << 4);
+    issue(0);
+    for (int kt = kt0; kt < kt1; kt++) {
+        asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+        const int sb = (kt - kt0) & 1;
+        if (kt + 1 < kt1) {
+            advance();
+            issue(sb ^ 1);
+        }
+        const char* As = smem + sb * C::ST + wm * C::WM * RB + of;
+        const char* Bs = smem + sb * C::ST + C::A_ST + wn * C::WN * RB + of;
+        bf16x8 b[FN][3];
+#pragma unroll
+        for (int j = 0; j < FN; j++)
+#pragma unroll
+            for (int pl = 0; pl < 3; pl++) b[j][pl] = *(const bf16x8*)(Bs + pl * C::PLB + j * 16 * RB);
+#pragma unroll
+        for (int i = 0; i < FM; i++) {
+            bf16x8 a[3];
+#pragma unroll
+            for (int pl = 0; pl < 3; pl++) a[pl] = *(const bf16x8*)(As + pl * C::PLA + i * 16 * RB);
+#pragma unroll
+            for (int j = 0; j < FN; j++) {
+                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], b[j][0], acc[i][j], 0, 0, 0);
+                accx[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], b[j][1], accx[i][j], 0, 0, 0);
+                accx[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[1], b[j][0], accx[i][j], 0, 0, 0);
+                accx[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], b[j][2], accx[i][j], 0, 0, 0);
+                accx[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[1], b[j][1], accx[i][j], 0, 0, 0);
+                accx[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[2], b[j][0], accx[i][j], 0, 0, 0);
+            }
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < FM; i++)
+#pragma unroll
+        for (int j = 0; j < FN; j++) acc[i][j] = acc[i][j] + accx[i][j];
+    __syncthreads();
+    if (tail) {
+        f4* slab = (f4*)(p.ws + ((int64_t)(t - p.dp_tiles) * p.tail_split + slice) * (BM * BN));
+#pragma unroll
+        for (int i = 0; i < FM; i++)
+#pragma unroll
+            for (int j = 0; j < FN; j++) slab[((wave * FM + i) * FN + j) * 64 + lane] = acc[i][j];
+        return;
+    }
+    float* E = (float*)smem;
+#pragma unroll
+    for (int j = 0; j < FN; j++)
+#pragma unroll
+        for (int i = 0; i < FM; i++)
+#pragma unroll
+            for (int q = 0; q < 4; q++)
+                E[(wm * C::WM + i * 16 + 4 * (lane >> 4) + q) * C::LDE + wn * C::WN + j * 16 + (lane & 15)] = acc[i][j][q];
+    __syncthreads();
+    dma_epilogue<float, BN>(p, E, BM, m0, n0);
+}
+
 // tail tiles: one workgroup per (tile, 16-row block) sums the block's K slices in slice order
 // (deterministic) into an LDS image, then the epilogue of those 16 rows
 template <int MODE, int BM, int BN, int WGM, int OCC, int NSTG>
@@ -424,6 +602,40 @@ void launch_dma_t(ConvParams p, hipStream_t st) {
     if (nt) k_conv_dma_tail<MODE, BM, BN, WGM, OCC, NSTG><<<(unsigned)(nt * (BM / 16)), 256, 0, st>>>(p);
 }
 
+template <int BM, int BN, int WGM>
+void launch_dma3_t(ConvParams p, hipStream_t st) {
+    p.gx = (int)cdiv(p.M, BM);
+    p.gy = (int)cdiv(p.Cout, BN);
+    p.group_m = dma_group_m();
+    p.zero = zero_page(stream_device(st));
+    const int T = p.gx * p.gy, KT = (p.K + 31) / 32;
+    const int slots = 2 * cu_count();
+    p.dp_tiles = T;
+    p.tail_split = 1;
+    p.split = 1;
+    if (p.split_fp32) {
+        if (T > slots) {
+            const int R = T % slots;
+            const int S = R > 0 ? std::min(slots / R, KT / 4) : 0;
+            if (R > 0 && R <= slots / 2 && S >= 2) {
+                p.dp_tiles = T - R;
+                p.tail_split = S;
+            }
+        } else {
+            const int S = std::min(std::min(slots / T, KT / 4), 16);
+            if (S >= 2) {
+                p.dp_tiles = 0;
+                p.tail_split = S;
+            }
+        }
+    }
+    const int nt = T - p.dp_tiles;
+    p.ws = nt ? dma_ws(st, (size_t)nt * p.tail_split * BM * BN * 4) : nullptr;
+    k_conv_dma3<BM, BN, WGM><<<(unsigned)(p.dp_tiles + nt * p.tail_split), 256, 0, st>>>(p);
+    // the slab layout (wave, fragment, lane) is MODE 1's for the same tile / wave grid
+    if (nt) k_conv_dma_tail<1, BM, BN, WGM, 2, 2><<<(unsigned)(nt * (BM / 16)), 256, 0, st>>>(p);
+}
+
 }  // namespace
 
 bool conv_dma_ok(const ConvParams& p) {
@@ -455,6 +667,14 @@ int conv_dma_choice_bf16(const ConvParams& p) {
 void launch_conv_dma(const ConvParams& p, bool bf16, hipStream_t st) {
     if (p.M <= 0) return;
     VTF_CHECK(conv_dma_ok(p), VTF_E_ARG, "conv_dma: channel counts / strides must be multiples of 8");
+    if (p.s3) {
+        // bf16x3: 128 x 64 tiles up to 64 output channels, 64 x 128 above
+        if (p.Cout <= 64)
+            launch_dma3_t<128, 64, 2>(p, st);
+        else
+            launch_dma3_t<64, 128, 2>(p, st);
+        return;
+    }
     VTF_CHECK(bf16 || p.in_sp, VTF_E_ARG, "conv_dma: bf16 or split-pair operands");
     VTF_CHECK(!p.out_sp || !bf16, VTF_E_ARG, "conv_dma: split-pair output is an fp32-mode output");
     if (bf16) {

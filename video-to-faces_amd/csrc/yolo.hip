@@ -26,12 +26,14 @@
 #include "boxes.hpp"
 #include "common.hpp"
 #include "conv.hpp"
+#include "conv_dev.hpp"
 #include "nms.hpp"
 
 namespace vtf {
 
 struct YUnit {
     int cin, cout, k, s, cin_pad;
+    int cout_p;    // bf16x3 mode: Cout padded to 8 (the pred convs' 18 -> 24; zero weight rows)
     void* w;       // [cout][k][k][cin_pad], element = precision
     float* alpha;  // folded BN (ConvUnit)
     float* beta;
@@ -41,6 +43,10 @@ struct YUnit {
 struct Yolo {
     int device = 0;
     bool bf16 = false;
+    // bf16x3 (fp32-grade products on the bf16 matrix cores, conv_dma MODE 2): activations and
+    // weights in the split-triple layout (6 bytes per element), pred-conv maps fp32
+    bool x3 = false;
+    size_t es() const { return x3 ? 6 : (bf16 ? 2 : 4); }
     hipStream_t st = 0;
     std::vector<YUnit> U;
     std::vector<void*> allocs;
@@ -129,7 +135,25 @@ static void build(Yolo& Y, const float* params, int64_t n_params) {
                     for (int x = 0; x < g.k; x++)
                         wt[(size_t)co * K + (y * g.k + x) * u.cin_pad + ci] =
                             w[(((size_t)co * g.cin + ci) * g.k + y) * g.k + x];
-        if (Y.bf16) {
+        u.cout_p = g.cout;
+        if (Y.x3) {
+            // split-triple rows [cout_p][K/8][b0 x 8 | b1 x 8 | b2 x 8] (conv_dev.hpp), zero rows past Cout
+            u.cout_p = (g.cout + 7) / 8 * 8;
+            std::vector<uint16_t> w3((size_t)u.cout_p * K * 3, 0);
+            for (int co = 0; co < g.cout; co++)
+                for (int k = 0; k < K; k++) {
+                    const float v = wt[(size_t)co * K + k];
+                    const uint16_t b0 = f2bf(v);
+                    const float r1 = v - __builtin_bit_cast(float, (uint32_t)b0 << 16);
+                    const uint16_t b1 = f2bf(r1);
+                    const uint16_t b2 = f2bf(r1 - __builtin_bit_cast(float, (uint32_t)b1 << 16));
+                    uint16_t* c = &w3[((size_t)co * (K / 8) + k / 8) * 24 + (k & 7)];
+                    c[0] = b0;
+                    c[8] = b1;
+                    c[16] = b2;
+                }
+            u.w = Y.upload(w3);
+        } else if (Y.bf16) {
             std::vector<uint16_t> wb(wt.size());
             for (size_t i = 0; i < wt.size(); i++) wb[i] = f2bf(wt[i]);
             u.w = Y.upload(wb);
@@ -138,7 +162,9 @@ static void build(Yolo& Y, const float* params, int64_t n_params) {
         }
         if (g.pred) {
             const float* b = take(g.cout);
-            u.bias = Y.upload(std::vector<float>(b, b + g.cout));
+            std::vector<float> bv(b, b + g.cout);
+            bv.resize(u.cout_p, 0.f);
+            u.bias = Y.upload(bv);
         } else {
             // BatchNorm2d(eps 1e-5) folded the way torch's CPU inference kernel does it
             // (invstd = 1/sqrt(var+eps), alpha = invstd*w, beta = b - mean*alpha)
@@ -209,10 +235,67 @@ __global__ void k_letterbox(const uint8_t* __restrict__ frames, int64_t fstride,
     for (int c = 0; c < 8; c++) o[c] = (T)v[c];
 }
 
+// the same pass writing the split-triple layout (8 channels = one 48-byte chunk per pixel)
+__global__ void k_letterbox_s3(const uint8_t* __restrict__ frames, int64_t fstride, int64_t rstride, int H, int W,
+                               int h, int w, int Hp, int Wp, int64_t total, char* __restrict__ out) {
+    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= total) return;
+    int dx = (int)(i % Wp);
+    int dy = (int)((i / Wp) % Hp);
+    int64_t b = i / ((int64_t)Wp * Hp);
+    float v[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    if (dy < h && dx < w) {
+        const uint8_t* base = frames + b * fstride;
+        int u[3];
+        if (h == H && w == W) {
+            const uint8_t* p = base + (int64_t)dy * rstride + dx * 3;
+            u[0] = p[0];
+            u[1] = p[1];
+            u[2] = p[2];
+        } else {
+            int sx0, sx1, a0, a1, sy0, sy1, b0, b1;
+            bool ex, ey;
+            lin_coef(dx, W, w, sx0, sx1, a0, a1, ex);
+            lin_coef(dy, H, h, sy0, sy1, b0, b1, ey);
+            (void)ey;
+            const uint8_t* r0 = base + (int64_t)sy0 * rstride;
+            const uint8_t* r1 = base + (int64_t)sy1 * rstride;
+#pragma unroll
+            for (int ch = 0; ch < 3; ch++) {
+                int h0 = ex ? r0[sx0 * 3 + ch] * 2048 : r0[sx0 * 3 + ch] * a0 + r0[sx1 * 3 + ch] * a1;
+                int h1 = ex ? r1[sx0 * 3 + ch] * 2048 : r1[sx0 * 3 + ch] * a0 + r1[sx1 * 3 + ch] * a1;
+                int t = ((((h0 >> 4) * b0) >> 16) + (((h1 >> 4) * b1) >> 16) + 2) >> 2;
+                u[ch] = min(255, max(0, t));
+            }
+        }
+        for (int oc = 0; oc < 3; oc++) v[oc] = __fdiv_rn((float)u[2 - oc], 255.f);
+    }
+    s3_store8(out + i * 48, v);
+}
+
+// NCHW fp32 (C <= 8) -> split-triple NHWC with 8 channels (vtf_yolo_net's input)
+__global__ void k_nchw_to_s3(const float* __restrict__ in, int64_t N, int C, int H, int W, char* __restrict__ out) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= N * H * W) return;
+    const int64_t n = i / ((int64_t)H * W), hw = i % ((int64_t)H * W);
+    float v[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    for (int c = 0; c < C; c++) v[c] = in[(n * C + c) * H * W + hw];
+    s3_store8(out + i * 48, v);
+}
+
+// first 18 channels of the padded (24-channel) fp32 pred-conv output
+__global__ void k_compact18(const float* __restrict__ in, int64_t rows, float* __restrict__ out) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= rows * 18) return;
+    out[i] = in[(i / 18) * 24 + i % 18];
+}
+
 static void launch_letterbox(const uint8_t* frames, int64_t fstride, int64_t rstride, int B, int H, int W, int h, int w,
-                             int Hp, int Wp, bool bf16, void* out, hipStream_t st) {
+                             int Hp, int Wp, bool bf16, void* out, hipStream_t st, bool x3 = false) {
     int64_t total = (int64_t)B * Hp * Wp;
-    if (bf16)
+    if (x3)
+        k_letterbox_s3<<<cdiv(total, 256), 256, 0, st>>>(frames, fstride, rstride, H, W, h, w, Hp, Wp, total, (char*)out);
+    else if (bf16)
         k_letterbox<__bf16><<<cdiv(total, 256), 256, 0, st>>>(frames, fstride, rstride, H, W, h, w, Hp, Wp, total,
                                                                (__bf16*)out);
     else
@@ -259,7 +342,24 @@ static void unit(Yolo& Y, int li, const void* in, int in_cs, int N, int H, int W
         p.res_post = 1;
     }
     p.up2 = up2 ? 1 : 0;
-    launch_conv(p, Y.bf16, Y.st);
+    if (Y.x3) {
+        // split-triple operands on the bf16 matrix cores; the pred convs write their padded
+        // 24-channel fp32 maps to scratch, compacted to the 18-channel layout the decode reads
+        p.s3 = 1;
+        p.split_fp32 = 1;  // tail tiles may be split along K (slice-order reduction; parity is a tolerance)
+        p.Cout = u.cout_p;
+        if (u.bias) {
+            float* tmp = Y.ar.get<float>(89, (size_t)p.M * u.cout_p);
+            p.out = tmp;
+            p.out_cstride = u.cout_p;
+            launch_conv_dma(p, false, Y.st);
+            k_compact18<<<cdiv(p.M * 18, 256), 256, 0, Y.st>>>(tmp, p.M, (float*)out);
+        } else {
+            launch_conv_dma(p, false, Y.st);
+        }
+    } else {
+        launch_conv(p, Y.bf16, Y.st);
+    }
     Y.flops += 2.0 * (double)p.M * u.cout * u.k * u.k * u.cin;
     Y.launches++;
 }
@@ -267,7 +367,7 @@ static void unit(Yolo& Y, int li, const void* in, int in_cs, int N, int H, int W
 // x0: NHWC [B,Hp,Wp,8] -> maps NHWC fp32 [B,Hp/32,Wp/32,18], [.., /16, ..], [.., /8, ..]
 static void net(Yolo& Y, const void* x0, int B, int Hp, int Wp, float* maps[3]) {
     VTF_CHECK(Hp % 32 == 0 && Wp % 32 == 0 && Hp > 0 && Wp > 0, VTF_E_ARG, "yolo: input must be padded to x32");
-    const size_t es = Y.bf16 ? 2 : 4;
+    const size_t es = Y.es();
     const size_t full = (size_t)B * Hp * Wp * 32;
     char* A = (char*)Y.ar.get(80, full * es);
     char* Bf = (char*)Y.ar.get(81, full * es);
@@ -543,8 +643,8 @@ static void detect(Yolo& Y, const uint8_t* frames, int on_dev, int B, int H, int
     int h, w;
     used_size(H, W, h, w);
     const int Hp = (h + 31) / 32 * 32, Wp = (w + 31) / 32 * 32;
-    void* x0 = Y.ar.get(105, (size_t)B * Hp * Wp * 8 * (Y.bf16 ? 2 : 4));
-    launch_letterbox(fr, fstride, rstride, B, H, W, h, w, Hp, Wp, Y.bf16, x0, st);
+    void* x0 = Y.ar.get(105, (size_t)B * Hp * Wp * 8 * Y.es());
+    launch_letterbox(fr, fstride, rstride, B, H, W, h, w, Hp, Wp, Y.bf16, x0, st, Y.x3);
     float* maps[3];
     maps_alloc(Y, B, Hp, Wp, maps);
     net(Y, x0, B, Hp, Wp, maps);
@@ -575,11 +675,13 @@ extern "C" {
 
 int vtf_yolo_create(const float* params, int64_t n_params, int device, int precision, vtf_yolo_t* out) {
     return guarded([&] {
-        VTF_CHECK(params && out && (precision == 0 || precision == 1), VTF_E_ARG, "bad argument");
+        VTF_CHECK(params && out && precision >= 0 && precision <= 2, VTF_E_ARG,
+                  "bad argument (precision 0 fp32, 1 bf16, 2 bf16x3)");
         DeviceGuard dg(device);
         auto* h = new vtf_yolo_s();
         h->y.device = device;
         h->y.bf16 = precision == 1;
+        h->y.x3 = precision == 2;
         try {
             build(h->y, params, n_params);
         } catch (...) {
@@ -655,8 +757,11 @@ int vtf_yolo_net(vtf_yolo_t h, const float* d_x, int B, int Hp, int Wp, float* d
     return guarded_on(h ? h->y.device : -1, [&] {
         VTF_CHECK(h && d_x && d_map0 && d_map1 && d_map2 && B > 0, VTF_E_ARG, "bad argument");
         Yolo& Y = h->y;
-        void* x0 = Y.ar.get(105, (size_t)B * Hp * Wp * 8 * (Y.bf16 ? 2 : 4));
-        launch_nchw_to_nhwc(d_x, B, 3, Hp, Wp, 8, x0, Y.bf16, Y.st);
+        void* x0 = Y.ar.get(105, (size_t)B * Hp * Wp * 8 * Y.es());
+        if (Y.x3)
+            k_nchw_to_s3<<<cdiv((int64_t)B * Hp * Wp, 256), 256, 0, Y.st>>>(d_x, B, 3, Hp, Wp, (char*)x0);
+        else
+            launch_nchw_to_nhwc(d_x, B, 3, Hp, Wp, 8, x0, Y.bf16, Y.st);
         float* maps[3] = {d_map0, d_map1, d_map2};
         net(Y, x0, B, Hp, Wp, maps);
         VTF_HIP(hipStreamSynchronize(Y.st));

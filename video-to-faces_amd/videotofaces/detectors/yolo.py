@@ -27,20 +27,23 @@ def input_size(H, W):
 
 class YOLOv3:
     """Handle around vtf_yolo_* (the reference's nn.Module YOLOv3, yolo.py:123-176).
-    precision 'fp32' (parity; 1e-4-level vs the reference) or 'bf16' (bf16 operands and
-    activations, fp32 accumulation)."""
+    precision 'fp32' (parity: fp32 MFMA; 1e-4-level vs the reference), 'x3' (fp32-grade: each fp32
+    operand as three bf16 terms, six bf16 MFMAs per product, fp32 exponent range) or 'bf16'
+    (bf16 operands and activations, fp32 accumulation)."""
+
+    _MODES = {'fp32': 0, 'bf16': 1, 'x3': 2}
 
     def __init__(self, device=None, params=None, precision='fp32'):
         self.device = nat.require_gpu(device)
-        if precision not in ('fp32', 'bf16'):
-            raise ValueError('precision must be fp32 or bf16')
+        if precision not in self._MODES:
+            raise ValueError('precision must be fp32, x3 or bf16')
         self.precision = precision
         if params is None:
             params = synth.make_params('yolo')
         flat = np.ascontiguousarray(synth.pack(params), dtype=np.float32)
         h = ctypes.c_void_p()
         nat.check(nat.lib().vtf_yolo_create(flat.ctypes.data, flat.size, self.device.index or 0,
-                                            int(precision == 'bf16'), ctypes.byref(h)))
+                                            self._MODES[precision], ctypes.byref(h)))
         self._h = h
 
     def __del__(self):
