@@ -22,7 +22,7 @@ def _cu(P, x, pre, s=1, p=0):
     x = F.conv2d(x, P[pre + '.conv.weight'], None, s, p)
     x = F.batch_norm(x, P[pre + '.bn.running_mean'], P[pre + '.bn.running_var'], P[pre + '.bn.weight'],
                      P[pre + '.bn.bias'], False, 0.0, 1e-3)
-    return F.relu(x)
+    return F.relu(x, inplace=True)  # nn.ReLU(inplace=True) (basic.py:26): same values
 
 
 def _block35(P, x, pre, scale):

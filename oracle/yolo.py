@@ -23,7 +23,7 @@ def _cu(P, x, pre, k, s=1):
     x = F.conv2d(x, P[pre + '.conv.weight'], None, s, (k - 1) // 2)
     x = F.batch_norm(x, P[pre + '.bn.running_mean'], P[pre + '.bn.running_var'], P[pre + '.bn.weight'],
                      P[pre + '.bn.bias'], False, 0.0, 1e-5)
-    return F.leaky_relu(x, 0.1)
+    return F.leaky_relu(x, 0.1, inplace=True)  # nn.LeakyReLU(inplace=True) (basic.py:33)
 
 
 def _det_block(P, x, pre):

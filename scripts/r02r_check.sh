@@ -1,0 +1,14 @@
+#!/bin/bash
+# Round-2 re-entry check: GPU tests + smoke, then the default bench (config 2, 10k frames).
+set -o pipefail
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+O=gpurun_out/r02r
+mkdir -p $O
+timeout -k 10 900 python -u -m pytest -x -v --timeout 300 --timeout-method thread -m gpu tests > $O/tests.log 2>&1
+rc=$?
+grep -E "passed|failed|error" $O/tests.log | tail -3
+[ $rc -ne 0 ] && exit $rc
+timeout -k 10 300 python3 -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > $O/smoke.log 2>&1 || exit $?
+tail -1 $O/smoke.log
+timeout -k 10 400 python3 bench.py > $O/bench_c2.json 2> $O/bench_c2.err || exit $?
+cat $O/bench_c2.json
