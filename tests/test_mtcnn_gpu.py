@@ -181,3 +181,22 @@ def test_fused_candidate_nets_match_layer_path(ms, monkeypatch):
     assert [x.shape for x in a] == [y.shape for y in b]
     for x, y in zip(a, b):
         np.testing.assert_allclose(x, y, rtol=1e-5, atol=2e-3)
+
+
+@pytest.mark.parametrize('ms', [5, 20])
+def test_span_convs_match_gather_path(ms, monkeypatch):
+    """RNet conv2 / ONet conv2 / conv3 on the span kernel (k_conv_span: the tile's contiguous input
+    run staged once, conv_dma.hip; default) against the implicit-GEMM gather (VTF_CONV_SPAN=0) on
+    the same 720p frames: same detections, boxes and scores within the fp32-grade tolerance of the
+    e2e golden test (same k order and MFMA chains; the gather path's tail tiles split K)."""
+    from videotofaces import synth
+    from videotofaces.detectors.mtcnn import MTCNN
+    fr = torch.from_numpy(synth.make_frames(4, seed=23)).cuda()
+    m = MTCNN('cuda:0')
+    a = m(fr, ms)
+    monkeypatch.setenv('VTF_CONV_SPAN', '0')
+    b = m(fr, ms)
+    assert [x.shape for x in a] == [y.shape for y in b]
+    assert sum(x.shape[0] for x in a) > 0
+    for x, y in zip(a, b):
+        np.testing.assert_allclose(x, y, rtol=1e-5, atol=2e-3)

@@ -314,6 +314,183 @@ __global__ __launch_bounds__(256, OCC) void k_conv_dma(ConvParams p) {
     dma_epilogue<T, BN>(p, E, BM, m0, n0);
 }
 
+// ---------------------------------------------------------------- span mode (split pairs)
+// Stride-1 unpadded convs (MTCNN RNet / ONet 3x3 on the candidate maps): the input pixels an M
+// tile reads over all KH x KW taps form ONE contiguous run of the NHWC input -- output m = (n, oh,
+// ow) reads idx(m) + kh W + kw with idx(m) = (n H + oh) W + ow -- so the tile's A operand is that
+// run ("span": <= SPAN pixels x Cin = 32 Q channels of split pairs), copied into LDS once per tile
+// by contiguous DMA, and every k-step's A fragment row is read from it at the lane's row offset
+// idx(m) - idx(m0) + kh W + kw.  The implicit-GEMM gather fetched each input piece once per tap
+// (9x for 3x3); here the tile's A traffic is its span.  B (weights) streams per k-step through NS
+// LDS stages as in k_conv_dma.  Span rows are 128 Q bytes, 16-B slot s of each 128-B group of row
+// r holding source slot s ^ ((r >> 1) & 7) (planes reordered [x0 of 4 chunks | x1 of 4 chunks] as
+// in MODE 1).  k order (tap-major, then channel) and MFMA chains are k_conv_dma MODE 1's: the
+// same bits when that kernel does not split K.
+template <int Q, int BM, int BN, int WGM, int SPAN, int OCC, int NS>
+struct SCfg {
+    static constexpr int WGN = 4 / WGM, WM = BM / WGM, WN = BN / WGN, FM = WM / 16, FN = WN / 16;
+    static constexpr int RBA = 128 * Q, A_BYTES = SPAN * RBA, B_ST = BN * 128, LDE = BN + 4;
+    static constexpr int SM0 = A_BYTES + NS * B_ST;
+    static constexpr int SM = SM0 > BM * LDE * 4 ? SM0 : BM * LDE * 4;
+    static constexpr int PB = BN / 32;  // 1-KB B pieces per wave and stage
+    static_assert(SPAN % 8 == 0 && FM >= 1 && FN >= 1 && NS >= 2 && NS <= 3 && SM * OCC <= 160 * 1024, "span tile");
+};
+
+// largest span (input pixels) of any BM-row tile of this conv; tiles start at multiples of BM, so
+// their offsets within an image repeat after OH*OW tiles
+int64_t conv_span_max(const ConvParams& p, int BM) {
+    const int64_t OHW = (int64_t)p.OH * p.OW, HW = (int64_t)p.H * p.W;
+    auto idx = [&](int64_t m) {
+        const int64_t n = m / OHW, r = m - n * OHW, oh = r / p.OW;
+        return n * HW + oh * p.W + (r - oh * p.OW);
+    };
+    const int64_t T = (p.M + BM - 1) / BM;
+    int64_t mx = 0;
+    for (int64_t t = 0; t < std::min<int64_t>(T, OHW + 1); t++) {
+        const int64_t m0 = t * BM, m1 = std::min<int64_t>(m0 + BM, p.M) - 1;
+        mx = std::max<int64_t>(mx, idx(m1) - idx(m0) + (int64_t)(p.KH - 1) * p.W + p.KW);
+    }
+    if (T > OHW + 1) {  // the last (partial) tile
+        const int64_t m0 = (T - 1) * BM;
+        mx = std::max<int64_t>(mx, idx(p.M - 1) - idx(m0) + (int64_t)(p.KH - 1) * p.W + p.KW);
+    }
+    return mx;
+}
+
+template <int Q, int BM, int BN, int WGM, int SPAN, int OCC, int NS>
+__global__ __launch_bounds__(256, OCC) void k_conv_span(ConvParams p) {
+    using C = SCfg<Q, BM, BN, WGM, SPAN, OCC, NS>;
+    constexpr int FM = C::FM, FN = C::FN, PB = C::PB, RBA = C::RBA;
+    __shared__ __attribute__((aligned(16))) char smem[C::SM];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wm = wave / C::WGN, wn = wave % C::WGN;
+    int t, slice, tile_m, tile_n;
+    bool tail;
+    work_item(p, blockIdx.x, t, slice, tail);  // every tile whole (dp_tiles = all)
+    tile_of(p, t, tile_m, tile_n);
+    const int64_t m0 = (int64_t)tile_m * BM;
+    const int n0 = tile_n * BN;
+    const int64_t mlast = min(m0 + BM, p.M) - 1;
+    const int OHW = p.OH * p.OW, HW = p.H * p.W;
+    auto idx = [&](int64_t m) -> int64_t {
+        const int64_t n = m / OHW;
+        const int r = (int)(m - n * OHW), oh = r / p.OW;
+        return n * HW + oh * p.W + (r - oh * p.OW);
+    };
+    const int64_t P0 = idx(m0), npix = (int64_t)p.N * HW;
+    const int span = (int)(idx(mlast) - P0) + (p.KH - 1) * p.W + p.KW;  // <= SPAN (host-checked)
+    const char* in = (const char*)p.in;
+    const char* wt = (const char*)p.w;
+    const char* zero = (const char*)p.zero;
+    // A span: 1-KB DMA pieces dealt round-robin to the waves (lane-linear LDS destination)
+    const int nA = (span * RBA + 1023) >> 10;
+    for (int j = wave; j < nA; j += 4) {
+        const int off = j * 1024 + lane * 16;
+        const int row = off / RBA, g = (off % RBA) >> 7, s = (off >> 4) & 7;
+        const int sp = s ^ ((row >> 1) & 7);
+        const int64_t pix = P0 + row;
+        const char* src =
+            row < span && pix < npix ? in + pix * (128 * Q) + g * 128 + (sp & 3) * 32 + (sp >> 2) * 16 : zero;
+        __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)src,
+                                         (void __attribute__((address_space(3)))*)(smem + off), 16, 0, 0);
+    }
+    // B: as k_conv_dma MODE 1 (row 32 j + 8 wave + (lane >> 3) of piece j, swizzled slot)
+    const int bsrc = (lane & 7) ^ (((lane >> 4) + 4 * (wave & 1)) & 7);
+    const int bkc = bsrc & 3, bpl = (bsrc >> 2) * 16;
+    int64_t bbase[PB];
+#pragma unroll
+    for (int j = 0; j < PB; j++) {
+        const int n = min(n0 + 32 * j + 8 * wave + (lane >> 3), p.Cout - 1);
+        bbase[j] = (int64_t)n * p.K * 4 + bpl + bkc * 32;
+    }
+    char* Bst = smem + C::A_BYTES;
+    auto issueB = [&](int kt, int s) {
+#pragma unroll
+        for (int j = 0; j < PB; j++)
+            __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)(wt + bbase[j] + (int64_t)kt * 128),
+                                             (void __attribute__((address_space(3)))*)(Bst + s * C::B_ST + (wave + 4 * j) * 1024),
+                                             16, 0, 0);
+    };
+    // the lane's A rows (span-relative) of its FM fragments; rows past M repeat the last row
+    int arow[FM];
+#pragma unroll
+    for (int i = 0; i < FM; i++) arow[i] = (int)(idx(min(m0 + wm * C::WM + i * 16 + (lane & 15), mlast)) - P0);
+    f4 acc[FM][FN], accx[FM][FN];
+#pragma unroll
+    for (int i = 0; i < FM; i++)
+#pragma unroll
+        for (int j = 0; j < FN; j++) acc[i][j] = accx[i][j] = f4{0.f, 0.f, 0.f, 0.f};
+    const int hsw = (lane & 15) >> 1;
+    const int o0 = (lane & 15) * 128 + (((lane >> 4) ^ hsw) << 4);
+    const int o1 = (lane & 15) * 128 + (((4 + (lane >> 4)) ^ hsw) << 4);
+    const int KT = p.K >> 5;
+    // prologue: B steps 0 .. NS - 2 in flight behind the span
+    int issued = 0;
+#pragma unroll
+    for (int s = 0; s < NS - 1; s++)
+        if (issued < KT) {
+            issueB(issued, issued % NS);
+            issued++;
+        }
+    int kh = 0, kw = 0, g = 0;
+    for (int kt = 0; kt < KT; kt++) {
+        // this wave's B step kt (and the span, issued first) landed: counted vmcnt leaves the
+        // later steps in flight; after the barrier for every wave, and the stage the next issue
+        // overwrites (step kt - 1's) is free
+        if (NS >= 3 && issued - kt - 1 >= 1)
+            wait_vm_barrier<(NS >= 3 ? PB : 0)>();
+        else
+            wait_vm_barrier<0>();
+        if (issued < KT) {
+            issueB(issued, issued % NS);
+            issued++;
+        }
+        const char* Bs = Bst + (kt % NS) * C::B_ST + wn * C::WN * 128;
+        h8 b0[FN], b1[FN];
+#pragma unroll
+        for (int j = 0; j < FN; j++) {
+            b0[j] = *(const h8*)(Bs + j * 16 * 128 + o0);
+            b1[j] = *(const h8*)(Bs + j * 16 * 128 + o1);
+        }
+        const int toff = kh * p.W + kw;
+#pragma unroll
+        for (int i = 0; i < FM; i++) {
+            const int r = arow[i] + toff, sw = (r >> 1) & 7;
+            const char* Ar = smem + r * RBA + g * 128;
+            const h8 a0 = *(const h8*)(Ar + (((lane >> 4) ^ sw) << 4));
+            const h8 a1 = *(const h8*)(Ar + (((4 + (lane >> 4)) ^ sw) << 4));
+#pragma unroll
+            for (int j = 0; j < FN; j++) {
+                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a0, b0[j], acc[i][j], 0, 0, 0);
+                accx[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a0, b1[j], accx[i][j], 0, 0, 0);
+                accx[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a1, b0[j], accx[i][j], 0, 0, 0);
+            }
+        }
+        if (++g == Q) {
+            g = 0;
+            if (++kw == p.KW) {
+                kw = 0;
+                kh++;
+            }
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < FM; i++)
+#pragma unroll
+        for (int j = 0; j < FN; j++) acc[i][j] = acc[i][j] + accx[i][j] * 0.00048828125f;
+    __syncthreads();  // no DMA outstanding; every wave is done with the span and the stages
+    float* E = (float*)smem;
+#pragma unroll
+    for (int j = 0; j < FN; j++)
+#pragma unroll
+        for (int i = 0; i < FM; i++)
+#pragma unroll
+            for (int q = 0; q < 4; q++)
+                E[(wm * C::WM + i * 16 + 4 * (lane >> 4) + q) * C::LDE + wn * C::WN + j * 16 + (lane & 15)] = acc[i][j][q];
+    __syncthreads();
+    dma_epilogue<float, BN>(p, E, BM, m0, n0);
+}
+
 // ---------------------------------------------------------------- MODE 2: bf16x3 (fp32-grade)
 // Operands in the split-triple layout (conv_dev.hpp: x = b0 + b1 + b2, three bf16 terms of 8
 // significant bits each), so every fp32 product is x w = b0 w0 + [b0 w1 + b1 w0 + b0 w2 + b1 w1 +
@@ -602,6 +779,30 @@ void launch_dma_t(ConvParams p, hipStream_t st) {
     if (nt) k_conv_dma_tail<MODE, BM, BN, WGM, OCC, NSTG><<<(unsigned)(nt * (BM / 16)), 256, 0, st>>>(p);
 }
 
+template <int Q, int BM, int BN, int WGM, int SPAN, int OCC, int NS>
+void launch_span_t(ConvParams p, hipStream_t st) {
+    p.gx = (int)cdiv(p.M, BM);
+    p.gy = (int)cdiv(p.Cout, BN);
+    p.group_m = dma_group_m();
+    p.zero = zero_page(stream_device(st));
+    p.dp_tiles = p.gx * p.gy;
+    p.tail_split = 1;
+    p.split = 1;
+    p.ws = nullptr;
+    k_conv_span<Q, BM, BN, WGM, SPAN, OCC, NS><<<(unsigned)p.dp_tiles, 256, 0, st>>>(p);
+}
+
+// span-mode eligibility (split-pair, stride-1 unpadded convs of 32 / 64 input channels whose
+// tiles' input runs fit the LDS span); env VTF_CONV_SPAN=0 keeps the implicit-GEMM gather
+constexpr int SPAN_BM = 128, SPAN_ROWS = 240;
+bool conv_span_ok(const ConvParams& p) {
+    const char* e = std::getenv("VTF_CONV_SPAN");  // read per launch: tests A/B both paths in one process
+    return (!e || std::atoi(e) != 0) && p.in_sp && !p.s3 && p.sh == 1 && p.sw == 1 && p.ph == 0 && p.pw == 0 &&
+           (p.Cin == 32 || p.Cin == 64) && (p.in_cstride == 0 || p.in_cstride == p.Cin) && p.Cout <= 64 &&
+           p.KH * p.KW >= 4 && !p.n_split && !p.res && !p.up2 && !p.res_up2 &&
+           conv_span_max(p, SPAN_BM) <= SPAN_ROWS;
+}
+
 template <int BM, int BN, int WGM>
 void launch_dma3_t(ConvParams p, hipStream_t st) {
     p.gx = (int)cdiv(p.M, BM);
@@ -698,6 +899,13 @@ void launch_conv_dma(const ConvParams& p, bool bf16, hipStream_t st) {
             const char* e = std::getenv("VTF_DMA_SPLIT64");
             return e ? std::atoi(e) : 128;
         }();
+        if (conv_span_ok(p)) {
+            if (p.Cin == 32)
+                launch_span_t<1, SPAN_BM, 64, 2, SPAN_ROWS, 3, 2>(p, st);
+            else
+                launch_span_t<2, SPAN_BM, 64, 2, SPAN_ROWS, 2, 2>(p, st);
+            return;
+        }
         if (p.Cout <= 64 && big == 256)
             launch_dma_t<1, 256, 64, 4>(p, st);
         else if (p.Cout <= 64 && big == 64)
