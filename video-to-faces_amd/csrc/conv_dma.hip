@@ -322,10 +322,16 @@ __global__ __launch_bounds__(256, OCC) void k_conv_dma(ConvParams p) {
 // by contiguous DMA, and every k-step's A fragment row is read from it at the lane's row offset
 // idx(m) - idx(m0) + kh W + kw.  The implicit-GEMM gather fetched each input piece once per tap
 // (9x for 3x3); here the tile's A traffic is its span.  B (weights) streams per k-step through NS
-// LDS stages as in k_conv_dma.  Span rows are 128 Q bytes, 16-B slot s of each 128-B group of row
-// r holding source slot s ^ ((r >> 1) & 7) (planes reordered [x0 of 4 chunks | x1 of 4 chunks] as
-// in MODE 1).  k order (tap-major, then channel) and MFMA chains are k_conv_dma MODE 1's: the
-// same bits when that kernel does not split K.
+// LDS stages as in k_conv_dma.  Span rows are 128 Q bytes (a pixel's 8 Q logical 16-B slots: per
+// 32-channel group [x0 of 4 chunks | x1 of 4 chunks] as in MODE 1), swizzled by a key of the
+// pixel (n, y, x) in OUTPUT-linear coordinates, v = n OH OW + y OW + x: the 16 rows of a fragment
+// read pixels with 16 consecutive v for every tap (v = m + kh OW + kw), while their span rows jump
+// at output-row and image wraps (by an odd count for valid convs: KW - 1 + 1 and the image tail).
+// Q = 1: physical slot = ls ^ ((v >> 1) & 7) -- the two lanes sharing a key are consecutive
+// outputs, i.e. rows of opposite parity (opposite 128-B bank halves); Q = 2: slot over the whole
+// 256-B row = (8 g + ls) ^ (v & 15).  Both conflict-free for the ds_read_b128 fragment reads.
+// k order (tap-major, then channel) and MFMA chains are k_conv_dma MODE 1's: the same bits when
+// that kernel does not split K.
 template <int Q, int BM, int BN, int WGM, int SPAN, int OCC, int NS>
 struct SCfg {
     static constexpr int WGN = 4 / WGM, WM = BM / WGM, WN = BN / WGN, FM = WM / 16, FN = WN / 16;
@@ -386,11 +392,23 @@ __global__ __launch_bounds__(256, OCC) void k_conv_span(ConvParams p) {
     const int nA = (span * RBA + 1023) >> 10;
     for (int j = wave; j < nA; j += 4) {
         const int off = j * 1024 + lane * 16;
-        const int row = off / RBA, g = (off % RBA) >> 7, s = (off >> 4) & 7;
-        const int sp = s ^ ((row >> 1) & 7);
+        const int row = off / RBA;
         const int64_t pix = P0 + row;
+        // the pixel's swizzle key: v = n OH OW + y OW + x (mod 16) of its (n, y, x)
+        const int64_t n = pix / HW;
+        const int rem = (int)(pix - n * HW), y = rem / p.W, x = rem - y * p.W;
+        const int v = (int)((n * OHW) & 15) + y * p.OW + x;
+        int g, ls;
+        if (Q == 1) {
+            g = 0;
+            ls = ((off >> 4) & 7) ^ ((v >> 1) & 7);
+        } else {
+            const int lg = ((off >> 4) & 15) ^ (v & 15);
+            g = lg >> 3;
+            ls = lg & 7;
+        }
         const char* src =
-            row < span && pix < npix ? in + pix * (128 * Q) + g * 128 + (sp & 3) * 32 + (sp >> 2) * 16 : zero;
+            row < span && pix < npix ? in + pix * (128 * Q) + g * 128 + (ls & 3) * 32 + (ls >> 2) * 16 : zero;
         __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)src,
                                          (void __attribute__((address_space(3)))*)(smem + off), 16, 0, 0);
     }
@@ -412,9 +430,13 @@ __global__ __launch_bounds__(256, OCC) void k_conv_span(ConvParams p) {
                                              16, 0, 0);
     };
     // the lane's A rows (span-relative) of its FM fragments; rows past M repeat the last row
-    int arow[FM];
+    int arow[FM], akey[FM];
 #pragma unroll
-    for (int i = 0; i < FM; i++) arow[i] = (int)(idx(min(m0 + wm * C::WM + i * 16 + (lane & 15), mlast)) - P0);
+    for (int i = 0; i < FM; i++) {
+        const int64_t m = min(m0 + wm * C::WM + i * 16 + (lane & 15), mlast);
+        arow[i] = (int)(idx(m) - P0);
+        akey[i] = (int)(m & 15);  // + kh OW + kw: the swizzle key of the pixel a tap reads
+    }
     f4 acc[FM][FN], accx[FM][FN];
 #pragma unroll
     for (int i = 0; i < FM; i++)
@@ -452,13 +474,21 @@ __global__ __launch_bounds__(256, OCC) void k_conv_span(ConvParams p) {
             b0[j] = *(const h8*)(Bs + j * 16 * 128 + o0);
             b1[j] = *(const h8*)(Bs + j * 16 * 128 + o1);
         }
-        const int toff = kh * p.W + kw;
+        const int toff = kh * p.W + kw, tkey = kh * p.OW + kw;
 #pragma unroll
         for (int i = 0; i < FM; i++) {
-            const int r = arow[i] + toff, sw = (r >> 1) & 7;
-            const char* Ar = smem + r * RBA + g * 128;
-            const h8 a0 = *(const h8*)(Ar + (((lane >> 4) ^ sw) << 4));
-            const h8 a1 = *(const h8*)(Ar + (((4 + (lane >> 4)) ^ sw) << 4));
+            const int v = akey[i] + tkey;
+            const char* Ar = smem + (arow[i] + toff) * RBA;
+            int s0, s1;
+            if (Q == 1) {
+                s0 = (lane >> 4) ^ ((v >> 1) & 7);
+                s1 = (4 + (lane >> 4)) ^ ((v >> 1) & 7);
+            } else {
+                s0 = (8 * g + (lane >> 4)) ^ (v & 15);
+                s1 = (8 * g + 4 + (lane >> 4)) ^ (v & 15);
+            }
+            const h8 a0 = *(const h8*)(Ar + (s0 << 4));
+            const h8 a1 = *(const h8*)(Ar + (s1 << 4));
 #pragma unroll
             for (int j = 0; j < FN; j++) {
                 acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a0, b0[j], acc[i][j], 0, 0, 0);
@@ -792,14 +822,15 @@ void launch_span_t(ConvParams p, hipStream_t st) {
     k_conv_span<Q, BM, BN, WGM, SPAN, OCC, NS><<<(unsigned)p.dp_tiles, 256, 0, st>>>(p);
 }
 
-// span-mode eligibility (split-pair, stride-1 unpadded convs of 32 / 64 input channels whose
+// span-mode eligibility (split-pair, stride-1 unpadded convs of 32 / 64 input channels, odd KW
+// (the swizzle pairs need odd row jumps), whose
 // tiles' input runs fit the LDS span); env VTF_CONV_SPAN=0 keeps the implicit-GEMM gather
 constexpr int SPAN_BM = 128, SPAN_ROWS = 240;
 bool conv_span_ok(const ConvParams& p) {
     const char* e = std::getenv("VTF_CONV_SPAN");  // read per launch: tests A/B both paths in one process
     return (!e || std::atoi(e) != 0) && p.in_sp && !p.s3 && p.sh == 1 && p.sw == 1 && p.ph == 0 && p.pw == 0 &&
            (p.Cin == 32 || p.Cin == 64) && (p.in_cstride == 0 || p.in_cstride == p.Cin) && p.Cout <= 64 &&
-           p.KH * p.KW >= 4 && !p.n_split && !p.res && !p.up2 && !p.res_up2 &&
+           p.KH * p.KW >= 4 && (p.KW & 1) && !p.n_split && !p.res && !p.up2 && !p.res_up2 &&
            conv_span_max(p, SPAN_BM) <= SPAN_ROWS;
 }
 

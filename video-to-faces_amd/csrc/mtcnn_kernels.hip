@@ -637,12 +637,14 @@ __global__ __launch_bounds__(256, PNET_GROUPS_PER_CU) void k_pnet(const uint8_t*
             // pooled-map slot of the lane's output: channel lrx of cell 4f + lkx (lanes 12..15 repeat
             // channels 10, 11, which conv2 never reads)
             const int qlane = lkx * PQ_C + (lrx < 12 ? lrx : 10 + (lrx & 1));
-            auto conv1_frags = [&](auto exact_t) {
-            constexpr bool EX = decltype(exact_t)::value;
             // fragments per iteration: the exact path holds one operand plane, so twice the
-            // fragments fit the same registers (more independent MFMA chains per wave)
-            constexpr int NU = EX ? 4 : 2;
-            for (int f0 = wv; f0 < NF1; f0 += 4 * NU) {
+            // fragments fit the same registers (more independent MFMA chains per wave); whole
+            // iterations first, then the remaining fragments one per wave (NU = 1) instead of an
+            // iteration padded with clamped (recomputed) fragments
+            auto conv1_frags = [&](auto exact_t, auto nu_t, int f0) -> int {
+            constexpr bool EX = decltype(exact_t)::value;
+            constexpr int NU = decltype(nu_t)::value;
+            for (; f0 + 4 * (NU - 1) < NF1; f0 += 4 * NU) {
                 int ab[NU];
 #pragma unroll
                 for (int u = 0; u < NU; u++) {
@@ -736,11 +738,14 @@ __global__ __launch_bounds__(256, PNET_GROUPS_PER_CU) void k_pnet(const uint8_t*
                     q[NPP * PQ_C] = x1;
                 }
             }
+            return f0;
             };
             if (exact)
-                conv1_frags(std::true_type{});
+                conv1_frags(std::true_type{}, std::integral_constant<int, 1>{},
+                            conv1_frags(std::true_type{}, std::integral_constant<int, 4>{}, wv));
             else
-                conv1_frags(std::false_type{});
+                conv1_frags(std::false_type{}, std::integral_constant<int, 1>{},
+                            conv1_frags(std::false_type{}, std::integral_constant<int, 2>{}, wv));
         }
         {
             constexpr int NPP = PP_H * PP_W;        // pooled cells
@@ -870,14 +875,23 @@ __global__ __launch_bounds__(256, PNET_GROUPS_PER_CU) void k_pnet(const uint8_t*
                         x[2][1][pl] = __builtin_bit_cast(f16x8, u1);
                     }
                     f32x4 c0 = {0.f, 0.f, 0.f, 0.f}, c1 = c0, d0 = c0, d1 = c0;
+                    if (two) {
 #pragma unroll
-                    for (int s3 = 0; s3 < 3; s3++) {
-                        c0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(w0[s3], x[s3][0][0], c0, 0, 0, 0);
-                        d0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(w1[s3], x[s3][0][0], d0, 0, 0, 0);
-                        d0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(w0[s3], x[s3][0][1], d0, 0, 0, 0);
-                        c1 = __builtin_amdgcn_mfma_f32_16x16x32_f16(w0[s3], x[s3][1][0], c1, 0, 0, 0);
-                        d1 = __builtin_amdgcn_mfma_f32_16x16x32_f16(w1[s3], x[s3][1][0], d1, 0, 0, 0);
-                        d1 = __builtin_amdgcn_mfma_f32_16x16x32_f16(w0[s3], x[s3][1][1], d1, 0, 0, 0);
+                        for (int s3 = 0; s3 < 3; s3++) {
+                            c0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(w0[s3], x[s3][0][0], c0, 0, 0, 0);
+                            d0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(w1[s3], x[s3][0][0], d0, 0, 0, 0);
+                            d0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(w0[s3], x[s3][0][1], d0, 0, 0, 0);
+                            c1 = __builtin_amdgcn_mfma_f32_16x16x32_f16(w0[s3], x[s3][1][0], c1, 0, 0, 0);
+                            d1 = __builtin_amdgcn_mfma_f32_16x16x32_f16(w1[s3], x[s3][1][0], d1, 0, 0, 0);
+                            d1 = __builtin_amdgcn_mfma_f32_16x16x32_f16(w0[s3], x[s3][1][1], d1, 0, 0, 0);
+                        }
+                    } else {  // the wave's last fragment has no partner (wave-uniform): one chain pair
+#pragma unroll
+                        for (int s3 = 0; s3 < 3; s3++) {
+                            c0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(w0[s3], x[s3][0][0], c0, 0, 0, 0);
+                            d0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(w1[s3], x[s3][0][0], d0, 0, 0, 0);
+                            d0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(w0[s3], x[s3][0][1], d0, 0, 0, 0);
+                        }
                     }
 #pragma unroll
                     for (int h = 0; h < 2; h++) {
