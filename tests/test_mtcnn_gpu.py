@@ -200,3 +200,22 @@ def test_span_convs_match_gather_path(ms, monkeypatch):
     assert sum(x.shape[0] for x in a) > 0
     for x, y in zip(a, b):
         np.testing.assert_allclose(x, y, rtol=1e-5, atol=2e-3)
+
+
+@pytest.mark.parametrize('ms', [5, 20])
+def test_span_pool_fusion_matches_separate_pool(ms, monkeypatch):
+    """RNet conv2 + pool1 and ONet conv2 + pool1 as one launch (k_conv_span_pool: pool-aligned
+    tiles, the conv map kept in LDS, only the pooled split pairs written; default) against the
+    span conv + separate max-pool launch (VTF_CONV_SPAN_POOL=0): same detections, boxes and scores
+    within the e2e tolerance (the same conv sums; the pool and the split are exact)."""
+    from videotofaces import synth
+    from videotofaces.detectors.mtcnn import MTCNN
+    fr = torch.from_numpy(synth.make_frames(4, seed=29)).cuda()
+    m = MTCNN('cuda:0')
+    a = m(fr, ms)
+    monkeypatch.setenv('VTF_CONV_SPAN_POOL', '0')
+    b = m(fr, ms)
+    assert [x.shape for x in a] == [y.shape for y in b]
+    assert sum(x.shape[0] for x in a) > 0
+    for x, y in zip(a, b):
+        np.testing.assert_allclose(x, y, rtol=1e-5, atol=2e-3)

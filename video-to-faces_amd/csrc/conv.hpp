@@ -60,6 +60,10 @@ bool conv_dma_ok(const ConvParams& p);
 // bf16 layer -> 0 k_conv, 1 conv_dma large tiles, 2 conv_dma 64 x 64 3-stage tiles (measured per shape)
 int conv_dma_choice_bf16(const ConvParams& p);
 void launch_conv_dma(const ConvParams& p, bool bf16, hipStream_t st);
+// split-pair conv (bias + PReLU) fused with MaxPool2d(k, s, ceil_mode=True) writing the pooled map
+// in split pairs (conv_dma.hip, k_conv_span_pool); returns false, launching nothing, when the
+// shape does not fit the fused tiles (env VTF_CONV_SPAN_POOL=0: never)
+bool launch_conv_span_pool(ConvParams p, int k, int s, void* pout, int& POH, int& POW, hipStream_t st);
 void launch_maxpool(const void* in, int N, int H, int W, int C, void* out, int out_cstride, int out_coff, bool bf16,
                     hipStream_t st);
 // torch MaxPool2d(k, s, ceil_mode) without padding, NHWC fp32; returns (OH, OW)

@@ -521,6 +521,178 @@ __global__ __launch_bounds__(256, OCC) void k_conv_span(ConvParams p) {
     dma_epilogue<float, BN>(p, E, BM, m0, n0);
 }
 
+// ---------------------------------------------------------------- span mode + fused max-pool
+// The span kernel for a conv followed by MaxPool2d(pk, ps, ceil) (RNet conv2 -> pool1, ONet
+// conv2 -> pool1; mtcnn.py:41-121): tiles are aligned to the pool instead of to BM rows -- a tile
+// is `cg` whole candidates (parts = 1) or one of `parts` row bands of one candidate, a band being
+// the conv rows its pool rows read (ONet: pool rows 0-4 <- conv rows 0-10, 5-9 <- 10-20; the
+// shared row is computed twice).  The conv tile (bias + PReLU applied) stays in LDS and the
+// workgroup writes only the pooled map, in the split-pair layout with the range flag: the conv
+// output never goes to HBM and the separate pool launch is gone.  M-row r of a tile = (candidate
+// cl, band row y, column x), r = (cl RP + y) OW + x; its span row = cl H W + y W + x (+ kh W + kw
+// per tap) relative to the band's first input pixel; the swizzle key is r + kh OW + kw, the
+// k_conv_span argument (row jumps at x / candidate wraps are KW and KH W - OW + 1: odd).
+struct SpanPool {
+    int k, s, POH, POW;  // pool window, stride, pooled map
+    int cg, parts;       // candidates per tile (parts = 1) / bands per candidate (cg = 1)
+    int RP, PH2;         // conv rows per band (max), pool rows per band
+    void* out;           // pooled map [N][POH][POW][Cout] split pairs
+};
+
+template <int BM, int BN, int SPAN>
+struct SPCfg {
+    static constexpr int WM = BM / 4, FM = WM / 16, FN = BN / 16;  // 4 waves x (WM rows, all BN cols)
+    static constexpr int A_BYTES = SPAN * 128, B_ST = BN * 128, LDE = BN + 4;
+    static constexpr int SM0 = A_BYTES + 2 * B_ST;
+    static constexpr int SM = SM0 > BM * LDE * 4 ? SM0 : BM * LDE * 4;
+    static constexpr int PB = BN / 32;
+    static_assert(SPAN % 8 == 0 && FM >= 1 && SM * 2 <= 160 * 1024, "span-pool tile");
+};
+
+template <int BM, int BN, int SPAN>
+__global__ __launch_bounds__(256, 2) void k_conv_span_pool(ConvParams p, SpanPool sp) {
+    using C = SPCfg<BM, BN, SPAN>;
+    constexpr int FM = C::FM, FN = C::FN, PB = C::PB;
+    __shared__ __attribute__((aligned(16))) char smem[C::SM];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int t = blockIdx.x;
+    const int HW = p.H * p.W;
+    // the tile: candidates n0 .. n0 + ncand - 1, conv rows oy0 .. oy0 + rp - 1, pool rows py0 .. py1 - 1
+    const int n0 = sp.parts == 1 ? t * sp.cg : t / sp.parts, part = sp.parts == 1 ? 0 : t % sp.parts;
+    const int ncand = min(sp.cg, p.N - n0);
+    const int py0 = part * sp.PH2, py1 = min(sp.POH, py0 + sp.PH2);
+    const int oy0 = py0 * sp.s, rp = min(p.OH, (py1 - 1) * sp.s + sp.k) - oy0;
+    const int rows = ncand * rp * p.OW;  // valid M rows of the tile (<= BM, host-checked)
+    const int64_t P0 = (int64_t)n0 * HW + (int64_t)oy0 * p.W;
+    const int span = (ncand - 1) * HW + (rp + p.KH - 1) * p.W;  // <= SPAN (host-checked)
+    const char* in = (const char*)p.in;
+    const char* wt = (const char*)p.w;
+    const char* zero = (const char*)p.zero;
+    // span DMA: pixel L = (cl, y, x) of the band, key v = (cl rp + y) OW + x
+    const int nA = (span * 128 + 1023) >> 10;
+    for (int j = wave; j < nA; j += 4) {
+        const int off = j * 1024 + lane * 16, row = off >> 7;
+        const int cl = row / HW, rem = row - cl * HW, y = rem / p.W, x = rem - y * p.W;
+        const int v = (cl * rp + y) * p.OW + x;
+        const int ls = ((off >> 4) & 7) ^ ((v >> 1) & 7);
+        const char* src = row < span ? in + (P0 + row) * 128 + (ls & 3) * 32 + (ls >> 2) * 16 : zero;
+        __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)src,
+                                         (void __attribute__((address_space(3)))*)(smem + off), 16, 0, 0);
+    }
+    const int bsrc = (lane & 7) ^ (((lane >> 4) + 4 * (wave & 1)) & 7);
+    int64_t bbase[PB];
+#pragma unroll
+    for (int j = 0; j < PB; j++) {
+        const int n = min(32 * j + 8 * wave + (lane >> 3), p.Cout - 1);
+        bbase[j] = (int64_t)n * p.K * 4 + (bsrc >> 2) * 16 + (bsrc & 3) * 32;
+    }
+    char* Bst = smem + C::A_BYTES;
+    auto issueB = [&](int kt, int s) {
+#pragma unroll
+        for (int j = 0; j < PB; j++)
+            __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)(wt + bbase[j] + (int64_t)kt * 128),
+                                             (void __attribute__((address_space(3)))*)(Bst + s * C::B_ST + (wave + 4 * j) * 1024),
+                                             16, 0, 0);
+    };
+    int arow[FM], akey[FM];
+#pragma unroll
+    for (int i = 0; i < FM; i++) {
+        const int r = min(wave * C::WM + i * 16 + (lane & 15), rows - 1);
+        const int cl = r / (rp * p.OW), q = r - cl * rp * p.OW, y = q / p.OW;
+        arow[i] = cl * HW + y * p.W + (q - y * p.OW);
+        akey[i] = r;
+    }
+    f4 acc[FM][FN], accx[FM][FN];
+#pragma unroll
+    for (int i = 0; i < FM; i++)
+#pragma unroll
+        for (int j = 0; j < FN; j++) acc[i][j] = accx[i][j] = f4{0.f, 0.f, 0.f, 0.f};
+    const int hsw = (lane & 15) >> 1;
+    const int o0 = (lane & 15) * 128 + (((lane >> 4) ^ hsw) << 4);
+    const int o1 = (lane & 15) * 128 + (((4 + (lane >> 4)) ^ hsw) << 4);
+    const int KT = p.K >> 5;
+    issueB(0, 0);
+    int kh = 0, kw = 0;
+    for (int kt = 0; kt < KT; kt++) {
+        wait_vm_barrier<0>();
+        if (kt + 1 < KT) issueB(kt + 1, (kt + 1) & 1);
+        const char* Bs = Bst + (kt & 1) * C::B_ST;
+        h8 b0[FN], b1[FN];
+#pragma unroll
+        for (int j = 0; j < FN; j++) {
+            b0[j] = *(const h8*)(Bs + j * 16 * 128 + o0);
+            b1[j] = *(const h8*)(Bs + j * 16 * 128 + o1);
+        }
+        const int toff = kh * p.W + kw, tkey = kh * p.OW + kw;
+#pragma unroll
+        for (int i = 0; i < FM; i++) {
+            const int sw = ((akey[i] + tkey) >> 1) & 7;
+            const char* Ar = smem + (arow[i] + toff) * 128;
+            const h8 a0 = *(const h8*)(Ar + (((lane >> 4) ^ sw) << 4));
+            const h8 a1 = *(const h8*)(Ar + (((4 + (lane >> 4)) ^ sw) << 4));
+#pragma unroll
+            for (int j = 0; j < FN; j++) {
+                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a0, b0[j], acc[i][j], 0, 0, 0);
+                accx[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a0, b1[j], accx[i][j], 0, 0, 0);
+                accx[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a1, b0[j], accx[i][j], 0, 0, 0);
+            }
+        }
+        if (++kw == p.KW) {
+            kw = 0;
+            kh++;
+        }
+    }
+    __syncthreads();  // no DMA outstanding; the span and the stages are free for the tile image
+    // conv epilogue into LDS: v = acc + 2^-11 accx, + bias, PReLU (conv_epilogue8's order)
+    float* E = (float*)smem;
+#pragma unroll
+    for (int j = 0; j < FN; j++) {
+        const int c = min(j * 16 + (lane & 15), p.Cout - 1);
+        const float bb = p.bias ? p.bias[c] : 0.f, pa = p.prelu ? p.prelu[c] : 0.f;
+#pragma unroll
+        for (int i = 0; i < FM; i++)
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                float x = acc[i][j][q] + accx[i][j][q] * 0.00048828125f;
+                if (p.bias) x = x + bb;
+                if (p.prelu) x = x > 0.f ? x : pa * x;
+                E[(wave * C::WM + i * 16 + 4 * (lane >> 4) + q) * C::LDE + j * 16 + (lane & 15)] = x;
+            }
+    }
+    __syncthreads();
+    // max-pool of the band (windows clipped at the conv map's last row / column, ceil mode) ->
+    // split pairs, 8 channels per item
+    const int C8 = p.Cout >> 3, npy = py1 - py0;
+    const int items = ncand * npy * sp.POW * C8;
+    bool bad = false;
+    for (int it = tid; it < items; it += 256) {
+        const int c8 = it % C8, q = it / C8, px = q % sp.POW, q2 = q / sp.POW, pyl = q2 % npy, cl = q2 / npy;
+        const int py = py0 + pyl;
+        float m[8];
+#pragma unroll
+        for (int e = 0; e < 8; e++) m[e] = -3.402823466e38f;
+        for (int dy = 0; dy < sp.k; dy++) {
+            const int y = py * sp.s + dy;
+            if (y >= p.OH) break;
+            for (int dx = 0; dx < sp.k; dx++) {
+                const int x = px * sp.s + dx;
+                if (x >= p.OW) break;
+                const float* e = E + ((cl * rp + (y - oy0)) * p.OW + x) * C::LDE + 8 * c8;
+                const f4 lo = *(const f4*)e, hi = *(const f4*)(e + 4);
+#pragma unroll
+                for (int u = 0; u < 4; u++) {
+                    m[u] = fmaxf(m[u], lo[u]);
+                    m[4 + u] = fmaxf(m[4 + u], hi[u]);
+                }
+            }
+        }
+        char* orow = (char*)sp.out + (((int64_t)(n0 + cl) * sp.POH + py) * sp.POW + px) * (int64_t)p.Cout * 4;
+        sp_store4(orow, 8 * c8, m[0], m[1], m[2], m[3], bad);
+        sp_store4(orow, 8 * c8 + 4, m[4], m[5], m[6], m[7], bad);
+    }
+    if (p.ovf && __ballot(bad) && lane == 0) atomicOr(p.ovf, 1);
+}
+
 // ---------------------------------------------------------------- MODE 2: bf16x3 (fp32-grade)
 // Operands in the split-triple layout (conv_dev.hpp: x = b0 + b1 + b2, three bf16 terms of 8
 // significant bits each), so every fp32 product is x w = b0 w0 + [b0 w1 + b1 w0 + b0 w2 + b1 w1 +
@@ -869,6 +1041,51 @@ void launch_dma3_t(ConvParams p, hipStream_t st) {
 }
 
 }  // namespace
+
+// conv (split pairs, bias + PReLU) + MaxPool2d(k, s, ceil_mode=True) in one launch
+// (k_conv_span_pool); false (nothing launched) when the shape does not fit its tiles
+constexpr int SPOOL_BM = 256, SPOOL_SPAN = 368;
+bool launch_conv_span_pool(ConvParams p, int k, int s, void* pout, int& POH, int& POW, hipStream_t st) {
+    const char* e = std::getenv("VTF_CONV_SPAN_POOL");
+    if ((e && std::atoi(e) == 0) || !p.in_sp || p.s3 || p.sh != 1 || p.sw != 1 || p.ph || p.pw || p.Cin != 32 ||
+        (p.in_cstride && p.in_cstride != p.Cin) || p.Cout > 64 || p.Cout % 8 || !(p.KW & 1) || p.res || p.up2 ||
+        p.n_split || p.alpha || p.relu || p.leaky || p.gelu || p.scale != 1.f || p.out_sp || p.N <= 0)
+        return false;
+    auto pool_out = [](int L, int k_, int s_) {  // torch pooling_output_shape, padding 0, ceil_mode
+        int o = ((L - k_ + s_ - 1) / s_) + 1;
+        if ((o - 1) * s_ >= L) o--;
+        return o;
+    };
+    SpanPool sp{};
+    sp.k = k;
+    sp.s = s;
+    sp.POH = pool_out(p.OH, k, s);
+    sp.POW = pool_out(p.OW, k, s);
+    sp.out = pout;
+    const int HW = p.H * p.W;
+    if (p.OH * p.OW <= SPOOL_BM) {
+        sp.parts = 1;
+        sp.cg = SPOOL_BM / (p.OH * p.OW);
+        sp.PH2 = sp.POH;
+        sp.RP = p.OH;
+    } else {
+        sp.cg = 1;
+        for (sp.parts = 2; sp.parts <= sp.POH; sp.parts++) {
+            sp.PH2 = (sp.POH + sp.parts - 1) / sp.parts;
+            sp.RP = std::min(p.OH, (sp.PH2 - 1) * s + k);
+            if (sp.RP * p.OW <= SPOOL_BM) break;
+        }
+        if (sp.parts > sp.POH) return false;
+    }
+    const int span = (sp.cg - 1) * HW + (sp.RP + p.KH - 1) * p.W;
+    if (span > SPOOL_SPAN || sp.cg * sp.RP * p.OW > SPOOL_BM) return false;
+    p.zero = zero_page(stream_device(st));
+    const int grid = sp.parts == 1 ? (int)cdiv(p.N, sp.cg) : p.N * sp.parts;
+    k_conv_span_pool<SPOOL_BM, 64, SPOOL_SPAN><<<(unsigned)grid, 256, 0, st>>>(p, sp);
+    POH = sp.POH;
+    POW = sp.POW;
+    return true;
+}
 
 bool conv_dma_ok(const ConvParams& p) {
     // the 16-B pieces need 8-channel granules; the staged epilogue 8-channel groups

@@ -563,6 +563,19 @@ static void run_candidates_sp(Mtcnn& m, bool onet, const void* x0, int64_t n, fl
         p.ovf = m.d_ovf;
         p.split_fp32 = 1;  // slice-order reduction of small grids (parity is a tolerance here)
         VTF_CHECK(C == L.cin && L.sp, VTF_E_ARG, "candidate net channel mismatch");
+        if (pool) {
+            // conv + pool in one launch when the shape fits (RNet conv2, ONet conv2): the conv
+            // map stays in LDS, only the pooled split pairs are written
+            float* pout = (out == X) ? Y : X;
+            int OH, OW;
+            if (launch_conv_span_pool(p, pk[li], 2, pout, OH, OW, m.st)) {
+                H = OH;
+                W = OW;
+                C = L.cout;
+                cur = pout;
+                continue;
+            }
+        }
         launch_conv_dma(p, false, m.st);
         H = p.OH;
         W = p.OW;
