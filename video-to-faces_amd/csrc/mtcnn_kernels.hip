@@ -1505,8 +1505,16 @@ void launch_cand_front(bool onet, const int4* sat, int H, int W, const float4* b
         const char* e = std::getenv("VTF_FRONT_DEBUG");
         return e ? std::atoi(e) : 0;
     }();
+    // pool rows per band of the ONet front (VTF_FRONT_PB, experiments): more rows per band = fewer
+    // barriers and more conv fragments per band for the 8 waves, against a larger conv ring
+    const char* pbe = std::getenv("VTF_FRONT_PB");
+    const int pb = pbe ? std::atoi(pbe) : 1;
     // w1h (split conv1 planes) selects conv1 on fp16 matrix cores; null keeps the fp32 MFMA path
-    if (onet && w1h)
+    if (onet && w1h && pb == 2)
+        k_cand_front<48, 2, 512, true><<<(unsigned)n, 512, 0, st>>>(sat, H, W, boxes, img, w1, w1h, b1, a1, out, err, dbg, ovf);
+    else if (onet && w1h && pb == 3)
+        k_cand_front<48, 3, 512, true><<<(unsigned)n, 512, 0, st>>>(sat, H, W, boxes, img, w1, w1h, b1, a1, out, err, dbg, ovf);
+    else if (onet && w1h)
         k_cand_front<48, 1, 512, true><<<(unsigned)n, 512, 0, st>>>(sat, H, W, boxes, img, w1, w1h, b1, a1, out, err, dbg, ovf);
     else if (onet)
         k_cand_front<48, 1, 512, false><<<(unsigned)n, 512, 0, st>>>(sat, H, W, boxes, img, w1, w1h, b1, a1, out, err, dbg, ovf);
