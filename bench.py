@@ -659,7 +659,11 @@ def run_gpu(args):
             'config': {'workload': workload, 'baseline_config': args.config, 'det_batch': args.det_batch if det else None,
                        'enc_batch': args.enc_batch, 'frames_per_step_per_gpu': args.det_batch if det else 0,
                        'lanes': getattr(pipe, 'L', 1),
-                       'parallelism': 'dp%d (frame-sharded, RCCL all-gather of embeddings)' % ctx.world},
+                       'parallelism': 'dp%d (frame-sharded, RCCL all-gather of embeddings)' % ctx.world,
+                       # the reference writes face crops as JPEG files and re-reads them for the
+                       # encoder (detection.py -> encoders); here crops go from HBM frames to the
+                       # encoder without that round trip, as without video decode
+                       'excluded': 'video decode, JPEG write/read of crops, file moves'},
             'faces_per_frame': round(faces / max(1, frames_all), 3) if det else None,
             'frames_per_s': round(frames_all / elapsed, 2) if det else None,
             'embeddings_gathered': int(gathered.shape[0]),

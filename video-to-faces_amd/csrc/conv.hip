@@ -450,8 +450,17 @@ static int pick_split(int64_t tiles, int KT, bool bf16, bool fp32_split) {
     // bf16: grids below 192 tiles; fp32 callers that accept a slice-order reduction
     // (split_fp32: ONet's dense layer, 120 tiles of K = 1152: 72 -> 51 us with the epilogue
     // kernel; RNet's 196 tiles of K = 576 measured slower split) below 160
-    if (!(bf16 || fp32_split) || tiles >= (bf16 ? 192 : 160) || KT < 8) return 1;
-    int s = (int)std::min<int64_t>(8, (512 + tiles - 1) / tiles);
+    // (VTF_SPLIT_TILES / VTF_SPLIT_WG: the bf16 tile threshold and workgroup target, experiments)
+    static const int thr = [] {
+        const char* e = std::getenv("VTF_SPLIT_TILES");
+        return e ? std::atoi(e) : 192;
+    }();
+    static const int tgt = [] {
+        const char* e = std::getenv("VTF_SPLIT_WG");
+        return e ? std::atoi(e) : 512;
+    }();
+    if (!(bf16 || fp32_split) || tiles >= (bf16 ? thr : 160) || KT < 8) return 1;
+    int s = (int)std::min<int64_t>(8, ((bf16 ? tgt : 512) + tiles - 1) / tiles);
     s = std::min(s, KT / 4);
     return s < 2 ? 1 : s;
 }
