@@ -539,19 +539,20 @@ struct SpanPool {
     void* out;           // pooled map [N][POH][POW][Cout] split pairs
 };
 
-template <int BM, int BN, int SPAN>
+template <int BM, int BN, int SPAN, int NS>
 struct SPCfg {
     static constexpr int WM = BM / 4, FM = WM / 16, FN = BN / 16;  // 4 waves x (WM rows, all BN cols)
     static constexpr int A_BYTES = SPAN * 128, B_ST = BN * 128, LDE = BN + 4;
-    static constexpr int SM0 = A_BYTES + 2 * B_ST;
+    static constexpr int SM0 = A_BYTES + NS * B_ST;
     static constexpr int SM = SM0 > BM * LDE * 4 ? SM0 : BM * LDE * 4;
     static constexpr int PB = BN / 32;
-    static_assert(SPAN % 8 == 0 && FM >= 1 && SM * 2 <= 160 * 1024, "span-pool tile");
+    static_assert(SPAN % 8 == 0 && FM >= 1 && NS >= 2 && NS <= 4 && SM * 2 <= 160 * 1024, "span-pool tile");
 };
 
-template <int BM, int BN, int SPAN>
+// NS B stages: NS - 1 weight k-steps in flight
+template <int BM, int BN, int SPAN, int NS>
 __global__ __launch_bounds__(256, 2) void k_conv_span_pool(ConvParams p, SpanPool sp) {
-    using C = SPCfg<BM, BN, SPAN>;
+    using C = SPCfg<BM, BN, SPAN, NS>;
     constexpr int FM = C::FM, FN = C::FN, PB = C::PB;
     __shared__ __attribute__((aligned(16))) char smem[C::SM];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -611,12 +612,30 @@ __global__ __launch_bounds__(256, 2) void k_conv_span_pool(ConvParams p, SpanPoo
     const int o0 = (lane & 15) * 128 + (((lane >> 4) ^ hsw) << 4);
     const int o1 = (lane & 15) * 128 + (((4 + (lane >> 4)) ^ hsw) << 4);
     const int KT = p.K >> 5;
-    issueB(0, 0);
+    int issued = 0;
+#pragma unroll
+    for (int s = 0; s < NS - 1; s++)
+        if (issued < KT) {
+            issueB(issued, issued % NS);
+            issued++;
+        }
     int kh = 0, kw = 0;
     for (int kt = 0; kt < KT; kt++) {
-        wait_vm_barrier<0>();
-        if (kt + 1 < KT) issueB(kt + 1, (kt + 1) & 1);
-        const char* Bs = Bst + (kt & 1) * C::B_ST;
+        // counted vmcnt: this wave's B step kt (and the span, issued first) landed, the later
+        // steps may still be in flight; after the barrier for every wave, and step kt - 1's
+        // stage (the next issue's) is free
+        const int ahead = issued - kt - 1;
+        if (NS >= 4 && ahead >= 2)
+            wait_vm_barrier<(NS >= 4 ? 2 * PB : 0)>();
+        else if (NS >= 3 && ahead >= 1)
+            wait_vm_barrier<(NS >= 3 ? PB : 0)>();
+        else
+            wait_vm_barrier<0>();
+        if (issued < KT) {
+            issueB(issued, issued % NS);
+            issued++;
+        }
+        const char* Bs = Bst + (kt % NS) * C::B_ST;
         h8 b0[FN], b1[FN];
 #pragma unroll
         for (int j = 0; j < FN; j++) {
@@ -1081,7 +1100,18 @@ bool launch_conv_span_pool(ConvParams p, int k, int s, void* pout, int& POH, int
     if (span > SPOOL_SPAN || sp.cg * sp.RP * p.OW > SPOOL_BM) return false;
     p.zero = zero_page(stream_device(st));
     const int grid = sp.parts == 1 ? (int)cdiv(p.N, sp.cg) : p.N * sp.parts;
-    k_conv_span_pool<SPOOL_BM, 64, SPOOL_SPAN><<<(unsigned)grid, 256, 0, st>>>(p, sp);
+    // B stages (VTF_SPOOL_NS, experiments): 2 / 3 / 4 measured 288 / 292 / 295 us per launch on
+    // c2 (the weight round trip is not what bounds it)
+    static const int ns = [] {
+        const char* e = std::getenv("VTF_SPOOL_NS");
+        return e ? std::atoi(e) : 2;
+    }();
+    if (ns == 3)
+        k_conv_span_pool<SPOOL_BM, 64, SPOOL_SPAN, 3><<<(unsigned)grid, 256, 0, st>>>(p, sp);
+    else if (ns == 4)
+        k_conv_span_pool<SPOOL_BM, 64, SPOOL_SPAN, 4><<<(unsigned)grid, 256, 0, st>>>(p, sp);
+    else
+        k_conv_span_pool<SPOOL_BM, 64, SPOOL_SPAN, 2><<<(unsigned)grid, 256, 0, st>>>(p, sp);
     POH = sp.POH;
     POW = sp.POW;
     return true;
