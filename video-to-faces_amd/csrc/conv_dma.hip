@@ -332,6 +332,15 @@ __global__ __launch_bounds__(256, OCC) void k_conv_dma(ConvParams p) {
 // 256-B row = (8 g + ls) ^ (v & 15).  Both conflict-free for the ds_read_b128 fragment reads.
 // k order (tap-major, then channel) and MFMA chains are k_conv_dma MODE 1's: the same bits when
 // that kernel does not split K.
+// a / d for 0 <= a < 2^22 and small d through the float reciprocal inv = 1 / d, corrected to the
+// exact quotient (the span kernels' per-lane index math: ~6 VALU instead of an integer division)
+__device__ inline int qdiv(int a, int d, float inv) {
+    int q = (int)(((float)a + 0.5f) * inv);
+    q -= q * d > a;
+    q += (q + 1) * d <= a;
+    return q;
+}
+
 template <int Q, int BM, int BN, int WGM, int SPAN, int OCC, int NS>
 struct SCfg {
     static constexpr int WGN = 4 / WGM, WM = BM / WGM, WN = BN / WGN, FM = WM / 16, FN = WN / 16;
@@ -378,13 +387,18 @@ __global__ __launch_bounds__(256, OCC) void k_conv_span(ConvParams p) {
     const int n0 = tile_n * BN;
     const int64_t mlast = min(m0 + BM, p.M) - 1;
     const int OHW = p.OH * p.OW, HW = p.H * p.W;
-    auto idx = [&](int64_t m) -> int64_t {
-        const int64_t n = m / OHW;
-        const int r = (int)(m - n * OHW), oh = r / p.OW;
-        return n * HW + oh * p.W + (r - oh * p.OW);
+    const float iOHW = 1.f / OHW, iOW = 1.f / p.OW, iHW = 1.f / HW, iW = 1.f / p.W;
+    // the tile's first output (n0i, oh0, ow0) once; lanes work relative to it: output m of the
+    // tile (d = m - m0 < BM) has its input pixel at rel(d) from P0 = (n0i H + oh0) W + ow0
+    const int64_t n0i = m0 / OHW;
+    const int r0 = (int)(m0 - n0i * OHW), oh0 = qdiv(r0, p.OW, iOW), base0 = oh0 * p.W + (r0 - oh0 * p.OW);
+    auto rel = [&](int d) -> int {
+        const int mr = r0 + d, dn = qdiv(mr, OHW, iOHW), r = mr - dn * OHW, oh = qdiv(r, p.OW, iOW);
+        return dn * HW + oh * p.W + (r - oh * p.OW) - base0;
     };
-    const int64_t P0 = idx(m0), npix = (int64_t)p.N * HW;
-    const int span = (int)(idx(mlast) - P0) + (p.KH - 1) * p.W + p.KW;  // <= SPAN (host-checked)
+    const int64_t P0 = n0i * HW + base0, npix = (int64_t)p.N * HW;
+    const int span = rel((int)(mlast - m0)) + (p.KH - 1) * p.W + p.KW;  // <= SPAN (host-checked)
+    const int key0 = (int)((n0i * OHW) & 15);
     const char* in = (const char*)p.in;
     const char* wt = (const char*)p.w;
     const char* zero = (const char*)p.zero;
@@ -395,9 +409,8 @@ __global__ __launch_bounds__(256, OCC) void k_conv_span(ConvParams p) {
         const int row = off / RBA;
         const int64_t pix = P0 + row;
         // the pixel's swizzle key: v = n OH OW + y OW + x (mod 16) of its (n, y, x)
-        const int64_t n = pix / HW;
-        const int rem = (int)(pix - n * HW), y = rem / p.W, x = rem - y * p.W;
-        const int v = (int)((n * OHW) & 15) + y * p.OW + x;
+        const int loc = base0 + row, dn = qdiv(loc, HW, iHW), rem = loc - dn * HW, y = qdiv(rem, p.W, iW);
+        const int v = key0 + dn * OHW + y * p.OW + (rem - y * p.W);
         int g, ls;
         if (Q == 1) {
             g = 0;
@@ -433,9 +446,9 @@ __global__ __launch_bounds__(256, OCC) void k_conv_span(ConvParams p) {
     int arow[FM], akey[FM];
 #pragma unroll
     for (int i = 0; i < FM; i++) {
-        const int64_t m = min(m0 + wm * C::WM + i * 16 + (lane & 15), mlast);
-        arow[i] = (int)(idx(m) - P0);
-        akey[i] = (int)(m & 15);  // + kh OW + kw: the swizzle key of the pixel a tap reads
+        const int d = (int)min((int64_t)(wm * C::WM + i * 16 + (lane & 15)), mlast - m0);
+        arow[i] = rel(d);
+        akey[i] = (int)((m0 + d) & 15);  // + kh OW + kw: the swizzle key of the pixel a tap reads
     }
     f4 acc[FM][FN], accx[FM][FN];
 #pragma unroll
@@ -565,6 +578,8 @@ __global__ __launch_bounds__(256, 2) void k_conv_span_pool(ConvParams p, SpanPoo
     const int oy0 = py0 * sp.s, rp = min(p.OH, (py1 - 1) * sp.s + sp.k) - oy0;
     const int rows = ncand * rp * p.OW;  // valid M rows of the tile (<= BM, host-checked)
     const int64_t P0 = (int64_t)n0 * HW + (int64_t)oy0 * p.W;
+    const int RPW = rp * p.OW;
+    const float iHW = 1.f / HW, iW = 1.f / p.W, iOW = 1.f / p.OW, iRPW = 1.f / RPW;
     const int span = (ncand - 1) * HW + (rp + p.KH - 1) * p.W;  // <= SPAN (host-checked)
     const char* in = (const char*)p.in;
     const char* wt = (const char*)p.w;
@@ -573,7 +588,7 @@ __global__ __launch_bounds__(256, 2) void k_conv_span_pool(ConvParams p, SpanPoo
     const int nA = (span * 128 + 1023) >> 10;
     for (int j = wave; j < nA; j += 4) {
         const int off = j * 1024 + lane * 16, row = off >> 7;
-        const int cl = row / HW, rem = row - cl * HW, y = rem / p.W, x = rem - y * p.W;
+        const int cl = qdiv(row, HW, iHW), rem = row - cl * HW, y = qdiv(rem, p.W, iW), x = rem - y * p.W;
         const int v = (cl * rp + y) * p.OW + x;
         const int ls = ((off >> 4) & 7) ^ ((v >> 1) & 7);
         const char* src = row < span ? in + (P0 + row) * 128 + (ls & 3) * 32 + (ls >> 2) * 16 : zero;
@@ -599,7 +614,7 @@ __global__ __launch_bounds__(256, 2) void k_conv_span_pool(ConvParams p, SpanPoo
 #pragma unroll
     for (int i = 0; i < FM; i++) {
         const int r = min(wave * C::WM + i * 16 + (lane & 15), rows - 1);
-        const int cl = r / (rp * p.OW), q = r - cl * rp * p.OW, y = q / p.OW;
+        const int cl = qdiv(r, RPW, iRPW), q = r - cl * RPW, y = qdiv(q, p.OW, iOW);
         arow[i] = cl * HW + y * p.W + (q - y * p.OW);
         akey[i] = r;
     }
@@ -683,9 +698,11 @@ __global__ __launch_bounds__(256, 2) void k_conv_span_pool(ConvParams p, SpanPoo
     // split pairs, 8 channels per item
     const int C8 = p.Cout >> 3, npy = py1 - py0;
     const int items = ncand * npy * sp.POW * C8;
+    const float iC8 = 1.f / C8, iPOW = 1.f / sp.POW, iNPY = 1.f / npy;
     bool bad = false;
     for (int it = tid; it < items; it += 256) {
-        const int c8 = it % C8, q = it / C8, px = q % sp.POW, q2 = q / sp.POW, pyl = q2 % npy, cl = q2 / npy;
+        const int q = qdiv(it, C8, iC8), c8 = it - q * C8, q2 = qdiv(q, sp.POW, iPOW), px = q - q2 * sp.POW;
+        const int cl = qdiv(q2, npy, iNPY), pyl = q2 - cl * npy;
         const int py = py0 + pyl;
         float m[8];
 #pragma unroll
