@@ -327,9 +327,8 @@ __global__ __launch_bounds__(256, OCC) void k_conv_dma(ConvParams p) {
 // pixel (n, y, x) in OUTPUT-linear coordinates, v = n OH OW + y OW + x: the 16 rows of a fragment
 // read pixels with 16 consecutive v for every tap (v = m + kh OW + kw), while their span rows jump
 // at output-row and image wraps (by an odd count for valid convs: KW - 1 + 1 and the image tail).
-// Q = 1: physical slot = ls ^ ((v >> 1) & 7) -- the two lanes sharing a key are consecutive
-// outputs, i.e. rows of opposite parity (opposite 128-B bank halves); Q = 2: slot over the whole
-// 256-B row = (8 g + ls) ^ (v & 15).  Both conflict-free for the ds_read_b128 fragment reads.
+// Q = 1: physical slot = ls ^ span_key(v); Q = 2: slot over the whole 256-B row = (8 g + ls) ^
+// span_key16(v) -- conflict-free for ds_read_b128's lane groups (span_key).
 // k order (tap-major, then channel) and MFMA chains are k_conv_dma MODE 1's: the same bits when
 // that kernel does not split K.
 // a / d for 0 <= a < 2^22 and small d through the float reciprocal inv = 1 / d, corrected to the
@@ -340,6 +339,17 @@ __device__ inline int qdiv(int a, int d, float inv) {
     q += (q + 1) * d <= a;
     return q;
 }
+
+// span-row swizzle keys of a pixel with output-linear index v (the 16 rows of a fragment read 16
+// consecutive v under every tap, rows of alternating parity).  ds_read_b128 serves its 64 lanes in
+// four 16-lane groups, e.g. {0-3, 12-15, 20-27}: rows 0-3 and 12-15 at chunk a, rows 4-11 at
+// chunk a + 1.  With 128-B rows (bank half = row parity) a group is conflict-free iff, per parity
+// class, the slots chunk ^ key are distinct; key = v & 6 gives rows u, u + 8 (same key, same
+// parity) chunks a, a + 1 for every alignment of the 16 keys, so it is.  256-B rows (Q = 2) put the
+// parity bit into slot bit 3 instead.  (Searched exhaustively; (v >> 1) & 7 conflicts for odd-
+// aligned keys.)
+__device__ inline int span_key(int v) { return v & 6; }
+__device__ inline int span_key16(int v) { return (v & 6) | ((v & 1) << 3); }
 
 template <int Q, int BM, int BN, int WGM, int SPAN, int OCC, int NS>
 struct SCfg {
@@ -414,9 +424,9 @@ __global__ __launch_bounds__(256, OCC) void k_conv_span(ConvParams p) {
         int g, ls;
         if (Q == 1) {
             g = 0;
-            ls = ((off >> 4) & 7) ^ ((v >> 1) & 7);
+            ls = ((off >> 4) & 7) ^ span_key(v);
         } else {
-            const int lg = ((off >> 4) & 15) ^ (v & 15);
+            const int lg = ((off >> 4) & 15) ^ span_key16(v);
             g = lg >> 3;
             ls = lg & 7;
         }
@@ -494,11 +504,11 @@ __global__ __launch_bounds__(256, OCC) void k_conv_span(ConvParams p) {
             const char* Ar = smem + (arow[i] + toff) * RBA;
             int s0, s1;
             if (Q == 1) {
-                s0 = (lane >> 4) ^ ((v >> 1) & 7);
-                s1 = (4 + (lane >> 4)) ^ ((v >> 1) & 7);
+                s0 = (lane >> 4) ^ span_key(v);
+                s1 = (4 + (lane >> 4)) ^ span_key(v);
             } else {
-                s0 = (8 * g + (lane >> 4)) ^ (v & 15);
-                s1 = (8 * g + 4 + (lane >> 4)) ^ (v & 15);
+                s0 = (8 * g + (lane >> 4)) ^ span_key16(v);
+                s1 = (8 * g + 4 + (lane >> 4)) ^ span_key16(v);
             }
             const h8 a0 = *(const h8*)(Ar + (s0 << 4));
             const h8 a1 = *(const h8*)(Ar + (s1 << 4));
@@ -590,7 +600,7 @@ __global__ __launch_bounds__(256, 2) void k_conv_span_pool(ConvParams p, SpanPoo
         const int off = j * 1024 + lane * 16, row = off >> 7;
         const int cl = qdiv(row, HW, iHW), rem = row - cl * HW, y = qdiv(rem, p.W, iW), x = rem - y * p.W;
         const int v = (cl * rp + y) * p.OW + x;
-        const int ls = ((off >> 4) & 7) ^ ((v >> 1) & 7);
+        const int ls = ((off >> 4) & 7) ^ span_key(v);
         const char* src = row < span ? in + (P0 + row) * 128 + (ls & 3) * 32 + (ls >> 2) * 16 : zero;
         __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)src,
                                          (void __attribute__((address_space(3)))*)(smem + off), 16, 0, 0);
@@ -660,7 +670,7 @@ __global__ __launch_bounds__(256, 2) void k_conv_span_pool(ConvParams p, SpanPoo
         const int toff = kh * p.W + kw, tkey = kh * p.OW + kw;
 #pragma unroll
         for (int i = 0; i < FM; i++) {
-            const int sw = ((akey[i] + tkey) >> 1) & 7;
+            const int sw = span_key(akey[i] + tkey);
             const char* Ar = smem + (arow[i] + toff) * 128;
             const h8 a0 = *(const h8*)(Ar + (((lane >> 4) ^ sw) << 4));
             const h8 a1 = *(const h8*)(Ar + (((4 + (lane >> 4)) ^ sw) << 4));
