@@ -2,7 +2,7 @@
 # Round-2 re-entry check: GPU tests + smoke, then the default bench (config 2, 10k frames).
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
-O=gpurun_out/r02r
+O=gpurun_out/${1:-r02r}
 mkdir -p $O
 timeout -k 10 900 python -u -m pytest -x -v --timeout 300 --timeout-method thread -m gpu tests > $O/tests.log 2>&1
 rc=$?
