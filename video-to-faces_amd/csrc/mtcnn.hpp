@@ -1,4 +1,6 @@
 #pragma once
+#include <vector>
+
 #include "common.hpp"
 
 namespace vtf {
@@ -55,7 +57,9 @@ struct ResampleLevels {  // precomputed pyramid levels of one det-batch (k_resam
 void launch_resample_sat_multi(const int4* sat, int B, int H, int W, const ResampleLevels& lv, hipStream_t st);
 void launch_pnet(bool dense, const uint8_t* frames, int64_t frame_stride, int64_t row_stride, int H, int W,
                  const PNetLevel* d_levels, int n_levels, int64_t total_tiles, const PNetW& w, const PNetOut& o,
-                 uint32_t* d_tile_ctr, hipStream_t st);
+                 uint32_t* d_tile_ctr, hipStream_t st, int64_t exact_tiles = 0);
+// leading tiles of the level plan that k_pnet's exact-levels variant takes (see launch_pnet)
+int64_t pnet_exact_tiles(const std::vector<PNetLevel>& lv, int H, int W, int64_t total_tiles);
 int cand_front_side(bool onet);
 void launch_cand_front(bool onet, const int4* sat, int H, int W, const float4* boxes, const int32_t* img, int64_t n,
                        const float* w1, const _Float16* w1h, const float* b1, const float* a1, float* out, int32_t* err,

@@ -324,14 +324,31 @@ struct PatchIdx {
 constexpr int PNET_TILE_CHUNK = 4;
 constexpr int PNET_GROUPS_PER_CU = (160 * 1024) / ((PNET_LDS + 511) / 512 * 512);  // LDS granule: 512 B
 static_assert(PNET_GROUPS_PER_CU >= 2, "k_pnet tile too large for 2 workgroups per CU");
-constexpr int PATCH_BYTES = (P_POOL - 4) * 4;  // frame patch staged in the (not yet used) pooled buffer, pad excluded
 
-template <bool DENSE>
-__global__ __launch_bounds__(256, PNET_GROUPS_PER_CU) void k_pnet(const uint8_t* __restrict__ frames, int64_t frame_stride,
+// LDS plan per variant.  X (exact-levels variant, the upsampled levels that hold ~88 % of the tiles
+// at min_face_size 5): the level tile is one fp16 plane (8 B per pixel, x1 = 0), so sA only has to
+// hold the split conv2 output (+ the 4-float zero pad), and conv3's weights sit at the start of the
+// pooled buffer (the next tile's prefetched patch is stored after a barrier instead of beside
+// them): 40.4 KB -> four workgroups per CU instead of three.
+template <bool X>
+struct PnLds {
+    static constexpr int A = X ? P_C2 + 4 : P_A;                     // floats
+    static constexpr int POOL = X ? PQ_C * PP_H * PP_W : P_POOL;      // floats (split pooled conv1)
+    static constexpr int W3 = X ? 0 : P_W3;                           // conv3 weights (floats)
+    static constexpr int PATCH = (POOL - 4) * 4;                      // staged frame patch (bytes)
+    static constexpr int BYTES = (A + POOL) * 4 + (PL_H + PL_W) * 4 + 16 + 64;
+    static constexpr int GPC = (160 * 1024) / ((BYTES + 511) / 512 * 512);
+    static_assert(!X || (2 * P_C2 >= PL_H * PL_W * 4 + 4 && POOL >= 2 * 32 * W3_ROW / 2 && GPC >= 4),
+                  "exact-levels k_pnet LDS plan");
+};
+
+template <bool DENSE, bool X>
+__global__ __launch_bounds__(256, PnLds<X>::GPC) void k_pnet(const uint8_t* __restrict__ frames, int64_t frame_stride,
                                                  int64_t row_stride, int H, int W,
                                                  const PNetLevel* __restrict__ lv, int n_levels,
                                                  int64_t total_tiles, uint32_t* __restrict__ tile_ctr, PNetW wg,
-                                                 PNetOut o) {
+                                                 PNetOut o, int64_t tile_base) {
+    using LP = PnLds<X>;
     const auto wc = to_const(wg);
     // conv2 / conv3 weights through buffer loads: one lane VGPR offset + constant SGPR offsets,
     // instead of a 64-bit address per k-step (which the compiler would keep live across tiles);
@@ -341,9 +358,10 @@ __global__ __launch_bounds__(256, PNET_GROUPS_PER_CU) void k_pnet(const uint8_t*
     const __amdgpu_buffer_rsrc_t rw2h = __builtin_amdgcn_make_buffer_rsrc((void*)wg.c2h, 0, 2 * 16 * 96 * 2, 0x00020000);
     const __amdgpu_buffer_rsrc_t rw1h = __builtin_amdgcn_make_buffer_rsrc((void*)wg.c1h, 0, 2 * 16 * 64 * 2, 0x00020000);
     const __amdgpu_buffer_rsrc_t rhh = __builtin_amdgcn_make_buffer_rsrc((void*)wg.hh, 0, 2 * 16 * 32 * 2, 0x00020000);
-    const bool split3 = wg.c3h != nullptr;  // conv3 on fp16 matrix cores (mtcnn_runtime: range bound)
-    __shared__ __attribute__((aligned(16))) float sA[P_A];     // level tile, later conv2 output
-    __shared__ __attribute__((aligned(16))) float sP[P_POOL];  // frame patch (u8) during the fill, then pooled conv1
+    // conv3 on fp16 matrix cores (mtcnn_runtime: range bound); the X variant is launched only then
+    const bool split3 = X || wg.c3h != nullptr;
+    __shared__ __attribute__((aligned(16))) float sA[LP::A];     // level tile, later conv2 output
+    __shared__ __attribute__((aligned(16))) float sP[LP::POOL];  // frame patch (u8) during the fill, then pooled conv1
     __shared__ ushort2 ybin[PL_H], xbin[PL_W];  // frame bin [start, end) of each level row / column
     __shared__ int s_tile, s_next, s_cend;
     __shared__ unsigned long long s_clk[8];  // phase clocks (VTF_PNET_DEBUG & 256)
@@ -371,11 +389,11 @@ __global__ __launch_bounds__(256, PNET_GROUPS_PER_CU) void k_pnet(const uint8_t*
     //      overlaps the tile's work instead of opening it
     // zero pad after the split level planes: read by conv1 (against zero weights) one pixel past
     // the last level pixel, and conv3's zero weight slots (k >= 144) point at it
-    if (tid < 4) sA[P_A - 4 + tid] = 0.f;
+    if (tid < 4) sA[LP::A - 4 + tid] = 0.f;
     // tiles are handed out in chunks of PNET_TILE_CHUNK: one same-address atomic per chunk (a
     // single counter hit once per tile serialises ~166k atomics per launch at the L2)
     if (tid == 0) {
-        s_tile = (int)atomicAdd(tile_ctr, (uint32_t)PNET_TILE_CHUNK);
+        s_tile = (int)(tile_base + atomicAdd(tile_ctr, (uint32_t)PNET_TILE_CHUNK));
         s_cend = s_tile + PNET_TILE_CHUNK;
     }
     for (;;) {
@@ -391,7 +409,7 @@ __global__ __launch_bounds__(256, PNET_GROUPS_PER_CU) void k_pnet(const uint8_t*
                 next_tile = (uint32_t)(blk + 1);
                 next_cend = (uint32_t)cend;
             } else {  // last tile of the chunk: request the next chunk now, used at the tile's end
-                next_tile = atomicAdd(tile_ctr, (uint32_t)PNET_TILE_CHUNK);
+                next_tile = (uint32_t)(tile_base + atomicAdd(tile_ctr, (uint32_t)PNET_TILE_CHUNK));
                 next_cend = next_tile + PNET_TILE_CHUNK;
             }
             s_next = (int)next_tile;  // read at conv3 (several barriers later) for the prefetch
@@ -433,7 +451,7 @@ __global__ __launch_bounds__(256, PNET_GROUPS_PER_CU) void k_pnet(const uint8_t*
             fx1 = xbin[rx].y;
         }
         const int pw3 = (fx1 - fx0) * 3;
-        const bool staged = !P.pre && (int64_t)(fy1 - fy0) * pw3 <= PATCH_BYTES;
+        const bool staged = !P.pre && (int64_t)(fy1 - fy0) * pw3 <= LP::PATCH;
         uint8_t* patch = (uint8_t*)sP;
         // (gathers below issue 8 loads per thread before the first use: latency-bound otherwise)
         if (staged && !(o.dbg & 64)) {
@@ -456,7 +474,7 @@ __global__ __launch_bounds__(256, PNET_GROUPS_PER_CU) void k_pnet(const uint8_t*
         }
         __syncthreads();
         mark(2);  // 2: frame patch staging
-        if (P.pre) {
+        if (!X && P.pre) {
             // large-bin level precomputed by k_resample_sat (bit-identical values)
             const float* pre = P.pre + (int64_t)b * 3 * P.lh * P.lw;
             const int64_t pl = (int64_t)P.lh * P.lw;
@@ -488,8 +506,9 @@ __global__ __launch_bounds__(256, PNET_GROUPS_PER_CU) void k_pnet(const uint8_t*
         const int hs_off = (nrows * pw3 + 7) & ~7;
         // upsampled levels on the split path: bins of 1 or 2 frame pixels per side, every level
         // value s * 2^-(8..10) exact in fp16 (conv1 skips the residual plane there)
-        const bool exact_fill = split3 && P.lh >= H && P.lw >= W;
-        const bool sep = staged && !(o.dbg & 1) && hs_off + nrows * PL_W * (exact_fill ? 8 : 6) <= PATCH_BYTES &&
+        // (X: every level is exact and the host checked that its patch + row sums fit)
+        const bool exact_fill = X || (split3 && P.lh >= H && P.lw >= W);
+        const bool sep = staged && !(o.dbg & 1) && hs_off + nrows * PL_W * (exact_fill ? 8 : 6) <= LP::PATCH &&
                          W < 128 * P.lw;
         if (sep && exact_fill) {
             // bins of n in {0, 1, 2} pixels: branch-free sums, 8-byte row-sum entries, one store
@@ -527,7 +546,7 @@ __global__ __launch_bounds__(256, PNET_GROUPS_PER_CU) void k_pnet(const uint8_t*
                 const float b0 = in ? (float)(v0[2] + m * v1[2]) * sc : 0.f;
                 lvl[i] = h4{(_Float16)r0, (_Float16)g0, (_Float16)b0, (_Float16)0.f};
             }
-        } else if (sep) {
+        } else if (!X && sep) {
             int16_t* hs = (int16_t*)(patch + hs_off);
             for (int i = tid; i < nrows * PL_W; i += 256) {
                 const int r = i / PL_W, q = i - r * PL_W;
@@ -560,7 +579,7 @@ __global__ __launch_bounds__(256, PNET_GROUPS_PER_CU) void k_pnet(const uint8_t*
                             in ? div_bin(div_bin((float)s2 * 0.00390625f, kh), kw) : 0.f);
             }
         }
-        for (int i = tid; i < ((o.dbg & 1) || P.pre || sep ? 0 : PL_H * PL_W); i += 256) {
+        for (int i = tid; i < (X || (o.dbg & 1) || P.pre || sep ? 0 : PL_H * PL_W); i += 256) {
             int r = i / PL_W, q = i - r * PL_W;
             const int2 yb = make_int2(ybin[r].x, ybin[r].y), xb = make_int2(xbin[q].x, xbin[q].y);
             float s0 = 0.f, s1 = 0.f, s2 = 0.f;
@@ -628,7 +647,7 @@ __global__ __launch_bounds__(256, PNET_GROUPS_PER_CU) void k_pnet(const uint8_t*
             // upsampled levels (lh >= H, lw >= W: every bin 1 or 2 frame pixels per side) hold
             // s / 2^(8..10) with |s| <= 1020, exact in fp16: the residual plane is zero there, so
             // its MFMA and its operand reads are skipped (the products it would add are all zero)
-            const bool exact = P.lh >= H && P.lw >= W;
+            const bool exact = X || (P.lh >= H && P.lw >= W);
             // fragment f = pooled cells 4f .. 4f+3 of one pooled row (PP_W % 4 == 0): a lane's
             // operand pixel is its per-lane offset plus a wave-uniform fragment offset
             static_assert(PP_W % 4 == 0, "a fragment's 4 pooled cells share a row");
@@ -981,7 +1000,7 @@ __global__ __launch_bounds__(256, PNET_GROUPS_PER_CU) void k_pnet(const uint8_t*
             const char* src = (const char*)wg.c3h;
             for (int c = wave; c < W3_PIECES; c += 4)
                 __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)(src + c * 1024 + lane * 16),
-                                                 (void __attribute__((address_space(3)))*)(sP + P_W3 + c * 256), 16, 0, 0);
+                                                 (void __attribute__((address_space(3)))*)(sP + LP::W3 + c * 256), 16, 0, 0);
             __syncthreads();
         }
         mark(5);  // 5: conv2
@@ -1002,7 +1021,7 @@ __global__ __launch_bounds__(256, PNET_GROUPS_PER_CU) void k_pnet(const uint8_t*
         //      flight during conv3 (which reads its weights from LDS: no later global load waits
         //      on them), and stored to the patch buffer after it -- the next tile's staging
         //      latency hides behind this tile's matrix work
-        uint8_t pfv[8];
+        uint32_t pfv[2] = {0u, 0u};  // the prefetched bytes, packed (4 per dword)
         int pf_n = 0;
         {
             constexpr int FPW = PT_H * PT_W / 64;  // 16-cell fragments per wave
@@ -1022,9 +1041,9 @@ __global__ __launch_bounds__(256, PNET_GROUPS_PER_CU) void k_pnet(const uint8_t*
                     // heads as the A operand: row = head lrx (0,1 conv4_1; 2..5 conv4_2), k-slot = ch
                     const int hrow = lrx < 2 ? lrx * 32 + ch : (lrx < 6 ? (lrx - 2) * 32 + ch : 0);
                     const float hv = lrx < 2 ? wc.c41w[hrow] : wc.c42w[hrow];
-                    hwA[mf][i] = lrx < 6 ? hv : 0.f;
+                    hwA[mf][i] = !X && lrx < 6 ? hv : 0.f;
                 }
-            const bool splith = wg.hh != nullptr;
+            const bool splith = X || wg.hh != nullptr;  // (X: launched only with the split heads)
             f16x8 hw0 = {}, hw1 = {};
             if (splith) {
                 const int hoff = (lrx * 32 + 8 * lkx) * 2;
@@ -1054,7 +1073,7 @@ __global__ __launch_bounds__(256, PNET_GROUPS_PER_CU) void k_pnet(const uint8_t*
                         const int gy0 = (2 * oy2 * H) / Q.lh, gy1 = ((2 * oy2 + ry + 1) * H + Q.lh - 1) / Q.lh;
                         const int gx0 = (2 * ox2 * W) / Q.lw, gx1 = ((2 * ox2 + rx + 1) * W + Q.lw - 1) / Q.lw;
                         const int w3 = (gx1 - gx0) * 3, nb = (gy1 - gy0) * w3;
-                        if ((int64_t)(gy1 - gy0) * w3 <= PATCH_BYTES && nb > 0) {
+                        if ((int64_t)(gy1 - gy0) * w3 <= LP::PATCH && nb > 0) {
                             pf_src = frames + (int64_t)b2i * frame_stride + (int64_t)gy0 * row_stride + gx0 * 3;
                             qw3 = w3;
                             nb2 = nb;
@@ -1067,7 +1086,7 @@ __global__ __launch_bounds__(256, PNET_GROUPS_PER_CU) void k_pnet(const uint8_t*
                 ix.init(tid, qw3);
 #pragma unroll
                 for (int j = 0; j < 8; j++) {
-                    pfv[j] = pf_src[min((int64_t)ix.r * row_stride + ix.q, last)];
+                    pfv[j >> 2] |= (uint32_t)pf_src[min((int64_t)ix.r * row_stride + ix.q, last)] << (8 * (j & 3));
                     ix.step();
                 }
                 pf_n = pf_rows ? nb2 : 0;
@@ -1098,8 +1117,8 @@ __global__ __launch_bounds__(256, PNET_GROUPS_PER_CU) void k_pnet(const uint8_t*
                     for (int j = 0; j < FH; j++) accc[j][0] = accc[j][1] = f32x4{0.f, 0.f, 0.f, 0.f};
                     // weights from the pooled buffer (rows of W3_ROW halves); k slots >= 144 (step 4,
                     // lane groups 2, 3) are zero: those lanes read the zero pad after the level planes
-                    const _Float16* sWh = (const _Float16*)(sP + P_W3) + lrx * W3_ROW + 8 * lkx;
-                    const _Float16* zpad = (const _Float16*)(sA + P_A - 4);
+                    const _Float16* sWh = (const _Float16*)(sP + LP::W3) + lrx * W3_ROW + 8 * lkx;
+                    const _Float16* zpad = (const _Float16*)(sA + LP::A - 4);
     #pragma unroll
                     for (int s5 = 0; s5 < 5; s5++) {
                         f16x8 w0[2], w1[2];
@@ -1235,11 +1254,12 @@ __global__ __launch_bounds__(256, PNET_GROUPS_PER_CU) void k_pnet(const uint8_t*
                 }
             }
         }
+        if (X) __syncthreads();  // conv3's weights (under the patch bytes) are no longer read
         if (pf_n > 0) {
             uint8_t* patch2 = (uint8_t*)sP;
 #pragma unroll
             for (int j = 0; j < 8; j++)
-                if (tid + j * 256 < pf_n) patch2[tid + j * 256] = pfv[j];
+                if (tid + j * 256 < pf_n) patch2[tid + j * 256] = (uint8_t)(pfv[j >> 2] >> (8 * (j & 3)));
         }
         pf_done = pf_n > 0;
         if (tid == 0) {  // every thread read s_tile / s_cend before this tile's barriers
@@ -1252,29 +1272,56 @@ __global__ __launch_bounds__(256, PNET_GROUPS_PER_CU) void k_pnet(const uint8_t*
     if (clk_on && tid < 8) atomicAdd(&o.clk[tid], s_clk[tid]);
 }
 
+// tiles of the leading levels the exact-levels variant can take: upsampled (lh >= H, lw >= W,
+// no precomputed level) and every tile's frame patch + 8-byte row sums within its staging buffer
+// (bounds: a tile's 42-pixel level span covers at most 42 H / lh + 2 frame rows / columns)
+int64_t pnet_exact_tiles(const std::vector<PNetLevel>& lv, int H, int W, int64_t total_tiles) {
+    for (const auto& L : lv) {
+        const int rows = (PL_H * H + L.lh - 1) / L.lh + 2, cols = (PL_W * W + L.lw - 1) / L.lw + 2;
+        const int hs_off = (rows * cols * 3 + 7) & ~7;
+        const bool fits = rows * cols * 3 <= PnLds<true>::PATCH && hs_off + rows * PL_W * 8 <= PnLds<true>::PATCH;
+        if (L.lh < H || L.lw < W || L.pre || !fits || W >= 128 * L.lw) return L.tile_beg;
+    }
+    return total_tiles;
+}
+
 void launch_pnet(bool dense, const uint8_t* frames, int64_t frame_stride, int64_t row_stride, int H, int W,
                  const PNetLevel* d_levels, int n_levels, int64_t total_tiles, const PNetW& w, const PNetOut& o,
-                 uint32_t* d_tile_ctr, hipStream_t st) {
+                 uint32_t* d_tile_ctr, hipStream_t st, int64_t exact_tiles) {
     if (total_tiles <= 0) return;
     VTF_CHECK(H < 65536 && W < 65536, VTF_E_LIMIT, "mtcnn: frames must be smaller than 65536 px per side");
-    VTF_HIP(hipMemsetAsync(d_tile_ctr, 0, 4, st));
     int dev = 0, cus = 256;
     VTF_HIP(hipGetDevice(&dev));
     VTF_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
-    // persistent workgroups per CU: PNET_GROUPS_PER_CU fills every CU; a smaller count leaves
-    // room for concurrently running lanes' kernels (env VTF_PNET_WG_PER_CU, experiments)
-    static const int wg_per_cu = [] {
-        const char* e = std::getenv("VTF_PNET_WG_PER_CU");
+    // persistent workgroups per CU: the variant's LDS limit fills every CU; a smaller count leaves
+    // room for concurrently running lanes' kernels (env VTF_PNET_WG_PER_CU / VTF_PNET_X_WG_PER_CU,
+    // experiments).  Tiles [0, exact_tiles) -- the leading upsampled levels, checked on the host --
+    // run on the exact-levels variant (X, four workgroups per CU) when the split mode is on
+    // (VTF_PNET_X=0: one launch of the general kernel).
+    auto wgs = [](const char* name, int mx) {
+        const char* e = std::getenv(name);
         const int v = e ? std::atoi(e) : 0;
-        return v >= 1 && v <= PNET_GROUPS_PER_CU ? v : PNET_GROUPS_PER_CU;
-    }();
-    int64_t grid = std::min<int64_t>(total_tiles, (int64_t)cus * wg_per_cu);
+        return v >= 1 && v <= mx ? v : mx;
+    };
+    const char* xe = std::getenv("VTF_PNET_X");
+    if (!w.c3h || !w.hh || dense || (xe && std::atoi(xe) == 0)) exact_tiles = 0;
+    exact_tiles = std::min(exact_tiles, total_tiles);
+    if (exact_tiles > 0) {
+        VTF_HIP(hipMemsetAsync(d_tile_ctr, 0, 4, st));
+        const int64_t grid = std::min<int64_t>(exact_tiles, (int64_t)cus * wgs("VTF_PNET_X_WG_PER_CU", PnLds<true>::GPC));
+        k_pnet<false, true><<<(unsigned)grid, 256, 0, st>>>(frames, frame_stride, row_stride, H, W, d_levels, n_levels,
+                                                             exact_tiles, d_tile_ctr, w, o, 0);
+    }
+    if (exact_tiles >= total_tiles) return;
+    VTF_HIP(hipMemsetAsync(d_tile_ctr, 0, 4, st));
+    const int64_t rest = total_tiles - exact_tiles;
+    const int64_t grid = std::min<int64_t>(rest, (int64_t)cus * wgs("VTF_PNET_WG_PER_CU", PnLds<false>::GPC));
     if (dense)
-        k_pnet<true><<<(unsigned)grid, 256, 0, st>>>(frames, frame_stride, row_stride, H, W, d_levels, n_levels,
-                                                      total_tiles, d_tile_ctr, w, o);
+        k_pnet<true, false><<<(unsigned)grid, 256, 0, st>>>(frames, frame_stride, row_stride, H, W, d_levels, n_levels,
+                                                             total_tiles, d_tile_ctr, w, o, exact_tiles);
     else
-        k_pnet<false><<<(unsigned)grid, 256, 0, st>>>(frames, frame_stride, row_stride, H, W, d_levels, n_levels,
-                                                       total_tiles, d_tile_ctr, w, o);
+        k_pnet<false, false><<<(unsigned)grid, 256, 0, st>>>(frames, frame_stride, row_stride, H, W, d_levels, n_levels,
+                                                              total_tiles, d_tile_ctr, w, o, exact_tiles);
 }
 
 // ----------------------------------------------------------------------------------- RNet / ONet

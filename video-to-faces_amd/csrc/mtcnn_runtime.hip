@@ -785,7 +785,8 @@ static void detect(Mtcnn& m, const uint8_t* frames, int on_dev, int B, int H, in
     if (po.dbg & 256) po.clk = m.ar.get<unsigned long long>(S_CLK, 8);
     if (po.clk) VTF_HIP(hipMemsetAsync(po.clk, 0, 64, st));
     if (m.prof) VTF_HIP(hipEventRecord(m.ev0, st));
-    launch_pnet(false, fr, fstride, rstride, H, W, d_lv, NL, tiles, m.pw, po, d_cnt + NL + 1, st);
+    launch_pnet(false, fr, fstride, rstride, H, W, d_lv, NL, tiles, m.pw, po, d_cnt + NL + 1, st,
+                pnet_exact_tiles(lv, H, W, tiles));
     if (m.prof) VTF_HIP(hipEventRecord(m.ev1, st));
     std::vector<uint32_t> cnt(NL + 1);
     d2h_sync(cnt.data(), d_cnt, (NL + 1) * 4, st);
