@@ -1552,10 +1552,11 @@ void launch_cand_front(bool onet, const int4* sat, int H, int W, const float4* b
         const char* e = std::getenv("VTF_FRONT_DEBUG");
         return e ? std::atoi(e) : 0;
     }();
-    // pool rows per band of the ONet front (VTF_FRONT_PB, experiments): more rows per band = fewer
+    // pool rows per band of the ONet front (VTF_FRONT_PB = 1 / 2 / 3): more rows per band = fewer
     // barriers and more conv fragments per band for the 8 waves, against a larger conv ring
+    // (78 KB at 3: two workgroups per CU either way); 3 measured 441 -> 402 us per det-batch
     const char* pbe = std::getenv("VTF_FRONT_PB");
-    const int pb = pbe ? std::atoi(pbe) : 1;
+    const int pb = pbe ? std::atoi(pbe) : 3;
     // w1h (split conv1 planes) selects conv1 on fp16 matrix cores; null keeps the fp32 MFMA path
     if (onet && w1h && pb == 2)
         k_cand_front<48, 2, 512, true><<<(unsigned)n, 512, 0, st>>>(sat, H, W, boxes, img, w1, w1h, b1, a1, out, err, dbg, ovf);
