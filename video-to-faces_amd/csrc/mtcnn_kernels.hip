@@ -321,7 +321,7 @@ struct PatchIdx {
     }
 };
 
-constexpr int PNET_TILE_CHUNK = 4;
+constexpr int PNET_TILE_CHUNK = 2;
 constexpr int PNET_GROUPS_PER_CU = (160 * 1024) / ((PNET_LDS + 511) / 512 * 512);  // LDS granule: 512 B
 static_assert(PNET_GROUPS_PER_CU >= 2, "k_pnet tile too large for 2 workgroups per CU");
 
