@@ -347,7 +347,7 @@ __global__ __launch_bounds__(256, PnLds<X>::GPC) void k_pnet(const uint8_t* __re
                                                  int64_t row_stride, int H, int W,
                                                  const PNetLevel* __restrict__ lv, int n_levels,
                                                  int64_t total_tiles, uint32_t* __restrict__ tile_ctr, PNetW wg,
-                                                 PNetOut o, int64_t tile_base) {
+                                                 PNetOut o, int64_t tile_base, int max_chunks) {
     using LP = PnLds<X>;
     const auto wc = to_const(wg);
     // conv2 / conv3 weights through buffer loads: one lane VGPR offset + constant SGPR offsets,
@@ -367,6 +367,7 @@ __global__ __launch_bounds__(256, PnLds<X>::GPC) void k_pnet(const uint8_t* __re
     __shared__ unsigned long long s_clk[8];  // phase clocks (VTF_PNET_DEBUG & 256)
     const int tid = threadIdx.x;
     bool pf_done = false;  // the first 2 KB of this tile's frame patch were staged by the previous tile
+    int n_chunks = 0;      // chunks taken after the first (thread 0)
     int L_prev = 0;
     // phase timing (debug): thread 0 reads the shader clock after each phase's closing barrier
     const bool clk_on = o.clk != nullptr;
@@ -408,6 +409,11 @@ __global__ __launch_bounds__(256, PnLds<X>::GPC) void k_pnet(const uint8_t* __re
             if (blk + 1 < cend) {
                 next_tile = (uint32_t)(blk + 1);
                 next_cend = (uint32_t)cend;
+            } else if (max_chunks > 0 && ++n_chunks >= max_chunks) {
+                // quota reached: the workgroup exits after this tile (a later workgroup of the
+                // grid takes over), so its CU slot can go to other streams' kernels meanwhile
+                next_tile = (uint32_t)total_tiles;
+                next_cend = next_tile;
             } else {  // last tile of the chunk: request the next chunk now, used at the tile's end
                 next_tile = (uint32_t)(tile_base + atomicAdd(tile_ctr, (uint32_t)PNET_TILE_CHUNK));
                 next_cend = next_tile + PNET_TILE_CHUNK;
@@ -1304,24 +1310,34 @@ void launch_pnet(bool dense, const uint8_t* frames, int64_t frame_stride, int64_
         return v >= 1 && v <= mx ? v : mx;
     };
     const char* xe = std::getenv("VTF_PNET_X");
+    // chunks per workgroup (VTF_PNET_QUOTA, 0 = persistent: every workgroup runs to the end of the
+    // tile range): with a quota the grid is ~tiles / (quota * chunk) workgroups that retire as they
+    // finish, so other lanes' kernels get CU slots during the launch instead of after it (a
+    // persistent launch holds every CU's registers and LDS for its whole ~4.5 ms).  c2 3 lanes:
+    // persistent 11.60-11.80k, quota 16 / 8 / 4 / 2: 11.98-11.99k / 12.20-12.23k / 12.34-12.39k /
+    // 12.31-12.37k faces/s (same box)
+    const char* qe = std::getenv("VTF_PNET_QUOTA");
+    const int quota = qe ? std::max(0, std::atoi(qe)) : 4;
     if (!w.c3h || !w.hh || dense || (xe && std::atoi(xe) == 0)) exact_tiles = 0;
     exact_tiles = std::min(exact_tiles, total_tiles);
     if (exact_tiles > 0) {
         VTF_HIP(hipMemsetAsync(d_tile_ctr, 0, 4, st));
-        const int64_t grid = std::min<int64_t>(exact_tiles, (int64_t)cus * wgs("VTF_PNET_X_WG_PER_CU", PnLds<true>::GPC));
+        int64_t grid = std::min<int64_t>(exact_tiles, (int64_t)cus * wgs("VTF_PNET_X_WG_PER_CU", PnLds<true>::GPC));
+        if (quota > 0) grid = std::max<int64_t>(grid, (exact_tiles + (int64_t)quota * PNET_TILE_CHUNK - 1) / ((int64_t)quota * PNET_TILE_CHUNK));
         k_pnet<false, true><<<(unsigned)grid, 256, 0, st>>>(frames, frame_stride, row_stride, H, W, d_levels, n_levels,
-                                                             exact_tiles, d_tile_ctr, w, o, 0);
+                                                             exact_tiles, d_tile_ctr, w, o, 0, quota);
     }
     if (exact_tiles >= total_tiles) return;
     VTF_HIP(hipMemsetAsync(d_tile_ctr, 0, 4, st));
     const int64_t rest = total_tiles - exact_tiles;
-    const int64_t grid = std::min<int64_t>(rest, (int64_t)cus * wgs("VTF_PNET_WG_PER_CU", PnLds<false>::GPC));
+    int64_t grid = std::min<int64_t>(rest, (int64_t)cus * wgs("VTF_PNET_WG_PER_CU", PnLds<false>::GPC));
+    if (quota > 0) grid = std::max<int64_t>(grid, (rest + (int64_t)quota * PNET_TILE_CHUNK - 1) / ((int64_t)quota * PNET_TILE_CHUNK));
     if (dense)
         k_pnet<true, false><<<(unsigned)grid, 256, 0, st>>>(frames, frame_stride, row_stride, H, W, d_levels, n_levels,
-                                                             total_tiles, d_tile_ctr, w, o, exact_tiles);
+                                                             total_tiles, d_tile_ctr, w, o, exact_tiles, quota);
     else
         k_pnet<false, false><<<(unsigned)grid, 256, 0, st>>>(frames, frame_stride, row_stride, H, W, d_levels, n_levels,
-                                                              total_tiles, d_tile_ctr, w, o, exact_tiles);
+                                                              total_tiles, d_tile_ctr, w, o, exact_tiles, quota);
 }
 
 // ----------------------------------------------------------------------------------- RNet / ONet
