@@ -17,7 +17,7 @@ for lib in $B $N; do
 done
 for rep in 1 2; do
   for lib in $B $N; do
-    VTF_HIP_LIB=$lib timeout -k 10 300 python3 bench.py --steps 300 --no-cpu-baseline --no-extras --sustain-frames 0 > $O/c2.json 2> $O/c2.err
+    VTF_HIP_LIB=$lib timeout -k 10 400 python3 bench.py --no-cpu-baseline --no-extras > $O/c2.json 2> $O/c2.err
     python3 -c "import json; d=json.load(open('$O/c2.json')); print('$(basename $lib)', 'c2', d['value'], d['ms_per_step'])"
   done
 done
