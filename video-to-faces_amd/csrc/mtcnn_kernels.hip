@@ -321,7 +321,7 @@ struct PatchIdx {
     }
 };
 
-constexpr int PNET_TILE_CHUNK = 2;
+constexpr int PNET_TILE_CHUNK = 4;  // default tiles per atomic chunk (VTF_PNET_CHUNK)
 constexpr int PNET_GROUPS_PER_CU = (160 * 1024) / ((PNET_LDS + 511) / 512 * 512);  // LDS granule: 512 B
 static_assert(PNET_GROUPS_PER_CU >= 2, "k_pnet tile too large for 2 workgroups per CU");
 
@@ -347,7 +347,7 @@ __global__ __launch_bounds__(256, PnLds<X>::GPC) void k_pnet(const uint8_t* __re
                                                  int64_t row_stride, int H, int W,
                                                  const PNetLevel* __restrict__ lv, int n_levels,
                                                  int64_t total_tiles, uint32_t* __restrict__ tile_ctr, PNetW wg,
-                                                 PNetOut o, int64_t tile_base, int max_chunks) {
+                                                 PNetOut o, int64_t tile_base, int max_chunks, int chunk) {
     using LP = PnLds<X>;
     const auto wc = to_const(wg);
     // conv2 / conv3 weights through buffer loads: one lane VGPR offset + constant SGPR offsets,
@@ -394,8 +394,8 @@ __global__ __launch_bounds__(256, PnLds<X>::GPC) void k_pnet(const uint8_t* __re
     // tiles are handed out in chunks of PNET_TILE_CHUNK: one same-address atomic per chunk (a
     // single counter hit once per tile serialises ~166k atomics per launch at the L2)
     if (tid == 0) {
-        s_tile = (int)(tile_base + atomicAdd(tile_ctr, (uint32_t)PNET_TILE_CHUNK));
-        s_cend = s_tile + PNET_TILE_CHUNK;
+        s_tile = (int)(tile_base + atomicAdd(tile_ctr, (uint32_t)chunk));
+        s_cend = s_tile + chunk;
     }
     for (;;) {
         __syncthreads();
@@ -415,8 +415,8 @@ __global__ __launch_bounds__(256, PnLds<X>::GPC) void k_pnet(const uint8_t* __re
                 next_tile = (uint32_t)total_tiles;
                 next_cend = next_tile;
             } else {  // last tile of the chunk: request the next chunk now, used at the tile's end
-                next_tile = (uint32_t)(tile_base + atomicAdd(tile_ctr, (uint32_t)PNET_TILE_CHUNK));
-                next_cend = next_tile + PNET_TILE_CHUNK;
+                next_tile = (uint32_t)(tile_base + atomicAdd(tile_ctr, (uint32_t)chunk));
+                next_cend = next_tile + chunk;
             }
             s_next = (int)next_tile;  // read at conv3 (several barriers later) for the prefetch
         }
@@ -1316,28 +1316,33 @@ void launch_pnet(bool dense, const uint8_t* frames, int64_t frame_stride, int64_
     // persistent launch holds every CU's registers and LDS for its whole ~4.5 ms).  c2 3 lanes:
     // persistent 11.60-11.80k, quota 16 / 8 / 4 / 2: 11.98-11.99k / 12.20-12.23k / 12.34-12.39k /
     // 12.31-12.37k faces/s (same box)
+    // tiles per atomic chunk (VTF_PNET_CHUNK, default PNET_TILE_CHUNK)
+    const char* ce = std::getenv("VTF_PNET_CHUNK");
+    const int chunk = ce && std::atoi(ce) > 0 ? std::atoi(ce) : PNET_TILE_CHUNK;
     const char* qe = std::getenv("VTF_PNET_QUOTA");
-    const int quota = qe ? std::max(0, std::atoi(qe)) : 4;
+    // (chunk x quota at 8 tiles per workgroup, full default run: 4 x 2 12.26-12.30k, 2 x 4
+    // 12.19-12.21k, 1 x 8 12.18k faces/s)
+    const int quota = qe ? std::max(0, std::atoi(qe)) : 2;
     if (!w.c3h || !w.hh || dense || (xe && std::atoi(xe) == 0)) exact_tiles = 0;
     exact_tiles = std::min(exact_tiles, total_tiles);
     if (exact_tiles > 0) {
         VTF_HIP(hipMemsetAsync(d_tile_ctr, 0, 4, st));
         int64_t grid = std::min<int64_t>(exact_tiles, (int64_t)cus * wgs("VTF_PNET_X_WG_PER_CU", PnLds<true>::GPC));
-        if (quota > 0) grid = std::max<int64_t>(grid, (exact_tiles + (int64_t)quota * PNET_TILE_CHUNK - 1) / ((int64_t)quota * PNET_TILE_CHUNK));
+        if (quota > 0) grid = std::max<int64_t>(grid, (exact_tiles + (int64_t)quota * chunk - 1) / ((int64_t)quota * chunk));
         k_pnet<false, true><<<(unsigned)grid, 256, 0, st>>>(frames, frame_stride, row_stride, H, W, d_levels, n_levels,
-                                                             exact_tiles, d_tile_ctr, w, o, 0, quota);
+                                                             exact_tiles, d_tile_ctr, w, o, 0, quota, chunk);
     }
     if (exact_tiles >= total_tiles) return;
     VTF_HIP(hipMemsetAsync(d_tile_ctr, 0, 4, st));
     const int64_t rest = total_tiles - exact_tiles;
     int64_t grid = std::min<int64_t>(rest, (int64_t)cus * wgs("VTF_PNET_WG_PER_CU", PnLds<false>::GPC));
-    if (quota > 0) grid = std::max<int64_t>(grid, (rest + (int64_t)quota * PNET_TILE_CHUNK - 1) / ((int64_t)quota * PNET_TILE_CHUNK));
+    if (quota > 0) grid = std::max<int64_t>(grid, (rest + (int64_t)quota * chunk - 1) / ((int64_t)quota * chunk));
     if (dense)
         k_pnet<true, false><<<(unsigned)grid, 256, 0, st>>>(frames, frame_stride, row_stride, H, W, d_levels, n_levels,
-                                                             total_tiles, d_tile_ctr, w, o, exact_tiles, quota);
+                                                             total_tiles, d_tile_ctr, w, o, exact_tiles, quota, chunk);
     else
         k_pnet<false, false><<<(unsigned)grid, 256, 0, st>>>(frames, frame_stride, row_stride, H, W, d_levels, n_levels,
-                                                              total_tiles, d_tile_ctr, w, o, exact_tiles, quota);
+                                                              total_tiles, d_tile_ctr, w, o, exact_tiles, quota, chunk);
 }
 
 // ----------------------------------------------------------------------------------- RNet / ONet
