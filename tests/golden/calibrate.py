@@ -1,4 +1,5 @@
-"""Calibrate the synthetic MTCNN face-logit biases.
+"""Calibrate the synthetic MTCNN face-logit biases; `encoders`, `yolo`, `rcnn`
+for the other models' calibrations.
 
 Random weights make the MTCNN gates meaningless, so each face-logit head's bias
 difference is chosen so that a fixed fraction of candidates pass its gate on synthetic 720p
@@ -157,8 +158,68 @@ def calibrate_rcnn(n_frames=2):
     print('RCNN_CALIB =', synth.RCNN_CALIB)
 
 
+def _blobs(crops, size, scale):
+    """cv2.dnn.blobFromImages(crops, scale, (size, size), 127.5, swapRB=True) restated
+    (oracle.facenet.resize_linear_u8: the INTER_LINEAR restatement)"""
+    from oracle.facenet import resize_linear_u8
+    out = []
+    for c in crops:
+        r = resize_linear_u8(c, size)[:, :, ::-1].transpose(2, 0, 1)
+        out.append((torch.from_numpy(np.ascontiguousarray(r)).float() - 127.5) * np.float32(scale))
+    return torch.stack(out)
+
+
+def _spread(X):
+    Xn = X / np.linalg.norm(X, axis=1, keepdims=True)
+    D = 1 - Xn @ Xn.T
+    n = len(X)
+    Dm = D + (1 - np.tri(n, k=-1)) * 1e4
+    return np.percentile(D[np.tril_indices(n, -1)], [5, 50, 95]), int((~(Dm.min(1) <= 0.25)).sum())
+
+
+def calibrate_encoders(n_frames=48):
+    """FaceNet's final BatchNorm1d running statistics (synth._encoder_calib): the mean and
+    variance of its input (Linear 1792->512 output) over the face crops of n_frames synthetic
+    720p frames (seed 7 -- not a test seed), written to videotofaces/calib_facenet_bn.npz.
+    Also prints the embeddings' cosine-distance spread with and without the calibration, for
+    FaceNet and for ViT-L (synth.VIT_QK_GAIN)."""
+    import oracle.facenet as ofn
+    from oracle.vit import vit
+    fr, faces = synth.make_frames(n_frames, seed=7, return_faces=True)
+    crops = synth.face_crops(fr, faces)
+    x = _blobs(crops, 160, 1 / 128)
+    p = synth.make_params('facenet', calibrated=False)
+    q = dict(p)
+    q['main.9.running_mean'] = np.zeros(512, np.float32)
+    q['main.9.running_var'] = np.full(512, 1 - 1e-3, np.float32)
+    q['main.9.weight'] = np.ones(512, np.float32)
+    q['main.9.bias'] = np.zeros(512, np.float32)
+    norm = ofn.F.normalize
+    ofn.F.normalize = lambda t, p=2, dim=1: t
+    try:
+        feat = ofn.inception_resnet_v1(q, x).numpy().astype(np.float64)
+    finally:
+        ofn.F.normalize = norm
+    mean, var = feat.mean(0).astype(np.float32), feat.var(0).astype(np.float32)
+    np.savez(synth._FACENET_BN, mean=mean, var=var, n_crops=np.array(len(crops)), seed=np.array(7))
+    print('facenet BN1d input: %d crops, |mean| %.3f, mean std %.4f' % (len(crops), np.linalg.norm(mean),
+                                                                      np.sqrt(var).mean()))
+    for tag, prm in (('uncalibrated', p), ('calibrated', synth.make_params('facenet'))):
+        pct, keep = _spread(ofn.inception_resnet_v1(prm, x).numpy())
+        print('facenet %s: cosine distance p5/p50/p95 %s, dedupe(0.25) keeps %d / %d'
+              % (tag, np.round(pct, 4), keep, len(crops)))
+    xv = _blobs(crops[:64], 128, 1 / 127.5)
+    for tag, prm in (('uncalibrated', synth.make_params('vit_l', calibrated=False)),
+                     ('q/k gain %g' % synth.VIT_QK_GAIN, synth.make_params('vit_l'))):
+        pct, keep = _spread(vit(prm, xv, 1024, 24).numpy())
+        print('vit_l %s: cosine distance p5/p50/p95 %s, dedupe(0.25) keeps %d / %d'
+              % (tag, np.round(pct, 4), keep, len(xv)))
+
+
 if __name__ == '__main__':
-    if sys.argv[1:] == ['rcnn']:
+    if sys.argv[1:] == ['encoders']:
+        calibrate_encoders()
+    elif sys.argv[1:] == ['rcnn']:
         calibrate_rcnn()
     elif sys.argv[1:] == ['yolo']:
         calibrate_yolo()

@@ -511,8 +511,19 @@ def gen_shapes():
 
 # BASELINE config 5 chain: YOLO on 1080p frames -> box filter/adjust -> ViT-L on the crops ->
 # cosine dedupe -> KMeans k=2..16 + scores; bench settings of the box filter
-CHAIN = dict(frames=16, det_batch=8, seed=109, mscore=0.4, msize=50, mborder=5, scale=(1.5, 1.5, 2.2, 1.2),
-             square=True)
+# (frames = synth.make_frame_sets(sets, per_set, 1080, 1920, seed, faces_per_frame): 128 frames)
+CHAIN = dict(sets=16, per_set=8, faces_per_frame=12, det_batch=8, seed=600, mscore=0.4, msize=50, mborder=5,
+             scale=(1.5, 1.5, 2.2, 1.2), square=True)
+
+
+def _sk_kmeans_sweep(X, ks, threads):
+    """cluster_faces' KMeans calls (grouping.py:99-101) with sklearn's OpenMP pool limited to
+    `threads` (its n_threads = _openmp_effective_n_threads() at fit time)."""
+    import sklearn.cluster
+    from threadpoolctl import threadpool_limits
+    with threadpool_limits(limits=threads, user_api='openmp'):
+        return np.stack([sklearn.cluster.KMeans(n_clusters=k, random_state=0, n_init='auto').fit(X).labels_
+                         for k in ks]).astype(np.int32)
 
 
 def gen_chain():
@@ -532,10 +543,10 @@ def gen_chain():
     v = importlib.import_module('ref_vtf.encoders.vit')
     ynet = _load(y.YOLOv3('cpu'), synth.make_params('yolo'))
     vnet = _load(v.ViT('cpu', 128, 16, 1024, 24), synth.make_params('vit_l'))
-    frames = synth.make_frames(c['frames'], 1080, 1920, seed=c['seed'])
-    rects, margins, raw = [], [], []
+    frames = synth.make_frame_sets(c['sets'], c['per_set'], 1080, 1920, c['seed'], c['faces_per_frame'])
+    rects, margins, raw, flagged = [], [], [], []
     sp = ('', '', None, False, False, False)
-    for j in range(0, c['frames'], c['det_batch']):
+    for j in range(0, len(frames), c['det_batch']):
         fb = frames[j:j + c['det_batch']]
         b, sc, _ = _yolo_ref(ynet, y, fb)
         for i, (bi, si) in enumerate(zip(b, sc)):
@@ -546,39 +557,89 @@ def gen_chain():
             rects.extend((j + i, x1, y1, x2, y2) for (x1, y1, x2, y2, _) in adj)
             # fp32 re-association on the GPU can flip a floor/ceil only for a coordinate within a
             # few ulp of an integer, and the score gate only for a score within noise of
-            # min_score: record both margins over the boxes the score gate could pass
+            # min_score: record both margins over the boxes the score gate could pass, and flag
+            # the frames where one is inside the detector's parity tolerance
             live = si >= c['mscore'] - 1e-3
             if live.any():
-                margins.append(min(np.abs(bi[live] - np.round(bi[live])).min(), np.abs(si - c['mscore']).min()))
+                cm = np.abs(bi[live] - np.round(bi[live])).min()
+                sm = np.abs(si - c['mscore']).min()
+                margins.append(min(cm, sm))
+                if cm < 2e-3 or sm < 1e-4:
+                    flagged.append(j + i)
     rects = np.array(rects, np.int32)
     blobs = []
     for f, x1, y1, x2, y2 in rects:
         r = resize_linear_u8(frames[f, y1:y2, x1:x2], 128)[:, :, ::-1].transpose(2, 0, 1)
         blobs.append((torch.from_numpy(np.ascontiguousarray(r)).float() - 127.5) * np.float32(1 / 127.5))
     with torch.inference_mode():
-        X = vnet(torch.stack(blobs)).numpy()
+        X = np.concatenate([vnet(torch.stack(blobs[i:i + 64])).numpy() for i in range(0, len(blobs), 64)])
     names = ['f%05d.jpg' % i for i in range(len(X))]
     with tempfile.TemporaryDirectory() as td:
         os.makedirs(os.path.join(td, 'faces'))
         for n in names:
             open(os.path.join(td, 'faces', n), 'w').close()
-        _, goods = dupes.remove_dupes_overall(X.copy(), names, ('enc', 0.25, False, td))
+        Xk, goods = dupes.remove_dupes_overall(X.copy(), names, ('enc', 0.25, False, td))
     Dm = sklearn.metrics.pairwise.cosine_distances(X)
     Dm += (1 - np.tri(len(X), k=-1).astype(Dm.dtype)) * 10000
-    ks = [k for k in range(2, 17) if k <= len(X)]
-    labels, scores = [], []
-    for k in ks:  # grouping.py:97-107 on the gathered embeddings (BASELINE config 5)
-        lb = sklearn.cluster.KMeans(n_clusters=k, random_state=0, n_init='auto').fit(X).labels_
-        labels.append(lb)
-        scores.append((sklearn.metrics.silhouette_score(X, lb), sklearn.metrics.calinski_harabasz_score(X, lb),
-                       sklearn.metrics.davies_bouldin_score(X, lb)))
+    # main.py:72-77: the sweep clusters the DEDUPED embeddings
+    ks = [k for k in range(2, 17) if k <= len(Xk)]
+    labels = _sk_kmeans_sweep(Xk, ks, 1)
+    labels_mt = _sk_kmeans_sweep(Xk, ks, os.cpu_count())
+    scores = [(sklearn.metrics.silhouette_score(Xk, lb), sklearn.metrics.calinski_harabasz_score(Xk, lb),
+               sklearn.metrics.davies_bouldin_score(Xk, lb)) for lb in labels]
     out = dict(params_json=np.array(json.dumps(c)), rects=rects, X=X,
                dedupe_keep=np.array([int(n[1:6]) for n in goods], np.int64), dedupe_mins=Dm.min(1),
-               dedupe_inds=Dm.argmin(1), k=np.array(ks), labels=np.stack(labels).astype(np.int32),
-               scores=np.array(scores, np.float64), min_int_margin=np.array(min(margins)))
+               dedupe_inds=Dm.argmin(1), k=np.array(ks), labels=labels, labels_mt=labels_mt,
+               mt_threads=np.array(os.cpu_count()), scores=np.array(scores, np.float64),
+               min_int_margin=np.array(min(margins)), flagged_frames=np.array(flagged, np.int64))
     np.savez_compressed(os.path.join(HERE, 'chain.npz'), **out)
     print('chain faces', len(X), 'kept after dedupe', len(goods), 'min |coord - round| %.4g' % min(margins),
-          'best k', ks[int(np.argmax([s[0] for s in scores]))])
+          'flagged frames', flagged,
+          'best k', ks[int(np.argmax([s[0] for s in scores]))],
+          'sklearn 1 vs %d threads: rows differing per k' % os.cpu_count(), (labels != labels_mt).sum(1).tolist())
+
+
+SCALE = dict(n=30000, seed=0, thr=0.25, ks=list(range(2, 17)))
+
+
+def gen_scale():
+    """Grouping at scale on realistic embeddings (BASELINE configs 4/5): N = 30k rows of
+    synth.video_embeddings grown from the chain's ViT-L outputs (chain.npz X; regenerate this
+    after gen_chain) -> the reference's embedding dedupe (dupes.py:60-65: cosine_distances +
+    strict-lower-triangle min/argmin, threshold 0.25) -> on the kept rows (main.py:72-77)
+    cluster_faces' KMeans sweep k = 2..16 and its three scores (grouping.py:97-107), sklearn
+    with 1 OpenMP thread (deterministic) and with every core (its M-step reduces per-thread
+    partial sums in lock order, so its last bits may depend on the thread count; rows where the
+    two disagree are recorded).  Stored as a hash of X, the dedupe result and int8 labels."""
+    import hashlib
+    import sklearn.metrics
+    c = SCALE
+    X = synth.video_embeddings(np.load(os.path.join(HERE, 'chain.npz'))['X'], c['n'], seed=c['seed'])
+    N = len(X)
+    Dm = sklearn.metrics.pairwise.cosine_distances(X)
+    mins = np.empty(N, np.float32)
+    inds = np.empty(N, np.int64)
+    # D += (1 - tri(N, k=-1)) * 10000 (dupes.py:62) one row block at a time: the same float32
+    # elementwise adds as the reference's full-matrix statement, without its N x N float64 temps
+    for i0 in range(0, N, 4096):
+        blk = Dm[i0:i0 + 4096]
+        blk += (1 - np.tri(N, k=-1)[i0:i0 + 4096].astype(blk.dtype)) * 10000
+        mins[i0:i0 + 4096], inds[i0:i0 + 4096] = blk.min(1), blk.argmin(1)
+    del Dm
+    keep = np.nonzero(~(mins <= c['thr']))[0]
+    Xk = X[keep]
+    ks = [k for k in c['ks'] if k <= len(Xk)]
+    labels = _sk_kmeans_sweep(Xk, ks, 1)
+    labels_mt = _sk_kmeans_sweep(Xk, ks, os.cpu_count())
+    scores = [(sklearn.metrics.silhouette_score(Xk, lb), sklearn.metrics.calinski_harabasz_score(Xk, lb),
+               sklearn.metrics.davies_bouldin_score(Xk, lb)) for lb in labels]
+    np.savez_compressed(os.path.join(HERE, 'scale.npz'), params_json=np.array(__import__('json').dumps(c)),
+                        X_sha256=np.frombuffer(hashlib.sha256(X.tobytes()).digest(), np.uint8),
+                        dedupe_mins=mins, dedupe_inds=inds.astype(np.int32), dedupe_keep=keep.astype(np.int32),
+                        k=np.array(ks), labels=labels.astype(np.int8), labels_mt=labels_mt.astype(np.int8),
+                        mt_threads=np.array(os.cpu_count()), scores=np.array(scores, np.float64))
+    print('scale: N', N, 'kept', len(keep), 'best k', ks[int(np.argmax([s[0] for s in scores]))],
+          'sklearn 1 vs %d threads: rows differing per k' % os.cpu_count(), (labels != labels_mt).sum(1).tolist())
 
 
 def gen_iom():
@@ -673,6 +734,7 @@ def gen_boxes():
 
 
 if __name__ == '__main__':
-    which = sys.argv[1:] or ['mtcnn', 'facenet', 'vit', 'grouping', 'yolo', 'kmeans', 'rcnn', 'dupes', 'boxes', 'shapes', 'chain', 'iom']
+    which = sys.argv[1:] or ['mtcnn', 'facenet', 'vit', 'grouping', 'yolo', 'kmeans', 'rcnn', 'dupes', 'boxes', 'shapes', 'chain',
+                             'scale', 'iom']
     for w in which:
         globals()['gen_' + w]()

@@ -102,3 +102,59 @@ def test_cluster_sweep_best_k(km):
     assert best == ks[int(np.argmax(g['scores'][:, 0]))]
     for i in range(len(ks)):
         np.testing.assert_array_equal(labels[i], g['labels'][i])
+
+
+@pytest.fixture(scope='module')
+def scale():
+    """tests/golden/scale.npz (make_golden.py gen_scale): 30k realistic embeddings regenerated
+    from the chain's ViT-L rows, checked by hash."""
+    import hashlib
+    import json
+    from videotofaces import synth
+    g = np.load(os.path.join(GOLDEN, 'scale.npz'))
+    c = json.loads(str(g['params_json']))
+    X = synth.video_embeddings(np.load(os.path.join(GOLDEN, 'chain.npz'))['X'], c['n'], seed=c['seed'])
+    assert hashlib.sha256(X.tobytes()).digest() == g['X_sha256'].tobytes()
+    return g, X
+
+
+def test_scale_dedupe_30k(scale):
+    """remove_dupes_overall('enc') at N = 30k on realistic embeddings: keep set exact except rows
+    whose reference minimum lies within 1e-5 (the fp32 GEMM noise of either side) of the 0.25
+    threshold; argmin exact except where the two nearest earlier faces are within 1e-5 of each
+    other (tie rule: the device resolves exact float ties to the lowest index, as numpy's argmin
+    does; it cannot order two distances that only the reference's BLAS rounding separates)."""
+    from videotofaces import dupes
+    g, X = scale
+    mins, inds = dupes.cosine_dedupe_device(torch.from_numpy(X).cuda())
+    rm, ri = g['dedupe_mins'], g['dedupe_inds']
+    np.testing.assert_allclose(mins, rm, rtol=0, atol=1e-5)
+    far = np.abs(rm - 0.25) > 1e-5
+    keep = ~(mins <= 0.25)
+    np.testing.assert_array_equal(np.nonzero(keep & far)[0], np.setdiff1d(g['dedupe_keep'], np.nonzero(~far)[0]))
+    moved = np.nonzero(inds != ri)[0]
+    # every differing argmin must point at a face the reference puts within 1e-5 of its minimum
+    Xn = X / np.maximum(np.linalg.norm(X, axis=1, keepdims=True), 1e-30)
+    d_alt = 1 - np.einsum('ij,ij->i', Xn[moved], Xn[inds[moved]])
+    assert np.all(np.abs(d_alt - rm[moved]) < 1e-5), moved
+    print('kept %d of %d; rows within 1e-5 of the threshold %d; argmin near-ties resolved differently %d'
+          % (int(keep.sum()), len(X), int((~far).sum()), len(moved)))
+
+
+def test_scale_kmeans_sweep_20k(scale):
+    """cluster_faces' sweep (grouping.py:97-107) on the ~20k deduped rows, D = 1024, k = 2..16:
+    labels bit-exact vs sklearn (1 OpenMP thread, deterministic; the golden records where
+    sklearn with every core differs from itself -- those rows are the only ones allowed to
+    differ), silhouette / CH / DB within rtol 1e-5."""
+    from videotofaces.grouping import cluster_sweep
+    g, X = scale
+    Xk = X[g['dedupe_keep']]
+    ks = [int(k) for k in g['k']]
+    labels, scores = cluster_sweep(Xk, ks, 0)
+    for i, k in enumerate(ks):
+        bad = np.nonzero(labels[i] != g['labels'][i])[0]
+        sk_self = np.nonzero(g['labels'][i] != g['labels_mt'][i])[0]
+        assert np.isin(bad, sk_self).all(), 'k=%d: %d rows differ from sklearn (sklearn self-disagreement %d)' % (
+            k, len(bad), len(sk_self))
+    np.testing.assert_allclose(np.array([s[1:] for s in scores]), g['scores'], rtol=1e-5)
+    print('N', len(Xk), 'best k', max(scores, key=lambda x: x[1])[0])

@@ -174,6 +174,32 @@ def test_kmeans_host_control_flow_vs_sklearn(km):
         np.testing.assert_array_equal(cg.kmeans(X, int(k), prep=prep), g['labels'][i], err_msg='k=%d' % k)
 
 
+def test_kmeans_host_control_flow_chain_deduped():
+    """The same on the config-5 chain's deduped ViT-L embeddings (tests/golden/chain.npz, the
+    reference flow main.py:72-77) against sklearn with one OpenMP thread."""
+    from oracle.kmeans import CpuGrouper
+    c = np.load(os.path.join(GOLDEN, 'chain.npz'))
+    Xk = c['X'][c['dedupe_keep']]
+    assert 0.3 < len(Xk) / len(c['X']) < 0.9, 'encoder calibration: dedupe keeps a real fraction'
+    cg = CpuGrouper()
+    prep = cg.prepare(Xk)
+    for i, k in enumerate(c['k'][::3]):
+        np.testing.assert_array_equal(cg.kmeans(Xk, int(k), prep=prep), c['labels'][3 * i], err_msg='k=%d' % k)
+
+
+def test_video_embeddings_regenerate():
+    """tests/golden/scale.npz's 30k embeddings regenerate bit-exactly from the chain's rows
+    (synth.video_embeddings: elementwise float64 on numpy's PCG64 stream)."""
+    import hashlib
+    import json
+    from videotofaces import synth
+    g = np.load(os.path.join(GOLDEN, 'scale.npz'))
+    c = json.loads(str(g['params_json']))
+    X = synth.video_embeddings(np.load(os.path.join(GOLDEN, 'chain.npz'))['X'], c['n'], seed=c['seed'])
+    assert hashlib.sha256(X.tobytes()).digest() == g['X_sha256'].tobytes()
+    assert 0.3 < len(g['dedupe_keep']) / c['n'] < 0.9
+
+
 def test_silhouette_restatement_vs_sklearn(km):
     from oracle.kmeans import silhouette_samples
     g, X = km

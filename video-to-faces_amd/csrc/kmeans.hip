@@ -10,8 +10,8 @@
 //                  max 0; sklearn/metrics/pairwise.py:391-441,582-660).
 //   k_estep        Lloyd E-step (_k_means_lloyd.pyx:_update_chunk_dense): |c|^2 - 2 x.c in
 //                  fp32, first strict minimum; counts label changes.
-//   k_msum/k_mred  M-step sums: float64 per-(row block, cluster, feature) partials reduced in
-//                  a fixed order (deterministic), rounded to fp32; counts as weights.
+//   k_seg_*, k_msum_seq  M-step sums in sklearn's single-thread order (sequential fp32 per
+//                  cluster and feature, rows in order) via a stable counting sort by label.
 //   k_average      _average_centers (c *= 1/w) and _center_shift (4-way unrolled fp32).
 //   k_pdist        full N x N euclidean matrix (pairwise_distances_chunked): float64 tile
 //                  GEMM + norms, rounded to fp32, sqrt, zero diagonal.  Kept resident in HBM
@@ -141,53 +141,89 @@ __global__ __launch_bounds__(256) void k_estep(const float* __restrict__ X, int6
     if (lane == 0 && nchg) atomicAdd(changed, nchg);
 }
 
-// M-step partial sums: grid (cdiv(D, 64), nb); thread = (column, cluster group of 16)
-template <int KC>
-__global__ __launch_bounds__(256) void k_msum(const float* __restrict__ X, int64_t N, int D,
-                                              const int32_t* __restrict__ labels, int k, int64_t rows_per_block,
-                                              double* __restrict__ part, int64_t* __restrict__ cpart) {
-    const int d = blockIdx.x * 64 + (threadIdx.x & 63);
-    const int j0 = (threadIdx.x >> 6) * KC;  // 4 groups of KC clusters per block
-    const int64_t b = blockIdx.y;
-    const int64_t i0 = b * rows_per_block, i1 = min(N, i0 + rows_per_block);
-    double acc[KC];
-    int64_t cnt[KC];
-#pragma unroll
-    for (int c = 0; c < KC; c++) {
-        acc[c] = 0.0;
-        cnt[c] = 0;
-    }
-    for (int64_t i = i0; i < i1; i++) {
-        int l = labels[i] - j0;
-        float v = d < D ? X[i * D + d] : 0.f;
-#pragma unroll
-        for (int c = 0; c < KC; c++)
-            if (l == c) {
-                acc[c] += (double)v;
-                cnt[c]++;
-            }
-    }
-#pragma unroll
-    for (int c = 0; c < KC; c++) {
-        int j = j0 + c;
-        if (j < k && d < D) part[(b * k + j) * D + d] = acc[c];
-        if (j < k && blockIdx.x == 0 && (threadIdx.x & 63) == 0) cpart[b * k + j] = cnt[c];
+// M-step sums in sklearn's single-thread order.  _update_chunk_dense (_k_means_lloyd.pyx:
+// 210-215) adds every row into its cluster's fp32 row in row order (chunks of 256 rows are
+// visited in order; with one OpenMP thread the thread-local buffer is the whole sum), so
+// sums[j][d] = (((0 + x_a[d]) + x_b[d]) + ...) over the rows a < b < ... labelled j.  A
+// sequential fp32 sum per (cluster, feature) is reproduced exactly by walking each cluster's
+// rows in increasing order: a stable counting sort of the rows by label (64-row segments:
+// per-segment counts by wave ballots, a per-cluster scan, a ranked scatter), then one wave per
+// (64 features, cluster) streams its rows with 16 loads in flight.  (sklearn with T threads
+// reduces T partial sums in lock-acquisition order, which is not reproducible; its rows that
+// differ from the one-thread result are recorded by the goldens.)
+__global__ __launch_bounds__(256) void k_seg_count(const int32_t* __restrict__ labels, int64_t N, int k,
+                                                   int64_t nseg, int32_t* __restrict__ cnt) {
+    const int lane = threadIdx.x & 63;
+    const int64_t s = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    if (s >= nseg) return;
+    const int64_t i = s * 64 + lane;
+    const int l = i < N ? labels[i] : -1;
+    for (int j = 0; j < k; j++) {
+        uint64_t m = __ballot(l == j);
+        if (lane == 0) cnt[(int64_t)j * nseg + s] = __popcll(m);
     }
 }
 
-__global__ void k_mred(const double* __restrict__ part, const int64_t* __restrict__ cpart, int64_t nb, int k, int D,
-                       float* __restrict__ sums, float* __restrict__ w) {
-    int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (e >= (int64_t)k * D) return;
-    int j = (int)(e / D), d = (int)(e % D);
-    double s = 0.0;
-    for (int64_t b = 0; b < nb; b++) s += part[(b * k + j) * D + d];
-    sums[e] = (float)s;
-    if (d == 0) {
-        int64_t c = 0;
-        for (int64_t b = 0; b < nb; b++) c += cpart[b * k + j];
-        w[j] = (float)c;
+// one block, thread j < k: counts -> exclusive offsets (cluster base + running segment sum)
+__global__ void k_seg_scan(int32_t* __restrict__ cnt, int k, int64_t nseg, int32_t* __restrict__ csize) {
+    __shared__ int64_t tot[64];
+    const int j = threadIdx.x;
+    int64_t t = 0;
+    if (j < k)
+        for (int64_t s = 0; s < nseg; s++) t += cnt[(int64_t)j * nseg + s];
+    tot[j] = t;
+    __syncthreads();
+    if (j >= k) return;
+    int64_t base = 0;
+    for (int q = 0; q < j; q++) base += tot[q];
+    csize[j] = (int32_t)t;
+    csize[64 + j] = (int32_t)base;
+    for (int64_t s = 0; s < nseg; s++) {
+        int32_t c = cnt[(int64_t)j * nseg + s];
+        cnt[(int64_t)j * nseg + s] = (int32_t)base;
+        base += c;
     }
+}
+
+__global__ __launch_bounds__(256) void k_seg_scatter(const int32_t* __restrict__ labels, int64_t N, int k,
+                                                     int64_t nseg, const int32_t* __restrict__ off,
+                                                     int32_t* __restrict__ order) {
+    const int lane = threadIdx.x & 63;
+    const int64_t s = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    if (s >= nseg) return;
+    const int64_t i = s * 64 + lane;
+    const int l = i < N ? labels[i] : -1;
+    const uint64_t below = (1ull << lane) - 1;
+    for (int j = 0; j < k; j++) {
+        uint64_t m = __ballot(l == j);
+        if (l == j) order[off[(int64_t)j * nseg + s] + __popcll(m & below)] = (int32_t)i;
+    }
+}
+
+// grid (cdiv(D, 64), k), one wave per block: sums[j][d] = sequential fp32 sum over the
+// cluster's rows (order[csize[64+j] ...]) in row order; weights[j] = row count (exact < 2^24)
+__global__ __launch_bounds__(64) void k_msum_seq(const float* __restrict__ X, int D, const int32_t* __restrict__ order,
+                                                 const int32_t* __restrict__ csize, float* __restrict__ sums,
+                                                 float* __restrict__ w) {
+    constexpr int U = 16;
+    const int j = blockIdx.y;
+    const int d = blockIdx.x * 64 + threadIdx.x;
+    const int n = csize[j];
+    const int32_t* rows = order + csize[64 + j];
+    const bool ok = d < D;
+    const float* xcol = X + (ok ? d : 0);
+    float acc = 0.f;
+    int t = 0;
+    for (; t + U <= n; t += U) {
+        float v[U];
+#pragma unroll
+        for (int u = 0; u < U; u++) v[u] = xcol[(int64_t)rows[t + u] * D];
+#pragma unroll
+        for (int u = 0; u < U; u++) acc += v[u];
+    }
+    for (; t < n; t++) acc += xcol[(int64_t)rows[t] * D];
+    if (ok) sums[(int64_t)j * D + d] = acc;
+    if (blockIdx.x == 0 && threadIdx.x == 0) w[j] = (float)n;
 }
 
 // _average_centers + _center_shift (_k_means_common.pyx:274-311), one block: each thread
@@ -202,7 +238,7 @@ __global__ void k_average(float* __restrict__ Cn, const float* __restrict__ w, c
         for (int j = 0; j < k; j++) {
             float* c = Cn + (int64_t)j * D;
             if (w[j] > 0.f) {
-                float alpha = 1.0f / w[j];
+                float alpha = (float)(1.0 / (double)w[j]);  // `floating alpha = 1.0 / weight` (C double)
                 c[d] *= alpha;
             } else {
                 c[d] = Cn[(int64_t)amax * D + d];
@@ -225,17 +261,50 @@ __global__ void k_average(float* __restrict__ Cn, const float* __restrict__ w, c
 }
 
 // ((X - centers[labels])**2).sum(axis=1) for empty-cluster relocation
+// (_relocate_empty_clusters_dense, _k_means_common.pyx:185): a float32 numpy row sum, i.e.
+// numpy's pairwise summation (loops_utils.h: < 8 sequential; <= 128 eight accumulators
+// combined ((r0+r1)+(r2+r3))+((r4+r5)+(r6+r7)) then the tail; else halves at a multiple of 8)
+struct SqDiff {
+    const float* x;
+    const float* c;
+    __device__ float operator()(int i) const {
+        float t = x[i] - c[i];
+        return t * t;
+    }
+};
+template <int L>
+__device__ float np_pairwise_sum(const SqDiff& f, int off, int n) {
+    if (n < 8) {
+        float r = 0.f;
+        for (int i = 0; i < n; i++) r += f(off + i);
+        return r;
+    }
+    if (n <= 128 || L == 0) {
+        float r[8];
+#pragma unroll
+        for (int q = 0; q < 8; q++) r[q] = f(off + q);
+        int i = 8;
+        for (; i < n - (n % 8); i += 8)
+#pragma unroll
+            for (int q = 0; q < 8; q++) r[q] += f(off + i + q);
+        float res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+        for (; i < n; i++) res += f(off + i);
+        return res;
+    }
+    if constexpr (L > 0) {
+        int n2 = n / 2;
+        n2 -= n2 % 8;
+        return np_pairwise_sum<L - 1>(f, off, n2) + np_pairwise_sum<L - 1>(f, off + n2, n - n2);
+    }
+    return 0.f;
+}
+
 __global__ void k_center_dist(const float* __restrict__ X, int64_t N, int D, const float* __restrict__ C,
                               const int32_t* __restrict__ labels, float* __restrict__ out) {
     int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= N) return;
-    const float* c = C + (int64_t)labels[i] * D;
-    float s = 0.f;
-    for (int d = 0; d < D; d++) {
-        float t = X[i * D + d] - c[d];
-        s += t * t;
-    }
-    out[i] = s;
+    SqDiff f{X + i * D, C + (int64_t)labels[i] * D};
+    out[i] = np_pairwise_sum<14>(f, 0, D);
 }
 
 // ------------------------------------------------------------------ pairwise euclidean (N x N)
@@ -471,15 +540,17 @@ int vtf_kmeans_step(vtf_group_t h, const float* d_X, int64_t N, int64_t D, const
         k_estep<<<waves_grid(N), 256, (size_t)k * D * 4, G.st>>>(d_X, N, (int)D, d_centers, csq, k, d_labels, chg);
         if (d_sums) {
             VTF_CHECK(d_weights, VTF_E_ARG, "null weights");
-            const int64_t rpb = 256;
-            const int64_t nb = (N + rpb - 1) / rpb;
             VTF_CHECK(k <= 64, VTF_E_LIMIT, "kmeans: k > 64");
-            double* part = G.ar.get<double>(3, (size_t)nb * k * D);
-            int64_t* cpart = G.ar.get<int64_t>(4, (size_t)nb * k);
-            // 4 waves x 16 clusters per block (k <= 64)
-            dim3 grid(cdiv(D, 64), (unsigned)nb);
-            k_msum<16><<<grid, 256, 0, G.st>>>(d_X, N, (int)D, d_labels, k, rpb, part, cpart);
-            k_mred<<<cdiv((int64_t)k * D, 256), 256, 0, G.st>>>(part, cpart, nb, k, (int)D, d_sums, d_weights);
+            VTF_CHECK(N < (1 << 24), VTF_E_LIMIT, "kmeans: N >= 2^24 (fp32 row counts)");
+            const int64_t nseg = cdiv(N, 64);
+            int32_t* cnt = G.ar.get<int32_t>(3, (size_t)nseg * k);
+            int32_t* order = G.ar.get<int32_t>(4, (size_t)N);
+            int32_t* csize = G.ar.get<int32_t>(6, 128);
+            const unsigned sg = (unsigned)cdiv(nseg, 4);
+            k_seg_count<<<sg, 256, 0, G.st>>>(d_labels, N, k, nseg, cnt);
+            k_seg_scan<<<1, 64, 0, G.st>>>(cnt, k, nseg, csize);
+            k_seg_scatter<<<sg, 256, 0, G.st>>>(d_labels, N, k, nseg, cnt, order);
+            k_msum_seq<<<dim3(cdiv(D, 64), k), 64, 0, G.st>>>(d_X, (int)D, order, csize, d_sums, d_weights);
         }
         unsigned long long c = 0;
         VTF_HIP(hipMemcpyAsync(&c, chg, 8, hipMemcpyDeviceToHost, G.st));
