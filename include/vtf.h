@@ -187,6 +187,11 @@ int vtf_gemm_split(const float* d_a, const float* d_b, int64_t M, int N, int K, 
  * for each row i, min and argmin over j < i of clip(1 - cos(X_i, X_j), 0, 2); row 0 gets
  * 10000 / 0 (the reference's masked diagonal).  d_X [N,D] fp32 -> d_min [N], d_arg [N]. */
 int vtf_cosine_dedupe(const float* d_X, int64_t N, int64_t D, float* d_min, int64_t* d_arg, void* hip_stream);
+/* The same for rows [row_begin, row_end) only (a rank's shard of the lower triangle, SURVEY.md
+ * §8e): row_begin a multiple of 128, row_end a multiple of 128 or N; d_min / d_arg hold
+ * row_end - row_begin entries.  Rows at or after row_end are not read. */
+int vtf_cosine_dedupe_rows(const float* d_X, int64_t N, int64_t D, int64_t row_begin, int64_t row_end, float* d_min,
+                           int64_t* d_arg, void* hip_stream);
 /* classify (grouping.py:50-66): argmin / min over c of cosine distance(X_i, R_c). */
 int vtf_cosine_classify(const float* d_X, int64_t N, const float* d_R, int64_t C, int64_t D, float* d_min,
                         int64_t* d_arg, void* hip_stream);
@@ -310,8 +315,9 @@ int vtf_colstats(vtf_group_t h, const float* d_X, int64_t N, int64_t D, float* d
  * formula rounded to fp32 and clipped at 0.  T <= 16. */
 int vtf_sqdist_rows(vtf_group_t h, const float* d_X, int64_t N, int64_t D, const int64_t* rows, int T, float* d_out);
 /* One Lloyd iteration (_k_means_lloyd.pyx lloyd_iter_chunked_dense): labels (in/out, int32)
- * from centers [k,D]; if d_sums: per-cluster sums [k,D] (float64-accumulated, fp32) and
- * weights [k] (counts).  *out_changed = number of labels that changed.  k <= 64. */
+ * from centers [k,D]; if d_sums: per-cluster sums [k,D] in sklearn's one-thread order
+ * (sequential fp32 over the cluster's rows in row order, _update_chunk_dense) and weights
+ * [k] (counts).  *out_changed = number of labels that changed.  k <= 64, N < 2^24. */
 int vtf_kmeans_step(vtf_group_t h, const float* d_X, int64_t N, int64_t D, const float* d_centers, int k,
                     int32_t* d_labels, float* d_sums, float* d_weights, int64_t* out_changed);
 /* _average_centers + _center_shift: sums -> centers in place, shift[k] = |new - old|. */
@@ -325,6 +331,14 @@ int vtf_pairwise_euclidean(vtf_group_t h, const float* d_X, int64_t N, int64_t D
 /* silhouette_samples from the distance matrix; labels encoded 0..k-1, freq int64 [k]. */
 int vtf_silhouette_samples(vtf_group_t h, const float* d_D, int64_t N, const int32_t* d_labels, int k,
                            const int64_t* d_freq, float* d_sil);
+/* silhouette_samples (sklearn/metrics/cluster/_unsupervised.py:203-315, called by
+ * silhouette_score at grouping.py:105) of M label sets at once, for rows [row_begin, row_end)
+ * only -- a rank's shard -- and without the N x N matrix (O(N*D) memory): d_labels uint8
+ * [M][N] encoded 0..k_m-1, ks host int32 [M] (2 <= k_m, sum k_m <= 160 per call), freq host
+ * int64 [sum k_m] (cluster sizes, set after set), d_sil float32 [M][row_end - row_begin].
+ * Replaces vtf_pairwise_euclidean + vtf_silhouette_samples for the sweep. */
+int vtf_silhouette_sweep(vtf_group_t h, const float* d_X, int64_t N, int64_t D, int64_t row_begin, int64_t row_end,
+                         const uint8_t* d_labels, int M, const int32_t* ks, const int64_t* freq, float* d_sil);
 /* Per-cluster float64 sums [k,D], sum of |x|^2 [k] and counts [k] (calinski_harabasz). */
 int vtf_cluster_sums(vtf_group_t h, const float* d_X, int64_t N, int64_t D, const int32_t* d_labels, int k,
                      double* d_sums, double* d_sqnorm, int64_t* d_counts);

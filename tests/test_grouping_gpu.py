@@ -158,3 +158,43 @@ def test_scale_kmeans_sweep_20k(scale):
             k, len(bad), len(sk_self))
     np.testing.assert_allclose(np.array([s[1:] for s in scores]), g['scores'], rtol=1e-5)
     print('N', len(Xk), 'best k', max(scores, key=lambda x: x[1])[0])
+
+
+def test_sweep_200k_rows_no_nxn():
+    """The k = 2..16 sweep at N = 200k, D = 1024 in one process (an N x N fp32 matrix would be
+    160 GB): KMeans fits, the one-pass silhouette over the distance rows, CH / DB.  A 256-row
+    sample of the silhouette is checked against a float64 numpy restatement (distances of those
+    rows to all N; tolerance 1e-5, the fp32 rounding of the per-cluster sums), and the device
+    memory in use after the sweep stays O(N D)."""
+    import time
+    from videotofaces import synth
+    from videotofaces.grouping import cluster_sweep
+    from videotofaces.kmeans import Grouper
+    basis = np.load(os.path.join(GOLDEN, 'chain.npz'))['X']
+    X = synth.video_embeddings(basis, 200000, seed=5)
+    ks = list(range(2, 17))
+    t = time.time()
+    labels, scores = cluster_sweep(X, ks, 0)
+    dt = time.time() - t
+    free, total = torch.cuda.mem_get_info()
+    print('sweep N=200k: %.1f s, device memory in use %.1f GB, best k %d'
+          % (dt, (total - free) / 1e9, max(scores, key=lambda s: s[1])[0]))
+    assert (total - free) < 40e9
+    for lb, k in zip(labels, ks):
+        assert lb.min() == 0 and lb.max() == k - 1
+    assert all(np.isfinite(s[1:]).all() for s in scores)
+    rows = np.random.default_rng(0).choice(len(X), 256, replace=False)
+    lb = labels[6]
+    sil = Grouper('cuda:0').silhouette_sweep(X, [lb], 0, len(X))[0][rows]
+    X64 = X.astype(np.float64)
+    n2 = (X64 * X64).sum(1)
+    d = np.sqrt(np.maximum((n2[rows, None] - 2 * X64[rows] @ X64.T + n2[None, :]).astype(np.float32), 0))
+    d[np.arange(len(rows)), rows] = 0
+    freq = np.bincount(lb)
+    cd = np.stack([d[:, lb == c].astype(np.float64).sum(1) for c in range(len(freq))], 1).astype(np.float32)
+    own = lb[rows]
+    a = cd[np.arange(len(rows)), own] / (freq[own] - 1)
+    cd[np.arange(len(rows)), own] = np.inf
+    b = (cd / freq).min(1)
+    ref = (b - a) / np.maximum(a, b)
+    np.testing.assert_allclose(sil, ref, rtol=0, atol=1e-5)

@@ -71,21 +71,25 @@ def _sweep_worker(rank, world, port, q):
     from videotofaces import synth
     from videotofaces.grouping import cluster_sweep
     X = synth.planted_clusters(N=400, D=32)
-    g = CpuGrouper()
-    prep = g.prepare(X)
     done = []
 
-    def compute(k):
-        done.append(k)
-        return g.kmeans(X, k, prep=prep), (float(k), 0.0, 0.0)
-    labels, scores = cluster_sweep(X, [2, 3, 4, 5, 6], 0, compute)
+    class Spy(CpuGrouper):
+        def kmeans(self, X, k, **kw):
+            done.append(k)
+            return super().kmeans(X, k, **kw)
+
+        def silhouette_sweep(self, X, label_sets, lo=0, hi=None):
+            done.append(('rows', lo, hi))
+            return super().silhouette_sweep(X, label_sets, lo, hi)
+    labels, scores = cluster_sweep(X, [2, 3, 4, 5, 6], 0, Spy())
     q.put((rank, done, [lb.tolist() for lb in labels], scores))
     dist.destroy_process_group()
 
 
-def test_cluster_sweep_sharded_by_k_gloo():
-    """The k sweep is split across ranks (i % world) and all-gathered in k order; every rank
-    ends with the full, identical result."""
+def test_cluster_sweep_sharded_gloo():
+    """The sweep split across 2 ranks: KMeans fits by k (i % world), the
+    silhouette by row ranges, CH/DB by k; every rank ends with labels and scores identical to
+    the one-process sweep."""
     world = 2
     ctx = mp.get_context('spawn')
     q = ctx.Queue()
@@ -96,11 +100,62 @@ def test_cluster_sweep_sharded_by_k_gloo():
     res = {r: (d, lb, sc) for r, d, lb, sc in (q.get(timeout=180) for _ in range(world))}
     for p in ps:
         p.join(timeout=60)
-    assert res[0][0] == [2, 4, 6] and res[1][0] == [3, 5]
+    assert res[0][0] == [2, 4, 6, ('rows', 0, 200)] and res[1][0] == [3, 5, ('rows', 200, 400)]
     assert res[0][1] == res[1][1] and res[0][2] == res[1][2]
-    assert [s[0] for s in res[0][2]] == [2, 3, 4, 5, 6]
     from oracle.kmeans import CpuGrouper
     from videotofaces import synth
+    from videotofaces.grouping import cluster_sweep
     X = synth.planted_clusters(N=400, D=32)
-    for k, lb in zip([2, 3, 4, 5, 6], res[0][1]):
-        assert lb == CpuGrouper().kmeans(X, k).tolist()
+    labels, scores = cluster_sweep(X, [2, 3, 4, 5, 6], 0, CpuGrouper())
+    assert res[0][1] == [lb.tolist() for lb in labels]
+    assert res[0][2] == scores
+
+
+def _dedupe_worker(rank, world, port, q):
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [root, os.path.join(root, 'video-to-faces_amd')]
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    import numpy as np
+    from oracle import grouping as og
+    from videotofaces.dupes import cosine_dedupe_sharded
+    X = np.random.default_rng(3).normal(0, 1, (1000, 16)).astype(np.float32)
+    rm, ri = og.cosine_dedupe(X)
+    seen = []
+
+    def rows_fn(lo, hi):
+        seen.append((lo, hi))
+        return rm[lo:hi], ri[lo:hi]
+    mins, inds = cosine_dedupe_sharded(X, rows_fn)
+    q.put((rank, seen, mins.tolist(), inds.tolist()))
+    dist.destroy_process_group()
+
+
+def test_cosine_dedupe_sharded_gloo():
+    """The lower-triangle dedupe row-block sharded over 3 ranks (128-aligned, balanced by area)
+    and all-gathered: every rank ends with the full (min, argmin) of every row."""
+    import numpy as np
+    from oracle import grouping as og
+    from videotofaces.dupes import dedupe_shards
+    world = 3
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_dedupe_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    res = {r: rest for r, *rest in (q.get(timeout=180) for _ in range(world))}
+    for p in ps:
+        p.join(timeout=60)
+    b = dedupe_shards(1000, world)
+    assert [res[r][0] for r in range(world)] == [[(b[r], b[r + 1])] for r in range(world)]
+    assert all(x % 128 == 0 for x in b[:-1]) and b[-1] == 1000
+    X = np.random.default_rng(3).normal(0, 1, (1000, 16)).astype(np.float32)
+    rm, ri = og.cosine_dedupe(X)
+    for r in range(world):
+        assert res[r][1] == rm.tolist() and res[r][2] == ri.tolist()
+    # area balance: each shard holds roughly 1/world of the lower triangle's tile pairs
+    nt = [(x + 127) // 128 for x in b]
+    pairs = [nt[r + 1] * (nt[r + 1] + 1) // 2 - nt[r] * (nt[r] + 1) // 2 for r in range(world)]
+    assert max(pairs) <= 2 * min(pairs) + 8

@@ -44,11 +44,11 @@ constexpr int CT = 128, CK = 32, CLD = CK + 4;
 
 // grid.x enumerates lower-triangle tile pairs (bi >= bj)
 __global__ __launch_bounds__(256) void k_cos_dedupe(const float* __restrict__ Xn, int64_t N, int Dp,
-                                                    uint64_t* __restrict__ key) {
+                                                    int64_t t_base, int64_t row0, uint64_t* __restrict__ key) {
     __shared__ __attribute__((aligned(16))) float As[CT * CLD];
     __shared__ __attribute__((aligned(16))) float Bs[CT * CLD];
     // tile pair from linear index t: bi = floor((sqrt(8t+1)-1)/2), bj = t - bi(bi+1)/2
-    int64_t t = blockIdx.x;
+    int64_t t = t_base + blockIdx.x;
     int64_t bi = (int64_t)((sqrt(8.0 * (double)t + 1.0) - 1.0) * 0.5);
     while ((bi + 1) * (bi + 2) / 2 <= t) bi++;
     while (bi * (bi + 1) / 2 > t) bi--;
@@ -115,14 +115,14 @@ __global__ __launch_bounds__(256) void k_cos_dedupe(const float* __restrict__ Xn
                 uint64_t o = ((uint64_t)hi << 32) | lo;
                 best = o < best ? o : best;
             }
-            if ((lane & 15) == 0 && best != ~0ull) atomicMin((unsigned long long*)&key[i], (unsigned long long)best);
+            if ((lane & 15) == 0 && best != ~0ull) atomicMin((unsigned long long*)&key[i - row0], (unsigned long long)best);
         }
     }
 }
 
 __global__ void k_unpack(const uint64_t* __restrict__ key, int64_t N, float* __restrict__ mn, int64_t* __restrict__ arg) {
     int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= N) return;
+    if (i >= N) return;  // (row-range-relative index: key, mn and arg all start at the range)
     uint64_t k = key[i];
     if (k == ~0ull) {  // row 0: every entry masked -> 0 + 10000 at j = 0
         mn[i] = 10000.f;
@@ -159,25 +159,42 @@ using namespace vtf;
 
 extern "C" {
 
+static void cosine_dedupe_rows(const float* d_X, int64_t N, int64_t D, int64_t r0, int64_t r1, float* d_min,
+                               int64_t* d_arg, hipStream_t st) {
+    VTF_CHECK(d_X && d_min && d_arg && N < (int64_t)1 << 31, VTF_E_ARG, "bad argument");
+    VTF_CHECK(0 <= r0 && r0 <= r1 && r1 <= N && r0 % CT == 0 && (r1 % CT == 0 || r1 == N), VTF_E_ARG,
+              "row range must be [a, b) with a, b multiples of 128 (or b = N)");
+    if (r1 == r0) return;
+    StreamScratch sc = stream_scratch(st);
+    Arena& ar = *sc.ar;
+    int Dp = (int)((D + CK - 1) / CK * CK);
+    float* Xn = ar.get<float>(0, N * Dp);
+    uint64_t* key = ar.get<uint64_t>(1, r1 - r0);
+    // rows r1.. are never read (tiles pair a row block with itself and earlier blocks only)
+    k_row_normalize<<<(unsigned)r1, 256, 0, st>>>(d_X, r1, (int)D, Dp, Xn);
+    k_init_keys<<<cdiv(r1 - r0, 256), 256, 0, st>>>(key, r1 - r0);
+    const int64_t b0 = r0 / CT, b1 = (r1 + CT - 1) / CT;
+    const int64_t t0 = b0 * (b0 + 1) / 2, t1 = b1 * (b1 + 1) / 2;
+    VTF_CHECK(t1 - t0 < (int64_t)1 << 31, VTF_E_LIMIT, "cosine_dedupe: N too large");
+    k_cos_dedupe<<<(unsigned)(t1 - t0), 256, 0, st>>>(Xn, N, Dp, t0, r0, key);
+    k_unpack<<<cdiv(r1 - r0, 256), 256, 0, st>>>(key, r1 - r0, d_min, d_arg);
+    VTF_HIP(hipGetLastError());
+}
+
 int vtf_cosine_dedupe(const float* d_X, int64_t N, int64_t D, float* d_min, int64_t* d_arg, void* hip_stream) {
     return guarded_on(stream_device((hipStream_t)hip_stream), [&] {
         VTF_CHECK(N >= 0 && D > 0, VTF_E_ARG, "bad argument");
         if (N == 0) return;
-        VTF_CHECK(d_X && d_min && d_arg && N < (int64_t)1 << 31, VTF_E_ARG, "bad argument");
-        hipStream_t st = (hipStream_t)hip_stream;
-        StreamScratch sc = stream_scratch(st);
-        Arena& ar = *sc.ar;
-        int Dp = (int)((D + CK - 1) / CK * CK);
-        float* Xn = ar.get<float>(0, N * Dp);
-        uint64_t* key = ar.get<uint64_t>(1, N);
-        k_row_normalize<<<(unsigned)N, 256, 0, st>>>(d_X, N, (int)D, Dp, Xn);
-        k_init_keys<<<cdiv(N, 256), 256, 0, st>>>(key, N);
-        int64_t nt = (N + CT - 1) / CT;
-        int64_t pairs = nt * (nt + 1) / 2;
-        VTF_CHECK(pairs < (int64_t)1 << 31, VTF_E_LIMIT, "cosine_dedupe: N too large");
-        k_cos_dedupe<<<(unsigned)pairs, 256, 0, st>>>(Xn, N, Dp, key);
-        k_unpack<<<cdiv(N, 256), 256, 0, st>>>(key, N, d_min, d_arg);
-        VTF_HIP(hipGetLastError());
+        cosine_dedupe_rows(d_X, N, D, 0, N, d_min, d_arg, (hipStream_t)hip_stream);
+    });
+}
+
+int vtf_cosine_dedupe_rows(const float* d_X, int64_t N, int64_t D, int64_t row_begin, int64_t row_end, float* d_min,
+                           int64_t* d_arg, void* hip_stream) {
+    return guarded_on(stream_device((hipStream_t)hip_stream), [&] {
+        VTF_CHECK(N >= 0 && D > 0, VTF_E_ARG, "bad argument");
+        if (N == 0) return;
+        cosine_dedupe_rows(d_X, N, D, row_begin, row_end, d_min, d_arg, (hipStream_t)hip_stream);
     });
 }
 

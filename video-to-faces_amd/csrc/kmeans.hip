@@ -416,6 +416,148 @@ __global__ __launch_bounds__(256) void k_silhouette(const float* __restrict__ Dm
     }
 }
 
+// ------------------------------------------------------------------ silhouette sweep (no N x N)
+// silhouette_samples for M label sets at once, rows [r0, r1) only (a rank's shard), without
+// the N x N matrix: sklearn's pairwise_distances_chunked + _silhouette_reduce
+// (_unsupervised.py:203-315) computes, per row i and cluster c, the float64 bincount sum of
+// D[i, j] over the members j of c, rounded to float32.  Here one workgroup owns 64 rows and
+// walks every column tile of 64: the 64 x 64 distance tile (float64 GEMM + norms, fp32, sqrt,
+// zero diagonal: k_pdist's formula) goes to LDS, and the per-(row, cluster) sums of every
+// label set advance as S += Dt x H, H[j][q] = [label_m(q)(j) == c(q)] over the C = sum k_m
+// cluster columns -- a one-hot GEMM in float64 (exact products, double accumulation).  After
+// the last tile the sums are rounded to fp32 and each (row, set) gets silhouette_samples'
+// arithmetic (k_silhouette).  Memory: O(N D) -- the sweep runs at any N that fits X.
+constexpr int SW_T = 64, SW_KB = 16, SW_CMAX = 160, SW_CB = SW_CMAX / 16, SW_MMAX = 32;
+
+struct SilTables {
+    int M, C;
+    int qm[SW_CMAX], qc[SW_CMAX];  // cluster column -> (set, cluster)
+    int off[SW_MMAX], k[SW_MMAX];  // set -> first column, clusters
+};
+
+__global__ __launch_bounds__(256) void k_sil_sweep(const float* __restrict__ X, int64_t N, int D,
+                                                   const double* __restrict__ nrm, const uint8_t* __restrict__ lab,
+                                                   const SilTables tb, const int64_t* __restrict__ freq,
+                                                   int64_t r0, int64_t r1, float* __restrict__ sil) {
+    // LDS: GEMM staging + distance tile + one-hot tile; reused for the fp32 sums at the end
+    constexpr int STAGE = 2 * SW_KB * (SW_T + 1) * 8 + SW_T * (SW_T + 1) * 4 + SW_T * SW_CMAX;
+    static_assert(STAGE >= SW_T * SW_CMAX * 4, "sum buffer overlays the staging");
+    __shared__ __attribute__((aligned(16))) unsigned char smem[STAGE];
+    double (*sA)[SW_T + 1] = reinterpret_cast<double (*)[SW_T + 1]>(smem);
+    double (*sB)[SW_T + 1] = reinterpret_cast<double (*)[SW_T + 1]>(smem + SW_KB * (SW_T + 1) * 8);
+    float (*Dt)[SW_T + 1] = reinterpret_cast<float (*)[SW_T + 1]>(smem + 2 * SW_KB * (SW_T + 1) * 8);
+    uint8_t (*Hs)[SW_CMAX] = reinterpret_cast<uint8_t (*)[SW_CMAX]>(smem + 2 * SW_KB * (SW_T + 1) * 8 +
+                                                                     SW_T * (SW_T + 1) * 4);
+    const int tid = threadIdx.x, tx = tid & 15, ty = tid >> 4;
+    const int64_t i0 = r0 + (int64_t)blockIdx.x * SW_T;
+    const int C = tb.C;
+    double S[4][SW_CB];
+#pragma unroll
+    for (int a = 0; a < 4; a++)
+#pragma unroll
+        for (int b = 0; b < SW_CB; b++) S[a][b] = 0.0;
+    for (int64_t j0 = 0; j0 < N; j0 += SW_T) {
+        double acc[4][4] = {};
+        for (int k0 = 0; k0 < D; k0 += SW_KB) {
+            for (int e = tid; e < SW_T * SW_KB; e += 256) {
+                int r = e / SW_KB, kk = e % SW_KB;
+                int64_t ia = i0 + r, jb = j0 + r;
+                sA[kk][r] = (ia < r1 && k0 + kk < D) ? (double)X[ia * D + k0 + kk] : 0.0;
+                sB[kk][r] = (jb < N && k0 + kk < D) ? (double)X[jb * D + k0 + kk] : 0.0;
+            }
+            __syncthreads();
+#pragma unroll
+            for (int kk = 0; kk < SW_KB; kk++) {
+                double av[4], bv[4];
+#pragma unroll
+                for (int q = 0; q < 4; q++) {
+                    av[q] = sA[kk][ty + 16 * q];
+                    bv[q] = sB[kk][tx + 16 * q];
+                }
+#pragma unroll
+                for (int p = 0; p < 4; p++)
+#pragma unroll
+                    for (int q = 0; q < 4; q++) acc[p][q] = fma(av[p], bv[q], acc[p][q]);
+            }
+            __syncthreads();
+        }
+        // distance tile (k_pdist's epilogue) and the one-hot tile of this column block
+#pragma unroll
+        for (int p = 0; p < 4; p++) {
+            int64_t i = i0 + ty + 16 * p;
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                int64_t j = j0 + tx + 16 * q;
+                float dv = 0.f;
+                if (i < r1 && j < N) {
+                    double dd = -2.0 * acc[p][q];
+                    dd += nrm[i];
+                    dd += nrm[j];
+                    float f = fmaxf((float)dd, 0.f);
+                    dv = i == j ? 0.f : sqrtf(f);
+                }
+                Dt[ty + 16 * p][tx + 16 * q] = dv;
+            }
+        }
+        for (int e = tid; e < SW_T * C; e += 256) {
+            int jj = e / C, q = e % C;
+            int64_t j = j0 + jj;
+            Hs[jj][q] = (j < N && lab[(int64_t)tb.qm[q] * N + j] == tb.qc[q]) ? 1 : 0;
+        }
+        __syncthreads();
+        // S[rows ty + 16a][cols tx + 16b] += sum_j Dt[row][j] * H[j][col]
+        const int jn = (int)min<int64_t>(SW_T, N - j0);
+        for (int jj = 0; jj < jn; jj++) {
+            double dv[4];
+#pragma unroll
+            for (int a = 0; a < 4; a++) dv[a] = (double)Dt[ty + 16 * a][jj];
+#pragma unroll
+            for (int b = 0; b < SW_CB; b++) {
+                int q = tx + 16 * b;
+                if (q < C && Hs[jj][q]) {
+#pragma unroll
+                    for (int a = 0; a < 4; a++) S[a][b] += dv[a];
+                }
+            }
+        }
+        __syncthreads();
+    }
+    // fp32 sums (cluster_distances is a float32 array) -> LDS, then silhouette per (row, set)
+    float (*Sf)[SW_CMAX] = reinterpret_cast<float (*)[SW_CMAX]>(smem);
+#pragma unroll
+    for (int a = 0; a < 4; a++)
+#pragma unroll
+        for (int b = 0; b < SW_CB; b++) {
+            int q = tx + 16 * b;
+            if (q < C) Sf[ty + 16 * a][q] = (float)S[a][b];
+        }
+    __syncthreads();
+    for (int e = tid; e < SW_T * tb.M; e += 256) {
+        int r = e % SW_T, m = e / SW_T;
+        int64_t i = i0 + r;
+        if (i >= r1) continue;
+        const int li = lab[(int64_t)m * N + i], o = tb.off[m];
+        const int64_t* fr = freq + o;
+        float inter = INFINITY, intra = 0.f;
+        for (int c = 0; c < tb.k[m]; c++) {
+            float cd = Sf[r][o + c];
+            if (c == li) {
+                intra = cd;
+            } else {
+                float mm = (float)((double)cd / (double)fr[c]);
+                inter = fminf(inter, mm);
+            }
+        }
+        float a = (float)((double)intra / (double)(fr[li] - 1));
+        float sv = inter - a;
+        float mx = (isnan(a) || isnan(inter)) ? NAN : fmaxf(a, inter);
+        sv = sv / mx;
+        if (isnan(sv)) sv = 0.f;
+        else if (isinf(sv)) sv = sv > 0 ? 3.402823466e38f : -3.402823466e38f;
+        sil[(int64_t)m * (r1 - r0) + (i - r0)] = sv;
+    }
+}
+
 // ------------------------------------------------------------------ cluster statistics (CH, DB)
 // sums[k][D] (double), sqn[k] = sum |x|^2 (double), cnt[k]: one block per row chunk,
 // atomics on double (order-independent up to float64 rounding)
@@ -605,6 +747,39 @@ int vtf_silhouette_samples(vtf_group_t h, const float* d_D, int64_t N, const int
         else
             k_silhouette<64><<<grid, 256, 0, st>>>(d_D, N, d_labels, k, d_freq, d_sil);
         VTF_HIP(hipGetLastError());
+    });
+}
+
+int vtf_silhouette_sweep(vtf_group_t h, const float* d_X, int64_t N, int64_t D, int64_t row_begin, int64_t row_end,
+                         const uint8_t* d_labels, int M, const int32_t* ks, const int64_t* freq, float* d_sil) {
+    return guarded_on(h ? h->g.device : -1, [&] {
+        VTF_CHECK(h && d_X && d_labels && ks && freq && d_sil && N > 1 && D > 0 && M > 0, VTF_E_ARG, "bad argument");
+        VTF_CHECK(0 <= row_begin && row_begin <= row_end && row_end <= N, VTF_E_ARG, "bad row range");
+        VTF_CHECK(M <= SW_MMAX, VTF_E_LIMIT, "silhouette_sweep: more than 32 label sets");
+        SilTables tb{};
+        tb.M = M;
+        int C = 0;
+        for (int m = 0; m < M; m++) {
+            VTF_CHECK(ks[m] >= 2 && ks[m] <= 255, VTF_E_ARG, "label set with fewer than 2 or more than 255 labels");
+            tb.off[m] = C;
+            tb.k[m] = ks[m];
+            VTF_CHECK(C + ks[m] <= SW_CMAX, VTF_E_LIMIT, "silhouette_sweep: more than 160 clusters in one pass");
+            for (int c = 0; c < ks[m]; c++, C++) {
+                tb.qm[C] = m;
+                tb.qc[C] = c;
+            }
+        }
+        tb.C = C;
+        if (row_end == row_begin) return;
+        Group& G = h->g;
+        double* nrm = G.ar.get<double>(5, N);
+        int64_t* dfreq = G.ar.get<int64_t>(7, C);
+        VTF_HIP(hipMemcpyAsync(dfreq, freq, (size_t)C * 8, hipMemcpyHostToDevice, G.st));
+        k_rownorm64<<<cdiv(N, 256), 256, 0, G.st>>>(d_X, N, (int)D, nrm);
+        k_sil_sweep<<<cdiv(row_end - row_begin, SW_T), 256, 0, G.st>>>(d_X, N, (int)D, nrm, d_labels, tb, dfreq,
+                                                                       row_begin, row_end, d_sil);
+        VTF_HIP(hipGetLastError());
+        VTF_HIP(hipStreamSynchronize(G.st));  // the host freq buffer may go away after return
     });
 }
 

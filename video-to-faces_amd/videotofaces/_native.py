@@ -52,6 +52,7 @@ SIGNATURES = {
     'vtf_blob_from_crops': [_p, _i32, _i32, _i32, _i64, _i64, _p, _i64, _i32, _f32, _f32, _p, _p],
     'vtf_gemm_split': [_p, _p, _i64, _i32, _i32, _p, _p, _p],
     'vtf_cosine_dedupe': [_p, _i64, _i64, _p, _p, _p],
+    'vtf_cosine_dedupe_rows': [_p, _i64, _i64, _i64, _i64, _p, _p, _p],
     'vtf_group_create': [_i32, _p],
     'vtf_group_destroy': [_p],
     'vtf_group_set_stream': [_p, _p],
@@ -62,6 +63,7 @@ SIGNATURES = {
     'vtf_center_dist': [_p, _p, _i64, _i64, _p, _p, _p],
     'vtf_pairwise_euclidean': [_p, _p, _i64, _i64, _p],
     'vtf_silhouette_samples': [_p, _p, _i64, _p, _i32, _p, _p],
+    'vtf_silhouette_sweep': [_p, _p, _i64, _i64, _i64, _i64, _p, _i32, _p, _p, _p],
     'vtf_cluster_sums': [_p, _p, _i64, _i64, _p, _i32, _p, _p, _p],
     'vtf_cluster_dist': [_p, _p, _i64, _i64, _p, _i32, _p, _p],
     'vtf_yolo_create': [_p, _i64, _i32, _i32, _p],

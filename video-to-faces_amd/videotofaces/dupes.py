@@ -8,6 +8,7 @@ matrix (the reference materialises an fp32 N x N plus an fp64 N x N mask).  The 
 (vtf_hamming_dedupe) instead of a Python-lambda pairwise_distances.
 """
 import ctypes
+import math
 import os
 import os.path as osp
 
@@ -19,13 +20,55 @@ from . import _native as nat
 
 def cosine_dedupe_device(X):
     """X: CUDA fp32 [N,D] -> (mins f32 [N], inds i64 [N]) exactly as dupes.py:60-64 computes
-    them: min / first argmin over j < i of clip(1 - cos(X_i, X_j), 0, 2); row 0 -> (10000, 0)."""
+    them: min / first argmin over j < i of clip(1 - cos(X_i, X_j), 0, 2); row 0 -> (10000, 0).
+    Under torch.distributed (every rank holding the same X) the rows are sharded across the
+    ranks (cosine_dedupe_sharded)."""
     X = X.to(torch.float32).contiguous()
+    if _world() > 1:
+        return cosine_dedupe_sharded(X)
+    return cosine_dedupe_rows(X, 0, X.shape[0])
+
+
+def cosine_dedupe_rows(X, lo, hi):
+    """rows [lo, hi) of cosine_dedupe_device (lo a multiple of 128, hi one or N)."""
     n, d = X.shape
-    mins = torch.empty(n, dtype=torch.float32, device=X.device)
-    inds = torch.empty(n, dtype=torch.int64, device=X.device)
-    nat.check(nat.lib().vtf_cosine_dedupe(nat.ptr(X), n, d, nat.ptr(mins), nat.ptr(inds), nat.stream_ptr(X.device)))
+    mins = torch.empty(hi - lo, dtype=torch.float32, device=X.device)
+    inds = torch.empty(hi - lo, dtype=torch.int64, device=X.device)
+    if hi > lo:
+        nat.check(nat.lib().vtf_cosine_dedupe_rows(nat.ptr(X), n, d, lo, hi, nat.ptr(mins), nat.ptr(inds),
+                                                   nat.stream_ptr(X.device)))
     return mins.cpu().numpy(), inds.cpu().numpy()
+
+
+def _world():
+    import torch.distributed as dist
+    return dist.get_world_size() if dist.is_available() and dist.is_initialized() else 1
+
+
+def dedupe_shards(n, world, tile=128):
+    """Row boundaries of the lower-triangle dedupe across `world` ranks: tile-aligned and
+    balanced by triangle area (rank r ends near n * sqrt((r+1) / world))."""
+    nt = -(-n // tile)
+    b = [min(n, int(round(nt * math.sqrt(r / world))) * tile) for r in range(world + 1)]
+    b[0], b[-1] = 0, n
+    for r in range(1, world + 1):
+        b[r] = max(b[r], b[r - 1])
+    return b
+
+
+def cosine_dedupe_sharded(X, rows_fn=None):
+    """the N x N dedupe row-block sharded across the ranks of the default process
+    group (each holds the gathered X), then one all-gather of the per-row (min, argmin) --
+    12 bytes a row.  rows_fn(lo, hi) -> (mins, inds) computes a shard (default: the device
+    kernel)."""
+    import torch.distributed as dist
+    world, rank = dist.get_world_size(), dist.get_rank()
+    n = X.shape[0]
+    b = dedupe_shards(n, world)
+    mins, inds = (rows_fn or (lambda lo, hi: cosine_dedupe_rows(X, lo, hi)))(b[rank], b[rank + 1])
+    parts = [None] * world
+    dist.all_gather_object(parts, (np.asarray(mins, np.float32), np.asarray(inds, np.int64)))
+    return np.concatenate([p[0] for p in parts]), np.concatenate([p[1] for p in parts])
 
 
 def pack_hashes(H):

@@ -86,34 +86,49 @@ def classify(X, R, classes, thr, log, paths, out_dir, device=None):
     return inds, classes
 
 
-def sweep_scores(X, k, random_state, grouper, prep=None):
-    """One k of cluster_faces (grouping.py:97-107): labels and (silhouette, CH, DB)."""
-    lb = grouper.kmeans(X, k, random_state=random_state, prep=prep)
-    return lb, (grouper.silhouette_score(X, lb), grouper.calinski_harabasz_score(X, lb),
-                grouper.davies_bouldin_score(X, lb))
-
-
-def cluster_sweep(X, clusters, random_state, compute=None, device=None):
-    """KMeans + scores for every k in `clusters`, in order.  With torch.distributed
-    initialised, rank r computes the k at positions i % world == r (each rank holds the
-    replicated X) and the results are all-gathered -- the parity-preserving sharding of
-    SURVEY.md §8e (no cross-rank reduction inside a fit)."""
+def _gather(obj):
     import torch.distributed as dist
-    if compute is None:
+    parts = [None] * dist.get_world_size()
+    dist.all_gather_object(parts, obj)
+    return parts
+
+
+def cluster_sweep(X, clusters, random_state, grouper=None, device=None):
+    """KMeans + (silhouette, CH, DB) for every k in `clusters`, in order -- cluster_faces'
+    loops (grouping.py:97-107).  With torch.distributed initialised (every rank holding the
+    gathered X) the work is sharded with no cross-rank reduction inside a
+    result, so every number equals the one-process result:
+      * KMeans fits by k: rank r fits the k at positions i % world == r; labels all-gathered;
+      * silhouette by rows: one pass over the distance rows of the rank's row range computes
+        silhouette_samples for EVERY k at once (no N x N matrix anywhere); the per-row values
+        are all-gathered and averaged in row order as silhouette_score's np.mean does;
+      * CH / DB by k, like the fits.
+    `grouper` defaults to the device Grouper (videotofaces.kmeans); tests pass a CPU stand-in."""
+    import torch.distributed as dist
+    if grouper is None:
         from .kmeans import Grouper
-        g = Grouper(device)
-        prep = g.prepare(X)
-        compute = lambda k: sweep_scores(X, k, random_state, g, prep)  # noqa: E731
+        grouper = Grouper(device)
+    g = grouper
+    X = np.ascontiguousarray(X, np.float32)
+    prep = g.prepare(X)
     world = dist.get_world_size() if dist.is_available() and dist.is_initialized() else 1
     rank = dist.get_rank() if world > 1 else 0
-    mine = {i: compute(k) for i, k in enumerate(clusters) if i % world == rank}
+    idx = [i for i in range(len(clusters)) if i % world == rank]
+    fits = {i: np.asarray(g.kmeans(X, clusters[i], random_state=random_state, prep=prep)) for i in idx}
     if world > 1:
-        parts = [None] * world
-        dist.all_gather_object(parts, {i: (np.asarray(lb), sc) for i, (lb, sc) in mine.items()})
-        for p in parts:
-            mine.update(p)
-    labels = [np.asarray(mine[i][0]) for i in range(len(clusters))]
-    scores = [(clusters[i],) + tuple(float(v) for v in mine[i][1]) for i in range(len(clusters))]
+        for p in _gather(fits):
+            fits.update(p)
+    labels = [fits[i] for i in range(len(clusters))]
+    n = X.shape[0]
+    lo, hi = n * rank // world, n * (rank + 1) // world
+    sil = g.silhouette_sweep(X, labels, lo, hi) if labels else np.zeros((0, 0), np.float32)
+    chdb = {i: (g.calinski_harabasz_score(X, labels[i]), g.davies_bouldin_score(X, labels[i])) for i in idx}
+    if world > 1:
+        sil = np.concatenate(_gather(sil), axis=1)
+        for p in _gather(chdb):
+            chdb.update(p)
+    scores = [(clusters[i], float(np.mean(sil[i])), float(chdb[i][0]), float(chdb[i][1]))
+              for i in range(len(clusters))]
     return labels, scores
 
 

@@ -10,8 +10,9 @@ Mirrors scikit-learn 1.7 (the reference's unpinned dependency, requirements.txt:
       sklearn/metrics/cluster/_unsupervised.py.
 The scalar control flow (RandomState draws, searchsorted over the float64 cumsum, argmin of
 candidate potentials, convergence tests) runs here on host numpy exactly as sklearn writes
-it; every pass over X (centring, k-means++ distance rows, E/M steps, the N x N distance
-matrix, silhouette rows, cluster statistics) is a libvtf_hip.so kernel.
+it; every pass over X (centring, k-means++ distance rows, E/M steps, the silhouette sweep over
+the distance rows -- never an N x N matrix -- and the cluster statistics) is a libvtf_hip.so
+kernel.
 """
 import ctypes
 
@@ -29,7 +30,6 @@ class Grouper:
         h = ctypes.c_void_p()
         nat.check(nat.lib().vtf_group_create(self.device.index or 0, ctypes.byref(h)))
         self._h = h
-        self._dist = None  # (X data_ptr, N, D) -> resident N x N distance matrix
 
     def __del__(self):
         h = getattr(self, '_h', None)
@@ -195,19 +195,6 @@ class Grouper:
         return np.asarray(self._to_host(labels), np.int32)
 
     # ------------------------------------------------------------------ scores
-    def distances(self, X):
-        """pairwise_distances(X) (euclidean, fp32 [N,N]) resident in HBM; cached per X."""
-        X = self._dev(X)
-        key = (X.data_ptr(), tuple(X.shape))
-        if self._dist is not None and self._dist[0] == key:
-            return self._dist[1]
-        N, D = X.shape
-        Dm = torch.empty((N, N), dtype=torch.float32, device=self.device)
-        self._bind()
-        nat.check(nat.lib().vtf_pairwise_euclidean(self._h, nat.ptr(X), N, D, nat.ptr(Dm)))
-        self._dist = (key, Dm, X)
-        return Dm
-
     @staticmethod
     def _encode(labels):
         """LabelEncoder().fit_transform + np.bincount (silhouette_samples prologue)."""
@@ -218,17 +205,37 @@ class Grouper:
                              % len(classes))
         return enc.astype(np.int32), np.bincount(enc).astype(np.int64), len(classes)
 
-    def silhouette_samples(self, X, labels):
+    def silhouette_sweep(self, X, label_sets, lo=0, hi=None):
+        """silhouette_samples(X, labels) for every label set, rows [lo, hi) -> float32 [M, hi-lo]
+        (vtf_silhouette_sweep: one pass over the distance rows per <= 160 clusters of label
+        sets, no N x N matrix)."""
         X = self._dev(X)
-        enc, freq, k = self._encode(labels)
-        Dm = self.distances(X)
-        N = X.shape[0]
-        dl = torch.from_numpy(enc).to(self.device)
-        df = torch.from_numpy(freq).to(self.device)
-        sil = torch.empty(N, dtype=torch.float32, device=self.device)
-        self._bind()
-        nat.check(nat.lib().vtf_silhouette_samples(self._h, nat.ptr(Dm), N, nat.ptr(dl), k, nat.ptr(df), nat.ptr(sil)))
-        return sil.cpu().numpy()
+        N, D = X.shape
+        hi = N if hi is None else hi
+        out = np.zeros((len(label_sets), hi - lo), np.float32)
+        enc = [self._encode(lb) for lb in label_sets]
+        i = 0
+        while i < len(enc):
+            j, c = i, 0
+            while j < len(enc) and j - i < 32 and c + enc[j][2] <= 160:
+                c += enc[j][2]
+                j += 1
+            if j == i:
+                raise ValueError('silhouette: %d labels (at most 160 per label set here)' % enc[i][2])
+            lab = np.stack([e[0] for e in enc[i:j]]).astype(np.uint8)
+            ks = np.ascontiguousarray([e[2] for e in enc[i:j]], np.int32)
+            freq = np.ascontiguousarray(np.concatenate([e[1] for e in enc[i:j]]), np.int64)
+            dl = torch.from_numpy(lab).to(self.device)
+            sil = torch.empty((j - i, hi - lo), dtype=torch.float32, device=self.device)
+            self._bind()
+            nat.check(nat.lib().vtf_silhouette_sweep(self._h, nat.ptr(X), N, D, lo, hi, nat.ptr(dl), j - i,
+                                                     ks.ctypes.data, freq.ctypes.data, nat.ptr(sil)))
+            out[i:j] = sil.cpu().numpy()
+            i = j
+        return out
+
+    def silhouette_samples(self, X, labels):
+        return self.silhouette_sweep(X, [labels])[0]
 
     def silhouette_score(self, X, labels):
         return float(np.mean(self.silhouette_samples(X, labels)))
