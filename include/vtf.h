@@ -27,6 +27,10 @@ extern "C" {
 #define VTF_E_LIMIT (-5)      /* an internal size limit was exceeded               */
 
 const char* vtf_last_error(void);
+/* Free the library's per-stream scratch (box ops, dedupe, conv tail workspaces) of a HIP
+ * stream the caller is about to destroy; waits for the stream.  Long-lived processes that
+ * create streams per request call this so device memory stays bounded. */
+int vtf_release_stream(void* hip_stream);
 int vtf_version(void);
 
 typedef struct vtf_mtcnn_s* vtf_mtcnn_t;

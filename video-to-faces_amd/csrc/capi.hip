@@ -31,13 +31,16 @@ int stream_device(hipStream_t st) {
     return dev;
 }
 
+namespace {
+struct Slot {
+    std::mutex mu;
+    Arena ar;
+};
+std::mutex g_mu;
+std::map<std::pair<int, hipStream_t>, std::unique_ptr<Slot>> g_slots;
+}  // namespace
+
 StreamScratch stream_scratch(hipStream_t st) {
-    struct Slot {
-        std::mutex mu;
-        Arena ar;
-    };
-    static std::mutex g_mu;
-    static std::map<std::pair<int, hipStream_t>, std::unique_ptr<Slot>> g_slots;
     const int dev = stream_device(st);
     Slot* s;
     {
@@ -49,6 +52,8 @@ StreamScratch stream_scratch(hipStream_t st) {
     return StreamScratch{&s->ar, std::unique_lock<std::mutex>(s->mu)};
 }
 
+void release_dma_ws(hipStream_t st);
+
 }  // namespace vtf
 
 using namespace vtf;
@@ -58,6 +63,24 @@ extern "C" {
 const char* vtf_last_error(void) { return g_err.c_str(); }
 
 int vtf_version(void) { return 1; }
+
+int vtf_release_stream(void* hip_stream) {
+    hipStream_t st = (hipStream_t)hip_stream;
+    return guarded_on(stream_device(st), [&] {
+        VTF_HIP(hipStreamSynchronize(st));
+        std::unique_ptr<Slot> s;
+        {
+            std::lock_guard<std::mutex> lk(g_mu);
+            auto it = g_slots.find({stream_device(st), st});
+            if (it != g_slots.end()) {
+                s = std::move(it->second);
+                g_slots.erase(it);
+            }
+        }
+        if (s) std::lock_guard<std::mutex> lk(s->mu);  // no entry point is still using it
+        release_dma_ws(st);
+    });
+}
 
 int vtf_batched_nms(const float* d_boxes, const float* d_scores, const int64_t* d_idxs, int64_t n,
                     double iou_threshold, int64_t* d_keep, int64_t* out_nkeep, void* hip_stream) {

@@ -942,16 +942,48 @@ __global__ __launch_bounds__(256) void k_conv_dma_tail(ConvParams p) {
     dma_epilogue<T, BN>(p, E, 16, (int64_t)tile_m * BM + wm * C::WM + i * 16, tile_n * BN);
 }
 
-// per-(device, stream) tail workspace: grows x1.5, outgrown buffers retired (hipFree would
-// synchronise the device while other streams' kernels may still use them)
+// per-(device, stream) tail workspace: grows x1.5.  An outgrown buffer may still be read by
+// kernels queued on its stream, so it is retired with an event recorded on that stream and
+// freed at a later grow once the event has completed (freeing it at once would need a
+// device-wide synchronisation that stalls the other lanes).  release_dma_ws(st) drops a
+// stream's entry (vtf_release_stream).
+namespace {
+struct DmaWs {
+    std::mutex mu;
+    std::map<std::pair<int, hipStream_t>, std::pair<float*, size_t>> m;
+    std::vector<std::pair<void*, hipEvent_t>> retired;
+    void reap() {
+        for (size_t i = 0; i < retired.size();) {
+            if (hipEventQuery(retired[i].second) == hipSuccess) {
+                (void)hipFree(retired[i].first);
+                (void)hipEventDestroy(retired[i].second);
+                retired[i] = retired.back();
+                retired.pop_back();
+            } else {
+                i++;
+            }
+        }
+    }
+    void retire(void* p, hipStream_t st) {
+        hipEvent_t ev;
+        VTF_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+        VTF_HIP(hipEventRecord(ev, st));
+        retired.push_back({p, ev});
+    }
+};
+DmaWs& dma_ws_state() {
+    static DmaWs* s = new DmaWs();  // process lifetime (no destruction-order issues at exit)
+    return *s;
+}
+}  // namespace
+
 float* dma_ws(hipStream_t st, size_t bytes) {
-    static std::mutex mu;
-    static std::map<std::pair<int, hipStream_t>, std::pair<float*, size_t>> m;
-    static std::vector<void*> retired;
-    std::lock_guard<std::mutex> g(mu);
-    auto& w = m[{stream_device(st), st}];
+    DmaWs& S = dma_ws_state();
+    std::lock_guard<std::mutex> g(S.mu);
+    auto& w = S.m[{stream_device(st), st}];
     if (w.second < bytes) {
-        if (w.first) retired.push_back(w.first);
+        S.reap();
+        if (w.first) S.retire(w.first, st);
         w.first = nullptr;
         w.second = 0;
         const size_t b = bytes + bytes / 2;
@@ -959,6 +991,17 @@ float* dma_ws(hipStream_t st, size_t bytes) {
         w.second = b;
     }
     return w.first;
+}
+
+void release_dma_ws_impl(hipStream_t st) {
+    DmaWs& S = dma_ws_state();
+    std::lock_guard<std::mutex> g(S.mu);
+    auto it = S.m.find({stream_device(st), st});
+    if (it != S.m.end()) {
+        if (it->second.first) S.retire(it->second.first, st);
+        S.m.erase(it);
+    }
+    S.reap();
 }
 
 // 16 zero bytes per device (the DMA source of padding, K-tail and M-tail pieces)
@@ -1087,6 +1130,10 @@ void launch_dma3_t(ConvParams p, hipStream_t st) {
 }
 
 }  // namespace
+
+// (vtf_release_stream, capi.hip)
+void release_dma_ws(hipStream_t st) { release_dma_ws_impl(st); }
+
 
 // conv (split pairs, bias + PReLU) + MaxPool2d(k, s, ceil_mode=True) in one launch
 // (k_conv_span_pool); false (nothing launched) when the shape does not fit its tiles

@@ -1318,11 +1318,12 @@ void launch_pnet(bool dense, const uint8_t* frames, int64_t frame_stride, int64_
     // 12.31-12.37k faces/s (same box)
     // tiles per atomic chunk (VTF_PNET_CHUNK, default PNET_TILE_CHUNK)
     const char* ce = std::getenv("VTF_PNET_CHUNK");
-    const int chunk = ce && std::atoi(ce) > 0 ? std::atoi(ce) : PNET_TILE_CHUNK;
+    // (clamped: the kernel keeps tile indices and chunk ends in int)
+    const int chunk = ce && std::atoi(ce) > 0 ? std::min(64, std::atoi(ce)) : PNET_TILE_CHUNK;
     const char* qe = std::getenv("VTF_PNET_QUOTA");
     // (chunk x quota at 8 tiles per workgroup, full default run: 4 x 2 12.26-12.30k, 2 x 4
     // 12.19-12.21k, 1 x 8 12.18k faces/s)
-    const int quota = qe ? std::max(0, std::atoi(qe)) : 2;
+    const int quota = qe ? std::min(1 << 16, std::max(0, std::atoi(qe))) : 2;
     if (!w.c3h || !w.hh || dense || (xe && std::atoi(xe) == 0)) exact_tiles = 0;
     exact_tiles = std::min(exact_tiles, total_tiles);
     if (exact_tiles > 0) {

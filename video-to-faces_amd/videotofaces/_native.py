@@ -27,6 +27,7 @@ _f32 = _c.c_float
 SIGNATURES = {
     'vtf_last_error': [],
     'vtf_version': [],
+    'vtf_release_stream': [_p],
     'vtf_mtcnn_create': [_p, _i64, _i32, _p],
     'vtf_mtcnn_destroy': [_p],
     'vtf_mtcnn_set_stream': [_p, _p],

@@ -55,7 +55,12 @@ def _rows_to_crops(rows, img_size, params, frame_offset=0, device=None):
 def filter_boxes(boxes, img_size, mscore, msize, mborder, *debug_io, device=None):
     """filter_boxes (detection.py:174-217) on the device box kernel: integer-rounded boxes that
     pass check_box (score, size, border), as (x1, y1, x2, y2, score) tuples.  The reference's
-    save_frames / save_rejects debug IO (its trailing arguments) is not mirrored."""
+    save_frames / save_rejects debug IO (its trailing arguments) is not mirrored.
+    This per-call wrapper (one H2D, a launch and a D2H) keeps the reference's signature; the
+    pipeline never calls it -- detect_crops runs the same kernel once per det-batch on the
+    detector's device rows.  There is deliberately no host implementation in the product (the
+    library is the only compute path; the numpy restatement lives in oracle/boxes.py, pinned by
+    tests/golden/boxes.npz, for tests only)."""
     from . import _native as nat
     b = np.asarray(boxes, np.float32).reshape(-1, 5)
     cr, src, _ = _rows_to_crops([b], img_size, nat.BoxParams.make(mscore, msize, mborder, adjust=False),

@@ -74,6 +74,9 @@ def classify(X, R, classes, thr, log, paths, out_dir, device=None):
         classes.append('other')
     if log:
         # the per-class distances of the CSV: the same device kernel against one class at a time
+        # (fp32 on the device; sklearn's cosine_distances rounds differently in the last bits --
+        # the CSV prints them with '%.4f', so the logged text matches wherever a value is not
+        # within ~1e-7 of a rounding boundary of the 4th decimal)
         R = np.asarray(R, np.float32)
         dist = np.stack([cosine_classify_device(X, R[c:c + 1], device)[0] for c in range(R.shape[0])], 1)
         fnames = [osp.basename(p) for p in paths]
