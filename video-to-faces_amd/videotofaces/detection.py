@@ -59,8 +59,8 @@ def filter_boxes(boxes, img_size, mscore, msize, mborder, *debug_io, device=None
     This per-call wrapper (one H2D, a launch and a D2H) keeps the reference's signature; the
     pipeline never calls it -- detect_crops runs the same kernel once per det-batch on the
     detector's device rows.  There is deliberately no host implementation in the product (the
-    library is the only compute path; the numpy restatement lives in oracle/boxes.py, pinned by
-    tests/golden/boxes.npz, for tests only)."""
+    library is the only compute path; the test suite's numpy restatement is pinned by
+    tests/golden/boxes.npz)."""
     from . import _native as nat
     b = np.asarray(boxes, np.float32).reshape(-1, 5)
     cr, src, _ = _rows_to_crops([b], img_size, nat.BoxParams.make(mscore, msize, mborder, adjust=False),
