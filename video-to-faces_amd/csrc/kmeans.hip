@@ -8,8 +8,9 @@
 //   k_sqdist_rows  _euclidean_distances(X[ids], X, squared=True) for float32 X: the
 //                  float64-upcast formula (-2 x.y + |x|^2 + |y|^2 in double, then float32,
 //                  max 0; sklearn/metrics/pairwise.py:391-441,582-660).
-//   k_estep        Lloyd E-step (_k_means_lloyd.pyx:_update_chunk_dense): |c|^2 - 2 x.c in
-//                  fp32, first strict minimum; counts label changes.
+//   k_estep        Lloyd E-step (_k_means_lloyd.pyx:_update_chunk_dense) in sklearn's bits:
+//                  numpy's einsum order for |c|^2, OpenBLAS's sgemm orders for -2 x.c (see
+//                  below), first strict minimum; counts label changes.
 //   k_seg_*, k_msum_seq  M-step sums in sklearn's single-thread order (sequential fp32 per
 //                  cluster and feature, rows in order) via a stable counting sort by label.
 //   k_average      _average_centers (c *= 1/w) and _center_shift (4-way unrolled fp32).
@@ -100,45 +101,132 @@ __global__ __launch_bounds__(256) void k_sqdist_rows(const float* __restrict__ X
     }
 }
 
-// ------------------------------------------------------------------ Lloyd
+// ------------------------------------------------------------------ Lloyd E-step, sklearn's bits
+// _update_chunk_dense (_k_means_lloyd.pyx:168-215) on 256-row chunks: pd = |c|^2 (row_norms
+// = np.einsum('ij,ij->i')), then scipy's sgemm adds -2 X C^T (_gemm RowMajor NoTrans/Trans ->
+// Fortran sgemm('T', 'N', k, m, D, -2, C, D, X, D, 1, pd, k)), first strict minimum.  Both
+// libraries' summation orders were measured bit for bit in the survey container (numpy 2.2
+// with its SSE baseline einsum, scipy's OpenBLAS 0.3.28 SKYLAKEX kernels; probes by
+// absorption -- 2^30, -2^30 and 1 at chosen positions -- then exact match on random data over
+// D in {512, 768, 1024}, k 2..16, chunk rows 1..256; scripts/sklearn_order.py):
+//   einsum  4 SSE lanes over d mod 4; each 16-element step adds the products of elements
+//           12..15, 8..11, 4..7, 0..3 in that order (mul, then add: no FMA in the baseline);
+//           4-element zero-padded tail steps; result (l0 + l1) + (l2 + l3).
+//   sgemm, small-matrix kernel when m*k*D <= 1e6, k*m <= 1200 and D >= 32: 16 lanes over
+//           d mod 16, sequential fma per lane; lanes summed as the adjacent-pair tree
+//           ((l0+l1)+(l2+l3))+... except the C tile's edge block -- chunk row >= m - m%4 and
+//           cluster >= k - k%4 -- which takes the halving tree (l_i + l_{i+8}, +4, +2, +1);
+//           pd = pd - 2 s (one rounding: the x2 is exact).
+//   sgemm, blocked kernel otherwise: D in K blocks (448, or the two halves of a remainder
+//           between 448 and 896 rounded up to 16), sequential fma per block from 0, and
+//           pd = pd - 2 acc after every block.
+// (Exact for D % 16 == 0; other D follow the same rules without that verification.)
+__device__ inline float np_einsum_sq(const float* __restrict__ c, int D) {
+    float l[4] = {0.f, 0.f, 0.f, 0.f};
+    int t = 0;
+    for (; D - t >= 16; t += 16)
+        for (int q = 3; q >= 0; q--)
+#pragma unroll
+            for (int u = 0; u < 4; u++) l[u] = __fadd_rn(__fmul_rn(c[t + 4 * q + u], c[t + 4 * q + u]), l[u]);
+    for (; t < D; t += 4)
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const float v = t + u < D ? c[t + u] : 0.f;
+            l[u] = __fadd_rn(__fmul_rn(v, v), l[u]);
+        }
+    return __fadd_rn(__fadd_rn(l[0], l[1]), __fadd_rn(l[2], l[3]));
+}
+
 __global__ void k_csq(const float* __restrict__ C, int k, int D, float* __restrict__ csq) {
     int j = blockIdx.x * blockDim.x + threadIdx.x;
     if (j >= k) return;
-    float s = 0.f;
-    for (int d = 0; d < D; d++) s += C[(int64_t)j * D + d] * C[(int64_t)j * D + d];
-    csq[j] = s;
+    csq[j] = np_einsum_sq(C + (int64_t)j * D, D);
 }
 
-// one wave per sample; centers staged in LDS
+__host__ __device__ inline bool sk_small_gemm(int64_t m, int k, int D) {
+    return (double)m * k * D <= 1e6 && (int64_t)k * m <= 1200 && D >= 32;
+}
+
+// one thread per (row, cluster): 16 rows x 16 clusters per block; X and C staged through LDS
+// in 32-deep slices; the per-row argmin over the clusters at the end (first strict minimum)
+constexpr int ES_R = 16, ES_C = 16, ES_K = 32;
 __global__ __launch_bounds__(256) void k_estep(const float* __restrict__ X, int64_t N, int D,
                                                const float* __restrict__ C, const float* __restrict__ csq, int k,
                                                int32_t* __restrict__ labels, unsigned long long* __restrict__ changed) {
-    extern __shared__ float sC[];  // [k][D]
-    for (int e = threadIdx.x; e < k * D; e += blockDim.x) sC[e] = C[e];
-    __syncthreads();
-    const int lane = threadIdx.x & 63;
-    const int64_t wid = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-    const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
-    unsigned long long nchg = 0;
-    for (int64_t i = wid; i < N; i += nw) {
-        float best = 0.f;
+    __shared__ float sX[ES_R][ES_K + 1], sCt[ES_C][ES_K + 1];
+    __shared__ float sD[ES_R][64 + 1];
+    const int tid = threadIdx.x, r = tid >> 4, cj = tid & 15;
+    const int64_t i0 = (int64_t)blockIdx.x * ES_R, i = i0 + r;
+    // sklearn's 256-row chunk of this row: local row index and the chunk's row count
+    const int64_t cs = (i0 / 256) * 256;
+    const int m = (int)min<int64_t>(256, N - cs);
+    const int il = (int)(i - cs);
+    const bool small = sk_small_gemm(m, k, D);
+    for (int j0 = 0; j0 < k; j0 += ES_C) {
+        const int j = j0 + cj;
+        float lane[16];
+#pragma unroll
+        for (int u = 0; u < 16; u++) lane[u] = 0.f;
+        float acc = 0.f, pd = j < k ? csq[j] : 0.f;
+        // K blocks of the blocked kernel (the small kernel ignores them)
+        int kb_end = D >= 2 * 448 ? 448 : (D > 448 ? ((D / 2 + 15) / 16) * 16 : D);
+        for (int t0 = 0; t0 < D; t0 += ES_K) {
+            for (int e = tid; e < ES_R * ES_K; e += 256) {
+                const int rr = e / ES_K, tt = e % ES_K;
+                sX[rr][tt] = (i0 + rr < N && t0 + tt < D) ? X[(i0 + rr) * D + t0 + tt] : 0.f;
+                sCt[rr][tt] = (j0 + rr < k && t0 + tt < D) ? C[(int64_t)(j0 + rr) * D + t0 + tt] : 0.f;
+            }
+            __syncthreads();
+            const int tn = min(ES_K, D - t0);
+            if (small) {
+#pragma unroll
+                for (int tt = 0; tt < ES_K; tt++)
+                    if (tt < tn) lane[(t0 + tt) & 15] = fmaf(sX[r][tt], sCt[cj][tt], lane[(t0 + tt) & 15]);
+            } else {
+                for (int tt = 0; tt < tn; tt++) {
+                    acc = fmaf(sX[r][tt], sCt[cj][tt], acc);
+                    if (t0 + tt + 1 == kb_end) {  // end of a K block: C += alpha * block
+                        pd = fmaf(-2.f, acc, pd);
+                        acc = 0.f;
+                        const int rest = D - kb_end;
+                        kb_end += rest >= 2 * 448 ? 448 : (rest > 448 ? ((rest / 2 + 15) / 16) * 16 : rest);
+                    }
+                }
+            }
+            __syncthreads();
+        }
+        if (small) {
+            float s;
+            if (il >= m - m % 4 && j >= k - k % 4) {  // edge block of the C tile: halving tree
+#pragma unroll
+                for (int w = 8; w >= 1; w >>= 1)
+#pragma unroll
+                    for (int u = 0; u < w; u++) lane[u] = __fadd_rn(lane[u], lane[u + w]);
+                s = lane[0];
+            } else {  // adjacent pairs
+#pragma unroll
+                for (int w = 1; w < 16; w <<= 1)
+#pragma unroll
+                    for (int u = 0; u < 16; u += 2 * w) lane[u] = __fadd_rn(lane[u], lane[u + w]);
+                s = lane[0];
+            }
+            pd = fmaf(-2.f, s, pd);
+        }
+        if (cj < 16) sD[r][j0 + cj < 64 ? (j0 + cj) : 64] = pd;
+        __syncthreads();
+        // (k <= 64: sD holds every cluster's distance for the rows of this block)
+    }
+    if (cj == 0 && i < N) {
+        float best = sD[r][0];
         int lab = 0;
-        for (int j = 0; j < k; j++) {
-            float s = 0.f;
-            for (int d = lane; d < D; d += 64) s = fmaf(X[i * D + d], sC[j * D + d], s);
-            s = wave_sum_f32(s);
-            float dist = csq[j] + (-2.f * s);
-            if (j == 0 || dist < best) {
-                best = dist;
+        for (int j = 1; j < k; j++)
+            if (sD[r][j] < best) {
+                best = sD[r][j];
                 lab = j;
             }
-        }
-        if (lane == 0) {
-            if (labels[i] != lab) nchg++;
-            labels[i] = lab;
-        }
+        if (labels[i] != lab) atomicAdd(changed, 1ull);
+        labels[i] = lab;
     }
-    if (lane == 0 && nchg) atomicAdd(changed, nchg);
 }
 
 // M-step sums in sklearn's single-thread order.  _update_chunk_dense (_k_means_lloyd.pyx:
@@ -671,15 +759,14 @@ int vtf_sqdist_rows(vtf_group_t h, const float* d_X, int64_t N, int64_t D, const
 int vtf_kmeans_step(vtf_group_t h, const float* d_X, int64_t N, int64_t D, const float* d_centers, int k,
                     int32_t* d_labels, float* d_sums, float* d_weights, int64_t* out_changed) {
     return guarded_on(h ? h->g.device : -1, [&] {
-        VTF_CHECK(h && d_X && d_centers && d_labels && N > 0 && D > 0 && k > 0 && k <= 256, VTF_E_ARG,
+        VTF_CHECK(h && d_X && d_centers && d_labels && N > 0 && D > 0 && k > 0 && k <= 64, VTF_E_ARG,
                   "bad argument");
-        VTF_CHECK((size_t)k * D * 4 <= 128 * 1024, VTF_E_LIMIT, "kmeans: k*D too large for LDS");
         Group& G = h->g;
         float* csq = G.ar.get<float>(1, k);
         unsigned long long* chg = G.ar.get<unsigned long long>(2, 1);
         VTF_HIP(hipMemsetAsync(chg, 0, 8, G.st));
         k_csq<<<cdiv(k, 64), 64, 0, G.st>>>(d_centers, k, (int)D, csq);
-        k_estep<<<waves_grid(N), 256, (size_t)k * D * 4, G.st>>>(d_X, N, (int)D, d_centers, csq, k, d_labels, chg);
+        k_estep<<<(unsigned)cdiv(N, ES_R), 256, 0, G.st>>>(d_X, N, (int)D, d_centers, csq, k, d_labels, chg);
         if (d_sums) {
             VTF_CHECK(d_weights, VTF_E_ARG, "null weights");
             VTF_CHECK(k <= 64, VTF_E_LIMIT, "kmeans: k > 64");
