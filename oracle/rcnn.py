@@ -158,6 +158,56 @@ def rpn(P, fmaps, pri, imsizes):
     return rpn_select(regs, logs, pri, imsizes)
 
 
+def _fma32(a, b, c):
+    return (np.asarray(a, np.float64) * np.asarray(b, np.float64) + np.asarray(c, np.float64)).astype(np.float32)
+
+
+def sleef_expf_u10(d):
+    """Sleef_expf16_u10 (AVX512 build inside libtorch_cpu.so, disassembled; Horner with fma,
+    2^q applied as two exact power-of-two products)"""
+    f = np.float32
+    d = np.asarray(d, np.float32)
+    q = np.rint((d * f(1.44269502162933349609375)).astype(np.float32)).astype(np.int32)
+    qf = q.astype(np.float32)
+    s = _fma32(qf, f(-0.693145751953125), d)
+    s = _fma32(qf, f(-1.428606765330187045e-06), s)
+    u = np.full_like(d, f(0.000198527617612853646278381))
+    for c in (0.00139304355252534151077271, 0.00833336077630519866943359, 0.0416664853692054748535156,
+              0.166666671633720397949219, 0.5):
+        u = _fma32(s, u, f(c))
+    u = (_fma32((s * s).astype(np.float32), u, s) + f(1)).astype(np.float32)
+    h = q >> 1
+    u = (u * np.exp2(h.astype(np.float64)).astype(np.float32)).astype(np.float32)
+    u = (u * np.exp2((q - h).astype(np.float64)).astype(np.float32)).astype(np.float32)
+    u = np.where(d < -104, f(0), u)
+    return np.where(d > 100, f(np.inf), u).astype(np.float32)
+
+
+def torch_sigmoid_survey(x, threads=8):
+    """torch.sigmoid of a contiguous float32 tensor exactly as torch 2.10 computes it on the
+    survey container's CPU (AVX512 capability, `threads` intra-op threads): 1 / (1 + exp(-x))
+    with Sleef_expf16_u10 on the 32-element vector steps of each parallel_for chunk and glibc
+    expf on each chunk's last (len % 32) elements (scripts/torch_sigmoid_order.py checks it
+    against torch bit for bit).  Used by rpn_select so that the GPU box's own torch build and
+    CPU (vector width, thread count) do not enter the oracle."""
+    import ctypes
+    x = np.ascontiguousarray(np.asarray(x, np.float32).ravel())
+    n = x.size
+    f = np.float32
+    out = (f(1) / (f(1) + sleef_expf_u10(f(0) - x)).astype(np.float32)).astype(np.float32)
+    if n == 0:
+        return out
+    libm = ctypes.CDLL('libm.so.6')
+    libm.expf.restype, libm.expf.argtypes = ctypes.c_float, [ctypes.c_float]
+    nt = min(threads, -(-n // 32768))
+    cs = -(-n // nt)
+    for c0 in range(0, n, cs):
+        c1 = min(n, c0 + cs)
+        for i in range(c1 - (c1 - c0) % 32, c1):
+            out[i] = f(1) / f(f(1) + f(libm.expf(float(-x[i]))))
+    return out
+
+
 def rpn_select(regs, logs, pri, imsizes):
     """filt_dec + sigmoid + clamp + remove_small + batched_nms(0.7) + top-1000 per image
     (rcnn.py:49-82) from the head outputs."""
@@ -171,7 +221,8 @@ def rpn_select(regs, logs, pri, imsizes):
         logits.append(log)
         lvlen.append(log.shape[1])
     boxes = torch.cat(boxes, axis=1)
-    obj = torch.cat(logits, axis=1).sigmoid()
+    cat = torch.cat(logits, axis=1)
+    obj = torch.from_numpy(torch_sigmoid_survey(cat.numpy())).reshape(cat.shape)
     dim = boxes.shape[1]
     boxes, obj = boxes.reshape(-1, 4), obj.flatten()
     idx = torch.nonzero(obj >= 0).squeeze(1)

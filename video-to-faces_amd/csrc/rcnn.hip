@@ -462,6 +462,10 @@ struct RDec {
     RLevel lv[R_LEVELS];
     int64_t Ltot, dim;
     float wu, hu;  // used (unpadded) image size: clamp_to_canvas bounds
+    // CPU threads of the reference run whose sigmoid rounding is reproduced (torch_sigmoid): it
+    // only matters above 32768 objectness values (det-batch >= 7); VTF_TORCH_THREADS, default 8
+    // (the survey container that made the goldens)
+    int torch_threads;
 };
 
 __device__ inline int level_of(const RDec& d, int64_t r, bool tops) {
@@ -484,6 +488,77 @@ __global__ void k_rpn_keys(RDec d, int64_t total, uint64_t* __restrict__ keys, i
     float logit = L.head[(b * L.h * L.w + cell) * 15 + a];
     keys[i] = ((uint64_t)(b * R_LEVELS + l) << 32) | desc_key(logit);
     vals[i] = (int32_t)p;
+}
+
+// torch's CPU sigmoid, bit for bit (rcnn.py:68 `torch.cat(logits).sigmoid()`): ATen's
+// sigmoid_kernel runs 1 / (1 + exp(-x)) with Vectorized<float>::exp = Sleef_expf16_u10 on the
+// 32-element vector steps of every parallel_for chunk and the scalar lambda (std::exp = glibc
+// expf) on each chunk's last (len % 32) elements; chunks = divup(numel, min(threads,
+// divup(numel, 32768))).  Measured in the survey container (AVX512 capability; the Sleef
+// routine disassembled from libtorch_cpu.so, constants read from the binary) and matched bit for
+// bit over 4e5 random logits (scripts/torch_sigmoid_order.py).
+__device__ inline float sleef_expf_u10(float d) {
+    const float q = rintf(d * 1.44269502162933349609375f);  // vcvtps2dq: round to nearest even
+    float s = fmaf(q, -0.693145751953125f, d);
+    s = fmaf(q, -1.428606765330187045e-06f, s);
+    float u = 0.000198527617612853646278381f;
+    u = fmaf(s, u, 0.00139304355252534151077271f);
+    u = fmaf(s, u, 0.00833336077630519866943359f);
+    u = fmaf(s, u, 0.0416664853692054748535156f);
+    u = fmaf(s, u, 0.166666671633720397949219f);
+    u = fmaf(s, u, 0.5f);
+    u = fmaf(s * s, u, s);
+    u = u + 1.0f;
+    const int qi = (int)q, h = qi >> 1;
+    u *= __int_as_float((h + 127) << 23);
+    u *= __int_as_float((qi - h + 127) << 23);
+    if (d < -104.f) u = 0.f;
+    if (100.f < d) u = INFINITY;
+    return u;
+}
+
+// glibc 2.35 expf (sysdeps/ieee754/flt-32/e_expf.c, EXP2F_TABLE_BITS 5): double-precision
+// k/N + r reduction, table 2^(i/32), cubic polynomial
+__constant__ uint64_t GLIBC_EXP2F_TAB[32] = {
+    0x3ff0000000000000ull, 0x3fefd9b0d3158574ull, 0x3fefb5586cf9890full, 0x3fef9301d0125b51ull,
+    0x3fef72b83c7d517bull, 0x3fef54873168b9aaull, 0x3fef387a6e756238ull, 0x3fef1e9df51fdee1ull,
+    0x3fef06fe0a31b715ull, 0x3feef1a7373aa9cbull, 0x3feedea64c123422ull, 0x3feece086061892dull,
+    0x3feebfdad5362a27ull, 0x3feeb42b569d4f82ull, 0x3feeab07dd485429ull, 0x3feea47eb03a5585ull,
+    0x3feea09e667f3bcdull, 0x3fee9f75e8ec5f74ull, 0x3feea11473eb0187ull, 0x3feea589994cce13ull,
+    0x3feeace5422aa0dbull, 0x3feeb737b0cdc5e5ull, 0x3feec49182a3f090ull, 0x3feed503b23e255dull,
+    0x3feee89f995ad3adull, 0x3feeff76f2fb5e47ull, 0x3fef199bdd85529cull, 0x3fef3720dcef9069ull,
+    0x3fef5818dcfba487ull, 0x3fef7c97337b9b5full, 0x3fefa4afa2a490daull, 0x3fefd0765b6e4540ull};
+
+__device__ inline float glibc_expf(float x) {
+    if (x != x) return x + x;
+    if (x > 88.72283172607421875f) return INFINITY;    // 0x1.62e42ep6f
+    if (x < -103.972076416015625f) return 0.f;         // -0x1.9fe368p6f
+    const double xd = (double)x;
+    const double z = 46.16624130844682704 * xd;        // 0x1.71547652b82fep+5 = 32 / ln 2
+    const double shift = 6755399441055744.0;           // 0x1.8p+52
+    double kd = z + shift;
+    const uint64_t ki = (uint64_t)__double_as_longlong(kd);
+    kd -= shift;
+    const double r = z - kd;
+    uint64_t t = GLIBC_EXP2F_TAB[ki % 32];
+    t += ki << (52 - 5);
+    const double sc = __longlong_as_double((long long)t);
+    const double zz = fma(1.6938359250920212e-06, r, 0.00023459809789509004);   // C0 r + C1
+    const double r2 = r * r;
+    double y = fma(0.021660849396613134, r, 1.0);                             // C2 r + 1
+    y = fma(zz, r2, y);
+    return (float)(y * sc);
+}
+
+// element j of a numel-element contiguous float tensor through torch.sigmoid on `threads` CPU
+// threads (the reference's own run: the chunk tails take the scalar glibc path)
+__device__ inline float torch_sigmoid(float x, int64_t j, int64_t numel, int threads) {
+    const int64_t nt = min<int64_t>(threads, (numel + 32767) / 32768);
+    const int64_t cs = (numel + nt - 1) / nt;
+    const int64_t c0 = (j / cs) * cs, c1 = min(numel, c0 + cs);
+    const bool scalar = j >= c1 - (c1 - c0) % 32;
+    const float e = scalar ? glibc_expf(-x) : sleef_expf_u10(0.f - x);
+    return __fdiv_rn(1.f, 1.f + e);
 }
 
 // filt_dec + sigmoid + clamp_to_canvas + remove_small(0) (rcnn.py:49-77; bbox.py:6-60)
@@ -513,7 +588,7 @@ __global__ void k_rpn_decode(RDec d, int64_t total, const int32_t* __restrict__ 
     bx.z = fminf(fmaxf(bx.z, 0.f), d.wu);
     bx.w = fminf(fmaxf(bx.w, 0.f), d.hu);
     boxes[j] = bx;
-    obj[j] = __fdiv_rn(1.f, 1.f + expf(-logit));
+    obj[j] = torch_sigmoid(logit, j, total, d.torch_threads);
     group[j] = (int32_t)(b * 10 + l);
     flag[j] = ((bx.z - bx.x) > 0.f && (bx.w - bx.y) > 0.f) ? 1 : 0;
 }
@@ -558,6 +633,8 @@ static RDec make_rdec(float* const heads[R_LEVELS], const RMap P[R_LEVELS], int 
     d.dim = toff;
     d.wu = (float)w_used;
     d.hu = (float)h_used;
+    const char* te = std::getenv("VTF_TORCH_THREADS");
+    d.torch_threads = te && std::atoi(te) > 0 ? std::atoi(te) : 8;
     return d;
 }
 
