@@ -676,9 +676,27 @@ static int64_t rpn_proposals(Rcnn& R, float* const heads[R_LEVELS], const RMap P
     nms_multi(R.ar, (const float*)cb, cs, cg, call, {(int64_t)n}, 10 * B, 0.7, keep, nk, st);
     const int64_t kn = nk.empty() ? 0 : nk[0];
     std::vector<int32_t> hk(kn), hg(std::max(n, 1));
+    std::vector<float> hs((size_t)std::max(n, 1));
     if (kn) VTF_HIP(hipMemcpyAsync(hk.data(), keep, kn * 4, hipMemcpyDeviceToHost, st));
     if (n) VTF_HIP(hipMemcpyAsync(hg.data(), cg, (size_t)n * 4, hipMemcpyDeviceToHost, st));
+    if (n && 4 * (int64_t)n > 4000) VTF_HIP(hipMemcpyAsync(hs.data(), cs, (size_t)n * 4, hipMemcpyDeviceToHost, st));
     VTF_HIP(hipStreamSynchronize(st));
+    if (4 * (int64_t)n > 4000) {
+        // batched_nms above 4000 coordinates (torchvision ops/boxes.py) returns
+        // keep_indices[scores[keep_indices].sort(descending=True)[1]] with keep_indices in index
+        // order and torch's default (unstable) CPU sort: std::sort of (score, position) pairs with
+        // ATen's KeyValueCompDesc (SortingKernel.cpp) -- its tie order reproduced exactly (checked
+        // against torch.sort on tie-heavy inputs, scripts/torch_sigmoid_order.py)
+        std::sort(hk.begin(), hk.end());
+        std::vector<std::pair<float, int64_t>> kv(kn);
+        for (int64_t t = 0; t < kn; t++) kv[t] = {hs[hk[t]], t};
+        std::sort(kv.begin(), kv.end(), [](const std::pair<float, int64_t>& a, const std::pair<float, int64_t>& b) {
+            return (std::isnan(a.first) && !std::isnan(b.first)) || (a.first > b.first);
+        });
+        std::vector<int32_t> ord(kn);
+        for (int64_t t = 0; t < kn; t++) ord[t] = hk[kv[t].second];
+        hk.swap(ord);
+    }
     // keep[imidx[keep] == i][:1000] for each image, concatenated (rcnn.py:80)
     std::vector<int32_t> sel, simg;
     std::vector<int> per(B, 0);
