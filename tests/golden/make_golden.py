@@ -599,6 +599,53 @@ def gen_chain():
           'sklearn 1 vs %d threads: rows differing per k' % os.cpu_count(), (labels != labels_mt).sum(1).tolist())
 
 
+C3 = dict(frames=32, seed=110, mscore=0.4, msize=50, mborder=5, scale=(1.5, 1.5, 2.2, 1.2), square=True)
+
+
+def gen_c3():
+    """BASELINE config 3's shapes end to end: YOLOv3 on one det-batch of 32 synthetic 720p
+    frames -> the reference's filter_boxes / adjust_boxes (bench settings = reference defaults)
+    -> FaceNet on the crops (blobFromImages restated: INTER_LINEAR 160x160, parity-unpinned
+    step).  Reference modules throughout; frames flagged where a box coordinate lies within
+    2e-3 px of an integer or a score within 1e-4 of min_score (as gen_chain)."""
+    import json
+    load_ref()
+    sys.path.insert(0, ROOT)
+    from oracle.facenet import resize_linear_u8
+    c = C3
+    y = importlib.import_module('ref_vtf.detectors.yolo')
+    det = importlib.import_module('ref_vtf.detection')
+    f = importlib.import_module('ref_vtf.encoders.facenet')
+    ynet = _load(y.YOLOv3('cpu'), synth.make_params('yolo'))
+    fnet = _load(f.InceptionResnetV1('cpu'), synth.make_params('facenet'))
+    frames = synth.make_frames(c['frames'], seed=c['seed'])
+    b, sc, _ = _yolo_ref(ynet, y, frames)
+    rects, flagged, counts, boxes, scores = [], [], [], [], []
+    sp = ('', '', None, False, False, False)
+    for i, (bi, si) in enumerate(zip(b, sc)):
+        rows = np.concatenate([bi, si[:, None]], 1)
+        counts.append(len(rows))
+        boxes.append(bi)
+        scores.append(si)
+        kept = det.filter_boxes(rows, (720, 1280), c['mscore'], c['msize'], c['mborder'], sp, None, 0)
+        adj = det.adjust_boxes(kept, (720, 1280), c['scale'], c['square'])
+        rects.extend((i, x1, y1, x2, y2) for (x1, y1, x2, y2, _) in adj)
+        live = si >= c['mscore'] - 1e-3
+        if live.any() and (np.abs(bi[live] - np.round(bi[live])).min() < 2e-3 or np.abs(si - c['mscore']).min() < 1e-4):
+            flagged.append(i)
+    rects = np.array(rects, np.int32).reshape(-1, 5)
+    blobs = []
+    for fi, x1, y1, x2, y2 in rects:
+        r = resize_linear_u8(frames[fi, y1:y2, x1:x2], 160)[:, :, ::-1].transpose(2, 0, 1)
+        blobs.append((torch.from_numpy(np.ascontiguousarray(r)).float() - 127.5) * np.float32(1 / 128))
+    with torch.inference_mode():
+        emb = fnet(torch.stack(blobs)).numpy() if blobs else np.zeros((0, 512), np.float32)
+    np.savez_compressed(os.path.join(HERE, 'c3.npz'), params_json=np.array(json.dumps(c)),
+                        counts=np.array(counts, np.int64), boxes=np.concatenate(boxes), scores=np.concatenate(scores),
+                        rects=rects, emb=emb, flagged_frames=np.array(flagged, np.int64))
+    print('c3: detections', sum(counts), 'crops', len(rects), 'flagged frames', flagged)
+
+
 SCALE = dict(n=30000, seed=0, thr=0.25, ks=list(range(2, 17)))
 
 
@@ -735,6 +782,6 @@ def gen_boxes():
 
 if __name__ == '__main__':
     which = sys.argv[1:] or ['mtcnn', 'facenet', 'vit', 'grouping', 'yolo', 'kmeans', 'rcnn', 'dupes', 'boxes', 'shapes', 'chain',
-                             'scale', 'iom']
+                             'scale', 'c3', 'iom']
     for w in which:
         globals()['gen_' + w]()

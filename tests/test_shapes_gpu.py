@@ -84,6 +84,47 @@ def test_yolo_1080p_b4(g, precision):
     np.testing.assert_allclose(np.concatenate(s), g['yolo_1080_b4_scores'], rtol=1e-6, atol=1e-4)
 
 
+@pytest.fixture(scope='module')
+def c3():
+    return np.load(os.path.join(GOLDEN, 'c3.npz'))
+
+
+@pytest.mark.parametrize('precision', ['x3', 'fp32'])
+def test_config3_det_batch32(c3, precision):
+    """BASELINE config 3's det-batch: YOLOv3 on 32 720p frames in ONE call (the bench's tile /
+    grid / split-K choices for B = 32) -> device box post-processing -> FaceNet on the device
+    crops, against the reference modules (tests/golden/make_golden.py gen_c3): counts exact,
+    boxes 1e-2 px, scores 1e-4; crop rectangles exact on every frame the golden does not flag
+    (a coordinate within 2e-3 px of an integer or a score within 1e-4 of min_score); FaceNet on
+    the golden rectangles fp32 within 1e-4, bf16 (the config's encoder precision) cos >= 0.999."""
+    import json
+    from videotofaces import synth, _native as nat
+    from videotofaces.detectors.yolo import YOLOv3
+    from videotofaces.encoders.facenet import InceptionResnetV1
+    c = json.loads(str(c3['params_json']))
+    frames = torch.from_numpy(synth.make_frames(c['frames'], seed=c['seed'])).cuda()
+    det = YOLOv3('cuda:0', precision=precision)
+    b, s, _ = det(frames)
+    np.testing.assert_array_equal([len(t) for t in s], c3['counts'])
+    np.testing.assert_allclose(np.concatenate(b), c3['boxes'], rtol=1e-6, atol=1e-2)
+    np.testing.assert_allclose(np.concatenate(s), c3['scores'], rtol=1e-6, atol=1e-4)
+    d, _ = det.detect_crops(frames, nat.BoxParams.make(c['mscore'], c['msize'], c['mborder'], tuple(c['scale']),
+                                                        c['square']))
+    got, ref = d.cpu().numpy(), c3['rects']
+    flagged = set(c3['flagged_frames'].tolist())
+    for f in range(c['frames']):
+        if f not in flagged:
+            np.testing.assert_array_equal(got[got[:, 0] == f], ref[ref[:, 0] == f], err_msg='frame %d' % f)
+    rects = torch.from_numpy(ref).cuda()
+    emb = InceptionResnetV1('cuda:0', precision='fp32').encode_crops(frames, rects).cpu().numpy()
+    np.testing.assert_allclose(emb, c3['emb'], rtol=0, atol=1e-4)
+    bf = InceptionResnetV1('cuda:0', precision='bf16').encode_crops(frames, rects).cpu().numpy()
+    cos = (bf * c3['emb']).sum(1) / np.linalg.norm(bf, axis=1)
+    print('c3: %d detections, %d crops, flagged frames %s; FaceNet bf16 cos min %.6f'
+          % (len(np.concatenate(s)), len(ref), sorted(flagged), cos.min()))
+    assert cos.min() > 0.999
+
+
 def test_facenet_fp32_batch128(g):
     from videotofaces.encoders.facenet import InceptionResnetV1
     x = (torch.from_numpy(_u8(103, (128, 3, 160, 160))).float() - 127.5) * (1 / 128)
