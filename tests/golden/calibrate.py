@@ -74,7 +74,7 @@ def _face_head(h, large, frac, gate):
     return W, np.array([-0.5 * b, 0.5 * b], np.float32)
 
 
-def main(n_frames=2, n_cal=8, large=45.0, frac2=0.06, frac3=0.3):
+def main(n_frames=2, n_cal=8, large=45.0, frac2=0.06, frac3=0.5):
     """PNet: the face-logit bias lets ~0.2% of level-0 cells pass the 0.6 gate (MTCNN_CALIB).
     RNet / ONet: random heads pass boxes regardless of content, and with min_face_size 5 almost
     every stage-1 box is a 5-10 px level-0 window, so the detector would report 5 px "faces"
