@@ -47,14 +47,15 @@ __device__ inline int4 sat_box(const int4* __restrict__ s, int W1, int y0, int y
 }
 
 // bin average from an exact integer bin sum: s / kh / kw with the reference's roundings
-// constant-address-space views of the weight structs (scalar loads, see common.hpp)
-#define CW const VTF_CONST float*
-struct PNetWC { CW c1w; CW c1b; CW p1; CW c2w; CW c2b; CW p2; CW c3w; CW c3b; CW p3; CW c41w; CW c41b; CW c42w; CW c42b; };
-#undef CW
-__device__ inline PNetWC to_const(const PNetW& w) {
-    return {cptr(w.c1w), cptr(w.c1b), cptr(w.p1), cptr(w.c2w), cptr(w.c2b), cptr(w.p2), cptr(w.c3w), cptr(w.c3b),
-            cptr(w.p3), cptr(w.c41w), cptr(w.c41b), cptr(w.c42w), cptr(w.c42b)};
-}
+// PNet weight layout (mtcnn_runtime.hip build_weights checks it): the fp32 tensors are packed
+// from PNetW::c1w in state_dict order, each padded to 4 floats; the fp16 split planes from
+// PNetW::c3h (conv3, conv2, conv1, heads).  k_pnet addresses everything from the two bases
+// with constant offsets: 2 pointers instead of 17 live across the persistent loop (the kernel
+// was spilling SGPRs into VGPR lanes).
+constexpr int PW_C1W = 0, PW_C1B = 272, PW_P1 = 284, PW_C2W = 296, PW_C2B = 1736, PW_P2 = 1752, PW_C3W = 1768,
+              PW_C3B = 6376, PW_P3 = 6408, PW_C41W = 6440, PW_C41B = 6504, PW_C42W = 6508, PW_C42B = 6636,
+              PW_F32 = 6640;
+constexpr int PH_C2H = 9216, PH_C1H = 12288, PH_HH = 14336;  // halves (conv3 planes at 0)
 
 // ----------------------------------------------------------------------------------- resample
 
@@ -349,15 +350,16 @@ __global__ __launch_bounds__(256, PnLds<X>::GPC) void k_pnet(const uint8_t* __re
                                                  int64_t total_tiles, uint32_t* __restrict__ tile_ctr, PNetW wg,
                                                  PNetOut o, int64_t tile_base, int max_chunks, int chunk) {
     using LP = PnLds<X>;
-    const auto wc = to_const(wg);
-    // conv2 / conv3 weights through buffer loads: one lane VGPR offset + constant SGPR offsets,
+    const VTF_CONST float* wf = cptr(wg.c1w);  // fp32 weights (scalar loads at constant offsets)
+    // conv / head weights through buffer loads: one lane VGPR offset + constant SGPR offsets,
     // instead of a 64-bit address per k-step (which the compiler would keep live across tiles);
-    // (k rows 90, 91 of conv2 are zeroed explicitly: soffset is outside the range check)
-    const __amdgpu_buffer_rsrc_t rw2 = __builtin_amdgcn_make_buffer_rsrc((void*)wg.c2w, 0, 90 * 16 * 4, 0x00020000);
-    const __amdgpu_buffer_rsrc_t rw3 = __builtin_amdgcn_make_buffer_rsrc((void*)wg.c3w, 0, 144 * 32 * 4, 0x00020000);
-    const __amdgpu_buffer_rsrc_t rw2h = __builtin_amdgcn_make_buffer_rsrc((void*)wg.c2h, 0, 2 * 16 * 96 * 2, 0x00020000);
-    const __amdgpu_buffer_rsrc_t rw1h = __builtin_amdgcn_make_buffer_rsrc((void*)wg.c1h, 0, 2 * 16 * 64 * 2, 0x00020000);
-    const __amdgpu_buffer_rsrc_t rhh = __builtin_amdgcn_make_buffer_rsrc((void*)wg.hh, 0, 2 * 16 * 32 * 2, 0x00020000);
+    // (k rows 90, 91 of conv2 are zeroed explicitly)
+    // (descriptors per tensor, built from the two bases: small constant soffsets stay immediates)
+    const __amdgpu_buffer_rsrc_t rw2 = __builtin_amdgcn_make_buffer_rsrc((void*)(wg.c1w + PW_C2W), 0, 90 * 16 * 4, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rw3 = __builtin_amdgcn_make_buffer_rsrc((void*)(wg.c1w + PW_C3W), 0, 144 * 32 * 4, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rw2h = __builtin_amdgcn_make_buffer_rsrc((void*)(wg.c3h + PH_C2H), 0, 2 * 16 * 96 * 2, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rw1h = __builtin_amdgcn_make_buffer_rsrc((void*)(wg.c3h + PH_C1H), 0, 2 * 16 * 64 * 2, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rhh = __builtin_amdgcn_make_buffer_rsrc((void*)(wg.c3h + PH_HH), 0, 2 * 16 * 32 * 2, 0x00020000);
     // conv3 on fp16 matrix cores (mtcnn_runtime: range bound); the X variant is launched only then
     const bool split3 = X || wg.c3h != nullptr;
     __shared__ __attribute__((aligned(16))) float sA[LP::A];     // level tile, later conv2 output
@@ -384,7 +386,7 @@ __global__ __launch_bounds__(256, PnLds<X>::GPC) void k_pnet(const uint8_t* __re
     const int lr = lane & 15, lk = lane >> 4;
 
     // ---- weights and im2col offsets, loaded once per persistent workgroup
-    const float b2 = wc.c2b[lr], a2 = wc.p2[lr];
+    const float b2 = wf[PW_C2B + lr], a2 = wf[PW_P2 + lr];
     // ---- tiles come from an atomic counter (dynamic: pyramid tiles differ in cost); the next
     //      index is requested as soon as the current one is known, so the atomic's round trip
     //      overlaps the tile's work instead of opening it
@@ -640,7 +642,7 @@ __global__ __launch_bounds__(256, PnLds<X>::GPC) void k_pnet(const uint8_t* __re
                 w0[s2] = __builtin_bit_cast(f16x8, __builtin_amdgcn_raw_buffer_load_b128(rw1h, woff, 64 * s2, 0));
                 w1[s2] = __builtin_bit_cast(f16x8, __builtin_amdgcn_raw_buffer_load_b128(rw1h, woff, 16 * 64 * 2 + 64 * s2, 0));
             }
-            const float b1 = lrx < 10 ? wc.c1b[lrx] : 0.f, a1 = lrx < 10 ? wc.p1[lrx] : 0.f;
+            const float b1 = lrx < 10 ? wf[PW_C1B + lrx] : 0.f, a1 = lrx < 10 ? wf[PW_P1 + lrx] : 0.f;
             const int corner = lrx & 3, dy = corner >> 1, dx = corner & 1;
             // the tile's conv1 window lies inside the level: no per-corner bounds checks
             const bool interior = 2 * (oy0 + PP_H - 1) + 1 < L1h && 2 * (ox0 + PP_W - 1) + 1 < L1w;
@@ -804,13 +806,13 @@ __global__ __launch_bounds__(256, PnLds<X>::GPC) void k_pnet(const uint8_t* __re
                         for (int ky = 0; ky < 3; ky++)
 #pragma unroll
                             for (int kx = 0; kx < 3; kx++) {
-                                const float w = wc.c1w[co * 27 + (c * 3 + ky) * 3 + kx];  // [co][ci][ky][kx]
+                                const float w = wf[PW_C1W + co * 27 + (c * 3 + ky) * 3 + kx];  // [co][ci][ky][kx]
                                 acc[0] = fmaf(x[c][ky][kx], w, acc[0]);
                                 acc[1] = fmaf(x[c][ky][kx + 1], w, acc[1]);
                                 acc[2] = fmaf(x[c][ky + 1][kx], w, acc[2]);
                                 acc[3] = fmaf(x[c][ky + 1][kx + 1], w, acc[3]);
                             }
-                    const float bb = wc.c1b[co], aa = wc.p1[co];
+                    const float bb = wf[PW_C1B + co], aa = wf[PW_P1 + co];
                     float out;
                     if (interior && aa >= 0.f) {
                         // PReLU with a non-negative slope is monotone, so max(prelu(v)) ==
@@ -873,8 +875,8 @@ __global__ __launch_bounds__(256, PnLds<X>::GPC) void k_pnet(const uint8_t* __re
                 float bb[4], aa[4];
 #pragma unroll
                 for (int i = 0; i < 4; i++) {
-                    bb[i] = wc.c2b[4 * lkx + i];
-                    aa[i] = wc.p2[4 * lkx + i];
+                    bb[i] = wf[PW_C2B + 4 * lkx + i];
+                    aa[i] = wf[PW_P2 + 4 * lkx + i];
                 }
                 _Float16* sO = (_Float16*)sA;
                 for (int f0 = wave; f0 < NF; f0 += 8) {
@@ -1042,11 +1044,11 @@ __global__ __launch_bounds__(256, PnLds<X>::GPC) void k_pnet(const uint8_t* __re
 #pragma unroll
                 for (int i = 0; i < 4; i++) {
                     const int ch = 16 * mf + 4 * lkx + i;
-                    cb3[mf][i] = wc.c3b[ch];
-                    ca3[mf][i] = wc.p3[ch];
+                    cb3[mf][i] = wf[PW_C3B + ch];
+                    ca3[mf][i] = wf[PW_P3 + ch];
                     // heads as the A operand: row = head lrx (0,1 conv4_1; 2..5 conv4_2), k-slot = ch
                     const int hrow = lrx < 2 ? lrx * 32 + ch : (lrx < 6 ? (lrx - 2) * 32 + ch : 0);
-                    const float hv = lrx < 2 ? wc.c41w[hrow] : wc.c42w[hrow];
+                    const float hv = lrx < 2 ? wf[PW_C41W + hrow] : wf[PW_C42W + hrow];
                     hwA[mf][i] = !X && lrx < 6 ? hv : 0.f;
                 }
             const bool splith = X || wg.hh != nullptr;  // (X: launched only with the split heads)
@@ -1097,8 +1099,8 @@ __global__ __launch_bounds__(256, PnLds<X>::GPC) void k_pnet(const uint8_t* __re
                 }
                 pf_n = pf_rows ? nb2 : 0;
             }
-            const float hb0 = wc.c41b[0], hb1 = wc.c41b[1], hb2 = wc.c42b[0], hb3 = wc.c42b[1];
-            const float hb4 = wc.c42b[2], hb5 = wc.c42b[3];
+            const float hb0 = wf[PW_C41B], hb1 = wf[PW_C41B + 1], hb2 = wf[PW_C42B], hb3 = wf[PW_C42B + 1];
+            const float hb4 = wf[PW_C42B + 2], hb5 = wf[PW_C42B + 3];
 #pragma unroll 1
             for (int hh = 0; hh < NHALF; hh++) {
                 f32x4 acc[FH][2];

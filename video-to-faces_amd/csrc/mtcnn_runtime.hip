@@ -428,6 +428,32 @@ static void build_weights(Mtcnn& m, const float* params, int64_t n_params) {
             }
         }
     }
+    // k_pnet addresses the PNet weights from two bases with constant offsets (mtcnn_kernels.hip
+    // PW_* / PH_*): the fp32 tensors are the first 13 of the packed buffer; the fp16 split
+    // planes are gathered into one buffer [conv3 | conv2 | conv1 | heads] (zeros where a plane is
+    // absent; the kernel only reads a plane when its path is enabled)
+    {
+        const int64_t want[13] = {0, 272, 284, 296, 1736, 1752, 1768, 6376, 6408, 6440, 6504, 6508, 6636};
+        for (int i = 0; i < 13; i++)
+            VTF_CHECK(off[i] == want[i], VTF_E_LIMIT, "mtcnn: PNet weight layout differs from k_pnet's offsets");
+        if (m.pw.c3h) {
+            VTF_CHECK(m.pw.c2h && m.pw.c1h, VTF_E_LIMIT, "mtcnn: split conv3 without split conv1/conv2 planes");
+            uint16_t* comb = nullptr;
+            VTF_HIP(hipMalloc((void**)&comb, 15360 * 2));
+            VTF_HIP(hipMemset(comb, 0, 15360 * 2));
+            VTF_HIP(hipMemcpy(comb, m.pw.c3h, 9216 * 2, hipMemcpyDeviceToDevice));
+            VTF_HIP(hipMemcpy(comb + 9216, m.pw.c2h, 3072 * 2, hipMemcpyDeviceToDevice));
+            VTF_HIP(hipMemcpy(comb + 12288, m.pw.c1h, 2048 * 2, hipMemcpyDeviceToDevice));
+            if (m.pw.hh) VTF_HIP(hipMemcpy(comb + 14336, m.pw.hh, 1024 * 2, hipMemcpyDeviceToDevice));
+            m.allocs.push_back((void*)comb);
+            m.pw.c3h = comb;
+            m.pw.c2h = comb + 9216;
+            m.pw.c1h = comb + 12288;
+            if (m.pw.hh) m.pw.hh = comb + 14336;
+        } else {
+            m.pw.hh = nullptr;  // the split heads read the conv3 split path's accumulators
+        }
+    }
     auto dev = [&](int i) { return m.d_w + off[i]; };
     m.rh1w = dev(25); m.rh1b = dev(26); m.rh2w = dev(27); m.rh2b = dev(28);
     m.oh1w = dev(44); m.oh1b = dev(45); m.oh2w = dev(46); m.oh2b = dev(47); m.oh3w = dev(48); m.oh3b = dev(49);
