@@ -263,6 +263,16 @@ __device__ inline void split_f16(float v, _Float16& x0, _Float16& x1) {
     x1 = (_Float16)((v - (float)x0) * 2048.f);
 }
 
+// the same split from u = 2048 v (the epilogues carry their values 2048-scaled, which is exact:
+// 2048 round(c + d 2^-11) = round(2048 c + d) is one fma, and bias / PReLU commute with the
+// scaling): x0 = fp16(u 2^-11) = fp16(v), x1 = fp16(u - 2048 x0) = fp16(2048 (v - x0)) -- one
+// v_fma_mix each (f16 widening and the final rounding are part of the instruction).  (A zero v
+// may give +0 where split_f16 gives -0: the products it feeds are zero either way.)
+__device__ inline void split_u(float u, _Float16& x0, _Float16& x1) {
+    x0 = (_Float16)fmaf(u, 0.00048828125f, 0.f);
+    x1 = (_Float16)fmaf((float)x0, -2048.f, u);
+}
+
 // 8 halves from an 8-byte aligned LDS address as two ds_read_b64 (2 LDS cycles each, 32-lane
 // bank groups over 64 banks).  The accesses are volatile so they are not merged into one
 // ds_read2_b64, which costs 8 cycles (half the bandwidth) and banks over 32 dwords per 16 lanes.
@@ -642,7 +652,8 @@ __global__ __launch_bounds__(256, PnLds<X>::GPC) void k_pnet(const uint8_t* __re
                 w0[s2] = __builtin_bit_cast(f16x8, __builtin_amdgcn_raw_buffer_load_b128(rw1h, woff, 64 * s2, 0));
                 w1[s2] = __builtin_bit_cast(f16x8, __builtin_amdgcn_raw_buffer_load_b128(rw1h, woff, 16 * 64 * 2 + 64 * s2, 0));
             }
-            const float b1 = lrx < 10 ? wf[PW_C1B + lrx] : 0.f, a1 = lrx < 10 ? wf[PW_P1 + lrx] : 0.f;
+            // bias 2048-scaled (exact): the epilogue works on u = 2048 v (split_u)
+            const float b1s = lrx < 10 ? wf[PW_C1B + lrx] * 2048.f : 0.f, a1 = lrx < 10 ? wf[PW_P1 + lrx] : 0.f;
             const int corner = lrx & 3, dy = corner >> 1, dx = corner & 1;
             // the tile's conv1 window lies inside the level: no per-corner bounds checks
             const bool interior = 2 * (oy0 + PP_H - 1) + 1 < L1h && 2 * (ox0 + PP_W - 1) + 1 < L1w;
@@ -668,8 +679,11 @@ __global__ __launch_bounds__(256, PnLds<X>::GPC) void k_pnet(const uint8_t* __re
             // fragments fit the same registers (more independent MFMA chains per wave); whole
             // iterations first, then the remaining fragments one per wave (NU = 1) instead of an
             // iteration padded with clamped (recomputed) fragments
-            auto conv1_frags = [&](auto exact_t, auto nu_t, int f0) -> int {
+            // FP: fastpool && unit_slope, a compile-time branch (uniform flags tested per fragment
+            // cost a branch each in the unrolled epilogue)
+            auto conv1_frags = [&](auto exact_t, auto fp_t, auto nu_t, int f0) -> int {
             constexpr bool EX = decltype(exact_t)::value;
+            constexpr bool FP = decltype(fp_t)::value;
             constexpr int NU = decltype(nu_t)::value;
             for (; f0 + 4 * (NU - 1) < NF1; f0 += 4 * NU) {
                 int ab[NU];
@@ -705,14 +719,11 @@ __global__ __launch_bounds__(256, PnLds<X>::GPC) void k_pnet(const uint8_t* __re
                             cm[u] = __builtin_amdgcn_mfma_f32_16x16x32_f16(xa[s2][u], w0[s2], cm[u], 0, 0, 0);
                             cd[u] = __builtin_amdgcn_mfma_f32_16x16x32_f16(xa[s2][u], w1[s2], cd[u], 0, 0, 0);
                         }
-                    typedef __attribute__((ext_vector_type(2))) float f32x2;
-                    const f32x2 k11 = {0.00048828125f, 0.00048828125f};
+                    // combined 2048-scaled: fma(c, 2048, d) = 2048 round(c + d 2^-11)
 #pragma unroll
-                    for (int u = 0; u < NU; u++) {
-                        const f32x2 lo = __builtin_elementwise_fma(f32x2{cd[u][0], cd[u][1]}, k11, f32x2{cm[u][0], cm[u][1]});
-                        const f32x2 hi = __builtin_elementwise_fma(f32x2{cd[u][2], cd[u][3]}, k11, f32x2{cm[u][2], cm[u][3]});
-                        cm[u] = f32x4{lo[0], lo[1], hi[0], hi[1]};
-                    }
+                    for (int u = 0; u < NU; u++)
+#pragma unroll
+                        for (int i = 0; i < 4; i++) cm[u][i] = fmaf(cm[u][i], 2048.f, cd[u][i]);
                 } else {
                     // cross terms first, scaled by 2^-11 (exact) into the main chain's accumulator:
                     // one accumulator per fragment, no combine step
@@ -737,10 +748,16 @@ __global__ __launch_bounds__(256, PnLds<X>::GPC) void k_pnet(const uint8_t* __re
                     const int f = f0 + 4 * u;
                     if (f >= NF1) break;
                     const f32x4 cc = cm[u];
+                    // 2048-scaled values (EX: cm already scaled; else the bias add scales it, one
+                    // rounding as before: fma(c, 2048, 2048 b) = 2048 round(c + b))
+                    constexpr float SC = EX ? 1.f : 2048.f;
                     float out;
-                    if (fastpool) {
-                        const float v = fmaxf(fmaxf(cc[0], cc[1]), fmaxf(cc[2], cc[3])) + b1;
-                        out = unit_slope ? fmaxf(v, a1 * v) : prelu(v, a1);
+                    if (FP) {
+                        const float v = fmaf(fmaxf(fmaxf(cc[0], cc[1]), fmaxf(cc[2], cc[3])), SC, b1s);
+                        out = fmaxf(v, a1 * v);
+                    } else if (fastpool) {
+                        const float v = fmaf(fmaxf(fmaxf(cc[0], cc[1]), fmaxf(cc[2], cc[3])), SC, b1s);
+                        out = prelu(v, a1);
                     } else {
                         const int pp = f * 4 + lkx;
                         const int py = pp / PP_W, px = pp % PP_W;
@@ -750,7 +767,7 @@ __global__ __launch_bounds__(256, PnLds<X>::GPC) void k_pnet(const uint8_t* __re
 #pragma unroll
                         for (int i = 0; i < 4; i++) {
                             const bool ok = (gy + (i >> 1) < L1h) && (gx + (i & 1) < L1w);
-                            const float v = prelu(cc[i] + b1, a1);
+                            const float v = prelu(fmaf(cc[i], SC, b1s), a1);
                             if (ok) {
                                 m = fmaxf(m, v);
                                 any = true;
@@ -759,7 +776,7 @@ __global__ __launch_bounds__(256, PnLds<X>::GPC) void k_pnet(const uint8_t* __re
                         out = any ? m : 0.f;  // outside the valid pooled map: keep finite
                     }
                     _Float16 x0, x1;
-                    split_f16(out, x0, x1);
+                    split_u(out, x0, x1);
                     _Float16* q = sQ + f * 4 * PQ_C + qlane;
                     q[0] = x0;
                     q[NPP * PQ_C] = x1;
@@ -767,12 +784,22 @@ __global__ __launch_bounds__(256, PnLds<X>::GPC) void k_pnet(const uint8_t* __re
             }
             return f0;
             };
-            if (exact)
-                conv1_frags(std::true_type{}, std::integral_constant<int, 1>{},
-                            conv1_frags(std::true_type{}, std::integral_constant<int, 4>{}, wv));
-            else
-                conv1_frags(std::false_type{}, std::integral_constant<int, 1>{},
-                            conv1_frags(std::false_type{}, std::integral_constant<int, 2>{}, wv));
+            using I1 = std::integral_constant<int, 1>;
+            using T = std::true_type;
+            using F = std::false_type;
+            if (exact) {
+                using I4 = std::integral_constant<int, 4>;
+                if (fastpool && unit_slope)
+                    conv1_frags(T{}, T{}, I1{}, conv1_frags(T{}, T{}, I4{}, wv));
+                else
+                    conv1_frags(T{}, F{}, I1{}, conv1_frags(T{}, F{}, I4{}, wv));
+            } else {
+                using I2 = std::integral_constant<int, 2>;
+                if (fastpool && unit_slope)
+                    conv1_frags(F{}, T{}, I1{}, conv1_frags(F{}, T{}, I2{}, wv));
+                else
+                    conv1_frags(F{}, F{}, I1{}, conv1_frags(F{}, F{}, I2{}, wv));
+            }
         }
         {
             constexpr int NPP = PP_H * PP_W;        // pooled cells
@@ -782,7 +809,9 @@ __global__ __launch_bounds__(256, PnLds<X>::GPC) void k_pnet(const uint8_t* __re
             // the tile's conv1 window lies inside the level: no per-corner bounds checks
             const bool interior = 2 * (oy0 + PP_H - 1) + 1 < L1h && 2 * (ox0 + PP_W - 1) + 1 < L1w;
             const int wv = __builtin_amdgcn_readfirstlane(wave);
-            for (int wt = wv; wt < ((o.dbg & 2) || split3 ? 0 : NWT); wt += 4) {
+            // (guarded, not only bounded: the compiler cannot prove wv >= 0, so a zero bound alone
+            //  keeps the fallback's code -- and its register demand -- in the exact variant)
+            for (int wt = wv; !X && wt < ((o.dbg & 2) || split3 ? 0 : NWT); wt += 4) {
                 const int g = wt / NCH, chunk = wt - g * NCH;
                 const bool live = chunk * 64 + lane < NPP;
                 const int pp = min(chunk * 64 + lane, NPP - 1);
@@ -872,10 +901,10 @@ __global__ __launch_bounds__(256, PnLds<X>::GPC) void k_pnet(const uint8_t* __re
 #pragma unroll
                 for (int jj = 0; jj < 4; jj++)
                     o2[jj] = lkx == 0 ? tapoff(8) + 2 * jj : lkx == 3 ? tapoff(8) + 8 : tapoff(4 * (lkx - 1) + jj) + 8;
-                float bb[4], aa[4];
+                float bb[4], aa[4];  // bias 2048-scaled (split_u)
 #pragma unroll
                 for (int i = 0; i < 4; i++) {
-                    bb[i] = wf[PW_C2B + 4 * lkx + i];
+                    bb[i] = wf[PW_C2B + 4 * lkx + i] * 2048.f;
                     aa[i] = wf[PW_P2 + 4 * lkx + i];
                 }
                 _Float16* sO = (_Float16*)sA;
@@ -927,11 +956,11 @@ __global__ __launch_bounds__(256, PnLds<X>::GPC) void k_pnet(const uint8_t* __re
                             f16x4 v0, v1;
 #pragma unroll
                             for (int i = 0; i < 4; i++) {
-                                const float acc2 = h ? c1[i] + d1[i] * 0.00048828125f : c0[i] + d0[i] * 0.00048828125f;
-                                const float v = prelu(acc2 + bb[i], aa[i]);
-                                const _Float16 x0 = (_Float16)v;
+                                const float u = h ? fmaf(c1[i], 2048.f, d1[i]) : fmaf(c0[i], 2048.f, d0[i]);
+                                _Float16 x0, x1;
+                                split_u(prelu(u + bb[i], aa[i]), x0, x1);
                                 v0[i] = x0;
-                                v1[i] = (_Float16)((v - (float)x0) * 2048.f);
+                                v1[i] = x1;
                             }
                             *(f16x4*)(sO + q * 16 + 4 * lkx) = v0;
                             *(f16x4*)(sO + NPOS * 16 + q * 16 + 4 * lkx) = v1;
@@ -939,13 +968,18 @@ __global__ __launch_bounds__(256, PnLds<X>::GPC) void k_pnet(const uint8_t* __re
                     }
                 }
             }
-            float w2[23];  // per tile (L1-resident): keeps the persistent register set small
-            const int w2off = (16 * lkx + lrx) * 4;
+            // fp32 fallback (conv2 on fp32 MFMA): weights per tile (L1-resident), keeping the
+            // persistent register set small; issued only when this path runs
+            const bool fp32_conv2 = !X && !split3 && !(o.dbg & 4);
+            float w2[23] = {};
+            if (fp32_conv2) {
+                const int w2off = (16 * lkx + lrx) * 4;
 #pragma unroll
-            for (int s = 0; s < 23; s++)
-                w2[s] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rw2, w2off, 256 * s, 0));
-            if (lkx >= 2) w2[22] = 0.f;  // k = 90, 91: zero padding
-            for (int f0 = wave; f0 < ((o.dbg & 4) || split3 ? 0 : NF); f0 += 8) {
+                for (int s = 0; s < 23; s++)
+                    w2[s] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rw2, w2off, 256 * s, 0));
+                if (lkx >= 2) w2[22] = 0.f;  // k = 90, 91: zero padding
+            }
+            for (int f0 = wave; fp32_conv2 && f0 < NF; f0 += 8) {
                 const int f1 = f0 + 4;
                 const bool two = f1 < NF;
                 int p0 = min(f0 * 16 + lrx, NPOS - 1), p1 = min((two ? f1 : f0) * 16 + lrx, NPOS - 1);
@@ -1044,7 +1078,7 @@ __global__ __launch_bounds__(256, PnLds<X>::GPC) void k_pnet(const uint8_t* __re
 #pragma unroll
                 for (int i = 0; i < 4; i++) {
                     const int ch = 16 * mf + 4 * lkx + i;
-                    cb3[mf][i] = wf[PW_C3B + ch];
+                    cb3[mf][i] = wf[PW_C3B + ch] * 2048.f;  // 2048-scaled, as the accumulators
                     ca3[mf][i] = wf[PW_P3 + ch];
                     // heads as the A operand: row = head lrx (0,1 conv4_1; 2..5 conv4_2), k-slot = ch
                     const int hrow = lrx < 2 ? lrx * 32 + ch : (lrx < 6 ? (lrx - 2) * 32 + ch : 0);
@@ -1155,7 +1189,7 @@ __global__ __launch_bounds__(256, PnLds<X>::GPC) void k_pnet(const uint8_t* __re
     #pragma unroll
                         for (int mf = 0; mf < 2; mf++)
     #pragma unroll
-                            for (int i = 0; i < 4; i++) acc[j][mf][i] = acc[j][mf][i] + accc[j][mf][i] * 0.00048828125f;
+                            for (int i = 0; i < 4; i++) acc[j][mf][i] = fmaf(acc[j][mf][i], 2048.f, accc[j][mf][i]);
                 }
                 // k-step s = (tap s/4, channel 4*(s%4) + lkx): the LDS offset is the lane-group base
                 // lkx * plane plus a compile-time constant (an instruction immediate, no registers)
@@ -1184,6 +1218,10 @@ __global__ __launch_bounds__(256, PnLds<X>::GPC) void k_pnet(const uint8_t* __re
                         }
                     }
                 }
+                if (nchunk > 0) {  // fp32 path: accumulators to the 2048-scaled form (exact)
+    #pragma unroll
+                    for (int j = 0; j < FH; j++) acc[j][0] *= 2048.f, acc[j][1] *= 2048.f;
+                }
     #pragma unroll
                 for (int j = 0; j < ((o.dbg & 32) ? 0 : FH); j++) {
                     const int cell = (wave * FPW + hh * FH + j) * 16 + lrx;
@@ -1195,10 +1233,10 @@ __global__ __launch_bounds__(256, PnLds<X>::GPC) void k_pnet(const uint8_t* __re
     #pragma unroll
                         for (int i = 0; i < 4; i++) {
                             _Float16 p0, p1;
-                            split_f16(prelu(acc[j][0][i] + cb3[0][i], ca3[0][i]), p0, p1);
+                            split_u(prelu(acc[j][0][i] + cb3[0][i], ca3[0][i]), p0, p1);
                             x0[i] = p0;
                             x1[i] = p1;
-                            split_f16(prelu(acc[j][1][i] + cb3[1][i], ca3[1][i]), p0, p1);
+                            split_u(prelu(acc[j][1][i] + cb3[1][i], ca3[1][i]), p0, p1);
                             x0[4 + i] = p0;
                             x1[4 + i] = p1;
                         }
@@ -1209,8 +1247,8 @@ __global__ __launch_bounds__(256, PnLds<X>::GPC) void k_pnet(const uint8_t* __re
                     } else {
     #pragma unroll
                         for (int i = 0; i < 4; i++) {
-                            const float fa = prelu(acc[j][0][i] + cb3[0][i], ca3[0][i]);
-                            const float fb = prelu(acc[j][1][i] + cb3[1][i], ca3[1][i]);
+                            const float fa = prelu(acc[j][0][i] + cb3[0][i], ca3[0][i]) * 0.00048828125f;
+                            const float fb = prelu(acc[j][1][i] + cb3[1][i], ca3[1][i]) * 0.00048828125f;
                             hacc = __builtin_amdgcn_mfma_f32_16x16x4f32(hwA[0][i], fa, hacc, 0, 0, 0);
                             hacc = __builtin_amdgcn_mfma_f32_16x16x4f32(hwA[1][i], fb, hacc, 0, 0, 0);
                         }
