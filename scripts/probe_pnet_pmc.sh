@@ -12,7 +12,9 @@ P2="SQ_INSTS_SALU SQ_INSTS_SMEM SQ_WAIT_INST_ANY SQ_WAIT_INST_LDS SQ_INSTS_VMEM_
 for m in $MASKS; do
     VTF_PNET_DEBUG=$m timeout -s KILL 120 rocprofv3 --pmc $P1 -d $O/p1_$m -o run --output-format csv -- python3 scripts/probe_pnet.py child > /dev/null 2>> $O/pmc.err
     VTF_PNET_DEBUG=$m timeout -s KILL 120 rocprofv3 --pmc $P2 -d $O/p2_$m -o run --output-format csv -- python3 scripts/probe_pnet.py child > /dev/null 2>> $O/pmc.err
+    VTF_PNET_DEBUG=$m timeout -s KILL 120 rocprofv3 --pmc SQ_INSTS_BRANCH SQ_WAVES -d $O/p3_$m -o run --output-format csv -- python3 scripts/probe_pnet.py child > /dev/null 2>> $O/pmc.err
 done
+KFILTER='true>' python3 scripts/probe_pnet_table.py $O $MASKS > $O/table_x.txt
 python3 scripts/probe_pnet_table.py $O $MASKS > $O/table.txt
 find $O -name '*.csv' -size +5M -delete
-cat $O/masks.txt $O/table.txt
+cat $O/masks.txt $O/table.txt $O/table_x.txt

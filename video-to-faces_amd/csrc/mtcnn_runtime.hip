@@ -695,6 +695,9 @@ static void plan_levels(int B, int H, int W, double minsize, std::vector<PNetLev
         L.tiles_y = cdiv(L.ph, PNET_TH);
         L.tiles_x = cdiv(L.pw, PNET_TW);
         L.tile_beg = tiles;
+        // k_pnet's bin math is 32-bit (udiv_est): numerators (lh + 1) H, (lw + 1) W below 2^31
+        VTF_CHECK((int64_t)(L.lh + 1) * H < ((int64_t)1 << 31) && (int64_t)(L.lw + 1) * W < ((int64_t)1 << 31),
+                  VTF_E_LIMIT, "mtcnn: pyramid level too large for PNet's 32-bit bin math");
         tiles += (int64_t)B * L.tiles_x * L.tiles_y;
         cells += (int64_t)B * L.ph * L.pw;
         lv.push_back(L);
@@ -1079,6 +1082,8 @@ int vtf_mtcnn_pnet_level(vtf_mtcnn_t h, const uint8_t* d_frames, int B, int H, i
         L.tiles_x = cdiv(L.pw, PNET_TW);
         L.tile_beg = 0;
         L.pre = nullptr;
+        VTF_CHECK((int64_t)(L.lh + 1) * H < ((int64_t)1 << 31) && (int64_t)(L.lw + 1) * W < ((int64_t)1 << 31),
+                  VTF_E_LIMIT, "mtcnn: pyramid level too large for PNet's 32-bit bin math");
         if ((int64_t)H > 2 * (int64_t)lh) {
             int4* sat = h->m.ar.get<int4>(S_SAT, (size_t)B * (H + 1) * (W + 1));
             launch_sat(d_frames, frame_stride, row_stride, B, H, W, sat, h->m.st);
