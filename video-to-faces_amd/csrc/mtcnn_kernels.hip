@@ -394,17 +394,18 @@ __global__ __launch_bounds__(256, PnLds<X>::GPC) void k_pnet(const uint8_t* __re
     int L_prev = 0;
     // phase timing (debug): thread 0 reads the shader clock after each phase's closing barrier
     const bool clk_on = o.clk != nullptr;
-    unsigned long long t_last = clk_on ? clock64() : 0;
+    __shared__ unsigned long long s_tlast;  // (in LDS: a 64-bit register live across the tile loop otherwise)
     // (the uniform flag is tested first and expected off: the common path falls through instead of
     //  taking an exec-skip branch per mark)
     auto mark = [&](int k) {
         if (__builtin_expect(clk_on, 0) && tid == 0) {
             const unsigned long long t = clock64();
-            s_clk[k] += t - t_last;
-            t_last = t;
+            s_clk[k] += t - s_tlast;
+            s_tlast = t;
         }
     };
     if (tid < 8) s_clk[tid] = 0;
+    if (tid == 0 && clk_on) s_tlast = clock64();
     const int lane = tid & 63, wave = tid >> 6;
     const int lr = lane & 15, lk = lane >> 4;
 
@@ -652,26 +653,40 @@ __global__ __launch_bounds__(256, PnLds<X>::GPC) void k_pnet(const uint8_t* __re
         //         wave-uniform in SGPRs (scalar loads), one lane per pooled cell (its 2x2 conv1
         //         window from a 3x4x4 input patch in registers), 5 channels per wave task.
         if (split3 && !(o.dbg & 2)) {
-            // conv1 on fp16 matrix cores (split level planes [2][y][x][4], split weights):
-            // K = 3 rows x 16 (kx, c) slots (12 real) in 2 steps of 32; A row r of fragment f is
-            // conv1 position (2py+dy, 2px+dx) of pooled cell 4f + r/4, corner r%4, so each lane's
-            // 4 accumulators are one pooling window (column = output channel, lane lrx)
+            // conv1 on 32x32x16 fp16 matrix cores (split level planes [2][y][x][4], split weights).
+            // A fragment is a 2 x 4 block of pooled cells (rows py0, py0 + 1; columns px0 .. +3):
+            // A row r = cell r / 4 of the block (row-major), pool corner r % 4, i.e. conv1 position
+            // (2 py + dy, 2 px + dx).  K = 3 steps (ky) of 16 slots (pixels kx 0..3 x 4 halves; kx
+            // 3 and channel 3 carry zero weights); lane half hk reads pixels 2 hk, 2 hk + 1 of its
+            // row.  N = 32 = [w0 | w1]: the main (x0 w0) and cross (x0 w1, + x1 w0 on residual
+            // levels) products of the 16 (10 real) channels side by side, so one MFMA chain per
+            // fragment covers both.  Accumulator register r of lane l is row (r & 3) + 8 (r >> 2) +
+            // 4 (l >> 5) of column l & 31: registers 4q .. 4q+3 are the 4 corners of cell 2q + (l >> 5).
+            // One permlane16_swap per register pair (q, q + 2) hands each half-row of lanes the
+            // other half's partials of the same channel: afterwards every lane holds main and cross
+            // of 2 cells (q = 0, 1 in the main lanes, q = 2, 3 in the cross lanes) and combines them
+            // 2048-scaled with one fma each (split_u) -- no padding rows, no duplicated lanes.
             constexpr int NPP = PP_H * PP_W;
-            constexpr int NF1 = NPP / 4;
-            constexpr int PLN = PL_H * PL_W * 4;  // halves per plane
-            static_assert(NPP % 4 == 0, "pool cells per fragment");
+            constexpr int FB = PP_W / 4;              // 4-cell column blocks per row pair
+            constexpr int NF1 = (PP_H / 2) * FB;      // fragments per tile
+            static_assert(PP_W % 4 == 0 && PP_H % 2 == 0, "conv1 fragments are 2 x 4 pooled cells");
+            typedef __attribute__((ext_vector_type(16))) float f32x16;
             const _Float16* sL = (const _Float16*)sA;
             _Float16* sQ = (_Float16*)sP;
-            const int woff = (lrx * 64 + 8 * lkx) * 2;
-            f16x8 w0[2], w1[2];
+            constexpr int PLN = PL_H * PL_W * 4;      // halves per plane
+            // (lane laundered per tile, as lrx / lkx: the lane-derived offsets and the weight loads
+            //  below would otherwise be hoisted out of the tile loop into long-lived registers)
+            int ln = lane;
+            asm volatile("" : "+v"(ln));
+            const int n32 = ln & 31, hk = ln >> 5;
+            // B: column n32 -> plane n32 >> 4, channel n32 & 15; k = 16 s + 8 hk .. +7
+            const int woff = ((n32 >> 4) * 16 * 64 + (n32 & 15) * 64 + 8 * hk) * 2;
+            f16x8 wb[3];
 #pragma unroll
-            for (int s2 = 0; s2 < 2; s2++) {
-                w0[s2] = __builtin_bit_cast(f16x8, __builtin_amdgcn_raw_buffer_load_b128(rw1h, woff, 64 * s2, 0));
-                w1[s2] = __builtin_bit_cast(f16x8, __builtin_amdgcn_raw_buffer_load_b128(rw1h, woff, 16 * 64 * 2 + 64 * s2, 0));
-            }
+            for (int s = 0; s < 3; s++)
+                wb[s] = __builtin_bit_cast(f16x8, __builtin_amdgcn_raw_buffer_load_b128(rw1h, woff, 32 * s, 0));
             // bias 2048-scaled (exact): the epilogue works on u = 2048 v (split_u)
             const float b1s = lrx < 10 ? wf[PW_C1B + lrx] * 2048.f : 0.f, a1 = lrx < 10 ? wf[PW_P1 + lrx] : 0.f;
-            const int corner = lrx & 3, dy = corner >> 1, dx = corner & 1;
             // the tile's conv1 window lies inside the level: no per-corner bounds checks
             const bool interior = 2 * (oy0 + PP_H - 1) + 1 < L1h && 2 * (ox0 + PP_W - 1) + 1 < L1w;
             // pool-then-activate is exact when every channel's slope is >= 0 (PReLU and rounding
@@ -682,140 +697,124 @@ __global__ __launch_bounds__(256, PnLds<X>::GPC) void k_pnet(const uint8_t* __re
             const bool fastpool = interior && mono;
             // upsampled levels (lh >= H, lw >= W: every bin 1 or 2 frame pixels per side) hold
             // s / 2^(8..10) with |s| <= 1020, exact in fp16: the residual plane is zero there, so
-            // its MFMA and its operand reads are skipped (the products it would add are all zero)
+            // its MFMAs and operand reads are skipped (the products they would add are all zero)
             const bool exact = X || (P.lh >= H && P.lw >= W);
-            // fragment f = pooled cells 4f .. 4f+3 of one pooled row (PP_W % 4 == 0): a lane's
-            // operand pixel is its per-lane offset plus a wave-uniform fragment offset
-            static_assert(PP_W % 4 == 0, "a fragment's 4 pooled cells share a row");
             const int wv = __builtin_amdgcn_readfirstlane(wave);
-            const int lpix = dy * PL_W + dx + 2 * (lrx >> 2);
-            // pooled-map slot of the lane's output: channel lrx of cell 4f + lkx (lanes 12..15 repeat
-            // channels 10, 11, which conv2 never reads)
-            const int qlane = lkx * PQ_C + (lrx < 12 ? lrx : 10 + (lrx & 1));
-            // fragments per iteration: the exact path holds one operand plane, so twice the
-            // fragments fit the same registers (more independent MFMA chains per wave); whole
-            // iterations first, then the remaining fragments one per wave (NU = 1) instead of an
-            // iteration padded with clamped (recomputed) fragments
-            // FP: fastpool && unit_slope, a compile-time branch (uniform flags tested per fragment
-            // cost a branch each in the unrolled epilogue)
-            auto conv1_frags = [&](auto exact_t, auto fp_t, auto nu_t, int f0) -> int {
-            constexpr bool EX = decltype(exact_t)::value;
-            constexpr bool FP = decltype(fp_t)::value;
-            constexpr int NU = decltype(nu_t)::value;
-            for (; f0 + 4 * (NU - 1) < NF1; f0 += 4 * NU) {
-                int ab[NU];
+            // the lane's A row: cell cq of the block, corner
+            const int r32 = ln & 31, cq = r32 >> 2, corner = r32 & 3;
+            const int lpix = (2 * (cq >> 2) + (corner >> 1)) * PL_W + 2 * (cq & 3) + (corner & 1) + 2 * hk;
+            // the cells this lane ends with: 2 q + 4 ((lane >> 4) & 1) + (lane >> 5), q = 0, 1
+            const int cbase = 4 * ((ln >> 4) & 1) + (ln >> 5);
+            // pooled-map slot of the lane's channel (lanes 12..15 repeat channels 10, 11, which
+            // conv2 never reads)
+            const int qch = lrx < 12 ? lrx : 10 + (lrx & 1);
+            // residual-level cross operand [0 | w0] (general variant only)
+            f16x8 wx[3] = {};
+            if (!exact) {
 #pragma unroll
-                for (int u = 0; u < NU; u++) {
-                    const int f = min(f0 + 4 * u, NF1 - 1);
-                    ab[u] = lpix + 2 * ((4 * f) / PP_W) * PL_W + 2 * ((4 * f) % PP_W);
-                }
-                // slots 8*(lkx&1) .. +7 of row ky = pixels x + 2*(lkx&1), +1 (4 halves each); row 3
-                // (s2 = 1, lkx >= 2) has zero weights: read row 2 instead
-                f16x8 xa[2][NU], xb[2][NU];  // level planes 0 / 1
-#pragma unroll
-                for (int s2 = 0; s2 < 2; s2++) {
-                    const int ky = min(2 * s2 + (lkx >> 1), 2);
-                    const int xo = (ky * PL_W + 2 * (lkx & 1)) * 4;
-#pragma unroll
-                    for (int u = 0; u < NU; u++) {
-                        xa[s2][u] = ld_h8(sL + ab[u] * 4 + xo);
-                        if (!EX) xb[s2][u] = ld_h8(sL + PLN + ab[u] * 4 + xo);
-                    }
-                }
-                f32x4 cm[NU];
-                if (EX) {
-                    // main and cross (x0 w1) chains independent, combined once: c + d * 2^-11 (the
-                    // scaling is exact, so the fma rounds once like the add)
-                    f32x4 cd[NU];
-#pragma unroll
-                    for (int u = 0; u < NU; u++) cm[u] = cd[u] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-                    for (int s2 = 0; s2 < 2; s2++)
-#pragma unroll
-                        for (int u = 0; u < NU; u++) {
-                            cm[u] = __builtin_amdgcn_mfma_f32_16x16x32_f16(xa[s2][u], w0[s2], cm[u], 0, 0, 0);
-                            cd[u] = __builtin_amdgcn_mfma_f32_16x16x32_f16(xa[s2][u], w1[s2], cd[u], 0, 0, 0);
-                        }
-                    // combined 2048-scaled: fma(c, 2048, d) = 2048 round(c + d 2^-11)
-#pragma unroll
-                    for (int u = 0; u < NU; u++)
-#pragma unroll
-                        for (int i = 0; i < 4; i++) cm[u][i] = fmaf(cm[u][i], 2048.f, cd[u][i]);
-                } else {
-                    // cross terms first, scaled by 2^-11 (exact) into the main chain's accumulator:
-                    // one accumulator per fragment, no combine step
-#pragma unroll
-                    for (int u = 0; u < NU; u++) {
-                        f32x4 cd = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-                        for (int s2 = 0; s2 < 2; s2++) {
-                            cd = __builtin_amdgcn_mfma_f32_16x16x32_f16(xa[s2][u], w1[s2], cd, 0, 0, 0);
-                            cd = __builtin_amdgcn_mfma_f32_16x16x32_f16(xb[s2][u], w0[s2], cd, 0, 0, 0);
-                        }
-                        cm[u] = cd * 0.00048828125f;
-                    }
-#pragma unroll
-                    for (int s2 = 0; s2 < 2; s2++)
-#pragma unroll
-                        for (int u = 0; u < NU; u++)
-                            cm[u] = __builtin_amdgcn_mfma_f32_16x16x32_f16(xa[s2][u], w0[s2], cm[u], 0, 0, 0);
-                }
-#pragma unroll
-                for (int u = 0; u < NU; u++) {
-                    const int f = f0 + 4 * u;
-                    if (f >= NF1) break;
-                    const f32x4 cc = cm[u];
-                    // 2048-scaled values (EX: cm already scaled; else the bias add scales it, one
-                    // rounding as before: fma(c, 2048, 2048 b) = 2048 round(c + b))
-                    constexpr float SC = EX ? 1.f : 2048.f;
-                    float out;
-                    if (FP) {
-                        const float v = fmaf(fmaxf(fmaxf(cc[0], cc[1]), fmaxf(cc[2], cc[3])), SC, b1s);
-                        out = fmaxf(v, a1 * v);
-                    } else if (fastpool) {
-                        const float v = fmaf(fmaxf(fmaxf(cc[0], cc[1]), fmaxf(cc[2], cc[3])), SC, b1s);
-                        out = prelu(v, a1);
-                    } else {
-                        const int pp = f * 4 + lkx;
-                        const int py = pp / PP_W, px = pp % PP_W;
-                        const int gy = 2 * (oy0 + py), gx = 2 * (ox0 + px);
-                        float m = -3.402823466e38f;
-                        bool any = false;
-#pragma unroll
-                        for (int i = 0; i < 4; i++) {
-                            const bool ok = (gy + (i >> 1) < L1h) && (gx + (i & 1) < L1w);
-                            const float v = prelu(fmaf(cc[i], SC, b1s), a1);
-                            if (ok) {
-                                m = fmaxf(m, v);
-                                any = true;
-                            }
-                        }
-                        out = any ? m : 0.f;  // outside the valid pooled map: keep finite
-                    }
-                    _Float16 x0, x1;
-                    split_u(out, x0, x1);
-                    _Float16* q = sQ + f * 4 * PQ_C + qlane;
-                    q[0] = x0;
-                    q[NPP * PQ_C] = x1;
+                for (int s = 0; s < 3; s++) {
+                    const f16x8 w = __builtin_bit_cast(
+                        f16x8, __builtin_amdgcn_raw_buffer_load_b128(rw1h, ((n32 & 15) * 64 + 8 * hk) * 2, 32 * s, 0));
+                    wx[s] = n32 >= 16 ? w : f16x8{};
                 }
             }
-            return f0;
+            // NU fragments per iteration (wave-strided: F = wv + 4 k); whole iterations first,
+            // then the remaining fragment one at a time.  FP: fastpool && unit_slope, a
+            // compile-time branch (uniform flags tested per fragment cost a branch each)
+            auto conv1_frags = [&](auto exact_t, auto fp_t, auto nu_t, int f0) -> int {
+                constexpr bool EX = decltype(exact_t)::value;
+                constexpr bool FP = decltype(fp_t)::value;
+                constexpr int NU = decltype(nu_t)::value;
+                for (; f0 + 4 * (NU - 1) < NF1; f0 += 4 * NU) {
+                    int fo[NU], py0[NU], px0[NU];
+#pragma unroll
+                    for (int u = 0; u < NU; u++) {
+                        const int f = f0 + 4 * u;
+                        const int br = f / FB;
+                        py0[u] = 2 * br;
+                        px0[u] = 4 * (f - br * FB);
+                        fo[u] = (lpix + 2 * py0[u] * PL_W + 2 * px0[u]) * 4;
+                    }
+                    f16x8 xa[3][NU], xb[3][NU];
+#pragma unroll
+                    for (int s = 0; s < 3; s++)
+#pragma unroll
+                        for (int u = 0; u < NU; u++) {
+                            xa[s][u] = ld_h8(sL + fo[u] + s * PL_W * 4);
+                            if (!EX) xb[s][u] = ld_h8(sL + PLN + fo[u] + s * PL_W * 4);
+                        }
+                    f32x16 acc[NU];
+#pragma unroll
+                    for (int u = 0; u < NU; u++) acc[u] = f32x16{};
+#pragma unroll
+                    for (int s = 0; s < 3; s++)
+#pragma unroll
+                        for (int u = 0; u < NU; u++) {
+                            acc[u] = __builtin_amdgcn_mfma_f32_32x32x16_f16(xa[s][u], wb[s], acc[u], 0, 0, 0);
+                            if (!EX) acc[u] = __builtin_amdgcn_mfma_f32_32x32x16_f16(xb[s][u], wx[s], acc[u], 0, 0, 0);
+                        }
+#pragma unroll
+                    for (int u = 0; u < NU; u++) {
+                        float uv[2][4];  // 2048-scaled combined corners of the lane's 2 cells
+#pragma unroll
+                        for (int q = 0; q < 2; q++)
+#pragma unroll
+                            for (int i = 0; i < 4; i++) {
+                                const auto sw = __builtin_amdgcn_permlane16_swap(
+                                    __float_as_uint(acc[u][4 * q + i]), __float_as_uint(acc[u][4 * (q + 2) + i]), false, false);
+                                uv[q][i] = fmaf(__uint_as_float(sw[0]), 2048.f, __uint_as_float(sw[1]));
+                            }
+#pragma unroll
+                        for (int q = 0; q < 2; q++) {
+                            const int c = 2 * q + cbase;
+                            const int py = py0[u] + (c >> 2), px = px0[u] + (c & 3);
+                            float out;
+                            if (FP) {
+                                const float v = fmaxf(fmaxf(uv[q][0], uv[q][1]), fmaxf(uv[q][2], uv[q][3])) + b1s;
+                                out = fmaxf(v, a1 * v);
+                            } else if (fastpool) {
+                                out = prelu(fmaxf(fmaxf(uv[q][0], uv[q][1]), fmaxf(uv[q][2], uv[q][3])) + b1s, a1);
+                            } else {
+                                const int gy = 2 * (oy0 + py), gx = 2 * (ox0 + px);
+                                float m = -3.402823466e38f;
+                                bool any = false;
+#pragma unroll
+                                for (int i = 0; i < 4; i++) {
+                                    const bool ok = (gy + (i >> 1) < L1h) && (gx + (i & 1) < L1w);
+                                    const float v = prelu(uv[q][i] + b1s, a1);
+                                    if (ok) {
+                                        m = fmaxf(m, v);
+                                        any = true;
+                                    }
+                                }
+                                out = any ? m : 0.f;  // outside the valid pooled map: keep finite
+                            }
+                            _Float16 x0, x1;
+                            split_u(out, x0, x1);
+                            _Float16* qp = sQ + (py * PP_W + px) * PQ_C + qch;
+                            qp[0] = x0;
+                            qp[NPP * PQ_C] = x1;
+                        }
+                    }
+                }
+                return f0;
             };
             using I1 = std::integral_constant<int, 1>;
+            using I2 = std::integral_constant<int, 2>;
             using T = std::true_type;
             using F = std::false_type;
+            // (the boundary / general-slope epilogue runs one fragment at a time: its per-corner
+            //  bounds logic would otherwise set the kernel's register peak for ~3 % of the tiles)
             if (exact) {
-                using I4 = std::integral_constant<int, 4>;
                 if (fastpool && unit_slope)
-                    conv1_frags(T{}, T{}, I1{}, conv1_frags(T{}, T{}, I4{}, wv));
+                    conv1_frags(T{}, T{}, I1{}, conv1_frags(T{}, T{}, I2{}, wv));
                 else
-                    conv1_frags(T{}, F{}, I1{}, conv1_frags(T{}, F{}, I4{}, wv));
+                    conv1_frags(T{}, F{}, I1{}, wv);
             } else {
-                using I2 = std::integral_constant<int, 2>;
                 if (fastpool && unit_slope)
                     conv1_frags(F{}, T{}, I1{}, conv1_frags(F{}, T{}, I2{}, wv));
                 else
-                    conv1_frags(F{}, F{}, I1{}, conv1_frags(F{}, F{}, I2{}, wv));
+                    conv1_frags(F{}, F{}, I1{}, wv);
             }
         }
         {
