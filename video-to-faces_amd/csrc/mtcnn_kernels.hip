@@ -322,26 +322,27 @@ __device__ inline PNetLevel load_level(const VTF_CONST PNetLevel* p) {
     return r;
 }
 
-// (row, column) of a linear byte index in a w-wide frame patch, stepped by one workgroup pass
-// (256): one division per thread instead of one per byte
-struct PatchIdx {
-    int r, q, w, dr, dq;
-    __device__ void init(int i, int w_) {
-        w = w_;
-        r = i / w;
-        q = i - r * w;
-        dr = 256 / w;
-        dq = 256 - dr * w;
-    }
-    __device__ void step() {
-        q += dq;
-        r += dr;
-        if (q >= w) {
-            q -= w;
-            r++;
+// bytes [i0, i0 + 8) of a frame patch of w-byte rows at row stride rs, read through a buffer
+// descriptor over the patch's byte extent (32-bit offsets; bytes past the extent read 0: no
+// clamping), packed little-endian into two dwords.  With w >= 8 the 8 bytes span at most one row
+// change: two bases and one select per byte (wave-uniform branch; narrower patches step per byte)
+__device__ inline uint2 patch_bytes8(__amdgpu_buffer_rsrc_t rsrc, int i0, int w, int rs) {
+    uint32_t v[2] = {0u, 0u};
+    int r = udiv_est(i0, w), q = i0 - r * w;
+    if (w >= 8) {
+        const int o0 = r * rs + q, o1 = o0 + rs - w, k = w - q;
+#pragma unroll
+        for (int j = 0; j < 8; j++)
+            v[j >> 2] |= (uint32_t)__builtin_amdgcn_raw_buffer_load_b8(rsrc, (j < k ? o0 : o1) + j, 0, 0) << (8 * (j & 3));
+    } else {
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+            v[j >> 2] |= (uint32_t)__builtin_amdgcn_raw_buffer_load_b8(rsrc, r * rs + q, 0, 0) << (8 * (j & 3));
+            if (++q == w) q = 0, r++;
         }
     }
-};
+    return make_uint2(v[0], v[1]);
+}
 
 constexpr int PNET_TILE_CHUNK = 4;  // default tiles per atomic chunk (VTF_PNET_CHUNK)
 constexpr int PNET_GROUPS_PER_CU = (160 * 1024) / ((PNET_LDS + 511) / 512 * 512);  // LDS granule: 512 B
@@ -491,22 +492,14 @@ __global__ __launch_bounds__(256, PnLds<X>::GPC) void k_pnet(const uint8_t* __re
         uint8_t* patch = (uint8_t*)sP;
         // (gathers below issue 8 loads per thread before the first use: latency-bound otherwise)
         if (staged && !(o.dbg & 64)) {
+            // 8 consecutive patch bytes per thread (one 8-byte LDS store); the first 2 KB were
+            // prefetched during the previous tile when pf_done
             const int nbytes = (fy1 - fy0) * pw3;
             const uint8_t* src = fr + (int64_t)fy0 * row_stride + fx0 * 3;
-            const int64_t last = (int64_t)(fy1 - fy0 - 1) * row_stride + pw3 - 1;
-            PatchIdx ix;
-            ix.init(tid + (pf_done ? 256 * 8 : 0), pw3);
-            for (int i0 = tid + (pf_done ? 256 * 8 : 0); i0 < nbytes; i0 += 256 * 8) {
-                uint8_t v[8];
-#pragma unroll
-                for (int j = 0; j < 8; j++) {
-                    v[j] = src[min((int64_t)ix.r * row_stride + ix.q, last)];
-                    ix.step();
-                }
-#pragma unroll
-                for (int j = 0; j < 8; j++)
-                    if (i0 + j * 256 < nbytes) patch[i0 + j * 256] = v[j];
-            }
+            const __amdgpu_buffer_rsrc_t rs_src = __builtin_amdgcn_make_buffer_rsrc(
+                (void*)src, 0, (int)((fy1 - fy0 - 1) * (int)row_stride + pw3), 0x00020000);
+            for (int i0 = 8 * tid + (pf_done ? 256 * 8 : 0); i0 < nbytes; i0 += 256 * 8)
+                *(uint2*)(patch + i0) = patch_bytes8(rs_src, i0, pw3, (int)row_stride);
         }
         __syncthreads();
         mark(2);  // 2: frame patch staging
@@ -1079,7 +1072,7 @@ __global__ __launch_bounds__(256, PnLds<X>::GPC) void k_pnet(const uint8_t* __re
         //      flight during conv3 (which reads its weights from LDS: no later global load waits
         //      on them), and stored to the patch buffer after it -- the next tile's staging
         //      latency hides behind this tile's matrix work
-        uint32_t pfv[2] = {0u, 0u};  // the prefetched bytes, packed (4 per dword)
+        uint2 pfv = make_uint2(0u, 0u);  // the prefetched bytes 8 tid .. +7, packed
         int pf_n = 0;
         {
             constexpr int FPW = PT_H * PT_W / 64;  // 16-cell fragments per wave
@@ -1140,14 +1133,9 @@ __global__ __launch_bounds__(256, PnLds<X>::GPC) void k_pnet(const uint8_t* __re
                         }
                     }
                 }
-                const int64_t last = pf_rows ? (int64_t)(nb2 / qw3 - 1) * row_stride + qw3 - 1 : 0;
-                PatchIdx ix;
-                ix.init(tid, qw3);
-#pragma unroll
-                for (int j = 0; j < 8; j++) {
-                    pfv[j >> 2] |= (uint32_t)pf_src[min((int64_t)ix.r * row_stride + ix.q, last)] << (8 * (j & 3));
-                    ix.step();
-                }
+                const int ext = pf_rows ? (nb2 / qw3 - 1) * (int)row_stride + qw3 : 1;
+                pfv = patch_bytes8(__builtin_amdgcn_make_buffer_rsrc((void*)pf_src, 0, ext, 0x00020000), 8 * tid, qw3,
+                                   (int)row_stride);
                 pf_n = pf_rows ? nb2 : 0;
             }
             const float hb0 = wf[PW_C41B], hb1 = wf[PW_C41B + 1], hb2 = wf[PW_C42B], hb3 = wf[PW_C42B + 1];
@@ -1318,12 +1306,7 @@ __global__ __launch_bounds__(256, PnLds<X>::GPC) void k_pnet(const uint8_t* __re
             }
         }
         if (X) __syncthreads();  // conv3's weights (under the patch bytes) are no longer read
-        if (pf_n > 0) {
-            uint8_t* patch2 = (uint8_t*)sP;
-#pragma unroll
-            for (int j = 0; j < 8; j++)
-                if (tid + j * 256 < pf_n) patch2[tid + j * 256] = (uint8_t)(pfv[j >> 2] >> (8 * (j & 3)));
-        }
+        if (pf_n > 0 && 8 * tid < pf_n) *(uint2*)((uint8_t*)sP + 8 * tid) = pfv;
         pf_done = pf_n > 0;
         if (tid == 0) {  // every thread read s_tile / s_cend before this tile's barriers
             s_tile = (int)next_tile;
@@ -1355,6 +1338,8 @@ void launch_pnet(bool dense, const uint8_t* frames, int64_t frame_stride, int64_
     VTF_CHECK(H < 65536 && W < 65536, VTF_E_LIMIT, "mtcnn: frames must be smaller than 65536 px per side");
     // k_pnet's index math is 32-bit (udiv_est): tile indices and bin numerators below 2^31
     VTF_CHECK(total_tiles < (int64_t)1 << 30, VTF_E_LIMIT, "mtcnn: too many PNet tiles in one launch");
+    // frame patches are read through 32-bit buffer offsets (patch_bytes8)
+    VTF_CHECK(row_stride > 0 && row_stride < (int64_t)1 << 24, VTF_E_LIMIT, "mtcnn: frame row stride too large");
     // (level sizes: checked where the level plan is built, mtcnn_runtime)
     int dev = 0, cus = 256;
     VTF_HIP(hipGetDevice(&dev));
