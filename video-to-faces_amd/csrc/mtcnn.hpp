@@ -27,6 +27,9 @@ struct PNetW {
     // k = 8g + j holds channel 4g + j (j < 4) or 16 + 4g + j - 4: exactly the conv3 accumulator
     // values lane group g owns, so the heads need no lane movement.  null -> fp32 heads
     const uint16_t* hh;
+    // PReLU slope classes (host): bit 0 every conv2 slope in [0, 1], bit 1 every conv3 slope in
+    // [0, 1] -- PReLU is then max(v, a v), two instructions instead of three
+    int unit_slopes;
 };
 struct PNetOut {
     // sparse (candidate) mode

@@ -273,6 +273,12 @@ __device__ inline void split_u(float u, _Float16& x0, _Float16& x1) {
     x1 = (_Float16)fmaf((float)x0, -2048.f, u);
 }
 
+// PReLU with the slope class known at compile time: slopes in [0, 1] (U) make it max(v, a v)
+template <bool U>
+__device__ inline float prelu_t(float v, float a) {
+    return U ? fmaxf(v, a * v) : prelu(v, a);
+}
+
 // 8 halves from an 8-byte aligned LDS address as two ds_read_b64 (2 LDS cycles each, 32-lane
 // bank groups over 64 banks).  The accesses are volatile so they are not merged into one
 // ds_read2_b64, which costs 8 cycles (half the bandwidth) and banks over 32 dwords per 16 lanes.
@@ -917,6 +923,8 @@ __global__ __launch_bounds__(256, PnLds<X>::GPC) void k_pnet(const uint8_t* __re
                     aa[i] = wf[PW_P2 + 4 * lkx + i];
                 }
                 _Float16* sO = (_Float16*)sA;
+                auto conv2_frags = [&](auto u_t) {
+                constexpr bool U2 = decltype(u_t)::value;
                 for (int f0 = wave; f0 < NF; f0 += 8) {
                     const int f1 = f0 + 4;
                     const bool two = f1 < NF;
@@ -967,7 +975,7 @@ __global__ __launch_bounds__(256, PnLds<X>::GPC) void k_pnet(const uint8_t* __re
                             for (int i = 0; i < 4; i++) {
                                 const float u = h ? fmaf(c1[i], 2048.f, d1[i]) : fmaf(c0[i], 2048.f, d0[i]);
                                 _Float16 x0, x1;
-                                split_u(prelu(u + bb[i], aa[i]), x0, x1);
+                                split_u(prelu_t<U2>(u + bb[i], aa[i]), x0, x1);
                                 v0[i] = x0;
                                 v1[i] = x1;
                             }
@@ -976,6 +984,11 @@ __global__ __launch_bounds__(256, PnLds<X>::GPC) void k_pnet(const uint8_t* __re
                         }
                     }
                 }
+                };
+                if (wg.unit_slopes & 1)
+                    conv2_frags(std::true_type{});
+                else
+                    conv2_frags(std::false_type{});
             }
             // fp32 fallback (conv2 on fp32 MFMA): weights per tile (L1-resident), keeping the
             // persistent register set small; issued only when this path runs
@@ -1138,8 +1151,10 @@ __global__ __launch_bounds__(256, PnLds<X>::GPC) void k_pnet(const uint8_t* __re
                                    (int)row_stride);
                 pf_n = pf_rows ? nb2 : 0;
             }
-            const float hb0 = wf[PW_C41B], hb1 = wf[PW_C41B + 1], hb2 = wf[PW_C42B], hb3 = wf[PW_C42B + 1];
-            const float hb4 = wf[PW_C42B + 2], hb5 = wf[PW_C42B + 3];
+            // head biases of the lane's accumulator rows 4 lkx + i (group 0: conv4_1 0, 1, conv4_2
+            // 0, 1; group 1: conv4_2 2, 3; groups 2, 3 hold no heads)
+            const f32x4 hbv = lkx == 0 ? f32x4{wf[PW_C41B], wf[PW_C41B + 1], wf[PW_C42B], wf[PW_C42B + 1]}
+                                       : f32x4{wf[PW_C42B + 2], wf[PW_C42B + 3], 0.f, 0.f};
 #pragma unroll 1
             for (int hh = 0; hh < NHALF; hh++) {
                 f32x4 acc[FH][2];
@@ -1227,53 +1242,75 @@ __global__ __launch_bounds__(256, PnLds<X>::GPC) void k_pnet(const uint8_t* __re
     #pragma unroll
                     for (int j = 0; j < FH; j++) acc[j][0] *= 2048.f, acc[j][1] *= 2048.f;
                 }
+                static_assert(FH == 2, "the heads epilogue pairs the two fragments of a pass");
+                // conv3 epilogue + both 1x1 heads per fragment, then the pair's head values
+                // regrouped so one softmax / gate per lane covers both fragments (U3: conv3's
+                // PReLU slope class)
+                auto heads = [&](auto u_t) {
+                    constexpr bool U3 = decltype(u_t)::value;
+                    f32x4 hq[FH];
     #pragma unroll
-                for (int j = 0; j < ((o.dbg & 32) ? 0 : FH); j++) {
-                    const int cell = (wave * FPW + hh * FH + j) * 16 + lrx;
-                    f32x4 hacc = {0.f, 0.f, 0.f, 0.f};
-                    if (splith) {
-                        // the lane's 8 activations are k = 8 * lkx .. +7 of one 16x16x32 step:
-                        // cross terms first, scaled by 2^-11 into the main product's accumulator
-                        f16x8 x0, x1;
+                    for (int j = 0; j < FH; j++) {
+                        f32x4 hacc = {0.f, 0.f, 0.f, 0.f};
+                        if (splith) {
+                            // the lane's 8 activations are k = 8 * lkx .. +7 of one 16x16x32 step:
+                            // cross terms first, scaled by 2^-11 into the main product's accumulator
+                            f16x8 x0, x1;
     #pragma unroll
-                        for (int i = 0; i < 4; i++) {
-                            _Float16 p0, p1;
-                            split_u(prelu(acc[j][0][i] + cb3[0][i], ca3[0][i]), p0, p1);
-                            x0[i] = p0;
-                            x1[i] = p1;
-                            split_u(prelu(acc[j][1][i] + cb3[1][i], ca3[1][i]), p0, p1);
-                            x0[4 + i] = p0;
-                            x1[4 + i] = p1;
+                            for (int i = 0; i < 4; i++) {
+                                _Float16 p0, p1;
+                                split_u(prelu_t<U3>(acc[j][0][i] + cb3[0][i], ca3[0][i]), p0, p1);
+                                x0[i] = p0;
+                                x1[i] = p1;
+                                split_u(prelu_t<U3>(acc[j][1][i] + cb3[1][i], ca3[1][i]), p0, p1);
+                                x0[4 + i] = p0;
+                                x1[4 + i] = p1;
+                            }
+                            hacc = __builtin_amdgcn_mfma_f32_16x16x32_f16(hw0, x1, hacc, 0, 0, 0);
+                            hacc = __builtin_amdgcn_mfma_f32_16x16x32_f16(hw1, x0, hacc, 0, 0, 0);
+                            hacc = hacc * 0.00048828125f;
+                            hacc = __builtin_amdgcn_mfma_f32_16x16x32_f16(hw0, x0, hacc, 0, 0, 0);
+                        } else {
+    #pragma unroll
+                            for (int i = 0; i < 4; i++) {
+                                const float fa = prelu_t<U3>(acc[j][0][i] + cb3[0][i], ca3[0][i]) * 0.00048828125f;
+                                const float fb = prelu_t<U3>(acc[j][1][i] + cb3[1][i], ca3[1][i]) * 0.00048828125f;
+                                hacc = __builtin_amdgcn_mfma_f32_16x16x4f32(hwA[0][i], fa, hacc, 0, 0, 0);
+                                hacc = __builtin_amdgcn_mfma_f32_16x16x4f32(hwA[1][i], fb, hacc, 0, 0, 0);
+                            }
                         }
-                        hacc = __builtin_amdgcn_mfma_f32_16x16x32_f16(hw0, x1, hacc, 0, 0, 0);
-                        hacc = __builtin_amdgcn_mfma_f32_16x16x32_f16(hw1, x0, hacc, 0, 0, 0);
-                        hacc = hacc * 0.00048828125f;
-                        hacc = __builtin_amdgcn_mfma_f32_16x16x32_f16(hw0, x0, hacc, 0, 0, 0);
-                    } else {
-    #pragma unroll
-                        for (int i = 0; i < 4; i++) {
-                            const float fa = prelu(acc[j][0][i] + cb3[0][i], ca3[0][i]) * 0.00048828125f;
-                            const float fb = prelu(acc[j][1][i] + cb3[1][i], ca3[1][i]) * 0.00048828125f;
-                            hacc = __builtin_amdgcn_mfma_f32_16x16x4f32(hwA[0][i], fa, hacc, 0, 0, 0);
-                            hacc = __builtin_amdgcn_mfma_f32_16x16x4f32(hwA[1][i], fb, hacc, 0, 0, 0);
-                        }
+                        // head biases added here, per lane group (group 0: a0 a1 r0 r1, group 1: r2
+                        // r3): the swap below then reads a VALU result -- the compiler's wait-state
+                        // count for v_permlane16_swap reading a 16x16x4 f32 MFMA result directly is
+                        // two short of the one it gives other VALU reads (stale values, seen on the
+                        // fp32 path)
+                        hq[j] = hacc + hbv;
                     }
-                    // hacc: lane (cell lrx, heads 4*lkx + i): group 0 = (a0, a1, r0, r1), group 1 = (r2, r3, -, -)
-                    const float r2 = __shfl_down(hacc[0], 16), r3 = __shfl_down(hacc[1], 16);
+                    // hq[j]: lane (cell lrx, heads 4 lkx + i): group 0 = (a0, a1, r0, r1), group 1 =
+                    // (r2, r3, -, -).  One permlane16_swap per register moves fragment 1's group-0
+                    // values into group 1 of hq[0] and fragment 0's group-1 values into group 0 of
+                    // hq[1]: lane groups 0 / 1 then hold fragment 0 / 1 whole, in the same registers
+    #pragma unroll
+                    for (int k = 0; k < 4; k++) {
+                        const auto sw = __builtin_amdgcn_permlane16_swap(__float_as_uint(hq[0][k]), __float_as_uint(hq[1][k]), false, false);
+                        hq[0][k] = __uint_as_float(sw[0]);
+                        hq[1][k] = __uint_as_float(sw[1]);
+                    }
+                    const int cell = (wave * FPW + hh * FH + (lkx & 1)) * 16 + lrx;
                     const int y = cell / PT_W, x = cell % PT_W;
                     const int oy = oy0 + y, ox = ox0 + x;
-                    const bool valid = (lkx == 0) && (oy < P.ph) && (ox < P.pw);
-                    const float a0 = hacc[0] + hb0, a1v = hacc[1] + hb1;
+                    const bool valid = (lkx < 2) && (oy < P.ph) && (ox < P.pw);
+                    const float a0 = hq[0][0], a1v = hq[0][1];
                     const float mx = fmaxf(a0, a1v);
                     const float e0 = expf(a0 - mx), e1 = expf(a1v - mx);
                     const float prob = __fdiv_rn(e1, e0 + e1);
-                    const float q0 = hacc[2] + hb2, q1 = hacc[3] + hb3, q2 = r2 + hb4, q3 = r3 + hb5;
+                    const float q0 = hq[0][2], q1 = hq[0][3], q2 = hq[1][0], q3 = hq[1][1];
                     if (DENSE) {
                         if (valid) {
                             int64_t plane = (int64_t)P.ph * P.pw;
-                            int64_t cell = (int64_t)oy * P.pw + ox;
-                            o.prob[(int64_t)b * plane + cell] = prob;
-                            float* rg = o.reg + (int64_t)b * 4 * plane + cell;
+                            int64_t pc = (int64_t)oy * P.pw + ox;
+                            o.prob[(int64_t)b * plane + pc] = prob;
+                            float* rg = o.reg + (int64_t)b * 4 * plane + pc;
                             rg[0] = q0;
                             rg[plane] = q1;
                             rg[2 * plane] = q2;
@@ -1302,6 +1339,12 @@ __global__ __launch_bounds__(256, PnLds<X>::GPC) void k_pnet(const uint8_t* __re
                             }
                         }
                     }
+                };
+                if (!(o.dbg & 32)) {
+                    if (wg.unit_slopes & 2)
+                        heads(std::true_type{});
+                    else
+                        heads(std::false_type{});
                 }
             }
         }

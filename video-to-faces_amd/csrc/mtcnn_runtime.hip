@@ -199,7 +199,7 @@ static void build_weights(Mtcnn& m, const float* params, int64_t n_params) {
         const float* b = m.d_w;
         int i = 0;
         auto nx = [&]() { return b + off[i++]; };
-        m.pw = PNetW{nx(), nx(), nx(), nx(), nx(), nx(), nx(), nx(), nx(), nx(), nx(), nx(), nx(), nullptr, nullptr, nullptr, nullptr};
+        m.pw = PNetW{nx(), nx(), nx(), nx(), nx(), nx(), nx(), nx(), nx(), nx(), nx(), nx(), nx(), nullptr, nullptr, nullptr, nullptr, 0};
     }
     // raw (reference layout) tensors by spec index
     std::vector<const float*> raw(NP);
@@ -427,6 +427,14 @@ static void build_weights(Mtcnn& m, const float* params, int64_t n_params) {
                 m.pw.hh = d;
             }
         }
+    }
+    {
+        auto unit = [&](int idx, int n) {
+            for (int c = 0; c < n; c++)
+                if (!(raw[idx][c] >= 0.f && raw[idx][c] <= 1.f)) return false;
+            return true;
+        };
+        m.pw.unit_slopes = (unit(5, 16) ? 1 : 0) | (unit(8, 32) ? 2 : 0);  // p2 [16], p3 [32]
     }
     // k_pnet addresses the PNet weights from two bases with constant offsets (mtcnn_kernels.hip
     // PW_* / PH_*): the fp32 tensors are the first 13 of the packed buffer; the fp16 split
