@@ -92,7 +92,7 @@ __global__ __launch_bounds__(BOX_THREADS) void k_box_post(const float* __restric
                                                           vtf_box_params p, int frame_offset,
                                                           int32_t* __restrict__ crops, int32_t* __restrict__ src,
                                                           int32_t* __restrict__ frame_counts,
-                                                          int32_t* __restrict__ total_out) {
+                                                          int32_t* __restrict__ total_out, int64_t cap) {
     __shared__ int s_beg[BOX_MAX_FRAMES + 1];
     __shared__ int s_kept[BOX_MAX_FRAMES];
     __shared__ int s_wave[BOX_WAVES + 1];
@@ -158,7 +158,7 @@ __global__ __launch_bounds__(BOX_THREADS) void k_box_post(const float* __restric
         }
         int nk = 0;
         const int pos = block_scan_excl(keep, s_wave, &nk);
-        if (keep) {
+        if (keep && base + pos < cap) {  // (past cap: counted, not written; the host reports it)
             int32_t* o = crops + (int64_t)(base + pos) * 5;
             o[0] = frame_offset + f;
             o[1] = x1;
@@ -179,10 +179,10 @@ __global__ __launch_bounds__(BOX_THREADS) void k_box_post(const float* __restric
 
 void launch_box_post(const float* d_rows, const int32_t* d_counts, int B, int H, int W, const vtf_box_params& p,
                      int frame_offset, int32_t* d_crops, int32_t* d_src, int32_t* d_frame_counts, int32_t* d_total,
-                     hipStream_t st) {
+                     hipStream_t st, int64_t cap) {
     VTF_CHECK(B > 0 && B <= BOX_MAX_FRAMES, VTF_E_LIMIT, "box post-processing: 1..4096 frames per call");
     k_box_post<<<1, BOX_THREADS, 0, st>>>(d_rows, d_counts, B, H, W, p, frame_offset, d_crops, d_src, d_frame_counts,
-                                          d_total);
+                                          d_total, cap);
     VTF_HIP(hipGetLastError());
 }
 
@@ -194,15 +194,19 @@ int64_t rows_to_crops(Arena& ar, int slot, const float* d_rows, const std::vecto
     for (int32_t c : counts) rows += std::max(0, c);
     if (out_n) *out_n = rows;
     VTF_CHECK(rows <= cap, VTF_E_CAPACITY, "crop capacity too small (bound: detector rows)");
-    // [0, B): counts in, [B, 2B): kept per frame, [2B]: total
-    int32_t* d = ar.get<int32_t>(slot, 2 * (size_t)B + 1);
-    std::vector<int32_t> h(2 * (size_t)B + 1, 0);
-    VTF_HIP(hipMemcpyAsync(d, counts.data(), (size_t)B * 4, hipMemcpyHostToDevice, st));
-    if (rows > 0) launch_box_post(d_rows, d, B, H, W, p, frame_offset, d_crops, d_src, d + B, d + 2 * B, st);
-    else VTF_HIP(hipMemsetAsync(d + B, 0, ((size_t)B + 1) * 4, st));
-    VTF_HIP(hipMemcpyAsync(h.data() + B, d + B, ((size_t)B + 1) * 4, hipMemcpyDeviceToHost, st));
-    VTF_HIP(hipStreamSynchronize(st));
-    if (h_frame_counts) std::copy(h.begin() + B, h.begin() + 2 * B, h_frame_counts);
+    // pinned mailbox (Arena::mail): [0, B) counts in, [B, 2B) kept per frame, [2B] total -- the
+    // kernel reads the counts and writes its results there directly (no blit copies, no memset)
+    Arena::Mail mb = ar.mail(slot, (2 * (size_t)B + 1) * 4);
+    int32_t* h = (int32_t*)mb.h;
+    int32_t* d = (int32_t*)mb.d;
+    std::copy(counts.begin(), counts.end(), h);
+    if (rows > 0) {
+        launch_box_post(d_rows, d, B, H, W, p, frame_offset, d_crops, d_src, d + B, d + 2 * B, st);
+        VTF_HIP(hipStreamSynchronize(st));
+    } else {
+        std::fill(h + B, h + 2 * B + 1, 0);
+    }
+    if (h_frame_counts) std::copy(h + B, h + 2 * B, h_frame_counts);
     if (out_n) *out_n = h[2 * (size_t)B];
     return h[2 * (size_t)B];
 }

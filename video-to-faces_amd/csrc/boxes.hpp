@@ -14,7 +14,7 @@ namespace vtf {
 constexpr int BOX_MAX_FRAMES = 4096;
 void launch_box_post(const float* d_rows, const int32_t* d_counts, int B, int H, int W, const vtf_box_params& p,
                      int frame_offset, int32_t* d_crops, int32_t* d_src, int32_t* d_frame_counts, int32_t* d_total,
-                     hipStream_t st);
+                     hipStream_t st, int64_t cap = INT64_MAX);
 
 // launch_box_post on a detector's device rows with host per-frame counts (negative = the frame is
 // absent from the detector's output, as R-CNN past its last proposal image: no crops).  Uploads the

@@ -58,10 +58,45 @@ struct Arena {
     std::vector<void*> ptr;
     std::vector<size_t> cap;
     std::vector<void*> retired;
+    // pinned host buffers mapped into the device address space ("mailboxes"): small tables the
+    // host hands to a kernel and small results a kernel hands back are read / written there
+    // directly, with no runtime blit copy (a pageable hipMemcpyAsync stages through a pinned
+    // buffer and runs a copy kernel per call) -- the host reads results after a stream sync
+    struct Mail {
+        void* h;
+        void* d;
+    };
+    std::vector<Mail> mptr;
+    std::vector<size_t> mcap;
+    std::vector<void*> mretired;
     ~Arena() {
         for (void* p : ptr)
             if (p) (void)hipFree(p);
         for (void* p : retired) (void)hipFree(p);
+        for (const Mail& m : mptr)
+            if (m.h) (void)hipHostFree(m.h);
+        for (void* p : mretired) (void)hipHostFree(p);
+    }
+    // a mailbox of at least `bytes`; retired (not freed) when it grows, like get()
+    Mail mail(int slot, size_t bytes) {
+        if ((int)mptr.size() <= slot) {
+            mptr.resize(slot + 1, Mail{nullptr, nullptr});
+            mcap.resize(slot + 1, 0);
+        }
+        if (bytes == 0) bytes = 16;
+        if (mcap[slot] < bytes) {
+            if (mptr[slot].h) mretired.push_back(mptr[slot].h);
+            const size_t b = ((bytes + bytes / 2) + 4095) & ~(size_t)4095;
+            void* h = nullptr;
+            void* d = nullptr;
+            // coherent (fine-grained): the device reads and writes go to host memory uncached, so a
+            // table rewritten by the host between launches is never read stale from the L2
+            VTF_HIP(hipHostMalloc(&h, b, hipHostMallocMapped | hipHostMallocCoherent));
+            VTF_HIP(hipHostGetDevicePointer(&d, h, 0));
+            mptr[slot] = Mail{h, d};
+            mcap[slot] = b;
+        }
+        return mptr[slot];
     }
     void* get(int slot, size_t bytes) {
         if ((int)ptr.size() <= slot) {

@@ -23,9 +23,10 @@ struct PNetW {
     const uint16_t* c3h;
     const uint16_t* c2h;  // conv2: [2][16][96], the 90 (tap, ci) products packed in 3 k-steps (mtcnn_runtime)
     const uint16_t* c1h;  // conv1: [2][16][64], k = ky * 16 + kx * 4 + c (c = 3, kx = 3, ky = 3, co >= 10 zero)
-    // both 1x1 heads as fp16 split planes [2][16 rows][32 k] (rows 0,1 conv4_1, 2..5 conv4_2);
-    // k = 8g + j holds channel 4g + j (j < 4) or 16 + 4g + j - 4: exactly the conv3 accumulator
-    // values lane group g owns, so the heads need no lane movement.  null -> fp32 heads
+    // both 1x1 heads as fp16 split planes [2][32 rows][32 k] (rows 0,1 conv4_1, 2..5 conv4_2, the
+    // rest zero); k = 16 s + 8 hk + i holds channel 16 s + 8 (i >> 2) + (i & 3) + 4 hk: exactly
+    // the conv3 accumulator registers 8 s + i of lane half hk (k_pnet's 32x32x16 conv3), so the
+    // heads need no lane movement.  null -> fp32 heads
     const uint16_t* hh;
     // PReLU slope classes (host): bit 0 every conv2 slope in [0, 1], bit 1 every conv3 slope in
     // [0, 1] -- PReLU is then max(v, a v), two instructions instead of three
@@ -48,7 +49,7 @@ struct PNetOut {
 };
 
 void launch_sat(const uint8_t* frames, int64_t frame_stride, int64_t row_stride, int B, int H, int W, int4* sat,
-                hipStream_t st);
+                hipStream_t st, uint32_t* zero = nullptr, int nzero = 0);
 void launch_resample_sat(const int4* sat, int B, int H, int W, int lh, int lw, float* out, hipStream_t st);
 struct ResampleLevels {  // precomputed pyramid levels of one det-batch (k_resample_sat_multi)
     static constexpr int MAXL = 32;
@@ -60,7 +61,7 @@ struct ResampleLevels {  // precomputed pyramid levels of one det-batch (k_resam
 void launch_resample_sat_multi(const int4* sat, int B, int H, int W, const ResampleLevels& lv, hipStream_t st);
 void launch_pnet(bool dense, const uint8_t* frames, int64_t frame_stride, int64_t row_stride, int H, int W,
                  const PNetLevel* d_levels, int n_levels, int64_t total_tiles, const PNetW& w, const PNetOut& o,
-                 uint32_t* d_tile_ctr, hipStream_t st, int64_t exact_tiles = 0);
+                 uint32_t* d_tile_ctr, hipStream_t st, int64_t exact_tiles = 0);  // d_tile_ctr: 2 zeroed words
 // leading tiles of the level plan that k_pnet's exact-levels variant takes (see launch_pnet)
 int64_t pnet_exact_tiles(const std::vector<PNetLevel>& lv, int H, int W, int64_t total_tiles);
 int cand_front_side(bool onet);
@@ -88,9 +89,11 @@ void launch_decode_stage1(const uint64_t* key_sorted, const int32_t* slot_sorted
                           int32_t* img, int32_t* call, hipStream_t st);
 void launch_gather_refine(const int32_t* idx, int64_t n, const float4* bin, const float* sin, const float4* rin,
                           const int32_t* iin, int refine, int plus_one, int square, float4* bout, float* sout,
-                          float4* rout, int32_t* iout, hipStream_t st);
+                          float4* rout, int32_t* iout, hipStream_t st, int32_t* zout = nullptr,
+                          int32_t* zw = nullptr, int nzw = 0);
 void launch_threshold(const float* s, int64_t n, float thr, int32_t* flag, hipStream_t st);
-void launch_flag_compact(const int32_t* flag, const int32_t* incl, int64_t n, int32_t* out, hipStream_t st);
+void launch_flag_compact(const int32_t* flag, const int32_t* incl, int64_t n, int32_t* out, hipStream_t st,
+                         int32_t* mail = nullptr, const int32_t* ctl = nullptr, int nctl = 0);
 void launch_landmarks(const float4* boxes, const float* lm, int64_t n, float* out, hipStream_t st);
 void launch_iom_chain(const float4* boxes, const int32_t* img, const int32_t* order, int64_t n, float thr,
                       int32_t* keep, hipStream_t st);

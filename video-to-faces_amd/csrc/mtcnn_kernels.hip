@@ -61,7 +61,11 @@ constexpr int PH_C2H = 9216, PH_C1H = 12288, PH_HH = 14336;  // halves (conv3 pl
 
 // row pass: block per frame row
 __global__ __launch_bounds__(256) void k_sat_rows(const uint8_t* __restrict__ frames, int64_t frame_stride,
-                                                  int64_t row_stride, int H, int W, int4* __restrict__ sat) {
+                                                  int64_t row_stride, int H, int W, int4* __restrict__ sat,
+                                                  uint32_t* __restrict__ zero, int nzero) {
+    // (folded memset: the det-batch's PNet candidate counters)
+    if (blockIdx.x == 0)
+        for (int i = threadIdx.x; i < nzero; i += 256) zero[i] = 0u;
     // row prefix sums in passes of 256 consecutive pixels (one per thread: coalesced byte loads
     // and 4 KB contiguous int4 stores), a block scan per pass with the carry in registers
     const int y = blockIdx.x % H, b = blockIdx.x / H;
@@ -165,8 +169,8 @@ __global__ __launch_bounds__(SAT_COLS * SAT_MAXG) void k_sat_cols(int H, int W, 
 }
 
 void launch_sat(const uint8_t* frames, int64_t frame_stride, int64_t row_stride, int B, int H, int W, int4* sat,
-                hipStream_t st) {
-    k_sat_rows<<<(unsigned)((int64_t)B * H), 256, 0, st>>>(frames, frame_stride, row_stride, H, W, sat);
+                hipStream_t st, uint32_t* zero, int nzero) {
+    k_sat_rows<<<(unsigned)((int64_t)B * H), 256, 0, st>>>(frames, frame_stride, row_stride, H, W, sat, zero, nzero);
     const int G = (H + SAT_PER - 1) / SAT_PER;
     VTF_CHECK(G <= SAT_MAXG, VTF_E_LIMIT, "mtcnn: frames taller than 1536 rows");
     k_sat_cols<<<(unsigned)(B * ((W + SAT_COLS) / SAT_COLS)), SAT_COLS * G, (size_t)G * SAT_COLS * sizeof(int4), st>>>(H, W, sat);
@@ -240,6 +244,12 @@ constexpr int P_POOL0 = (10 * PP_H * PP_W > PQ_C * PP_H * PP_W) ? 10 * PP_H * PP
 // and conv3's split weights [2][32][144] halves (floats 512..5119, rows of 72 dwords: conflict-free
 // for the 16-byte A-operand reads), so conv3 issues no global loads
 constexpr int P_W3 = 512, W3_ROW = 144;
+// Bank swizzles for conv3's 16-byte operand reads (ds_read_b128 serves 16 lanes per LDS cycle:
+// {0-3,12-15,20-27}, {4-11,16-19,28-31} and the same for lanes 32-63).  C3_SWZ: weight rows
+// >= 16 of each plane hold every tap's channel halves swapped ([8..15 | 0..7], mtcnn_runtime),
+// so the 32x32 path's 16 rows per lane group land on 16 distinct 4-bank slots (72-dword rows
+// alone give each slot twice).  C2_SWZ: conv2's split output stores odd rows' 16 channels
+// swapped the same way, so a lane group's two cell rows read disjoint slots.
 constexpr int P_POOL = P_POOL0 > P_W3 + 2 * 32 * W3_ROW / 2 ? P_POOL0 : P_W3 + 2 * 32 * W3_ROW / 2;
 constexpr int P_LVLH = PL_H * PL_W * 4;                // level as fp16 split planes [2][y][x][4] (in floats)
 constexpr int P_A0 = P_C2 > P_LVL ? P_C2 : P_LVL;
@@ -365,7 +375,7 @@ struct PnLds {
     static constexpr int POOL = X ? PQ_C * PP_H * PP_W : P_POOL;      // floats (split pooled conv1)
     static constexpr int W3 = X ? 0 : P_W3;                           // conv3 weights (floats)
     static constexpr int PATCH = (POOL - 4) * 4;                      // staged frame patch (bytes)
-    static constexpr int BYTES = (A + POOL) * 4 + (PL_H + PL_W) * 4 + 16 + 64;
+    static constexpr int BYTES = (A + POOL) * 4 + (PL_H + PL_W) * 4 + 16 + 64 + 256;  // + s_c3
     static constexpr int GPC = (160 * 1024) / ((BYTES + 511) / 512 * 512);
     static_assert(!X || (2 * P_C2 >= PL_H * PL_W * 4 + 4 && POOL >= 2 * 32 * W3_ROW / 2 && GPC >= 4),
                   "exact-levels k_pnet LDS plan");
@@ -387,7 +397,7 @@ __global__ __launch_bounds__(256, PnLds<X>::GPC) void k_pnet(const uint8_t* __re
     const __amdgpu_buffer_rsrc_t rw3 = __builtin_amdgcn_make_buffer_rsrc((void*)(wg.c1w + PW_C3W), 0, 144 * 32 * 4, 0x00020000);
     const __amdgpu_buffer_rsrc_t rw2h = __builtin_amdgcn_make_buffer_rsrc((void*)(wg.c3h + PH_C2H), 0, 2 * 16 * 96 * 2, 0x00020000);
     const __amdgpu_buffer_rsrc_t rw1h = __builtin_amdgcn_make_buffer_rsrc((void*)(wg.c3h + PH_C1H), 0, 2 * 16 * 64 * 2, 0x00020000);
-    const __amdgpu_buffer_rsrc_t rhh = __builtin_amdgcn_make_buffer_rsrc((void*)(wg.c3h + PH_HH), 0, 2 * 16 * 32 * 2, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rhh = __builtin_amdgcn_make_buffer_rsrc((void*)(wg.c3h + PH_HH), 0, 2 * 32 * 32 * 2, 0x00020000);
     // conv3 on fp16 matrix cores (mtcnn_runtime: range bound); the X variant is launched only then
     const bool split3 = X || wg.c3h != nullptr;
     __shared__ __attribute__((aligned(16))) float sA[LP::A];     // level tile, later conv2 output
@@ -395,7 +405,9 @@ __global__ __launch_bounds__(256, PnLds<X>::GPC) void k_pnet(const uint8_t* __re
     __shared__ ushort2 ybin[PL_H], xbin[PL_W];  // frame bin [start, end) of each level row / column
     __shared__ int s_tile, s_next, s_cend;
     __shared__ unsigned long long s_clk[8];  // phase clocks (VTF_PNET_DEBUG & 256)
-    const int tid = threadIdx.x;
+    // conv3 bias / PReLU slope in the 32x32 accumulator order: [bias | slope][lane half][16]
+    __shared__ __attribute__((aligned(16))) float s_c3[64];
+    const int tid0 = threadIdx.x, tid = tid0;
     bool pf_done = false;  // the first 2 KB of this tile's frame patch were staged by the previous tile
     int n_chunks = 0;      // chunks taken after the first (thread 0)
     int L_prev = 0;
@@ -413,8 +425,7 @@ __global__ __launch_bounds__(256, PnLds<X>::GPC) void k_pnet(const uint8_t* __re
     };
     if (tid < 8) s_clk[tid] = 0;
     if (tid == 0 && clk_on) s_tlast = clock64();
-    const int lane = tid & 63, wave = tid >> 6;
-    const int lr = lane & 15, lk = lane >> 4;
+    const int lr = tid & 15;  // (the tile loop re-derives the lane coordinates per tile)
 
     // ---- weights and im2col offsets, loaded once per persistent workgroup
     const float b2 = wf[PW_C2B + lr], a2 = wf[PW_P2 + lr];
@@ -424,6 +435,10 @@ __global__ __launch_bounds__(256, PnLds<X>::GPC) void k_pnet(const uint8_t* __re
     // zero pad after the split level planes: read by conv1 (against zero weights) one pixel past
     // the last level pixel, and conv3's zero weight slots (k >= 144) point at it
     if (tid < 4) sA[LP::A - 4 + tid] = 0.f;
+    if (tid < 64) {  // register r of lane half h holds channel (r & 3) + 8 (r >> 2) + 4 h
+        const int r = tid & 15, ch = (r & 3) + 8 * (r >> 2) + 4 * ((tid >> 4) & 1);
+        s_c3[tid] = tid < 32 ? wf[PW_C3B + ch] : wf[PW_P3 + ch];
+    }
     // tiles are handed out in chunks of PNET_TILE_CHUNK: one same-address atomic per chunk (a
     // single counter hit once per tile serialises ~166k atomics per launch at the L2)
     if (tid == 0) {
@@ -434,6 +449,14 @@ __global__ __launch_bounds__(256, PnLds<X>::GPC) void k_pnet(const uint8_t* __re
         __syncthreads();
         mark(0);  // 0: end-of-tile prefetch store + loop barrier
         // (wave-uniform: the level table and tile geometry below become scalar loads)
+        // thread coordinates laundered per tile: everything derived from them below is recomputed
+        // inside the tile instead of being hoisted out of the persistent loop into long-lived
+        // registers (the kernel runs at the 128-register limit of four workgroups per CU)
+        int tid = tid0;
+        asm volatile("" : "+v"(tid));
+        const int lane = tid & 63, wave = tid >> 6;
+        const int lr = lane & 15, lk = lane >> 4;
+        (void)lr, (void)lk;
         const int64_t blk = __builtin_amdgcn_readfirstlane(s_tile);
         if (blk >= total_tiles) break;
         uint32_t next_tile = 0, next_cend = 0;
@@ -550,15 +573,24 @@ __global__ __launch_bounds__(256, PnLds<X>::GPC) void k_pnet(const uint8_t* __re
             // per level pixel (plane 0 only; the value is its own fp16 split: x1 = 0)
             typedef __attribute__((ext_vector_type(4))) short s16x4;
             s16x4* hs = (s16x4*)(patch + hs_off);
-            for (int i = tid; i < nrows * PL_W; i += 256) {
-                const int r = i / PL_W, q = i - r * PL_W;
-                const ushort2 xb = xbin[q];
-                const int n = xb.y - xb.x;
-                const uint8_t* row = patch + r * pw3 + (n ? (xb.x - fx0) * 3 : 0);
-                const uint8_t* row2 = n > 1 ? row + 3 : row;
-                const int m = n > 1 ? 1 : 0;
-                const int a0 = row[2] + m * row2[2], a1 = row[1] + m * row2[1], a2 = row[0] + m * row2[0];
-                hs[i] = s16x4{(short)(2 * a0 - 255 * n), (short)(2 * a1 - 255 * n), (short)(2 * a2 - 255 * n), 0};
+            // 2-D thread map: column fq of every 6th row from fr0 (252 of the 256 threads), so the
+            // column's bin is read and decoded once per tile instead of once per element
+            // (tid laundered per tile: the map would otherwise be hoisted into long-lived registers)
+            int tl = tid;
+            asm volatile("" : "+v"(tl));
+            const int fq = tl % PL_W, fr0 = tl < 6 * PL_W ? tl / PL_W : PL_H;
+            const ushort2 xbq = xbin[fq];
+            const int nq = xbq.y - xbq.x, mq = nq > 1 ? 1 : 0;
+            {
+                const uint8_t* col = patch + (nq ? (xbq.x - fx0) * 3 : 0);
+                const uint8_t* col2 = col + 3 * mq;
+                const int sub = 255 * nq;
+                for (int r = fr0; r < nrows; r += 6) {
+                    const uint8_t* row = col + r * pw3;
+                    const uint8_t* row2 = col2 + r * pw3;
+                    const int a0 = row[2] + mq * row2[2], a1 = row[1] + mq * row2[1], a2 = row[0] + mq * row2[0];
+                    hs[r * PL_W + fq] = s16x4{(short)(2 * a0 - sub), (short)(2 * a1 - sub), (short)(2 * a2 - sub), 0};
+                }
             }
             __syncthreads();
             typedef __attribute__((ext_vector_type(4))) _Float16 h4;
@@ -566,20 +598,20 @@ __global__ __launch_bounds__(256, PnLds<X>::GPC) void k_pnet(const uint8_t* __re
             // conv1's operand reads run one pixel past plane 0 (against zero weights) into plane
             // 1, which this path leaves stale: that pixel must be finite
             if (tid == 0) lvl[PL_H * PL_W] = h4{(_Float16)0.f, (_Float16)0.f, (_Float16)0.f, (_Float16)0.f};
-            for (int i = tid; i < PL_H * PL_W; i += 256) {
-                const int r = i / PL_W, q = i - r * PL_W;
-                const ushort2 yb = ybin[r], xb = xbin[q];
-                const int kh = yb.y - yb.x, kw = xb.y - xb.x;
-                const s16x4* h = hs + (kh ? yb.x - fy0 : 0) * PL_W + q;
+            // s / kh / kw with kh, kw in {1, 2}: a power-of-two scale, exact
+            const float scw = nq > 1 ? 0.001953125f : 0.00390625f;
+            for (int r = fr0; r < PL_H; r += 6) {
+                const ushort2 yb = ybin[r];
+                const int kh = yb.y - yb.x;
+                const s16x4* h = hs + (kh ? yb.x - fy0 : 0) * PL_W + fq;
                 const s16x4 v0 = h[0], v1 = h[kh > 1 ? PL_W : 0];
                 const int m = kh > 1 ? 1 : 0;
-                // s / kh / kw with kh, kw in {1, 2}: a power-of-two scale, exact
-                const float sc = 0.00390625f * (kh > 1 ? 0.5f : 1.f) * (kw > 1 ? 0.5f : 1.f);
-                const bool in = kh > 0 && kw > 0;
+                const float sc = kh > 1 ? 0.5f * scw : scw;
+                const bool in = kh > 0 && nq > 0;
                 const float r0 = in ? (float)(v0[0] + m * v1[0]) * sc : 0.f;
                 const float g0 = in ? (float)(v0[1] + m * v1[1]) * sc : 0.f;
                 const float b0 = in ? (float)(v0[2] + m * v1[2]) * sc : 0.f;
-                lvl[i] = h4{(_Float16)r0, (_Float16)g0, (_Float16)b0, (_Float16)0.f};
+                lvl[r * PL_W + fq] = h4{(_Float16)r0, (_Float16)g0, (_Float16)b0, (_Float16)0.f};
             }
         } else if (!X && sep) {
             int16_t* hs = (int16_t*)(patch + hs_off);
@@ -979,8 +1011,10 @@ __global__ __launch_bounds__(256, PnLds<X>::GPC) void k_pnet(const uint8_t* __re
                                 v0[i] = x0;
                                 v1[i] = x1;
                             }
-                            *(f16x4*)(sO + q * 16 + 4 * lkx) = v0;
-                            *(f16x4*)(sO + NPOS * 16 + q * 16 + 4 * lkx) = v1;
+                            // (odd rows: channel halves swapped, see C2_SWZ)
+                            const int qo = q * 16 + ((4 * lkx) ^ (8 * ((q / PC_W) & 1)));
+                            *(f16x4*)(sO + qo) = v0;
+                            *(f16x4*)(sO + NPOS * 16 + qo) = v1;
                         }
                     }
                 }
@@ -1107,12 +1141,26 @@ __global__ __launch_bounds__(256, PnLds<X>::GPC) void k_pnet(const uint8_t* __re
                     const float hv = lrx < 2 ? wf[PW_C41W + hrow] : wf[PW_C42W + hrow];
                     hwA[mf][i] = !X && lrx < 6 ? hv : 0.f;
                 }
+            // split conv3 + split heads (every X launch; the general variant when the host bounds
+            // hold): conv3 and the heads on 32x32x16 matrix cores (below); otherwise the 16x16
+            // fallbacks (fp32 conv3 and / or fp32 heads)
             const bool splith = X || wg.hh != nullptr;  // (X: launched only with the split heads)
-            f16x8 hw0 = {}, hw1 = {};
-            if (splith) {
-                const int hoff = (lrx * 32 + 8 * lkx) * 2;
-                hw0 = __builtin_bit_cast(f16x8, __builtin_amdgcn_raw_buffer_load_b128(rhh, hoff, 0, 0));
-                hw1 = __builtin_bit_cast(f16x8, __builtin_amdgcn_raw_buffer_load_b128(rhh, hoff, 16 * 32 * 2, 0));
+            const bool c3_32 = split3 && splith && !(o.dbg & 8);
+            // heads as the A operand of two 32x32x16 steps: [plane][step], row = head (lane & 31;
+            // rows >= 6 zero), k-slot (s, hk, i) = channel 16 s + 8 (i >> 2) + (i & 3) + 4 hk --
+            // exactly the conv3 accumulator registers 8 s + i of lane half hk (mtcnn_runtime packs
+            // [2][32][32] halves that way)
+            f16x8 hw[2][2] = {};
+            if (c3_32) {
+                int ln = lane;
+                asm volatile("" : "+v"(ln));
+                const int hoff = ((ln & 31) * 32 + 8 * (ln >> 5)) * 2;
+#pragma unroll
+                for (int pl = 0; pl < 2; pl++)
+#pragma unroll
+                    for (int s = 0; s < 2; s++)
+                        hw[pl][s] = __builtin_bit_cast(
+                            f16x8, __builtin_amdgcn_raw_buffer_load_b128(rhh, hoff, pl * 32 * 32 * 2 + s * 32, 0));
             }
             // (issued after the head weights: loads complete in order, and the frame bytes are
             //  the slow ones; the scheduling barrier keeps the order)
@@ -1155,6 +1203,161 @@ __global__ __launch_bounds__(256, PnLds<X>::GPC) void k_pnet(const uint8_t* __re
             // 0, 1; group 1: conv4_2 2, 3; groups 2, 3 hold no heads)
             const f32x4 hbv = lkx == 0 ? f32x4{wf[PW_C41B], wf[PW_C41B + 1], wf[PW_C42B], wf[PW_C42B + 1]}
                                        : f32x4{wf[PW_C42B + 2], wf[PW_C42B + 3], 0.f, 0.f};
+            // stage-1 gate of one cell: softmax over the face logits (mtcnn.py:37), p >= 0.6
+            // (mtcnn.py:183), wave-aggregated candidate append; DENSE writes the parity maps
+            auto gate = [&](bool valid, int oy, int ox, float a0, float a1v, float q0, float q1, float q2, float q3) {
+                auto softmax1 = [&]() {
+                    const float mx = fmaxf(a0, a1v);
+                    const float e0 = expf(a0 - mx), e1 = expf(a1v - mx);
+                    return __fdiv_rn(e1, e0 + e1);
+                };
+                if (DENSE) {
+                    const float prob = softmax1();
+                    if (valid) {
+                        int64_t plane = (int64_t)P.ph * P.pw;
+                        int64_t pc = (int64_t)oy * P.pw + ox;
+                        o.prob[(int64_t)b * plane + pc] = prob;
+                        float* rg = o.reg + (int64_t)b * 4 * plane + pc;
+                        rg[0] = q0;
+                        rg[plane] = q1;
+                        rg[2 * plane] = q2;
+                        rg[3 * plane] = q3;
+                    }
+                } else {
+                    // mask = prob >= 0.6 (the python scalar compares as fp32).  The softmax is
+                    // evaluated only where it can pass: with d = a1 - a0 (the same fp32 difference
+                    // the reference exponentiates when a1 > a0), d < 0.4 gives prob <= 1 / (1 +
+                    // expf(-0.4)) = 0.5987 < 0.6, a margin far above expf's and the division's
+                    // rounding; a NaN d takes the exact path.  ~0.1 % of the cells pass, so nearly
+                    // every wave skips the two expf and the division (wave-uniform branch).
+                    const bool near = valid && !(a1v - a0 < 0.4f) && !(o.dbg & 16);
+                    float prob = 0.f;
+                    bool pass = false;
+                    if (__ballot(near)) {
+                        prob = softmax1();
+                        pass = near && prob >= 0.6f;
+                    }
+                    uint64_t bal = __ballot(pass);
+                    if (bal) {
+                        int leader = __builtin_ctzll(bal);
+                        uint32_t base = 0;
+                        if (lane == leader) {
+                            base = atomicAdd(o.count, (uint32_t)__popcll(bal));
+                            atomicAdd(&o.level_count[L], (uint32_t)__popcll(bal));
+                        }
+                        base = __shfl(base, leader);
+                        if (pass) {
+                            uint32_t slot = base + (uint32_t)__popcll(bal & ((1ull << lane) - 1ull));
+                            if (slot < o.cap) {
+                                uint32_t lin = (uint32_t)(((int64_t)b * P.ph + oy) * P.pw + ox);
+                                o.key[slot] = ((uint64_t)L << 32) | lin;
+                                o.score[slot] = prob;
+                                o.regv[slot] = make_float4(q0, q1, q2, q3);
+                            }
+                        }
+                    }
+                }
+            };
+            if (c3_32) {
+                // conv3 (16 -> 32, 3x3) transposed on v_mfma_f32_32x32x16_f16: C (32 channels x 32
+                // cells) = W3 (32 x 144) x im2col (144 x 32 cells), one k-step per tap (16 channels,
+                // K = 144 exactly: no padding slots).  A = the split weights in LDS (row = channel
+                // lane & 31, k = 16 tap + 8 hk ..), B = conv2's split output (column = cell lane & 31).
+                // Main products x0 w0 into an accumulator seeded with the bias, the cross terms x0 w1 +
+                // x1 w0 into a second one; 27 MFMAs per 32 cells (60 of 16x16x32 before, 8 issue
+                // cycles each).  Accumulator register r of lane l: channel (r & 3) + 8 (r >> 2) + 4 hk
+                // of cell l & 31; both heads are two more 32x32x16 steps over those registers.
+                typedef __attribute__((ext_vector_type(16))) float f32x16;
+                typedef const volatile __attribute__((address_space(3))) f32x4 lds_f32x4;
+                constexpr int NPOS = PC_H * PC_W;
+                const _Float16* sH = (const _Float16*)sA;
+                int ln = lane;
+                asm volatile("" : "+v"(ln));
+                const int c32 = ln & 31, hk = ln >> 5;
+                // (rows >= 16 hold each tap's channel halves swapped, see C3_SWZ)
+                const _Float16* sWh = (const _Float16*)(sP + LP::W3) + c32 * W3_ROW + 8 * (hk ^ (c32 >> 4));
+                const float* cst = s_c3 + 16 * hk;  // [bias | slope] rows of the lane half
+                const f32x4 hb = hk == 0 ? f32x4{wf[PW_C41B], wf[PW_C41B + 1], wf[PW_C42B], wf[PW_C42B + 1]}
+                                         : f32x4{wf[PW_C42B + 2], wf[PW_C42B + 3], 0.f, 0.f};
+#pragma unroll 1
+                for (int hh = 0; hh < NHALF; hh++) {
+                    const int cell = (wave * FPW + hh * FH) * 16 + c32;
+                    const int cy = cell / PT_W, cx = cell % PT_W;
+                    // (cy = even first row + c32 >> 4; odd conv2 rows swapped: the half this lane reads
+                    //  flips with the tap row's parity)
+                    const _Float16* xs = sH + (cy * PC_W + cx) * 16 + 8 * (hk ^ (c32 >> 4));
+                    const _Float16* xsf = sH + (cy * PC_W + cx) * 16 + 8 * (hk ^ (c32 >> 4) ^ 1);
+                    f32x16 am, ac = {};
+#pragma unroll
+                    for (int i = 0; i < 4; i++) {
+                        const f32x4 v = *(lds_f32x4*)(cst + 4 * i);
+                        am[4 * i] = v[0], am[4 * i + 1] = v[1], am[4 * i + 2] = v[2], am[4 * i + 3] = v[3];
+                    }
+                    // operands one tap ahead (two register stages; the scheduling barriers keep
+                    // the compiler from hoisting all 36 reads, which would spill)
+                    f16x8 op[2][4];
+                    auto ld_tap = [&](int t, f16x8* d) {
+                        const int to = ((t / 3) * PC_W + t % 3) * 16;
+                        d[0] = *(const f16x8*)(sWh + 16 * t);
+                        d[1] = *(const f16x8*)(sWh + 32 * W3_ROW + 16 * t);
+                        const _Float16* xt = ((t / 3) & 1) ? xsf : xs;
+                        d[2] = *(const f16x8*)(xt + to);
+                        d[3] = *(const f16x8*)(xt + NPOS * 16 + to);
+                    };
+                    ld_tap(0, op[0]);
+#pragma unroll
+                    for (int t = 0; t < 9; t++) {
+                        if (t + 1 < 9) ld_tap(t + 1, op[(t + 1) & 1]);
+                        const f16x8* c = op[t & 1];
+                        am = __builtin_amdgcn_mfma_f32_32x32x16_f16(c[0], c[2], am, 0, 0, 0);
+                        ac = __builtin_amdgcn_mfma_f32_32x32x16_f16(c[1], c[2], ac, 0, 0, 0);
+                        ac = __builtin_amdgcn_mfma_f32_32x32x16_f16(c[0], c[3], ac, 0, 0, 0);
+                        __builtin_amdgcn_sched_barrier(0);
+                    }
+                    if (o.dbg & 32) continue;
+                    auto epi = [&](auto u_t) {
+                        constexpr bool U3 = decltype(u_t)::value;
+                        // 2048 (bias + main) + cross, PReLU (commutes with the scaling), split
+                        f16x8 x0h[2], x1h[2];
+#pragma unroll
+                        for (int i = 0; i < 4; i++) {
+                            const f32x4 a = *(lds_f32x4*)(cst + 32 + 4 * i);
+#pragma unroll
+                            for (int k = 0; k < 4; k++) {
+                                const int r = 4 * i + k;
+                                _Float16 p0, p1;
+                                split_u(prelu_t<U3>(fmaf(am[r], 2048.f, ac[r]), a[k]), p0, p1);
+                                x0h[r >> 3][r & 7] = p0;
+                                x1h[r >> 3][r & 7] = p1;
+                            }
+                        }
+                        // heads: cross terms first, scaled by 2^-11 into the main products' chain
+                        f32x16 hc = {};
+#pragma unroll
+                        for (int s = 0; s < 2; s++) {
+                            hc = __builtin_amdgcn_mfma_f32_32x32x16_f16(hw[0][s], x1h[s], hc, 0, 0, 0);
+                            hc = __builtin_amdgcn_mfma_f32_32x32x16_f16(hw[1][s], x0h[s], hc, 0, 0, 0);
+                        }
+                        hc = hc * 0.00048828125f;
+#pragma unroll
+                        for (int s = 0; s < 2; s++)
+                            hc = __builtin_amdgcn_mfma_f32_32x32x16_f16(hw[0][s], x0h[s], hc, 0, 0, 0);
+                        // registers 0..3 of lane half 0: heads 0..3 (a0 a1 r0 r1), of half 1: heads
+                        // 4, 5 (r2 r3); biases added (VALU) before the swap that hands half 1's r2,
+                        // r3 to half 0 (lanes l and l + 32 hold the same cell)
+                        const f32x4 hq = f32x4{hc[0], hc[1], hc[2], hc[3]} + hb;
+                        const auto s2 = __builtin_amdgcn_permlane32_swap(__float_as_uint(hq[0]), __float_as_uint(hq[0]), false, false);
+                        const auto s3 = __builtin_amdgcn_permlane32_swap(__float_as_uint(hq[1]), __float_as_uint(hq[1]), false, false);
+                        const int oy = oy0 + cy, ox = ox0 + cx;
+                        const bool valid = hk == 0 && oy < P.ph && ox < P.pw;
+                        gate(valid, oy, ox, hq[0], hq[1], hq[2], hq[3], __uint_as_float(s2[1]), __uint_as_float(s3[1]));
+                    };
+                    if (wg.unit_slopes & 2)
+                        epi(std::true_type{});
+                    else
+                        epi(std::false_type{});
+                }
+            } else
 #pragma unroll 1
             for (int hh = 0; hh < NHALF; hh++) {
                 f32x4 acc[FH][2];
@@ -1180,6 +1383,7 @@ __global__ __launch_bounds__(256, PnLds<X>::GPC) void k_pnet(const uint8_t* __re
                     // weights from the pooled buffer (rows of W3_ROW halves); k slots >= 144 (step 4,
                     // lane groups 2, 3) are zero: those lanes read the zero pad after the level planes
                     const _Float16* sWh = (const _Float16*)(sP + LP::W3) + lrx * W3_ROW + 8 * lkx;
+                    const _Float16* sWhs = (const _Float16*)(sP + LP::W3) + lrx * W3_ROW + 8 * (lkx ^ 1);  // rows >= 16
                     const _Float16* zpad = (const _Float16*)(sA + LP::A - 4);
     #pragma unroll
                     for (int s5 = 0; s5 < 5; s5++) {
@@ -1187,15 +1391,18 @@ __global__ __launch_bounds__(256, PnLds<X>::GPC) void k_pnet(const uint8_t* __re
                         const bool zw = s5 == 4 && lkx >= 2;
     #pragma unroll
                         for (int mf = 0; mf < 2; mf++) {
-                            w0[mf] = *(const f16x8*)(zw ? zpad : sWh + (mf * 16) * W3_ROW + 32 * s5);
-                            w1[mf] = *(const f16x8*)(zw ? zpad : sWh + (32 + mf * 16) * W3_ROW + 32 * s5);
+                            const _Float16* sw = mf ? sWhs : sWh;
+                            w0[mf] = *(const f16x8*)(zw ? zpad : sw + (mf * 16) * W3_ROW + 32 * s5);
+                            w1[mf] = *(const f16x8*)(zw ? zpad : sw + (32 + mf * 16) * W3_ROW + 32 * s5);
                         }
                         const int tap = min(2 * s5 + (lkx >> 1), 8);
-                        const int xo = ((tap / 3) * PC_W + (tap % 3)) * 16 + 8 * (lkx & 1);
+                        const int xo = ((tap / 3) * PC_W + (tap % 3)) * 16;
+                        const int hx = 8 * ((lkx & 1) ^ ((tap / 3) & 1));  // + the cell row's parity (j & 1)
     #pragma unroll
                         for (int j = 0; j < FH; j++) {
-                            const f16x8 x0 = *(const f16x8*)(sH + ab[j] * 16 + xo);
-                            const f16x8 x1 = *(const f16x8*)(sH + NPOS * 16 + ab[j] * 16 + xo);
+                            const int xj = xo + (hx ^ (8 * (j & 1)));
+                            const f16x8 x0 = *(const f16x8*)(sH + ab[j] * 16 + xj);
+                            const f16x8 x1 = *(const f16x8*)(sH + NPOS * 16 + ab[j] * 16 + xj);
     #pragma unroll
                             for (int mf = 0; mf < 2; mf++) {
                                 acc[j][mf] = __builtin_amdgcn_mfma_f32_16x16x32_f16(w0[mf], x0, acc[j][mf], 0, 0, 0);
@@ -1252,32 +1459,13 @@ __global__ __launch_bounds__(256, PnLds<X>::GPC) void k_pnet(const uint8_t* __re
     #pragma unroll
                     for (int j = 0; j < FH; j++) {
                         f32x4 hacc = {0.f, 0.f, 0.f, 0.f};
-                        if (splith) {
-                            // the lane's 8 activations are k = 8 * lkx .. +7 of one 16x16x32 step:
-                            // cross terms first, scaled by 2^-11 into the main product's accumulator
-                            f16x8 x0, x1;
+                        // (the split heads run on the 32x32 path above: here the fp32 heads)
     #pragma unroll
-                            for (int i = 0; i < 4; i++) {
-                                _Float16 p0, p1;
-                                split_u(prelu_t<U3>(acc[j][0][i] + cb3[0][i], ca3[0][i]), p0, p1);
-                                x0[i] = p0;
-                                x1[i] = p1;
-                                split_u(prelu_t<U3>(acc[j][1][i] + cb3[1][i], ca3[1][i]), p0, p1);
-                                x0[4 + i] = p0;
-                                x1[4 + i] = p1;
-                            }
-                            hacc = __builtin_amdgcn_mfma_f32_16x16x32_f16(hw0, x1, hacc, 0, 0, 0);
-                            hacc = __builtin_amdgcn_mfma_f32_16x16x32_f16(hw1, x0, hacc, 0, 0, 0);
-                            hacc = hacc * 0.00048828125f;
-                            hacc = __builtin_amdgcn_mfma_f32_16x16x32_f16(hw0, x0, hacc, 0, 0, 0);
-                        } else {
-    #pragma unroll
-                            for (int i = 0; i < 4; i++) {
-                                const float fa = prelu_t<U3>(acc[j][0][i] + cb3[0][i], ca3[0][i]) * 0.00048828125f;
-                                const float fb = prelu_t<U3>(acc[j][1][i] + cb3[1][i], ca3[1][i]) * 0.00048828125f;
-                                hacc = __builtin_amdgcn_mfma_f32_16x16x4f32(hwA[0][i], fa, hacc, 0, 0, 0);
-                                hacc = __builtin_amdgcn_mfma_f32_16x16x4f32(hwA[1][i], fb, hacc, 0, 0, 0);
-                            }
+                        for (int i = 0; i < 4; i++) {
+                            const float fa = prelu_t<U3>(acc[j][0][i] + cb3[0][i], ca3[0][i]) * 0.00048828125f;
+                            const float fb = prelu_t<U3>(acc[j][1][i] + cb3[1][i], ca3[1][i]) * 0.00048828125f;
+                            hacc = __builtin_amdgcn_mfma_f32_16x16x4f32(hwA[0][i], fa, hacc, 0, 0, 0);
+                            hacc = __builtin_amdgcn_mfma_f32_16x16x4f32(hwA[1][i], fb, hacc, 0, 0, 0);
                         }
                         // head biases added here, per lane group (group 0: a0 a1 r0 r1, group 1: r2
                         // r3): the swap below then reads a VALU result -- the compiler's wait-state
@@ -1300,45 +1488,7 @@ __global__ __launch_bounds__(256, PnLds<X>::GPC) void k_pnet(const uint8_t* __re
                     const int y = cell / PT_W, x = cell % PT_W;
                     const int oy = oy0 + y, ox = ox0 + x;
                     const bool valid = (lkx < 2) && (oy < P.ph) && (ox < P.pw);
-                    const float a0 = hq[0][0], a1v = hq[0][1];
-                    const float mx = fmaxf(a0, a1v);
-                    const float e0 = expf(a0 - mx), e1 = expf(a1v - mx);
-                    const float prob = __fdiv_rn(e1, e0 + e1);
-                    const float q0 = hq[0][2], q1 = hq[0][3], q2 = hq[1][0], q3 = hq[1][1];
-                    if (DENSE) {
-                        if (valid) {
-                            int64_t plane = (int64_t)P.ph * P.pw;
-                            int64_t pc = (int64_t)oy * P.pw + ox;
-                            o.prob[(int64_t)b * plane + pc] = prob;
-                            float* rg = o.reg + (int64_t)b * 4 * plane + pc;
-                            rg[0] = q0;
-                            rg[plane] = q1;
-                            rg[2 * plane] = q2;
-                            rg[3 * plane] = q3;
-                        }
-                    } else {
-                        // mask = prob >= 0.6 (mtcnn.py:183; the python scalar compares as fp32)
-                        bool pass = valid && (prob >= 0.6f) && !(o.dbg & 16);
-                        uint64_t bal = __ballot(pass);
-                        if (bal) {
-                            int leader = __builtin_ctzll(bal);
-                            uint32_t base = 0;
-                            if (lane == leader) {
-                                base = atomicAdd(o.count, (uint32_t)__popcll(bal));
-                                atomicAdd(&o.level_count[L], (uint32_t)__popcll(bal));
-                            }
-                            base = __shfl(base, leader);
-                            if (pass) {
-                                uint32_t slot = base + (uint32_t)__popcll(bal & ((1ull << lane) - 1ull));
-                                if (slot < o.cap) {
-                                    uint32_t lin = (uint32_t)(((int64_t)b * P.ph + oy) * P.pw + ox);
-                                    o.key[slot] = ((uint64_t)L << 32) | lin;
-                                    o.score[slot] = prob;
-                                    o.regv[slot] = make_float4(q0, q1, q2, q3);
-                                }
-                            }
-                        }
-                    }
+                    gate(valid, oy, ox, hq[0][0], hq[0][1], hq[0][2], hq[0][3], hq[1][0], hq[1][1]);
                 };
                 if (!(o.dbg & 32)) {
                     if (wg.unit_slopes & 2)
@@ -1414,15 +1564,15 @@ void launch_pnet(bool dense, const uint8_t* frames, int64_t frame_stride, int64_
     const int quota = qe ? std::min(1 << 16, std::max(0, std::atoi(qe))) : 2;
     if (!w.c3h || !w.hh || dense || (xe && std::atoi(xe) == 0)) exact_tiles = 0;
     exact_tiles = std::min(exact_tiles, total_tiles);
+    // (d_tile_ctr: two counters the caller zeroed, one per launch -- no fill kernels here)
     if (exact_tiles > 0) {
-        VTF_HIP(hipMemsetAsync(d_tile_ctr, 0, 4, st));
         int64_t grid = std::min<int64_t>(exact_tiles, (int64_t)cus * wgs("VTF_PNET_X_WG_PER_CU", PnLds<true>::GPC));
         if (quota > 0) grid = std::max<int64_t>(grid, (exact_tiles + (int64_t)quota * chunk - 1) / ((int64_t)quota * chunk));
         k_pnet<false, true><<<(unsigned)grid, 256, 0, st>>>(frames, frame_stride, row_stride, H, W, d_levels, n_levels,
                                                              exact_tiles, d_tile_ctr, w, o, 0, quota, chunk);
     }
     if (exact_tiles >= total_tiles) return;
-    VTF_HIP(hipMemsetAsync(d_tile_ctr, 0, 4, st));
+    d_tile_ctr += 1;
     const int64_t rest = total_tiles - exact_tiles;
     int64_t grid = std::min<int64_t>(rest, (int64_t)cus * wgs("VTF_PNET_WG_PER_CU", PnLds<false>::GPC));
     if (quota > 0) grid = std::max<int64_t>(grid, (rest + (int64_t)quota * chunk - 1) / ((int64_t)quota * chunk));
@@ -1766,9 +1916,13 @@ __global__ void k_gather_refine(const int32_t* __restrict__ idx, int64_t n, cons
                                 const float* __restrict__ sin, const float4* __restrict__ rin,
                                 const int32_t* __restrict__ iin, int refine, int plus_one, int square,
                                 float4* __restrict__ bout, float* __restrict__ sout, float4* __restrict__ rout,
-                                int32_t* __restrict__ iout) {
+                                int32_t* __restrict__ iout, int32_t* __restrict__ zout, int32_t* __restrict__ zw, int nzw) {
     int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    // folded memsets: zout[k] = 0 (the next NMS's call ids), zw[0..nzw) = 0 (stage guards / error
+    // counters) -- one launch instead of a fill kernel each
+    if (k < nzw) zw[k] = 0;
     if (k >= n) return;
+    if (zout) zout[k] = 0;
     int32_t e = idx ? idx[k] : (int32_t)k;
     float4 b = bin[e];
     float4 r = rin ? rin[e] : make_float4(0.f, 0.f, 0.f, 0.f);
@@ -1806,9 +1960,16 @@ __global__ void k_threshold(const float* __restrict__ s, int64_t n, float thr, i
 }
 
 __global__ void k_flag_compact(const int32_t* __restrict__ flag, const int32_t* __restrict__ incl, int64_t n,
-                               int32_t* __restrict__ out) {
+                               int32_t* __restrict__ out, int32_t* __restrict__ mail, const int32_t* __restrict__ ctl,
+                               int nctl) {
     int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (k < n && flag[k]) out[incl[k] - 1] = (int32_t)k;
+    // the count (and the stage's control words) straight to the host mailbox: read after the
+    // stream sync, no blit copy
+    if (mail && k == n - 1) {
+        mail[0] = incl[n - 1];
+        for (int i = 0; i < nctl; i++) mail[1 + i] = ctl[i];
+    }
 }
 
 // landmarks from pre-refine boxes (mtcnn.py:235-239): out [n][5][2]
@@ -1883,16 +2044,18 @@ void launch_decode_stage1(const uint64_t* key_sorted, const int32_t* slot_sorted
 }
 void launch_gather_refine(const int32_t* idx, int64_t n, const float4* bin, const float* sin, const float4* rin,
                           const int32_t* iin, int refine, int plus_one, int square, float4* bout, float* sout,
-                          float4* rout, int32_t* iout, hipStream_t st) {
-    if (n > 0)
-        k_gather_refine<<<cdiv(n, 256), 256, 0, st>>>(idx, n, bin, sin, rin, iin, refine, plus_one, square, bout, sout,
-                                                       rout, iout);
+                          float4* rout, int32_t* iout, hipStream_t st, int32_t* zout, int32_t* zw, int nzw) {
+    VTF_CHECK(nzw >= 0 && nzw <= 256, VTF_E_ARG, "gather_refine: at most 256 zeroed words");
+    if (n > 0 || nzw > 0)
+        k_gather_refine<<<std::max(1, cdiv(n, 256)), 256, 0, st>>>(idx, n, bin, sin, rin, iin, refine, plus_one, square,
+                                                                    bout, sout, rout, iout, zout, zw, nzw);
 }
 void launch_threshold(const float* s, int64_t n, float thr, int32_t* flag, hipStream_t st) {
     if (n > 0) k_threshold<<<cdiv(n, 256), 256, 0, st>>>(s, n, thr, flag);
 }
-void launch_flag_compact(const int32_t* flag, const int32_t* incl, int64_t n, int32_t* out, hipStream_t st) {
-    if (n > 0) k_flag_compact<<<cdiv(n, 256), 256, 0, st>>>(flag, incl, n, out);
+void launch_flag_compact(const int32_t* flag, const int32_t* incl, int64_t n, int32_t* out, hipStream_t st,
+                         int32_t* mail, const int32_t* ctl, int nctl) {
+    if (n > 0) k_flag_compact<<<cdiv(n, 256), 256, 0, st>>>(flag, incl, n, out, mail, ctl, nctl);
 }
 void launch_landmarks(const float4* boxes, const float* lm, int64_t n, float* out, hipStream_t st) {
     if (n > 0) k_landmarks<<<cdiv(n, 256), 256, 0, st>>>(boxes, lm, n, out);

@@ -1,6 +1,7 @@
 // MTCNN detector runtime: weights, pyramid plan, stage orchestration (host side).
 // Mirrors MTCNN.forward (src/videotofaces/detectors/mtcnn.py:167-252) step by step; every
-// data-dependent size is read back once per stage (7 host syncs per det-batch).
+// data-dependent size is read back once per stage (detect(): 1 + 3 NMS + 2 compaction syncs, the
+// final rows left pending for the caller's one sync).
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
@@ -29,14 +30,17 @@ __global__ void k_desc_keys(const float* s, int64_t n, uint64_t* k) {
 // is element order[pos[k]].  One workgroup: a stable counting sort by image (per-image counts,
 // their exclusive scan, then each 1024-row chunk ranks its rows among equal images).
 __global__ __launch_bounds__(1024) void k_mtcnn_rows(const int32_t* __restrict__ order, const int32_t* __restrict__ pos,
-                                                     int nf, const int32_t* __restrict__ img,
+                                                     const int32_t* __restrict__ d_nf, const int32_t* __restrict__ img,
                                                      const float4* __restrict__ box, const float* __restrict__ score,
                                                      const float* __restrict__ lm, int B, float* __restrict__ rows,
-                                                     float* __restrict__ lmo, int32_t* __restrict__ counts) {
+                                                     float* __restrict__ lmo, int32_t* __restrict__ counts,
+                                                     int32_t* __restrict__ mail) {
     __shared__ int s_cnt[4096];
     __shared__ int s_base[4096];
     __shared__ int s_img[1024];
     const int tid = threadIdx.x;
+    const int nf = *d_nf;  // kept rows (the IoM compaction's inclusive count)
+    if (tid == 0) mail[0] = nf;
     for (int b = tid; b < B; b += 1024) s_cnt[b] = 0;
     __syncthreads();
     for (int k = tid; k < nf; k += 1024) atomicAdd(&s_cnt[img[order[pos[k]]]], 1);
@@ -46,6 +50,7 @@ __global__ __launch_bounds__(1024) void k_mtcnn_rows(const int32_t* __restrict__
         for (int b = 0; b < B; b++) {
             s_base[b] = acc;
             counts[b] = s_cnt[b];
+            mail[1 + b] = s_cnt[b];
             acc += s_cnt[b];
             s_cnt[b] = 0;
         }
@@ -119,7 +124,12 @@ struct Mtcnn {
     // weights; 2 split-fp16 guarded: a device flag reports an operand >= 2^14 and the net re-runs
     // in fp32
     int cand_x[2] = {0, 0};
-    int* d_ovf = nullptr;  // [0] conv-layer guard, [1] fused front-half guard
+    // stage control words: [0] conv-layer guard, [1] fused front-half guard, [2] out-of-frame
+    // candidate counter (err), [3] spare; zeroed by the gather launch that opens each stage
+    int* d_ovf = nullptr;
+    // level plan last uploaded to S_LVC (re-uploaded only when it changes)
+    std::vector<PNetLevel> lv_host;
+    const PNetLevel* lv_dev = nullptr;
     // fused RNet / ONet front half (mtcnn_cand.hip); used when the split mode is allowed
     CandFusedW cf[2]{};
     bool fused = false;
@@ -138,8 +148,10 @@ struct Mtcnn {
 enum Slot {
     S_FRAMES = 0, S_LEVELS, S_COUNT, S_KEY, S_SCORE, S_REGV, S_KEY2, S_SLOT, S_SLOT2, S_B1, S_S1, S_R1, S_I1, S_C1,
     S_KEEP, S_B2, S_S2, S_R2, S_I2, S_C2, S_PROB, S_REG, S_LM, S_ERR, S_FLAG, S_INCL, S_IDX, S_LMK, S_OUTB, S_OUTS,
-    S_OUTL, S_OUTI, S_SORT, S_SCAN, S_PRE, S_CROP, S_SAT
+    S_OUTL, S_OUTI, S_SORT, S_SCAN, S_PRE, S_CROP, S_SAT, S_LVC
 };
+// host mailboxes (Arena::mail): stage-1 counts, stage-2/3 compaction results, final rows, box post
+enum MailSlot { M_COUNT = 0, M_STAGE = 1, M_ROWS = 2, M_BOXES = 3 };
 
 // ---- weights: reference state_dict order (specs.py mtcnn_spec) -> transposed device layout
 static void build_weights(Mtcnn& m, const float* params, int64_t n_params) {
@@ -296,7 +308,7 @@ static void build_weights(Mtcnn& m, const float* params, int64_t n_params) {
         const double o1 = bound(29, 32, 27, 1.0), o2 = bound(32, 64, 32 * 9, o1), o3 = bound(35, 64, 64 * 9, o2),
                      o4 = bound(38, 128, 64 * 4, o3);
         m.cand_x[1] = !allow_x ? 0 : (o1 < 16384.0 && o2 < 16384.0 && o3 < 16384.0 && o4 < 16384.0 ? 1 : 2);
-        VTF_HIP(hipMalloc((void**)&m.d_ovf, 8));
+        VTF_HIP(hipMalloc((void**)&m.d_ovf, 16));
         // the fused front half is opt-in (VTF_MTCNN_FUSED=1): correct (tests/test_mtcnn_gpu.py) but
         // measured slower than the layer path on MI355X (ONet 347 vs ~300 ns per candidate chip-wide,
         // RNet 93 vs ~80; profiles/r02b_probe_cand.txt): at 137 KB of LDS one workgroup per CU
@@ -351,8 +363,10 @@ static void build_weights(Mtcnn& m, const float* params, int64_t n_params) {
                             const float w = W[((size_t)co * ci_n + ci) * 9 + tap];
                             const _Float16 w0 = (_Float16)w;
                             const _Float16 w1 = (_Float16)((w - (float)w0) * 2048.f);
-                            std::memcpy(&h[(size_t)co * 144 + tap * 16 + ci], &w0, 2);
-                            std::memcpy(&h[(size_t)(co_n + co) * 144 + tap * 16 + ci], &w1, 2);
+                            // rows >= 16: the tap's channel halves swapped (k_pnet C3_SWZ)
+                            const int cs = co >= 16 ? ci ^ 8 : ci;
+                            std::memcpy(&h[(size_t)co * 144 + tap * 16 + cs], &w0, 2);
+                            std::memcpy(&h[(size_t)(co_n + co) * 144 + tap * 16 + cs], &w1, 2);
                         }
                 uint16_t* d = nullptr;
                 VTF_HIP(hipMalloc((void**)&d, h.size() * 2));
@@ -409,17 +423,20 @@ static void build_weights(Mtcnn& m, const float* params, int64_t n_params) {
             }
             m.pw.c3h = split(raw[6], 32, 16);
             if (bound(6, 32, 144, b2) < 16384.0) {  // conv3 activations feed the split heads
-                std::vector<uint16_t> h(2 * 16 * 32, 0);
+                // [2][32 rows][32 k]: k = 16 s + 8 hk + i holds channel 16 s + 8 (i >> 2) + (i & 3)
+                // + 4 hk -- the conv3 accumulator register 8 s + i of lane half hk (k_pnet's 32x32
+                // conv3); rows 0, 1 conv4_1, 2..5 conv4_2, the rest zero
+                std::vector<uint16_t> h(2 * 32 * 32, 0);
                 for (int r = 0; r < 6; r++)
-                    for (int g = 0; g < 4; g++)
-                        for (int j = 0; j < 8; j++) {
-                            const int ch = j < 4 ? 4 * g + j : 16 + 4 * g + (j - 4);
-                            const float w = r < 2 ? raw[9][r * 32 + ch] : raw[11][(r - 2) * 32 + ch];
-                            const _Float16 w0 = (_Float16)w;
-                            const _Float16 w1 = (_Float16)((w - (float)w0) * 2048.f);
-                            std::memcpy(&h[(size_t)r * 32 + 8 * g + j], &w0, 2);
-                            std::memcpy(&h[(size_t)(16 + r) * 32 + 8 * g + j], &w1, 2);
-                        }
+                    for (int k = 0; k < 32; k++) {
+                        const int s = k >> 4, hk = (k >> 3) & 1, i = k & 7;
+                        const int ch = 16 * s + 8 * (i >> 2) + (i & 3) + 4 * hk;
+                        const float w = r < 2 ? raw[9][r * 32 + ch] : raw[11][(r - 2) * 32 + ch];
+                        const _Float16 w0 = (_Float16)w;
+                        const _Float16 w1 = (_Float16)((w - (float)w0) * 2048.f);
+                        std::memcpy(&h[(size_t)r * 32 + k], &w0, 2);
+                        std::memcpy(&h[(size_t)(32 + r) * 32 + k], &w1, 2);
+                    }
                 uint16_t* d = nullptr;
                 VTF_HIP(hipMalloc((void**)&d, h.size() * 2));
                 VTF_HIP(hipMemcpy(d, h.data(), h.size() * 2, hipMemcpyHostToDevice));
@@ -447,12 +464,12 @@ static void build_weights(Mtcnn& m, const float* params, int64_t n_params) {
         if (m.pw.c3h) {
             VTF_CHECK(m.pw.c2h && m.pw.c1h, VTF_E_LIMIT, "mtcnn: split conv3 without split conv1/conv2 planes");
             uint16_t* comb = nullptr;
-            VTF_HIP(hipMalloc((void**)&comb, 15360 * 2));
-            VTF_HIP(hipMemset(comb, 0, 15360 * 2));
+            VTF_HIP(hipMalloc((void**)&comb, 16384 * 2));
+            VTF_HIP(hipMemset(comb, 0, 16384 * 2));
             VTF_HIP(hipMemcpy(comb, m.pw.c3h, 9216 * 2, hipMemcpyDeviceToDevice));
             VTF_HIP(hipMemcpy(comb + 9216, m.pw.c2h, 3072 * 2, hipMemcpyDeviceToDevice));
             VTF_HIP(hipMemcpy(comb + 12288, m.pw.c1h, 2048 * 2, hipMemcpyDeviceToDevice));
-            if (m.pw.hh) VTF_HIP(hipMemcpy(comb + 14336, m.pw.hh, 1024 * 2, hipMemcpyDeviceToDevice));
+            if (m.pw.hh) VTF_HIP(hipMemcpy(comb + 14336, m.pw.hh, 2048 * 2, hipMemcpyDeviceToDevice));
             m.allocs.push_back((void*)comb);
             m.pw.c3h = comb;
             m.pw.c2h = comb + 9216;
@@ -469,7 +486,7 @@ static void build_weights(Mtcnn& m, const float* params, int64_t n_params) {
 
 // RNet / ONet on NHWC fp32 crops x0 [n,S,S,8] (mtcnn.py:58-76 / 101-121), layer by layer on
 // the MFMA conv kernel; pools are torch MaxPool2d(ceil_mode=True).
-enum RSlot { S_RA = 70, S_RB = 71, S_BOXPOST = 72, S_CLK = 73 };  // nms_multi owns slots 40-61
+enum RSlot { S_RA = 70, S_RB = 71, S_BOXPOST = 72, S_CLK = 73 };  // nms_multi owns slots 40-63
 // first = 1: x0 is the fused front end's pooled conv1 map [n,P,P,32] (k_cand_front)
 static void run_candidates(Mtcnn& m, bool onet, const float* x0, int64_t n, float4* reg, float* lm, float* prob,
                            int first = 0, int force_fp32 = 0) {
@@ -635,8 +652,11 @@ static void run_candidates_sp(Mtcnn& m, bool onet, const void* x0, int64_t n, fl
 // stage 2 / 3 nets on the stage's candidates (mtcnn.py:213-216 / 228-230): the fused front half
 // (crop .. pool2 in LDS, split fp16) + the remaining layers batched; on a fused-guard trip
 // (an operand beyond the fp16 range) or without the split mode, the layer-by-layer path.
+// deferred != null: the caller zeroed d_ovf / err in the stage's opening launch and reads the guard
+// back with its compaction sync (*deferred = true when the guarded split path ran); it then calls
+// cand_rerun_fp32 if the guard tripped.
 static void cand_nets(Mtcnn& m, bool onet, const int4* sat, int H, int W, const float4* boxes, const int32_t* img,
-                      int64_t n, float4* reg, float* lm, float* prob, int32_t* err) {
+                      int64_t n, float4* reg, float* lm, float* prob, int32_t* err, bool* deferred = nullptr) {
     if (n <= 0) return;
     hipStream_t st = m.st;
     const int net = onet ? 1 : 0;
@@ -659,11 +679,15 @@ static void cand_nets(Mtcnn& m, bool onet, const int4* sat, int H, int W, const 
     for (size_t li = 1; li < (onet ? m.ol : m.rl).size(); li++) sp_ok = sp_ok && (onet ? m.ol : m.rl)[li].sp;
     if (sp_ok) {
         // split-pair path: front end writes split pairs, layers on the LDS-DMA conv kernel
-        VTF_HIP(hipMemsetAsync(m.d_ovf, 0, 4, st));
+        if (!deferred) VTF_HIP(hipMemsetAsync(m.d_ovf, 0, 4, st));
         launch_cand_front(onet, sat, H, W, boxes, img, n, m.fw[rl], m.cf[net].w1h, onet ? m.ol[0].b : m.rl[0].b,
                           onet ? m.ol[0].a : m.rl[0].a, x0, err, st, m.d_ovf);
         run_candidates_sp(m, onet, x0, n, reg, lm, prob);
         if (m.cand_x[net] == 1) return;  // operand range proven from the weights
+        if (deferred) {
+            *deferred = true;
+            return;
+        }
         int ovf = 0;
         VTF_HIP(hipMemcpyAsync(&ovf, m.d_ovf, 4, hipMemcpyDeviceToHost, st));
         VTF_HIP(hipStreamSynchronize(st));
@@ -731,33 +755,78 @@ static void d2h_sync(void* dst, const void* src, size_t bytes, hipStream_t st) {
     VTF_HIP(hipStreamSynchronize(st));
 }
 
-// compaction of rows whose score passes `> thr`: returns count, indices in d_idx (order kept)
-static int64_t threshold_compact(Mtcnn& m, const float* d_s, int64_t n, float thr, int32_t* d_idx) {
+// the guarded split path tripped (an operand reached the fp16 range): the stage's nets again on
+// the fp32 path (the error counter recounts out-of-frame candidates)
+static void cand_rerun_fp32(Mtcnn& m, bool onet, const int4* sat, int H, int W, const float4* boxes,
+                            const int32_t* img, int64_t n, float4* reg, float* lm, float* prob, int32_t* err) {
+    hipStream_t st = m.st;
+    const int net = onet ? 1 : 0;
+    const int P = cand_front_side(onet);
+    float* x0 = m.ar.get<float>(S_CROP, (size_t)n * P * P * 32);
+    VTF_HIP(hipMemsetAsync(err, 0, 4, st));
+    launch_cand_front(onet, sat, H, W, boxes, img, n, m.fw[net], nullptr, onet ? m.ol[0].b : m.rl[0].b,
+                      onet ? m.ol[0].a : m.rl[0].a, x0, err, st);
+    run_candidates(m, onet, x0, n, reg, lm, prob, 1, 1);
+}
+
+// compaction of rows whose score passes `> thr`: returns count, indices in d_idx (order kept).
+// The count and the stage's control words (ctl[0] conv guard, [1] fused guard, [2] err) come back
+// through the mailbox in the one sync of the stage.
+static int64_t threshold_compact(Mtcnn& m, const float* d_s, int64_t n, float thr, int32_t* d_idx, int32_t ctl[3]) {
+    ctl[0] = ctl[1] = ctl[2] = 0;
+    if (n <= 0) return 0;
+    Arena::Mail mb = m.ar.mail(M_STAGE, 16);
     int32_t* flag = m.ar.get<int32_t>(S_FLAG, n);
     int32_t* incl = m.ar.get<int32_t>(S_INCL, n);
     launch_threshold(d_s, n, thr, flag, m.st);
     inclusive_scan_i32(m.ar, S_SCAN, flag, incl, n, m.st);
-    launch_flag_compact(flag, incl, n, d_idx, m.st);
-    int32_t cnt = 0;
-    d2h_sync(&cnt, incl + n - 1, 4, m.st);
-    return cnt;
+    launch_flag_compact(flag, incl, n, d_idx, m.st, (int32_t*)mb.d, m.d_ovf, 3);
+    VTF_HIP(hipStreamSynchronize(m.st));
+    const int32_t* h = (const int32_t*)mb.h;
+    ctl[0] = h[1], ctl[1] = h[2], ctl[2] = h[3];
+    return h[0];
+}
+
+__global__ void k_mail_u32(const uint32_t* __restrict__ src, uint32_t* __restrict__ dst, int n) {
+    for (int i = threadIdx.x; i < n; i += blockDim.x) dst[i] = src[i];
 }
 
 // final detections in HBM: rows [n,5] (x1,y1,x2,y2,score) and landmarks [n,10] grouped by image
-// in the reference's order; counts per image (host)
+// in the reference's order.  pending: the last stage's launches are queued, not synced -- the
+// row count and the per-image counts arrive in `mail` ([0] n, [1 + b] count of image b) at the
+// caller's next sync, and d_counts holds the counts in HBM for device consumers (box post).
+// Otherwise (an early exit) n and counts are final on the host.
 struct DetectOut {
     const float* rows = nullptr;
     const float* lms = nullptr;
+    const int32_t* d_counts = nullptr;
+    const int32_t* mail = nullptr;
+    bool pending = false;
     int64_t n = 0;
     std::vector<int32_t> counts;
+    // after the caller's sync: n and counts from the mailbox
+    void settle(Mtcnn& m) {
+        if (!pending) return;
+        pending = false;
+        n = mail[0];
+        for (size_t b = 0; b < counts.size(); b++) counts[b] = mail[1 + b];
+        m.stats[7] = n;
+    }
 };
 
+// MTCNN.forward (mtcnn.py:167-252) for one det-batch.  Host syncs: the stage-1 candidate count,
+// one per batched_nms call (nms_multi), one per stage-2/3 compaction (its count, the stage's
+// guard and error words come back together through a mailbox); the final rows are left pending.
+// Small host->device tables go through pinned mailboxes and memsets are folded into the stage
+// launches, so the det-batch runs no runtime blit copy or fill kernel.
 static void detect(Mtcnn& m, const uint8_t* frames, int on_dev, int B, int H, int W, int64_t fstride,
                    int64_t rstride, double minsize, DetectOut& out) {
     VTF_CHECK(B > 0 && H > 0 && W > 0 && minsize > 0, VTF_E_ARG, "mtcnn: bad shape");
     hipStream_t st = m.st;
     std::memset(m.stats, 0, sizeof(m.stats));
     out.rows = out.lms = nullptr;
+    out.d_counts = out.mail = nullptr;
+    out.pending = false;
     out.n = 0;
     out.counts.assign(B, 0);
     const uint8_t* fr = frames;
@@ -779,13 +848,16 @@ static void detect(Mtcnn& m, const uint8_t* frames, int on_dev, int B, int H, in
     if (NL == 0) return;
     VTF_CHECK(NL < 4096 && cells < (int64_t)1 << 31, VTF_E_LIMIT, "mtcnn: pyramid too large for one call");
     VTF_CHECK(B <= 4096, VTF_E_LIMIT, "mtcnn: at most 4096 frames per call");
+    // counters: [0] candidates, [1..NL] per level, [NL+1], [NL+2] the two PNet launches' tile
+    // counters -- zeroed by the SAT row pass (the first launch of the det-batch)
+    uint32_t* d_cnt = m.ar.get<uint32_t>(S_COUNT, NL + 3);
     // downsampled levels whose adaptive-pool bins exceed 2 frame pixels are resampled by a
     // separate fully parallel kernel (one thread per level value) into HBM; inside the fused
     // tile kernel their long serial bin sums would leave a few workgroups as a long tail.
     // summed-area table of the preprocessed frames: O(1) exact bin sums for the downsampled
     // levels and the stage-2/3 candidate crops
     int4* sat = m.ar.get<int4>(S_SAT, (size_t)B * (H + 1) * (W + 1));
-    launch_sat(fr, fstride, rstride, B, H, W, sat, st);
+    launch_sat(fr, fstride, rstride, B, H, W, sat, st, d_cnt, NL + 3);
     {
         int64_t pre_elems = 0;
         for (auto& L : lv)
@@ -807,10 +879,15 @@ static void detect(Mtcnn& m, const uint8_t* frames, int on_dev, int B, int H, in
         }
         launch_resample_sat_multi(sat, B, H, W, rl, st);
     }
-    PNetLevel* d_lv = m.ar.get<PNetLevel>(S_LEVELS, NL);
-    VTF_HIP(hipMemcpyAsync(d_lv, lv.data(), NL * sizeof(PNetLevel), hipMemcpyHostToDevice, st));
-    uint32_t* d_cnt = m.ar.get<uint32_t>(S_COUNT, NL + 2);
-    VTF_HIP(hipMemsetAsync(d_cnt, 0, (NL + 2) * 4, st));
+    // the level plan (and the precomputed levels' addresses in it) is uploaded only when it
+    // changes: a video's det-batches share one frame size
+    PNetLevel* d_lv = m.ar.get<PNetLevel>(S_LVC, NL);
+    if (m.lv_dev != d_lv || m.lv_host.size() != lv.size() ||
+        std::memcmp(m.lv_host.data(), lv.data(), lv.size() * sizeof(PNetLevel)) != 0) {
+        VTF_HIP(hipMemcpyAsync(d_lv, lv.data(), NL * sizeof(PNetLevel), hipMemcpyHostToDevice, st));
+        m.lv_host = lv;
+        m.lv_dev = d_lv;
+    }
     PNetOut po{};
     po.count = d_cnt;
     po.level_count = d_cnt + 1;
@@ -825,8 +902,10 @@ static void detect(Mtcnn& m, const uint8_t* frames, int on_dev, int B, int H, in
     launch_pnet(false, fr, fstride, rstride, H, W, d_lv, NL, tiles, m.pw, po, d_cnt + NL + 1, st,
                 pnet_exact_tiles(lv, H, W, tiles));
     if (m.prof) VTF_HIP(hipEventRecord(m.ev1, st));
-    std::vector<uint32_t> cnt(NL + 1);
-    d2h_sync(cnt.data(), d_cnt, (NL + 1) * 4, st);
+    Arena::Mail mc = m.ar.mail(M_COUNT, (size_t)(NL + 1) * 4);
+    k_mail_u32<<<1, 256, 0, st>>>(d_cnt, (uint32_t*)mc.d, NL + 1);
+    VTF_HIP(hipStreamSynchronize(st));
+    std::vector<uint32_t> cnt((const uint32_t*)mc.h, (const uint32_t*)mc.h + NL + 1);
     if (po.clk) {  // debug: average workgroup clocks per tile and phase (k_pnet mark() points)
         unsigned long long c[8];
         d2h_sync(c, po.clk, 64, st);
@@ -867,52 +946,60 @@ static void detect(Mtcnn& m, const uint8_t* frames, int on_dev, int B, int H, in
     nms_multi(m.ar, (const float*)b1, s1, i1, c1, calls, B, 0.5, keep, nk, st);
     int64_t k1 = std::accumulate(nk.begin(), nk.end(), (int64_t)0);
     m.stats[2] = k1;
-    // concatenate levels (keep order) -> batched_nms(0.7) (mtcnn.py:203-206)
+    // concatenate levels (keep order) -> batched_nms(0.7) (mtcnn.py:203-206); the gather also
+    // zeroes the single call's ids
     float4* b2 = m.ar.get<float4>(S_B2, k1);
     float* s2 = m.ar.get<float>(S_S2, k1);
     float4* r2 = m.ar.get<float4>(S_R2, k1);
     int32_t* i2 = m.ar.get<int32_t>(S_I2, k1);
     int32_t* c2 = m.ar.get<int32_t>(S_C2, k1);
-    launch_gather_refine(keep, k1, b1, s1, r1, i1, 0, 0, 0, b2, s2, r2, i2, st);
-    VTF_HIP(hipMemsetAsync(c2, 0, k1 * 4, st));
+    launch_gather_refine(keep, k1, b1, s1, r1, i1, 0, 0, 0, b2, s2, r2, i2, st, c2);
     nms_multi(m.ar, (const float*)b2, s2, i2, c2, {k1}, B, 0.7, keep, nk, st);
     int64_t k2 = nk[0];
     m.stats[3] = k2;
-    // refine(plus_one=False) + square (mtcnn.py:207-208) -> stage-2 proposals
-    launch_gather_refine(keep, k2, b2, s2, r2, i2, 1, 0, 1, b1, s1, nullptr, i1, st);
+    if (k2 == 0) return;
+    // refine(plus_one=False) + square (mtcnn.py:207-208) -> stage-2 proposals; the launch zeroes
+    // the stage's guard and error words
+    int32_t* err = m.d_ovf + 2;
+    launch_gather_refine(keep, k2, b2, s2, r2, i2, 1, 0, 1, b1, s1, nullptr, i1, st, nullptr, m.d_ovf, 4);
     // ---------------- stage 2: crop 24x24 + RNet (mtcnn.py:213-222)
     float* prob = m.ar.get<float>(S_PROB, k2);
     float4* reg = m.ar.get<float4>(S_REG, k2);
-    int32_t* err = m.ar.get<int32_t>(S_ERR, 1);
-    VTF_HIP(hipMemsetAsync(err, 0, 4, st));
-    cand_nets(m, false, sat, H, W, b1, i1, k2, reg, nullptr, prob, err);
-    int32_t nerr = 0;
-    d2h_sync(&nerr, err, 4, st);
-    VTF_CHECK(nerr == 0, VTF_E_DEGENERATE,
+    int32_t* idx = m.ar.get<int32_t>(S_IDX, k2);
+    int32_t ctl[3];
+    bool deferred = false;
+    cand_nets(m, false, sat, H, W, b1, i1, k2, reg, nullptr, prob, err, &deferred);
+    int64_t n2 = threshold_compact(m, prob, k2, 0.7f, idx, ctl);
+    if (deferred && ctl[0]) {  // the guarded split path tripped: RNet again in fp32
+        cand_rerun_fp32(m, false, sat, H, W, b1, i1, k2, reg, nullptr, prob, err);
+        n2 = threshold_compact(m, prob, k2, 0.7f, idx, ctl);
+    }
+    VTF_CHECK(ctl[2] == 0, VTF_E_DEGENERATE,
               "stage 2: a candidate box lies outside the frame; the reference skips it in "
               "_get_cropped_candidates (mtcnn.py:159) and then fails indexing (IndexError)");
-    int32_t* idx = m.ar.get<int32_t>(S_IDX, k2);
-    int64_t n2 = threshold_compact(m, prob, k2, 0.7f, idx);
     m.stats[4] = n2;
     if (n2 == 0) return;
-    launch_gather_refine(idx, n2, b1, prob, reg, i1, 0, 0, 0, b2, s2, r2, i2, st);
-    VTF_HIP(hipMemsetAsync(c2, 0, n2 * 4, st));
+    launch_gather_refine(idx, n2, b1, prob, reg, i1, 0, 0, 0, b2, s2, r2, i2, st, c2);
     nms_multi(m.ar, (const float*)b2, s2, i2, c2, {n2}, B, 0.7, keep, nk, st);
     int64_t k3 = nk[0];
     m.stats[5] = k3;
-    launch_gather_refine(keep, k3, b2, s2, r2, i2, 1, 1, 1, b1, s1, nullptr, i1, st);
+    if (k3 == 0) return;
+    launch_gather_refine(keep, k3, b2, s2, r2, i2, 1, 1, 1, b1, s1, nullptr, i1, st, nullptr, m.d_ovf, 4);
     // ---------------- stage 3: crop 48x48 + ONet (mtcnn.py:228-242)
     prob = m.ar.get<float>(S_PROB, k3);
     reg = m.ar.get<float4>(S_REG, k3);
     float* lm = m.ar.get<float>(S_LM, k3 * 10);
-    VTF_HIP(hipMemsetAsync(err, 0, 4, st));
-    cand_nets(m, true, sat, H, W, b1, i1, k3, reg, lm, prob, err);
-    d2h_sync(&nerr, err, 4, st);
-    VTF_CHECK(nerr == 0, VTF_E_DEGENERATE,
+    idx = m.ar.get<int32_t>(S_IDX, k3);
+    deferred = false;
+    cand_nets(m, true, sat, H, W, b1, i1, k3, reg, lm, prob, err, &deferred);
+    int64_t n3 = threshold_compact(m, prob, k3, 0.7f, idx, ctl);
+    if (deferred && ctl[0]) {  // the guarded split path tripped: ONet again in fp32
+        cand_rerun_fp32(m, true, sat, H, W, b1, i1, k3, reg, lm, prob, err);
+        n3 = threshold_compact(m, prob, k3, 0.7f, idx, ctl);
+    }
+    VTF_CHECK(ctl[2] == 0, VTF_E_DEGENERATE,
               "stage 3: a candidate box lies outside the frame; the reference skips it in "
               "_get_cropped_candidates (mtcnn.py:159) and then fails indexing (IndexError)");
-    idx = m.ar.get<int32_t>(S_IDX, k3);
-    int64_t n3 = threshold_compact(m, prob, k3, 0.7f, idx);
     m.stats[6] = n3;
     if (n3 == 0) return;
     launch_gather_refine(idx, n3, b1, prob, reg, i1, 0, 0, 0, b2, s2, r2, i2, st);
@@ -936,19 +1023,19 @@ static void detect(Mtcnn& m, const uint8_t* frames, int on_dev, int B, int H, in
     inclusive_scan_i32(m.ar, S_SCAN, kflag, incl, n3, st);
     int32_t* pos = m.ar.get<int32_t>(S_IDX, n3);
     launch_flag_compact(kflag, incl, n3, pos, st);
-    int32_t nf = 0;
-    d2h_sync(&nf, incl + n3 - 1, 4, st);
-    m.stats[7] = nf;
-    if (nf == 0) return;
-    // final rows grouped by image in IoM keep order (element of keep row k = order[pos[k]])
-    float* rows = m.ar.get<float>(S_OUTB, (size_t)nf * 5);
-    float* lmo = m.ar.get<float>(S_OUTS, (size_t)nf * 10);
+    // final rows grouped by image in IoM keep order (element of keep row k = order[pos[k]]),
+    // sized by the n3 bound; the kept count is read on the device (incl[n3 - 1]) and, with the
+    // per-image counts, reaches the host through the mailbox at the caller's sync
+    float* rows = m.ar.get<float>(S_OUTB, (size_t)n3 * 5);
+    float* lmo = m.ar.get<float>(S_OUTS, (size_t)n3 * 10);
     int32_t* dcnt = m.ar.get<int32_t>(S_OUTI, B);
-    k_mtcnn_rows<<<1, 1024, 0, st>>>(order, pos, nf, i2, b3, s2, lmk, B, rows, lmo, dcnt);
-    d2h_sync(out.counts.data(), dcnt, (size_t)B * 4, st);
+    Arena::Mail mr = m.ar.mail(M_ROWS, (size_t)(B + 1) * 4);
+    k_mtcnn_rows<<<1, 1024, 0, st>>>(order, pos, incl + n3 - 1, i2, b3, s2, lmk, B, rows, lmo, dcnt, (int32_t*)mr.d);
     out.rows = rows;
     out.lms = lmo;
-    out.n = nf;
+    out.d_counts = dcnt;
+    out.mail = (const int32_t*)mr.h;
+    out.pending = true;
 }
 
 }  // namespace vtf
@@ -1021,6 +1108,8 @@ int vtf_mtcnn_detect(vtf_mtcnn_t h, const uint8_t* frames, int frames_on_device,
         VTF_CHECK(h && frames && out_counts, VTF_E_ARG, "null argument");
         DetectOut r;
         detect(h->m, frames, frames_on_device, B, H, W, frame_stride, row_stride, min_face_size, r);
+        if (r.pending) VTF_HIP(hipStreamSynchronize(h->m.st));
+        r.settle(h->m);
         if (out_total) *out_total = r.n;
         VTF_CHECK(r.n <= cap, VTF_E_CAPACITY, "output capacity too small");
         std::copy(r.counts.begin(), r.counts.end(), out_counts);
@@ -1039,9 +1128,26 @@ int vtf_mtcnn_detect_crops(vtf_mtcnn_t h, const uint8_t* frames, int frames_on_d
         VTF_CHECK(h && frames && params && out_n, VTF_E_ARG, "null argument");
         DetectOut r;
         detect(h->m, frames, frames_on_device, B, H, W, frame_stride, row_stride, min_face_size, r);
-        VTF_CHECK(r.n == 0 || d_crops, VTF_E_ARG, "null argument");
-        rows_to_crops(h->m.ar, S_BOXPOST, r.rows, r.counts, H, W, *params, frame_offset, d_crops, nullptr,
-                      out_frame_counts, cap, out_n, h->m.st);
+        if (!r.pending) {  // no rows: the early exits settle on the host
+            rows_to_crops(h->m.ar, S_BOXPOST, r.rows, r.counts, H, W, *params, frame_offset, d_crops, nullptr,
+                          out_frame_counts, cap, out_n, h->m.st);
+            return;
+        }
+        // box post-processing straight on the device rows and counts; its per-frame counts and
+        // total land in a mailbox, read with the detector's rows in one sync.  Crops past `cap`
+        // are counted, not written (the caller retries with the reported size).
+        VTF_CHECK(cap <= 0 || d_crops, VTF_E_ARG, "null argument");
+        Arena::Mail mb = h->m.ar.mail(M_BOXES, ((size_t)B + 1) * 4);
+        int32_t* hb = (int32_t*)mb.h;
+        int32_t* db = (int32_t*)mb.d;
+        launch_box_post(r.rows, r.d_counts, B, H, W, *params, frame_offset, d_crops, nullptr, db, db + B, h->m.st,
+                        std::max<int64_t>(cap, 0));
+        VTF_HIP(hipStreamSynchronize(h->m.st));
+        r.settle(h->m);
+        const int64_t total = hb[B];
+        *out_n = total;
+        VTF_CHECK(total <= cap, VTF_E_CAPACITY, "crop capacity too small (bound: detector rows)");
+        if (out_frame_counts) std::copy(hb, hb + B, out_frame_counts);
     });
 }
 
@@ -1105,6 +1211,7 @@ int vtf_mtcnn_pnet_level(vtf_mtcnn_t h, const uint8_t* d_frames, int B, int H, i
         po.prob = d_prob;
         po.reg = d_reg;
         uint32_t* ctr = h->m.ar.get<uint32_t>(S_COUNT, 4);
+        VTF_HIP(hipMemsetAsync(ctr, 0, 8, h->m.st));
         launch_pnet(true, d_frames, frame_stride, row_stride, H, W, d_lv, 1, (int64_t)B * L.tiles_x * L.tiles_y,
                     h->m.pw, po, ctr, h->m.st);
         VTF_HIP(hipStreamSynchronize(h->m.st));

@@ -25,11 +25,26 @@
 
 namespace vtf {
 
-__global__ void k_call_max(const float4* __restrict__ boxes, const int64_t* __restrict__ call_beg,
-                           const int64_t* __restrict__ call_n, const int32_t* __restrict__ trick_calls,
-                           float* __restrict__ call_max) {
-    int c = trick_calls[blockIdx.x];
-    int64_t beg = call_beg[c], n = call_n[c];
+// nms_multi's first launch.  Block 0 copies the call / segment tables from the host mailbox
+// (pinned, mapped) into device memory for the later kernels and zeroes the coordinate-trick base of
+// every call without one; block 1 + i computes the box maximum of trick call trick[i] (the
+// coordinate-trick offset base, torchvision batched_nms), reading its bounds from the mailbox.
+__global__ void k_nms_prep(const uint8_t* __restrict__ mail, uint8_t* __restrict__ tables, int bytes,
+                           const float4* __restrict__ boxes, size_t o_cbeg, size_t o_cn, size_t o_van, size_t o_trick,
+                           int C, float* __restrict__ call_max, int32_t* __restrict__ ovf_flag) {
+    if (blockIdx.x == 0) {
+        if (threadIdx.x == 0) *ovf_flag = 0;
+        const uint32_t* src = (const uint32_t*)mail;
+        uint32_t* dst = (uint32_t*)tables;
+        for (int i = threadIdx.x; i < bytes / 4; i += blockDim.x) dst[i] = src[i];
+        const int64_t* cn = (const int64_t*)(mail + o_cn);
+        const uint8_t* van = mail + o_van;
+        for (int c = threadIdx.x; c < C; c += blockDim.x)
+            if (van[c] || cn[c] == 0) call_max[c] = 0.f;
+        return;
+    }
+    const int c = ((const int32_t*)(mail + o_trick))[blockIdx.x - 1];
+    const int64_t beg = ((const int64_t*)(mail + o_cbeg))[c], n = ((const int64_t*)(mail + o_cn))[c];
     float m = -INFINITY;
     for (int64_t i = threadIdx.x; i < n; i += blockDim.x) {
         float4 b = boxes[beg + i];
@@ -84,6 +99,86 @@ struct MaskTask {
 };
 constexpr int MASK_CHUNK = 8;  // column blocks per mask task
 
+// mask tasks of a segment of nb row blocks: row block rb takes ceil((nb - rb) / MASK_CHUNK) tasks, so
+// the first rb row blocks take ntasks(nb) - ntasks(nb - rb) (sum_{j=1..n} ceil(j / 8) in closed form)
+__host__ __device__ inline int64_t ntasks(int64_t n) {
+    const int64_t q = n / MASK_CHUNK, r = n % MASK_CHUNK;
+    return (q + 1) * (MASK_CHUNK / 2 * q + r);
+}
+
+// Segment plan on the device (one workgroup): from the sorted segment starts, each segment's
+// count, mask offset (sum of nb^2 * 64 words before it), coordinate-trick base and its mask tasks
+// (rb, column-block chunk) -- what the host used to build after a device->host round trip.  Tasks
+// are enumerated segment by segment, row block by row block (any order is correct: each task
+// writes its own mask words).
+constexpr int PLAN_T = 1024;
+__global__ __launch_bounds__(PLAN_T) void k_nms_plan(const int64_t* __restrict__ sstart, const uint32_t* __restrict__ seg_hi,
+                                                      int sbits, const uint8_t* __restrict__ call_van,
+                                                      const float* __restrict__ call_max, int S, int32_t* __restrict__ scnt,
+                                                      int64_t* __restrict__ moff, float* __restrict__ offb,
+                                                      int64_t* __restrict__ toff, MaskTask* __restrict__ tasks,
+                                                      int32_t* __restrict__ n_tasks, int64_t max_tasks) {
+    __shared__ int64_t w_m[PLAN_T / 64], w_t[PLAN_T / 64];
+    __shared__ int64_t carry_m, carry_t;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    if (tid == 0) carry_m = carry_t = 0;
+    __syncthreads();
+    // pass 1: counts, exclusive prefix sums of mask words and tasks (chunks of PLAN_T segments)
+    for (int s0 = 0; s0 < S; s0 += PLAN_T) {
+        const int s = s0 + tid;
+        int64_t nm = 0, nt = 0;
+        if (s < S) {
+            const int64_t m = sstart[s + 1] - sstart[s];
+            const int64_t nb = (m + 63) >> 6;
+            nm = nb * nb * 64;
+            nt = ntasks(nb);
+            scnt[s] = (int32_t)m;
+            const uint32_t c = seg_hi[s] >> sbits;
+            offb[s] = call_van[c] ? 0.f : call_max[c] + 1.0f;
+        }
+        int64_t im = nm, it = nt;  // inclusive wave scans
+        for (int o = 1; o < 64; o <<= 1) {
+            const int64_t a = __shfl_up(im, o), b = __shfl_up(it, o);
+            if (lane >= o) im += a, it += b;
+        }
+        if (lane == 63) w_m[wave] = im, w_t[wave] = it;
+        __syncthreads();
+        int64_t bm = carry_m, bt = carry_t;
+        for (int w = 0; w < wave; w++) bm += w_m[w], bt += w_t[w];
+        if (s < S) {
+            moff[s] = bm + im - nm;
+            toff[s] = bt + it - nt;
+        }
+        __syncthreads();
+        if (tid == PLAN_T - 1) carry_m = bm + im, carry_t = bt + it;
+        __syncthreads();
+    }
+    const int64_t T = carry_t;
+    if (tid == 0) {
+        toff[S] = T;
+        *n_tasks = (int32_t)min(T, max_tasks);
+    }
+    __syncthreads();
+    // pass 2: every task, by binary search of its segment and row block
+    for (int64_t t = tid; t < min(T, max_tasks); t += PLAN_T) {
+        int lo = 0, hi = S - 1;  // last segment with toff <= t
+        while (lo < hi) {
+            const int mid = (lo + hi + 1) >> 1;
+            if (toff[mid] <= t) lo = mid; else hi = mid - 1;
+        }
+        const int s = lo;
+        const int64_t local = t - toff[s];
+        const int64_t nb = ((int64_t)scnt[s] + 63) >> 6, all = ntasks(nb);
+        int64_t a = 0, b = nb - 1;  // last rb with P(rb) = all - ntasks(nb - rb) <= local
+        while (a < b) {
+            const int64_t mid = (a + b + 1) >> 1;
+            if (all - ntasks(nb - mid) <= local) a = mid; else b = mid - 1;
+        }
+        const int64_t rb = a, c0 = rb + MASK_CHUNK * (local - (all - ntasks(nb - rb)));
+        tasks[t] = MaskTask{s, (int32_t)rb, (int32_t)c0, (int32_t)min(nb, c0 + MASK_CHUNK)};
+    }
+}
+
 __device__ inline float4 load_box(const float4* __restrict__ boxes, const int32_t* __restrict__ img,
                                   int32_t e, float off_base) {
     float4 b = boxes[e];
@@ -103,8 +198,10 @@ __global__ __launch_bounds__(64) void k_iou_mask(const float4* __restrict__ boxe
                                                  const int64_t* __restrict__ seg_beg, const int32_t* __restrict__ seg_n,
                                                  const int64_t* __restrict__ seg_mask_off,
                                                  const float* __restrict__ seg_offbase, double thr,
-                                                 uint64_t* __restrict__ mask) {
-    MaskTask t = tasks[blockIdx.x];
+                                                 uint64_t* __restrict__ mask, const int32_t* __restrict__ n_tasks) {
+  const int T = *n_tasks;  // written by k_nms_plan; the grid is a bound, waves stride over the tasks
+  for (int ti = blockIdx.x; ti < T; ti += gridDim.x) {
+    MaskTask t = tasks[ti];
     const int lane = threadIdx.x;
     const int64_t beg = seg_beg[t.seg];
     const int m = seg_n[t.seg];
@@ -147,6 +244,8 @@ __global__ __launch_bounds__(64) void k_iou_mask(const float4* __restrict__ boxe
         }
         out[(int64_t)cb * 64] = bits;
     }
+    __syncthreads();  // cb_box is rewritten by the next task
+  }
 }
 
 // OR over the 64 lanes with DPP row shifts and row broadcasts (VALU, no LDS crossbar):
@@ -174,7 +273,8 @@ __global__ __launch_bounds__(64 * SCAN_WAVES) void k_nms_scan(const uint64_t* __
                                                               const int64_t* __restrict__ seg_beg,
                                                               const int32_t* __restrict__ seg_n,
                                                               const int64_t* __restrict__ seg_mask_off,
-                                                              uint8_t* __restrict__ keep_sorted) {
+                                                              uint8_t* __restrict__ keep_sorted, int cap_nb,
+                                                              int32_t* __restrict__ ovf_flag) {
     extern __shared__ uint64_t removed[];
     __shared__ uint64_t s_kept;
     const int s = blockIdx.x;
@@ -182,6 +282,10 @@ __global__ __launch_bounds__(64 * SCAN_WAVES) void k_nms_scan(const uint64_t* __
     const int m = seg_n[s];
     if (m == 0) return;
     const int nb = (m + 63) >> 6;
+    if (nb > cap_nb) {  // the LDS bitset holds cap_nb words (uniform exit, flag for the host)
+        if (threadIdx.x == 0) *ovf_flag = 1;
+        return;
+    }
     const uint64_t* msk = mask + seg_mask_off[s];
     const int64_t beg = seg_beg[s];
     for (int w = threadIdx.x; w < nb; w += 64 * SCAN_WAVES) removed[w] = 0;
@@ -272,7 +376,7 @@ __global__ void k_call_kept(const int64_t* __restrict__ call_start, const int32_
     int64_t b = call_start[c], e = call_start[c + 1];
     int32_t lo = b > 0 ? incl[b - 1] : 0;
     int32_t hi = e > 0 ? incl[e - 1] : 0;
-    out[c] = hi - lo;
+    out[c] = hi - lo;  // (out: the host mailbox)
 }
 
 // host staging of several small tables for one H2D copy (16-B aligned members)
@@ -319,7 +423,7 @@ void inclusive_scan_i32(Arena& ar, int slot, const int32_t* in, int32_t* out, in
     VTF_HIP(rocprim::inclusive_scan(t, tmp, in, out, (size_t)n, rocprim::plus<int32_t>(), st));
 }
 
-// Arena slots used here: 40..59
+// Arena slots used here: 40..63 (device), mailboxes 40, 41
 void nms_multi(Arena& ar, const float* d_boxes, const float* d_scores, const int32_t* d_img,
                const int32_t* d_elem_call, const std::vector<int64_t>& call_n, int n_img, double thr,
                int32_t* d_keep, std::vector<int64_t>& nkeep, hipStream_t st) {
@@ -345,12 +449,12 @@ void nms_multi(Arena& ar, const float* d_boxes, const float* d_scores, const int
     if (N == 0) return;
     VTF_CHECK(N < (int64_t)1 << 31, VTF_E_LIMIT, "nms_multi: too many boxes");
 
-    // small host->device tables, packed into one transfer (each hipMemcpyAsync from pageable
-    // memory is a staged copy + blit kernel: ~4.5 us apiece on the lane's stream)
+    // small host tables (calls, segments) in the handle's pinned mailbox: k_nms_prep copies them
+    // to device memory in the same launch that computes the coordinate-trick bases, so there is no
+    // runtime blit copy and no memset
     int sbits = 0, cbits = 0;
     while ((1 << sbits) < n_img) sbits++;
     while ((1 << cbits) < C) cbits++;
-    const int end_bit = 32 + sbits + cbits;
     std::vector<uint32_t> seg_hi(S), call_hi(C);
     for (int c = 0; c < C; c++) {
         call_hi[c] = (uint32_t)c << sbits;
@@ -361,24 +465,23 @@ void nms_multi(Arena& ar, const float* d_boxes, const float* d_scores, const int
     const size_t o_van = pk.add(vanilla.data(), C), o_sbase = pk.add(seg_base.data(), (C + 1) * 4);
     const size_t o_trick = pk.add(trick.data(), trick.size() * 4), o_seghi = pk.add(seg_hi.data(), S * 4);
     const size_t o_callhi = pk.add(call_hi.data(), C * 4);
-    uint8_t* d_t1 = (uint8_t*)ar.get(40, pk.buf.size());
-    VTF_HIP(hipMemcpyAsync(d_t1, pk.buf.data(), pk.buf.size(), hipMemcpyHostToDevice, st));
+    (void)o_sbase;
+    const int tbytes = (int)((pk.buf.size() + 3) & ~(size_t)3);
+    Arena::Mail mt = ar.mail(40, tbytes);
+    std::memcpy(mt.h, pk.buf.data(), pk.buf.size());
+    // results mailbox: kept count per call, then the scan's overflow flag (zeroed by k_nms_prep)
+    Arena::Mail mr = ar.mail(41, (size_t)(C + 1) * 4);
+    uint8_t* d_t1 = (uint8_t*)ar.get(40, tbytes);
     const int64_t* d_cbeg = (const int64_t*)(d_t1 + o_cbeg);
-    const int64_t* d_cn = (const int64_t*)(d_t1 + o_cn);
     const uint8_t* d_van = d_t1 + o_van;
     const uint32_t* d_seghi = (const uint32_t*)(d_t1 + o_seghi);
     const uint32_t* d_callhi = (const uint32_t*)(d_t1 + o_callhi);
-    (void)o_sbase;
-
-    // device -> host results of phase 1 share one buffer: segment starts, then call maxima
-    uint8_t* d_r1 = (uint8_t*)ar.get(52, (size_t)(S + 1) * 8 + (size_t)C * 4);
-    int64_t* d_sstart = (int64_t*)d_r1;
-    float* d_cmax = (float*)(d_r1 + (size_t)(S + 1) * 8);
-    // per-segment coordinate-trick offset base (max + 1), 0 for vanilla segments
-    VTF_HIP(hipMemsetAsync(d_cmax, 0, C * 4, st));
-    if (!trick.empty())
-        k_call_max<<<(int)trick.size(), 256, 0, st>>>((const float4*)d_boxes, d_cbeg, d_cn,
-                                                       (const int32_t*)(d_t1 + o_trick), d_cmax);
+    (void)d_cbeg;
+    float* d_cmax = ar.get<float>(52, C);
+    int32_t* h_res = (int32_t*)mr.h;
+    int32_t* d_res = (int32_t*)mr.d;
+    k_nms_prep<<<1 + (int)trick.size(), 256, 0, st>>>((const uint8_t*)mt.d, d_t1, tbytes, (const float4*)d_boxes, o_cbeg,
+                                                      o_cn, o_van, o_trick, C, d_cmax, d_res + C);
 
     // sort 1: (call, segment image, score desc), stable over position order
     uint64_t* k0 = ar.get<uint64_t>(46, N);
@@ -387,55 +490,41 @@ void nms_multi(Arena& ar, const float* d_boxes, const float* d_scores, const int
     int32_t* ord = ar.get<int32_t>(49, N);
     k_seg_keys<<<cdiv(N, 256), 256, 0, st>>>(d_scores, d_img, d_elem_call, d_van, N, 1, sbits, k0, v0);
     merge_pairs_u64(ar, 50, k0, k1, v0, ord, N, st);
-    (void)end_bit;
     // segment bounds by binary search on the sorted keys
+    int64_t* d_sstart = ar.get<int64_t>(51, (size_t)S + 1);
     k_seg_bounds<<<cdiv(S + 1, 256), 256, 0, st>>>(k1, N, d_seghi, S, d_sstart);
-    std::vector<uint8_t> r1((size_t)(S + 1) * 8 + (size_t)C * 4);
-    VTF_HIP(hipMemcpyAsync(r1.data(), d_r1, r1.size(), hipMemcpyDeviceToHost, st));
-    VTF_HIP(hipStreamSynchronize(st));
-    const int64_t* sstart = (const int64_t*)r1.data();
-    const float* cmax = (const float*)(r1.data() + (size_t)(S + 1) * 8);
-    std::vector<int32_t> scnt(S);
-    for (int s2 = 0; s2 < S; s2++) scnt[s2] = (int32_t)(sstart[s2 + 1] - sstart[s2]);
 
-    // segment tables, mask offsets, row-block tasks
-    std::vector<int64_t> sbeg(S), moff(S);
-    std::vector<float> offb(S, 0.f);
-    std::vector<MaskTask> tasks;
-    int64_t pos = 0, mtot = 0;
-    int maxnb = 0;
+    // segment plan + mask tasks on the device (k_nms_plan); the host only sizes buffers and grids
+    // from bounds over the calls' counts: a segment of call c has at most call_n[c] boxes, and
+    // sum_s nb_s <= call_n / 64 + (segments holding a box)
+    int64_t mwords = 0, tbound = 0, nbmax = 0;
     for (int c = 0; c < C; c++) {
-        for (int s = seg_base[c]; s < seg_base[c + 1]; s++) {
-            sbeg[s] = pos;
-            moff[s] = mtot;
-            int m = scnt[s];
-            int nb = (m + 63) / 64;
-            maxnb = std::max(maxnb, nb);
-            if (!vanilla[c]) offb[s] = cmax[c] + 1.0f;
-            for (int rb = 0; rb < nb; rb++)
-                for (int c0 = rb; c0 < nb; c0 += MASK_CHUNK) tasks.push_back({s, rb, c0, std::min(nb, c0 + MASK_CHUNK)});
-            pos += m;
-            mtot += (int64_t)nb * nb * 64;
-        }
+        const int64_t n = call_n[c];
+        if (n == 0) continue;
+        const int64_t nseg = seg_base[c + 1] - seg_base[c];
+        const int64_t nbc = (n + 63) / 64, nbsum = n / 64 + std::min(nseg, n);
+        nbmax = std::max(nbmax, nbc);
+        mwords += nbc * nbsum * 64;          // sum nb_s^2 <= max nb * sum nb
+        tbound += nbc * nbsum / 8 + 2 * nbsum + 1;  // ntasks(n) <= n^2 / 8 + 2 n
     }
-    VTF_CHECK(maxnb * 8 <= 160 * 1024, VTF_E_LIMIT, "nms_multi: a segment exceeds 1.3M boxes");
-    HostPack pk2;
-    const size_t o_sbeg = pk2.add(sbeg.data(), S * 8), o_moff = pk2.add(moff.data(), S * 8);
-    const size_t o_scnt = pk2.add(scnt.data(), S * 4), o_offb = pk2.add(offb.data(), S * 4);
-    const size_t o_tasks = pk2.add(tasks.data(), tasks.size() * sizeof(MaskTask));
-    uint8_t* d_t2 = (uint8_t*)ar.get(53, pk2.buf.size());
-    VTF_HIP(hipMemcpyAsync(d_t2, pk2.buf.data(), pk2.buf.size(), hipMemcpyHostToDevice, st));
-    const int64_t* d_sbeg = (const int64_t*)(d_t2 + o_sbeg);
-    const int64_t* d_moff = (const int64_t*)(d_t2 + o_moff);
-    const int32_t* d_scnt = (const int32_t*)(d_t2 + o_scnt);
-    const float* d_offb = (const float*)(d_t2 + o_offb);
-    const MaskTask* d_tasks = (const MaskTask*)(d_t2 + o_tasks);
-    uint64_t* d_mask = ar.get<uint64_t>(56, mtot);
-    if (!tasks.empty())
-        k_iou_mask<<<(int)tasks.size(), 64, 0, st>>>((const float4*)d_boxes, d_img, ord, d_tasks, d_sbeg, d_scnt,
-                                                      d_moff, d_offb, thr, d_mask);
+    int32_t* d_scnt = ar.get<int32_t>(53, S);
+    int64_t* d_moff = ar.get<int64_t>(54, S);
+    float* d_offb = ar.get<float>(55, S);
+    int64_t* d_toff = ar.get<int64_t>(60, (size_t)S + 1);
+    MaskTask* d_tasks = ar.get<MaskTask>(62, tbound);
+    int32_t* d_ntask = ar.get<int32_t>(63, 1);
+    k_nms_plan<<<1, PLAN_T, 0, st>>>(d_sstart, d_seghi, sbits, d_van, d_cmax, S, d_scnt, d_moff, d_offb, d_toff,
+                                     d_tasks, d_ntask, tbound);
+    uint64_t* d_mask = ar.get<uint64_t>(56, mwords);
+    // one wave per task, striding: ~32 waves per CU bound the grid (most tasks cover 8 x 64 x 64 IoUs)
+    k_iou_mask<<<(int)std::max<int64_t>(1, std::min<int64_t>(tbound, 8192)), 64, 0, st>>>(
+        (const float4*)d_boxes, d_img, ord, d_tasks, d_sstart, d_scnt, d_moff, d_offb, thr, d_mask, d_ntask);
     uint8_t* keep_sorted = ar.get<uint8_t>(57, N);
-    k_nms_scan<<<S, 64 * SCAN_WAVES, maxnb * 8, st>>>(d_mask, d_sbeg, d_scnt, d_moff, keep_sorted);
+    // LDS bitset sized by the largest segment possible (one whole call); a segment beyond the LDS
+    // limit raises the mailbox flag instead of overflowing
+    const int cap_nb = (int)std::min<int64_t>(nbmax, 160 * 1024 / 8);
+    k_nms_scan<<<S, 64 * SCAN_WAVES, (size_t)cap_nb * 8, st>>>(d_mask, d_sstart, d_scnt, d_moff, keep_sorted, cap_nb,
+                                                               d_res + C);
     uint8_t* keep_elem = ar.get<uint8_t>(58, N);
     k_scatter_flags<<<cdiv(N, 256), 256, 0, st>>>(ord, keep_sorted, N, keep_elem);
 
@@ -448,12 +537,10 @@ void nms_multi(Arena& ar, const float* d_boxes, const float* d_scores, const int
     inclusive_scan_i32(ar, 59, flag, incl, N, st);
     k_compact<<<cdiv(N, 256), 256, 0, st>>>(ord, flag, incl, N, d_keep);
     k_seg_bounds<<<cdiv(C + 1, 256), 256, 0, st>>>(k1, N, d_callhi, C, d_sstart);
-    int32_t* d_ckept = ar.get<int32_t>(61, C);
-    k_call_kept<<<cdiv(C, 256), 256, 0, st>>>(d_sstart, incl, C, d_ckept);
-    std::vector<int32_t> ck(C);
-    VTF_HIP(hipMemcpyAsync(ck.data(), d_ckept, C * 4, hipMemcpyDeviceToHost, st));
+    k_call_kept<<<cdiv(C, 256), 256, 0, st>>>(d_sstart, incl, C, d_res);
     VTF_HIP(hipStreamSynchronize(st));
-    for (int c = 0; c < C; c++) nkeep[c] = ck[c];
+    VTF_CHECK(h_res[C] == 0, VTF_E_LIMIT, "nms_multi: a segment exceeds 1.3M boxes");
+    for (int c = 0; c < C; c++) nkeep[c] = h_res[c];
 }
 
 }  // namespace vtf
