@@ -1573,15 +1573,17 @@ void launch_pnet(bool dense, const uint8_t* frames, int64_t frame_stride, int64_
     }
     if (exact_tiles >= total_tiles) return;
     d_tile_ctr += 1;
+    PNetOut og = o;  // (phase clocks of the general launch in words 8..15)
+    if (og.clk && exact_tiles > 0) og.clk += 8;
     const int64_t rest = total_tiles - exact_tiles;
     int64_t grid = std::min<int64_t>(rest, (int64_t)cus * wgs("VTF_PNET_WG_PER_CU", PnLds<false>::GPC));
     if (quota > 0) grid = std::max<int64_t>(grid, (rest + (int64_t)quota * chunk - 1) / ((int64_t)quota * chunk));
     if (dense)
         k_pnet<true, false><<<(unsigned)grid, 256, 0, st>>>(frames, frame_stride, row_stride, H, W, d_levels, n_levels,
-                                                             total_tiles, d_tile_ctr, w, o, exact_tiles, quota, chunk);
+                                                             total_tiles, d_tile_ctr, w, og, exact_tiles, quota, chunk);
     else
         k_pnet<false, false><<<(unsigned)grid, 256, 0, st>>>(frames, frame_stride, row_stride, H, W, d_levels, n_levels,
-                                                              total_tiles, d_tile_ctr, w, o, exact_tiles, quota, chunk);
+                                                              total_tiles, d_tile_ctr, w, og, exact_tiles, quota, chunk);
 }
 
 // ----------------------------------------------------------------------------------- RNet / ONet

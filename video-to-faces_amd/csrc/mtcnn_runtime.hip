@@ -896,23 +896,33 @@ static void detect(Mtcnn& m, const uint8_t* frames, int on_dev, int B, int H, in
     po.score = m.ar.get<float>(S_SCORE, cells);
     po.regv = m.ar.get<float4>(S_REGV, cells);
     if (const char* e = getenv("VTF_PNET_DEBUG")) po.dbg = atoi(e);
-    if (po.dbg & 256) po.clk = m.ar.get<unsigned long long>(S_CLK, 8);
-    if (po.clk) VTF_HIP(hipMemsetAsync(po.clk, 0, 64, st));
+    // (phase clocks: [0, 8) the exact-levels launch, [8, 16) the general one)
+    if (po.dbg & 256) po.clk = m.ar.get<unsigned long long>(S_CLK, 16);
+    if (po.clk) VTF_HIP(hipMemsetAsync(po.clk, 0, 128, st));
+    const int64_t x_tiles = pnet_exact_tiles(lv, H, W, tiles);
     if (m.prof) VTF_HIP(hipEventRecord(m.ev0, st));
     launch_pnet(false, fr, fstride, rstride, H, W, d_lv, NL, tiles, m.pw, po, d_cnt + NL + 1, st,
-                pnet_exact_tiles(lv, H, W, tiles));
+                x_tiles);
     if (m.prof) VTF_HIP(hipEventRecord(m.ev1, st));
     Arena::Mail mc = m.ar.mail(M_COUNT, (size_t)(NL + 1) * 4);
     k_mail_u32<<<1, 256, 0, st>>>(d_cnt, (uint32_t*)mc.d, NL + 1);
     VTF_HIP(hipStreamSynchronize(st));
     std::vector<uint32_t> cnt((const uint32_t*)mc.h, (const uint32_t*)mc.h + NL + 1);
     if (po.clk) {  // debug: average workgroup clocks per tile and phase (k_pnet mark() points)
-        unsigned long long c[8];
-        d2h_sync(c, po.clk, 64, st);
+        unsigned long long c[16];
+        d2h_sync(c, po.clk, 128, st);
         static const char* nm[7] = {"tail", "head", "stage", "fill", "conv1", "conv2", "conv3+heads"};
         fprintf(stderr, "k_pnet phase clocks per tile (%lld tiles):", (long long)tiles);
-        for (int k = 0; k < 7; k++) fprintf(stderr, " %s %.0f", nm[k], (double)c[k] / (double)tiles);
+        for (int k = 0; k < 7; k++) fprintf(stderr, " %s %.0f", nm[k], (double)(c[k] + c[8 + k]) / (double)tiles);
         fprintf(stderr, "\n");
+        const int64_t xt = std::min(x_tiles, tiles), gt = tiles - xt;
+        for (int v = 0; v < 2; v++) {
+            const int64_t nt = v ? gt : xt;
+            if (nt <= 0) continue;
+            fprintf(stderr, "  %s variant (%lld tiles):", v ? "general" : "exact-levels", (long long)nt);
+            for (int k = 0; k < 7; k++) fprintf(stderr, " %s %.0f", nm[k], (double)c[8 * v + k] / (double)nt);
+            fprintf(stderr, "\n");
+        }
     }
     if (m.prof) {
         float ms = 0.f;
