@@ -59,6 +59,13 @@ constexpr int PH_C2H = 9216, PH_C1H = 12288, PH_HH = 14336;  // halves (conv3 pl
 
 // ----------------------------------------------------------------------------------- resample
 
+// fp16 split of an fp32 value: v = x0 + x1 * 2^-11 to ~2^-24 relative (x0 = fp16(v), the
+// residual v - x0 exact in fp32), the operand form of k_pnet's fp16 matrix-core convolutions
+__device__ inline void split_f16(float v, _Float16& x0, _Float16& x1) {
+    x0 = (_Float16)v;
+    x1 = (_Float16)((v - (float)x0) * 2048.f);
+}
+
 // row pass: block per frame row
 __global__ __launch_bounds__(256) void k_sat_rows(const uint8_t* __restrict__ frames, int64_t frame_stride,
                                                   int64_t row_stride, int H, int W, int4* __restrict__ sat,
@@ -214,6 +221,16 @@ __global__ void k_resample_sat_multi(const int4* __restrict__ sat, int B, int H,
     const int y0 = (int)(((int64_t)ly * H) / lh), y1 = (int)(((int64_t)(ly + 1) * H + lh - 1) / lh);
     const int x0 = (int)(((int64_t)lx * W) / lw), x1 = (int)(((int64_t)(lx + 1) * W + lw - 1) / lw);
     const int4 s = sat_box(sat + (int64_t)b * (H + 1) * (W + 1), W + 1, y0, y1, x0, x1);
+    if (lv.split) {  // fp16 split pixels [B][lh][lw] x (x0 RGB0 | x1 RGB0), k_pnet's level-tile form
+        typedef __attribute__((ext_vector_type(8))) _Float16 h8;
+        _Float16 r0, r1, g0, g1, b0, b1;
+        split_f16(bin_avg(s.x, y1 - y0, x1 - x0), r0, r1);
+        split_f16(bin_avg(s.y, y1 - y0, x1 - x0), g0, g1);
+        split_f16(bin_avg(s.z, y1 - y0, x1 - x0), b0, b1);
+        const _Float16 z = (_Float16)0.f;
+        ((h8*)lv.out[l])[j] = h8{r0, g0, b0, z, r1, g1, b1, z};
+        return;
+    }
     const int64_t plane = (int64_t)lh * lw, o = (int64_t)b * 3 * plane + (int64_t)ly * lw + lx;
     float* out = lv.out[l];
     out[o] = bin_avg(s.x, y1 - y0, x1 - x0);
@@ -264,14 +281,20 @@ __device__ inline float div_bin(float x, int k) {
     return (k & (k - 1)) == 0 ? x * __int_as_float((127 - __builtin_ctz(k)) << 23) : __fdiv_rn(x, (float)k);
 }
 
+// x / k for the bin averages of the downsampled levels: for k <= 3 the fma-corrected reciprocal
+// q + (x - q k) y (y = RN(1/k), q = RN(x y)) equals the correctly rounded division on every
+// x = s 2^-8 (|s| <= 2295, a bin of at most 9 pixels) and on every such quotient divided again
+// (exhaustive check over 55k cases): 3 instructions instead of the ~10 of the IEEE
+// division; larger k take the division
+__device__ inline float div_small(float x, int k) {
+    if (k > 3) return __fdiv_rn(x, (float)k);
+    const float y = k == 3 ? __int_as_float(0x3eaaaaab) : (k == 2 ? 0.5f : 1.0f);
+    const float q = x * y;
+    return fmaf(fmaf(-q, (float)k, x), y, q);
+}
+
 // workgroups per CU from the LDS footprint (160 KB per CU)
 constexpr int PNET_LDS = (P_A + P_POOL) * 4 + (PL_H + PL_W) * 4 + 16;
-// fp16 split of an fp32 value: v = x0 + x1 * 2^-11 to ~2^-24 relative (x0 = fp16(v), the
-// residual v - x0 exact in fp32), the operand form of k_pnet's fp16 matrix-core convolutions
-__device__ inline void split_f16(float v, _Float16& x0, _Float16& x1) {
-    x0 = (_Float16)v;
-    x1 = (_Float16)((v - (float)x0) * 2048.f);
-}
 
 // the same split from u = 2048 v (the epilogues carry their values 2048-scaled, which is exact:
 // 2048 round(c + d 2^-11) = round(2048 c + d) is one fma, and bias / PReLU commute with the
@@ -527,13 +550,51 @@ __global__ __launch_bounds__(256, PnLds<X>::GPC) void k_pnet(const uint8_t* __re
             const uint8_t* src = fr + (int64_t)fy0 * row_stride + fx0 * 3;
             const __amdgpu_buffer_rsrc_t rs_src = __builtin_amdgcn_make_buffer_rsrc(
                 (void*)src, 0, (int)((fy1 - fy0 - 1) * (int)row_stride + pw3), 0x00020000);
-            for (int i0 = 8 * tid + (pf_done ? 256 * 8 : 0); i0 < nbytes; i0 += 256 * 8)
-                *(uint2*)(patch + i0) = patch_bytes8(rs_src, i0, pw3, (int)row_stride);
+            // four 2 KB rounds in flight per trip (the loads of a round no longer wait for the
+            // previous round's stores: the downsampled levels' 7-14 KB patches were latency-bound)
+            for (int i0 = 8 * tid + (pf_done ? 256 * 8 : 0); i0 < nbytes; i0 += 4 * 256 * 8) {
+                uint2 pv[4];
+#pragma unroll
+                for (int u = 0; u < 4; u++)
+                    pv[u] = i0 + u * 2048 < nbytes ? patch_bytes8(rs_src, i0 + u * 2048, pw3, (int)row_stride)
+                                                   : make_uint2(0u, 0u);
+#pragma unroll
+                for (int u = 0; u < 4; u++)
+                    if (i0 + u * 2048 < nbytes) *(uint2*)(patch + i0 + u * 2048) = pv[u];
+            }
         }
         __syncthreads();
         mark(2);  // 2: frame patch staging
-        if (!X && P.pre) {
-            // large-bin level precomputed by k_resample_sat (bit-identical values)
+        if (!X && P.pre && P.pad == 1) {
+            // downsampled level precomputed by k_resample_sat_multi as fp16 split pixels (16 B:
+            // x0 RGB0 | x1 RGB0, bit-identical to store_level's split of the bin average): the fill
+            // is one 16-byte load and two 8-byte LDS stores per level pixel, all loads in flight
+            typedef __attribute__((ext_vector_type(2))) uint32_t u32x2;
+            const uint4* pre4 = (const uint4*)P.pre + (int64_t)b * P.lh * P.lw;
+            u32x2* lvl = (u32x2*)sA;
+            int tl = tid;
+            asm volatile("" : "+v"(tl));
+            const int fq = tl % PL_W, fr0 = tl < 6 * PL_W ? tl / PL_W : PL_H;
+            const int lx = 2 * ox0 + fq;
+            const bool inx = lx < P.lw;
+            const int64_t cx = min(lx, P.lw - 1);
+            uint4 v[7];
+#pragma unroll
+            for (int j = 0; j < 7; j++) {
+                const int r = min(fr0 + 6 * j, PL_H - 1), ly = 2 * oy0 + r;
+                const uint4 t = pre4[(int64_t)min(ly, P.lh - 1) * P.lw + cx];
+                v[j] = inx && ly < P.lh ? t : make_uint4(0u, 0u, 0u, 0u);
+            }
+#pragma unroll
+            for (int j = 0; j < 7; j++) {
+                const int r = fr0 + 6 * j;
+                if (r < PL_H) {
+                    lvl[r * PL_W + fq] = u32x2{v[j].x, v[j].y};
+                    lvl[PL_H * PL_W + r * PL_W + fq] = u32x2{v[j].z, v[j].w};
+                }
+            }
+        } else if (!X && P.pre) {
+            // large-bin level precomputed by k_resample_sat (fp32 planes; bit-identical values)
             const float* pre = P.pre + (int64_t)b * 3 * P.lh * P.lw;
             const int64_t pl = (int64_t)P.lh * P.lw;
             for (int i0 = tid; i0 < ((o.dbg & 1) ? 0 : PL_H * PL_W); i0 += 256 * 4) {
@@ -614,36 +675,46 @@ __global__ __launch_bounds__(256, PnLds<X>::GPC) void k_pnet(const uint8_t* __re
                 lvl[r * PL_W + fq] = h4{(_Float16)r0, (_Float16)g0, (_Float16)b0, (_Float16)0.f};
             }
         } else if (!X && sep) {
+            // downsampled levels (bins of 1-3 frame pixels per side: lh >= H / 2, the rest are
+            // precomputed): the exact fill's 2-D thread map (column fq of every 6th row, the
+            // column's bin decoded once) and the bin divisions by the fma-corrected reciprocal
+            // (div_small: bit-identical to the correctly rounded division on this domain)
             int16_t* hs = (int16_t*)(patch + hs_off);
-            for (int i = tid; i < nrows * PL_W; i += 256) {
-                const int r = i / PL_W, q = i - r * PL_W;
-                const int xs = xbin[q].x, n = xbin[q].y - xs;
-                const uint8_t* row = patch + r * pw3 + (xs - fx0) * 3;
-                int a0 = 0, a1 = 0, a2 = 0;
-                for (int x = 0; x < n; x++) {
-                    a0 += row[3 * x + 2];
-                    a1 += row[3 * x + 1];
-                    a2 += row[3 * x];
+            int tl = tid;
+            asm volatile("" : "+v"(tl));
+            const int fq = tl % PL_W, fr0 = tl < 6 * PL_W ? tl / PL_W : PL_H;
+            const ushort2 xbq = xbin[fq];
+            const int nq = xbq.y - xbq.x;
+            {
+                const uint8_t* col = patch + (nq ? (xbq.x - fx0) * 3 : 0);
+                for (int r = fr0; r < nrows; r += 6) {
+                    const uint8_t* row = col + r * pw3;
+                    int a0 = 0, a1 = 0, a2 = 0;
+                    for (int x = 0; x < nq; x++) {
+                        a0 += row[3 * x + 2];
+                        a1 += row[3 * x + 1];
+                        a2 += row[3 * x];
+                    }
+                    int16_t* o = hs + 3 * (r * PL_W + fq);
+                    o[0] = (int16_t)(2 * a0 - 255 * nq);
+                    o[1] = (int16_t)(2 * a1 - 255 * nq);
+                    o[2] = (int16_t)(2 * a2 - 255 * nq);
                 }
-                hs[3 * i] = (int16_t)(2 * a0 - 255 * n);
-                hs[3 * i + 1] = (int16_t)(2 * a1 - 255 * n);
-                hs[3 * i + 2] = (int16_t)(2 * a2 - 255 * n);
             }
             __syncthreads();
-            for (int i = tid; i < PL_H * PL_W; i += 256) {
-                const int r = i / PL_W, q = i - r * PL_W;
-                const int ys = ybin[r].x, kh = ybin[r].y - ys, kw = xbin[q].y - xbin[q].x;
-                const int16_t* h = hs + ((ys - fy0) * PL_W + q) * 3;
+            for (int r = fr0; r < PL_H; r += 6) {
+                const int ys = ybin[r].x, kh = ybin[r].y - ys;
+                const int16_t* h = hs + ((kh ? ys - fy0 : 0) * PL_W + fq) * 3;
                 int s0 = 0, s1 = 0, s2 = 0;
                 for (int y = 0; y < kh; y++) {
                     s0 += h[y * PL_W * 3];
                     s1 += h[y * PL_W * 3 + 1];
                     s2 += h[y * PL_W * 3 + 2];
                 }
-                const bool in = kh > 0 && kw > 0;
-                store_level(sA, split3, i, in ? div_bin(div_bin((float)s0 * 0.00390625f, kh), kw) : 0.f,
-                            in ? div_bin(div_bin((float)s1 * 0.00390625f, kh), kw) : 0.f,
-                            in ? div_bin(div_bin((float)s2 * 0.00390625f, kh), kw) : 0.f);
+                const bool in = kh > 0 && nq > 0;
+                store_level(sA, split3, r * PL_W + fq, in ? div_small(div_small((float)s0 * 0.00390625f, kh), nq) : 0.f,
+                            in ? div_small(div_small((float)s1 * 0.00390625f, kh), nq) : 0.f,
+                            in ? div_small(div_small((float)s2 * 0.00390625f, kh), nq) : 0.f);
             }
         }
         for (int i = tid; i < (X || (o.dbg & 1) || P.pre || sep ? 0 : PL_H * PL_W); i += 256) {

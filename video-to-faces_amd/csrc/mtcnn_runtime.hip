@@ -859,14 +859,25 @@ static void detect(Mtcnn& m, const uint8_t* frames, int on_dev, int B, int H, in
     int4* sat = m.ar.get<int4>(S_SAT, (size_t)B * (H + 1) * (W + 1));
     launch_sat(fr, fstride, rstride, B, H, W, sat, st, d_cnt, NL + 3);
     {
+        // split mode: every downsampled level is precomputed as fp16 split pixels (16 B; k_pnet's
+        // fill is then a straight 16-byte copy -- the in-kernel bin sums of these levels were
+        // latency-bound on 7-14 KB frame patches: 10k + 19k of ~68k workgroup cycles per tile);
+        // fp32 mode: only the large-bin levels (H > 2 lh), as fp32 planes
+        const bool split = m.pw.c3h != nullptr;
+        auto is_pre = [&](const PNetLevel& L) {
+            return split ? (L.lh < H || L.lw < W) : (int64_t)H > 2 * (int64_t)L.lh;
+        };
         int64_t pre_elems = 0;
         for (auto& L : lv)
-            if ((int64_t)H > 2 * (int64_t)L.lh) pre_elems += (int64_t)B * 3 * L.lh * L.lw;
+            if (is_pre(L)) pre_elems += (int64_t)B * (split ? 4 : 3) * L.lh * L.lw;
         float* pre = pre_elems ? m.ar.get<float>(S_PRE, pre_elems) : nullptr;
         ResampleLevels rl{};
+        rl.split = split ? 1 : 0;
         for (auto& L : lv) {
             L.pre = nullptr;
-            if ((int64_t)H > 2 * (int64_t)L.lh) {
+            L.pad = 0;
+            if (is_pre(L)) {
+                L.pad = rl.split;
                 VTF_CHECK(rl.n < ResampleLevels::MAXL, VTF_E_LIMIT, "mtcnn: too many precomputed levels");
                 L.pre = pre;
                 rl.lh[rl.n] = L.lh;
@@ -874,7 +885,7 @@ static void detect(Mtcnn& m, const uint8_t* frames, int on_dev, int B, int H, in
                 rl.out[rl.n] = pre;
                 rl.beg[rl.n + 1] = rl.beg[rl.n] + (int64_t)B * L.lh * L.lw;
                 rl.n++;
-                pre += (int64_t)B * 3 * L.lh * L.lw;
+                pre += (int64_t)B * (split ? 4 : 3) * L.lh * L.lw;
             }
         }
         launch_resample_sat_multi(sat, B, H, W, rl, st);
