@@ -62,7 +62,10 @@ struct ResampleLevels {  // precomputed pyramid levels of one det-batch (k_resam
 void launch_resample_sat_multi(const int4* sat, int B, int H, int W, const ResampleLevels& lv, hipStream_t st);
 void launch_pnet(bool dense, const uint8_t* frames, int64_t frame_stride, int64_t row_stride, int H, int W,
                  const PNetLevel* d_levels, int n_levels, int64_t total_tiles, const PNetW& w, const PNetOut& o,
-                 uint32_t* d_tile_ctr, hipStream_t st, int64_t exact_tiles = 0);  // d_tile_ctr: 2 zeroed words
+                 uint32_t* d_tile_ctr, hipStream_t st, int64_t exact_tiles = 0,
+                 int64_t pre_from = INT64_MAX);  // d_tile_ctr: 3 zeroed words
+// first tile of the trailing levels precomputed as fp16 split pixels (k_pnet's PR variant)
+int64_t pnet_pre_from(const std::vector<PNetLevel>& lv, int64_t total_tiles);
 // leading tiles of the level plan that k_pnet's exact-levels variant takes (see launch_pnet)
 int64_t pnet_exact_tiles(const std::vector<PNetLevel>& lv, int H, int W, int64_t total_tiles);
 int cand_front_side(bool onet);

@@ -404,13 +404,17 @@ struct PnLds {
                   "exact-levels k_pnet LDS plan");
 };
 
-template <bool DENSE, bool X>
-__global__ __launch_bounds__(256, PnLds<X>::GPC) void k_pnet(const uint8_t* __restrict__ frames, int64_t frame_stride,
+// PR: the pre-resampled variant (round 3) -- tiles of the downsampled levels, all precomputed as
+// fp16 split pixels by k_resample_sat_multi, on the exact-levels LDS plan (four workgroups per CU):
+// the two-plane level tile (28 KB) does not fit beside the pooled map, so conv1 runs in two halves
+// of 10 pooled rows, each on 22 level rows (14.8 KB) loaded straight from the precomputed level.
+template <bool DENSE, bool X, bool PR = false>
+__global__ __launch_bounds__(256, PnLds<X || PR>::GPC) void k_pnet(const uint8_t* __restrict__ frames, int64_t frame_stride,
                                                  int64_t row_stride, int H, int W,
                                                  const PNetLevel* __restrict__ lv, int n_levels,
                                                  int64_t total_tiles, uint32_t* __restrict__ tile_ctr, PNetW wg,
                                                  PNetOut o, int64_t tile_base, int max_chunks, int chunk) {
-    using LP = PnLds<X>;
+    using LP = PnLds<X || PR>;
     const VTF_CONST float* wf = cptr(wg.c1w);  // fp32 weights (scalar loads at constant offsets)
     // conv / head weights through buffer loads: one lane VGPR offset + constant SGPR offsets,
     // instead of a 64-bit address per k-step (which the compiler would keep live across tiles);
@@ -422,7 +426,7 @@ __global__ __launch_bounds__(256, PnLds<X>::GPC) void k_pnet(const uint8_t* __re
     const __amdgpu_buffer_rsrc_t rw1h = __builtin_amdgcn_make_buffer_rsrc((void*)(wg.c3h + PH_C1H), 0, 2 * 16 * 64 * 2, 0x00020000);
     const __amdgpu_buffer_rsrc_t rhh = __builtin_amdgcn_make_buffer_rsrc((void*)(wg.c3h + PH_HH), 0, 2 * 32 * 32 * 2, 0x00020000);
     // conv3 on fp16 matrix cores (mtcnn_runtime: range bound); the X variant is launched only then
-    const bool split3 = X || wg.c3h != nullptr;
+    const bool split3 = X || PR || wg.c3h != nullptr;
     __shared__ __attribute__((aligned(16))) float sA[LP::A];     // level tile, later conv2 output
     __shared__ __attribute__((aligned(16))) float sP[LP::POOL];  // frame patch (u8) during the fill, then pooled conv1
     __shared__ ushort2 ybin[PL_H], xbin[PL_W];  // frame bin [start, end) of each level row / column
@@ -565,7 +569,7 @@ __global__ __launch_bounds__(256, PnLds<X>::GPC) void k_pnet(const uint8_t* __re
         }
         __syncthreads();
         mark(2);  // 2: frame patch staging
-        if (!X && P.pre && P.pad == 1) {
+        if (!X && !PR && P.pre && P.pad == 1) {
             // downsampled level precomputed by k_resample_sat_multi as fp16 split pixels (16 B:
             // x0 RGB0 | x1 RGB0, bit-identical to store_level's split of the bin average): the fill
             // is one 16-byte load and two 8-byte LDS stores per level pixel, all loads in flight
@@ -626,7 +630,7 @@ __global__ __launch_bounds__(256, PnLds<X>::GPC) void k_pnet(const uint8_t* __re
         // upsampled levels on the split path: bins of 1 or 2 frame pixels per side, every level
         // value s * 2^-(8..10) exact in fp16 (conv1 skips the residual plane there)
         // (X: every level is exact and the host checked that its patch + row sums fit)
-        const bool exact_fill = X || (split3 && P.lh >= H && P.lw >= W);
+        const bool exact_fill = X || (!PR && split3 && P.lh >= H && P.lw >= W);
         const bool sep = staged && !(o.dbg & 1) && hs_off + nrows * PL_W * (exact_fill ? 8 : 6) <= LP::PATCH &&
                          W < 128 * P.lw;
         if (sep && exact_fill) {
@@ -674,7 +678,7 @@ __global__ __launch_bounds__(256, PnLds<X>::GPC) void k_pnet(const uint8_t* __re
                 const float b0 = in ? (float)(v0[2] + m * v1[2]) * sc : 0.f;
                 lvl[r * PL_W + fq] = h4{(_Float16)r0, (_Float16)g0, (_Float16)b0, (_Float16)0.f};
             }
-        } else if (!X && sep) {
+        } else if (!X && !PR && sep) {
             // downsampled levels (bins of 1-3 frame pixels per side: lh >= H / 2, the rest are
             // precomputed): the exact fill's 2-D thread map (column fq of every 6th row, the
             // column's bin decoded once) and the bin divisions by the fma-corrected reciprocal
@@ -717,7 +721,7 @@ __global__ __launch_bounds__(256, PnLds<X>::GPC) void k_pnet(const uint8_t* __re
                             in ? div_small(div_small((float)s2 * 0.00390625f, kh), nq) : 0.f);
             }
         }
-        for (int i = tid; i < (X || (o.dbg & 1) || P.pre || sep ? 0 : PL_H * PL_W); i += 256) {
+        for (int i = tid; i < (X || PR || (o.dbg & 1) || P.pre || sep ? 0 : PL_H * PL_W); i += 256) {
             int r = i / PL_W, q = i - r * PL_W;
             const int2 yb = make_int2(ybin[r].x, ybin[r].y), xb = make_int2(xbin[q].x, xbin[q].y);
             float s0 = 0.f, s1 = 0.f, s2 = 0.f;
@@ -800,7 +804,7 @@ __global__ __launch_bounds__(256, PnLds<X>::GPC) void k_pnet(const uint8_t* __re
             // upsampled levels (lh >= H, lw >= W: every bin 1 or 2 frame pixels per side) hold
             // s / 2^(8..10) with |s| <= 1020, exact in fp16: the residual plane is zero there, so
             // its MFMAs and operand reads are skipped (the products they would add are all zero)
-            const bool exact = X || (P.lh >= H && P.lw >= W);
+            const bool exact = X || (!PR && P.lh >= H && P.lw >= W);
             const int wv = __builtin_amdgcn_readfirstlane(wave);
             // the lane's A row: cell cq of the block, corner
             const int r32 = ln & 31, cq = r32 >> 2, corner = r32 & 3;
@@ -823,11 +827,14 @@ __global__ __launch_bounds__(256, PnLds<X>::GPC) void k_pnet(const uint8_t* __re
             // NU fragments per iteration (wave-strided: F = wv + 4 k); whole iterations first,
             // then the remaining fragment one at a time.  FP: fastpool && unit_slope, a
             // compile-time branch (uniform flags tested per fragment cost a branch each)
+            // fragments [f0, f_end) of the level tile in sL whose first row is level row lrow0 of the
+            // tile (PR: a half tile of 22 rows, planes pln halves apart)
+            int f_end = NF1, lrow0 = 0, pln = PLN;
             auto conv1_frags = [&](auto exact_t, auto fp_t, auto nu_t, int f0) -> int {
                 constexpr bool EX = decltype(exact_t)::value;
                 constexpr bool FP = decltype(fp_t)::value;
                 constexpr int NU = decltype(nu_t)::value;
-                for (; f0 + 4 * (NU - 1) < NF1; f0 += 4 * NU) {
+                for (; f0 + 4 * (NU - 1) < f_end; f0 += 4 * NU) {
                     int fo[NU], py0[NU], px0[NU];
 #pragma unroll
                     for (int u = 0; u < NU; u++) {
@@ -835,7 +842,7 @@ __global__ __launch_bounds__(256, PnLds<X>::GPC) void k_pnet(const uint8_t* __re
                         const int br = f / FB;
                         py0[u] = 2 * br;
                         px0[u] = 4 * (f - br * FB);
-                        fo[u] = (lpix + 2 * py0[u] * PL_W + 2 * px0[u]) * 4;
+                        fo[u] = (lpix + (2 * py0[u] - lrow0) * PL_W + 2 * px0[u]) * 4;
                     }
                     f16x8 xa[3][NU], xb[3][NU];
 #pragma unroll
@@ -843,7 +850,7 @@ __global__ __launch_bounds__(256, PnLds<X>::GPC) void k_pnet(const uint8_t* __re
 #pragma unroll
                         for (int u = 0; u < NU; u++) {
                             xa[s][u] = ld_h8(sL + fo[u] + s * PL_W * 4);
-                            if (!EX) xb[s][u] = ld_h8(sL + PLN + fo[u] + s * PL_W * 4);
+                            if (!EX) xb[s][u] = ld_h8(sL + pln + fo[u] + s * PL_W * 4);
                         }
                     f32x16 acc[NU];
 #pragma unroll
@@ -907,7 +914,50 @@ __global__ __launch_bounds__(256, PnLds<X>::GPC) void k_pnet(const uint8_t* __re
             using F = std::false_type;
             // (the boundary / general-slope epilogue runs one fragment at a time: its per-corner
             //  bounds logic would otherwise set the kernel's register peak for ~3 % of the tiles)
-            if (exact) {
+            if (PR) {
+                // two halves: level rows [20 h, 20 h + 22) of both split planes (16-byte pixels of
+                // the precomputed level, one load each, all in flight), then the 25 fragments of
+                // pooled rows [10 h, 10 h + 10)
+                typedef __attribute__((ext_vector_type(2))) uint32_t u32x2;
+                constexpr int HR = PL_H / 2 + 1;  // 22 level rows per half
+                static_assert(2 * HR * PL_W * 8 + 8 <= LP::A * 4, "PR half tile fits the level buffer");
+                const uint4* pre4 = (const uint4*)P.pre + (int64_t)b * P.lh * P.lw;
+                u32x2* lvl = (u32x2*)sA;
+                int tl = tid;
+                asm volatile("" : "+v"(tl));
+                const int fq = tl % PL_W, fr0 = tl < 6 * PL_W ? tl / PL_W : HR;
+                const int lx = 2 * ox0 + fq;
+                const bool inx = lx < P.lw;
+                const int64_t cx = min(lx, P.lw - 1);
+                pln = HR * PL_W * 4;
+                for (int h = 0; h < 2; h++) {
+                    if (h) __syncthreads();  // the first half's fragments have read sA
+                    uint4 v[4];
+#pragma unroll
+                    for (int j = 0; j < 4; j++) {
+                        const int r = min(fr0 + 6 * j, HR - 1), ly = 2 * oy0 + 20 * h + r;
+                        const uint4 t = pre4[(int64_t)min(ly, P.lh - 1) * P.lw + cx];
+                        v[j] = inx && ly < P.lh ? t : make_uint4(0u, 0u, 0u, 0u);
+                    }
+#pragma unroll
+                    for (int j = 0; j < 4; j++) {
+                        const int r = fr0 + 6 * j;
+                        if (r < HR) {
+                            lvl[r * PL_W + fq] = u32x2{v[j].x, v[j].y};
+                            lvl[HR * PL_W + r * PL_W + fq] = u32x2{v[j].z, v[j].w};
+                        }
+                    }
+                    // conv1's operand reads run one pixel past plane 1 (against zero weights)
+                    if (tid == 0) lvl[2 * HR * PL_W] = u32x2{0u, 0u};
+                    __syncthreads();
+                    f_end = NF1 / 2 * (h + 1);
+                    lrow0 = 20 * h;
+                    if (fastpool && unit_slope)
+                        conv1_frags(F{}, T{}, I1{}, conv1_frags(F{}, T{}, I2{}, NF1 / 2 * h + wv));
+                    else
+                        conv1_frags(F{}, F{}, I1{}, NF1 / 2 * h + wv);
+                }
+            } else if (exact) {
                 if (fastpool && unit_slope)
                     conv1_frags(T{}, T{}, I1{}, conv1_frags(T{}, T{}, I2{}, wv));
                 else
@@ -929,7 +979,7 @@ __global__ __launch_bounds__(256, PnLds<X>::GPC) void k_pnet(const uint8_t* __re
             const int wv = __builtin_amdgcn_readfirstlane(wave);
             // (guarded, not only bounded: the compiler cannot prove wv >= 0, so a zero bound alone
             //  keeps the fallback's code -- and its register demand -- in the exact variant)
-            for (int wt = wv; !X && wt < ((o.dbg & 2) || split3 ? 0 : NWT); wt += 4) {
+            for (int wt = wv; !X && !PR && wt < ((o.dbg & 2) || split3 ? 0 : NWT); wt += 4) {
                 const int g = wt / NCH, chunk = wt - g * NCH;
                 const bool live = chunk * 64 + lane < NPP;
                 const int pp = min(chunk * 64 + lane, NPP - 1);
@@ -1215,7 +1265,7 @@ __global__ __launch_bounds__(256, PnLds<X>::GPC) void k_pnet(const uint8_t* __re
             // split conv3 + split heads (every X launch; the general variant when the host bounds
             // hold): conv3 and the heads on 32x32x16 matrix cores (below); otherwise the 16x16
             // fallbacks (fp32 conv3 and / or fp32 heads)
-            const bool splith = X || wg.hh != nullptr;  // (X: launched only with the split heads)
+            const bool splith = X || PR || wg.hh != nullptr;  // (X, PR: launched only with the split heads)
             const bool c3_32 = split3 && splith && !(o.dbg & 8);
             // heads as the A operand of two 32x32x16 steps: [plane][step], row = head (lane & 31;
             // rows >= 6 zero), k-slot (s, hk, i) = channel 16 s + 8 (i >> 2) + (i & 3) + 4 hk --
@@ -1569,7 +1619,7 @@ __global__ __launch_bounds__(256, PnLds<X>::GPC) void k_pnet(const uint8_t* __re
                 }
             }
         }
-        if (X) __syncthreads();  // conv3's weights (under the patch bytes) are no longer read
+        if (X || (PR && pf_n > 0)) __syncthreads();  // conv3's weights (under the patch bytes) are no longer read
         if (pf_n > 0 && 8 * tid < pf_n) *(uint2*)((uint8_t*)sP + 8 * tid) = pfv;
         pf_done = pf_n > 0;
         if (tid == 0) {  // every thread read s_tile / s_cend before this tile's barriers
@@ -1585,6 +1635,15 @@ __global__ __launch_bounds__(256, PnLds<X>::GPC) void k_pnet(const uint8_t* __re
 // tiles of the leading levels the exact-levels variant can take: upsampled (lh >= H, lw >= W,
 // no precomputed level) and every tile's frame patch + 8-byte row sums within its staging buffer
 // (bounds: a tile's 42-pixel level span covers at most 42 H / lh + 2 frame rows / columns)
+int64_t pnet_pre_from(const std::vector<PNetLevel>& lv, int64_t total_tiles) {
+    int64_t from = total_tiles;
+    for (size_t i = lv.size(); i-- > 0;) {
+        if (!(lv[i].pre && lv[i].pad == 1)) break;
+        from = lv[i].tile_beg;
+    }
+    return from;
+}
+
 int64_t pnet_exact_tiles(const std::vector<PNetLevel>& lv, int H, int W, int64_t total_tiles) {
     for (const auto& L : lv) {
         const int rows = (PL_H * H + L.lh - 1) / L.lh + 2, cols = (PL_W * W + L.lw - 1) / L.lw + 2;
@@ -1597,7 +1656,7 @@ int64_t pnet_exact_tiles(const std::vector<PNetLevel>& lv, int H, int W, int64_t
 
 void launch_pnet(bool dense, const uint8_t* frames, int64_t frame_stride, int64_t row_stride, int H, int W,
                  const PNetLevel* d_levels, int n_levels, int64_t total_tiles, const PNetW& w, const PNetOut& o,
-                 uint32_t* d_tile_ctr, hipStream_t st, int64_t exact_tiles) {
+                 uint32_t* d_tile_ctr, hipStream_t st, int64_t exact_tiles, int64_t pre_from) {
     if (total_tiles <= 0) return;
     VTF_CHECK(H < 65536 && W < 65536, VTF_E_LIMIT, "mtcnn: frames must be smaller than 65536 px per side");
     // k_pnet's index math is 32-bit (udiv_est): tile indices and bin numerators below 2^31
@@ -1635,7 +1694,7 @@ void launch_pnet(bool dense, const uint8_t* frames, int64_t frame_stride, int64_
     const int quota = qe ? std::min(1 << 16, std::max(0, std::atoi(qe))) : 2;
     if (!w.c3h || !w.hh || dense || (xe && std::atoi(xe) == 0)) exact_tiles = 0;
     exact_tiles = std::min(exact_tiles, total_tiles);
-    // (d_tile_ctr: two counters the caller zeroed, one per launch -- no fill kernels here)
+    // (d_tile_ctr: three counters the caller zeroed, one per launch -- no fill kernels here)
     if (exact_tiles > 0) {
         int64_t grid = std::min<int64_t>(exact_tiles, (int64_t)cus * wgs("VTF_PNET_X_WG_PER_CU", PnLds<true>::GPC));
         if (quota > 0) grid = std::max<int64_t>(grid, (exact_tiles + (int64_t)quota * chunk - 1) / ((int64_t)quota * chunk));
@@ -1643,18 +1702,32 @@ void launch_pnet(bool dense, const uint8_t* frames, int64_t frame_stride, int64_
                                                              exact_tiles, d_tile_ctr, w, o, 0, quota, chunk);
     }
     if (exact_tiles >= total_tiles) return;
-    d_tile_ctr += 1;
-    PNetOut og = o;  // (phase clocks of the general launch in words 8..15)
+    // the trailing levels precomputed as split pixels run on the PR variant (four workgroups per CU)
+    // when the split mode is on (VTF_PNET_PR=0: the general kernel takes them)
+    const char* pe = std::getenv("VTF_PNET_PR");
+    if (!w.c3h || !w.hh || dense || (pe && std::atoi(pe) == 0)) pre_from = total_tiles;
+    pre_from = std::max(exact_tiles, std::min(pre_from, total_tiles));
+    PNetOut og = o;  // (phase clocks of the launches after X in words 8..15)
     if (og.clk && exact_tiles > 0) og.clk += 8;
-    const int64_t rest = total_tiles - exact_tiles;
-    int64_t grid = std::min<int64_t>(rest, (int64_t)cus * wgs("VTF_PNET_WG_PER_CU", PnLds<false>::GPC));
-    if (quota > 0) grid = std::max<int64_t>(grid, (rest + (int64_t)quota * chunk - 1) / ((int64_t)quota * chunk));
-    if (dense)
-        k_pnet<true, false><<<(unsigned)grid, 256, 0, st>>>(frames, frame_stride, row_stride, H, W, d_levels, n_levels,
-                                                             total_tiles, d_tile_ctr, w, og, exact_tiles, quota, chunk);
-    else
-        k_pnet<false, false><<<(unsigned)grid, 256, 0, st>>>(frames, frame_stride, row_stride, H, W, d_levels, n_levels,
-                                                              total_tiles, d_tile_ctr, w, og, exact_tiles, quota, chunk);
+    if (pre_from > exact_tiles) {  // general variant: tiles [exact_tiles, pre_from)
+        const int64_t rest = pre_from - exact_tiles;
+        int64_t grid = std::min<int64_t>(rest, (int64_t)cus * wgs("VTF_PNET_WG_PER_CU", PnLds<false>::GPC));
+        if (quota > 0) grid = std::max<int64_t>(grid, (rest + (int64_t)quota * chunk - 1) / ((int64_t)quota * chunk));
+        if (dense)
+            k_pnet<true, false><<<(unsigned)grid, 256, 0, st>>>(frames, frame_stride, row_stride, H, W, d_levels, n_levels,
+                                                                 pre_from, d_tile_ctr + 1, w, og, exact_tiles, quota, chunk);
+        else
+            k_pnet<false, false><<<(unsigned)grid, 256, 0, st>>>(frames, frame_stride, row_stride, H, W, d_levels, n_levels,
+                                                                  pre_from, d_tile_ctr + 1, w, og, exact_tiles, quota, chunk);
+    }
+    if (pre_from < total_tiles) {  // PR variant: tiles [pre_from, total_tiles)
+        const int64_t rest = total_tiles - pre_from;
+        int64_t grid = std::min<int64_t>(rest, (int64_t)cus * PnLds<true>::GPC);
+        if (quota > 0) grid = std::max<int64_t>(grid, (rest + (int64_t)quota * chunk - 1) / ((int64_t)quota * chunk));
+        k_pnet<false, false, true><<<(unsigned)grid, 256, 0, st>>>(frames, frame_stride, row_stride, H, W, d_levels,
+                                                                    n_levels, total_tiles, d_tile_ctr + 2, w, og, pre_from,
+                                                                    quota, chunk);
+    }
 }
 
 // ----------------------------------------------------------------------------------- RNet / ONet

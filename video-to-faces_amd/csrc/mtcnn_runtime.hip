@@ -848,16 +848,16 @@ static void detect(Mtcnn& m, const uint8_t* frames, int on_dev, int B, int H, in
     if (NL == 0) return;
     VTF_CHECK(NL < 4096 && cells < (int64_t)1 << 31, VTF_E_LIMIT, "mtcnn: pyramid too large for one call");
     VTF_CHECK(B <= 4096, VTF_E_LIMIT, "mtcnn: at most 4096 frames per call");
-    // counters: [0] candidates, [1..NL] per level, [NL+1], [NL+2] the two PNet launches' tile
-    // counters -- zeroed by the SAT row pass (the first launch of the det-batch)
-    uint32_t* d_cnt = m.ar.get<uint32_t>(S_COUNT, NL + 3);
+    // counters: [0] candidates, [1..NL] per level, [NL+1..NL+3] the PNet launches' tile counters
+    // -- zeroed by the SAT row pass (the first launch of the det-batch)
+    uint32_t* d_cnt = m.ar.get<uint32_t>(S_COUNT, NL + 4);
     // downsampled levels whose adaptive-pool bins exceed 2 frame pixels are resampled by a
     // separate fully parallel kernel (one thread per level value) into HBM; inside the fused
     // tile kernel their long serial bin sums would leave a few workgroups as a long tail.
     // summed-area table of the preprocessed frames: O(1) exact bin sums for the downsampled
     // levels and the stage-2/3 candidate crops
     int4* sat = m.ar.get<int4>(S_SAT, (size_t)B * (H + 1) * (W + 1));
-    launch_sat(fr, fstride, rstride, B, H, W, sat, st, d_cnt, NL + 3);
+    launch_sat(fr, fstride, rstride, B, H, W, sat, st, d_cnt, NL + 4);
     {
         // split mode: every downsampled level is precomputed as fp16 split pixels (16 B; k_pnet's
         // fill is then a straight 16-byte copy -- the in-kernel bin sums of these levels were
@@ -913,7 +913,7 @@ static void detect(Mtcnn& m, const uint8_t* frames, int on_dev, int B, int H, in
     const int64_t x_tiles = pnet_exact_tiles(lv, H, W, tiles);
     if (m.prof) VTF_HIP(hipEventRecord(m.ev0, st));
     launch_pnet(false, fr, fstride, rstride, H, W, d_lv, NL, tiles, m.pw, po, d_cnt + NL + 1, st,
-                x_tiles);
+                x_tiles, pnet_pre_from(lv, tiles));
     if (m.prof) VTF_HIP(hipEventRecord(m.ev1, st));
     Arena::Mail mc = m.ar.mail(M_COUNT, (size_t)(NL + 1) * 4);
     k_mail_u32<<<1, 256, 0, st>>>(d_cnt, (uint32_t*)mc.d, NL + 1);
@@ -1232,7 +1232,7 @@ int vtf_mtcnn_pnet_level(vtf_mtcnn_t h, const uint8_t* d_frames, int B, int H, i
         po.prob = d_prob;
         po.reg = d_reg;
         uint32_t* ctr = h->m.ar.get<uint32_t>(S_COUNT, 4);
-        VTF_HIP(hipMemsetAsync(ctr, 0, 8, h->m.st));
+        VTF_HIP(hipMemsetAsync(ctr, 0, 12, h->m.st));
         launch_pnet(true, d_frames, frame_stride, row_stride, H, W, d_lv, 1, (int64_t)B * L.tiles_x * L.tiles_y,
                     h->m.pw, po, ctr, h->m.st);
         VTF_HIP(hipStreamSynchronize(h->m.st));
