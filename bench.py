@@ -529,7 +529,8 @@ def roofline_det(args, pipe, shared, solo):
         peak = F16X_PEAK_TFLOPS
         kname = ('k_pnet (fused pyramid resample + PNet; convs on fp16 matrix cores with split operands, '
                  'fp32-grade; peak = fp16 dense / 3 products; one "launch" = the det-batch\'s exact-levels '
-                 'k_pnet<false,true> + general k_pnet<false,false> pair: rocprof lists them as two rows)')
+                 'k_pnet<false,true,false> + pre-resampled k_pnet<false,false,true> pair: rocprof lists them as '
+                 'two rows; the downsampled levels\' resample runs before, in k_resample_sat_multi)')
     ach = fl / (s_avg / 1e3) / 1e12 if s_avg > 0 else 0.0
     c_ach = (c_fl / max(1, c_n)) / (c_avg / 1e3) / 1e12 if c_avg > 0 else 0.0
     traffic = None

@@ -15,7 +15,7 @@ from collections import Counter
 
 def main():
     path = sys.argv[1]
-    anchor = sys.argv[2] if len(sys.argv) > 2 else 'k_pnet<false, true>'
+    anchor = sys.argv[2] if len(sys.argv) > 2 else 'k_pnet<false, true'
     if os.path.isdir(path):
         path = glob.glob(os.path.join(path, '**', '*results.db'), recursive=True)[0]
     c = sqlite3.connect(path)
