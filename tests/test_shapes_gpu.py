@@ -73,6 +73,53 @@ def test_mtcnn_b16_device_crops(g):
     assert not (diff & ~near).any()
 
 
+@pytest.mark.parametrize('env', [{'VTF_PNET_PR': '0'}, {'VTF_PNET_X': '0', 'VTF_PNET_PR': '0'}])
+def test_mtcnn_b16_pnet_variants(g, env, monkeypatch):
+    """k_pnet's launch plans on config 2's det-batch against the same reference golden: the default
+    (exact-levels variant + the PR variant on the levels precomputed as split pixels), the general
+    variant instead of PR (VTF_PNET_PR=0) and one general launch for every tile (VTF_PNET_X=0 too)
+    -- counts exact, boxes 2e-3 px each; the plans read the same level values (bit-identical
+    fills), so they also agree with each other to the same tolerance."""
+    from videotofaces import synth
+    from videotofaces.detectors.mtcnn import MTCNN
+    frames = torch.from_numpy(synth.make_frames(16, seed=100)).cuda()
+    m = MTCNN('cuda:0')
+    base = m(frames, 5)
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    alt = m(frames, 5)
+    for res in (base, alt):
+        np.testing.assert_array_equal([r.shape[0] for r in res], g['mtcnn_b16_ms5_counts'])
+        np.testing.assert_allclose(np.concatenate(res), g['mtcnn_b16_ms5_boxes'], rtol=1e-5, atol=2e-3)
+    np.testing.assert_allclose(np.concatenate(alt), np.concatenate(base), rtol=1e-5, atol=2e-3)
+
+
+def test_mtcnn_detect_crops_capacity_retry():
+    """detect_crops with a crop capacity far below the kept count: the device box pass counts past
+    the capacity without writing, the call reports VTF_E_CAPACITY with the needed size, and the
+    retry (videotofaces._native.run_detect_crops) returns exactly the crops of a roomy call."""
+    from videotofaces import synth, _native as nat
+    from videotofaces.detectors.mtcnn import MTCNN
+    frames = torch.from_numpy(synth.make_frames(16, seed=100)).cuda()
+    m = MTCNN('cuda:0')
+    bp = nat.BoxParams.make(0.4, 0, 5, (1.5, 1.5, 2.2, 1.2), True)
+    ref, ref_counts = m.detect_crops(frames, 5, bp)
+    assert ref.shape[0] > 2
+    L = nat.lib()
+    m._bind_stream()
+    base, on_dev, B, H, W, fs, rs, keep = nat.frames_view(frames, m.device)
+    calls = []
+
+    def call(d, c, cap, n):
+        calls.append(cap)
+        return L.vtf_mtcnn_detect_crops(m._h, base, on_dev, B, H, W, fs, rs, 5.0, nat.ctypes.byref(bp), 0, d, c,
+                                        cap, n)
+    got, counts = nat.run_detect_crops(call, m.device, B, 1)
+    assert calls[0] == 1 and len(calls) == 2 and calls[1] == ref.shape[0]
+    np.testing.assert_array_equal(got.cpu().numpy(), ref.cpu().numpy())
+    np.testing.assert_array_equal(counts, ref_counts)
+
+
 @pytest.mark.parametrize('precision', ['fp32', 'x3'])
 def test_yolo_1080p_b4(g, precision):
     from videotofaces import synth
