@@ -111,7 +111,7 @@ __host__ __device__ inline int64_t ntasks(int64_t n) {
 // (rb, column-block chunk) -- what the host used to build after a device->host round trip.  Tasks
 // are enumerated segment by segment, row block by row block (any order is correct: each task
 // writes its own mask words).
-constexpr int PLAN_T = 1024;
+constexpr int PLAN_T = 256;  // (1024 threads waited ~0.27 ms for a CU slot beside the other lanes' k_pnet workgroups; c2 unchanged either way)
 __global__ __launch_bounds__(PLAN_T) void k_nms_plan(const int64_t* __restrict__ sstart, const uint32_t* __restrict__ seg_hi,
                                                       int sbits, const uint8_t* __restrict__ call_van,
                                                       const float* __restrict__ call_max, int S, int32_t* __restrict__ scnt,
