@@ -10,7 +10,7 @@ struct PNetLevel {
     int ph, pw;       // PNet output size
     float scale;      // fp32(s)
     int tiles_x, tiles_y;
-    int pad;          // 1: `pre` holds fp16 split pixels (16 B, k_resample_sat_multi split mode)
+    int pad;          // 1: `pre` holds fp16 split pixels (12 B, k_resample_sat_multi split mode)
     int64_t tile_beg; // first workgroup of this level
     const float* pre; // precomputed level [B][3][lh][lw] (large-bin downsampled levels) or null
 };
@@ -54,7 +54,7 @@ void launch_resample_sat(const int4* sat, int B, int H, int W, int lh, int lw, f
 struct ResampleLevels {  // precomputed pyramid levels of one det-batch (k_resample_sat_multi)
     static constexpr int MAXL = 32;
     int n;
-    int split;  // 1: [B][lh][lw] fp16 split pixels (x0 RGB0 | x1 RGB0, 16 B), else fp32 [B][3][lh][lw]
+    int split;  // 1: [B][lh][lw] fp16 split pixels (x0 RGB | x1 RGB, 12 B), else fp32 [B][3][lh][lw]
     int lh[MAXL], lw[MAXL];
     int64_t beg[MAXL + 1];  // first output element (b, y, x) of each level in the flattened grid
     float* out[MAXL];       // [B][3][lh][lw]

@@ -221,14 +221,15 @@ __global__ void k_resample_sat_multi(const int4* __restrict__ sat, int B, int H,
     const int y0 = (int)(((int64_t)ly * H) / lh), y1 = (int)(((int64_t)(ly + 1) * H + lh - 1) / lh);
     const int x0 = (int)(((int64_t)lx * W) / lw), x1 = (int)(((int64_t)(lx + 1) * W + lw - 1) / lw);
     const int4 s = sat_box(sat + (int64_t)b * (H + 1) * (W + 1), W + 1, y0, y1, x0, x1);
-    if (lv.split) {  // fp16 split pixels [B][lh][lw] x (x0 RGB0 | x1 RGB0), k_pnet's level-tile form
+    if (lv.split) {  // fp16 split pixels [B][lh][lw] x (x0 RGB | x1 RGB), k_pnet's level-tile halves
         typedef __attribute__((ext_vector_type(8))) _Float16 h8;
         _Float16 r0, r1, g0, g1, b0, b1;
         split_f16(bin_avg(s.x, y1 - y0, x1 - x0), r0, r1);
         split_f16(bin_avg(s.y, y1 - y0, x1 - x0), g0, g1);
         split_f16(bin_avg(s.z, y1 - y0, x1 - x0), b0, b1);
-        const _Float16 z = (_Float16)0.f;
-        ((h8*)lv.out[l])[j] = h8{r0, g0, b0, z, r1, g1, b1, z};
+        // 12 bytes (no pad halves): r0 g0 | b0 r1 | g1 b1
+        auto hb = [](_Float16 h) { return (uint32_t)__builtin_bit_cast(uint16_t, h); };
+        ((uint3*)lv.out[l])[j] = make_uint3(hb(r0) | hb(g0) << 16, hb(b0) | hb(r1) << 16, hb(g1) | hb(b1) << 16);
         return;
     }
     const int64_t plane = (int64_t)lh * lw, o = (int64_t)b * 3 * plane + (int64_t)ly * lw + lx;
@@ -570,11 +571,11 @@ __global__ __launch_bounds__(256, PnLds<X || PR>::GPC) void k_pnet(const uint8_t
         __syncthreads();
         mark(2);  // 2: frame patch staging
         if (!X && !PR && P.pre && P.pad == 1) {
-            // downsampled level precomputed by k_resample_sat_multi as fp16 split pixels (16 B:
-            // x0 RGB0 | x1 RGB0, bit-identical to store_level's split of the bin average): the fill
-            // is one 16-byte load and two 8-byte LDS stores per level pixel, all loads in flight
+            // downsampled level precomputed by k_resample_sat_multi as fp16 split pixels (12 B:
+            // x0 RGB | x1 RGB, bit-identical to store_level's split of the bin average): the fill
+            // is one 12-byte load and two 8-byte LDS stores per level pixel, all loads in flight
             typedef __attribute__((ext_vector_type(2))) uint32_t u32x2;
-            const uint4* pre4 = (const uint4*)P.pre + (int64_t)b * P.lh * P.lw;
+            const uint3* pre3 = (const uint3*)P.pre + (int64_t)b * P.lh * P.lw;
             u32x2* lvl = (u32x2*)sA;
             int tl = tid;
             asm volatile("" : "+v"(tl));
@@ -582,19 +583,19 @@ __global__ __launch_bounds__(256, PnLds<X || PR>::GPC) void k_pnet(const uint8_t
             const int lx = 2 * ox0 + fq;
             const bool inx = lx < P.lw;
             const int64_t cx = min(lx, P.lw - 1);
-            uint4 v[7];
+            uint3 v[7];
 #pragma unroll
             for (int j = 0; j < 7; j++) {
                 const int r = min(fr0 + 6 * j, PL_H - 1), ly = 2 * oy0 + r;
-                const uint4 t = pre4[(int64_t)min(ly, P.lh - 1) * P.lw + cx];
-                v[j] = inx && ly < P.lh ? t : make_uint4(0u, 0u, 0u, 0u);
+                const uint3 t = pre3[(int64_t)min(ly, P.lh - 1) * P.lw + cx];
+                v[j] = inx && ly < P.lh ? t : make_uint3(0u, 0u, 0u);
             }
 #pragma unroll
             for (int j = 0; j < 7; j++) {
                 const int r = fr0 + 6 * j;
                 if (r < PL_H) {
-                    lvl[r * PL_W + fq] = u32x2{v[j].x, v[j].y};
-                    lvl[PL_H * PL_W + r * PL_W + fq] = u32x2{v[j].z, v[j].w};
+                    lvl[r * PL_W + fq] = u32x2{v[j].x, v[j].y & 0xffffu};
+                    lvl[PL_H * PL_W + r * PL_W + fq] = u32x2{(v[j].y >> 16) | (v[j].z << 16), v[j].z >> 16};
                 }
             }
         } else if (!X && P.pre) {
@@ -915,13 +916,13 @@ __global__ __launch_bounds__(256, PnLds<X || PR>::GPC) void k_pnet(const uint8_t
             // (the boundary / general-slope epilogue runs one fragment at a time: its per-corner
             //  bounds logic would otherwise set the kernel's register peak for ~3 % of the tiles)
             if (PR) {
-                // two halves: level rows [20 h, 20 h + 22) of both split planes (16-byte pixels of
+                // two halves: level rows [20 h, 20 h + 22) of both split planes (12-byte pixels of
                 // the precomputed level, one load each, all in flight), then the 25 fragments of
                 // pooled rows [10 h, 10 h + 10)
                 typedef __attribute__((ext_vector_type(2))) uint32_t u32x2;
                 constexpr int HR = PL_H / 2 + 1;  // 22 level rows per half
                 static_assert(2 * HR * PL_W * 8 + 8 <= LP::A * 4, "PR half tile fits the level buffer");
-                const uint4* pre4 = (const uint4*)P.pre + (int64_t)b * P.lh * P.lw;
+                const uint3* pre3 = (const uint3*)P.pre + (int64_t)b * P.lh * P.lw;
                 u32x2* lvl = (u32x2*)sA;
                 int tl = tid;
                 asm volatile("" : "+v"(tl));
@@ -932,19 +933,19 @@ __global__ __launch_bounds__(256, PnLds<X || PR>::GPC) void k_pnet(const uint8_t
                 pln = HR * PL_W * 4;
                 for (int h = 0; h < 2; h++) {
                     if (h) __syncthreads();  // the first half's fragments have read sA
-                    uint4 v[4];
+                    uint3 v[4];
 #pragma unroll
                     for (int j = 0; j < 4; j++) {
                         const int r = min(fr0 + 6 * j, HR - 1), ly = 2 * oy0 + 20 * h + r;
-                        const uint4 t = pre4[(int64_t)min(ly, P.lh - 1) * P.lw + cx];
-                        v[j] = inx && ly < P.lh ? t : make_uint4(0u, 0u, 0u, 0u);
+                        const uint3 t = pre3[(int64_t)min(ly, P.lh - 1) * P.lw + cx];
+                        v[j] = inx && ly < P.lh ? t : make_uint3(0u, 0u, 0u);
                     }
 #pragma unroll
                     for (int j = 0; j < 4; j++) {
                         const int r = fr0 + 6 * j;
                         if (r < HR) {
-                            lvl[r * PL_W + fq] = u32x2{v[j].x, v[j].y};
-                            lvl[HR * PL_W + r * PL_W + fq] = u32x2{v[j].z, v[j].w};
+                            lvl[r * PL_W + fq] = u32x2{v[j].x, v[j].y & 0xffffu};
+                            lvl[HR * PL_W + r * PL_W + fq] = u32x2{(v[j].y >> 16) | (v[j].z << 16), v[j].z >> 16};
                         }
                     }
                     // conv1's operand reads run one pixel past plane 1 (against zero weights)

@@ -859,8 +859,8 @@ static void detect(Mtcnn& m, const uint8_t* frames, int on_dev, int B, int H, in
     int4* sat = m.ar.get<int4>(S_SAT, (size_t)B * (H + 1) * (W + 1));
     launch_sat(fr, fstride, rstride, B, H, W, sat, st, d_cnt, NL + 4);
     {
-        // split mode: every downsampled level is precomputed as fp16 split pixels (16 B; k_pnet's
-        // fill is then a straight 16-byte copy -- the in-kernel bin sums of these levels were
+        // split mode: every downsampled level is precomputed as fp16 split pixels (12 B; k_pnet's
+        // fill is then a straight 12-byte copy -- the in-kernel bin sums of these levels were
         // latency-bound on 7-14 KB frame patches: 10k + 19k of ~68k workgroup cycles per tile);
         // fp32 mode: only the large-bin levels (H > 2 lh), as fp32 planes
         const bool split = m.pw.c3h != nullptr;
@@ -869,7 +869,7 @@ static void detect(Mtcnn& m, const uint8_t* frames, int on_dev, int B, int H, in
         };
         int64_t pre_elems = 0;
         for (auto& L : lv)
-            if (is_pre(L)) pre_elems += (int64_t)B * (split ? 4 : 3) * L.lh * L.lw;
+            if (is_pre(L)) pre_elems += (int64_t)B * 3 * L.lh * L.lw;  // 12 B per pixel either way
         float* pre = pre_elems ? m.ar.get<float>(S_PRE, pre_elems) : nullptr;
         ResampleLevels rl{};
         rl.split = split ? 1 : 0;
@@ -885,7 +885,7 @@ static void detect(Mtcnn& m, const uint8_t* frames, int on_dev, int B, int H, in
                 rl.out[rl.n] = pre;
                 rl.beg[rl.n + 1] = rl.beg[rl.n] + (int64_t)B * L.lh * L.lw;
                 rl.n++;
-                pre += (int64_t)B * (split ? 4 : 3) * L.lh * L.lw;
+                pre += (int64_t)B * 3 * L.lh * L.lw;
             }
         }
         launch_resample_sat_multi(sat, B, H, W, rl, st);
