@@ -48,9 +48,9 @@ struct PNetOut {
     unsigned long long* clk;  // [8] summed shader clocks per phase over workgroups (null: off)
 };
 
-void launch_sat(const uint8_t* frames, int64_t frame_stride, int64_t row_stride, int B, int H, int W, int4* sat,
+void launch_sat(const uint8_t* frames, int64_t frame_stride, int64_t row_stride, int B, int H, int W, int3* sat,
                 hipStream_t st, uint32_t* zero = nullptr, int nzero = 0);
-void launch_resample_sat(const int4* sat, int B, int H, int W, int lh, int lw, float* out, hipStream_t st);
+void launch_resample_sat(const int3* sat, int B, int H, int W, int lh, int lw, float* out, hipStream_t st);
 struct ResampleLevels {  // precomputed pyramid levels of one det-batch (k_resample_sat_multi)
     static constexpr int MAXL = 32;
     int n;
@@ -59,7 +59,7 @@ struct ResampleLevels {  // precomputed pyramid levels of one det-batch (k_resam
     int64_t beg[MAXL + 1];  // first output element (b, y, x) of each level in the flattened grid
     float* out[MAXL];       // [B][3][lh][lw]
 };
-void launch_resample_sat_multi(const int4* sat, int B, int H, int W, const ResampleLevels& lv, hipStream_t st);
+void launch_resample_sat_multi(const int3* sat, int B, int H, int W, const ResampleLevels& lv, hipStream_t st);
 void launch_pnet(bool dense, const uint8_t* frames, int64_t frame_stride, int64_t row_stride, int H, int W,
                  const PNetLevel* d_levels, int n_levels, int64_t total_tiles, const PNetW& w, const PNetOut& o,
                  uint32_t* d_tile_ctr, hipStream_t st, int64_t exact_tiles = 0,
@@ -69,7 +69,7 @@ int64_t pnet_pre_from(const std::vector<PNetLevel>& lv, int64_t total_tiles);
 // leading tiles of the level plan that k_pnet's exact-levels variant takes (see launch_pnet)
 int64_t pnet_exact_tiles(const std::vector<PNetLevel>& lv, int H, int W, int64_t total_tiles);
 int cand_front_side(bool onet);
-void launch_cand_front(bool onet, const int4* sat, int H, int W, const float4* boxes, const int32_t* img, int64_t n,
+void launch_cand_front(bool onet, const int3* sat, int H, int W, const float4* boxes, const int32_t* img, int64_t n,
                        const float* w1, const _Float16* w1h, const float* b1, const float* a1, float* out, int32_t* err,
                        hipStream_t st, int* ovf = nullptr);
 // Fused RNet / ONet front half (mtcnn_cand.hip): crop + conv1 + PReLU + pool + conv2 + PReLU +
@@ -83,7 +83,7 @@ struct CandFusedW {
     const float *b2, *a2;
 };
 int cand_fused_side(bool onet);
-void launch_cand_fused(bool onet, const int4* sat, int H, int W, const float4* boxes, const int32_t* img, int64_t n,
+void launch_cand_fused(bool onet, const int3* sat, int H, int W, const float4* boxes, const int32_t* img, int64_t n,
                        const CandFusedW& w, float* out, int32_t* err, int32_t* ovf, hipStream_t st);
 void launch_heads(const float* x, int64_t n, int D, const float* w1, const float* b1, const float* w2,
                   const float* b2, const float* w3, const float* b3, float* prob, float4* reg, float* lm,

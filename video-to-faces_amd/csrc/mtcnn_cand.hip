@@ -71,7 +71,7 @@ __device__ inline int p1_index(int pix, int c) { return pix * 32 + ((((c >> 3) ^
 
 template <int S, int C2, int PB1, int PB2, int MG>
 __global__ __launch_bounds__((Cfg<S, C2, PB1, PB2, MG>::NT)) void k_cand_fused(
-    const int4* __restrict__ sat, int H, int W, const float4* __restrict__ boxes, const int32_t* __restrict__ img,
+    const int3* __restrict__ sat, int H, int W, const float4* __restrict__ boxes, const int32_t* __restrict__ img,
     int64_t n, const _Float16* __restrict__ w1h, const float* __restrict__ b1, const float* __restrict__ a1,
     const _Float16* __restrict__ w2h, const float* __restrict__ b2, const float* __restrict__ a2,
     float* __restrict__ out, int32_t* __restrict__ err, int32_t* __restrict__ ovf, int dbg) {
@@ -108,16 +108,16 @@ __global__ __launch_bounds__((Cfg<S, C2, PB1, PB2, MG>::NT)) void k_cand_fused(
             continue;  // uniform: every thread of the workgroup takes it
         }
         // ---- crop: S x S adaptive-pool bins from the SAT, split into the two planes
-        const int4* sk = sat + (int64_t)img[k] * (H + 1) * (W + 1);
+        const int3* sk = sat + (int64_t)img[k] * (H + 1) * (W + 1);
         for (int i = tid; i < CP * CP; i += NT) {
             const int r = i / CP, q = i - r * CP;
             h4 v0 = {0, 0, 0, 0}, v1 = {0, 0, 0, 0};
             if (r < S && q < S && !(dbg & 1)) {
                 const int ys = (r * hc) / S, ye = ((r + 1) * hc + S - 1) / S;
                 const int xs = (q * wc) / S, xe = ((q + 1) * wc + S - 1) / S;
-                const int4* ra = sk + (int64_t)(y0 + ys) * (W + 1) + x0;
-                const int4* rb = sk + (int64_t)(y0 + ye) * (W + 1) + x0;
-                const int4 a = ra[xs], b = ra[xe], c = rb[xs], d = rb[xe];
+                const int3* ra = sk + (int64_t)(y0 + ys) * (W + 1) + x0;
+                const int3* rb = sk + (int64_t)(y0 + ye) * (W + 1) + x0;
+                const int3 a = ra[xs], b = ra[xe], c = rb[xs], d = rb[xe];
                 const float c0 = bin_avg(d.x - b.x - c.x + a.x, ye - ys, xe - xs);
                 const float c1 = bin_avg(d.y - b.y - c.y + a.y, ye - ys, xe - xs);
                 const float c2 = bin_avg(d.z - b.z - c.z + a.z, ye - ys, xe - xs);
@@ -255,7 +255,7 @@ __global__ __launch_bounds__((Cfg<S, C2, PB1, PB2, MG>::NT)) void k_cand_fused(
 }
 
 template <int S, int C2, int PB1, int PB2, int MG>
-void launch_t(const int4* sat, int H, int W, const float4* boxes, const int32_t* img, int64_t n, const CandFusedW& w,
+void launch_t(const int3* sat, int H, int W, const float4* boxes, const int32_t* img, int64_t n, const CandFusedW& w,
               float* out, int32_t* err, int32_t* ovf, hipStream_t st) {
     using C = Cfg<S, C2, PB1, PB2, MG>;
     static_assert(C::SMEM <= 160 * 1024, "LDS budget");
@@ -282,7 +282,7 @@ void launch_t(const int4* sat, int H, int W, const float4* boxes, const int32_t*
 
 int cand_fused_side(bool onet) { return onet ? Cfg<48, 64, 2, 2, 3>::P2 : Cfg<24, 48, 3, 4, 2>::P2; }
 
-void launch_cand_fused(bool onet, const int4* sat, int H, int W, const float4* boxes, const int32_t* img, int64_t n,
+void launch_cand_fused(bool onet, const int3* sat, int H, int W, const float4* boxes, const int32_t* img, int64_t n,
                        const CandFusedW& w, float* out, int32_t* err, int32_t* ovf, hipStream_t st) {
     if (n <= 0) return;
     if (onet)

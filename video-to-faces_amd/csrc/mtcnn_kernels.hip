@@ -39,10 +39,11 @@ typedef __attribute__((ext_vector_type(8))) _Float16 f16x8;
 // in fp32, and so is every partial sum of such values over an adaptive-pool bin (|sum| < 2^16
 // with 8 fractional bits), so the reference's sequential fp32 bin sum (adaptive_avg_pool2d,
 // row-major) equals the integer box sum of v = 2u - 255 times 2^-8, bit for bit.
-// sat[b][y][x] = (R, G, B, 0) sums over rows < y, cols < x; y in [0,H], x in [0,W].
-__device__ inline int4 sat_box(const int4* __restrict__ s, int W1, int y0, int y1, int x0, int x1) {
-    const int4 a = s[(int64_t)y0 * W1 + x0], b = s[(int64_t)y0 * W1 + x1];
-    const int4 c = s[(int64_t)y1 * W1 + x0], d = s[(int64_t)y1 * W1 + x1];
+// sat[b][y][x] = (R, G, B) sums over rows < y, cols < x; y in [0,H], x in [0,W] (12 bytes per
+// entry: the SAT passes and every corner read are HBM / MALL-bound, a pad word was a quarter of it).
+__device__ inline int4 sat_box(const int3* __restrict__ s, int W1, int y0, int y1, int x0, int x1) {
+    const int3 a = s[(int64_t)y0 * W1 + x0], b = s[(int64_t)y0 * W1 + x1];
+    const int3 c = s[(int64_t)y1 * W1 + x0], d = s[(int64_t)y1 * W1 + x1];
     return make_int4(d.x - b.x - c.x + a.x, d.y - b.y - c.y + a.y, d.z - b.z - c.z + a.z, 0);
 }
 
@@ -68,17 +69,17 @@ __device__ inline void split_f16(float v, _Float16& x0, _Float16& x1) {
 
 // row pass: block per frame row
 __global__ __launch_bounds__(256) void k_sat_rows(const uint8_t* __restrict__ frames, int64_t frame_stride,
-                                                  int64_t row_stride, int H, int W, int4* __restrict__ sat,
+                                                  int64_t row_stride, int H, int W, int3* __restrict__ sat,
                                                   uint32_t* __restrict__ zero, int nzero) {
     // (folded memset: the det-batch's PNet candidate counters)
     if (blockIdx.x == 0)
         for (int i = threadIdx.x; i < nzero; i += 256) zero[i] = 0u;
     // row prefix sums in passes of 256 consecutive pixels (one per thread: coalesced byte loads
-    // and 4 KB contiguous int4 stores), a block scan per pass with the carry in registers
+    // and 3 KB contiguous 12-byte stores), a block scan per pass with the carry in registers
     const int y = blockIdx.x % H, b = blockIdx.x / H;
     const int W1 = W + 1;
     const uint8_t* row = frames + (int64_t)b * frame_stride + (int64_t)y * row_stride;
-    int4* out = sat + ((int64_t)b * (H + 1) + y + 1) * W1;
+    int3* out = sat + ((int64_t)b * (H + 1) + y + 1) * W1;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     __shared__ int3 wt[2][4];
     int3 carry = make_int3(0, 0, 0);
@@ -121,12 +122,12 @@ __global__ __launch_bounds__(256) void k_sat_rows(const uint8_t* __restrict__ fr
             carry.z += t.z;
         }
         const int x = x0 + tid;
-        if (x < W) out[x + 1] = make_int4(wb.x + r, wb.y + g, wb.z + bl, 0);
+        if (x < W) out[x + 1] = make_int3(wb.x + r, wb.y + g, wb.z + bl);
     }
-    if (tid == 0) out[0] = make_int4(0, 0, 0, 0);
+    if (tid == 0) out[0] = make_int3(0, 0, 0);
     if (y == 0) {
-        int4* r0 = sat + (int64_t)b * (H + 1) * W1;
-        for (int x = tid; x < W1; x += 256) r0[x] = make_int4(0, 0, 0, 0);
+        int3* r0 = sat + (int64_t)b * (H + 1) * W1;
+        for (int x = tid; x < W1; x += 256) r0[x] = make_int3(0, 0, 0);
     }
 }
 
@@ -134,7 +135,7 @@ __global__ __launch_bounds__(256) void k_sat_rows(const uint8_t* __restrict__ fr
 // keeps its rows in registers (the SAT is read once and written once), group totals combined
 // in LDS
 constexpr int SAT_COLS = 16, SAT_PER = 24, SAT_MAXG = 64;
-__global__ __launch_bounds__(SAT_COLS * SAT_MAXG) void k_sat_cols(int H, int W, int4* __restrict__ sat) {
+__global__ __launch_bounds__(SAT_COLS * SAT_MAXG) void k_sat_cols(int H, int W, int3* __restrict__ sat) {
     const int W1 = W + 1;
     const int G = blockDim.x / SAT_COLS;
     const int ncb = (W1 + SAT_COLS - 1) / SAT_COLS;
@@ -143,24 +144,24 @@ __global__ __launch_bounds__(SAT_COLS * SAT_MAXG) void k_sat_cols(int H, int W, 
     const int x = cb * SAT_COLS + c;
     const int per = (H + G - 1) / G;
     const int ys = 1 + g * per, ye = min(H + 1, ys + per);
-    int4* col = sat + (int64_t)b * (H + 1) * W1 + min(x, W1 - 1);
+    int3* col = sat + (int64_t)b * (H + 1) * W1 + min(x, W1 - 1);
     // [G][SAT_COLS] group totals, sized by the launch (7.7 KB at 720p): small enough to co-reside
     // with another lane's persistent k_pnet (3 x 49 KB of the CU's 160 KB), so a det-batch's SAT
     // does not wait for the other lanes' pyramid kernels to drain
-    extern __shared__ int4 tot_s[];
-    int4 (*tot)[SAT_COLS] = (int4 (*)[SAT_COLS])tot_s;
-    int4 v[SAT_PER];
-    int4 acc = make_int4(0, 0, 0, 0);
+    extern __shared__ int3 tot_s[];
+    int3 (*tot)[SAT_COLS] = (int3 (*)[SAT_COLS])tot_s;
+    int3 v[SAT_PER];
+    int3 acc = make_int3(0, 0, 0);
 #pragma unroll
     for (int i = 0; i < SAT_PER; i++) {
-        v[i] = (x < W1 && ys + i < ye) ? col[(int64_t)(ys + i) * W1] : make_int4(0, 0, 0, 0);
+        v[i] = (x < W1 && ys + i < ye) ? col[(int64_t)(ys + i) * W1] : make_int3(0, 0, 0);
         acc.x += v[i].x;
         acc.y += v[i].y;
         acc.z += v[i].z;
     }
     tot[g][c] = acc;
     __syncthreads();
-    int4 off = make_int4(0, 0, 0, 0);
+    int3 off = make_int3(0, 0, 0);
     for (int k = 0; k < g; k++) {
         off.x += tot[k][c].x;
         off.y += tot[k][c].y;
@@ -175,17 +176,17 @@ __global__ __launch_bounds__(SAT_COLS * SAT_MAXG) void k_sat_cols(int H, int W, 
     }
 }
 
-void launch_sat(const uint8_t* frames, int64_t frame_stride, int64_t row_stride, int B, int H, int W, int4* sat,
+void launch_sat(const uint8_t* frames, int64_t frame_stride, int64_t row_stride, int B, int H, int W, int3* sat,
                 hipStream_t st, uint32_t* zero, int nzero) {
     k_sat_rows<<<(unsigned)((int64_t)B * H), 256, 0, st>>>(frames, frame_stride, row_stride, H, W, sat, zero, nzero);
     const int G = (H + SAT_PER - 1) / SAT_PER;
     VTF_CHECK(G <= SAT_MAXG, VTF_E_LIMIT, "mtcnn: frames taller than 1536 rows");
-    k_sat_cols<<<(unsigned)(B * ((W + SAT_COLS) / SAT_COLS)), SAT_COLS * G, (size_t)G * SAT_COLS * sizeof(int4), st>>>(H, W, sat);
+    k_sat_cols<<<(unsigned)(B * ((W + SAT_COLS) / SAT_COLS)), SAT_COLS * G, (size_t)G * SAT_COLS * sizeof(int3), st>>>(H, W, sat);
 }
 
 // MTCNN._resample of the preprocessed frames (mtcnn.py:133-139, 150-151) from the SAT:
 // out [B][3][lh][lw], one thread per level pixel (all three channels)
-__global__ void k_resample_sat(const int4* __restrict__ sat, int B, int H, int W, int lh, int lw,
+__global__ void k_resample_sat(const int3* __restrict__ sat, int B, int H, int W, int lh, int lw,
                                float* __restrict__ out) {
     int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     int64_t n = (int64_t)B * lh * lw;
@@ -202,13 +203,13 @@ __global__ void k_resample_sat(const int4* __restrict__ sat, int B, int H, int W
     out[o + 2 * plane] = bin_avg(s.z, y1 - y0, x1 - x0);
 }
 
-void launch_resample_sat(const int4* sat, int B, int H, int W, int lh, int lw, float* out, hipStream_t st) {
+void launch_resample_sat(const int3* sat, int B, int H, int W, int lh, int lw, float* out, hipStream_t st) {
     int64_t n = (int64_t)B * lh * lw;
     k_resample_sat<<<cdiv(n, 256), 256, 0, st>>>(sat, B, H, W, lh, lw, out);
 }
 
 // every precomputed level of a det-batch in one launch (the small levels alone are launch-bound)
-__global__ void k_resample_sat_multi(const int4* __restrict__ sat, int B, int H, int W, ResampleLevels lv) {
+__global__ void k_resample_sat_multi(const int3* __restrict__ sat, int B, int H, int W, ResampleLevels lv) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= lv.beg[lv.n]) return;
     int l = 0;
@@ -222,7 +223,6 @@ __global__ void k_resample_sat_multi(const int4* __restrict__ sat, int B, int H,
     const int x0 = (int)(((int64_t)lx * W) / lw), x1 = (int)(((int64_t)(lx + 1) * W + lw - 1) / lw);
     const int4 s = sat_box(sat + (int64_t)b * (H + 1) * (W + 1), W + 1, y0, y1, x0, x1);
     if (lv.split) {  // fp16 split pixels [B][lh][lw] x (x0 RGB | x1 RGB), k_pnet's level-tile halves
-        typedef __attribute__((ext_vector_type(8))) _Float16 h8;
         _Float16 r0, r1, g0, g1, b0, b1;
         split_f16(bin_avg(s.x, y1 - y0, x1 - x0), r0, r1);
         split_f16(bin_avg(s.y, y1 - y0, x1 - x0), g0, g1);
@@ -239,7 +239,7 @@ __global__ void k_resample_sat_multi(const int4* __restrict__ sat, int B, int H,
     out[o + 2 * plane] = bin_avg(s.z, y1 - y0, x1 - x0);
 }
 
-void launch_resample_sat_multi(const int4* sat, int B, int H, int W, const ResampleLevels& lv, hipStream_t st) {
+void launch_resample_sat_multi(const int3* sat, int B, int H, int W, const ResampleLevels& lv, hipStream_t st) {
     VTF_CHECK(lv.n >= 0 && lv.n <= ResampleLevels::MAXL, VTF_E_LIMIT, "mtcnn: too many precomputed levels");
     if (lv.n == 0 || lv.beg[lv.n] == 0) return;
     k_resample_sat_multi<<<cdiv(lv.beg[lv.n], 256), 256, 0, st>>>(sat, B, H, W, lv);
@@ -1744,7 +1744,7 @@ void launch_pnet(bool dense, const uint8_t* frames, int64_t frame_stride, int64_
 // ring of 2*PB+1 rows (the pool window's shared row is kept, not recomputed).
 // w1: [28][32] (k, co; row 27 and channels >= Cout zero); b1, a1: [32].
 template <int S, int PB, int NT, bool XS>
-__global__ __launch_bounds__(NT) void k_cand_front(const int4* __restrict__ sat, int H, int W,
+__global__ __launch_bounds__(NT) void k_cand_front(const int3* __restrict__ sat, int H, int W,
                                                    const float4* __restrict__ boxes, const int32_t* __restrict__ img,
                                                    const float* __restrict__ w1, const _Float16* __restrict__ w1h,
                                                    const float* __restrict__ b1, const float* __restrict__ a1,
@@ -1787,9 +1787,9 @@ __global__ __launch_bounds__(NT) void k_cand_front(const int4* __restrict__ sat,
     }
     // crop bins from the SAT: every thread issues all of its corner loads before using any
     // (the gathers are latency-bound; PIX * 4 loads in flight per thread)
-    const int4* sk = sat + (int64_t)img[k] * (H + 1) * (W + 1);
+    const int3* sk = sat + (int64_t)img[k] * (H + 1) * (W + 1);
     if (!(dbg & 1)) {
-        int4 cn[PIX][4];
+        int3 cn[PIX][4];
         int kh[PIX], kw[PIX];
 #pragma unroll
         for (int j = 0; j < PIX; j++) {
@@ -1799,8 +1799,8 @@ __global__ __launch_bounds__(NT) void k_cand_front(const int4* __restrict__ sat,
             const int xs = (q * wc) / S, xe = ((q + 1) * wc + S - 1) / S;
             kh[j] = ye - ys;
             kw[j] = xe - xs;
-            const int4* a = sk + (int64_t)(y0 + ys) * (W + 1) + x0;
-            const int4* b = sk + (int64_t)(y0 + ye) * (W + 1) + x0;
+            const int3* a = sk + (int64_t)(y0 + ys) * (W + 1) + x0;
+            const int3* b = sk + (int64_t)(y0 + ye) * (W + 1) + x0;
             cn[j][0] = a[xs];
             cn[j][1] = a[xe];
             cn[j][2] = b[xs];
@@ -1810,7 +1810,7 @@ __global__ __launch_bounds__(NT) void k_cand_front(const int4* __restrict__ sat,
         for (int j = 0; j < PIX; j++) {
             const int i = tid + j * NT;
             if (i < S * S) {
-                const int4 &a = cn[j][0], &b = cn[j][1], &c = cn[j][2], &d = cn[j][3];
+                const int3 &a = cn[j][0], &b = cn[j][1], &c = cn[j][2], &d = cn[j][3];
                 const float r = bin_avg(d.x - b.x - c.x + a.x, kh[j], kw[j]);
                 const float g = bin_avg(d.y - b.y - c.y + a.y, kh[j], kw[j]);
                 const float bl = bin_avg(d.z - b.z - c.z + a.z, kh[j], kw[j]);
@@ -1951,7 +1951,7 @@ __global__ __launch_bounds__(NT) void k_cand_front(const int4* __restrict__ sat,
 
 int cand_front_side(bool onet) { return onet ? 23 : 11; }
 
-void launch_cand_front(bool onet, const int4* sat, int H, int W, const float4* boxes, const int32_t* img, int64_t n,
+void launch_cand_front(bool onet, const int3* sat, int H, int W, const float4* boxes, const int32_t* img, int64_t n,
                        const float* w1, const _Float16* w1h, const float* b1, const float* a1, float* out, int32_t* err,
                        hipStream_t st, int* ovf) {
     if (n <= 0) return;

@@ -655,7 +655,7 @@ static void run_candidates_sp(Mtcnn& m, bool onet, const void* x0, int64_t n, fl
 // deferred != null: the caller zeroed d_ovf / err in the stage's opening launch and reads the guard
 // back with its compaction sync (*deferred = true when the guarded split path ran); it then calls
 // cand_rerun_fp32 if the guard tripped.
-static void cand_nets(Mtcnn& m, bool onet, const int4* sat, int H, int W, const float4* boxes, const int32_t* img,
+static void cand_nets(Mtcnn& m, bool onet, const int3* sat, int H, int W, const float4* boxes, const int32_t* img,
                       int64_t n, float4* reg, float* lm, float* prob, int32_t* err, bool* deferred = nullptr) {
     if (n <= 0) return;
     hipStream_t st = m.st;
@@ -757,7 +757,7 @@ static void d2h_sync(void* dst, const void* src, size_t bytes, hipStream_t st) {
 
 // the guarded split path tripped (an operand reached the fp16 range): the stage's nets again on
 // the fp32 path (the error counter recounts out-of-frame candidates)
-static void cand_rerun_fp32(Mtcnn& m, bool onet, const int4* sat, int H, int W, const float4* boxes,
+static void cand_rerun_fp32(Mtcnn& m, bool onet, const int3* sat, int H, int W, const float4* boxes,
                             const int32_t* img, int64_t n, float4* reg, float* lm, float* prob, int32_t* err) {
     hipStream_t st = m.st;
     const int net = onet ? 1 : 0;
@@ -856,7 +856,7 @@ static void detect(Mtcnn& m, const uint8_t* frames, int on_dev, int B, int H, in
     // tile kernel their long serial bin sums would leave a few workgroups as a long tail.
     // summed-area table of the preprocessed frames: O(1) exact bin sums for the downsampled
     // levels and the stage-2/3 candidate crops
-    int4* sat = m.ar.get<int4>(S_SAT, (size_t)B * (H + 1) * (W + 1));
+    int3* sat = m.ar.get<int3>(S_SAT, (size_t)B * (H + 1) * (W + 1));
     launch_sat(fr, fstride, rstride, B, H, W, sat, st, d_cnt, NL + 4);
     {
         // split mode: every downsampled level is precomputed as fp16 split pixels (12 B; k_pnet's
@@ -1220,7 +1220,7 @@ int vtf_mtcnn_pnet_level(vtf_mtcnn_t h, const uint8_t* d_frames, int B, int H, i
         VTF_CHECK((int64_t)(L.lh + 1) * H < ((int64_t)1 << 31) && (int64_t)(L.lw + 1) * W < ((int64_t)1 << 31),
                   VTF_E_LIMIT, "mtcnn: pyramid level too large for PNet's 32-bit bin math");
         if ((int64_t)H > 2 * (int64_t)lh) {
-            int4* sat = h->m.ar.get<int4>(S_SAT, (size_t)B * (H + 1) * (W + 1));
+            int3* sat = h->m.ar.get<int3>(S_SAT, (size_t)B * (H + 1) * (W + 1));
             launch_sat(d_frames, frame_stride, row_stride, B, H, W, sat, h->m.st);
             float* pre = h->m.ar.get<float>(S_PRE, (int64_t)B * 3 * lh * lw);
             launch_resample_sat(sat, B, H, W, lh, lw, pre, h->m.st);
@@ -1243,7 +1243,7 @@ int vtf_mtcnn_resample(vtf_mtcnn_t h, const uint8_t* d_frames, int B, int H, int
                        int64_t row_stride, int lh, int lw, float* d_out) {
     return guarded_on(h ? h->m.device : -1, [&] {
         VTF_CHECK(h && d_frames && d_out, VTF_E_ARG, "null argument");
-        int4* sat = h->m.ar.get<int4>(S_SAT, (size_t)B * (H + 1) * (W + 1));
+        int3* sat = h->m.ar.get<int3>(S_SAT, (size_t)B * (H + 1) * (W + 1));
         launch_sat(d_frames, frame_stride, row_stride, B, H, W, sat, h->m.st);
         launch_resample_sat(sat, B, H, W, lh, lw, d_out, h->m.st);
         VTF_HIP(hipStreamSynchronize(h->m.st));
