@@ -509,6 +509,24 @@ def gen_shapes():
     print('shapes', {k: v.shape for k, v in out.items()})
 
 
+def gen_b1():
+    """BASELINE config 1's shape: MTCNN on 720p frames one at a time (det-batch 1) at the
+    RealMTCNN default min_face_size 5 -- four single-frame calls (seeds 110..113); with one image
+    per call every batched_nms segment is the whole call."""
+    load_ref()
+    m = importlib.import_module('ref_vtf.detectors.mtcnn')
+    net = _load(m.MTCNN('cpu'), synth.make_params('mtcnn'))
+    out = {'seeds': np.arange(110, 114)}
+    for seed in out['seeds']:
+        frames = synth.make_frames(1, seed=int(seed))
+        with torch.inference_mode():
+            res, ldm = net(list(frames), 5, return_landmarks=True)
+        out['b1_%d_boxes' % seed] = res[0].astype(np.float32)
+        out['b1_%d_landmarks' % seed] = ldm[0].astype(np.float32) if len(ldm) else np.zeros((0, 5, 2), np.float32)
+        print('b1 seed', seed, res[0].shape)
+    np.savez_compressed(os.path.join(HERE, 'b1.npz'), **out)
+
+
 # BASELINE config 5 chain: YOLO on 1080p frames -> box filter/adjust -> ViT-L on the crops ->
 # cosine dedupe -> KMeans k=2..16 + scores; bench settings of the box filter
 # (frames = synth.make_frame_sets(sets, per_set, 1080, 1920, seed, faces_per_frame): 128 frames)
@@ -782,6 +800,6 @@ def gen_boxes():
 
 if __name__ == '__main__':
     which = sys.argv[1:] or ['mtcnn', 'facenet', 'vit', 'grouping', 'yolo', 'kmeans', 'rcnn', 'dupes', 'boxes', 'shapes', 'chain',
-                             'scale', 'c3', 'iom']
+                             'scale', 'c3', 'iom', 'b1']
     for w in which:
         globals()['gen_' + w]()

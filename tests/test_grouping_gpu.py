@@ -18,26 +18,56 @@ def g():
 def test_cosine_dedupe_vs_golden(g):
     from videotofaces import dupes
     mins, inds = dupes.cosine_dedupe_device(torch.from_numpy(g['X']).cuda())
-    np.testing.assert_allclose(mins, g['dedupe_mins'], atol=1e-5, rtol=0)
+    np.testing.assert_array_equal(mins, g['dedupe_mins'])
     np.testing.assert_array_equal(inds, g['dedupe_inds'])
     keep = np.nonzero(~(mins <= 0.25))[0]
     np.testing.assert_array_equal(keep, g['dedupe_keep'])
 
 
-def test_cosine_dedupe_large_vs_oracle():
+@pytest.mark.parametrize('D,valu', [(512, '0'), (512, '1'), (1000, '0'), (1024, '0')])
+def test_cosine_dedupe_large_vs_oracle(D, valu, monkeypatch):
+    """mins and argmins bit-exact vs the pinned restatement of sklearn's bits
+    (oracle/grouping_oracle.c), both kernel forms: the fp32-MFMA tiles (K blocks on 4-steps) and
+    the VALU fmaf tiles (VTF_COS_VALU=1; D = 1000 has a K block ending at 724 and also runs the
+    MFMA form since 724 % 4 == 0)."""
     from videotofaces import dupes
     from oracle import grouping as og
+    monkeypatch.setenv('VTF_COS_VALU', valu)
     rng = np.random.default_rng(5)
-    X = rng.normal(0, 1, (3000, 512)).astype(np.float32)
+    X = rng.normal(0, 1, (3000, D)).astype(np.float32)
     X[1500:1510] = X[10:20] + 1e-3
+    X[2000:2003] = X[100]  # exact ties: the first index wins, as numpy's argmin
     X[7] = 0  # zero-norm row (sklearn normalize maps the norm to 1)
     mins, inds = dupes.cosine_dedupe_device(torch.from_numpy(X).cuda())
     rm, ri = og.cosine_dedupe(X)
-    np.testing.assert_allclose(mins, rm, atol=1e-5)
-    D = og.cosine_lower(X)
-    rows = np.nonzero(inds != ri)[0]
-    # argmin may differ only where two earlier faces are within fp32 GEMM rounding
-    assert np.all(np.abs(D[rows, inds[rows]] - D[rows, ri[rows]]) < 1e-5)
+    np.testing.assert_array_equal(mins, rm)
+    np.testing.assert_array_equal(inds, ri)
+
+
+def test_cosine_dedupe_row_ranges_join():
+    """The row-range entry (vtf_cosine_dedupe_rows, used per rank by cosine_dedupe_sharded) over
+    uneven shards of N = 1000 (not a multiple of 128) joins to the full-range result bit for bit;
+    likewise the silhouette sweep over uneven row splits."""
+    from videotofaces import dupes
+    from videotofaces.kmeans import Grouper
+    rng = np.random.default_rng(9)
+    N = 1000
+    X = rng.normal(0, 1, (N, 256)).astype(np.float32)
+    X[600:650] = X[0:50] + 0.05
+    Xd = torch.from_numpy(X).cuda()
+    fm, fi = dupes.cosine_dedupe_rows(Xd, 0, N)
+    for w in (2, 3, 5):
+        b = dupes.dedupe_shards(N, w)
+        parts = [dupes.cosine_dedupe_rows(Xd, b[r], b[r + 1]) for r in range(w)]
+        np.testing.assert_array_equal(np.concatenate([p[0] for p in parts]), fm)
+        np.testing.assert_array_equal(np.concatenate([p[1] for p in parts]), fi)
+    gr = Grouper('cuda:0')
+    lbs = [gr.kmeans(X, k) for k in (2, 5)]
+    full = gr.silhouette_sweep(X, lbs, 0, N)
+    for cuts in ((0, 333, 1000), (0, 1, 517, 999, 1000)):
+        parts = [gr.silhouette_sweep(X, lbs, lo, hi) for lo, hi in zip(cuts[:-1], cuts[1:])]
+        for i in range(len(lbs)):
+            np.testing.assert_array_equal(np.concatenate([p[i] for p in parts]), full[i])
 
 
 def test_classify_vs_golden(g):
@@ -119,26 +149,21 @@ def scale():
 
 
 def test_scale_dedupe_30k(scale):
-    """remove_dupes_overall('enc') at N = 30k on realistic embeddings: keep set exact except rows
-    whose reference minimum lies within 1e-5 (the fp32 GEMM noise of either side) of the 0.25
-    threshold; argmin exact except where the two nearest earlier faces are within 1e-5 of each
-    other (tie rule: the device resolves exact float ties to the lowest index, as numpy's argmin
-    does; it cannot order two distances that only the reference's BLAS rounding separates)."""
+    """remove_dupes_overall('enc') at N = 30k on realistic embeddings (D = 1024): mins, argmins
+    and the keep set bit-exact vs sklearn's own output (the golden)."""
+    import time
     from videotofaces import dupes
     g, X = scale
-    mins, inds = dupes.cosine_dedupe_device(torch.from_numpy(X).cuda())
-    rm, ri = g['dedupe_mins'], g['dedupe_inds']
-    np.testing.assert_allclose(mins, rm, rtol=0, atol=1e-5)
-    far = np.abs(rm - 0.25) > 1e-5
-    keep = ~(mins <= 0.25)
-    np.testing.assert_array_equal(np.nonzero(keep & far)[0], np.setdiff1d(g['dedupe_keep'], np.nonzero(~far)[0]))
-    moved = np.nonzero(inds != ri)[0]
-    # every differing argmin must point at a face the reference puts within 1e-5 of its minimum
-    Xn = X / np.maximum(np.linalg.norm(X, axis=1, keepdims=True), 1e-30)
-    d_alt = 1 - np.einsum('ij,ij->i', Xn[moved], Xn[inds[moved]])
-    assert np.all(np.abs(d_alt - rm[moved]) < 1e-5), moved
-    print('kept %d of %d; rows within 1e-5 of the threshold %d; argmin near-ties resolved differently %d'
-          % (int(keep.sum()), len(X), int((~far).sum()), len(moved)))
+    Xd = torch.from_numpy(X).cuda()
+    dupes.cosine_dedupe_device(Xd)
+    torch.cuda.synchronize()
+    t = time.time()
+    mins, inds = dupes.cosine_dedupe_device(Xd)
+    dt = time.time() - t
+    np.testing.assert_array_equal(mins, g['dedupe_mins'])
+    np.testing.assert_array_equal(inds, g['dedupe_inds'])
+    np.testing.assert_array_equal(np.nonzero(~(mins <= 0.25))[0], g['dedupe_keep'])
+    print('kept %d of %d, exact; %.1f ms' % (int((~(mins <= 0.25)).sum()), len(X), dt * 1e3))
 
 
 def test_scale_kmeans_sweep_20k(scale):

@@ -104,20 +104,20 @@ def _random_boxes(n, n_img, seed, grid=False):
 
 @pytest.mark.parametrize('n,n_img,thr,grid', [(0, 1, 0.5, False), (1, 1, 0.5, False), (300, 4, 0.5, True),
                                               (1000, 3, 0.7, False), (1001, 3, 0.7, False), (5000, 16, 0.5, True),
-                                              (3000, 1, 0.45, False)])
+                                              (3000, 1, 0.45, False), (20000, 7, 0.3, True)])
 def test_batched_nms_exact(n, n_img, thr, grid):
     from videotofaces.detectors.mtcnn import batched_nms
     from oracle import nms as onms
     b, s, i = _random_boxes(n, n_img, seed=n + n_img, grid=grid)
     ref = onms.batched_nms(b, s, i, thr)
     got = batched_nms(b.cuda(), s.cuda(), i.cuda(), thr).cpu()
+    # exact order on both paths: above 1000 boxes (vanilla) the reference's final order is
+    # torch's unstable CPU sort, whose order among the tied scores (10 % of the boxes share 0.75)
+    # the library reproduces (nms.hpp torch_unstable_desc_order)
+    assert got.tolist() == ref.tolist()
     if n > 1000:
-        # vanilla path: the reference's final order comes from torch's unstable sort; the
-        # keep SET is exact, the order among equal scores is implementation-defined
-        assert sorted(got.tolist()) == sorted(ref.tolist())
-        assert torch.equal(s[got], s[ref])
-    else:
-        assert got.tolist() == ref.tolist()
+        ks = s[ref]
+        print('vanilla path: %d kept, %d equal-score neighbours' % (len(ref), int((ks[1:] == ks[:-1]).sum())))
 
 
 def _match(res, counts, boxes, atol):

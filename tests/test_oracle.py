@@ -104,6 +104,32 @@ def test_oracle_facenet_vs_golden():
     np.testing.assert_allclose(y, gf['emb'], atol=1e-6, rtol=0)
 
 
+def _skylakex_blas():
+    import threadpoolctl
+    return any(d.get('internal_api') == 'openblas' and d.get('architecture') == 'SkylakeX'
+               and 'numpy' in d.get('filepath', '') for d in threadpoolctl.threadpool_info())
+
+
+@pytest.mark.parametrize('N,D', [(200, 512), (150, 1024), (120, 768), (100, 1000), (90, 200)])
+def test_cosine_restatement_vs_sklearn(N, D):
+    """oracle/grouping_oracle.c == sklearn cosine_distances bit for bit on every matrix entry
+    (the orders were measured on numpy's OpenBLAS SkylakeX kernels: the comparison runs only
+    where sklearn runs on those kernels; the goldens pin the same bits everywhere else)."""
+    if not _skylakex_blas():
+        pytest.skip('numpy BLAS is not OpenBLAS SkylakeX: sklearn bits differ from the pinned ones')
+    from oracle import grouping as og
+    rng = np.random.default_rng(D)
+    X = rng.normal(0, 1, (N, D)).astype(np.float32)
+    X[N // 2:N // 2 + 5] = X[3:8] + np.float32(1e-3)
+    X[1] = 0
+    ref = og.cosine_lower_sklearn(X)
+    got = og.cosine_lower(X)
+    np.testing.assert_array_equal(got, ref)
+    mins, inds = og.cosine_dedupe(X)
+    np.testing.assert_array_equal(mins, ref.min(1))
+    np.testing.assert_array_equal(inds, ref.argmin(1))
+
+
 def test_oracle_grouping_vs_golden():
     from oracle import grouping as og
     gg = np.load(os.path.join(GOLDEN, 'grouping.npz'))

@@ -1,8 +1,8 @@
 """GPU parity at the BENCHMARKED shapes (BASELINE configs 2-5), against golden vectors made by
 the reference's own modules (tests/golden/make_golden.py gen_shapes / gen_chain):
 
-* MTCNN 720p, det-batch 16 at min_face_size 5 (config 2) and det-batch 4 at 20 (main.py:18's
-  default batch): batched_nms offsets depend on the batch composition (mtcnn.py:196,205,219);
+* MTCNN 720p, det-batch 16 at min_face_size 5 (config 2), det-batch 4 at 20 (main.py:18's
+  default batch) and det-batch 1 at 5 (config 1): batched_nms offsets depend on the batch composition (mtcnn.py:196,205,219);
 * YOLOv3 on 1080p frames, det-batch 4 (configs 3/5 detector at the config-5 frame size);
 * FaceNet fp32 at batch 128 and ViT-L at batch 8 and 128 (the multi-tile / split-K GEMM paths
   that run at enc-batch 128);
@@ -47,6 +47,23 @@ def test_mtcnn_benchmark_batches(g, name, n, seed, ms):
     res = MTCNN('cuda:0')(torch.from_numpy(frames).cuda(), ms)
     np.testing.assert_array_equal([r.shape[0] for r in res], g[name + '_counts'])
     np.testing.assert_allclose(np.concatenate(res), g[name + '_boxes'], rtol=1e-5, atol=2e-3)
+
+
+def test_mtcnn_det_batch1_720p():
+    """BASELINE config 1's shape: MTCNN on single 720p frames (det-batch 1, min_face_size 5),
+    four calls, against the reference module (tests/golden/make_golden.py gen_b1): counts exact,
+    boxes 2e-3 px, landmarks 2e-3 px."""
+    from videotofaces import synth
+    from videotofaces.detectors.mtcnn import MTCNN
+    gb = np.load(os.path.join(GOLDEN, 'b1.npz'))
+    m = MTCNN('cuda:0')
+    for seed in gb['seeds']:
+        frames = synth.make_frames(1, seed=int(seed))
+        res, ldm = m(torch.from_numpy(frames).cuda(), 5, return_landmarks=True)
+        ref = gb['b1_%d_boxes' % seed]
+        assert res[0].shape == ref.shape, (seed, res[0].shape, ref.shape)
+        np.testing.assert_allclose(res[0], ref, rtol=1e-5, atol=2e-3)
+        np.testing.assert_allclose(ldm[0], gb['b1_%d_landmarks' % seed], rtol=1e-5, atol=2e-3)
 
 
 def test_mtcnn_b16_device_crops(g):
@@ -141,8 +158,8 @@ def test_config3_det_batch32(c3, precision):
     """BASELINE config 3's det-batch: YOLOv3 on 32 720p frames in ONE call (the bench's tile /
     grid / split-K choices for B = 32) -> device box post-processing -> FaceNet on the device
     crops, against the reference modules (tests/golden/make_golden.py gen_c3): counts exact,
-    boxes 1e-2 px, scores 1e-4; crop rectangles exact on every frame the golden does not flag
-    (a coordinate within 2e-3 px of an integer or a score within 1e-4 of min_score); FaceNet on
+    boxes 1e-2 px, scores 1e-4; crop rectangles exact on every frame, including those the golden
+    flags (a coordinate within 2e-3 px of an integer or a score within 1e-4 of min_score); FaceNet on
     the golden rectangles fp32 within 1e-4, bf16 (the config's encoder precision) cos >= 0.998."""
     import json
     from videotofaces import synth, _native as nat
@@ -159,9 +176,11 @@ def test_config3_det_batch32(c3, precision):
                                                         c['square']))
     got, ref = d.cpu().numpy(), c3['rects']
     flagged = set(c3['flagged_frames'].tolist())
+    # every frame, the flagged ones included (their outcome is reported first)
+    same = [f for f in sorted(flagged) if np.array_equal(got[got[:, 0] == f], ref[ref[:, 0] == f])]
+    print('c3 flagged frames %s: identical %s' % (sorted(flagged), same))
     for f in range(c['frames']):
-        if f not in flagged:
-            np.testing.assert_array_equal(got[got[:, 0] == f], ref[ref[:, 0] == f], err_msg='frame %d' % f)
+        np.testing.assert_array_equal(got[got[:, 0] == f], ref[ref[:, 0] == f], err_msg='frame %d' % f)
     rects = torch.from_numpy(ref).cuda()
     emb = InceptionResnetV1('cuda:0', precision='fp32').encode_crops(frames, rects).cpu().numpy()
     np.testing.assert_allclose(emb, c3['emb'], rtol=0, atol=1e-4)
@@ -199,9 +218,10 @@ def test_vit_l_batches(g, precision):
 def test_config5_chain(chain, precision):
     """Config 5 end to end on 128 1080p frames (488 faces): YOLO -> device box post-processing
     -> ViT-L on device crops -> fused cosine dedupe -> KMeans k=2..16 + scores on the DEDUPED
-    rows (main.py:72-77).  Crop rectangles are exact on every frame the golden does not flag
-    (a box coordinate within 2e-3 px of an integer or a score within 1e-4 of min_score: the
-    detector's fp32 tolerance decides those floors/ceils and gates); the encoder then runs on the
+    rows (main.py:72-77).  Crop rectangles are exact on every frame, including the ones the
+    golden flags (a box coordinate within 2e-3 px of an integer or a score within 1e-4 of
+    min_score, where the detector's fp32 tolerance could decide a floor or a gate; the count of
+    those that match is reported first); the encoder then runs on the
     golden rectangles, so the grouping half is checked on the reference's rows."""
     from videotofaces import synth, dupes
     from videotofaces.detection import detect_crops
@@ -219,20 +239,19 @@ def test_config5_chain(chain, precision):
         parts.append(d)
     got = torch.cat(parts).cpu().numpy()
     flagged = set(chain['flagged_frames'].tolist())
-    same_flagged = 0
+    same_flagged = sum(int(np.array_equal(got[got[:, 0] == f], chain['rects'][chain['rects'][:, 0] == f]))
+                       for f in flagged)
+    print('flagged frames %d, of which identical %d' % (len(flagged), same_flagged))
     for f in range(len(frames)):
         a, b = got[got[:, 0] == f], chain['rects'][chain['rects'][:, 0] == f]
-        if f in flagged:
-            same_flagged += int(a.shape == b.shape and np.array_equal(a, b))
-        else:
-            np.testing.assert_array_equal(a, b, err_msg='frame %d' % f)
-    print('flagged frames %d, of which identical %d' % (len(flagged), same_flagged))
+        np.testing.assert_array_equal(a, b, err_msg='frame %d' % f)
     enc = ViT('cuda:0', synth.make_params('vit_l'), isL=True, precision=precision)
     X = enc.encode_crops(frames, torch.from_numpy(chain['rects']).cuda())
     np.testing.assert_allclose(X.cpu().numpy(), chain['X'], rtol=0, atol=1e-4)
-    mins, inds = dupes.cosine_dedupe_device(X)
-    np.testing.assert_allclose(mins, chain['dedupe_mins'], rtol=0, atol=1e-5)
+    mins, inds = dupes.cosine_dedupe_device(torch.from_numpy(chain['X']).cuda())
+    np.testing.assert_array_equal(mins, chain['dedupe_mins'])
     np.testing.assert_array_equal(inds, chain['dedupe_inds'])
+    mins, inds = dupes.cosine_dedupe_device(X)  # on the device embeddings (within 1e-4)
     np.testing.assert_array_equal(np.nonzero(~(mins <= 0.25))[0], chain['dedupe_keep'])
     ks = [int(k) for k in chain['k']]
     # on the golden's own embeddings (bit-exact input) the labels equal sklearn's (1 OpenMP
@@ -250,16 +269,15 @@ def test_config5_chain(chain, precision):
 
 
 def test_cosine_dedupe_keep_set_10k():
-    """remove_dupes_overall('enc') at N = 10k (configs 4/5 scale): keep set exact vs the
-    reference's formula (sklearn cosine_distances + strict lower triangle); argmin exact wherever
-    the best earlier face beats the runner-up by more than fp32 GEMM noise (1e-5)."""
+    """remove_dupes_overall('enc') at N = 10k (configs 4/5 scale): mins, argmins and the keep set
+    bit-exact vs the pinned restatement of sklearn's bits (oracle/grouping_oracle.c)."""
     from oracle import grouping as og
     from videotofaces import dupes
     rng = np.random.default_rng(31)
     N, D = 10000, 512
     X = rng.normal(0, 1, (N, D)).astype(np.float32)
     # near-duplicates of earlier rows at cosine distances spread over 0.02 .. 0.5 (both sides of
-    # the 0.25 threshold), away from the threshold by more than the noise
+    # the 0.25 threshold)
     src = rng.integers(0, N // 2, 600)
     dst = rng.choice(np.arange(N // 2, N), 600, replace=False)
     for s_, d_ in zip(src, dst):
@@ -267,15 +285,8 @@ def test_cosine_dedupe_keep_set_10k():
         noise = rng.normal(0, 1, D).astype(np.float32)
         X[d_] = X[s_] + noise * np.float32(np.sqrt(2 * t / (1 - t)) * 0.999)  # ~ distance t
     mins, inds = dupes.cosine_dedupe_device(torch.from_numpy(X).cuda())
-    Dm = og.cosine_lower(X)
-    rm, ri = Dm.min(1), Dm.argmin(1)
-    np.testing.assert_allclose(mins, rm, rtol=0, atol=1e-5)
-    # the keep decision (mins <= 0.25) is exact for every row whose reference minimum is not
-    # within the 1e-5 distance noise of the threshold (the test reports how many are)
-    far = np.abs(rm - 0.25) > 1e-5
-    np.testing.assert_array_equal((mins <= 0.25)[far], (rm <= 0.25)[far])
-    print('rows within 1e-5 of the threshold:', int((~far).sum()))
-    part = np.partition(Dm, 1, axis=1)
-    clear = (part[:, 1] - part[:, 0]) > 1e-5
-    np.testing.assert_array_equal(inds[clear], ri[clear])
-    print('dupes', int((rm <= 0.25).sum()), 'rows with a clear argmin', int(clear.sum()), 'of', N)
+    rm, ri = og.cosine_dedupe(X)
+    np.testing.assert_array_equal(mins, rm)
+    np.testing.assert_array_equal(inds, ri)
+    np.testing.assert_array_equal(mins <= 0.25, rm <= 0.25)
+    print('dupes', int((rm <= 0.25).sum()), 'of', N)

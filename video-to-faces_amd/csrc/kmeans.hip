@@ -23,6 +23,7 @@
 #include <vector>
 
 #include "common.hpp"
+#include "sk_order.hpp"
 
 namespace vtf {
 
@@ -121,21 +122,7 @@ __global__ __launch_bounds__(256) void k_sqdist_rows(const float* __restrict__ X
 //           between 448 and 896 rounded up to 16), sequential fma per block from 0, and
 //           pd = pd - 2 acc after every block.
 // (Exact for D % 16 == 0; other D follow the same rules without that verification.)
-__device__ inline float np_einsum_sq(const float* __restrict__ c, int D) {
-    float l[4] = {0.f, 0.f, 0.f, 0.f};
-    int t = 0;
-    for (; D - t >= 16; t += 16)
-        for (int q = 3; q >= 0; q--)
-#pragma unroll
-            for (int u = 0; u < 4; u++) l[u] = __fadd_rn(__fmul_rn(c[t + 4 * q + u], c[t + 4 * q + u]), l[u]);
-    for (; t < D; t += 4)
-#pragma unroll
-        for (int u = 0; u < 4; u++) {
-            const float v = t + u < D ? c[t + u] : 0.f;
-            l[u] = __fadd_rn(__fmul_rn(v, v), l[u]);
-        }
-    return __fadd_rn(__fadd_rn(l[0], l[1]), __fadd_rn(l[2], l[3]));
-}
+// (np_einsum_sq and the K blocking live in sk_order.hpp.)
 
 __global__ void k_csq(const float* __restrict__ C, int k, int D, float* __restrict__ csq) {
     int j = blockIdx.x * blockDim.x + threadIdx.x;
@@ -169,7 +156,7 @@ __global__ __launch_bounds__(256) void k_estep(const float* __restrict__ X, int6
         for (int u = 0; u < 16; u++) lane[u] = 0.f;
         float acc = 0.f, pd = j < k ? csq[j] : 0.f;
         // K blocks of the blocked kernel (the small kernel ignores them)
-        int kb_end = D >= 2 * 448 ? 448 : (D > 448 ? ((D / 2 + 15) / 16) * 16 : D);
+        int kb_end = blas_kblock(D, false);
         for (int t0 = 0; t0 < D; t0 += ES_K) {
             for (int e = tid; e < ES_R * ES_K; e += 256) {
                 const int rr = e / ES_K, tt = e % ES_K;
@@ -188,8 +175,7 @@ __global__ __launch_bounds__(256) void k_estep(const float* __restrict__ X, int6
                     if (t0 + tt + 1 == kb_end) {  // end of a K block: C += alpha * block
                         pd = fmaf(-2.f, acc, pd);
                         acc = 0.f;
-                        const int rest = D - kb_end;
-                        kb_end += rest >= 2 * 448 ? 448 : (rest > 448 ? ((rest / 2 + 15) / 16) * 16 : rest);
+                        kb_end += blas_kblock(D - kb_end, false);
                     }
                 }
             }

@@ -39,8 +39,10 @@ __global__ void k_nms_prep(const uint8_t* __restrict__ mail, uint8_t* __restrict
         for (int i = threadIdx.x; i < bytes / 4; i += blockDim.x) dst[i] = src[i];
         const int64_t* cn = (const int64_t*)(mail + o_cn);
         const uint8_t* van = mail + o_van;
-        for (int c = threadIdx.x; c < C; c += blockDim.x)
+        for (int c = threadIdx.x; c < C; c += blockDim.x) {
             if (van[c] || cn[c] == 0) call_max[c] = 0.f;
+            ovf_flag[1 + c] = 0;  // tie flags
+        }
         return;
     }
     const int c = ((const int32_t*)(mail + o_trick))[blockIdx.x - 1];
@@ -379,6 +381,18 @@ __global__ void k_call_kept(const int64_t* __restrict__ call_start, const int32_
     out[c] = hi - lo;  // (out: the host mailbox)
 }
 
+// vanilla calls whose kept set holds two equal scores (adjacent in the stable output order):
+// there torch's unstable sort may order them differently, the host reorders that call
+__global__ void k_tie_flags(const int32_t* __restrict__ keep, const int32_t* __restrict__ incl, int64_t N,
+                            const float* __restrict__ scores, const int32_t* __restrict__ elem_call,
+                            const uint8_t* __restrict__ call_van, int32_t* __restrict__ tie) {
+    const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x + 1;
+    if (N == 0 || p >= incl[N - 1]) return;
+    const int32_t a = keep[p - 1], b = keep[p];
+    const int32_t c = elem_call[b];
+    if (elem_call[a] == c && call_van[c] && scores[a] == scores[b]) tie[c] = 1;  // (tie: the host mailbox)
+}
+
 // host staging of several small tables for one H2D copy (16-B aligned members)
 struct HostPack {
     std::vector<uint8_t> buf;
@@ -469,8 +483,9 @@ void nms_multi(Arena& ar, const float* d_boxes, const float* d_scores, const int
     const int tbytes = (int)((pk.buf.size() + 3) & ~(size_t)3);
     Arena::Mail mt = ar.mail(40, tbytes);
     std::memcpy(mt.h, pk.buf.data(), pk.buf.size());
-    // results mailbox: kept count per call, then the scan's overflow flag (zeroed by k_nms_prep)
-    Arena::Mail mr = ar.mail(41, (size_t)(C + 1) * 4);
+    // results mailbox: kept count per call, the scan's overflow flag (zeroed by k_nms_prep), then
+    // a tie flag per call (zeroed by k_nms_prep)
+    Arena::Mail mr = ar.mail(41, (size_t)(2 * C + 1) * 4);
     uint8_t* d_t1 = (uint8_t*)ar.get(40, tbytes);
     const int64_t* d_cbeg = (const int64_t*)(d_t1 + o_cbeg);
     const uint8_t* d_van = d_t1 + o_van;
@@ -538,9 +553,29 @@ void nms_multi(Arena& ar, const float* d_boxes, const float* d_scores, const int
     k_compact<<<cdiv(N, 256), 256, 0, st>>>(ord, flag, incl, N, d_keep);
     k_seg_bounds<<<cdiv(C + 1, 256), 256, 0, st>>>(k1, N, d_callhi, C, d_sstart);
     k_call_kept<<<cdiv(C, 256), 256, 0, st>>>(d_sstart, incl, C, d_res);
+    bool any_van = false;
+    for (int c = 0; c < C; c++) any_van |= vanilla[c] != 0;
+    if (any_van && N > 1)
+        k_tie_flags<<<cdiv(N - 1, 256), 256, 0, st>>>(d_keep, incl, N, d_scores, d_elem_call, d_van, d_res + C + 1);
     VTF_HIP(hipStreamSynchronize(st));
     VTF_CHECK(h_res[C] == 0, VTF_E_LIMIT, "nms_multi: a segment exceeds 1.3M boxes");
     for (int c = 0; c < C; c++) nkeep[c] = h_res[c];
+    // torch's unstable final sort on the (rare) vanilla calls with equal kept scores
+    int64_t off = 0;
+    for (int c = 0; c < C; c++) {
+        if (any_van && h_res[C + 1 + c] && nkeep[c] > 1) {
+            std::vector<int32_t> hk(nkeep[c]);
+            std::vector<float> hs(call_n[c]);
+            VTF_HIP(hipMemcpyAsync(hk.data(), d_keep + off, nkeep[c] * 4, hipMemcpyDeviceToHost, st));
+            VTF_HIP(hipMemcpyAsync(hs.data(), d_scores + call_beg[c], call_n[c] * 4, hipMemcpyDeviceToHost, st));
+            VTF_HIP(hipStreamSynchronize(st));
+            const int64_t b = call_beg[c];
+            torch_unstable_desc_order(hk, [&](int32_t e) { return hs[e - b]; });
+            VTF_HIP(hipMemcpyAsync(d_keep + off, hk.data(), nkeep[c] * 4, hipMemcpyHostToDevice, st));
+            VTF_HIP(hipStreamSynchronize(st));
+        }
+        off += nkeep[c];
+    }
 }
 
 }  // namespace vtf

@@ -687,15 +687,7 @@ static int64_t rpn_proposals(Rcnn& R, float* const heads[R_LEVELS], const RMap P
         // order and torch's default (unstable) CPU sort: std::sort of (score, position) pairs with
         // ATen's KeyValueCompDesc (SortingKernel.cpp) -- its tie order reproduced exactly (checked
         // against torch.sort on tie-heavy inputs, scripts/torch_sigmoid_order.py)
-        std::sort(hk.begin(), hk.end());
-        std::vector<std::pair<float, int64_t>> kv(kn);
-        for (int64_t t = 0; t < kn; t++) kv[t] = {hs[hk[t]], t};
-        std::sort(kv.begin(), kv.end(), [](const std::pair<float, int64_t>& a, const std::pair<float, int64_t>& b) {
-            return (std::isnan(a.first) && !std::isnan(b.first)) || (a.first > b.first);
-        });
-        std::vector<int32_t> ord(kn);
-        for (int64_t t = 0; t < kn; t++) ord[t] = hk[kv[t].second];
-        hk.swap(ord);
+        torch_unstable_desc_order(hk, [&](int32_t e) { return hs[e]; });
     }
     // keep[imidx[keep] == i][:1000] for each image, concatenated (rcnn.py:80)
     std::vector<int32_t> sel, simg;
