@@ -49,7 +49,6 @@ F16X_PEAK_TFLOPS = round(BF16_PEAK_TFLOPS / 3, 1)
 # bf16x3 operands (three bf16 terms each): six bf16 products per fp32-grade product
 X3_PEAK_TFLOPS = round(BF16_PEAK_TFLOPS / 6, 1)
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E (MI355X_MICROARCH.md)
-LBL_BYTES_PER_FLOP = 2075e6 / 38.66e9  # PNet layer-by-layer fp32 bytes per FLOP
 VIT_GFLOP = {'vit_b': 11.27, 'vit_l': 39.78}  # per face at 128x128
 ENC_NAMES = {'facenet': 'FaceNet', 'vit_b': 'ViT-B/16', 'vit_l': 'ViT-L/16'}
 CONFIGS = {
@@ -58,7 +57,7 @@ CONFIGS = {
                det_batch=32),
     'c4': dict(det_model='none', enc_model='vit_l', enc_precision='f16x', frame='224'),
     'c5': dict(det_model='yolo', det_precision='x3', enc_model='vit_l', enc_precision='f16x', frame='1080p',
-               det_batch=32, grouping=True),
+               det_batch=32, grouping=True, pool=0),
 }
 
 
@@ -80,7 +79,9 @@ def parse(argv=None):
                     help='FaceNet: bf16 | fp32; ViT: f16x (guarded split-fp16) | fp32')
     ap.add_argument('--frame', choices=['720p', '1080p', '224'])
     ap.add_argument('--min-face-size', type=float, default=5.0)
-    ap.add_argument('--pool', type=int, default=32, help='distinct synthetic frames per rank (cycled)')
+    ap.add_argument('--pool', type=int, default=None,
+                    help='distinct synthetic frames of the global frame sequence, cycled (default 32; c5: 0 = '
+                         'every frame of the run distinct, generated on the device)')
     ap.add_argument('--lanes', type=int, default=3, help='concurrent det-batch pipelines (threads + HIP streams) per GPU')
     ap.add_argument('--sustain-frames', type=int, default=10000,
                     help='frames of the sustained leg (BASELINE config 2: 10k frames), 0 = skip')
@@ -102,6 +103,8 @@ def parse(argv=None):
     if a.det_precision is None:
         a.det_precision = 'fp32'
     a.grouping = preset.get('grouping', False)
+    if a.pool is None:
+        a.pool = preset.get('pool', 32)
     if a.enc_model == 'facenet' and a.enc_precision == 'f16x':
         a.enc_precision = 'bf16'
     if a.enc_model != 'facenet' and a.enc_precision == 'bf16':
@@ -245,35 +248,68 @@ def _make_detector(args, dev, fp32=False):
             os.environ['VTF_MTCNN_FP32'] = old
 
 
+def rank_frames(args, ctx, n_steps, seed=1000):
+    """This rank's part of ONE global synthetic frame sequence: the run's world * n_steps
+    det-batches split by parallel.shard_batches (whole det-batches, rank order = frame order).
+    Returns (frames on the device, offset of the rank's first frame in them, host copy of up to
+    32 of the frames for the CPU-baseline / host-frame / drift legs).
+      pool > 0: the sequence cycles `pool` frames (synth.make_frames, seeded; frame g is pool
+                frame g % pool), kept on the device once;
+      pool = 0: every frame distinct (synth.make_frames_device: frame g's content depends only on
+                (seed, g)), the rank's shard generated on the device."""
+    from videotofaces import synth
+    from videotofaces.parallel import shard_batches
+    B = args.det_batch
+    lo, hi = shard_batches(ctx.world * n_steps * B, B, ctx.rank, ctx.world)
+    if args.pool > 0:
+        pool_n = max(B, args.pool // B * B)
+        frames_np = synth.make_frames(pool_n, args.H, args.W, seed=seed)
+        return torch.from_numpy(frames_np).to(ctx.device), lo % pool_n, frames_np
+    frames = synth.make_frames_device(lo, hi, args.H, args.W, seed=seed, device=ctx.device)
+    return frames, 0, frames[:max(B, 32 // B * B)].cpu().numpy()
+
+
 class DetEncPipeline:
     """L lanes of (detector, encoder, HIP stream) on alternate det-batches from host threads (the
     ctypes calls release the GIL): one lane's host syncs and small stage-2/3 kernels overlap
     another lane's pyramid kernel.  Batches stay whole and independent, so per-batch results are
     exactly the single-lane results.  Detector rows never leave HBM: detect_crops returns device
-    crop rectangles that the lane's encoder consumes in batches of exactly enc_batch."""
+    crop rectangles that the lane's encoder consumes in batches of exactly enc_batch.
+    Step i reads frames [offset + i * B, + B) (modulo the frames held) of `frames`, the rank's
+    shard of the global sequence (rank_frames).  `make_det` / `make_enc` build one lane's
+    detector / encoder (default: the HIP models; tests pass CPU stand-ins)."""
 
-    def __init__(self, args, dev, frames_np):
+    def __init__(self, args, dev, frames, offset, frames_np, make_det=None, make_enc=None):
         self.args, self.dev = args, dev
         self.B = args.det_batch
         self.frames_np = frames_np
-        self.pool_n = frames_np.shape[0]
-        self.frames = torch.from_numpy(frames_np).to(dev)
+        self.frames = frames
+        self.pool_n = frames.shape[0]
+        self.offset = offset
         self.L = max(1, args.lanes)
-        self.dets = [_make_detector(args, dev) for _ in range(self.L)]
-        self.encs = [_make_encoder(args, dev) for _ in range(self.L)]
+        self.make_det = make_det or (lambda: _make_detector(args, dev))
+        self.make_enc = make_enc or (lambda: _make_encoder(args, dev))
+        self.dets = [self.make_det() for _ in range(self.L)]
+        self.encs = [self.make_enc() for _ in range(self.L)]
         self.D = 512 if args.enc_model == 'facenet' else self.encs[0].dim
-        self.streams = [torch.cuda.Stream(dev) for _ in range(self.L)]
-        self.bp = _box_params(args)
+        self.gpu = dev.type == 'cuda'
+        self.streams = [torch.cuda.Stream(dev) if self.gpu else None for _ in range(self.L)]
+        self.bp = _box_params(args) if self.gpu else None
         self.host = None  # host-frame leg: (pinned frames, device ring per lane, slots per lane)
         self.minsize = args.min_face_size
 
+    def _stream(self, lane):
+        import contextlib
+        return torch.cuda.stream(self.streams[lane]) if self.gpu else contextlib.nullcontext()
+
     def detect_step(self, lane, i, det=None):
-        j = (i * self.B) % self.pool_n
         det = det or self.dets[lane]
         if self.host is None:
+            j = (self.offset + i * self.B) % self.pool_n
             src, off = self.frames[j:j + self.B], j
         else:  # frames from pinned host memory: async H2D on the lane stream into a ring slot
             pinned, ring, R = self.host
+            j = (i * self.B) % pinned.shape[0]
             slot = lane * R + (i // self.L) % R
             off = slot * self.B
             ring[off:off + self.B].copy_(pinned[j:j + self.B], non_blocking=True)
@@ -295,7 +331,7 @@ class DetEncPipeline:
         def lane_fn(lane):
             try:
                 enc = self.encs[lane]
-                with torch.cuda.stream(self.streams[lane]):
+                with self._stream(lane):
                     pend, npend, slots = [], 0, []
                     for k in range(lane, n, self.L):
                         if self.host is not None and npend:
@@ -331,7 +367,8 @@ class DetEncPipeline:
         if errs:
             raise errs[0]
         for s in self.streams:
-            s.synchronize()
+            if s is not None:
+                s.synchronize()
         # lane streams -> global (step, face) order
         parts, offs = [], [0] * self.L
         flat = [torch.cat(e) if e else torch.zeros((0, self.D), device=self.dev) for e in lane_embs]
@@ -347,10 +384,13 @@ class DetEncPipeline:
         HIP events on the lane stream (vtf_*_profile)."""
         d = self.dets[0]
         d.profile(True)
-        with torch.cuda.stream(self.streams[0]):
+        stats = []
+        with self._stream(0):
             for i in range(steps):
                 self.detect_step(0, i)
+                stats.append(getattr(d, 'last_stats', None))
         self.streams[0].synchronize()
+        self.solo_stats = [st for st in stats if st is not None]
         return d.profile(False)
 
     def host_frames(self, ring_slots=4):
@@ -542,18 +582,60 @@ def roofline_det(args, pipe, shared, solo):
          'flops_per_launch': fl, 'launches': s_n, 'timing': 'solo leg: one lane, HIP events on its stream',
          'shared': {'avg_launch_ms': round(c_avg, 4), 'achieved': round(c_ach, 3), 'frac': round(c_ach / peak, 4),
                     'launches': c_n, 'concurrent_lanes': pipe.L}}
-    hbm = None
-    if not yolo:
-        # north-star "memory-bound HBM roofline on the detector conv path": SURVEY.md §8d's
-        # layer-by-layer PNet bytes over the same launch time (an equivalent rate; the fused
-        # kernel moves `traffic` bytes)
-        b = fl * LBL_BYTES_PER_FLOP
-        hbm = {'bytes_per_launch': round(b), 'achieved': round(b / (s_avg / 1e3) / 1e9, 1) if s_avg else 0.0,
-               'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
-               'frac': round(b / (s_avg / 1e3) / 1e9 / HBM_PEAK_GBS, 4) if s_avg else 0.0,
-               'shared_frac': round(c_fl / max(1, c_n) * LBL_BYTES_PER_FLOP / (c_avg / 1e3) / 1e9 / HBM_PEAK_GBS, 4)
-               if c_avg else 0.0}
-    return r, hbm
+    return r, None
+
+
+# RNet / ONet FLOPs per candidate (2 x MACs of every conv and dense layer, mtcnn.py:41-109):
+# RNet 24x24: conv1 22^2*28*27, conv2 9^2*48*252, conv3 3^2*64*192, dense 576*128, heads 128*6;
+# ONet 48x48: conv1 46^2*32*27, conv2 21^2*64*288, conv3 8^2*64*576, conv4 3^2*128*256,
+# dense 1152*256, heads 256*16
+RNET_FLOP = 2 * (22 * 22 * 28 * 27 + 9 * 9 * 48 * 252 + 9 * 64 * 192 + 576 * 128 + 128 * 6)
+ONET_FLOP = 2 * (46 * 46 * 32 * 27 + 21 * 21 * 64 * 288 + 64 * 64 * 576 + 9 * 128 * 256 + 1152 * 256 + 256 * 16)
+
+
+def roofline_e2e(args, faces_per_step, ms_per_step, solo, solo_stats):
+    """SURVEY.md §8d's end-to-end bound: faces/s roofline = faces / sum over the stages of
+    max(FLOPs / peak, bytes / HBM BW), per GPU and per step (one det-batch, or one enc-batch for
+    the encoder-only config).  Stage FLOPs are the algorithmic counts (pyramid+PNet from the
+    level plan, RNet / ONet per candidate x the candidates the detector passed in the solo leg,
+    the encoder per face); peaks are the ones the stages compute at (split-fp16 / bf16x3 for
+    the fp32-grade detector convs, the encoder's mode); bytes are the stage's compulsory input
+    (frames, or the uint8 crops).  `frac` = achieved faces/s per GPU / roofline faces/s."""
+    stages = []
+
+    def add(name, flops, peak, nbytes):
+        t = max(flops / (peak * 1e12), nbytes / (HBM_PEAK_GBS * 1e9))
+        stages.append({'stage': name, 'gflop': round(flops / 1e9, 3), 'peak_tflops': peak,
+                       'mbytes': round(nbytes / 1e6, 3), 'bound_us': round(t * 1e6, 2)})
+    enc_gf = 2.835 if args.enc_model == 'facenet' else VIT_GFLOP[args.enc_model]
+    if args.enc_model == 'facenet':
+        enc_peak = BF16_PEAK_TFLOPS if args.enc_precision == 'bf16' else FP32_PEAK_TFLOPS
+    else:
+        enc_peak = FP32_PEAK_TFLOPS if args.enc_precision == 'fp32' else F16X_PEAK_TFLOPS
+    side = 160 if args.enc_model == 'facenet' else 128
+    if args.det_model != 'none' and solo is not None:
+        s_ms, s_n, s_fl, _ = solo
+        fl = s_fl / max(1, s_n)
+        frame_bytes = args.det_batch * args.H * args.W * 3
+        if args.det_model == 'yolo':
+            peak = {'bf16': BF16_PEAK_TFLOPS, 'x3': X3_PEAK_TFLOPS}.get(args.det_precision, FP32_PEAK_TFLOPS)
+            add('YOLOv3 (letterbox + Darknet53 + neck + heads)', fl, peak, frame_bytes)
+        else:
+            add('pyramid + PNet', fl, F16X_PEAK_TFLOPS, frame_bytes)
+            st = np.array(solo_stats, dtype=np.float64) if solo_stats else None
+            n2 = float(st[:, 3].mean()) if st is not None else 0.0
+            n3 = float(st[:, 5].mean()) if st is not None else 0.0
+            add('RNet (%.0f candidates)' % n2, n2 * RNET_FLOP, F16X_PEAK_TFLOPS, n2 * 24 * 24 * 3 * 4)
+            add('ONet (%.0f candidates)' % n3, n3 * ONET_FLOP, F16X_PEAK_TFLOPS, n3 * 48 * 48 * 3 * 4)
+    add('%s (%.1f faces)' % (ENC_NAMES[args.enc_model], faces_per_step), faces_per_step * enc_gf * 1e9, enc_peak,
+        faces_per_step * side * side * 3)
+    bound_ms = sum(x['bound_us'] for x in stages) / 1e3
+    roof = faces_per_step / (bound_ms / 1e3) if bound_ms > 0 else None
+    ach = faces_per_step / (ms_per_step / 1e3) if ms_per_step > 0 else 0.0
+    return {'faces_per_s_per_gpu': round(ach, 2), 'roofline_faces_per_s_per_gpu': round(roof, 2) if roof else None,
+            'frac': round(ach / roof, 4) if roof else None, 'bound_ms_per_step': round(bound_ms, 4),
+            'ms_per_step': round(ms_per_step, 4), 'stages': stages,
+            'note': 'SURVEY.md 8d: faces / sum_stages max(FLOPs/peak, bytes/BW); per GPU, per det-batch'}
 
 
 def roofline_enc(args, ms_per_step):
@@ -574,17 +656,53 @@ def roofline_enc(args, ms_per_step):
 
 
 # ------------------------------------------------------------------ main
+def grouping_leg(X, ctx, dev, rows_fn=None, grouper=None):
+    """main.py:72-77 on the gathered embeddings X (every rank holds them): the cosine dedupe
+    (dupes.py:60-65) row-sharded across the ranks, then KMeans + silhouette / CH / DB for
+    k = 2..16 on the kept rows (grouping.py:97-107), sharded by k and by silhouette rows.
+    rows_fn / grouper replace the device kernels (CPU tests).  Returns (record, mins, labels,
+    scores); times are max over ranks."""
+    from videotofaces import dupes
+    from videotofaces.grouping import cluster_sweep
+    X = X.contiguous()
+    ctx.sync()
+    ctx.barrier()
+    t0 = time.perf_counter()
+    if rows_fn is None:
+        mins, _ = dupes.cosine_dedupe_device(X, sharded=True)
+    else:
+        Xh = X.cpu().numpy()
+        mins, _ = dupes.cosine_dedupe_sharded(Xh, rows_fn) if ctx.world > 1 else rows_fn(0, Xh.shape[0])
+    ctx.sync()
+    t_dd = time.perf_counter() - t0
+    Xk = X.cpu().numpy()[~(mins <= 0.25)]
+    ks = [k for k in range(2, 17) if k <= Xk.shape[0]]
+    t1 = time.perf_counter()
+    labels, scores = cluster_sweep(Xk, ks, 0, grouper=grouper, device=dev, sharded=True)
+    ctx.sync()
+    t_sw = time.perf_counter() - t1
+    ctx.barrier()
+    tg, t_dd, t_sw = ctx.reduce([time.perf_counter() - t0, t_dd, t_sw], dist.ReduceOp.MAX)
+    best = max(scores, key=lambda s: s[1])[0] if scores else None
+    rec = {'faces': int(X.shape[0]), 'dupes_at_0.25': int((mins <= 0.25).sum()), 'clustered': int(Xk.shape[0]),
+           'clustered_frac': round(Xk.shape[0] / max(1, X.shape[0]), 4),
+           'k': [ks[0], ks[-1]] if ks else [], 'seconds': round(tg, 4), 'dedupe_s': round(t_dd, 4),
+           'sweep_s': round(t_sw, 4), 'best_k_silhouette': best,
+           'note': 'fused cosine dedupe of the gathered embeddings (rows sharded across ranks), then KMeans + '
+                   'silhouette/CH/DB for each k on the kept rows (main.py:72-77), k sharded across ranks '
+                   '(max over ranks)'}
+    return rec, mins, labels, scores
+
+
 def run_gpu(args):
     ctx = Ctx('nccl')
     dev = ctx.device
-    from videotofaces import synth
     if args.det_model == 'none':
         pipe = EncodePipeline(args, dev, ctx.rank)
     else:
-        B = args.det_batch
-        pool_n = max(B, args.pool // B * B)
-        frames_np = synth.make_frames(pool_n, args.H, args.W, seed=1000 + ctx.rank)
-        pipe = DetEncPipeline(args, dev, frames_np)
+        warm = max(args.warmup, max(1, args.lanes))
+        frames, offset, frames_np = rank_frames(args, ctx, warm + args.steps)
+        pipe = DetEncPipeline(args, dev, frames, offset, frames_np)
     ctx.sync()
     faces, elapsed, gathered, _ = measure(pipe, args.steps, max(args.warmup, getattr(pipe, 'L', 1)), ctx)
     det = args.det_model != 'none'
@@ -620,36 +738,13 @@ def run_gpu(args):
         solo = pipe.solo(2)
     grouping = None
     if args.grouping:
-        from videotofaces import dupes
-        from videotofaces.grouping import cluster_sweep
-        X = gathered.contiguous()
-        ctx.sync()
-        ctx.barrier()
-        t0 = time.perf_counter()
-        mins, _ = dupes.cosine_dedupe_device(X)
-        ctx.sync()
-        t_dd = time.perf_counter() - t0
-        # main.py:72-77: the sweep clusters the embeddings the dedupe keeps
-        Xh = X.cpu().numpy()[~(mins <= 0.25)]
-        ks = [k for k in range(2, 17) if k <= Xh.shape[0]]
-        t1 = time.perf_counter()
-        labels, scores = cluster_sweep(Xh, ks, 0, device=dev)
-        ctx.sync()
-        t_sw = time.perf_counter() - t1
-        ctx.barrier()
-        tg, t_dd, t_sw = ctx.reduce([time.perf_counter() - t0, t_dd, t_sw], dist.ReduceOp.MAX)
-        best = max(scores, key=lambda s: s[1])[0] if scores else None
-        grouping = {'faces': int(X.shape[0]), 'dupes_at_0.25': int((mins <= 0.25).sum()), 'clustered': int(Xh.shape[0]),
-                    'k': [ks[0], ks[-1]] if ks else [], 'seconds': round(tg, 4), 'dedupe_s': round(t_dd, 4),
-                    'sweep_s': round(t_sw, 4), 'best_k_silhouette': best,
-                    'note': 'fused cosine dedupe of the gathered embeddings, then KMeans + silhouette/CH/DB for '
-                            'each k on the kept rows (main.py:72-77), k sharded across ranks (max over ranks)'}
+        grouping = grouping_leg(gathered, ctx, dev)[0]
     if ctx.rank == 0:
         steps = args.steps
         frames_all = ctx.world * steps * (args.det_batch if det else 0)
         dtype_enc = args.enc_precision if args.enc_precision != 'f16x' else 'fp32 (split-fp16 MFMA)'
         if det:
-            roof, hbm = roofline_det(args, pipe, shared, solo)
+            roof, _ = roofline_det(args, pipe, shared, solo)
             wl = ('YOLOv3(%s)' % args.det_precision if args.det_model == 'yolo'
                   else 'MTCNN(min_face_size=%g)' % args.min_face_size) + '+' + ENC_NAMES[args.enc_model]
             dtype = '%s det / %s enc' % (args.det_precision if args.det_model == 'yolo' else 'fp32 (split-fp16 MFMA)',
@@ -660,7 +755,7 @@ def run_gpu(args):
                             args.det_min_border))
             metric = 'faces/sec end-to-end (detect+encode) on %dx%d synthetic frames' % (args.W, args.H)
         else:
-            roof, hbm = roofline_enc(args, elapsed * 1e3 / steps), None
+            roof = roofline_enc(args, elapsed * 1e3 / steps)
             dtype = dtype_enc
             workload = '%s encoder only, enc-batch %d, pre-cropped 224x224 uint8 faces in HBM' % (
                 ENC_NAMES[args.enc_model], args.enc_batch)
@@ -682,10 +777,11 @@ def run_gpu(args):
             'faces_per_frame': round(faces / max(1, frames_all), 3) if det else None,
             'frames_per_s': round(frames_all / elapsed, 2) if det else None,
             'embeddings_gathered': int(gathered.shape[0]),
-            'roofline': roof, 'cpu_baseline': None,
+            'roofline': roof,
+            'roofline_e2e': roofline_e2e(args, faces / max(1, ctx.world * steps), elapsed * 1e3 / steps,
+                                         solo if det else None, getattr(pipe, 'solo_stats', None)),
+            'cpu_baseline': None,
         }
-        if hbm:
-            res['hbm_equiv'] = hbm
         res.update(out)
         if grouping:
             res['grouping'] = grouping

@@ -113,3 +113,110 @@ def test_measure_world2_gloo_matches_world1():
     assert res[0][1] == res[1][1] == f1 == g1.shape[0]
     assert res[0][2] == res[1][2]  # max over ranks
     assert res[0][3] == res[1][3] == g1.tolist()
+
+
+# ---- DetEncPipeline over one global frame sequence, with CPU stand-ins for the HIP models
+H_, W_, BS_, STEPS_ = 48, 64, 4, 6
+
+
+class StubDetector:
+    """crops: per frame, the 8x8 cells whose green mean is above the frame's 80th percentile
+    (at most 3, row-major); deterministic in the frame content"""
+
+    def detect_crops(self, src, minsize, bp, off):
+        out = []
+        for f in range(src.shape[0]):
+            g = src[f, :, :, 1].float().reshape(H_ // 8, 8, W_ // 8, 8).mean((1, 3))
+            cells = torch.nonzero(g > torch.quantile(g, 0.8))[:3]
+            for cy, cx in cells.tolist():
+                out.append([off + f, cx * 8, cy * 8, cx * 8 + 16, cy * 8 + 16])
+        return torch.tensor(out, dtype=torch.int32).reshape(-1, 5), None
+
+
+class StubEncoder:
+    dim = 12
+
+    def encode_crops(self, frames, crops):
+        rows = []
+        for f, x1, y1, x2, y2 in crops.tolist():
+            c = frames[f, y1:y2, x1:x2].float()
+            rows.append(torch.cat([c.mean((0, 1)), c.std((0, 1)), c[::4, ::4].reshape(-1, 3).amax(0),
+                                   c[:, :, 1].reshape(-1)[:3]]))
+        return torch.stack(rows) if rows else torch.zeros((0, self.dim))
+
+
+def _pipe_args():
+    import bench
+    a = bench.parse(['--config', 'c2', '--det-batch', str(BS_), '--pool', '0', '--lanes', '2', '--enc-batch', '5',
+                     '--enc-model', 'vit_b'])
+    a.H, a.W = H_, W_
+    return a
+
+
+def _pipeline_run(ctx):
+    """frames of the rank's shard (rank_frames, pool 0: distinct frames from one global sequence)
+    -> stand-in detector / encoder lanes -> measure (all-gather-v) -> grouping_leg (dedupe rows
+    sharded + the k sweep sharded) with the oracle restatements as the device kernels"""
+    import numpy as np
+    import bench
+    from oracle import grouping as og
+    from oracle.kmeans import CpuGrouper
+    a = _pipe_args()
+    frames, offset, fnp = bench.rank_frames(a, ctx, STEPS_)
+    pipe = bench.DetEncPipeline(a, ctx.device, frames, offset, fnp, StubDetector, StubEncoder)
+    faces, _, X, _ = bench.measure(pipe, STEPS_, 0, ctx)
+    Xh = X.numpy()
+    rm, ri = og.cosine_dedupe(Xh)
+    rec, mins, labels, scores = bench.grouping_leg(X, ctx, ctx.device, rows_fn=lambda lo, hi: (rm[lo:hi], ri[lo:hi]),
+                                                   grouper=CpuGrouper())
+    return faces, Xh.tolist(), np.asarray(mins).tolist(), [np.asarray(lb).tolist() for lb in labels], scores, rec
+
+
+def _pipe_worker(rank, world, port, q):
+    sys.path[:0] = [ROOT, os.path.join(ROOT, 'video-to-faces_amd')]
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port), WORLD_SIZE=str(world), RANK=str(rank),
+                      LOCAL_RANK=str(rank))
+    import bench
+    ctx = bench.Ctx('gloo', device=torch.device('cpu'))
+    q.put((rank, _pipeline_run(ctx)))
+    ctx.close()
+
+
+def test_det_enc_pipeline_world2_matches_world1_gloo():
+    """SURVEY.md §8e as bench.py runs it: each rank takes its whole det-batches of ONE global
+    frame sequence (parallel.shard_batches), detects and encodes them on two lanes, the
+    embeddings are all-gathered in frame order, then the dedupe and the k sweep run sharded.
+    World 2 (gloo) gathers exactly the embeddings of world 1 over the same 2 x 6 det-batches and
+    ends with the same dedupe minima, labels and scores."""
+    import bench
+    world = 2
+    mpc = mp.get_context('spawn')
+    q = mpc.Queue()
+    port = _free_port()
+    ps = [mpc.Process(target=_pipe_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    res = dict(q.get(timeout=300) for _ in range(world))
+    for p in ps:
+        p.join(timeout=60)
+    assert res[0][:5] == res[1][:5]
+
+    # world 1 over the same global sequence: the one rank takes all 2 x STEPS_ det-batches
+    ctx1 = bench.Ctx('gloo', device=torch.device('cpu'))
+    b2 = bench
+    a = _pipe_args()
+    frames, offset, fnp = b2.rank_frames(a, ctx1, world * STEPS_)
+    pipe = b2.DetEncPipeline(a, ctx1.device, frames, offset, fnp, StubDetector, StubEncoder)
+    faces1, _, X1, _ = b2.measure(pipe, world * STEPS_, 0, ctx1)
+    assert res[0][0] == faces1 and res[0][1] == X1.numpy().tolist()
+    assert len(res[0][1]) > 40
+    import numpy as np
+    from oracle import grouping as og
+    from oracle.kmeans import CpuGrouper
+    rm, ri = og.cosine_dedupe(X1.numpy())
+    _, mins1, labels1, scores1 = b2.grouping_leg(X1, ctx1, ctx1.device, rows_fn=lambda lo, hi: (rm[lo:hi], ri[lo:hi]),
+                                                 grouper=CpuGrouper())
+    assert res[0][2] == np.asarray(mins1).tolist()
+    assert res[0][3] == [np.asarray(lb).tolist() for lb in labels1]
+    assert res[0][4] == scores1
+    print('faces', faces1, 'kept', res[0][5]['clustered'])

@@ -81,7 +81,7 @@ def _sweep_worker(rank, world, port, q):
         def silhouette_sweep(self, X, label_sets, lo=0, hi=None):
             done.append(('rows', lo, hi))
             return super().silhouette_sweep(X, label_sets, lo, hi)
-    labels, scores = cluster_sweep(X, [2, 3, 4, 5, 6], 0, Spy())
+    labels, scores = cluster_sweep(X, [2, 3, 4, 5, 6], 0, Spy(), sharded=True)
     q.put((rank, done, [lb.tolist() for lb in labels], scores))
     dist.destroy_process_group()
 
@@ -159,3 +159,37 @@ def test_cosine_dedupe_sharded_gloo():
     nt = [(x + 127) // 128 for x in b]
     pairs = [nt[r + 1] * (nt[r + 1] + 1) // 2 - nt[r] * (nt[r] + 1) // 2 for r in range(world)]
     assert max(pairs) <= 2 * min(pairs) + 8
+
+
+def _mismatch_worker(rank, world, port, q):
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [root, os.path.join(root, 'video-to-faces_amd')]
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    from oracle.kmeans import CpuGrouper
+    from videotofaces import synth
+    from videotofaces.grouping import cluster_sweep
+    X = synth.planted_clusters(N=100 + rank, D=8)  # ranks disagree
+    try:
+        cluster_sweep(X, [2, 3], 0, CpuGrouper(), sharded=True)
+        q.put((rank, 'no error'))
+    except ValueError as e:
+        q.put((rank, str(e)))
+    dist.destroy_process_group()
+
+
+def test_sharded_sweep_refuses_different_inputs_gloo():
+    """A sharded grouping step whose ranks hold different embeddings raises on every rank
+    instead of stitching shards of different inputs together."""
+    world = 2
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_mismatch_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    res = dict(q.get(timeout=180) for _ in range(world))
+    for p in ps:
+        p.join(timeout=60)
+    assert all('ranks hold different inputs' in res[r] for r in range(world)), res

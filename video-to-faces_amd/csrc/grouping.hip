@@ -36,7 +36,7 @@ __global__ void k_row_normalize(const float* __restrict__ X, int64_t N, int D, i
     int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= N) return;
     const float* x = X + i * D;
-    float nrm = __fsqrt_rn(np_einsum_sq(x, D));
+    float nrm = sqrtf(np_einsum_sq(x, D));  // correctly rounded (hipcc's __fsqrt_rn is the 1-ulp v_sqrt_f32)
     if (nrm == 0.f) nrm = 1.f;
     for (int k = 0; k < Dp; k++) Xn[i * Dp + k] = k < D ? __fdiv_rn(x[k], nrm) : 0.f;
 }

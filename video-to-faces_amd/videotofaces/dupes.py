@@ -18,13 +18,16 @@ import torch
 from . import _native as nat
 
 
-def cosine_dedupe_device(X):
+def cosine_dedupe_device(X, sharded=False):
     """X: CUDA fp32 [N,D] -> (mins f32 [N], inds i64 [N]) exactly as dupes.py:60-64 computes
-    them: min / first argmin over j < i of clip(1 - cos(X_i, X_j), 0, 2); row 0 -> (10000, 0).
-    Under torch.distributed (every rank holding the same X) the rows are sharded across the
-    ranks (cosine_dedupe_sharded)."""
+    them, in sklearn's bits: min / first argmin over j < i of clip(1 - cos(X_i, X_j), 0, 2);
+    row 0 -> (10000, 0).  sharded=True (a collective: every rank of the default process group
+    must call it with the same X, which is checked) splits the rows across the ranks
+    (cosine_dedupe_sharded)."""
     X = X.to(torch.float32).contiguous()
-    if _world() > 1:
+    if sharded and _world() > 1:
+        from .parallel import check_replicated
+        check_replicated(X.cpu().numpy(), 'cosine_dedupe_device')
         return cosine_dedupe_sharded(X)
     return cosine_dedupe_rows(X, 0, X.shape[0])
 
@@ -58,17 +61,19 @@ def dedupe_shards(n, world, tile=128):
 
 def cosine_dedupe_sharded(X, rows_fn=None):
     """the N x N dedupe row-block sharded across the ranks of the default process
-    group (each holds the gathered X), then one all-gather of the per-row (min, argmin) --
-    12 bytes a row.  rows_fn(lo, hi) -> (mins, inds) computes a shard (default: the device
-    kernel)."""
+    group (each holds the gathered X), then one tensor all-gather-v (RCCL on GPUs) of the per-row
+    (min, argmin), packed as two float64 words a row (both exact: fp32 minima, indices < 2^31).
+    rows_fn(lo, hi) -> (mins, inds) computes a shard (default: the device kernel)."""
     import torch.distributed as dist
+    from .parallel import all_gather_cpu
     world, rank = dist.get_world_size(), dist.get_rank()
     n = X.shape[0]
     b = dedupe_shards(n, world)
     mins, inds = (rows_fn or (lambda lo, hi: cosine_dedupe_rows(X, lo, hi)))(b[rank], b[rank + 1])
-    parts = [None] * world
-    dist.all_gather_object(parts, (np.asarray(mins, np.float32), np.asarray(inds, np.int64)))
-    return np.concatenate([p[0] for p in parts]), np.concatenate([p[1] for p in parts])
+    pk = torch.from_numpy(np.stack([np.asarray(mins, np.float32).astype(np.float64),
+                                    np.asarray(inds, np.int64).astype(np.float64)], 1).reshape(-1, 2))
+    allv = all_gather_cpu(pk).numpy()
+    return allv[:, 0].astype(np.float32), allv[:, 1].astype(np.int64)
 
 
 def pack_hashes(H):
@@ -143,14 +148,20 @@ def nearest_dupes(hashes, prev, hash_thr):
     return flags, log
 
 
-def remove_dupes_overall(X, filenames, dup_params, device=None):
-    """dupes.py:51-93; `device` (an addition) picks the GPU, default cuda:0."""
+def remove_dupes_overall(X, filenames, dup_params, device=None, sharded=False):
+    """dupes.py:51-93; `device` (an addition) picks the GPU, default cuda:0.  sharded=True (an
+    addition, a collective over the default process group: every rank passes the same X) splits
+    the embedding dedupe's rows across the ranks; only rank 0 then touches out_dir."""
     measure_type, threshold, save_dupes, out_dir = dup_params
     if measure_type == 'hash':
         mins, inds = hamming_lower(X, device)
     else:
         dev = nat.require_gpu(device)
-        mins, inds = cosine_dedupe_device(torch.from_numpy(np.ascontiguousarray(X, np.float32)).to(dev))
+        mins, inds = cosine_dedupe_device(torch.from_numpy(np.ascontiguousarray(X, np.float32)).to(dev), sharded)
+    if sharded and _world() > 1:
+        import torch.distributed as dist
+        if dist.get_rank() != 0:
+            out_dir = None
     idx = (mins <= threshold).nonzero()[0]
     sidx = set(idx.tolist())
     dupes = [fn for i, fn in enumerate(filenames) if i in sidx]

@@ -89,47 +89,45 @@ def classify(X, R, classes, thr, log, paths, out_dir, device=None):
     return inds, classes
 
 
-def _gather(obj):
-    import torch.distributed as dist
-    parts = [None] * dist.get_world_size()
-    dist.all_gather_object(parts, obj)
-    return parts
-
-
-def cluster_sweep(X, clusters, random_state, grouper=None, device=None):
+def cluster_sweep(X, clusters, random_state, grouper=None, device=None, sharded=False):
     """KMeans + (silhouette, CH, DB) for every k in `clusters`, in order -- cluster_faces'
-    loops (grouping.py:97-107).  With torch.distributed initialised (every rank holding the
-    gathered X) the work is sharded with no cross-rank reduction inside a
-    result, so every number equals the one-process result:
+    loops (grouping.py:97-107).  sharded=True (a collective over the default process group:
+    every rank passes the same X, which is checked) splits the work across the ranks
+     with no cross-rank reduction inside a result, so every number equals the
+    one-process result; the results travel by tensor all-gathers (RCCL on GPUs):
       * KMeans fits by k: rank r fits the k at positions i % world == r; labels all-gathered;
       * silhouette by rows: one pass over the distance rows of the rank's row range computes
         silhouette_samples for EVERY k at once (no N x N matrix anywhere); the per-row values
         are all-gathered and averaged in row order as silhouette_score's np.mean does;
       * CH / DB by k, like the fits.
     `grouper` defaults to the device Grouper (videotofaces.kmeans); tests pass a CPU stand-in."""
+    import torch
     import torch.distributed as dist
     if grouper is None:
         from .kmeans import Grouper
         grouper = Grouper(device)
     g = grouper
     X = np.ascontiguousarray(X, np.float32)
-    prep = g.prepare(X)
-    world = dist.get_world_size() if dist.is_available() and dist.is_initialized() else 1
+    world = dist.get_world_size() if sharded and dist.is_available() and dist.is_initialized() else 1
     rank = dist.get_rank() if world > 1 else 0
-    idx = [i for i in range(len(clusters)) if i % world == rank]
+    if world > 1:
+        from .parallel import all_gather_cpu, all_gather_slots, check_replicated
+        check_replicated(X, 'cluster_sweep')
+    prep = g.prepare(X)
+    K, n = len(clusters), X.shape[0]
+    idx = [i for i in range(K) if i % world == rank]
     fits = {i: np.asarray(g.kmeans(X, clusters[i], random_state=random_state, prep=prep)) for i in idx}
     if world > 1:
-        for p in _gather(fits):
-            fits.update(p)
-    labels = [fits[i] for i in range(len(clusters))]
-    n = X.shape[0]
+        fits = dict(enumerate(all_gather_slots(fits, K, (n,), torch.int64)))
+    labels = [fits[i] for i in range(K)]
     lo, hi = n * rank // world, n * (rank + 1) // world
     sil = g.silhouette_sweep(X, labels, lo, hi) if labels else np.zeros((0, 0), np.float32)
     chdb = {i: (g.calinski_harabasz_score(X, labels[i]), g.davies_bouldin_score(X, labels[i])) for i in idx}
     if world > 1:
-        sil = np.concatenate(_gather(sil), axis=1)
-        for p in _gather(chdb):
-            chdb.update(p)
+        if K:  # row-major [rows, K] blocks in rank order -> [K, n]
+            sil = all_gather_cpu(torch.from_numpy(np.ascontiguousarray(np.asarray(sil, np.float32).T))).numpy().T
+        chdb = dict(enumerate(tuple(float(v) for v in a)
+                              for a in all_gather_slots(chdb, K, (2,), torch.float64)))
     scores = [(clusters[i], float(np.mean(sil[i])), float(chdb[i][0]), float(chdb[i][1]))
               for i in range(len(clusters))]
     return labels, scores
