@@ -509,6 +509,21 @@ def gen_shapes():
     print('shapes', {k: v.shape for k, v in out.items()})
 
 
+def gen_meta():
+    """Host settings the goldens' bits depend on: torch's intra-op thread count (torch's CPU
+    sigmoid splits a tensor into per-thread chunks: Sleef on vector steps, glibc on chunk tails,
+    which rcnn.hip reproduces at VTF_TORCH_THREADS, default 8) and numpy's BLAS (the cosine
+    dedupe's ssyrk order)."""
+    import json
+    import threadpoolctl
+    blas = [(d.get('internal_api'), d.get('version'), d.get('architecture'), os.path.basename(d.get('filepath', '')))
+            for d in threadpoolctl.threadpool_info() if d.get('user_api') == 'blas']
+    meta = {'torch_threads': torch.get_num_threads(), 'numpy': np.__version__, 'blas': blas}
+    with open(os.path.join(HERE, 'meta.json'), 'w') as f:
+        json.dump(meta, f, indent=1)
+    print('meta', meta)
+
+
 def gen_b1():
     """BASELINE config 1's shape: MTCNN on 720p frames one at a time (det-batch 1) at the
     RealMTCNN default min_face_size 5 -- four single-frame calls (seeds 110..113); with one image
@@ -800,6 +815,6 @@ def gen_boxes():
 
 if __name__ == '__main__':
     which = sys.argv[1:] or ['mtcnn', 'facenet', 'vit', 'grouping', 'yolo', 'kmeans', 'rcnn', 'dupes', 'boxes', 'shapes', 'chain',
-                             'scale', 'c3', 'iom', 'b1']
+                             'scale', 'c3', 'iom', 'b1', 'meta']
     for w in which:
         globals()['gen_' + w]()

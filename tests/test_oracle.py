@@ -316,3 +316,13 @@ def test_oracle_iom_chain_vs_reference(case):
     keep = om.nms_iom_chain(torch.from_numpy(gi[case + '_boxes']), torch.from_numpy(gi[case + '_scores']),
                             torch.from_numpy(gi[case + '_classes']), 0.7)
     np.testing.assert_array_equal(np.asarray(keep), gi[case + '_keep'])
+
+
+def test_golden_host_meta():
+    """The goldens record the host settings their bits depend on (make_golden.py gen_meta): the
+    device RPN reproduces torch's CPU sigmoid chunking at VTF_TORCH_THREADS (default 8) and the
+    cosine dedupe the SkylakeX ssyrk order -- both must be what the goldens were made with."""
+    import json
+    meta = json.load(open(os.path.join(GOLDEN, 'meta.json')))
+    assert meta['torch_threads'] == int(os.environ.get('VTF_TORCH_THREADS', '8'))
+    assert any(b[0] == 'openblas' and b[2] == 'SkylakeX' for b in meta['blas'])

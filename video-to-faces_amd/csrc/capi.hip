@@ -37,19 +37,21 @@ struct Slot {
     Arena ar;
 };
 std::mutex g_mu;
-std::map<std::pair<int, hipStream_t>, std::unique_ptr<Slot>> g_slots;
+std::map<std::pair<int, hipStream_t>, std::shared_ptr<Slot>> g_slots;
 }  // namespace
 
 StreamScratch stream_scratch(hipStream_t st) {
     const int dev = stream_device(st);
-    Slot* s;
+    std::shared_ptr<Slot> s;
     {
         std::lock_guard<std::mutex> lk(g_mu);
         auto& p = g_slots[{dev, st}];
-        if (!p) p.reset(new Slot());
-        s = p.get();
+        if (!p) p = std::make_shared<Slot>();
+        s = p;  // a reference taken under g_mu: a concurrent release cannot free the slot under us
     }
-    return StreamScratch{&s->ar, std::unique_lock<std::mutex>(s->mu)};
+    Arena* ar = &s->ar;
+    std::unique_lock<std::mutex> lk(s->mu);
+    return StreamScratch{std::move(s), ar, std::move(lk)};
 }
 
 void release_dma_ws(hipStream_t st);
@@ -64,11 +66,14 @@ const char* vtf_last_error(void) { return g_err.c_str(); }
 
 int vtf_version(void) { return 1; }
 
+// The caller must not enqueue work on the stream from another thread during the release: the
+// slot's arena is freed once the last entry point that already holds it returns (its
+// StreamScratch keeps a reference), after this call has dropped the registry's.
 int vtf_release_stream(void* hip_stream) {
     hipStream_t st = (hipStream_t)hip_stream;
     return guarded_on(stream_device(st), [&] {
         VTF_HIP(hipStreamSynchronize(st));
-        std::unique_ptr<Slot> s;
+        std::shared_ptr<Slot> s;
         {
             std::lock_guard<std::mutex> lk(g_mu);
             auto it = g_slots.find({stream_device(st), st});
@@ -77,7 +82,10 @@ int vtf_release_stream(void* hip_stream) {
                 g_slots.erase(it);
             }
         }
-        if (s) std::lock_guard<std::mutex> lk(s->mu);  // no entry point is still using it
+        if (s) {
+            std::lock_guard<std::mutex> lk(s->mu);  // wait for an entry point still inside
+        }
+        s.reset();  // freed here, or by the last StreamScratch still holding it
         release_dma_ws(st);
     });
 }

@@ -6,6 +6,7 @@
 
 #include <cstdint>
 #include <cstdio>
+#include <memory>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -145,7 +146,11 @@ int guarded_on(int device, F&& f) {
 // Scratch of the stateless entry points (NMS, cosine dedupe / classify, blob): one arena per
 // (device, stream), held under its own lock for the call.  A process-global arena would hand
 // one device's buffer to a launch on another device, or one lane's buffer to a concurrent lane.
+// A stream's scratch arena, locked for the caller: `keep` holds the slot alive (a concurrent
+// vtf_release_stream only drops the registry's reference), `lock` serialises entry points on
+// the stream.  Member order matters: the lock is released before the reference.
 struct StreamScratch {
+    std::shared_ptr<void> keep;
     Arena* ar;
     std::unique_lock<std::mutex> lock;
 };

@@ -745,8 +745,8 @@ int vtf_sqdist_rows(vtf_group_t h, const float* d_X, int64_t N, int64_t D, const
 int vtf_kmeans_step(vtf_group_t h, const float* d_X, int64_t N, int64_t D, const float* d_centers, int k,
                     int32_t* d_labels, float* d_sums, float* d_weights, int64_t* out_changed) {
     return guarded_on(h ? h->g.device : -1, [&] {
-        VTF_CHECK(h && d_X && d_centers && d_labels && N > 0 && D > 0 && k > 0 && k <= 64, VTF_E_ARG,
-                  "bad argument");
+        VTF_CHECK(h && d_X && d_centers && d_labels && N > 0 && D > 0 && k > 0, VTF_E_ARG, "bad argument");
+        VTF_CHECK(k <= 64, VTF_E_LIMIT, "kmeans: at most 64 clusters (the E-step keeps every center's distance in LDS)");
         Group& G = h->g;
         float* csq = G.ar.get<float>(1, k);
         unsigned long long* chg = G.ar.get<unsigned long long>(2, 1);

@@ -174,6 +174,10 @@ class Grouper:
         N = Xc.shape[0]
         if n_clusters > N:
             raise ValueError('n_samples=%d should be >= n_clusters=%d.' % (N, n_clusters))
+        if n_clusters > 64:
+            # vtf_kmeans_step keeps a block's distances to every center in LDS (csrc/kmeans.hip)
+            raise ValueError('KMeans on the device supports at most 64 clusters (n_clusters=%d); the '
+                             'reference sweeps k = 2..16 (grouping.py:97)' % n_clusters)
         tol_abs = np.mean(p['var']) * tol                      # _tolerance (_kmeans.py:279-287)
         rs = np.random.RandomState(random_state) if not isinstance(random_state, np.random.RandomState) \
             else random_state
