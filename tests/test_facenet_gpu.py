@@ -39,6 +39,22 @@ def test_bf16_drift_reported(g):
     assert cos.min() > 0.99
 
 
+@pytest.mark.parametrize('n', [128, 5])
+def test_bf16_fused_blocks_bit_identical(n, monkeypatch):
+    """The fused bf16 Block17 (csrc/facenet_fused.hip: one launch per block, activations in LDS)
+    runs the unfused launches' MFMA k order and epilogue arithmetic: embeddings bit-identical to
+    VTF_FN_FUSED=0 (four implicit-GEMM launches per block), at enc-batch 128 and a ragged 5."""
+    from videotofaces.encoders.facenet import InceptionResnetV1
+    m = InceptionResnetV1('cuda:0', precision='bf16')
+    u8 = torch.from_numpy(np.random.default_rng(n).integers(0, 256, (n, 3, 160, 160), dtype=np.uint8))
+    x = (u8.float() - 127.5) * (1 / 128)
+    fused = m(x).cpu().numpy()
+    monkeypatch.setenv('VTF_FN_FUSED', '0')
+    plain = m(x).cpu().numpy()
+    print('fused vs unfused: max |diff| %.3g, identical %s' % (np.abs(fused - plain).max(), np.array_equal(fused, plain)))
+    np.testing.assert_array_equal(fused, plain)
+
+
 def test_blob_kernel_matches_restated_inter_linear():
     from videotofaces.encoders.facenet import blob_from_images
     from oracle.facenet import resize_linear_u8

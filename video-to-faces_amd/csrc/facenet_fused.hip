@@ -1,0 +1,522 @@
+// FaceNet Block17 (src/videotofaces/encoders/facenet.py:36-56) as ONE launch per block in the
+// bf16 mode: one workgroup per image (8 x 8 pixels x 896 channels), the whole branch chain kept
+// on chip.
+//
+// The unfused form is four implicit-GEMM launches per block at batch 128 (M = 8192 rows):
+// merged 1x1 896 -> 128|128, 1x7 128 -> 128, 7x1 128 -> 128, 1x1 256 -> 896 + residual -- each a
+// latency-bound GEMM (MFMA busy 2-3 %), ~74 us per block.  Here the activations
+// between the four GEMMs never leave LDS:
+//   stage 1  C1[64][256] = X[64][896] W_m^T, BN + ReLU            -> B1 (LDS, bf16)
+//   stage 2  C2[64][128] = im2col_1x7(B1[:, 128:256]) W_a^T, BN+ReLU -> B2 (LDS)
+//   stage 3  C3[64][128] = im2col_7x1(B2) W_b^T, BN + ReLU          -> B1[:, 128:256] (the concat)
+//   stage 4  Y[64][896] = ReLU(0.1 (B1 W_o^T + b_o) + X)            -> HBM, 7 passes of 128 channels
+// Weights stream HBM/L2 -> LDS through an LDS-DMA ring (global_load_lds_dwordx4, counted vmcnt,
+// one barrier per k-step); the stage-1 input rows ride in the same ring.  Every GEMM runs the
+// unfused kernels' k order -- 32-deep v_mfma_f32_16x16x32_bf16 chunks in ascending k from a zero
+// accumulator -- and the same epilogue arithmetic (conv_dev.hpp conv_epilogue8), so the block's
+// output is bit-identical to the four launches (tests/test_facenet_gpu.py).
+//
+// LDS images: weight / X rows of 128 B (one 64-deep k-step), 16-B slot s of row r holding source
+// slot s ^ ((r >> 1) & 7) (swizzle applied on the DMA source address; conflict-free fragment
+// reads, as conv_dma.hip); B1 / B2 rows padded to 528 / 272 B so the 16 rows of a fragment read
+// land on 16 distinct bank slots.
+#include "common.hpp"
+#include "conv.hpp"
+#include "conv_dev.hpp"
+
+namespace vtf {
+
+namespace {
+
+constexpr int RB = 128;                 // image row bytes per 64-deep k-step
+constexpr int B1S = 256 * 2 + 16;       // B1 row stride (bytes): 256 channels + pad
+constexpr int B2S = 128 * 2 + 16;       // B2 row stride
+constexpr int S1_X = 64 * RB;           // stage-1 slot: X rows (8 KB) ...
+constexpr int S1_SLOT = S1_X + 256 * RB;  // ... + W_m rows (32 KB)
+constexpr int S1_R = 3;                 // stage-1 ring slots (2 groups in flight)
+constexpr int R_OFF = 0;                // ring base
+constexpr int B1_OFF = S1_R * S1_SLOT;  // 120 KB
+constexpr int ZERO_OFF = B1_OFF + 64 * B1S;
+constexpr int LDS_BYTES = ZERO_OFF + 16;
+// stages 2-4 reuse the stage-1 ring region: B2, the weight ring (128 rows per slot), the epilogue image
+constexpr int S2_SLOT = 128 * RB;       // 16 KB
+constexpr int S2_R = 4;                 // 3 groups in flight
+constexpr int B2_OFF = 0;
+constexpr int R2_OFF = 64 * B2S;        // 17,408
+constexpr int E_OFF = R2_OFF + S2_R * S2_SLOT;  // 82,944; fp32 [64][128 + 4]
+constexpr int E_LD = 132;
+static_assert(E_OFF + 64 * E_LD * 4 <= B1_OFF, "stage-4 image inside the stage-1 ring region");
+static_assert(LDS_BYTES <= 160 * 1024, "LDS plan");
+
+typedef __attribute__((ext_vector_type(4))) float f4;
+
+struct B17P {
+    const __bf16* x;  // [N][64][896]
+    __bf16* y;
+    const __bf16 *wm, *wa, *wb, *wo;  // [256][896], [128][896], [128][896], [896][256]
+    const float *alm, *bem, *ala, *bea, *alb, *beb, *bo;
+    float scale;
+};
+
+__device__ inline void glds16(const void* g, void* l) {
+    __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)g,
+                                     (void __attribute__((address_space(3)))*)l, 16, 0, 0);
+}
+
+template <int N>
+__device__ inline void wait_vm_barrier() {
+    asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(N) : "memory");
+}
+
+// DMA rows [0, rows) x 128 B (bytes kb .. kb+127 of each row of a matrix with row pitch `pitch`)
+// into a swizzled LDS image: rows / 32 one-KB pieces per wave
+template <int ROWS>
+__device__ inline void dma_rows(const char* src, int64_t pitch, int64_t kb, char* dst, int wave, int lane) {
+    const int sl = (lane & 7) ^ (((lane >> 4) + 4 * (wave & 1)) & 7);
+#pragma unroll
+    for (int j = 0; j < ROWS / 32; j++) {
+        const int r = 32 * j + 8 * wave + (lane >> 3);
+        glds16(src + r * pitch + kb + sl * 16, dst + (wave + 4 * j) * 1024);
+    }
+}
+
+// fragment of a swizzled 128-B-row image: rows 16 i + (lane & 15), k half h (0: k 0..31, 1: 32..63)
+__device__ inline bf16x8 frag_sw(const char* img, int i, int h, int lane) {
+    const int r = lane & 15, s = (4 * h + (lane >> 4)) ^ (r >> 1);
+    return *(const bf16x8*)(img + (16 * i + r) * RB + s * 16);
+}
+
+__device__ inline float relu_bf(float v) { return fmaxf(v, 0.f); }
+
+// workgroup barrier for LDS traffic only: __syncthreads() would also wait vmcnt(0), draining the
+// weight DMAs in flight
+__device__ inline void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+// BN + ReLU epilogue of a [64][NC-per-wave] accumulator block into an LDS bf16 image
+template <int FM, int FN>
+__device__ inline void bn_relu_to_lds(const f4 (&acc)[FM][FN], const float* al, const float* be, int n0, char* dst,
+                                      int stride, int lane) {
+#pragma unroll
+    for (int j = 0; j < FN; j++) {
+        const int n = n0 + 16 * j + (lane & 15);
+        const float a = al[n], b = be[n];
+#pragma unroll
+        for (int i = 0; i < FM; i++)
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                const int m = 16 * i + 4 * (lane >> 4) + q;
+                *(__bf16*)(dst + m * stride + n * 2) = (__bf16)relu_bf(fmaf(acc[i][j][q], a, b));
+            }
+    }
+}
+
+__global__ __launch_bounds__(256, 1) void k_block17(B17P p) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int img = blockIdx.x;
+    const char* X = (const char*)(p.x + (int64_t)img * 64 * 896);
+    char* B1 = smem + B1_OFF;
+    char* B2 = smem + B2_OFF;
+    const char* ZERO = smem + ZERO_OFF;
+    if (tid < 4) ((float*)(smem + ZERO_OFF))[tid] = 0.f;
+
+    // ---------------- stage 1: X[64][896] x W_m^T -> B1 (wave: output channels 64 wave .. +64)
+    {
+        constexpr int S = 14, G = 2 + 8;  // k-steps; DMA instructions per wave per group
+        auto issue = [&](int s) {
+            char* slot = smem + R_OFF + (s % S1_R) * S1_SLOT;
+            dma_rows<64>(X, 896 * 2, (int64_t)s * RB, slot, wave, lane);
+            dma_rows<256>((const char*)p.wm, 896 * 2, (int64_t)s * RB, slot + S1_X, wave, lane);
+        };
+        f4 acc[4][4];
+#pragma unroll
+        for (int i = 0; i < 4; i++)
+#pragma unroll
+            for (int j = 0; j < 4; j++) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
+        issue(0);
+        issue(1);
+        for (int s = 0; s < S; s++) {
+            if (s + 1 < S)
+                wait_vm_barrier<G>();
+            else
+                wait_vm_barrier<0>();
+            if (s + 2 < S) issue(s + 2);
+            const char* slot = smem + R_OFF + (s % S1_R) * S1_SLOT;
+            const char* W = slot + S1_X + 64 * wave * RB;
+#pragma unroll
+            for (int h = 0; h < 2; h++) {
+                bf16x8 b[4];
+#pragma unroll
+                for (int j = 0; j < 4; j++) b[j] = frag_sw(W, j, h, lane);
+#pragma unroll
+                for (int i = 0; i < 4; i++) {
+                    const bf16x8 a = frag_sw(slot, i, h, lane);
+#pragma unroll
+                    for (int j = 0; j < 4; j++) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b[j], acc[i][j], 0, 0, 0);
+                }
+            }
+        }
+        bn_relu_to_lds<4, 4>(acc, p.alm, p.bem, 64 * wave, B1, B1S, lane);
+    }
+    __syncthreads();  // B1 complete; the stage-1 ring is free
+
+    // ---------------- stages 2 and 3: 1 x 7 and 7 x 1 convs, 128 -> 128 (wave: channels 32 wave .. +32)
+    auto conv7 = [&](const __bf16* w, const float* al, const float* be, const char* in, int in_stride, int in_coff,
+                     bool along_w, char* out, int out_stride, int out_coff) {
+        constexpr int S = 14, G = 4;
+        auto issue = [&](int s) {
+            dma_rows<128>((const char*)w, 896 * 2, (int64_t)s * RB, smem + R2_OFF + (s % S2_R) * S2_SLOT, wave, lane);
+        };
+        f4 acc[4][2];
+#pragma unroll
+        for (int i = 0; i < 4; i++)
+#pragma unroll
+            for (int j = 0; j < 2; j++) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
+        issue(0);
+        issue(1);
+        issue(2);
+        // the lane's A rows: output pixel (y, x) of row 16 i + (lane & 15)
+        const int r = lane & 15;
+        for (int s = 0; s < S; s++) {
+            if (s + 2 < S)
+                wait_vm_barrier<2 * G>();
+            else if (s + 1 < S)
+                wait_vm_barrier<G>();
+            else
+                wait_vm_barrier<0>();
+            if (s + 3 < S) issue(s + 3);
+            const char* W = smem + R2_OFF + (s % S2_R) * S2_SLOT + 32 * wave * RB;
+            const int t = s >> 1, c0 = in_coff + 64 * (s & 1);
+#pragma unroll
+            for (int h = 0; h < 2; h++) {
+                bf16x8 b[2];
+#pragma unroll
+                for (int j = 0; j < 2; j++) b[j] = frag_sw(W, j, h, lane);
+#pragma unroll
+                for (int i = 0; i < 4; i++) {
+                    const int y = 2 * i + (r >> 3), x = r & 7;
+                    const int yy = along_w ? y : y + t - 3, xx = along_w ? x + t - 3 : x;
+                    const bool ok = (unsigned)yy < 8u && (unsigned)xx < 8u;
+                    const char* src = ok ? in + (yy * 8 + xx) * in_stride + (c0 + 32 * h + 8 * (lane >> 4)) * 2 : ZERO;
+                    const bf16x8 a = *(const bf16x8*)src;
+#pragma unroll
+                    for (int j = 0; j < 2; j++) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b[j], acc[i][j], 0, 0, 0);
+                }
+            }
+        }
+        // (out may alias the columns `in` read: barrier before writing)
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < 2; j++) {
+            const int n = 32 * wave + 16 * j + (lane & 15);
+            const float a = al[n], b = be[n];
+#pragma unroll
+            for (int i = 0; i < 4; i++)
+#pragma unroll
+                for (int q = 0; q < 4; q++) {
+                    const int m = 16 * i + 4 * (lane >> 4) + q;
+                    *(__bf16*)(out + m * out_stride + (out_coff + n) * 2) = (__bf16)relu_bf(fmaf(acc[i][j][q], a, b));
+                }
+        }
+        __syncthreads();
+    };
+    conv7(p.wa, p.ala, p.bea, B1, B1S, 128, true, B2, B2S, 0);
+    conv7(p.wb, p.alb, p.beb, B2, B2S, 0, false, B1, B1S, 128);
+
+    // ---------------- stage 4: B1[64][256] x W_o^T + b_o, x scale, + X, ReLU -> Y (7 passes of 128 channels)
+    {
+        constexpr int S = 28, G = 4;  // (pass, k-step) groups
+        auto issue = [&](int s) {
+            const int pass = s >> 2, ks = s & 3;
+            dma_rows<128>((const char*)p.wo + (int64_t)pass * 128 * 256 * 2, 256 * 2, (int64_t)ks * RB,
+                          smem + R2_OFF + (s % S2_R) * S2_SLOT, wave, lane);
+        };
+        float* E = (float*)(smem + E_OFF);
+        char* Y = (char*)(p.y + (int64_t)img * 64 * 896);
+        issue(0);
+        issue(1);
+        issue(2);
+        f4 acc[4][2];
+        for (int s = 0; s < S; s++) {
+            const int ks = s & 3;
+            if (ks == 0) {
+#pragma unroll
+                for (int i = 0; i < 4; i++)
+#pragma unroll
+                    for (int j = 0; j < 2; j++) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
+            }
+            if (s + 2 < S)
+                wait_vm_barrier<2 * G>();
+            else if (s + 1 < S)
+                wait_vm_barrier<G>();
+            else
+                wait_vm_barrier<0>();
+            if (s + 3 < S) issue(s + 3);
+            const char* W = smem + R2_OFF + (s % S2_R) * S2_SLOT + 32 * wave * RB;
+#pragma unroll
+            for (int h = 0; h < 2; h++) {
+                bf16x8 b[2];
+#pragma unroll
+                for (int j = 0; j < 2; j++) b[j] = frag_sw(W, j, h, lane);
+#pragma unroll
+                for (int i = 0; i < 4; i++) {
+                    const int m = 16 * i + (lane & 15);
+                    const bf16x8 a = *(const bf16x8*)(B1 + m * B1S + (64 * ks + 32 * h + 8 * (lane >> 4)) * 2);
+#pragma unroll
+                    for (int j = 0; j < 2; j++) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b[j], acc[i][j], 0, 0, 0);
+                }
+            }
+            if (ks == 3) {
+                // pass epilogue through an fp32 image: 8 consecutive channels per thread (16-B
+                // residual loads and output stores), conv_epilogue8's arithmetic
+                const int pass = s >> 2;
+#pragma unroll
+                for (int i = 0; i < 4; i++)
+#pragma unroll
+                    for (int j = 0; j < 2; j++)
+#pragma unroll
+                        for (int q = 0; q < 4; q++)
+                            E[(16 * i + 4 * (lane >> 4) + q) * E_LD + 32 * wave + 16 * j + (lane & 15)] = acc[i][j][q];
+                lds_barrier();
+#pragma unroll
+                for (int u = 0; u < 4; u++) {
+                    const int e = tid + 256 * u, m = e >> 4, g = e & 15, c0 = pass * 128 + 8 * g;
+                    const f4 lo = *(const f4*)(E + m * E_LD + 8 * g), hi = *(const f4*)(E + m * E_LD + 8 * g + 4);
+                    const float v[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+                    const bf16x8 rx = *(const bf16x8*)(X + ((int64_t)m * 896 + c0) * 2);
+                    bf16x8 o;
+#pragma unroll
+                    for (int k = 0; k < 8; k++) {
+                        float t = v[k] + p.bo[c0 + k];
+                        if (p.scale != 1.f) t = t * p.scale;
+                        t = t + (float)rx[k];
+                        o[k] = (__bf16)fmaxf(t, 0.f);
+                    }
+                    *(bf16x8*)(Y + ((int64_t)m * 896 + c0) * 2) = o;
+                }
+                lds_barrier();  // E is rewritten by the next pass
+            }
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Block35 branches (facenet.py:14-33) in one launch per block: one workgroup per image (17 x 17
+// pixels, 289 rows padded to 19 fragments of 16), waves split the rows (fragments w, w+4, ...).
+//   stage 1  C1[289][96] = X[289][256] W_m^T (merged heads b0 | b1 | b2), BN + ReLU:
+//            b0 -> CAT[:, 0:32] (HBM), b1 / b2 heads -> T[:, 0:64] (LDS)
+//   stage 2  3x3 32 -> 32 on T[:, 0:32]   -> CAT[:, 32:64]
+//   stage 3  3x3 32 -> 32 on T[:, 32:64]  -> T[:, 0:32] (b2 middle)
+//   stage 4  3x3 32 -> 32 on T[:, 0:32]   -> CAT[:, 64:96]
+// The block tail (1x1 96 -> 256 + residual) stays one implicit-GEMM launch on CAT.  Operands
+// straight from global memory into registers (each wave owns its rows; the weights are small and
+// L2-resident), one 32-deep chunk ahead; same k order and epilogue as the unfused launches.
+constexpr int T5S = 64 * 2 + 16;  // T row stride (bytes)
+constexpr int B35_ROWS = 289, B35_FR = 19;
+constexpr int B35_LDS = B35_FR * 16 * T5S + 16;
+
+struct B35P {
+    const __bf16* x;  // [N][289][256]
+    __bf16* cat;      // [N][289][96]
+    const __bf16 *wm, *w1, *w2a, *w2b;  // [96][256], [32][288] x 3
+    const float *alm, *bem, *al1, *be1, *al2a, *be2a, *al2b, *be2b;
+};
+
+template <int NF>
+__device__ inline void b35_store(const f4 (&acc)[5][NF], int nf, int wave, int lane, int n0, const float* al,
+                                 const float* be, int oc, char* lds, int lstride, int lcoff, __bf16* g, int gcoff) {
+#pragma unroll
+    for (int j = 0; j < NF; j++) {
+        const int n = n0 + 16 * j + (lane & 15);
+        const float a = al[n], b = be[n];
+#pragma unroll
+        for (int f = 0; f < 5; f++) {
+            if (f >= nf) break;
+            const int fr = wave + 4 * f;
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                const int m = 16 * fr + 4 * (lane >> 4) + q;
+                if (m >= B35_ROWS) continue;
+                const __bf16 v = (__bf16)relu_bf(fmaf(acc[f][j][q], a, b));
+                const int c = n - oc;  // channel within the destination
+                if (g)
+                    g[(int64_t)m * 96 + gcoff + c] = v;
+                else
+                    *(__bf16*)(lds + m * lstride + (lcoff + c) * 2) = v;
+            }
+        }
+    }
+}
+
+__global__ __launch_bounds__(256, 1) void k_block35_br(B35P p) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int img = blockIdx.x;
+    const int nf = wave < 3 ? 5 : 4;  // fragments w, w + 4, ..., < 19
+    char* T = smem;
+    const char* ZERO = smem + B35_FR * 16 * T5S;
+    if (tid < 4) ((float*)(smem + B35_FR * 16 * T5S))[tid] = 0.f;
+    const __bf16* X = p.x + (int64_t)img * B35_ROWS * 256;
+    __bf16* CAT = p.cat + (int64_t)img * B35_ROWS * 96;
+    const int r = lane & 15, kq = 8 * (lane >> 4);
+
+    // ---- stage 1 (K = 256: 8 chunks of 32; N = 96: 6 fragments)
+    {
+        f4 acc[5][6];
+#pragma unroll
+        for (int f = 0; f < 5; f++)
+#pragma unroll
+            for (int j = 0; j < 6; j++) acc[f][j] = f4{0.f, 0.f, 0.f, 0.f};
+        const bf16x8* arow[5];
+#pragma unroll
+        for (int f = 0; f < 5; f++) {
+            const int m = min(16 * (wave + 4 * f) + r, B35_ROWS - 1);  // padding rows: any finite row
+            arow[f] = (const bf16x8*)(X + (int64_t)m * 256 + kq);
+        }
+        const bf16x8* brow[6];
+#pragma unroll
+        for (int j = 0; j < 6; j++) brow[j] = (const bf16x8*)(p.wm + (16 * j + r) * 256 + kq);
+        bf16x8 a[2][5], b[2][6];
+#pragma unroll
+        for (int f = 0; f < 5; f++) a[0][f] = arow[f][0];
+#pragma unroll
+        for (int j = 0; j < 6; j++) b[0][j] = brow[j][0];
+#pragma unroll
+        for (int c = 0; c < 8; c++) {
+            const int cur = c & 1;
+            if (c + 1 < 8) {
+#pragma unroll
+                for (int f = 0; f < 5; f++) a[cur ^ 1][f] = arow[f][4 * (c + 1)];
+#pragma unroll
+                for (int j = 0; j < 6; j++) b[cur ^ 1][j] = brow[j][4 * (c + 1)];
+            }
+#pragma unroll
+            for (int f = 0; f < 5; f++)
+                if (f < nf)
+#pragma unroll
+                    for (int j = 0; j < 6; j++)
+                        acc[f][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[cur][f], b[cur][j], acc[f][j], 0, 0, 0);
+        }
+        // b0 (channels 0..31) -> CAT[:, 0:32]; heads (32..95) -> T[:, 0:64]
+        f4 a0[5][2], a1[5][4];
+#pragma unroll
+        for (int f = 0; f < 5; f++) {
+            a0[f][0] = acc[f][0];
+            a0[f][1] = acc[f][1];
+#pragma unroll
+            for (int j = 0; j < 4; j++) a1[f][j] = acc[f][2 + j];
+        }
+        b35_store<2>(a0, nf, wave, lane, 0, p.alm, p.bem, 0, nullptr, 0, 0, CAT, 0);
+        b35_store<4>(a1, nf, wave, lane, 32, p.alm, p.bem, 32, T, T5S, 0, nullptr, 0);
+    }
+    __syncthreads();
+
+    // ---- 3x3 32 -> 32, pad 1, on T[:, icoff : icoff + 32] (K = 9 taps x 32: one chunk per tap)
+    auto conv3 = [&](const __bf16* w, const float* al, const float* be, int icoff, char* lds_out, int lcoff,
+                     int gcoff) {
+        f4 acc[5][2];
+#pragma unroll
+        for (int f = 0; f < 5; f++)
+#pragma unroll
+            for (int j = 0; j < 2; j++) acc[f][j] = f4{0.f, 0.f, 0.f, 0.f};
+        int py[5], px[5];
+#pragma unroll
+        for (int f = 0; f < 5; f++) {
+            const int m = 16 * (wave + 4 * f) + r;
+            py[f] = m < B35_ROWS ? m / 17 : -100;
+            px[f] = m < B35_ROWS ? m - 17 * (m / 17) : 0;
+        }
+        const bf16x8* brow[2];
+#pragma unroll
+        for (int j = 0; j < 2; j++) brow[j] = (const bf16x8*)(w + (16 * j + r) * 288 + kq);
+        bf16x8 b[2][2];
+#pragma unroll
+        for (int j = 0; j < 2; j++) b[0][j] = brow[j][0];
+#pragma unroll
+        for (int t = 0; t < 9; t++) {
+            const int cur = t & 1;
+            if (t + 1 < 9)
+#pragma unroll
+                for (int j = 0; j < 2; j++) b[cur ^ 1][j] = brow[j][4 * (t + 1)];
+            const int dy = t / 3 - 1, dx = t % 3 - 1;
+#pragma unroll
+            for (int f = 0; f < 5; f++) {
+                if (f >= nf) break;
+                const int yy = py[f] + dy, xx = px[f] + dx;
+                const bool ok = (unsigned)yy < 17u && (unsigned)xx < 17u;
+                const char* src = ok ? T + (yy * 17 + xx) * T5S + (icoff + kq) * 2 : ZERO;
+                const bf16x8 a = *(const bf16x8*)src;
+#pragma unroll
+                for (int j = 0; j < 2; j++) acc[f][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b[cur][j], acc[f][j], 0, 0, 0);
+            }
+        }
+        __syncthreads();  // every wave is done reading T before a stage writes it
+        b35_store<2>(acc, nf, wave, lane, 0, al, be, 0, lds_out, T5S, lcoff, lds_out ? nullptr : CAT, gcoff);
+        __syncthreads();
+    };
+    conv3(p.w1, p.al1, p.be1, 0, nullptr, 0, 32);    // b1: T[:, 0:32] -> CAT[:, 32:64]
+    conv3(p.w2a, p.al2a, p.be2a, 32, T, 0, 0);      // b2 middle: T[:, 32:64] -> T[:, 0:32]
+    conv3(p.w2b, p.al2b, p.be2b, 0, nullptr, 0, 64);  // b2 tail: T[:, 0:32] -> CAT[:, 64:96]
+}
+
+}  // namespace
+
+// one Block17 (bf16 NHWC [N, 8, 8, 896] -> same): weights as FaceNet's layer table holds them
+void launch_block17_fused(const void* x, void* y, int N, const void* wm, const float* alm, const float* bem,
+                          const void* wa, const float* ala, const float* bea, const void* wb, const float* alb,
+                          const float* beb, const void* wo, const float* bo, float scale, hipStream_t st) {
+    if (N <= 0) return;
+    B17P p;
+    p.x = (const __bf16*)x;
+    p.y = (__bf16*)y;
+    p.wm = (const __bf16*)wm;
+    p.wa = (const __bf16*)wa;
+    p.wb = (const __bf16*)wb;
+    p.wo = (const __bf16*)wo;
+    p.alm = alm;
+    p.bem = bem;
+    p.ala = ala;
+    p.bea = bea;
+    p.alb = alb;
+    p.beb = beb;
+    p.bo = bo;
+    p.scale = scale;
+    static bool attr = [] {
+        VTF_HIP(hipFuncSetAttribute((const void*)k_block17, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES));
+        return true;
+    }();
+    (void)attr;
+    k_block17<<<N, 256, LDS_BYTES, st>>>(p);
+    VTF_HIP(hipGetLastError());
+}
+
+}  // namespace vtf
+
+namespace vtf {
+
+// Block35 branches (bf16 NHWC [N, 17, 17, 256] -> CAT [N, 17, 17, 96])
+void launch_block35_branches(const void* x, void* cat, int N, const void* wm, const float* alm, const float* bem,
+                             const void* w1, const float* al1, const float* be1, const void* w2a, const float* al2a,
+                             const float* be2a, const void* w2b, const float* al2b, const float* be2b,
+                             hipStream_t st) {
+    if (N <= 0) return;
+    B35P p;
+    p.x = (const __bf16*)x;
+    p.cat = (__bf16*)cat;
+    p.wm = (const __bf16*)wm;
+    p.w1 = (const __bf16*)w1;
+    p.w2a = (const __bf16*)w2a;
+    p.w2b = (const __bf16*)w2b;
+    p.alm = alm;
+    p.bem = bem;
+    p.al1 = al1;
+    p.be1 = be1;
+    p.al2a = al2a;
+    p.be2a = be2a;
+    p.al2b = al2b;
+    p.be2b = be2b;
+    k_block35_br<<<N, 256, B35_LDS, st>>>(p);
+    VTF_HIP(hipGetLastError());
+}
+
+}  // namespace vtf

@@ -5,6 +5,7 @@
 // same input (the first conv of every Inception branch) run as one merged launch whose output
 // channels are split between the concat buffer and the branch temporaries.
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <vector>
 
@@ -14,6 +15,21 @@
 #include "conv.hpp"
 
 namespace vtf {
+
+void launch_block17_fused(const void* x, void* y, int N, const void* wm, const float* alm, const float* bem,
+                          const void* wa, const float* ala, const float* bea, const void* wb, const float* alb,
+                          const float* beb, const void* wo, const float* bo, float scale, hipStream_t st);
+
+void launch_block35_branches(const void* x, void* cat, int N, const void* wm, const float* alm, const float* bem,
+                             const void* w1, const float* al1, const float* be1, const void* w2a, const float* al2a,
+                             const float* be2a, const void* w2b, const float* al2b, const float* be2b,
+                             hipStream_t st);
+
+// bf16 Block17 as one launch per block (facenet_fused.hip); VTF_FN_FUSED=0: the four launches
+static bool fused_blocks() {
+    const char* e = std::getenv("VTF_FN_FUSED");  // (read per forward: tests switch it in-process)
+    return !(e && std::atoi(e) == 0);
+}
 
 struct Layer {
     int cin, cout, kh, kw, sh, sw, ph, pw;
@@ -327,6 +343,20 @@ static void forward(Facenet& F, const void* x, int N, float* emb) {
     Act t1{}, t2{};
     // 5 x Block35 (facenet.py:14-33), scale 0.17
     for (int k = 0; k < 5; k++) {
+        if (F.bf16 && fused_blocks() && X.H == 17 && X.W == 17 && X.C == 256) {
+            // the three branches in one launch into CAT, then the tail conv
+            const Layer* lm = nullptr;
+            for (auto& e : F.LM)
+                if (e.first == li) lm = &e.second;
+            VTF_CHECK(lm, VTF_E_ARG, "facenet: no merged Block35 head");
+            const Layer &l1 = F.L[li + 2], &l2a = F.L[li + 4], &l2b = F.L[li + 5];
+            launch_block35_branches(X.p, CAT, N, lm->w, lm->alpha, lm->beta, l1.w, l1.alpha, l1.beta, l2a.w, l2a.alpha,
+                                    l2a.beta, l2b.w, l2b.alpha, l2b.beta, F.st);
+            li += 6;
+            conv(F, li++, Act{CAT, X.H, X.W, 96}, N, Y, 256, 0, X.p, 0.17f, true);
+            swap(256);
+            continue;
+        }
         // branch 0 -> CAT[0:32]; branch 1 / 2 heads -> T1[0:32] / T1[32:64]
         conv_merged(F, li, X, N, CAT, 96, 0, 32, T1, 64, 0);
         li += 2;
@@ -351,6 +381,18 @@ static void forward(Facenet& F, const void* x, int N, float* emb) {
     }
     // 10 x Block17 (facenet.py:36-56), scale 0.10
     for (int k = 0; k < 10; k++) {
+        if (F.bf16 && fused_blocks() && X.H == 8 && X.W == 8 && X.C == 896) {
+            const Layer* lm = nullptr;
+            for (auto& e : F.LM)
+                if (e.first == li) lm = &e.second;
+            VTF_CHECK(lm, VTF_E_ARG, "facenet: no merged Block17 head");
+            const Layer &la = F.L[li + 2], &lb = F.L[li + 3], &lo = F.L[li + 4];
+            launch_block17_fused(X.p, Y, N, lm->w, lm->alpha, lm->beta, la.w, la.alpha, la.beta, lb.w, lb.alpha,
+                                 lb.beta, lo.w, lo.b, 0.10f, F.st);
+            li += 5;
+            swap(896);
+            continue;
+        }
         conv_merged(F, li, X, N, CAT, 256, 0, 128, T1, 128, 0);
         li += 2;
         t1 = Act{T1, X.H, X.W, 128};
