@@ -220,3 +220,24 @@ def test_det_enc_pipeline_world2_matches_world1_gloo():
     assert res[0][3] == [np.asarray(lb).tolist() for lb in labels1]
     assert res[0][4] == scores1
     print('faces', faces1, 'kept', res[0][5]['clustered'])
+
+
+def test_rank_frames_one_global_sequence():
+    """rank_frames hands each rank its det-batches of one global frame sequence: with a cycled
+    pool the rank's first frame is pool frame (rank's global offset) mod pool; with pool 0 the
+    rank's frames are exactly the global sequence's frames [lo, hi) (content depends only on the
+    frame index)."""
+    import types
+    import bench
+    from videotofaces import synth
+    from videotofaces.parallel import shard_batches
+    a = bench.parse(['--det-batch', '4', '--pool', '8'])
+    a.H, a.W = 24, 32
+    ctx = types.SimpleNamespace(world=3, rank=1, device=torch.device('cpu'))
+    frames, off, fnp = bench.rank_frames(a, ctx, 5)
+    lo, hi = shard_batches(3 * 5 * 4, 4, 1, 3)
+    assert (lo, hi) == (20, 40) and off == lo % 8 and frames.shape[0] == 8 and fnp.shape[0] == 8
+    a.pool = 0
+    frames, off, fnp = bench.rank_frames(a, ctx, 5)
+    ref = synth.make_frames_device(0, 60, 24, 32, seed=1000)
+    assert off == 0 and torch.equal(frames, ref[20:40])

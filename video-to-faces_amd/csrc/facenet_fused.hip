@@ -20,6 +20,8 @@
 // slot s ^ ((r >> 1) & 7) (swizzle applied on the DMA source address; conflict-free fragment
 // reads, as conv_dma.hip); B1 / B2 rows padded to 528 / 272 B so the 16 rows of a fragment read
 // land on 16 distinct bank slots.
+#include <algorithm>
+
 #include "common.hpp"
 #include "conv.hpp"
 #include "conv_dev.hpp"
@@ -459,6 +461,129 @@ __global__ __launch_bounds__(256, 1) void k_block35_br(B35P p) {
     conv3(p.w2b, p.al2b, p.be2b, 0, nullptr, 0, 64);  // b2 tail: T[:, 0:32] -> CAT[:, 64:96]
 }
 
+// ---------------------------------------------------------------------------------------------
+// FaceNet stem 3x3 stride-1 convs with few input channels (conv2d_2a 32 -> 32, conv2d_2b 32 -> 64,
+// facenet.py:127-128) as "patch" convs: a tile of 8 x 16 output pixels reads its (8+2) x (16+2)
+// input patch once into LDS and all nine taps from there.  The implicit-GEMM launches gathered
+// every tap from L2 (9x the input bytes: ~0.5 GB per enc-batch for conv2d_2b, L2-bound).
+// Persistent workgroups (weights staged in LDS once), the next tile's patch loaded into registers
+// during the current tile's MFMAs.  k order (tap-major, 32 channels per chunk) and the BN + ReLU
+// epilogue are the unfused kernels', so the output is bit-identical.
+constexpr int CP_TH = 8, CP_TW = 16, CP_PH = CP_TH + 2, CP_PW = CP_TW + 2, CP_CIN = 32;
+constexpr int CP_PS = CP_CIN * 2 + 16;     // patch pixel stride (bytes): 16 consecutive pixels -> 16 bank slots
+constexpr int CP_WS = 9 * CP_CIN * 2 + 16;  // weight row stride (bytes)
+constexpr int CP_PIECES = CP_PH * CP_PW * CP_CIN * 2 / 16;  // 16-B patch pieces (720)
+constexpr int CP_PPT = (CP_PIECES + 255) / 256;             // per thread
+
+struct CPatchP {
+    const __bf16* in;  // [N][H][W][32]
+    __bf16* out;       // [N][OH][OW][COUT]
+    const __bf16* w;   // [COUT][9 * 32]
+    const float *al, *be;
+    int N, H, W, OH, OW, pad, tiles_x, tiles_y, tiles;
+};
+
+template <int COUT>
+__global__ __launch_bounds__(256, 2) void k_conv_patch(CPatchP p) {
+    constexpr int FN = COUT / 16;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    char* Wl = smem;                              // [COUT][CP_WS]
+    char* P = smem + COUT * CP_WS;                // patch [CP_PH * CP_PW][CP_PS]
+    char* E = P + CP_PH * CP_PW * CP_PS;          // output staging [128][COUT] bf16
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    // weights once per workgroup
+    for (int e = tid; e < COUT * 9 * CP_CIN / 8; e += 256) {
+        const int n = e / (9 * CP_CIN / 8), c = e - n * (9 * CP_CIN / 8);
+        *(bf16x8*)(Wl + n * CP_WS + c * 16) = *(const bf16x8*)(p.w + (int64_t)n * 9 * CP_CIN + 8 * c);
+    }
+    float al[FN], be[FN];
+#pragma unroll
+    for (int j = 0; j < FN; j++) {
+        al[j] = p.al[16 * j + (lane & 15)];
+        be[j] = p.be[16 * j + (lane & 15)];
+    }
+    auto tile_geo = [&](int t, int& n, int& oy0, int& ox0) {
+        const int per = p.tiles_x * p.tiles_y;
+        n = t / per;
+        const int r = t - n * per, ty = r / p.tiles_x;
+        oy0 = ty * CP_TH;
+        ox0 = (r - ty * p.tiles_x) * CP_TW;
+    };
+    bf16x8 pr[CP_PPT];
+    auto load_patch = [&](int t) {
+        int n, oy0, ox0;
+        tile_geo(t, n, oy0, ox0);
+#pragma unroll
+        for (int u = 0; u < CP_PPT; u++) {
+            const int e = tid + 256 * u;
+            bf16x8 v = {};
+            if (e < CP_PIECES) {
+                const int pix = e >> 2, c = e & 3;  // 4 pieces of 8 channels per pixel
+                const int py = pix / CP_PW, px = pix - py * CP_PW;
+                const int iy = oy0 - p.pad + py, ix = ox0 - p.pad + px;
+                if ((unsigned)iy < (unsigned)p.H && (unsigned)ix < (unsigned)p.W)
+                    v = *(const bf16x8*)(p.in + (((int64_t)n * p.H + iy) * p.W + ix) * CP_CIN + 8 * c);
+            }
+            pr[u] = v;
+        }
+    };
+    auto store_patch = [&]() {
+#pragma unroll
+        for (int u = 0; u < CP_PPT; u++) {
+            const int e = tid + 256 * u;
+            if (e < CP_PIECES) *(bf16x8*)(P + (e >> 2) * CP_PS + (e & 3) * 16) = pr[u];
+        }
+    };
+    int t = blockIdx.x;
+    if (t < p.tiles) load_patch(t);
+    // the lane's two A rows (fragments 2 wave, 2 wave + 1): tile pixel (ty, tx)
+    const int r = lane & 15, kq = 8 * (lane >> 4);
+    for (; t < p.tiles; t += gridDim.x) {
+        __syncthreads();  // the previous tile's patch and staging reads are done (weights on the first pass)
+        store_patch();
+        __syncthreads();
+        if (t + gridDim.x < p.tiles) load_patch(t + gridDim.x);
+        f4 acc[2][FN];
+#pragma unroll
+        for (int i = 0; i < 2; i++)
+#pragma unroll
+            for (int j = 0; j < FN; j++) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int tap = 0; tap < 9; tap++) {
+            const int dy = tap / 3, dx = tap % 3;
+            bf16x8 b[FN];
+#pragma unroll
+            for (int j = 0; j < FN; j++) b[j] = *(const bf16x8*)(Wl + (16 * j + r) * CP_WS + (tap * CP_CIN + kq) * 2);
+#pragma unroll
+            for (int i = 0; i < 2; i++) {
+                const int m = 16 * (2 * wave + i) + r, ty = m >> 4, tx = m & 15;
+                const bf16x8 a = *(const bf16x8*)(P + ((ty + dy) * CP_PW + tx + dx) * CP_PS + kq * 2);
+#pragma unroll
+                for (int j = 0; j < FN; j++) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b[j], acc[i][j], 0, 0, 0);
+            }
+        }
+        // BN + ReLU -> bf16 staging [128][COUT] -> 16-B stores of the in-bounds pixels
+#pragma unroll
+        for (int i = 0; i < 2; i++)
+#pragma unroll
+            for (int j = 0; j < FN; j++)
+#pragma unroll
+                for (int q = 0; q < 4; q++) {
+                    const int m = 16 * (2 * wave + i) + 4 * (lane >> 4) + q;
+                    *(__bf16*)(E + (m * COUT + 16 * j + (lane & 15)) * 2) = (__bf16)relu_bf(fmaf(acc[i][j][q], al[j], be[j]));
+                }
+        __syncthreads();
+        int n, oy0, ox0;
+        tile_geo(t, n, oy0, ox0);
+        for (int e = tid; e < 128 * COUT / 8; e += 256) {
+            const int m = e / (COUT / 8), c = e - m * (COUT / 8);
+            const int oy = oy0 + (m >> 4), ox = ox0 + (m & 15);
+            if (oy < p.OH && ox < p.OW)
+                *(bf16x8*)(p.out + (((int64_t)n * p.OH + oy) * p.OW + ox) * COUT + 8 * c) = *(const bf16x8*)(E + (m * COUT + 8 * c) * 2);
+        }
+    }
+}
+
 }  // namespace
 
 // one Block17 (bf16 NHWC [N, 8, 8, 896] -> same): weights as FaceNet's layer table holds them
@@ -517,6 +642,58 @@ void launch_block35_branches(const void* x, void* cat, int N, const void* wm, co
     p.be2b = be2b;
     k_block35_br<<<N, 256, B35_LDS, st>>>(p);
     VTF_HIP(hipGetLastError());
+}
+
+}  // namespace vtf
+
+namespace vtf {
+
+static int cus() {
+    static int n = [] {
+        int dev = 0, c = 256;
+        if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev);
+        return c;
+    }();
+    return n;
+}
+
+// FaceNet stem patch conv (3x3, stride 1, 32 input channels, bf16; cout 32 or 64); false = not this shape
+bool launch_conv_patch(const ConvParams& q, hipStream_t st) {
+    if (q.Cin != CP_CIN || q.KH != 3 || q.KW != 3 || q.sh != 1 || q.sw != 1 || q.ph != q.pw || q.ph > 1 ||
+        (q.Cout != 32 && q.Cout != 64) || q.in_cstride || q.out_cstride != q.Cout || q.out_coff || q.res || q.bias ||
+        !q.alpha || !q.relu || q.n_split)
+        return false;
+    CPatchP p;
+    p.in = (const __bf16*)q.in;
+    p.out = (__bf16*)q.out;
+    p.w = (const __bf16*)q.w;
+    p.al = q.alpha;
+    p.be = q.beta;
+    p.N = q.N;
+    p.H = q.H;
+    p.W = q.W;
+    p.OH = q.OH;
+    p.OW = q.OW;
+    p.pad = q.ph;
+    p.tiles_x = (q.OW + CP_TW - 1) / CP_TW;
+    p.tiles_y = (q.OH + CP_TH - 1) / CP_TH;
+    p.tiles = q.N * p.tiles_x * p.tiles_y;
+    if (p.tiles <= 0) return true;
+    const int grid = std::min(p.tiles, 2 * cus());
+    const size_t lds = (size_t)q.Cout * CP_WS + CP_PH * CP_PW * CP_PS + 128 * q.Cout * 2;
+    static bool attr = [] {
+        for (const void* f : {(const void*)k_conv_patch<32>, (const void*)k_conv_patch<64>})
+            VTF_HIP(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                        64 * CP_WS + CP_PH * CP_PW * CP_PS + 128 * 64 * 2));
+        return true;
+    }();
+    (void)attr;
+    if (q.Cout == 32)
+        k_conv_patch<32><<<grid, 256, lds, st>>>(p);
+    else
+        k_conv_patch<64><<<grid, 256, lds, st>>>(p);
+    VTF_HIP(hipGetLastError());
+    return true;
 }
 
 }  // namespace vtf

@@ -25,6 +25,8 @@ void launch_block35_branches(const void* x, void* cat, int N, const void* wm, co
                              const float* be2a, const void* w2b, const float* al2b, const float* be2b,
                              hipStream_t st);
 
+bool launch_conv_patch(const ConvParams& q, hipStream_t st);
+
 // bf16 Block17 as one launch per block (facenet_fused.hip); VTF_FN_FUSED=0: the four launches
 static bool fused_blocks() {
     const char* e = std::getenv("VTF_FN_FUSED");  // (read per forward: tests switch it in-process)
@@ -271,7 +273,8 @@ static void conv(Facenet& F, int li, const Act& in, int N, void* out, int out_cs
         p.scale = 1.f;
         p.relu = 1;
     }
-    launch_conv(p, F.bf16, F.st);
+    // the stem's 3x3 stride-1 convs on 32 channels: patch convs in the fused bf16 mode
+    if (!(F.bf16 && fused_blocks() && launch_conv_patch(p, F.st))) launch_conv(p, F.bf16, F.st);
     if (out_act) *out_act = Act{out, p.OH, p.OW, out_cstride};
 }
 
