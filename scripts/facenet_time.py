@@ -15,12 +15,13 @@ import torch  # noqa: E402
 def main():
     from videotofaces.encoders.facenet import InceptionResnetV1
     reps = int(sys.argv[1]) if len(sys.argv) > 1 else 20
+    modes = sys.argv[2].split(',') if len(sys.argv) > 2 else ['1', '0']
     m = InceptionResnetV1('cuda:0', precision='bf16')
     u8 = torch.from_numpy(np.random.default_rng(0).integers(0, 256, (128, 3, 160, 160), dtype=np.uint8))
     x = ((u8.float() - 127.5) * (1 / 128)).cuda()
     res = {}
     for rnd in range(3):
-        for mode in ('1', '0'):
+        for mode in modes:
             os.environ['VTF_FN_FUSED'] = mode
             m(x)
             torch.cuda.synchronize()

@@ -40,10 +40,12 @@ def test_bf16_drift_reported(g):
 
 
 @pytest.mark.parametrize('n', [128, 5])
-def test_bf16_fused_blocks_bit_identical(n, monkeypatch):
-    """The fused bf16 Block17 (csrc/facenet_fused.hip: one launch per block, activations in LDS)
-    runs the unfused launches' MFMA k order and epilogue arithmetic: embeddings bit-identical to
-    VTF_FN_FUSED=0 (four implicit-GEMM launches per block), at enc-batch 128 and a ragged 5."""
+def test_bf16_fused_blocks_vs_unfused(n, g, monkeypatch):
+    """The fused bf16 blocks (csrc/facenet_fused.hip: Block17 and the Block35 branches one launch
+    per block with the activations in LDS, the stem's 32-channel 3x3 convs as patch convs) run the
+    unfused kernels' MFMA k order and epilogue arithmetic; the unfused launches split K on small
+    grids (slice-order sums), so the two bf16 paths agree to bf16 rounding, not bit for bit.  Both
+    are checked against the fp32 golden's drift bar, and against each other (cos >= 0.9995)."""
     from videotofaces.encoders.facenet import InceptionResnetV1
     m = InceptionResnetV1('cuda:0', precision='bf16')
     u8 = torch.from_numpy(np.random.default_rng(n).integers(0, 256, (n, 3, 160, 160), dtype=np.uint8))
@@ -51,8 +53,15 @@ def test_bf16_fused_blocks_bit_identical(n, monkeypatch):
     fused = m(x).cpu().numpy()
     monkeypatch.setenv('VTF_FN_FUSED', '0')
     plain = m(x).cpu().numpy()
-    print('fused vs unfused: max |diff| %.3g, identical %s' % (np.abs(fused - plain).max(), np.array_equal(fused, plain)))
-    np.testing.assert_array_equal(fused, plain)
+    cos = (fused * plain).sum(1)
+    print('fused vs unfused: max |diff| %.3g, cos min %.6f, identical %s'
+          % (np.abs(fused - plain).max(), cos.min(), np.array_equal(fused, plain)))
+    assert cos.min() > 0.9995
+    xg = (torch.from_numpy(g['u8']).float() - 127.5) * (1 / 128)
+    for mode in ('1', '0'):
+        monkeypatch.setenv('VTF_FN_FUSED', mode)
+        e = m(xg).cpu().numpy()
+        assert (e * g['emb']).sum(1).min() > 0.99, mode
 
 
 def test_blob_kernel_matches_restated_inter_linear():

@@ -40,14 +40,17 @@ constexpr int R_OFF = 0;                // ring base
 constexpr int B1_OFF = S1_R * S1_SLOT;  // 120 KB
 constexpr int ZERO_OFF = B1_OFF + 64 * B1S;
 constexpr int LDS_BYTES = ZERO_OFF + 16;
-// stages 2-4 reuse the stage-1 ring region: B2, the weight ring (128 rows per slot), the epilogue image
+// stages 2-4 reuse the stage-1 ring region: B2 (stages 2-3) / the stage-4 epilogue image E (fp32
+// [64][128 + 4]) at its start, then ONE weight ring for all of stages 2-4 (128 rows x 64 k per
+// slot; 56 groups: 14 of W_a, 14 of W_b, 28 of W_o) that keeps streaming across the stage
+// boundaries and epilogues
 constexpr int S2_SLOT = 128 * RB;       // 16 KB
-constexpr int S2_R = 4;                 // 3 groups in flight
+constexpr int S2_R = 5;                 // 4 groups in flight
 constexpr int B2_OFF = 0;
-constexpr int R2_OFF = 64 * B2S;        // 17,408
-constexpr int E_OFF = R2_OFF + S2_R * S2_SLOT;  // 82,944; fp32 [64][128 + 4]
+constexpr int E_OFF = 0;
 constexpr int E_LD = 132;
-static_assert(E_OFF + 64 * E_LD * 4 <= B1_OFF, "stage-4 image inside the stage-1 ring region");
+constexpr int R2_OFF = 64 * E_LD * 4;   // 33,792
+static_assert(64 * B2S <= R2_OFF && R2_OFF + S2_R * S2_SLOT <= B1_OFF, "stage 2-4 LDS plan");
 static_assert(LDS_BYTES <= 160 * 1024, "LDS plan");
 
 typedef __attribute__((ext_vector_type(4))) float f4;
@@ -65,9 +68,11 @@ __device__ inline void glds16(const void* g, void* l) {
                                      (void __attribute__((address_space(3)))*)l, 16, 0, 0);
 }
 
+// this wave's DMA groups up to the one N instructions back have landed and its LDS writes are
+// done; after the barrier every wave's are
 template <int N>
 __device__ inline void wait_vm_barrier() {
-    asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(N) : "memory");
+    asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(N) : "memory");
 }
 
 // DMA rows [0, rows) x 128 B (bytes kb .. kb+127 of each row of a matrix with row pitch `pitch`)
@@ -121,6 +126,21 @@ __global__ __launch_bounds__(256, 1) void k_block17(B17P p) {
     char* B2 = smem + B2_OFF;
     const char* ZERO = smem + ZERO_OFF;
     if (tid < 4) ((float*)(smem + ZERO_OFF))[tid] = 0.f;
+    // stages 2-4's weight groups (see below)
+    auto issue2 = [&](int g) {
+        const char* w;
+        int64_t pitch, kb;
+        if (g < 28) {
+            w = (const char*)(g < 14 ? p.wa : p.wb);
+            pitch = 896 * 2;
+            kb = (int64_t)(g % 14) * RB;
+        } else {
+            w = (const char*)p.wo + (int64_t)((g - 28) >> 2) * 128 * 256 * 2;
+            pitch = 256 * 2;
+            kb = (int64_t)((g - 28) & 3) * RB;
+        }
+        dma_rows<128>(w, pitch, kb, smem + R2_OFF + (g % S2_R) * S2_SLOT, wave, lane);
+    };
 
     // ---------------- stage 1: X[64][896] x W_m^T -> B1 (wave: output channels 64 wave .. +64)
     {
@@ -158,103 +178,46 @@ __global__ __launch_bounds__(256, 1) void k_block17(B17P p) {
                 }
             }
         }
+        // stages 2-4's first weight groups go out before the epilogue (the stage-1 ring is free once
+        // every wave is past this barrier), so the ring never restarts
+        lds_barrier();
+        issue2(0);
+        issue2(1);
+        issue2(2);
+        issue2(3);
         bn_relu_to_lds<4, 4>(acc, p.alm, p.bem, 64 * wave, B1, B1S, lane);
     }
-    __syncthreads();  // B1 complete; the stage-1 ring is free
 
-    // ---------------- stages 2 and 3: 1 x 7 and 7 x 1 convs, 128 -> 128 (wave: channels 32 wave .. +32)
-    auto conv7 = [&](const __bf16* w, const float* al, const float* be, const char* in, int in_stride, int in_coff,
-                     bool along_w, char* out, int out_stride, int out_coff) {
-        constexpr int S = 14, G = 4;
-        auto issue = [&](int s) {
-            dma_rows<128>((const char*)w, 896 * 2, (int64_t)s * RB, smem + R2_OFF + (s % S2_R) * S2_SLOT, wave, lane);
-        };
+    // ---------------- stages 2-4 on one weight ring (wave: output channels 32 wave .. +32)
+    //   groups  0..13: 1 x 7 on B1[:, 128:256] -> B2         (k = tap * 128 + channel)
+    //   groups 14..27: 7 x 1 on B2 -> B1[:, 128:256]
+    //   groups 28..55: pass (g - 28) / 4 of W_o (128 output channels), k-step (g - 28) % 4
+    {
+        constexpr int NG = 56, G = 4;
         f4 acc[4][2];
-#pragma unroll
-        for (int i = 0; i < 4; i++)
-#pragma unroll
-            for (int j = 0; j < 2; j++) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
-        issue(0);
-        issue(1);
-        issue(2);
-        // the lane's A rows: output pixel (y, x) of row 16 i + (lane & 15)
-        const int r = lane & 15;
-        for (int s = 0; s < S; s++) {
-            if (s + 2 < S)
+        const int r = lane & 15, kq = 8 * (lane >> 4);
+        float* E = (float*)(smem + E_OFF);
+        char* Y = (char*)(p.y + (int64_t)img * 64 * 896);
+        int issued = 4;
+        for (int g = 0; g < NG; g++) {
+            const int ahead = issued - g - 1;
+            if (ahead >= 3)
+                wait_vm_barrier<3 * G>();
+            else if (ahead == 2)
                 wait_vm_barrier<2 * G>();
-            else if (s + 1 < S)
+            else if (ahead == 1)
                 wait_vm_barrier<G>();
             else
                 wait_vm_barrier<0>();
-            if (s + 3 < S) issue(s + 3);
-            const char* W = smem + R2_OFF + (s % S2_R) * S2_SLOT + 32 * wave * RB;
-            const int t = s >> 1, c0 = in_coff + 64 * (s & 1);
-#pragma unroll
-            for (int h = 0; h < 2; h++) {
-                bf16x8 b[2];
-#pragma unroll
-                for (int j = 0; j < 2; j++) b[j] = frag_sw(W, j, h, lane);
-#pragma unroll
-                for (int i = 0; i < 4; i++) {
-                    const int y = 2 * i + (r >> 3), x = r & 7;
-                    const int yy = along_w ? y : y + t - 3, xx = along_w ? x + t - 3 : x;
-                    const bool ok = (unsigned)yy < 8u && (unsigned)xx < 8u;
-                    const char* src = ok ? in + (yy * 8 + xx) * in_stride + (c0 + 32 * h + 8 * (lane >> 4)) * 2 : ZERO;
-                    const bf16x8 a = *(const bf16x8*)src;
-#pragma unroll
-                    for (int j = 0; j < 2; j++) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b[j], acc[i][j], 0, 0, 0);
-                }
-            }
-        }
-        // (out may alias the columns `in` read: barrier before writing)
-        __syncthreads();
-#pragma unroll
-        for (int j = 0; j < 2; j++) {
-            const int n = 32 * wave + 16 * j + (lane & 15);
-            const float a = al[n], b = be[n];
-#pragma unroll
-            for (int i = 0; i < 4; i++)
-#pragma unroll
-                for (int q = 0; q < 4; q++) {
-                    const int m = 16 * i + 4 * (lane >> 4) + q;
-                    *(__bf16*)(out + m * out_stride + (out_coff + n) * 2) = (__bf16)relu_bf(fmaf(acc[i][j][q], a, b));
-                }
-        }
-        __syncthreads();
-    };
-    conv7(p.wa, p.ala, p.bea, B1, B1S, 128, true, B2, B2S, 0);
-    conv7(p.wb, p.alb, p.beb, B2, B2S, 0, false, B1, B1S, 128);
-
-    // ---------------- stage 4: B1[64][256] x W_o^T + b_o, x scale, + X, ReLU -> Y (7 passes of 128 channels)
-    {
-        constexpr int S = 28, G = 4;  // (pass, k-step) groups
-        auto issue = [&](int s) {
-            const int pass = s >> 2, ks = s & 3;
-            dma_rows<128>((const char*)p.wo + (int64_t)pass * 128 * 256 * 2, 256 * 2, (int64_t)ks * RB,
-                          smem + R2_OFF + (s % S2_R) * S2_SLOT, wave, lane);
-        };
-        float* E = (float*)(smem + E_OFF);
-        char* Y = (char*)(p.y + (int64_t)img * 64 * 896);
-        issue(0);
-        issue(1);
-        issue(2);
-        f4 acc[4][2];
-        for (int s = 0; s < S; s++) {
-            const int ks = s & 3;
-            if (ks == 0) {
+            if (issued < NG) issue2(issued++);
+            const int st = g < 14 ? 0 : (g < 28 ? 1 : 2), ks = st < 2 ? g - 14 * st : (g - 28) & 3;
+            if (st < 2 ? ks == 0 : ks == 0) {
 #pragma unroll
                 for (int i = 0; i < 4; i++)
 #pragma unroll
                     for (int j = 0; j < 2; j++) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
             }
-            if (s + 2 < S)
-                wait_vm_barrier<2 * G>();
-            else if (s + 1 < S)
-                wait_vm_barrier<G>();
-            else
-                wait_vm_barrier<0>();
-            if (s + 3 < S) issue(s + 3);
-            const char* W = smem + R2_OFF + (s % S2_R) * S2_SLOT + 32 * wave * RB;
+            const char* W = smem + R2_OFF + (g % S2_R) * S2_SLOT + 32 * wave * RB;
 #pragma unroll
             for (int h = 0; h < 2; h++) {
                 bf16x8 b[2];
@@ -262,16 +225,34 @@ __global__ __launch_bounds__(256, 1) void k_block17(B17P p) {
                 for (int j = 0; j < 2; j++) b[j] = frag_sw(W, j, h, lane);
 #pragma unroll
                 for (int i = 0; i < 4; i++) {
-                    const int m = 16 * i + (lane & 15);
-                    const bf16x8 a = *(const bf16x8*)(B1 + m * B1S + (64 * ks + 32 * h + 8 * (lane >> 4)) * 2);
+                    const char* src;
+                    if (st < 2) {  // 1 x 7 / 7 x 1 implicit GEMM: tap ks / 2, channels 64 (ks & 1) + 32 h
+                        const int t = ks >> 1, y = 2 * i + (r >> 3), x = r & 7;
+                        const int yy = st == 0 ? y : y + t - 3, xx = st == 0 ? x + t - 3 : x;
+                        const bool ok = (unsigned)yy < 8u && (unsigned)xx < 8u;
+                        const int c = 64 * (ks & 1) + 32 * h + kq;
+                        src = !ok ? ZERO : (st == 0 ? B1 + (yy * 8 + xx) * B1S + (128 + c) * 2 : B2 + (yy * 8 + xx) * B2S + c * 2);
+                    } else {
+                        src = B1 + (16 * i + r) * B1S + (64 * ks + 32 * h + kq) * 2;
+                    }
+                    const bf16x8 a = *(const bf16x8*)src;
 #pragma unroll
                     for (int j = 0; j < 2; j++) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b[j], acc[i][j], 0, 0, 0);
                 }
             }
-            if (ks == 3) {
-                // pass epilogue through an fp32 image: 8 consecutive channels per thread (16-B
-                // residual loads and output stores), conv_epilogue8's arithmetic
-                const int pass = s >> 2;
+            if (st < 2 && ks == 13) {
+                // BN + ReLU into the next operand (read only after the next group's barrier)
+                const float* al = st == 0 ? p.ala : p.alb;
+                const float* be = st == 0 ? p.bea : p.beb;
+                if (st == 0)
+                    bn_relu_to_lds<4, 2>(acc, al, be, 32 * wave, B2, B2S, lane);
+                else
+                    bn_relu_to_lds<4, 2>(acc, al, be, 32 * wave, B1 + 128 * 2, B1S, lane);
+            } else if (st == 2 && ks == 3) {
+                // pass epilogue through the fp32 image E (B2 is dead by now): 8 consecutive channels
+                // per thread (16-B residual loads and output stores), conv_epilogue8's arithmetic;
+                // E is rewritten four groups (four barriers) later
+                const int pass = (g - 28) >> 2;
 #pragma unroll
                 for (int i = 0; i < 4; i++)
 #pragma unroll
@@ -282,8 +263,8 @@ __global__ __launch_bounds__(256, 1) void k_block17(B17P p) {
                 lds_barrier();
 #pragma unroll
                 for (int u = 0; u < 4; u++) {
-                    const int e = tid + 256 * u, m = e >> 4, g = e & 15, c0 = pass * 128 + 8 * g;
-                    const f4 lo = *(const f4*)(E + m * E_LD + 8 * g), hi = *(const f4*)(E + m * E_LD + 8 * g + 4);
+                    const int e = tid + 256 * u, m = e >> 4, gg = e & 15, c0 = pass * 128 + 8 * gg;
+                    const f4 lo = *(const f4*)(E + m * E_LD + 8 * gg), hi = *(const f4*)(E + m * E_LD + 8 * gg + 4);
                     const float v[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
                     const bf16x8 rx = *(const bf16x8*)(X + ((int64_t)m * 896 + c0) * 2);
                     bf16x8 o;
@@ -296,7 +277,6 @@ __global__ __launch_bounds__(256, 1) void k_block17(B17P p) {
                     }
                     *(bf16x8*)(Y + ((int64_t)m * 896 + c0) * 2) = o;
                 }
-                lds_barrier();  // E is rewritten by the next pass
             }
         }
     }
@@ -315,7 +295,11 @@ __global__ __launch_bounds__(256, 1) void k_block17(B17P p) {
 // L2-resident), one 32-deep chunk ahead; same k order and epilogue as the unfused launches.
 constexpr int T5S = 64 * 2 + 16;  // T row stride (bytes)
 constexpr int B35_ROWS = 289, B35_FR = 19;
-constexpr int B35_LDS = B35_FR * 16 * T5S + 16;
+constexpr int WM5S = 256 * 2 + 16, W35S = 288 * 2 + 16;  // resident weight row strides (conflict-free)
+constexpr int B35_WM = 0, B35_W3 = B35_WM + 96 * WM5S, B35_T = B35_W3 + 3 * 32 * W35S;
+constexpr int B35_ZERO = B35_T + B35_FR * 16 * T5S;
+constexpr int B35_LDS = B35_ZERO + 16;
+static_assert(B35_LDS <= 160 * 1024, "Block35 LDS plan");
 
 struct B35P {
     const __bf16* x;  // [N][289][256]
@@ -350,19 +334,31 @@ __device__ inline void b35_store(const f4 (&acc)[5][NF], int nf, int wave, int l
     }
 }
 
+// Block35 branches: every weight (103 KB) resident in LDS from the start (one burst of loads), so
+// the only global reads in the loops are the wave's own input rows (stage 1, three chunks ahead)
 __global__ __launch_bounds__(256, 1) void k_block35_br(B35P p) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int img = blockIdx.x;
     const int nf = wave < 3 ? 5 : 4;  // fragments w, w + 4, ..., < 19
-    char* T = smem;
-    const char* ZERO = smem + B35_FR * 16 * T5S;
-    if (tid < 4) ((float*)(smem + B35_FR * 16 * T5S))[tid] = 0.f;
+    char* T = smem + B35_T;
+    const char* ZERO = smem + B35_ZERO;
+    if (tid < 4) ((float*)(smem + B35_ZERO))[tid] = 0.f;
     const __bf16* X = p.x + (int64_t)img * B35_ROWS * 256;
     __bf16* CAT = p.cat + (int64_t)img * B35_ROWS * 96;
     const int r = lane & 15, kq = 8 * (lane >> 4);
+    // weights -> LDS (padded rows)
+    for (int e = tid; e < 96 * 32; e += 256) {
+        const int n = e >> 5, c = e & 31;
+        *(bf16x8*)(smem + B35_WM + n * WM5S + c * 16) = *(const bf16x8*)(p.wm + n * 256 + 8 * c);
+    }
+    for (int e = tid; e < 3 * 32 * 36; e += 256) {
+        const int cv = e / (32 * 36), rem = e - cv * 32 * 36, n = rem / 36, c = rem - n * 36;
+        const __bf16* w = cv == 0 ? p.w1 : (cv == 1 ? p.w2a : p.w2b);
+        *(bf16x8*)(smem + B35_W3 + (cv * 32 + n) * W35S + c * 16) = *(const bf16x8*)(w + n * 288 + 8 * c);
+    }
 
-    // ---- stage 1 (K = 256: 8 chunks of 32; N = 96: 6 fragments)
+    // ---- stage 1 (K = 256: 8 chunks of 32; N = 96: 6 fragments); input rows 3 chunks ahead
     {
         f4 acc[5][6];
 #pragma unroll
@@ -375,29 +371,26 @@ __global__ __launch_bounds__(256, 1) void k_block35_br(B35P p) {
             const int m = min(16 * (wave + 4 * f) + r, B35_ROWS - 1);  // padding rows: any finite row
             arow[f] = (const bf16x8*)(X + (int64_t)m * 256 + kq);
         }
-        const bf16x8* brow[6];
+        bf16x8 a[4][5];
 #pragma unroll
-        for (int j = 0; j < 6; j++) brow[j] = (const bf16x8*)(p.wm + (16 * j + r) * 256 + kq);
-        bf16x8 a[2][5], b[2][6];
+        for (int c = 0; c < 3; c++)
 #pragma unroll
-        for (int f = 0; f < 5; f++) a[0][f] = arow[f][0];
-#pragma unroll
-        for (int j = 0; j < 6; j++) b[0][j] = brow[j][0];
+            for (int f = 0; f < 5; f++) a[c][f] = arow[f][4 * c];
+        __syncthreads();  // resident weights stored
 #pragma unroll
         for (int c = 0; c < 8; c++) {
-            const int cur = c & 1;
-            if (c + 1 < 8) {
+            if (c + 3 < 8)
 #pragma unroll
-                for (int f = 0; f < 5; f++) a[cur ^ 1][f] = arow[f][4 * (c + 1)];
+                for (int f = 0; f < 5; f++) a[(c + 3) & 3][f] = arow[f][4 * (c + 3)];
+            bf16x8 b[6];
 #pragma unroll
-                for (int j = 0; j < 6; j++) b[cur ^ 1][j] = brow[j][4 * (c + 1)];
-            }
+            for (int j = 0; j < 6; j++) b[j] = *(const bf16x8*)(smem + B35_WM + (16 * j + r) * WM5S + (32 * c + kq) * 2);
 #pragma unroll
             for (int f = 0; f < 5; f++)
                 if (f < nf)
 #pragma unroll
                     for (int j = 0; j < 6; j++)
-                        acc[f][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[cur][f], b[cur][j], acc[f][j], 0, 0, 0);
+                        acc[f][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[c & 3][f], b[j], acc[f][j], 0, 0, 0);
         }
         // b0 (channels 0..31) -> CAT[:, 0:32]; heads (32..95) -> T[:, 0:64]
         f4 a0[5][2], a1[5][4];
@@ -414,32 +407,25 @@ __global__ __launch_bounds__(256, 1) void k_block35_br(B35P p) {
     __syncthreads();
 
     // ---- 3x3 32 -> 32, pad 1, on T[:, icoff : icoff + 32] (K = 9 taps x 32: one chunk per tap)
-    auto conv3 = [&](const __bf16* w, const float* al, const float* be, int icoff, char* lds_out, int lcoff,
-                     int gcoff) {
+    int py[5], px[5];
+#pragma unroll
+    for (int f = 0; f < 5; f++) {
+        const int m = 16 * (wave + 4 * f) + r;
+        py[f] = m < B35_ROWS ? m / 17 : -100;
+        px[f] = m < B35_ROWS ? m - 17 * (m / 17) : 0;
+    }
+    auto conv3 = [&](int cv, const float* al, const float* be, int icoff, char* lds_out, int lcoff, int gcoff) {
         f4 acc[5][2];
 #pragma unroll
         for (int f = 0; f < 5; f++)
 #pragma unroll
             for (int j = 0; j < 2; j++) acc[f][j] = f4{0.f, 0.f, 0.f, 0.f};
-        int py[5], px[5];
-#pragma unroll
-        for (int f = 0; f < 5; f++) {
-            const int m = 16 * (wave + 4 * f) + r;
-            py[f] = m < B35_ROWS ? m / 17 : -100;
-            px[f] = m < B35_ROWS ? m - 17 * (m / 17) : 0;
-        }
-        const bf16x8* brow[2];
-#pragma unroll
-        for (int j = 0; j < 2; j++) brow[j] = (const bf16x8*)(w + (16 * j + r) * 288 + kq);
-        bf16x8 b[2][2];
-#pragma unroll
-        for (int j = 0; j < 2; j++) b[0][j] = brow[j][0];
+        const char* W = smem + B35_W3 + cv * 32 * W35S;
 #pragma unroll
         for (int t = 0; t < 9; t++) {
-            const int cur = t & 1;
-            if (t + 1 < 9)
+            bf16x8 b[2];
 #pragma unroll
-                for (int j = 0; j < 2; j++) b[cur ^ 1][j] = brow[j][4 * (t + 1)];
+            for (int j = 0; j < 2; j++) b[j] = *(const bf16x8*)(W + (16 * j + r) * W35S + (32 * t + kq) * 2);
             const int dy = t / 3 - 1, dx = t % 3 - 1;
 #pragma unroll
             for (int f = 0; f < 5; f++) {
@@ -449,16 +435,16 @@ __global__ __launch_bounds__(256, 1) void k_block35_br(B35P p) {
                 const char* src = ok ? T + (yy * 17 + xx) * T5S + (icoff + kq) * 2 : ZERO;
                 const bf16x8 a = *(const bf16x8*)src;
 #pragma unroll
-                for (int j = 0; j < 2; j++) acc[f][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b[cur][j], acc[f][j], 0, 0, 0);
+                for (int j = 0; j < 2; j++) acc[f][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b[j], acc[f][j], 0, 0, 0);
             }
         }
         __syncthreads();  // every wave is done reading T before a stage writes it
         b35_store<2>(acc, nf, wave, lane, 0, al, be, 0, lds_out, T5S, lcoff, lds_out ? nullptr : CAT, gcoff);
         __syncthreads();
     };
-    conv3(p.w1, p.al1, p.be1, 0, nullptr, 0, 32);    // b1: T[:, 0:32] -> CAT[:, 32:64]
-    conv3(p.w2a, p.al2a, p.be2a, 32, T, 0, 0);      // b2 middle: T[:, 32:64] -> T[:, 0:32]
-    conv3(p.w2b, p.al2b, p.be2b, 0, nullptr, 0, 64);  // b2 tail: T[:, 0:32] -> CAT[:, 64:96]
+    conv3(0, p.al1, p.be1, 0, nullptr, 0, 32);    // b1: T[:, 0:32] -> CAT[:, 32:64]
+    conv3(1, p.al2a, p.be2a, 32, T, 0, 0);       // b2 middle: T[:, 32:64] -> T[:, 0:32]
+    conv3(2, p.al2b, p.be2b, 0, nullptr, 0, 64);  // b2 tail: T[:, 0:32] -> CAT[:, 64:96]
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -640,6 +626,11 @@ void launch_block35_branches(const void* x, void* cat, int N, const void* wm, co
     p.be2a = be2a;
     p.al2b = al2b;
     p.be2b = be2b;
+    static bool attr = [] {
+        VTF_HIP(hipFuncSetAttribute((const void*)k_block35_br, hipFuncAttributeMaxDynamicSharedMemorySize, B35_LDS));
+        return true;
+    }();
+    (void)attr;
     k_block35_br<<<N, 256, B35_LDS, st>>>(p);
     VTF_HIP(hipGetLastError());
 }
