@@ -1,6 +1,7 @@
-// FaceNet Block17 (src/videotofaces/encoders/facenet.py:36-56) as ONE launch per block in the
-// bf16 mode: one workgroup per image (8 x 8 pixels x 896 channels), the whole branch chain kept
-// on chip.
+// FaceNet bf16 blocks as single launches (src/videotofaces/encoders/facenet.py:14-56, 126-128).
+//
+// Block17 as ONE launch per block: one workgroup per image (8 x 8 pixels x 896 channels), the
+// whole branch chain kept on chip.
 //
 // The unfused form is four implicit-GEMM launches per block at batch 128 (M = 8192 rows):
 // merged 1x1 896 -> 128|128, 1x7 128 -> 128, 7x1 128 -> 128, 1x1 256 -> 896 + residual -- each a
@@ -10,17 +11,22 @@
 //   stage 2  C2[64][128] = im2col_1x7(B1[:, 128:256]) W_a^T, BN+ReLU -> B2 (LDS)
 //   stage 3  C3[64][128] = im2col_7x1(B2) W_b^T, BN + ReLU          -> B1[:, 128:256] (the concat)
 //   stage 4  Y[64][896] = ReLU(0.1 (B1 W_o^T + b_o) + X)            -> HBM, 7 passes of 128 channels
-// Weights stream HBM/L2 -> LDS through an LDS-DMA ring (global_load_lds_dwordx4, counted vmcnt,
-// one barrier per k-step); the stage-1 input rows ride in the same ring.  Every GEMM runs the
-// unfused kernels' k order -- 32-deep v_mfma_f32_16x16x32_bf16 chunks in ascending k from a zero
-// accumulator -- and the same epilogue arithmetic (conv_dev.hpp conv_epilogue8), so the block's
-// output is bit-identical to the four launches (tests/test_facenet_gpu.py).
+// Every GEMM runs the unfused kernels' k order -- 32-deep v_mfma_f32_16x16x32_bf16 chunks in
+// ascending k from a zero accumulator -- and the same epilogue arithmetic (conv_dev.hpp
+// conv_epilogue8); the unfused launches split K on small grids, so the two paths agree to bf16
+// rounding (identical at small batches; tests/test_facenet_gpu.py).  LDS images are padded (row
+// strides 16 B past a multiple of 256 B) so the 16 rows of a fragment read land on 16 distinct
+// bank slots.
 //
-// LDS images: weight / X rows of 128 B (one 64-deep k-step), 16-B slot s of row r holding source
-// slot s ^ ((r >> 1) & 7) (swizzle applied on the DMA source address; conflict-free fragment
-// reads, as conv_dma.hip); B1 / B2 rows padded to 528 / 272 B so the 16 rows of a fragment read
-// land on 16 distinct bank slots.
+// What bounds it (measured, VTF_B17_CLK stage clocks): every workgroup streams the block's 1.38 MB
+// of weights from L2, at ~12 B/cycle per CU -- the same per-CU L2 rate the unfused 64 x 64 GEMM
+// tiles run at.  An LDS-DMA weight ring (57 us: ~150 cycles of issue per 1-KB piece), register
+// rings 4 and 8 chunks deep, an L2 warm-up and free scheduling all measured within 3 % of each
+// other: 57 us per block against 74 us for the four launches.
 #include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
 
 #include "common.hpp"
 #include "conv.hpp"
@@ -30,28 +36,9 @@ namespace vtf {
 
 namespace {
 
-constexpr int RB = 128;                 // image row bytes per 64-deep k-step
 constexpr int B1S = 256 * 2 + 16;       // B1 row stride (bytes): 256 channels + pad
 constexpr int B2S = 128 * 2 + 16;       // B2 row stride
-constexpr int S1_X = 64 * RB;           // stage-1 slot: X rows (8 KB) ...
-constexpr int S1_SLOT = S1_X + 256 * RB;  // ... + W_m rows (32 KB)
-constexpr int S1_R = 3;                 // stage-1 ring slots (2 groups in flight)
-constexpr int R_OFF = 0;                // ring base
-constexpr int B1_OFF = S1_R * S1_SLOT;  // 120 KB
-constexpr int ZERO_OFF = B1_OFF + 64 * B1S;
-constexpr int LDS_BYTES = ZERO_OFF + 16;
-// stages 2-4 reuse the stage-1 ring region: B2 (stages 2-3) / the stage-4 epilogue image E (fp32
-// [64][128 + 4]) at its start, then ONE weight ring for all of stages 2-4 (128 rows x 64 k per
-// slot; 56 groups: 14 of W_a, 14 of W_b, 28 of W_o) that keeps streaming across the stage
-// boundaries and epilogues
-constexpr int S2_SLOT = 128 * RB;       // 16 KB
-constexpr int S2_R = 5;                 // 4 groups in flight
-constexpr int B2_OFF = 0;
-constexpr int E_OFF = 0;
-constexpr int E_LD = 132;
-constexpr int R2_OFF = 64 * E_LD * 4;   // 33,792
-static_assert(64 * B2S <= R2_OFF && R2_OFF + S2_R * S2_SLOT <= B1_OFF, "stage 2-4 LDS plan");
-static_assert(LDS_BYTES <= 160 * 1024, "LDS plan");
+constexpr int E_LD = 132;               // stage-4 fp32 epilogue image row stride (floats)
 
 typedef __attribute__((ext_vector_type(4))) float f4;
 
@@ -61,43 +48,10 @@ struct B17P {
     const __bf16 *wm, *wa, *wb, *wo;  // [256][896], [128][896], [128][896], [896][256]
     const float *alm, *bem, *ala, *bea, *alb, *beb, *bo;
     float scale;
+    unsigned long long* clk;  // debug (VTF_B17_CLK): thread 0's shader clock at the stage ends, [N][5]
 };
 
-__device__ inline void glds16(const void* g, void* l) {
-    __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)g,
-                                     (void __attribute__((address_space(3)))*)l, 16, 0, 0);
-}
-
-// this wave's DMA groups up to the one N instructions back have landed and its LDS writes are
-// done; after the barrier every wave's are
-template <int N>
-__device__ inline void wait_vm_barrier() {
-    asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(N) : "memory");
-}
-
-// DMA rows [0, rows) x 128 B (bytes kb .. kb+127 of each row of a matrix with row pitch `pitch`)
-// into a swizzled LDS image: rows / 32 one-KB pieces per wave
-template <int ROWS>
-__device__ inline void dma_rows(const char* src, int64_t pitch, int64_t kb, char* dst, int wave, int lane) {
-    const int sl = (lane & 7) ^ (((lane >> 4) + 4 * (wave & 1)) & 7);
-#pragma unroll
-    for (int j = 0; j < ROWS / 32; j++) {
-        const int r = 32 * j + 8 * wave + (lane >> 3);
-        glds16(src + r * pitch + kb + sl * 16, dst + (wave + 4 * j) * 1024);
-    }
-}
-
-// fragment of a swizzled 128-B-row image: rows 16 i + (lane & 15), k half h (0: k 0..31, 1: 32..63)
-__device__ inline bf16x8 frag_sw(const char* img, int i, int h, int lane) {
-    const int r = lane & 15, s = (4 * h + (lane >> 4)) ^ (r >> 1);
-    return *(const bf16x8*)(img + (16 * i + r) * RB + s * 16);
-}
-
 __device__ inline float relu_bf(float v) { return fmaxf(v, 0.f); }
-
-// workgroup barrier for LDS traffic only: __syncthreads() would also wait vmcnt(0), draining the
-// weight DMAs in flight
-__device__ inline void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
 // BN + ReLU epilogue of a [64][NC-per-wave] accumulator block into an LDS bf16 image
 template <int FM, int FN>
@@ -117,169 +71,224 @@ __device__ inline void bn_relu_to_lds(const f4 (&acc)[FM][FN], const float* al, 
     }
 }
 
+// Weight fragments stream straight from L2 into registers (each wave loads only its own output
+// channels' rows: no redundancy, no LDS staging); chunk c + R - 1's loads are issued while chunk c
+// computes (R = 8 chunks of 32 k).
+constexpr int X_S = 896 * 2 + 16;          // resident input image row stride (bytes)
+constexpr int K17_X = 0;                    // X image [64][X_S] (stage 1), then B2 / E (stages 2-4)
+constexpr int K17_B1 = 64 * X_S;            // 115,712
+constexpr int K17_ZERO = K17_B1 + 64 * B1S;
+constexpr int K17_LDS = K17_ZERO + 16;
+constexpr int K17_E = 64 * B2S;             // E after B2 (stage 4 only; B2 is dead by then anyway)
+static_assert(K17_E + 64 * E_LD * 4 <= K17_B1 && K17_LDS <= 160 * 1024, "Block17 LDS plan");
+
+// chunk loop with a register ring of R chunks: load(c, slot) issues chunk c's fragments into ring
+// slot `slot` (compile-time), comp(c, slot) consumes them
+template <int NC, int R, class L, class C>
+__device__ inline void reg_ring(L load, C comp) {
+#pragma unroll
+    for (int u = 0; u < R - 1 && u < NC; u++) load(u, u % R);
+    __builtin_amdgcn_sched_barrier(0);
+    // fully unrolled (slots are compile-time): hipcc's waitcnt insertion is exact on straight-line
+    // code, conservative across a loop back-edge; the sched_barriers keep the loads where they
+    // are (the machine scheduler otherwise sinks them next to their use: vmcnt(1) waits, no overlap)
+#pragma unroll
+    for (int c = 0; c < NC; c++) {
+        if (c + R - 1 < NC) load(c + R - 1, (c + R - 1) % R);
+        __builtin_amdgcn_sched_barrier(0);
+        comp(c, c % R);
+    }
+}
+
 __global__ __launch_bounds__(256, 1) void k_block17(B17P p) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int img = blockIdx.x;
     const char* X = (const char*)(p.x + (int64_t)img * 64 * 896);
-    char* B1 = smem + B1_OFF;
-    char* B2 = smem + B2_OFF;
-    const char* ZERO = smem + ZERO_OFF;
-    if (tid < 4) ((float*)(smem + ZERO_OFF))[tid] = 0.f;
-    // stages 2-4's weight groups (see below)
-    auto issue2 = [&](int g) {
-        const char* w;
-        int64_t pitch, kb;
-        if (g < 28) {
-            w = (const char*)(g < 14 ? p.wa : p.wb);
-            pitch = 896 * 2;
-            kb = (int64_t)(g % 14) * RB;
-        } else {
-            w = (const char*)p.wo + (int64_t)((g - 28) >> 2) * 128 * 256 * 2;
-            pitch = 256 * 2;
-            kb = (int64_t)((g - 28) & 3) * RB;
-        }
-        dma_rows<128>(w, pitch, kb, smem + R2_OFF + (g % S2_R) * S2_SLOT, wave, lane);
+    char* XL = smem + K17_X;
+    char* B1 = smem + K17_B1;
+    char* B2 = smem + K17_X;
+    const char* ZERO = smem + K17_ZERO;
+    const int r = lane & 15, kq = 8 * (lane >> 4);
+    auto stamp = [&](int k) {
+        if (p.clk && tid == 0) p.clk[img * 5 + k] = clock64();
     };
-
-    // ---------------- stage 1: X[64][896] x W_m^T -> B1 (wave: output channels 64 wave .. +64)
+    stamp(0);
+    if (tid < 4) ((float*)(smem + K17_ZERO))[tid] = 0.f;
+    // L2 warm-up: the 128 workgroups read the same weights in lockstep, so every first touch would
+    // wait on one HBM miss per XCD; one dword per 128-B line of a 1/16 slice of the block's
+    // weights (workgroups go to the 8 XCDs round-robin: the 16 of one XCD cover all of them),
+    // consumed (kept live) only after stage 1
+    uint32_t wv[3];
     {
-        constexpr int S = 14, G = 2 + 8;  // k-steps; DMA instructions per wave per group
-        auto issue = [&](int s) {
-            char* slot = smem + R_OFF + (s % S1_R) * S1_SLOT;
-            dma_rows<64>(X, 896 * 2, (int64_t)s * RB, slot, wave, lane);
-            dma_rows<256>((const char*)p.wm, 896 * 2, (int64_t)s * RB, slot + S1_X, wave, lane);
-        };
+        constexpr int LM = 256 * 896 * 2 / 128, LA = 128 * 896 * 2 / 128, LO = 896 * 256 * 2 / 128;
+        constexpr int LW = LM + 2 * LA + LO, SL = (LW + 15) / 16;
+        static_assert(SL <= 3 * 256, "warm-up loads per thread");
+        const int j = (img >> 3) & 15;
+#pragma unroll
+        for (int u = 0; u < 3; u++) {
+            const int l = min(j * SL + tid + 256 * u, LW - 1);
+            const char* a = l < LM ? (const char*)p.wm + l * 128
+                          : l < LM + LA ? (const char*)p.wa + (l - LM) * 128
+                          : l < LM + 2 * LA ? (const char*)p.wb + (l - LM - LA) * 128
+                          : (const char*)p.wo + (l - LM - 2 * LA) * 128;
+            wv[u] = *(const uint32_t*)a;
+        }
+    }
+    // ---- the input image -> LDS, one burst (7168 16-B pieces, 28 per thread)
+    {
+        constexpr int NP = 64 * 112 / 256;
+        bf16x8 v[NP];
+#pragma unroll
+        for (int u = 0; u < NP; u++) {
+            const int e = tid + 256 * u;
+            v[u] = *(const bf16x8*)(X + (e / 112) * 1792 + (e % 112) * 16);
+        }
+#pragma unroll
+        for (int u = 0; u < NP; u++) {
+            const int e = tid + 256 * u;
+            *(bf16x8*)(XL + (e / 112) * X_S + (e % 112) * 16) = v[u];
+        }
+    }
+    __syncthreads();
+
+    // ---- stage 1: X[64][896] x W_m^T -> B1 (wave: output channels 64 wave .. +64; 28 chunks of 32)
+    {
         f4 acc[4][4];
 #pragma unroll
         for (int i = 0; i < 4; i++)
 #pragma unroll
             for (int j = 0; j < 4; j++) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
-        issue(0);
-        issue(1);
-        for (int s = 0; s < S; s++) {
-            if (s + 1 < S)
-                wait_vm_barrier<G>();
-            else
-                wait_vm_barrier<0>();
-            if (s + 2 < S) issue(s + 2);
-            const char* slot = smem + R_OFF + (s % S1_R) * S1_SLOT;
-            const char* W = slot + S1_X + 64 * wave * RB;
+        const __bf16* wrow = p.wm + (int64_t)(64 * wave + r) * 896 + kq;
+        bf16x8 b[8][4];
+        reg_ring<28, 8>(
+            [&](int c, int sl) {
 #pragma unroll
-            for (int h = 0; h < 2; h++) {
-                bf16x8 b[4];
-#pragma unroll
-                for (int j = 0; j < 4; j++) b[j] = frag_sw(W, j, h, lane);
+                for (int j = 0; j < 4; j++) b[sl][j] = *(const bf16x8*)(wrow + j * 16 * 896 + 32 * c);
+            },
+            [&](int c, int sl) {
 #pragma unroll
                 for (int i = 0; i < 4; i++) {
-                    const bf16x8 a = frag_sw(slot, i, h, lane);
+                    const bf16x8 a = *(const bf16x8*)(XL + (16 * i + r) * X_S + (32 * c + kq) * 2);
 #pragma unroll
-                    for (int j = 0; j < 4; j++) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b[j], acc[i][j], 0, 0, 0);
+                    for (int j = 0; j < 4; j++) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b[sl][j], acc[i][j], 0, 0, 0);
                 }
-            }
-        }
-        // stages 2-4's first weight groups go out before the epilogue (the stage-1 ring is free once
-        // every wave is past this barrier), so the ring never restarts
-        lds_barrier();
-        issue2(0);
-        issue2(1);
-        issue2(2);
-        issue2(3);
+            });
         bn_relu_to_lds<4, 4>(acc, p.alm, p.bem, 64 * wave, B1, B1S, lane);
+        asm volatile("" ::"v"(wv[0] | wv[1] | wv[2]));
     }
+    __syncthreads();  // B1 complete; the X image is dead (B2 / E take its place)
+    stamp(1);
 
-    // ---------------- stages 2-4 on one weight ring (wave: output channels 32 wave .. +32)
-    //   groups  0..13: 1 x 7 on B1[:, 128:256] -> B2         (k = tap * 128 + channel)
-    //   groups 14..27: 7 x 1 on B2 -> B1[:, 128:256]
-    //   groups 28..55: pass (g - 28) / 4 of W_o (128 output channels), k-step (g - 28) % 4
-    {
-        constexpr int NG = 56, G = 4;
+    // ---- stages 2 and 3: 1 x 7 / 7 x 1, 128 -> 128 (wave: channels 32 wave .. +32; k = tap * 128 + c)
+    auto conv7 = [&](const __bf16* w, bool along_w, const char* in, int in_stride, int in_coff, const float* al,
+                     const float* be, char* out, int out_stride) {
         f4 acc[4][2];
-        const int r = lane & 15, kq = 8 * (lane >> 4);
-        float* E = (float*)(smem + E_OFF);
-        char* Y = (char*)(p.y + (int64_t)img * 64 * 896);
-        int issued = 4;
-        for (int g = 0; g < NG; g++) {
-            const int ahead = issued - g - 1;
-            if (ahead >= 3)
-                wait_vm_barrier<3 * G>();
-            else if (ahead == 2)
-                wait_vm_barrier<2 * G>();
-            else if (ahead == 1)
-                wait_vm_barrier<G>();
-            else
-                wait_vm_barrier<0>();
-            if (issued < NG) issue2(issued++);
-            const int st = g < 14 ? 0 : (g < 28 ? 1 : 2), ks = st < 2 ? g - 14 * st : (g - 28) & 3;
-            if (st < 2 ? ks == 0 : ks == 0) {
 #pragma unroll
-                for (int i = 0; i < 4; i++)
+        for (int i = 0; i < 4; i++)
 #pragma unroll
-                    for (int j = 0; j < 2; j++) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
-            }
-            const char* W = smem + R2_OFF + (g % S2_R) * S2_SLOT + 32 * wave * RB;
+            for (int j = 0; j < 2; j++) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
+        const __bf16* wrow = w + (int64_t)(32 * wave + r) * 896 + kq;
+        bf16x8 b[8][2];
+        reg_ring<28, 8>(
+            [&](int c, int sl) {
 #pragma unroll
-            for (int h = 0; h < 2; h++) {
-                bf16x8 b[2];
-#pragma unroll
-                for (int j = 0; j < 2; j++) b[j] = frag_sw(W, j, h, lane);
+                for (int j = 0; j < 2; j++) b[sl][j] = *(const bf16x8*)(wrow + j * 16 * 896 + 32 * c);
+            },
+            [&](int c, int sl) {
+                const int t = c >> 2, ch = in_coff + 32 * (c & 3) + kq;
 #pragma unroll
                 for (int i = 0; i < 4; i++) {
-                    const char* src;
-                    if (st < 2) {  // 1 x 7 / 7 x 1 implicit GEMM: tap ks / 2, channels 64 (ks & 1) + 32 h
-                        const int t = ks >> 1, y = 2 * i + (r >> 3), x = r & 7;
-                        const int yy = st == 0 ? y : y + t - 3, xx = st == 0 ? x + t - 3 : x;
-                        const bool ok = (unsigned)yy < 8u && (unsigned)xx < 8u;
-                        const int c = 64 * (ks & 1) + 32 * h + kq;
-                        src = !ok ? ZERO : (st == 0 ? B1 + (yy * 8 + xx) * B1S + (128 + c) * 2 : B2 + (yy * 8 + xx) * B2S + c * 2);
-                    } else {
-                        src = B1 + (16 * i + r) * B1S + (64 * ks + 32 * h + kq) * 2;
-                    }
-                    const bf16x8 a = *(const bf16x8*)src;
+                    const int y = 2 * i + (r >> 3), x = r & 7;
+                    const int yy = along_w ? y : y + t - 3, xx = along_w ? x + t - 3 : x;
+                    const bool ok = (unsigned)yy < 8u && (unsigned)xx < 8u;
+                    const bf16x8 a = *(const bf16x8*)(ok ? in + (yy * 8 + xx) * in_stride + ch * 2 : ZERO);
 #pragma unroll
-                    for (int j = 0; j < 2; j++) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b[j], acc[i][j], 0, 0, 0);
+                    for (int j = 0; j < 2; j++) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b[sl][j], acc[i][j], 0, 0, 0);
                 }
+            });
+        bn_relu_to_lds<4, 2>(acc, al, be, 32 * wave, out, out_stride, lane);
+        __syncthreads();
+    };
+    conv7(p.wa, true, B1, B1S, 128, p.ala, p.bea, B2, B2S);
+    stamp(2);
+    conv7(p.wb, false, B2, B2S, 0, p.alb, p.beb, B1 + 128 * 2, B1S);
+    stamp(3);
+
+    // ---- stage 4: B1[64][256] x W_o^T + b_o, x scale, + X, ReLU -> Y; 7 passes of 128 channels
+    //      (8 chunks each); two register sets: pass q + 1's weights load during pass q's MFMAs and
+    //      epilogue
+    {
+        float* E = (float*)(smem + K17_E);
+        char* Y = (char*)(p.y + (int64_t)img * 64 * 896);
+        bf16x8 bA[8][2], bB[8][2];
+        auto loadp = [&](int pass, bf16x8(&b)[8][2]) {
+#pragma unroll
+            for (int cc = 0; cc < 8; cc++)
+#pragma unroll
+                for (int j = 0; j < 2; j++)
+                    b[cc][j] = *(const bf16x8*)(p.wo + (int64_t)(pass * 128 + 32 * wave + 16 * j + r) * 256 + 32 * cc + kq);
+        };
+        auto runp = [&](int pass, const bf16x8(&b)[8][2]) {
+            bf16x8 rx[4];  // this pass's residual rows (used by its epilogue)
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                const int e = tid + 256 * u;
+                rx[u] = *(const bf16x8*)(X + ((int64_t)(e >> 4) * 896 + pass * 128 + 8 * (e & 15)) * 2);
             }
-            if (st < 2 && ks == 13) {
-                // BN + ReLU into the next operand (read only after the next group's barrier)
-                const float* al = st == 0 ? p.ala : p.alb;
-                const float* be = st == 0 ? p.bea : p.beb;
-                if (st == 0)
-                    bn_relu_to_lds<4, 2>(acc, al, be, 32 * wave, B2, B2S, lane);
-                else
-                    bn_relu_to_lds<4, 2>(acc, al, be, 32 * wave, B1 + 128 * 2, B1S, lane);
-            } else if (st == 2 && ks == 3) {
-                // pass epilogue through the fp32 image E (B2 is dead by now): 8 consecutive channels
-                // per thread (16-B residual loads and output stores), conv_epilogue8's arithmetic;
-                // E is rewritten four groups (four barriers) later
-                const int pass = (g - 28) >> 2;
+            f4 acc[4][2];
 #pragma unroll
-                for (int i = 0; i < 4; i++)
+            for (int i = 0; i < 4; i++)
 #pragma unroll
-                    for (int j = 0; j < 2; j++)
+                for (int j = 0; j < 2; j++) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-                        for (int q = 0; q < 4; q++)
-                            E[(16 * i + 4 * (lane >> 4) + q) * E_LD + 32 * wave + 16 * j + (lane & 15)] = acc[i][j][q];
-                lds_barrier();
+            for (int cc = 0; cc < 8; cc++)
 #pragma unroll
-                for (int u = 0; u < 4; u++) {
-                    const int e = tid + 256 * u, m = e >> 4, gg = e & 15, c0 = pass * 128 + 8 * gg;
-                    const f4 lo = *(const f4*)(E + m * E_LD + 8 * gg), hi = *(const f4*)(E + m * E_LD + 8 * gg + 4);
-                    const float v[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-                    const bf16x8 rx = *(const bf16x8*)(X + ((int64_t)m * 896 + c0) * 2);
-                    bf16x8 o;
+                for (int i = 0; i < 4; i++) {
+                    const bf16x8 a = *(const bf16x8*)(B1 + (16 * i + r) * B1S + (32 * cc + kq) * 2);
 #pragma unroll
-                    for (int k = 0; k < 8; k++) {
-                        float t = v[k] + p.bo[c0 + k];
-                        if (p.scale != 1.f) t = t * p.scale;
-                        t = t + (float)rx[k];
-                        o[k] = (__bf16)fmaxf(t, 0.f);
-                    }
-                    *(bf16x8*)(Y + ((int64_t)m * 896 + c0) * 2) = o;
+                    for (int j = 0; j < 2; j++) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b[cc][j], acc[i][j], 0, 0, 0);
                 }
+            // 8 consecutive channels per thread (16-B residual loads and output stores),
+            // conv_epilogue8's arithmetic
+#pragma unroll
+            for (int i = 0; i < 4; i++)
+#pragma unroll
+                for (int j = 0; j < 2; j++)
+#pragma unroll
+                    for (int q = 0; q < 4; q++)
+                        E[(16 * i + 4 * (lane >> 4) + q) * E_LD + 32 * wave + 16 * j + (lane & 15)] = acc[i][j][q];
+            __syncthreads();
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                const int e = tid + 256 * u, m = e >> 4, gg = e & 15, c0 = pass * 128 + 8 * gg;
+                const f4 lo = *(const f4*)(E + m * E_LD + 8 * gg), hi = *(const f4*)(E + m * E_LD + 8 * gg + 4);
+                const float v[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+                bf16x8 o;
+#pragma unroll
+                for (int k = 0; k < 8; k++) {
+                    float t = v[k] + p.bo[c0 + k];
+                    if (p.scale != 1.f) t = t * p.scale;
+                    t = t + (float)rx[u][k];
+                    o[k] = (__bf16)fmaxf(t, 0.f);
+                }
+                *(bf16x8*)(Y + ((int64_t)m * 896 + c0) * 2) = o;
+            }
+            __syncthreads();  // E is rewritten by the next pass
+        };
+        loadp(0, bA);
+        for (int q = 0; q < 7; q += 2) {
+            if (q + 1 < 7) loadp(q + 1, bB);
+            __builtin_amdgcn_sched_barrier(0);
+            runp(q, bA);
+            if (q + 1 < 7) {
+                if (q + 2 < 7) loadp(q + 2, bA);
+                __builtin_amdgcn_sched_barrier(0);
+                runp(q + 1, bB);
             }
         }
     }
+    stamp(4);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -347,15 +356,32 @@ __global__ __launch_bounds__(256, 1) void k_block35_br(B35P p) {
     const __bf16* X = p.x + (int64_t)img * B35_ROWS * 256;
     __bf16* CAT = p.cat + (int64_t)img * B35_ROWS * 96;
     const int r = lane & 15, kq = 8 * (lane >> 4);
-    // weights -> LDS (padded rows)
-    for (int e = tid; e < 96 * 32; e += 256) {
-        const int n = e >> 5, c = e & 31;
-        *(bf16x8*)(smem + B35_WM + n * WM5S + c * 16) = *(const bf16x8*)(p.wm + n * 256 + 8 * c);
-    }
-    for (int e = tid; e < 3 * 32 * 36; e += 256) {
-        const int cv = e / (32 * 36), rem = e - cv * 32 * 36, n = rem / 36, c = rem - n * 36;
-        const __bf16* w = cv == 0 ? p.w1 : (cv == 1 ? p.w2a : p.w2b);
-        *(bf16x8*)(smem + B35_W3 + (cv * 32 + n) * W35S + c * 16) = *(const bf16x8*)(w + n * 288 + 8 * c);
+    // weights -> LDS (padded rows): every load of the burst issued before the first store (a
+    // load-store loop would pay one global round trip per iteration)
+    {
+        constexpr int NWM = 96 * 32, NW3 = 3 * 32 * 36, NP = (NWM + NW3 + 255) / 256;  // 16-B pieces
+        bf16x8 v[NP];
+#pragma unroll
+        for (int u = 0; u < NP; u++) {
+            const int e = tid + 256 * u;
+            if (e < NWM) {
+                v[u] = *(const bf16x8*)(p.wm + (e >> 5) * 256 + 8 * (e & 31));
+            } else if (e < NWM + NW3) {
+                const int e3 = e - NWM, cv = e3 / (32 * 36), rem = e3 - cv * 32 * 36, n = rem / 36, c = rem - n * 36;
+                const __bf16* w = cv == 0 ? p.w1 : (cv == 1 ? p.w2a : p.w2b);
+                v[u] = *(const bf16x8*)(w + n * 288 + 8 * c);
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < NP; u++) {
+            const int e = tid + 256 * u;
+            if (e < NWM) {
+                *(bf16x8*)(smem + B35_WM + (e >> 5) * WM5S + (e & 31) * 16) = v[u];
+            } else if (e < NWM + NW3) {
+                const int e3 = e - NWM, cv = e3 / (32 * 36), rem = e3 - cv * 32 * 36, n = rem / 36, c = rem - n * 36;
+                *(bf16x8*)(smem + B35_W3 + (cv * 32 + n) * W35S + c * 16) = v[u];
+            }
+        }
     }
 
     // ---- stage 1 (K = 256: 8 chunks of 32; N = 96: 6 fragments); input rows 3 chunks ahead
@@ -592,13 +618,30 @@ void launch_block17_fused(const void* x, void* y, int N, const void* wm, const f
     p.beb = beb;
     p.bo = bo;
     p.scale = scale;
+    p.clk = nullptr;
     static bool attr = [] {
-        VTF_HIP(hipFuncSetAttribute((const void*)k_block17, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES));
+        VTF_HIP(hipFuncSetAttribute((const void*)k_block17, hipFuncAttributeMaxDynamicSharedMemorySize, K17_LDS));
         return true;
     }();
     (void)attr;
-    k_block17<<<N, 256, LDS_BYTES, st>>>(p);
+    const char* dbg = std::getenv("VTF_B17_CLK");  // debug: per-stage shader clocks, printed to stderr
+    std::vector<unsigned long long> hc;
+    if (dbg && std::atoi(dbg)) {
+        VTF_HIP(hipMallocAsync((void**)&p.clk, (size_t)N * 5 * 8, st));
+        hc.resize((size_t)N * 5);
+    }
+    k_block17<<<N, 256, K17_LDS, st>>>(p);
     VTF_HIP(hipGetLastError());
+    if (p.clk) {
+        VTF_HIP(hipMemcpyAsync(hc.data(), p.clk, hc.size() * 8, hipMemcpyDeviceToHost, st));
+        VTF_HIP(hipStreamSynchronize(st));
+        VTF_HIP(hipFreeAsync(p.clk, st));
+        double d[4] = {0, 0, 0, 0};
+        for (int i = 0; i < N; i++)
+            for (int k = 0; k < 4; k++) d[k] += (double)(hc[i * 5 + k + 1] - hc[i * 5 + k]) / N;
+        fprintf(stderr, "k_block17 cycles per stage (mean over %d workgroups): s1 %.0f s2 %.0f s3 %.0f s4 %.0f\n", N,
+                d[0], d[1], d[2], d[3]);
+    }
 }
 
 }  // namespace vtf
