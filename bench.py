@@ -614,8 +614,8 @@ def roofline_e2e(args, faces_per_step, ms_per_step, solo, solo_stats):
         enc_peak = FP32_PEAK_TFLOPS if args.enc_precision == 'fp32' else F16X_PEAK_TFLOPS
     side = 160 if args.enc_model == 'facenet' else 128
     if args.det_model != 'none' and solo is not None:
-        s_ms, s_n, s_fl, _ = solo
-        fl = s_fl / max(1, s_n)
+        s_ms, s_n, s_fl, s_frames = solo
+        fl = s_fl / max(1.0, s_frames / args.det_batch)  # per det-batch (YOLO counts a launch per conv)
         frame_bytes = args.det_batch * args.H * args.W * 3
         if args.det_model == 'yolo':
             peak = {'bf16': BF16_PEAK_TFLOPS, 'x3': X3_PEAK_TFLOPS}.get(args.det_precision, FP32_PEAK_TFLOPS)
