@@ -739,6 +739,17 @@ def run_gpu(args):
     grouping = None
     if args.grouping:
         grouping = grouping_leg(gathered, ctx, dev)[0]
+        # The random-weight encoder maps synthetic faces close together, so at ~10k faces most
+        # rows have an earlier neighbour within the 0.25 dedupe threshold.  A second leg grows
+        # a long-video set from the gathered rows (synth.video_embeddings: 40 identities + 40 %
+        # detector junk + noise, the generator of the 30k scale golden) at N = 30k, where the
+        # dedupe keeps a realistic share, and times the same sharded dedupe + k sweep on it.
+        from videotofaces import synth
+        Xg = gathered.cpu().numpy()
+        Xv = synth.video_embeddings(Xg[np.unique(Xg, axis=0, return_index=True)[1]], 30000, seed=5)
+        rec = grouping_leg(torch.from_numpy(Xv).to(dev), ctx, dev)[0]
+        rec['note'] = ('synth.video_embeddings(gathered rows, 30000, seed=5): ' + rec['note'])
+        out['grouping_video'] = rec
     if ctx.rank == 0:
         steps = args.steps
         frames_all = ctx.world * steps * (args.det_batch if det else 0)
