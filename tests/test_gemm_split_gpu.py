@@ -58,12 +58,17 @@ def test_gemm_split_refuses_out_of_range():
 def test_vit_l_sp_gemm_matches_conv_split_bitwise():
     """ViT-L split mode on pre-split operands vs k_conv's staging-split mode at batch 8 (M = 520
     token rows: 5 M-tiles, the last partial): identical bits with the same (VALU) attention; the
-    fp32-MFMA attention of the split mode stays within 1e-5 of it."""
+    split mode's attentions on the matrix cores stay close to it: the fp32-MFMA one (an exact fmaf
+    chain, measured bit-identical) within 1e-5, the split-fp16 one on split q|k|v (22-bit q, k, v
+    and P; the default) within 3e-5 -- both under the 1e-4 golden tolerance, where the fp32 path
+    itself sits at 5e-5 from the reference."""
     from videotofaces.encoders.vit import ViT
     x = (torch.rand((8, 3, 128, 128), generator=torch.Generator().manual_seed(3)) * 2 - 1).float()
     mfma = ViT('cuda:0', isL=True, precision='f16x')(x).cpu().numpy()
-    os.environ['VTF_VIT_ATTN'] = 'valu'
+    os.environ['VTF_VIT_ATTN'] = 'mfma32'
     try:
+        mfma32 = ViT('cuda:0', isL=True, precision='f16x')(x).cpu().numpy()
+        os.environ['VTF_VIT_ATTN'] = 'valu'
         new = ViT('cuda:0', isL=True, precision='f16x')(x).cpu().numpy()
         os.environ['VTF_VIT_GEMM'] = 'conv'
         old = ViT('cuda:0', isL=True, precision='f16x')(x).cpu().numpy()
@@ -71,4 +76,6 @@ def test_vit_l_sp_gemm_matches_conv_split_bitwise():
         os.environ.pop('VTF_VIT_GEMM', None)
         del os.environ['VTF_VIT_ATTN']
     np.testing.assert_array_equal(new, old)
-    np.testing.assert_allclose(mfma, new, atol=1e-5, rtol=0)
+    print('split-fp16 attention vs VALU: max abs', np.abs(mfma - new).max(), '; fp32 MFMA:', np.abs(mfma32 - new).max())
+    np.testing.assert_allclose(mfma, new, atol=3e-5, rtol=0)
+    np.testing.assert_allclose(mfma32, new, atol=1e-5, rtol=0)

@@ -305,6 +305,158 @@ __global__ __launch_bounds__(256, 2) void k_vit_attention_mfma(const float* __re
         if (__ballot(bad) && lane == 0) atomicOr(ovf, 1);
 }
 
+// The split mode's default attention: fp32-grade products on the fp16 matrix cores
+// (v_mfma_f32_16x16x32_f16, x0 y0 + 2^-11 (x0 y1 + x1 y0) as k_gemm_x3) with q|k|v read in the
+// split-pair layout the q|k|v GEMM writes.  Computed transposed, S^T = K Q^T, so that each lane
+// owns one query column: the softmax over the keys is a register reduction plus two lane
+// shuffles, and P^T goes from the accumulators straight into the B operand of O^T = V^T P^T
+// (the accumulator-as-operand map: element j of lane group g is key 32s + 4g + (j & 3) +
+// 16 (j >> 2)); V^T's fragments are transposed LDS reads (ds_read_b64_tr_b16) of V's row-major
+// planes.  One workgroup of 5 waves per (image, head), wave w = queries 16w..16w+15 (wave 4:
+// query 64 only).  Q goes global -> registers; K and V planes in LDS: 2 x 2 x 80 rows x 160 B
+// = 51 KB (row stride 160 B: conflict-free row and transposed reads), 3 workgroups per CU.
+// ds_read_b64_tr_b16: lane 4q + p of each 16-lane group addresses row q, columns 4p..4p+3 of a
+// 4 x 16 block of 16-bit elements; lane i receives column i (row q in element q).  EXEC all ones.
+__device__ inline __attribute__((ext_vector_type(4))) _Float16 lds_tr16(const _Float16* p) {
+    typedef __attribute__((__vector_size__(4 * sizeof(__fp16)))) __fp16 fp16x4;
+    const fp16x4 r = __builtin_amdgcn_ds_read_tr16_b64_v4f16((__attribute__((address_space(3))) fp16x4*)(p));
+    return __builtin_bit_cast(__attribute__((ext_vector_type(4))) _Float16, r);
+}
+constexpr int XR = 80;   // LDS rows (keys 65..79 zero)
+constexpr int XRS = 80;  // plane row stride in halves (160 B)
+__global__ __launch_bounds__(320) void k_vit_attention_x3(const void* __restrict__ qkv, int64_t N, int D, int heads,
+                                                          void* __restrict__ out, int* __restrict__ ovf) {
+    typedef __attribute__((ext_vector_type(4))) float f4;
+    typedef __attribute__((ext_vector_type(8))) _Float16 h8;
+    typedef __attribute__((ext_vector_type(4))) _Float16 h4;
+    typedef __attribute__((ext_vector_type(4))) int i4;
+    __shared__ __attribute__((aligned(16))) _Float16 sm[4 * XR * XRS];  // K0 | K1 | V0 | V1
+    const int64_t n = blockIdx.x / heads;
+    const int h = blockIdx.x % heads;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, lr = lane & 15, g = lane >> 4;
+    const int64_t rowb = (int64_t)3 * D * 4;  // SP row bytes (4 per element)
+    const char* base = (const char*)qkv + n * VT * rowb + (int64_t)h * VHD * 4;
+    // K / V pieces: 2 operands x 65 rows x 16 (8 chunks x 2 planes) x 16 B
+    constexpr int NP = 2 * VT * 16;
+    constexpr int PPT = (NP + 319) / 320;
+    i4 pc[PPT];
+#pragma unroll
+    for (int u = 0; u < PPT; u++) {
+        const int i = tid + 320 * u;
+        if (i < NP) {
+            const int op = i / (VT * 16), r = (i / 16) % VT, q = i % 16;
+            pc[u] = *(const i4*)(base + r * rowb + (int64_t)(op + 1) * D * 4 + q * 16);
+        }
+    }
+    // this wave's queries as B fragments of S^T: k-step s = dims 32s..32s+31, lane group g takes
+    // chunk 4s + g (x0 plane, x1 plane); queries past 64 read row 64 (columns never stored)
+    const int t = min(16 * wave + lr, VT - 1);
+    h8 q0[2], q1[2];
+#pragma unroll
+    for (int s = 0; s < 2; s++) {
+        const char* p = base + t * rowb + (4 * s + g) * 32;
+        q0[s] = *(const h8*)p;
+        q1[s] = *(const h8*)(p + 16);
+    }
+    // rows 65..79 of the four planes zeroed (P^T is 0 there; V must be finite)
+    for (int i = tid; i < 4 * (XR - VT) * XRS / 8; i += 320) {
+        const int pl = i / ((XR - VT) * XRS / 8), o = i % ((XR - VT) * XRS / 8);
+        *(i4*)(sm + pl * XR * XRS + VT * XRS + 8 * o) = i4{0, 0, 0, 0};
+    }
+#pragma unroll
+    for (int u = 0; u < PPT; u++) {
+        const int i = tid + 320 * u;
+        if (i < NP) {
+            const int op = i / (VT * 16), r = (i / 16) % VT, q = i % 16;
+            // chunk q >> 1 (elements 8j..8j+7), plane q & 1
+            *(i4*)(sm + (2 * op + (q & 1)) * XR * XRS + r * XRS + 8 * (q >> 1)) = pc[u];
+        }
+    }
+    __syncthreads();
+    const _Float16* K0 = sm;
+    const _Float16* K1 = sm + XR * XRS;
+    const _Float16* V0 = sm + 2 * XR * XRS;
+    const _Float16* V1 = sm + 3 * XR * XRS;
+    // S^T blocks: keys 16cb..16cb+15 x this wave's 16 queries
+    f4 sc[5];
+#pragma unroll
+    for (int cb = 0; cb < 5; cb++) {
+        f4 a = {0.f, 0.f, 0.f, 0.f}, ax = a;
+#pragma unroll
+        for (int s = 0; s < 2; s++) {
+            const int o = (16 * cb + lr) * XRS + 32 * s + 8 * g;
+            const h8 k0 = *(const h8*)(K0 + o), k1 = *(const h8*)(K1 + o);
+            a = __builtin_amdgcn_mfma_f32_16x16x32_f16(k0, q0[s], a, 0, 0, 0);
+            ax = __builtin_amdgcn_mfma_f32_16x16x32_f16(k0, q1[s], ax, 0, 0, 0);
+            ax = __builtin_amdgcn_mfma_f32_16x16x32_f16(k1, q0[s], ax, 0, 0, 0);
+        }
+        sc[cb] = (a + ax * 0.00048828125f) * 0.125f;  // / sqrt(64) (vit.py:24)
+    }
+    // column softmax over the 65 keys: lane holds keys 16cb + 4g + i of query column lr
+    float m = -INFINITY;
+#pragma unroll
+    for (int cb = 0; cb < 5; cb++)
+#pragma unroll
+        for (int i = 0; i < 4; i++)
+            if (cb < 4 || (g == 0 && i == 0)) m = fmaxf(m, sc[cb][i]);
+    m = fmaxf(m, __shfl_xor(m, 16));
+    m = fmaxf(m, __shfl_xor(m, 32));
+    float sum = 0.f;
+#pragma unroll
+    for (int cb = 0; cb < 5; cb++)
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            const float e = (cb < 4 || (g == 0 && i == 0)) ? expf(sc[cb][i] - m) : 0.f;
+            sc[cb][i] = e;
+            sum += e;
+        }
+    sum += __shfl_xor(sum, 16);
+    sum += __shfl_xor(sum, 32);
+    const float inv = 1.0f / sum;
+    // P^T split into B fragments: k-step s2 = key tiles 2 s2 (elements 0..3) and 2 s2 + 1 (4..7)
+    h8 p0[3], p1[3];
+#pragma unroll
+    for (int s2 = 0; s2 < 3; s2++)
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+            const int cb = 2 * s2 + (j >> 2);
+            const float v = cb < 5 ? sc[cb][j & 3] * inv : 0.f;
+            const _Float16 x0 = (_Float16)v;
+            p0[s2][j] = x0;
+            p1[s2][j] = (_Float16)((v - (float)x0) * 2048.f);
+        }
+    // O^T blocks: dims 16db..16db+15 x this wave's queries; A = V^T by transposed reads: lane
+    // 4q + p of group g addresses key row 32 s2 + 4g (+16) + q, dims 16db + 4p..4p+3
+    const int qq = lr >> 2, pp = lr & 3;
+    bool bad = false;
+#pragma unroll
+    for (int db = 0; db < 4; db++) {
+        f4 a = {0.f, 0.f, 0.f, 0.f}, ax = a;
+#pragma unroll
+        for (int s2 = 0; s2 < 3; s2++) {
+            const int o = (32 * s2 + 4 * g + qq) * XRS + 16 * db + 4 * pp;
+            h4 v0a = lds_tr16((V0 + o));
+            h4 v1a = lds_tr16((V1 + o));
+            h4 v0b = v0a, v1b = v1a;  // keys 80..95 (P^T = 0 there): any finite values
+            if (s2 < 2) {
+                v0b = lds_tr16((V0 + o + 16 * XRS));
+                v1b = lds_tr16((V1 + o + 16 * XRS));
+            }
+            const h8 v0 = __builtin_shufflevector(v0a, v0b, 0, 1, 2, 3, 4, 5, 6, 7);
+            const h8 v1 = __builtin_shufflevector(v1a, v1b, 0, 1, 2, 3, 4, 5, 6, 7);
+            a = __builtin_amdgcn_mfma_f32_16x16x32_f16(v0, p0[s2], a, 0, 0, 0);
+            ax = __builtin_amdgcn_mfma_f32_16x16x32_f16(v0, p1[s2], ax, 0, 0, 0);
+            ax = __builtin_amdgcn_mfma_f32_16x16x32_f16(v1, p0[s2], ax, 0, 0, 0);
+        }
+        const f4 o = a + ax * 0.00048828125f;  // O[query 16w + lr][dims 16db + 4g .. +3]
+        const int tq = 16 * wave + lr;
+        if (tq < VT)
+            sp_store4((char*)out + (n * VT + tq) * (int64_t)D * 4, h * VHD + 16 * db + 4 * g, o[0], o[1], o[2], o[3],
+                      bad);
+    }
+    if (__ballot(bad) && lane == 0) atomicOr(ovf, 1);
+}
+
 struct Lin {
     const float *w, *b;  // [out][in], [out]
     int in, out;
@@ -319,8 +471,9 @@ struct Vit {
     // split mode on pre-split operands (gemm_x3.hip) when every weight is inside the fp16 range;
     // VTF_VIT_GEMM=conv keeps k_conv's staging-split mode (A/B timing, bit-identical results)
     bool sp_ok = false;
-    // split mode: attention on the fp32 matrix cores (VTF_VIT_ATTN=valu: the VALU kernel)
-    bool attn_mfma = true;
+    // split-mode attention: 2 split-fp16 MFMA on split q|k|v (default), 1 fp32 MFMA
+    // (VTF_VIT_ATTN=mfma32), 0 the VALU kernel (VTF_VIT_ATTN=valu); 1 and 0 read fp32 q|k|v
+    int attn = 2;
     int* d_ovf = nullptr;
     hipStream_t st = 0;
     const float *cls = nullptr, *pos = nullptr, *pw = nullptr, *pb = nullptr;  // patch conv [D][16][16][8]
@@ -396,7 +549,7 @@ static void vit_build(Vit& V, const float* params, int64_t n_params) {
         V.blocks.push_back(B);
     }
     const char* ae = std::getenv("VTF_VIT_ATTN");
-    V.attn_mfma = !(ae && std::string(ae) == "valu");
+    V.attn = !ae ? 2 : std::string(ae) == "valu" ? 0 : std::string(ae) == "mfma32" ? 1 : 2;
     const char* ge = std::getenv("VTF_VIT_GEMM");
     V.sp_ok = !(ge && std::string(ge) == "conv");
     for (const auto& B : V.blocks) V.sp_ok = V.sp_ok && B.qkv.sp && B.proj.sp && B.fc1.sp && B.fc2.sp;
@@ -485,8 +638,10 @@ static void vit_forward(Vit& V, const float* x_nhwc8, int64_t N, float* emb) {
         const unsigned lg = (unsigned)cdiv(M, LN_ROWS);
         for (const auto& B : V.blocks) {
             k_layernorm<true><<<lg, 256, 0, V.st>>>(X, M, D, D, B.n1w, B.n1b, 1e-12f, Hn, D, V.d_ovf);
-            linear_sp(V, B.qkv, Hn, M, QKV, false, nullptr, false);
-            if (V.attn_mfma)
+            linear_sp(V, B.qkv, Hn, M, QKV, V.attn == 2, nullptr, false);
+            if (V.attn == 2)
+                k_vit_attention_x3<<<(unsigned)(N * V.heads), 320, 0, V.st>>>(QKV, N, D, V.heads, A, V.d_ovf);
+            else if (V.attn == 1)
                 k_vit_attention_mfma<true><<<(unsigned)(N * V.heads), 256, 0, V.st>>>(QKV, N, D, V.heads, A, V.d_ovf);
             else
                 k_vit_attention<true><<<(unsigned)(N * V.heads), 256, 0, V.st>>>(QKV, N, D, V.heads, A, V.d_ovf);
