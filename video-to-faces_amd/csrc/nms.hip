@@ -8,11 +8,14 @@
 //   * NMS: stable descending score order; areas (x2-x1)*(y2-y1) in fp32; keep i unless
 //     suppressed; suppress j if inter / ((area_i + area_j) - inter) > thr (fp32 IoU promoted
 //     to double).  Output: keep indices ordered by (score desc, index asc).
-// Design (MI355X): a radix sort gives the stable order; an IoU bitmask kernel (one wave per
-// 64-row block, 64x64 tiles, box broadcast through LDS) writes u64 suppression words; a
-// single-wave scan per segment resolves the greedy dependence 64 rows at a time in
-// registers (readlane) and ORs kept rows into an LDS "removed" bitset -- no barriers.
+// Design (MI355X): a stable merge sort gives every segment's order; an IoU bitmask kernel (one
+// wave per 64-row block x column-block chunk, boxes broadcast through LDS) writes u64
+// suppression words; one workgroup per segment resolves the greedy chain 64 rows per step
+// (fixed-point diagonal in one wave, helper waves OR the kept rows into an LDS bitset, one
+// barrier per step).
 // Build with -ffp-contract=off: every IoU op is rounded exactly like the CPU kernel.
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <rocprim/device/device_merge_sort.hpp>
 #include <rocprim/device/device_radix_sort.hpp>
@@ -265,12 +268,18 @@ __device__ inline uint64_t wave_or(uint64_t v) {
     return ((uint64_t)wave_or32((uint32_t)(v >> 32)) << 32) | wave_or32((uint32_t)v);
 }
 
-// One workgroup (8 waves) per segment: greedy resolution, 64 rows per step.  Wave 0 resolves
-// the diagonal 64x64 block in registers (readlane); then the kept rows' words of every later
-// column block are loaded coalesced (64 rows x 8 B) and OR-reduced across each wave into the LDS
-// bitset -- the 8 waves take interleaved groups of column blocks, so 8x the loads are in flight
-// (the scan is a serial chain of these steps).
-constexpr int SCAN_WAVES = 8;
+// One workgroup per segment: greedy resolution, 64 rows (one row block) per step, ONE barrier
+// per step.  Wave 0 owns the serial chain: it resolves the diagonal 64x64 block of step cb by
+// fixed-point iteration (K = alive & ~OR_{q in K} diag_q from K = alive: each round is one wave
+// OR; row r's status depends only on rows < r and the greedy keep set is the unique fixed
+// point, so the rounds stop at the chain depth -- 2-4 on MTCNN's candidates -- instead of
+// visiting every kept row in turn), then ORs its kept rows' words of column block cb + 1 itself
+// (the only word the next diagonal needs from this step).  After the barrier the helper waves
+// OR the same kept rows' words of column blocks >= cb + 2 into the LDS bitset while wave 0 is
+// already on step cb + 1: a column block w is read by wave 0 at step w, and its last helper
+// update (step w - 2) finished before the barrier of step w - 1.  Every wave keeps the mask
+// words of the next two steps in flight (coalesced 64 rows x 8 B per column block).
+constexpr int SCAN_WAVES = 16, SCAN_G = 4;  // helper waves take SCAN_G column blocks each per round
 __global__ __launch_bounds__(64 * SCAN_WAVES) void k_nms_scan(const uint64_t* __restrict__ mask,
                                                               const int64_t* __restrict__ seg_beg,
                                                               const int32_t* __restrict__ seg_n,
@@ -278,7 +287,8 @@ __global__ __launch_bounds__(64 * SCAN_WAVES) void k_nms_scan(const uint64_t* __
                                                               uint8_t* __restrict__ keep_sorted, int cap_nb,
                                                               int32_t* __restrict__ ovf_flag) {
     extern __shared__ uint64_t removed[];
-    __shared__ uint64_t s_kept;
+    __shared__ uint64_t s_kept[2];
+    constexpr int G = SCAN_G, HW = SCAN_WAVES - 1;
     const int s = blockIdx.x;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int m = seg_n[s];
@@ -291,63 +301,67 @@ __global__ __launch_bounds__(64 * SCAN_WAVES) void k_nms_scan(const uint64_t* __
     const uint64_t* msk = mask + seg_mask_off[s];
     const int64_t beg = seg_beg[s];
     for (int w = threadIdx.x; w < nb; w += 64 * SCAN_WAVES) removed[w] = 0;
-    // the words a row block needs (its diagonal word and the first round of later column
-    // words) are loaded one block ahead, unconditionally: the global-load round trip overlaps the
-    // previous block's scan instead of following it (the kept mask is applied after the load)
-    constexpr int G = 8;
-    auto load_block = [&](int cb, uint64_t& dg, uint64_t (&v)[G]) {
-        const uint64_t* blk = msk + (int64_t)cb * nb * 64 + lane;
-        dg = (wave == 0 && cb * 64 + lane < m) ? blk[(int64_t)cb * 64] : 0ull;
+    // word (row block rb, column block c, row lane); column blocks past nb - 1 read block nb - 1
+    // (never used: the loads stay unconditional and in bounds)
+    auto word = [&](int rb, int c) { return msk[((int64_t)rb * nb + min(c, nb - 1)) * 64 + lane]; };
+    // wave 0: diagonal and next-column words; helpers: their first-round column words
+    uint64_t d1 = 0, x1 = 0, d2 = 0, x2 = 0, v1[G], v2[G];
+    auto load = [&](int cb, uint64_t& d, uint64_t& x, uint64_t (&v)[G]) {
+        if (wave == 0) {
+            d = cb * 64 + lane < m ? word(cb, cb) : 0ull;
+            x = word(cb, cb + 1);
+        } else {
 #pragma unroll
-        for (int g = 0; g < G; g++) v[g] = blk[(int64_t)min(cb + 1 + wave * G + g, nb - 1) * 64];
+            for (int g = 0; g < G; g++) v[g] = word(cb, cb + 2 + (wave - 1) * G + g);
+        }
     };
-    uint64_t dg_n, v_n[G];
-    load_block(0, dg_n, v_n);
+    load(0, d1, x1, v1);
+    if (nb > 1) load(1, d2, x2, v2);
+    uint64_t own = 0;  // wave 0: OR of step cb - 1's kept rows over column block cb
     __syncthreads();
     for (int cb = 0; cb < nb; cb++) {
-        const uint64_t* blk = msk + (int64_t)cb * nb * 64 + lane;
-        const uint64_t diag = dg_n;
+        const uint64_t dg = d1, nx = x1;
         uint64_t v[G];
 #pragma unroll
-        for (int g = 0; g < G; g++) v[g] = v_n[g];
-        if (cb + 1 < nb) load_block(cb + 1, dg_n, v_n);
+        for (int g = 0; g < G; g++) v[g] = v1[g];
+        d1 = d2, x1 = x2;
+#pragma unroll
+        for (int g = 0; g < G; g++) v1[g] = v2[g];
+        if (cb + 2 < nb) load(cb + 2, d2, x2, v2);
         if (wave == 0) {
-            const int row = cb * 64 + lane;
             const int nrow = min(64, m - cb * 64);
             const uint64_t valid = nrow == 64 ? ~0ull : ((1ull << nrow) - 1ull);
-            uint64_t rem = removed[cb];
-            uint64_t kept = 0;
-            // visit only the rows still alive, in order: each kept row t ORs its diagonal word
-            // (lane t, read with a uniform lane index) into the removed set
-            uint64_t alive = valid & ~rem;
-            while (alive) {
-                const int t = __builtin_ctzll(alive);
-                const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)diag, t);
-                const uint32_t hi = __builtin_amdgcn_readlane((uint32_t)(diag >> 32), t);
-                kept |= 1ull << t;
-                rem |= ((uint64_t)hi << 32) | lo;
-                alive = valid & ~rem & (t == 63 ? 0ull : (~0ull << (t + 1)));
+            const uint64_t alive = valid & ~(removed[cb] | own);
+            uint64_t kept = alive;
+            for (;;) {
+                const uint64_t sup = wave_or(((kept >> lane) & 1ull) ? dg : 0ull);
+                const uint64_t k2 = alive & ~sup;
+                if (k2 == kept) break;
+                kept = k2;
             }
+            const int row = cb * 64 + lane;
             if (row < m) keep_sorted[beg + row] = (uint8_t)((kept >> lane) & 1ull);
-            if (lane == 0) s_kept = kept;
+            if (lane == 0) s_kept[cb & 1] = kept;
+            own = wave_or(((kept >> lane) & 1ull) ? nx : 0ull);
         }
         __syncthreads();
-        const uint64_t kept = s_kept;
-        if (kept != 0) {
-            const uint64_t mine = ((kept >> lane) & 1ull) ? ~0ull : 0ull;
-            for (int w0 = cb + 1 + wave * G; w0 < nb; w0 += SCAN_WAVES * G) {
-                if (w0 != cb + 1 + wave * G) {  // rounds past the first: loaded here
+        if (wave > 0) {
+            const uint64_t kept = s_kept[cb & 1];
+            if (kept != 0) {
+                const uint64_t mine = ((kept >> lane) & 1ull) ? ~0ull : 0ull;
+                for (int w0 = cb + 2 + (wave - 1) * G; w0 < nb; w0 += HW * G) {
+                    if (w0 != cb + 2 + (wave - 1) * G) {  // rounds past the first: loaded here
 #pragma unroll
-                    for (int g = 0; g < G; g++) v[g] = blk[(int64_t)min(w0 + g, nb - 1) * 64];
-                }
+                        for (int g = 0; g < G; g++) v[g] = word(cb, w0 + g);
+                    }
 #pragma unroll
-                for (int g = 0; g < G; g++) {
-                    const uint64_t r = wave_or(v[g] & mine);
-                    if (lane == 0 && w0 + g < nb) removed[w0 + g] |= r;
+                    for (int g = 0; g < G; g++) {
+                        const uint64_t r = wave_or(v[g] & mine);
+                        if (lane == 0 && w0 + g < nb) removed[w0 + g] |= r;
+                    }
                 }
             }
         }
-        __syncthreads();
     }
 }
 
@@ -435,6 +449,14 @@ void inclusive_scan_i32(Arena& ar, int slot, const int32_t* in, int32_t* out, in
     VTF_HIP(rocprim::inclusive_scan(nullptr, tmp, in, out, (size_t)n, rocprim::plus<int32_t>(), st));
     void* t = ar.get(slot, tmp);
     VTF_HIP(rocprim::inclusive_scan(t, tmp, in, out, (size_t)n, rocprim::plus<int32_t>(), st));
+}
+
+static bool nms_debug() {
+    static const bool on = [] {
+        const char* e = std::getenv("VTF_NMS_DEBUG");
+        return e && std::atoi(e) != 0;
+    }();
+    return on;
 }
 
 // Arena slots used here: 40..63 (device), mailboxes 40, 41
@@ -540,6 +562,20 @@ void nms_multi(Arena& ar, const float* d_boxes, const float* d_scores, const int
     const int cap_nb = (int)std::min<int64_t>(nbmax, 160 * 1024 / 8);
     k_nms_scan<<<S, 64 * SCAN_WAVES, (size_t)cap_nb * 8, st>>>(d_mask, d_sstart, d_scnt, d_moff, keep_sorted, cap_nb,
                                                                d_res + C);
+    if (nms_debug()) {  // VTF_NMS_DEBUG=1: per-call segment sizes on stderr (synchronises)
+        std::vector<int64_t> ss(S + 1);
+        VTF_HIP(hipMemcpyAsync(ss.data(), d_sstart, (S + 1) * 8, hipMemcpyDeviceToHost, st));
+        VTF_HIP(hipStreamSynchronize(st));
+        int64_t mx = 0, pairs = 0, nbs = 0;
+        for (int i = 0; i < S; i++) {
+            const int64_t m = ss[i + 1] - ss[i], nb = (m + 63) / 64;
+            mx = std::max(mx, m);
+            pairs += m * (m - 1) / 2;
+            nbs += nb;
+        }
+        fprintf(stderr, "nms_multi: C %d N %lld S %d max seg %lld sum nb %lld pairs %lld\n", C, (long long)N, S,
+                (long long)mx, (long long)nbs, (long long)pairs);
+    }
     uint8_t* keep_elem = ar.get<uint8_t>(58, N);
     k_scatter_flags<<<cdiv(N, 256), 256, 0, st>>>(ord, keep_sorted, N, keep_elem);
 
