@@ -24,6 +24,9 @@ typedef struct { float s; int64_t i; } si_t;
 static int cmp_desc_stable(const void* a, const void* b) {
     const si_t* x = (const si_t*)a;
     const si_t* y = (const si_t*)b;
+    /* torch's sort: NaN above every number, NaNs equal among themselves */
+    const int xn = x->s != x->s, yn = y->s != y->s;
+    if (xn != yn) return xn ? -1 : 1;
     if (x->s > y->s) return -1;
     if (x->s < y->s) return 1;
     return (x->i < y->i) ? -1 : (x->i > y->i);

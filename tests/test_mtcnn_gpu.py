@@ -104,8 +104,12 @@ def _random_boxes(n, n_img, seed, grid=False):
 
 @pytest.mark.parametrize('n,n_img,thr,grid', [(0, 1, 0.5, False), (1, 1, 0.5, False), (300, 4, 0.5, True),
                                               (1000, 3, 0.7, False), (1001, 3, 0.7, False), (5000, 16, 0.5, True),
-                                              (3000, 1, 0.45, False), (20000, 7, 0.3, True)])
+                                              (3000, 1, 0.45, False), (20000, 7, 0.3, True), (16384, 1, 0.7, False),
+                                              (9000, 2, 0.6, True), (66000, 8, 0.5, False)])
 def test_batched_nms_exact(n, n_img, thr, grid):
+    """Calls of up to 65536 boxes take the per-segment sort (segments of up to 4096 boxes in LDS,
+    longer ones -- 16384 in one image -- in global memory); larger calls (66000) the device-wide
+    merge sort; all give the same order."""
     from videotofaces.detectors.mtcnn import batched_nms
     from oracle import nms as onms
     b, s, i = _random_boxes(n, n_img, seed=n + n_img, grid=grid)
@@ -118,6 +122,38 @@ def test_batched_nms_exact(n, n_img, thr, grid):
     if n > 1000:
         ks = s[ref]
         print('vanilla path: %d kept, %d equal-score neighbours' % (len(ref), int((ks[1:] == ks[:-1]).sum())))
+
+
+def test_batched_nms_degenerate_boxes_exact():
+    """Zero-area, inverted (x2 < x1) and NaN boxes: their unions are <= 0 or NaN, so k_iou_mask
+    decides those pairs by the reference's IEEE division instead of the division-free test."""
+    from videotofaces.detectors.mtcnn import batched_nms
+    from oracle import nms as onms
+    b, s, i = _random_boxes(3000, 3, seed=5, grid=True)
+    b = b.clone()
+    b[::7, 2] = b[::7, 0]                    # zero width
+    b[1::11, 2] = b[1::11, 0] - 3.0          # inverted
+    b[2::13, 3] = b[2::13, 1] - 1.0
+    b[3::97, 0] = float('nan')               # NaN coordinate
+    for n in (3000, 900):                    # vanilla and coordinate-trick paths
+        ref = onms.batched_nms(b[:n], s[:n], i[:n], 0.5)
+        got = batched_nms(b[:n].cuda(), s[:n].cuda(), i[:n].cuda(), 0.5).cpu()
+        assert got.tolist() == ref.tolist()
+
+
+@pytest.mark.parametrize('n', [3000, 900])
+def test_batched_nms_nan_scores_exact(n):
+    """NaN scores sort above every number and tie among themselves (torch's sort); on the vanilla
+    path the kept NaNs are ties the host reorders like torch's unstable final sort."""
+    from videotofaces.detectors.mtcnn import batched_nms
+    from oracle import nms as onms
+    b, s, i = _random_boxes(n, 3, seed=11, grid=False)
+    s = s.clone()
+    s[::37] = float('nan')
+    s[5::41] = -float('nan')
+    ref = onms.batched_nms(b, s, i, 0.5)
+    got = batched_nms(b.cuda(), s.cuda(), i.cuda(), 0.5).cpu()
+    assert got.tolist() == ref.tolist()
 
 
 def _match(res, counts, boxes, atol):

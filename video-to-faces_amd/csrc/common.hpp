@@ -177,9 +177,10 @@ inline uint16_t f2bf(float f) {
     return (uint16_t)(u >> 16);
 }
 
-// Sortable descending key of a float: larger float -> smaller key (NaN-free inputs).
+// descending-order sort key of a float; every NaN maps to one key above +inf, as torch's sort
+// treats NaNs as equal and greater than every number
 __host__ __device__ inline uint32_t desc_key(float f) {
-    uint32_t u = f2u(f);
+    uint32_t u = f != f ? 0x7fc00000u : f2u(f);
     uint32_t asc = (u & 0x80000000u) ? ~u : (u | 0x80000000u);
     return ~asc;
 }

@@ -8,12 +8,13 @@
 //   * NMS: stable descending score order; areas (x2-x1)*(y2-y1) in fp32; keep i unless
 //     suppressed; suppress j if inter / ((area_i + area_j) - inter) > thr (fp32 IoU promoted
 //     to double).  Output: keep indices ordered by (score desc, index asc).
-// Design (MI355X): a stable merge sort gives every segment's order; an IoU bitmask kernel (one
-// wave per 64-row block x column-block chunk, boxes broadcast through LDS) writes u64
-// suppression words; one workgroup per segment resolves the greedy chain 64 rows per step
-// (fixed-point diagonal in one wave, helper waves OR the kept rows into an LDS bitset, one
-// barrier per step).
+// Design (MI355X): a stable merge sort by (call, image, score desc) gives every segment's order;
+// an IoU bitmask kernel (one wave per 64-row block x column-block chunk, boxes broadcast through
+// LDS) writes u64 suppression words; one workgroup per segment resolves the greedy chain 64 rows
+// per step (fixed-point diagonal, one barrier per step) and writes the segment's kept list; one
+// last launch merges a vanilla call's image lists into torchvision's output order.
 // Build with -ffp-contract=off: every IoU op is rounded exactly like the CPU kernel.
+#include <cmath>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -34,9 +35,11 @@ namespace vtf {
 // coordinate-trick offset base, torchvision batched_nms), reading its bounds from the mailbox.
 __global__ void k_nms_prep(const uint8_t* __restrict__ mail, uint8_t* __restrict__ tables, int bytes,
                            const float4* __restrict__ boxes, size_t o_cbeg, size_t o_cn, size_t o_van, size_t o_trick,
-                           int C, float* __restrict__ call_max, int32_t* __restrict__ ovf_flag) {
+                           int C, float* __restrict__ call_max, int32_t* __restrict__ ovf_flag,
+                           int32_t* __restrict__ seg_ctr, int n_ctr) {
     if (blockIdx.x == 0) {
         if (threadIdx.x == 0) *ovf_flag = 0;
+        for (int i = threadIdx.x; i < n_ctr; i += blockDim.x) seg_ctr[i] = 0;  // segment counters
         const uint32_t* src = (const uint32_t*)mail;
         uint32_t* dst = (uint32_t*)tables;
         for (int i = threadIdx.x; i < bytes / 4; i += blockDim.x) dst[i] = src[i];
@@ -50,16 +53,18 @@ __global__ void k_nms_prep(const uint8_t* __restrict__ mail, uint8_t* __restrict
     }
     const int c = ((const int32_t*)(mail + o_trick))[blockIdx.x - 1];
     const int64_t beg = ((const int64_t*)(mail + o_cbeg))[c], n = ((const int64_t*)(mail + o_cn))[c];
+    // torch's max propagates NaN (boxes.max() in batched_nms): so does this one
+    auto nmax = [](float a, float b) { return (a != a || b != b) ? NAN : fmaxf(a, b); };
     float m = -INFINITY;
     for (int64_t i = threadIdx.x; i < n; i += blockDim.x) {
         float4 b = boxes[beg + i];
-        m = fmaxf(m, fmaxf(fmaxf(b.x, b.y), fmaxf(b.z, b.w)));
+        m = nmax(m, nmax(nmax(b.x, b.y), nmax(b.z, b.w)));
     }
     __shared__ float red[256];
     red[threadIdx.x] = m;
     __syncthreads();
     for (int s = blockDim.x / 2; s > 0; s >>= 1) {
-        if ((int)threadIdx.x < s) red[threadIdx.x] = fmaxf(red[threadIdx.x], red[threadIdx.x + s]);
+        if ((int)threadIdx.x < s) red[threadIdx.x] = nmax(red[threadIdx.x], red[threadIdx.x + s]);
         __syncthreads();
     }
     if (threadIdx.x == 0) call_max[c] = red[0];
@@ -95,6 +100,189 @@ __global__ void k_seg_bounds(const uint64_t* __restrict__ keys, int64_t N, const
         if (keys[mid] < target) lo = mid + 1; else hi = mid;
     }
     seg_start[s] = lo;
+}
+
+// exclusive prefix of cnt[0, S) into koff[0, S] (LDS) by one block of NT threads (part: NT ints)
+template <int NT>
+__device__ inline void block_prefix(const int32_t* __restrict__ cnt, int S, int32_t* koff, int32_t* part) {
+    const int tid = threadIdx.x;
+    const int q = (S + NT - 1) / NT, a0 = min(S, tid * q), a1 = min(S, a0 + q);
+    int sum = 0;
+    for (int i = a0; i < a1; i++) sum += cnt[i];
+    part[tid] = sum;
+    __syncthreads();
+    if (tid < 64) {  // one wave scans the NT partial sums
+        int carry = 0;
+        for (int b = 0; b < NT; b += 64) {
+            const int v = part[b + tid];
+            int x = v;
+            for (int o = 1; o < 64; o <<= 1) {
+                const int y = __shfl_up(x, o);
+                if (tid >= o) x += y;
+            }
+            part[b + tid] = carry + x - v;
+            carry += __shfl(x, 63);
+        }
+        if (tid == 0) koff[S] = carry;
+    }
+    __syncthreads();
+    sum = part[tid];
+    for (int i = a0; i < a1; i++) {
+        koff[i] = sum;
+        sum += cnt[i];
+    }
+    __syncthreads();
+}
+
+// Segmented sort without a device-wide sort (segments of calls bounded by NMS_SORT_BOUND boxes): count
+// per segment, scatter (slot order within a segment is arbitrary: the key carries the element index),
+// then one workgroup per segment sorts its (descending-score key, element index) keys -- unique keys,
+// so the order equals the stable sort by (segment, score desc) over position order.  The network is
+// the ascending-only bitonic form (the first step of each merge compares mirrored pairs), so a
+// segment needs no padding: positions >= m act as +inf and are never read or written.  Segments of
+// up to NMS_SORT_LDS keys sort in LDS, longer ones in place in global memory (one workgroup, the
+// same network; the workgroup's waves share the CU's L1, so a barrier orders their accesses).
+constexpr int NMS_SORT_LDS = 4096;      // 32 KB of LDS per workgroup
+constexpr int64_t NMS_SORT_BOUND = 65536;  // larger calls take the device-wide merge sort
+__device__ inline int seg_of(const int32_t* __restrict__ img, const int32_t* __restrict__ elem_call,
+                             const uint8_t* __restrict__ van, const int32_t* __restrict__ sbase, int64_t e) {
+    const int c = elem_call[e];
+    return sbase[c] + (van[c] ? img[e] : 0);
+}
+// Per-block LDS histograms keep the global atomics to one per (block, segment): a call's boxes
+// mostly share few segments, and per-element atomics on those few addresses serialised (~90 us
+// per call).  A wave whose elements all fall in one segment adds them with one LDS atomic.
+constexpr int SEG_T = 1024, SEG_HIST = 4096;
+__global__ __launch_bounds__(SEG_T) void k_seg_count(const int32_t* __restrict__ img, const int32_t* __restrict__ elem_call,
+                                                     const uint8_t* __restrict__ van, const int32_t* __restrict__ sbase,
+                                                     int64_t N, int S, int32_t* __restrict__ cnt) {
+    __shared__ int32_t h[SEG_HIST];
+    const int tid = threadIdx.x, lane = tid & 63;
+    const bool lds = S <= SEG_HIST;
+    if (lds) {
+        for (int i = tid; i < S; i += SEG_T) h[i] = 0;
+        __syncthreads();
+    }
+    const int64_t e = (int64_t)blockIdx.x * SEG_T + tid;
+    const bool valid = e < N;
+    const int sg = valid ? seg_of(img, elem_call, van, sbase, e) : -1;
+    if (!lds) {
+        if (valid) atomicAdd(&cnt[sg], 1);
+        return;
+    }
+    const int s0 = __builtin_amdgcn_readfirstlane(sg);
+    const uint64_t all = __ballot(valid), same = __ballot(valid && sg == s0);
+    if (same == all) {
+        if (lane == 0 && all) atomicAdd(&h[s0], (int)__popcll(all));
+    } else if (valid) {
+        atomicAdd(&h[sg], 1);
+    }
+    __syncthreads();
+    for (int i = tid; i < S; i += SEG_T)
+        if (h[i]) atomicAdd(&cnt[i], h[i]);
+}
+// keys of segment s at [sstart[s], sstart[s + 1]) in any slot order: (desc score key | element)
+__global__ __launch_bounds__(SEG_T) void k_seg_scatter(const float* __restrict__ scores, const int32_t* __restrict__ img,
+                                                       const int32_t* __restrict__ elem_call,
+                                                       const uint8_t* __restrict__ van, const int32_t* __restrict__ sbase,
+                                                       int64_t N, int S, const int32_t* __restrict__ cnt,
+                                                       int32_t* __restrict__ fill, int64_t* __restrict__ sstart,
+                                                       uint64_t* __restrict__ tmp) {
+    extern __shared__ int32_t soff[];  // [S + 1], then (S <= SEG_HIST) block counts h[S] and bases hb[S]
+    __shared__ int32_t part[SEG_T];
+    const int tid = threadIdx.x, lane = tid & 63;
+    const bool lds = S <= SEG_HIST;
+    int32_t* h = soff + S + 1;
+    int32_t* hb = h + S;
+    if (lds)
+        for (int i = tid; i < S; i += SEG_T) h[i] = 0;
+    block_prefix<SEG_T>(cnt, S, soff, part);  // (ends with a barrier)
+    if (blockIdx.x == 0)
+        for (int i = tid; i <= S; i += SEG_T) sstart[i] = soff[i];
+    const int64_t e = (int64_t)blockIdx.x * SEG_T + tid;
+    const bool valid = e < N;
+    const int sg = valid ? seg_of(img, elem_call, van, sbase, e) : 0;
+    const uint64_t key = valid ? ((uint64_t)desc_key(scores[e]) << 32) | (uint32_t)e : 0;
+    if (!lds) {
+        if (valid) tmp[soff[sg] + atomicAdd(&fill[sg], 1)] = key;
+        return;
+    }
+    // local rank: one LDS atomic per wave when the wave's elements share a segment
+    const int s0 = __builtin_amdgcn_readfirstlane(sg);
+    const uint64_t all = __ballot(valid), same = __ballot(valid && sg == s0);
+    int r;
+    if (same == all) {
+        int b = 0;
+        if (lane == 0 && all) b = atomicAdd(&h[s0], (int)__popcll(all));
+        b = __shfl(b, 0);
+        r = b + (int)__popcll(all & ((1ull << lane) - 1ull));
+    } else {
+        r = valid ? atomicAdd(&h[sg], 1) : 0;
+    }
+    __syncthreads();
+    for (int i = tid; i < S; i += SEG_T)
+        if (h[i]) hb[i] = atomicAdd(&fill[i], h[i]);
+    __syncthreads();
+    if (valid) tmp[soff[sg] + hb[sg] + r] = key;
+}
+// ascending bitonic network over a[0, m) (1024 threads, one workgroup)
+template <class P>
+__device__ inline void bitonic_asc(P a, int m) {
+    const int tid = threadIdx.x;
+    int n2 = 1;
+    while (n2 < m) n2 <<= 1;
+    for (int k = 2; k <= n2; k <<= 1) {
+        const int h = k >> 1;
+        for (int t = tid; t < n2 / 2; t += 1024) {  // merge step 1: mirrored pairs of each k block
+            const int b = t / h, o = t - b * h;
+            const int i = b * k + o, l = b * k + k - 1 - o;
+            if (l < m) {
+                const uint64_t x = a[i], y = a[l];
+                if (x > y) a[i] = y, a[l] = x;
+            }
+        }
+        __syncthreads();
+        for (int j = h >> 1; j > 0; j >>= 1) {  // half-cleaners
+            for (int t = tid; t < n2 / 2; t += 1024) {
+                const int i = 2 * t - (t & (j - 1)), l = i + j;
+                if (l < m) {
+                    const uint64_t x = a[i], y = a[l];
+                    if (x > y) a[i] = y, a[l] = x;
+                }
+            }
+            __syncthreads();
+        }
+    }
+}
+__global__ __launch_bounds__(1024) void k_seg_sort(const int64_t* __restrict__ sstart, const uint64_t* __restrict__ tmp,
+                                                   uint64_t* __restrict__ ck, int32_t* __restrict__ ord) {
+    __shared__ uint64_t a[NMS_SORT_LDS];
+    const int tid = threadIdx.x;
+    const int64_t beg = sstart[blockIdx.x];
+    const int m = (int)(sstart[blockIdx.x + 1] - beg);
+    if (m == 0) return;
+    if (m <= NMS_SORT_LDS) {
+        for (int i = tid; i < m; i += 1024) a[i] = tmp[beg + i];
+        __syncthreads();
+        bitonic_asc(a, m);
+        for (int i = tid; i < m; i += 1024) {
+            const uint64_t v = a[i];
+            ck[beg + i] = v;
+            ord[beg + i] = (int32_t)(uint32_t)v;
+        }
+    } else {
+        uint64_t* g = ck + beg;
+        for (int i = tid; i < m; i += 1024) g[i] = tmp[beg + i];
+        __syncthreads();
+        bitonic_asc(g, m);
+        for (int i = tid; i < m; i += 1024) ord[beg + i] = (int32_t)(uint32_t)g[i];
+    }
+}
+// the merge-sort path's keys ((call, image) | desc score) -> (desc score, element index)
+__global__ void k_composite(const uint64_t* __restrict__ k1, const int32_t* __restrict__ ord, int64_t N,
+                            uint64_t* __restrict__ ck) {
+    const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (p < N) ck[p] = ((uint64_t)(uint32_t)k1[p] << 32) | (uint32_t)ord[p];
 }
 
 struct MaskTask {
@@ -197,14 +385,42 @@ __device__ inline float4 load_box(const float4* __restrict__ boxes, const int32_
     return b;
 }
 
-// One wave per (segment, 64-row block, chunk of column blocks >= rb).
+// IoU test without the division.  The reference suppresses j when (double)fl(inter / uni) > thr
+// (torchvision nms_kernel.cpp: float IoU, double threshold).  fl(q) is a float, so that is
+// fl(q) >= F, F the smallest float above thr; under round-to-nearest-even fl(q) >= F iff
+// q > mid, or q == mid with F's significand even, mid = (F- + F) / 2 the midpoint below F.  For
+// uni > 0 that is inter > mid * uni (or >=) in double, where mid (25 bits) times uni (24 bits)
+// and inter are exact: the same decision bit for bit.  uni <= 0 or NaN (degenerate boxes) take
+// the IEEE division, as the reference does.
+struct IouThr {
+    double thr, mid;
+    int ge;  // F's significand is even: q == mid suppresses
+};
+
+// One wave per (segment, 64-row block, chunk of column blocks >= rb): lane = row, the 64 column
+// boxes of a block are broadcast from LDS and all 64 tested unrolled (branch-free; the diagonal
+// block's lower triangle and columns past the segment are masked afterwards).
+__device__ inline float vmax(float a, float b) {
+    float r;
+    asm("v_max_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+__device__ inline float vmin(float a, float b) {
+    float r;
+    asm("v_min_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+
+template <bool GE>
 __global__ __launch_bounds__(64) void k_iou_mask(const float4* __restrict__ boxes, const int32_t* __restrict__ img,
                                                  const int32_t* __restrict__ order, const MaskTask* __restrict__ tasks,
                                                  const int64_t* __restrict__ seg_beg, const int32_t* __restrict__ seg_n,
                                                  const int64_t* __restrict__ seg_mask_off,
-                                                 const float* __restrict__ seg_offbase, double thr,
+                                                 const float* __restrict__ seg_offbase, IouThr th,
                                                  uint64_t* __restrict__ mask, const int32_t* __restrict__ n_tasks) {
   const int T = *n_tasks;  // written by k_nms_plan; the grid is a bound, waves stride over the tasks
+  __shared__ float4 cb_box[64];
+  __shared__ float cb_area[64];
   for (int ti = blockIdx.x; ti < T; ti += gridDim.x) {
     MaskTask t = tasks[ti];
     const int lane = threadIdx.x;
@@ -213,8 +429,6 @@ __global__ __launch_bounds__(64) void k_iou_mask(const float4* __restrict__ boxe
     const int nb = (m + 63) >> 6;
     const float ob = seg_offbase[t.seg];
     const int row = t.rb * 64 + lane;
-    __shared__ float4 cb_box[64];
-    __shared__ float cb_area[64];
     float4 bi = make_float4(0.f, 0.f, 0.f, 0.f);
     float ai = 0.f;
     if (row < m) {
@@ -233,19 +447,42 @@ __global__ __launch_bounds__(64) void k_iou_mask(const float4* __restrict__ boxe
         cb_box[lane] = bj;
         cb_area[lane] = (bj.z - bj.x) * (bj.w - bj.y);
         __syncthreads();
-        int ncol = min(64, m - cb * 64);
-        uint64_t bits = 0;
-        if (row < m) {
-            int j0 = (cb == t.rb) ? lane + 1 : 0;
-            for (int j = j0; j < ncol; j++) {
-                float4 b = cb_box[j];
-                float xx1 = fmaxf(bi.x, b.x), yy1 = fmaxf(bi.y, b.y);
-                float xx2 = fminf(bi.z, b.z), yy2 = fminf(bi.w, b.w);
-                float w = fmaxf(0.f, xx2 - xx1), h = fmaxf(0.f, yy2 - yy1);
-                float inter = w * h;
-                float ovr = __fdiv_rn(inter, (ai + cb_area[j]) - inter);
-                if ((double)ovr > thr) bits |= (1ull << j);
-            }
+        const int ncol = min(64, m - cb * 64);
+        uint32_t bl = 0, bh = 0, sl = 0, sh = 0;
+#pragma unroll
+        for (int j = 0; j < 64; j++) {
+            const float4 b = cb_box[j];
+            // fast path: max / min as v_max / v_min (a NaN coordinate makes uni NaN, and that pair
+            // goes to the exact path, which follows the reference's std::max / std::min selects)
+            const float xx1 = vmax(bi.x, b.x), yy1 = vmax(bi.y, b.y);
+            const float xx2 = vmin(bi.z, b.z), yy2 = vmin(bi.w, b.w);
+            const float w = vmax(0.f, xx2 - xx1), h = vmax(0.f, yy2 - yy1);
+            const float inter = w * h;
+            const float uni = (ai + cb_area[j]) - inter;
+            const double l = (double)inter, r = th.mid * (double)uni;
+            const uint32_t sup = (GE ? l >= r : l > r) ? 1u : 0u;
+            const uint32_t slw = uni > 0.f && uni < INFINITY ? 0u : 1u;
+            if (j < 32) bl |= sup << j, sl |= slw << j;
+            else bh |= sup << (j - 32), sh |= slw << (j - 32);
+        }
+        uint64_t bits = ((uint64_t)bh << 32) | bl, slow = ((uint64_t)sh << 32) | sl;
+        uint64_t valid = ncol == 64 ? ~0ull : ((1ull << ncol) - 1ull);
+        if (cb == t.rb) valid &= lane == 63 ? 0ull : (~0ull << (lane + 1));
+        if (row >= m) valid = 0;
+        bits &= valid & ~slow;
+        slow &= valid;
+        while (slow) {  // degenerate unions (rare): the reference's IEEE division
+            const int j = __builtin_ctzll(slow);
+            slow &= slow - 1;
+            const float4 b = cb_box[j];
+            // std::max / std::min as the reference writes them ((a < b) ? b : a)
+            const float xx1 = bi.x < b.x ? b.x : bi.x, yy1 = bi.y < b.y ? b.y : bi.y;
+            const float xx2 = b.z < bi.z ? b.z : bi.z, yy2 = b.w < bi.w ? b.w : bi.w;
+            const float dw = xx2 - xx1, dh = yy2 - yy1;
+            const float w = 0.f < dw ? dw : 0.f, h = 0.f < dh ? dh : 0.f;
+            const float inter = w * h;
+            const float ovr = __fdiv_rn(inter, (ai + cb_area[j]) - inter);
+            if ((double)ovr > th.thr) bits |= 1ull << j;
         }
         out[(int64_t)cb * 64] = bits;
     }
@@ -284,18 +521,22 @@ __global__ __launch_bounds__(64 * SCAN_WAVES) void k_nms_scan(const uint64_t* __
                                                               const int64_t* __restrict__ seg_beg,
                                                               const int32_t* __restrict__ seg_n,
                                                               const int64_t* __restrict__ seg_mask_off,
-                                                              uint8_t* __restrict__ keep_sorted, int cap_nb,
-                                                              int32_t* __restrict__ ovf_flag) {
+                                                              const uint64_t* __restrict__ ck,
+                                                              uint64_t* __restrict__ klist, int32_t* __restrict__ kcnt,
+                                                              int cap_nb, int32_t* __restrict__ ovf_flag) {
     extern __shared__ uint64_t removed[];
     __shared__ uint64_t s_kept[2];
     constexpr int G = SCAN_G, HW = SCAN_WAVES - 1;
     const int s = blockIdx.x;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int m = seg_n[s];
-    if (m == 0) return;
+    if (m == 0) {
+        if (threadIdx.x == 0) kcnt[s] = 0;
+        return;
+    }
     const int nb = (m + 63) >> 6;
     if (nb > cap_nb) {  // the LDS bitset holds cap_nb words (uniform exit, flag for the host)
-        if (threadIdx.x == 0) *ovf_flag = 1;
+        if (threadIdx.x == 0) *ovf_flag = 1, kcnt[s] = 0;
         return;
     }
     const uint64_t* msk = mask + seg_mask_off[s];
@@ -318,6 +559,7 @@ __global__ __launch_bounds__(64 * SCAN_WAVES) void k_nms_scan(const uint64_t* __
     load(0, d1, x1, v1);
     if (nb > 1) load(1, d2, x2, v2);
     uint64_t own = 0;  // wave 0: OR of step cb - 1's kept rows over column block cb
+    int kpos = 0;      // wave 0: kept rows so far (the segment's kept list is written in order)
     __syncthreads();
     for (int cb = 0; cb < nb; cb++) {
         const uint64_t dg = d1, nx = x1;
@@ -339,8 +581,13 @@ __global__ __launch_bounds__(64 * SCAN_WAVES) void k_nms_scan(const uint64_t* __
                 if (k2 == kept) break;
                 kept = k2;
             }
-            const int row = cb * 64 + lane;
-            if (row < m) keep_sorted[beg + row] = (uint8_t)((kept >> lane) & 1ull);
+            // kept list entry: (descending-score key, element index) -- the order key of the
+            // call's output, so k_nms_out can merge a vanilla call's image lists by binary search
+            if ((kept >> lane) & 1ull) {
+                const int64_t p = beg + cb * 64 + lane;
+                klist[beg + kpos + __builtin_popcountll(kept & ((1ull << lane) - 1ull))] = ck[p];
+            }
+            kpos += __builtin_popcountll(kept);
             if (lane == 0) s_kept[cb & 1] = kept;
             own = wave_or(((kept >> lane) & 1ull) ? nx : 0ull);
         }
@@ -363,48 +610,82 @@ __global__ __launch_bounds__(64 * SCAN_WAVES) void k_nms_scan(const uint64_t* __
             }
         }
     }
+    if (threadIdx.x == 0) kcnt[s] = kpos;
 }
 
-__global__ void k_scatter_flags(const int32_t* __restrict__ order, const uint8_t* __restrict__ keep_sorted,
-                                int64_t N, uint8_t* __restrict__ keep_elem) {
-    int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (k < N) keep_elem[order[k]] = keep_sorted[k];
+// lower bound of key in the sorted list l[0, n)
+__device__ inline int lower_bound_u64(const uint64_t* __restrict__ l, int n, uint64_t key) {
+    int lo = 0, hi = n;
+    while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (l[mid] < key) lo = mid + 1; else hi = mid;
+    }
+    return lo;
 }
 
-__global__ void k_flag_in_order(const int32_t* __restrict__ order, const uint8_t* __restrict__ keep_elem,
-                                int64_t N, int32_t* __restrict__ flag) {
-    int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (k < N) flag[k] = keep_elem[order[k]];
-}
-
-__global__ void k_compact(const int32_t* __restrict__ order, const int32_t* __restrict__ flag,
-                          const int32_t* __restrict__ incl, int64_t N, int32_t* __restrict__ keep_out) {
-    int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (k >= N || !flag[k]) return;
-    keep_out[incl[k] - 1] = order[k];
-}
-
-// kept count of call c = incl[end_c - 1] - incl[beg_c - 1], bounds from the sorted keys
-__global__ void k_call_kept(const int64_t* __restrict__ call_start, const int32_t* __restrict__ incl, int C,
-                            int32_t* __restrict__ out) {
-    int c = blockIdx.x * blockDim.x + threadIdx.x;
-    if (c >= C) return;
-    int64_t b = call_start[c], e = call_start[c + 1];
-    int32_t lo = b > 0 ? incl[b - 1] : 0;
-    int32_t hi = e > 0 ? incl[e - 1] : 0;
-    out[c] = hi - lo;  // (out: the host mailbox)
-}
-
-// vanilla calls whose kept set holds two equal scores (adjacent in the stable output order):
-// there torch's unstable sort may order them differently, the host reorders that call
-__global__ void k_tie_flags(const int32_t* __restrict__ keep, const int32_t* __restrict__ incl, int64_t N,
-                            const float* __restrict__ scores, const int32_t* __restrict__ elem_call,
-                            const uint8_t* __restrict__ call_van, int32_t* __restrict__ tie) {
-    const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x + 1;
-    if (N == 0 || p >= incl[N - 1]) return;
-    const int32_t a = keep[p - 1], b = keep[p];
-    const int32_t c = elem_call[b];
-    if (elem_call[a] == c && call_van[c] && scores[a] == scores[b]) tie[c] = 1;  // (tie: the host mailbox)
+// Output order of every call in one launch: the kept lists (k_nms_scan) already hold each
+// segment's kept elements in (score desc, index asc) order.  A coordinate-trick call is one
+// segment: its list is its output.  A vanilla call's output is the merge of its image segments'
+// lists: an element's rank is its own list index plus, in every other image's list, the count of
+// smaller (desc-score key, index) entries (binary search) -- torchvision's final stable-by-index
+// score sort.  An equal-score entry with a smaller index in any list of the call flags the call
+// for the host's unstable-order fix (torch sorts the vanilla result unstably).  Block 0 also
+// writes the per-call kept counts.  koff: exclusive prefix of the kept counts over the segments
+// (call-major), recomputed in LDS by every block (S <= NMS_OUT_MAXS).
+constexpr int NMS_OUT_MAXS = 15000;  // (S + 1) x 4 B of dynamic LDS (+ static) within the 64 KB default
+constexpr int OUT_G = 16;             // lanes per element: each searches every 16th image list
+__global__ __launch_bounds__(256) void k_nms_out(const uint64_t* __restrict__ klist, const int32_t* __restrict__ kcnt,
+                                                 const int64_t* __restrict__ sstart, const uint32_t* __restrict__ seg_hi,
+                                                 const int32_t* __restrict__ seg_base, int sbits, int n_img,
+                                                 const uint8_t* __restrict__ van, int S, int C, int64_t N,
+                                                 int32_t* __restrict__ keep, int32_t* __restrict__ res) {
+    extern __shared__ int32_t koff[];  // [S + 1]
+    __shared__ int32_t part[256];
+    const int tid = threadIdx.x, g = tid & (OUT_G - 1);
+    block_prefix<256>(kcnt, S, koff, part);
+    if (blockIdx.x == 0)
+        for (int c = tid; c < C; c += 256) res[c] = koff[seg_base[c + 1]] - koff[seg_base[c]];
+    const int64_t p = ((int64_t)blockIdx.x * 256 + tid) / OUT_G;  // this lane group's element
+    if (p >= N) return;  // (uniform over the group)
+    int lo = 0, hi = S - 1;  // last segment starting at or before p
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (sstart[mid] <= p) lo = mid; else hi = mid - 1;
+    }
+    const int sg = lo;
+    const int i = (int)(p - sstart[sg]);
+    if (i >= kcnt[sg]) return;
+    const uint64_t key = klist[p];
+    const uint32_t c = seg_hi[sg] >> sbits;
+    if (!van[c]) {
+        if (g == 0) keep[koff[sg] + i] = (int32_t)(uint32_t)key;
+        return;
+    }
+    const int s0 = seg_base[c];
+    int rank = 0;
+    bool tie = false;
+    for (int t = s0 + g; t < s0 + n_img; t += OUT_G) {
+        const int n = kcnt[t];
+        if (t == sg || n == 0) continue;
+        const uint64_t* l = klist + sstart[t];
+        int a = 0, b = n;  // lower bound of key
+        while (a < b) {
+            const int mid = (a + b) >> 1;
+            if (l[mid] < key) a = mid + 1; else b = mid;
+        }
+        rank += a;
+        tie |= a > 0 && (l[a - 1] >> 32) == (key >> 32);
+    }
+#pragma unroll
+    for (int o = 1; o < OUT_G; o <<= 1) {
+        rank += __shfl_xor(rank, o, OUT_G);
+        tie |= __shfl_xor((int)tie, o, OUT_G) != 0;
+    }
+    if (g == 0) {
+        tie |= i > 0 && (klist[p - 1] >> 32) == (key >> 32);
+        keep[koff[s0] + i + rank] = (int32_t)(uint32_t)key;
+        if (tie) res[C + 1 + c] = 1;
+    }
 }
 
 // host staging of several small tables for one H2D copy (16-B aligned members)
@@ -451,6 +732,17 @@ void inclusive_scan_i32(Arena& ar, int slot, const int32_t* in, int32_t* out, in
     VTF_HIP(rocprim::inclusive_scan(t, tmp, in, out, (size_t)n, rocprim::plus<int32_t>(), st));
 }
 
+// the division-free IoU test's constants for threshold thr (k_iou_mask)
+static IouThr iou_thr(double thr) {
+    VTF_CHECK(std::isfinite(thr) && std::fabs(thr) < 1e30, VTF_E_ARG, "nms: iou threshold must be finite");
+    float f = (float)thr;
+    if (!((double)f > thr)) f = std::nextafter(f, INFINITY);  // F: the smallest float above thr
+    const float fm = std::nextafter(f, -INFINITY);
+    uint32_t bits;
+    std::memcpy(&bits, &f, 4);
+    return IouThr{thr, ((double)fm + (double)f) * 0.5, (bits & 1u) == 0};
+}
+
 static bool nms_debug() {
     static const bool on = [] {
         const char* e = std::getenv("VTF_NMS_DEBUG");
@@ -491,17 +783,15 @@ void nms_multi(Arena& ar, const float* d_boxes, const float* d_scores, const int
     int sbits = 0, cbits = 0;
     while ((1 << sbits) < n_img) sbits++;
     while ((1 << cbits) < C) cbits++;
-    std::vector<uint32_t> seg_hi(S), call_hi(C);
+    std::vector<uint32_t> seg_hi(S);
     for (int c = 0; c < C; c++) {
-        call_hi[c] = (uint32_t)c << sbits;
         for (int s2 = seg_base[c]; s2 < seg_base[c + 1]; s2++) seg_hi[s2] = ((uint32_t)c << sbits) | (uint32_t)(s2 - seg_base[c]);
     }
     HostPack pk;
     const size_t o_cbeg = pk.add(call_beg.data(), C * 8), o_cn = pk.add(call_n.data(), C * 8);
     const size_t o_van = pk.add(vanilla.data(), C), o_sbase = pk.add(seg_base.data(), (C + 1) * 4);
+    VTF_CHECK(S <= NMS_OUT_MAXS, VTF_E_LIMIT, "nms_multi: too many segments (calls x images)");
     const size_t o_trick = pk.add(trick.data(), trick.size() * 4), o_seghi = pk.add(seg_hi.data(), S * 4);
-    const size_t o_callhi = pk.add(call_hi.data(), C * 4);
-    (void)o_sbase;
     const int tbytes = (int)((pk.buf.size() + 3) & ~(size_t)3);
     Arena::Mail mt = ar.mail(40, tbytes);
     std::memcpy(mt.h, pk.buf.data(), pk.buf.size());
@@ -512,24 +802,43 @@ void nms_multi(Arena& ar, const float* d_boxes, const float* d_scores, const int
     const int64_t* d_cbeg = (const int64_t*)(d_t1 + o_cbeg);
     const uint8_t* d_van = d_t1 + o_van;
     const uint32_t* d_seghi = (const uint32_t*)(d_t1 + o_seghi);
-    const uint32_t* d_callhi = (const uint32_t*)(d_t1 + o_callhi);
+    const int32_t* d_sbase = (const int32_t*)(d_t1 + o_sbase);
     (void)d_cbeg;
     float* d_cmax = ar.get<float>(52, C);
     int32_t* h_res = (int32_t*)mr.h;
     int32_t* d_res = (int32_t*)mr.d;
+    // segmented sort path when every segment fits the LDS sort (a segment holds at most its call's
+    // boxes); otherwise the device-wide merge sort
+    int64_t segbound = 0;
+    for (int c = 0; c < C; c++) segbound = std::max(segbound, call_n[c]);
+    const bool lds_sort = segbound <= NMS_SORT_BOUND;
+    int32_t* d_sctr = ar.get<int32_t>(45, 2 * (size_t)S);
     k_nms_prep<<<1 + (int)trick.size(), 256, 0, st>>>((const uint8_t*)mt.d, d_t1, tbytes, (const float4*)d_boxes, o_cbeg,
-                                                      o_cn, o_van, o_trick, C, d_cmax, d_res + C);
+                                                      o_cn, o_van, o_trick, C, d_cmax, d_res + C, d_sctr,
+                                                      lds_sort ? 2 * S : 0);
 
-    // sort 1: (call, segment image, score desc), stable over position order
+    // sort 1: (call, segment image, score desc), stable over position order -> ck (desc score key |
+    // element index) and ord (element index), segment starts
     uint64_t* k0 = ar.get<uint64_t>(46, N);
     uint64_t* k1 = ar.get<uint64_t>(47, N);
-    int32_t* v0 = ar.get<int32_t>(48, N);
     int32_t* ord = ar.get<int32_t>(49, N);
-    k_seg_keys<<<cdiv(N, 256), 256, 0, st>>>(d_scores, d_img, d_elem_call, d_van, N, 1, sbits, k0, v0);
-    merge_pairs_u64(ar, 50, k0, k1, v0, ord, N, st);
-    // segment bounds by binary search on the sorted keys
     int64_t* d_sstart = ar.get<int64_t>(51, (size_t)S + 1);
-    k_seg_bounds<<<cdiv(S + 1, 256), 256, 0, st>>>(k1, N, d_seghi, S, d_sstart);
+    uint64_t* ck = k1;
+    if (lds_sort) {
+        k_seg_count<<<cdiv(N, SEG_T), SEG_T, 0, st>>>(d_img, d_elem_call, d_van, d_sbase, N, S, d_sctr);
+        const size_t sc_lds = (size_t)(S + 1 + (S <= SEG_HIST ? 2 * S : 0)) * 4;
+        k_seg_scatter<<<cdiv(N, SEG_T), SEG_T, sc_lds, st>>>(d_scores, d_img, d_elem_call, d_van, d_sbase, N, S, d_sctr,
+                                                            d_sctr + S, d_sstart, k0);
+        k_seg_sort<<<S, 1024, 0, st>>>(d_sstart, k0, k1, ord);
+    } else {
+        int32_t* v0 = ar.get<int32_t>(48, N);
+        k_seg_keys<<<cdiv(N, 256), 256, 0, st>>>(d_scores, d_img, d_elem_call, d_van, N, 1, sbits, k0, v0);
+        merge_pairs_u64(ar, 50, k0, k1, v0, ord, N, st);
+        // segment bounds by binary search on the sorted keys
+        k_seg_bounds<<<cdiv(S + 1, 256), 256, 0, st>>>(k1, N, d_seghi, S, d_sstart);
+        ck = k0;
+        k_composite<<<cdiv(N, 256), 256, 0, st>>>(k1, ord, N, ck);
+    }
 
     // segment plan + mask tasks on the device (k_nms_plan); the host only sizes buffers and grids
     // from bounds over the calls' counts: a segment of call c has at most call_n[c] boxes, and
@@ -554,14 +863,21 @@ void nms_multi(Arena& ar, const float* d_boxes, const float* d_scores, const int
                                      d_tasks, d_ntask, tbound);
     uint64_t* d_mask = ar.get<uint64_t>(56, mwords);
     // one wave per task, striding: ~32 waves per CU bound the grid (most tasks cover 8 x 64 x 64 IoUs)
-    k_iou_mask<<<(int)std::max<int64_t>(1, std::min<int64_t>(tbound, 8192)), 64, 0, st>>>(
-        (const float4*)d_boxes, d_img, ord, d_tasks, d_sstart, d_scnt, d_moff, d_offb, thr, d_mask, d_ntask);
-    uint8_t* keep_sorted = ar.get<uint8_t>(57, N);
+    const IouThr ith = iou_thr(thr);
+    const int ig = (int)std::max<int64_t>(1, std::min<int64_t>(tbound, 8192));
+    if (ith.ge)
+        k_iou_mask<true><<<ig, 64, 0, st>>>((const float4*)d_boxes, d_img, ord, d_tasks, d_sstart, d_scnt, d_moff, d_offb,
+                                            ith, d_mask, d_ntask);
+    else
+        k_iou_mask<false><<<ig, 64, 0, st>>>((const float4*)d_boxes, d_img, ord, d_tasks, d_sstart, d_scnt, d_moff,
+                                             d_offb, ith, d_mask, d_ntask);
+    uint64_t* d_klist = ar.get<uint64_t>(57, N);
+    int32_t* d_kcnt = ar.get<int32_t>(58, S);
     // LDS bitset sized by the largest segment possible (one whole call); a segment beyond the LDS
     // limit raises the mailbox flag instead of overflowing
-    const int cap_nb = (int)std::min<int64_t>(nbmax, 160 * 1024 / 8);
-    k_nms_scan<<<S, 64 * SCAN_WAVES, (size_t)cap_nb * 8, st>>>(d_mask, d_sstart, d_scnt, d_moff, keep_sorted, cap_nb,
-                                                               d_res + C);
+    const int cap_nb = (int)std::min<int64_t>(nbmax, (160 * 1024 - 64) / 8);  // (+ the static s_kept)
+    k_nms_scan<<<S, 64 * SCAN_WAVES, (size_t)cap_nb * 8, st>>>(d_mask, d_sstart, d_scnt, d_moff, ck, d_klist, d_kcnt,
+                                                               cap_nb, d_res + C);
     if (nms_debug()) {  // VTF_NMS_DEBUG=1: per-call segment sizes on stderr (synchronises)
         std::vector<int64_t> ss(S + 1);
         VTF_HIP(hipMemcpyAsync(ss.data(), d_sstart, (S + 1) * 8, hipMemcpyDeviceToHost, st));
@@ -576,23 +892,11 @@ void nms_multi(Arena& ar, const float* d_boxes, const float* d_scores, const int
         fprintf(stderr, "nms_multi: C %d N %lld S %d max seg %lld sum nb %lld pairs %lld\n", C, (long long)N, S,
                 (long long)mx, (long long)nbs, (long long)pairs);
     }
-    uint8_t* keep_elem = ar.get<uint8_t>(58, N);
-    k_scatter_flags<<<cdiv(N, 256), 256, 0, st>>>(ord, keep_sorted, N, keep_elem);
-
-    // sort 2: (call, score desc), stable over position order -> output order
-    k_seg_keys<<<cdiv(N, 256), 256, 0, st>>>(d_scores, d_img, d_elem_call, d_van, N, 0, sbits, k0, v0);
-    merge_pairs_u64(ar, 50, k0, k1, v0, ord, N, st);
-    int32_t* flag = (int32_t*)k0;  // reuse
-    int32_t* incl = ((int32_t*)k0) + N;
-    k_flag_in_order<<<cdiv(N, 256), 256, 0, st>>>(ord, keep_elem, N, flag);
-    inclusive_scan_i32(ar, 59, flag, incl, N, st);
-    k_compact<<<cdiv(N, 256), 256, 0, st>>>(ord, flag, incl, N, d_keep);
-    k_seg_bounds<<<cdiv(C + 1, 256), 256, 0, st>>>(k1, N, d_callhi, C, d_sstart);
-    k_call_kept<<<cdiv(C, 256), 256, 0, st>>>(d_sstart, incl, C, d_res);
+    // output order, kept counts and vanilla tie flags in one launch
+    k_nms_out<<<cdiv(N * OUT_G, 256), 256, (size_t)(S + 1) * 4, st>>>(d_klist, d_kcnt, d_sstart, d_seghi, d_sbase, sbits, n_img,
+                                                              d_van, S, C, N, d_keep, d_res);
     bool any_van = false;
     for (int c = 0; c < C; c++) any_van |= vanilla[c] != 0;
-    if (any_van && N > 1)
-        k_tie_flags<<<cdiv(N - 1, 256), 256, 0, st>>>(d_keep, incl, N, d_scores, d_elem_call, d_van, d_res + C + 1);
     VTF_HIP(hipStreamSynchronize(st));
     VTF_CHECK(h_res[C] == 0, VTF_E_LIMIT, "nms_multi: a segment exceeds 1.3M boxes");
     for (int c = 0; c < C; c++) nkeep[c] = h_res[c];
