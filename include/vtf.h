@@ -196,9 +196,15 @@ int vtf_cosine_dedupe(const float* d_X, int64_t N, int64_t D, float* d_min, int6
  * row_end - row_begin entries.  Rows at or after row_end are not read. */
 int vtf_cosine_dedupe_rows(const float* d_X, int64_t N, int64_t D, int64_t row_begin, int64_t row_end, float* d_min,
                            int64_t* d_arg, void* hip_stream);
-/* classify (grouping.py:50-66): argmin / min over c of cosine distance(X_i, R_c). */
+/* classify (grouping.py:50-55): min / first argmin over c of sklearn cosine_distances(X, R)[i, c]
+ * in sklearn's own bits (normalize; X_n @ R_n.T as numpy's OpenBLAS sgemm / sgemv / sdot orders;
+ * clip(1 - G, 0, 2)).  d_X [N,D], d_R [C,D] fp32 -> d_min [N] fp32, d_arg [N] int64. */
 int vtf_cosine_classify(const float* d_X, int64_t N, const float* d_R, int64_t C, int64_t D, float* d_min,
                         int64_t* d_arg, void* hip_stream);
+/* the full matrix dist = cosine_distances(X, R) of classify (grouping.py:51) in the same bits:
+ * d_dist [N,C] fp32 (the per-class distances of log_classification.csv, grouping.py:58-64). */
+int vtf_cosine_distances_xr(const float* d_X, int64_t N, const float* d_R, int64_t C, int64_t D, float* d_dist,
+                            void* hip_stream);
 
 /* ---------------------------------------------------------------- hash dedupe
  * dupes.ahash (dupes.py:11-15) of N face crops of device frames (frames as in

@@ -6,7 +6,7 @@ requirements.txt:5): dupes.py:60-65 and grouping.py:50-53.
 
 cosine_dedupe / cosine_distances_exact: the C restatement (grouping_oracle.c) of
 sklearn cosine_distances in the bits of numpy 2.2's einsum and OpenBLAS 0.3.29's SkylakeX
-ssyrk, pinned bit for bit against sklearn itself in the survey container
+ssyrk (dedupe) and sgemm / sgemv / sdot (classify_distances_exact), pinned bit for bit against sklearn itself in the survey container
 (tests/test_oracle.py::test_cosine_restatement_vs_sklearn, the grouping / scale goldens).  It
 does not depend on the host's BLAS, so the GPU box (another CPU) checks against the same
 bits.  cosine_lower_sklearn calls sklearn directly (used to pin the restatement here).
@@ -60,3 +60,16 @@ def cosine_lower(X):
 def classify(X, R):
     D = sklearn.metrics.pairwise.cosine_distances(X, R)
     return D.min(axis=1), D.argmin(axis=1)
+
+
+def classify_distances_exact(X, R):
+    """grouping.py:51 cosine_distances(X, R) in the reference's bits (grouping_oracle.c: numpy's
+    OpenBLAS sgemm blocked / small-matrix, sgemv 4x4 / 4x2 / 4x1 kernels over 8 threads, sdot)."""
+    X = np.ascontiguousarray(X, np.float32)
+    R = np.ascontiguousarray(R, np.float32)
+    out = np.empty((X.shape[0], R.shape[0]), np.float32)
+    if X.shape[0]:
+        _lib().ora_cos_classify_dist(X.ctypes.data_as(ctypes.c_void_p), ctypes.c_int64(X.shape[0]),
+                                     R.ctypes.data_as(ctypes.c_void_p), ctypes.c_int64(R.shape[0]),
+                                     ctypes.c_int64(X.shape[1]), ctypes.c_int(0), out.ctypes.data_as(ctypes.c_void_p))
+    return out

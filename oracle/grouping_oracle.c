@@ -125,3 +125,119 @@ void ora_cos_distances(const float* X, int64_t N, int64_t D, float* out) {
         }
     free(xn);
 }
+
+/* ---- classify (grouping.py:50-53): cosine_distances(X, R) in the reference's bits ----
+ * X_n @ R_n.T is numpy matmul on two distinct buffers -> cblas_sgemm(RowMajor, NoTrans, Trans,
+ * N, C, D) = Fortran sgemm('T', 'N', C, N, D, 1, R_n, D, X_n, D, 0, G, C): the E-step's form
+ * (kmeans.hip) with alpha 1 and beta 0.  mode 0: the library's choice (sk_gemm_mode); 1: the
+ * blocked kernel (K blocks of gemm's rule, one fmaf chain per block from 0, G += block); 2: the
+ * small-matrix kernel (16 lanes over d mod 16, one fmaf chain per lane, adjacent-pair lane tree,
+ * halving tree on the C tile's edge block). */
+static float gemm_dot(const float* a, const float* b, int D, int mode, int edge) {
+    if (mode == 5) {
+        /* sgemv_t's 4x2 kernel: 4 lanes over d mod 4, product then add; (l0 + l1) + (l2 + l3) */
+        float l[4] = {0.f, 0.f, 0.f, 0.f};
+        for (int k = 0; k < D; k++) {
+            const float p = a[k] * b[k];
+            l[k & 3] = l[k & 3] + p;
+        }
+        return (l[0] + l[1]) + (l[2] + l[3]);
+    }
+    if (mode == 3 || mode == 4 || mode == 6) {
+        /* 3: sgemv_t's 4x4 kernel (numpy matmul with one side a single row): 8 lanes over d mod 8,
+         *    one fmaf chain per lane; (l_u + l_{u+4}), then (a0 + a1) + (a2 + a3).
+         * 6: sgemv_t's 4x1 kernel: the same lanes and tree, product then add (no fma).
+         * 4: sdot (a single row times a single row): 64 lanes over d mod 64 as 8 accumulators of
+         *    8 lanes, combined (((c0 + c1) + (c2 + c3)) + (c4 + c5)) + (c6 + c7), then the 8
+         *    lanes as in 3.  (Probed for D % 64 == 0.) */
+        const int L = mode == 4 ? 64 : 8;
+        float l[64];
+        for (int u = 0; u < L; u++) l[u] = 0.f;
+        for (int k = 0; k < D; k++) {
+            if (mode == 6) {
+                const float p = a[k] * b[k];
+                l[k % L] = l[k % L] + p;
+            } else {
+                l[k % L] = fmaf(a[k], b[k], l[k % L]);
+            }
+        }
+        float v[8];
+        for (int u = 0; u < 8; u++) v[u] = l[u];
+        if (mode == 4)
+            for (int u = 0; u < 8; u++) {
+                const float c01 = l[u] + l[8 + u], c23 = l[16 + u] + l[24 + u];
+                const float c45 = l[32 + u] + l[40 + u], c67 = l[48 + u] + l[56 + u];
+                v[u] = ((c01 + c23) + c45) + c67;
+            }
+        const float a0 = v[0] + v[4], a1 = v[1] + v[5], a2 = v[2] + v[6], a3 = v[3] + v[7];
+        return (a0 + a1) + (a2 + a3);
+    }
+    if (mode == 2) {
+        float l[16];
+        for (int u = 0; u < 16; u++) l[u] = 0.f;
+        for (int k = 0; k < D; k++) l[k & 15] = fmaf(a[k], b[k], l[k & 15]);
+        if (edge) {
+            for (int w = 8; w >= 1; w >>= 1)
+                for (int u = 0; u < w; u++) l[u] = l[u] + l[u + w];
+        } else {
+            for (int w = 1; w < 16; w <<= 1)
+                for (int u = 0; u < 16; u += 2 * w) l[u] = l[u] + l[u + w];
+        }
+        return l[0];
+    }
+    float tot = 0.f;
+    for (int k0 = 0; k0 < D;) {
+        int k1 = k0 + kblock(D - k0, 0);
+        float acc = 0.f;
+        for (int k = k0; k < k1; k++) acc = fmaf(a[k], b[k], acc);
+        tot = tot + acc;
+        k0 = k1;
+    }
+    return tot;
+}
+
+int ora_sk_gemm_mode(int64_t N, int64_t C, int64_t D) {
+    if (N == 1 && C == 1) return 4;
+    if (N == 1 || C == 1) return 3;
+    return ((double)N * C * D <= 1e6 && C * N <= 1200 && D >= 32) ? 2 : 1;
+}
+
+/* Which sgemv_t kernel computes output o of n (numpy's gemv calls: one output per row of the
+ * many-row side).  OpenBLAS splits the outputs over its threads when m * n >= 460800 (m = D;
+ * measured: 8 threads in the survey container, ranges of ceil(rest / threads left) outputs, at
+ * least 4); in each range groups of 4 take the 4x4 kernel, then 2 the 4x2 and 1 the 4x1. */
+int ora_gemv_kernel(int64_t o, int64_t n, int64_t D, int threads) {
+    int64_t a = 0;
+    int T = (double)n * D >= 460800.0 ? threads : 1;
+    for (int t = 0; a < n; t++) {
+        int64_t w = T - t > 1 ? (n - a + (T - t) - 1) / (T - t) : n - a;
+        if (w < 4) w = 4;
+        if (w > n - a) w = n - a;
+        if (o < a + w) {
+            const int64_t r = o - a, q = w / 4 * 4;
+            if (r < q) return 3;
+            return (w & 2) && r < q + 2 ? 5 : 6;
+        }
+        a += w;
+    }
+    return 3;
+}
+
+void ora_cos_classify_dist(const float* X, int64_t N, const float* R, int64_t C, int64_t D, int mode, float* out) {
+    float* xn = (float*)malloc(sizeof(float) * (size_t)(N * D));
+    float* rn = (float*)malloc(sizeof(float) * (size_t)(C * D));
+    ora_normalize(X, N, D, xn);
+    ora_normalize(R, C, D, rn);
+    if (mode == 0) mode = ora_sk_gemm_mode(N, C, D);
+#pragma omp parallel for schedule(static)
+    for (int64_t i = 0; i < N; i++)
+        for (int64_t c = 0; c < C; c++) {
+            const int edge = i >= N - N % 4 && c >= C - C % 4;
+            int md = mode;
+            if (mode == 3) md = C == 1 ? ora_gemv_kernel(i, N, D, 8) : ora_gemv_kernel(c, C, D, 8);
+            float d = 1.0f - gemm_dot(xn + i * D, rn + c * D, (int)D, md, edge);
+            out[i * C + c] = d < 0.f ? 0.f : (d > 2.f ? 2.f : d);
+        }
+    free(xn);
+    free(rn);
+}

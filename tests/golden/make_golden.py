@@ -813,8 +813,42 @@ def gen_boxes():
     np.savez_compressed(os.path.join(HERE, 'boxes.npz'), **out)
 
 
+# classify cases: (name, N, C, D, thr, seed) -- every numpy matmul order sklearn takes for
+# X_n @ R_n.T (grouping_oracle.c): blocked sgemm (planted 10k x 8), small-matrix sgemm with an
+# edge block (301 x 3), sgemv with 8 OpenBLAS threads (1003 x 1: 4x4 / 4x2 / 4x1 kernels per
+# range), sgemv single thread (150 x 1), vector @ matrix (1 x 13), sdot (1 x 1)
+CLASSIFY_CASES = [('planted', 10000, 8, 512, 0.9, 0), ('small', 301, 3, 768, 0.9, 1), ('gemv8', 1003, 1, 512, 0.9, 2),
+                  ('gemv1', 150, 1, 1024, 0.9, 3), ('vecmat', 1, 13, 512, 0.9, 4), ('dot', 1, 1, 1024, 0.9, 5),
+                  ('nothr', 500, 5, 512, None, 6)]
+
+
+def gen_classify():
+    """The reference's classify (grouping.py:50-66) on synth.classify_set data: the assigned
+    indices (with 'other'), sklearn's distance matrix, and the log_classification.csv text."""
+    import hashlib
+    load_ref()
+    grouping = importlib.import_module('ref_vtf.grouping')
+    import sklearn.metrics
+    out = {}
+    for name, N, C, D, thr, seed in CLASSIFY_CASES:
+        X, R = synth.classify_set(N, C, D, thr or 0.9, seed)
+        classes = ['c%d' % i for i in range(C)]
+        paths = ['/x/face_%05d.jpg' % i for i in range(N)]
+        with tempfile.TemporaryDirectory() as td:
+            os.makedirs(os.path.join(td, 'faces'))
+            inds, classes = grouping.classify(X, R, classes, thr, True, paths, td)
+            csv = open(os.path.join(td, 'faces', 'log_classification.csv')).read()
+        out[name + '_inds'] = np.asarray(inds, np.int64)
+        out[name + '_ncls'] = np.int64(len(classes))
+        out[name + '_dist'] = sklearn.metrics.pairwise.cosine_distances(X, R)
+        out[name + '_csv_sha'] = np.array(hashlib.sha256(csv.encode()).hexdigest())
+        out[name + '_x_sha'] = np.array(hashlib.sha256(X.tobytes() + R.tobytes()).hexdigest())
+    np.savez_compressed(os.path.join(HERE, 'classify.npz'), **out)
+    print('classify', {k: v.shape for k, v in out.items()})
+
+
 if __name__ == '__main__':
     which = sys.argv[1:] or ['mtcnn', 'facenet', 'vit', 'grouping', 'yolo', 'kmeans', 'rcnn', 'dupes', 'boxes', 'shapes', 'chain',
-                             'scale', 'c3', 'iom', 'b1', 'meta']
+                             'scale', 'c3', 'iom', 'b1', 'classify', 'meta']
     for w in which:
         globals()['gen_' + w]()

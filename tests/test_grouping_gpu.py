@@ -77,6 +77,54 @@ def test_classify_vs_golden(g):
     assert classes == ['a', 'b', 'c', 'other']
 
 
+def _classify_cases():
+    import sys
+    sys.path.insert(0, GOLDEN)
+    from make_golden import CLASSIFY_CASES
+    return CLASSIFY_CASES
+
+
+@pytest.mark.parametrize('case', _classify_cases(), ids=lambda c: c[0])
+def test_classify_sklearn_bits_vs_golden(case, tmp_path):
+    """classify (grouping.py:50-66) in sklearn's exact bits, every matmul form sklearn reaches:
+    the planted 10k x 8 set (a third of the rows within +-2e-6 of the 'other' threshold, 41 of
+    them exactly on it; a third near-tied between two classes, 405 exact ties) and the small /
+    gemv (1 and 8 BLAS threads) / vector-matrix / dot shapes.  Assigned indices (incl. 'other'),
+    the full distance matrix and the log_classification.csv text equal the reference's."""
+    import hashlib
+    from videotofaces import grouping, synth
+    name, N, C, D, thr, seed = case
+    g = np.load(os.path.join(GOLDEN, 'classify.npz'))
+    X, R = synth.classify_set(N, C, D, thr or 0.9, seed)
+    assert hashlib.sha256(X.tobytes() + R.tobytes()).hexdigest() == str(g[name + '_x_sha'])
+    np.testing.assert_array_equal(grouping.cosine_distances_device(X, R), g[name + '_dist'])
+    os.makedirs(tmp_path / 'faces')
+    paths = ['/x/face_%05d.jpg' % i for i in range(N)]
+    inds, classes = grouping.classify(X, R, ['c%d' % i for i in range(C)], thr, True, paths, str(tmp_path))
+    np.testing.assert_array_equal(inds, g[name + '_inds'])
+    assert len(classes) == int(g[name + '_ncls'])
+    csv = open(tmp_path / 'faces' / 'log_classification.csv').read()
+    assert hashlib.sha256(csv.encode()).hexdigest() == str(g[name + '_csv_sha'])
+    if name == 'planted':
+        print('other %d, on the threshold %d' % (int((inds == C).sum()), int((g[name + '_dist'].min(1) == np.float32(thr)).sum())))
+
+
+def test_classify_nan_rows_vs_oracle():
+    """a NaN row: numpy's min is NaN and argmin the first NaN (the reference's dist.min /
+    argmin); zero rows normalise with norm 1 (distance 1)"""
+    from videotofaces import grouping, synth
+    from oracle import grouping as og
+    X, R = synth.classify_set(64, 4, 512, 0.9, seed=11)
+    X[5, 7] = np.nan
+    X[9] = 0
+    ref = og.classify_distances_exact(X, R)
+    got = grouping.cosine_distances_device(X, R)
+    np.testing.assert_array_equal(got, ref)
+    mins, inds = grouping.cosine_classify_device(X, R)
+    np.testing.assert_array_equal(mins, ref.min(1))
+    np.testing.assert_array_equal(inds, ref.argmin(1))
+
+
 @pytest.fixture(scope='module')
 def km():
     from videotofaces import synth

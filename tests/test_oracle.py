@@ -1,6 +1,7 @@
 """CPU: pin the oracle (tests' CPU restatement) against golden vectors made from the
 reference's own modules (tests/golden/make_golden.py)."""
 import os
+import sys
 
 import numpy as np
 import pytest
@@ -128,6 +129,47 @@ def test_cosine_restatement_vs_sklearn(N, D):
     mins, inds = og.cosine_dedupe(X)
     np.testing.assert_array_equal(mins, ref.min(1))
     np.testing.assert_array_equal(inds, ref.argmin(1))
+
+
+def _openblas_threads():
+    import threadpoolctl
+    return [d.get('num_threads') for d in threadpoolctl.threadpool_info()
+            if d.get('internal_api') == 'openblas' and 'numpy' in d.get('filepath', '')]
+
+
+@pytest.mark.parametrize('N,C,D', [(10000, 8, 512), (600, 3, 512), (301, 3, 768), (37, 5, 1024), (2, 2, 512),
+                                   (1003, 1, 512), (900, 1, 512), (899, 1, 512), (451, 1, 1024), (150, 1, 1024),
+                                   (7, 1, 768), (1, 13, 512), (1, 5, 1024), (1, 1, 512), (1, 1, 1024)])
+def test_classify_restatement_vs_sklearn(N, C, D):
+    """oracle/grouping_oracle.c == sklearn cosine_distances(X, R) bit for bit for every matmul
+    form sklearn reaches (blocked / small sgemm, sgemv's three kernels and its 8-thread split,
+    sdot); the orders were measured on numpy's OpenBLAS SkylakeX kernels with 8 threads."""
+    if not _skylakex_blas() or _openblas_threads() != [8]:
+        pytest.skip('numpy BLAS is not 8-thread OpenBLAS SkylakeX: sklearn bits differ from the pinned ones')
+    import sklearn.metrics
+    from oracle import grouping as og
+    from videotofaces import synth
+    X, R = synth.classify_set(N, C, D, 0.9, seed=N + C + D)
+    np.testing.assert_array_equal(og.classify_distances_exact(X, R), sklearn.metrics.pairwise.cosine_distances(X, R))
+
+
+def test_oracle_classify_vs_golden():
+    """the pinned restatement reproduces the reference's classify goldens (any host CPU)"""
+    import hashlib
+    from oracle import grouping as og
+    from videotofaces import synth
+    sys.path.insert(0, GOLDEN)
+    from make_golden import CLASSIFY_CASES
+    g = np.load(os.path.join(GOLDEN, 'classify.npz'))
+    for name, N, C, D, thr, seed in CLASSIFY_CASES:
+        X, R = synth.classify_set(N, C, D, thr or 0.9, seed)
+        assert hashlib.sha256(X.tobytes() + R.tobytes()).hexdigest() == str(g[name + '_x_sha'])
+        dist = og.classify_distances_exact(X, R)
+        np.testing.assert_array_equal(dist, g[name + '_dist'])
+        inds = dist.argmin(1)
+        if thr:
+            inds[dist.min(1) >= thr] = C
+        np.testing.assert_array_equal(inds, g[name + '_inds'])
 
 
 def test_oracle_grouping_vs_golden():

@@ -22,7 +22,8 @@
 // the block's end; distance + clip + row-min in the epilogue, one 64-bit atomicMin per (row,
 // tile) on the key (dist bits << 32 | j): dist >= 0 so float bits order like the floats, and
 // ties resolve to the smallest j = numpy's first argmin.  Nothing N x N ever touches HBM.
-// classify (grouping.py:50-66): argmin / min over C references of cosine distance.
+// classify (grouping.py:50-66): argmin / min over C references of cosine distance, in sklearn's
+// bits (k_classify below).
 #include "common.hpp"
 #include "sk_order.hpp"
 
@@ -30,15 +31,42 @@ namespace vtf {
 
 typedef __attribute__((ext_vector_type(4))) float f32x4;
 
-// Xn [N][Dp] = X / ||X|| in sklearn normalize's bits (zero norm -> 1), zero-padded to Dp;
-// one thread per row (numpy's einsum order is a 4-lane sequential chain)
-__global__ void k_row_normalize(const float* __restrict__ X, int64_t N, int D, int Dp, float* __restrict__ Xn) {
-    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= N) return;
-    const float* x = X + i * D;
-    float nrm = sqrtf(np_einsum_sq(x, D));  // correctly rounded (hipcc's __fsqrt_rn is the 1-ulp v_sqrt_f32)
+// Xn [N][Dp] = X / ||X|| in sklearn normalize's bits (zero norm -> 1), zero-padded to Dp.  One
+// wave per row: the row is read coalesced into LDS, lanes 0-3 run numpy einsum's four sequential
+// chains over it (sk_order.hpp's order), every lane writes the normalised row coalesced.
+constexpr int NRM_W = 4;  // rows (waves) per block
+__global__ __launch_bounds__(64 * NRM_W) void k_row_normalize(const float* __restrict__ X, int64_t N, int D, int Dp,
+                                                               float* __restrict__ Xn) {
+    extern __shared__ float srow[];  // [NRM_W][D]
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int64_t i = (int64_t)blockIdx.x * NRM_W + w;
+    const bool valid = i < N;
+    float* r = srow + w * D;
+    const float* x = X + (valid ? i : 0) * D;
+    if (valid)
+        for (int k = lane; k < D; k += 64) r[k] = x[k];
+    __syncthreads();
+    float l = 0.f;  // lane u < 4: numpy's SSE lane u
+    if (lane < 4) {
+        int t = 0;
+        for (; D - t >= 16; t += 16)
+            for (int q = 3; q >= 0; q--) {
+                const float v = r[t + 4 * q + lane];
+                l = __fadd_rn(__fmul_rn(v, v), l);
+            }
+        for (; t < D; t += 4) {
+            const float v = t + lane < D ? r[t + lane] : 0.f;
+            l = __fadd_rn(__fmul_rn(v, v), l);
+        }
+    }
+    const float l1 = __shfl(l, 1), l2 = __shfl(l, 2), l3 = __shfl(l, 3);
+    float nrm = sqrtf(__fadd_rn(__fadd_rn(__shfl(l, 0), l1), __fadd_rn(l2, l3)));  // correctly rounded
     if (nrm == 0.f) nrm = 1.f;
-    for (int k = 0; k < Dp; k++) Xn[i * Dp + k] = k < D ? __fdiv_rn(x[k], nrm) : 0.f;
+    if (valid)
+        for (int k = lane; k < Dp; k += 64) Xn[i * Dp + k] = k < D ? __fdiv_rn(r[k], nrm) : 0.f;
+}
+static void row_normalize(const float* X, int64_t N, int D, int Dp, float* Xn, hipStream_t st) {
+    k_row_normalize<<<cdiv(N, NRM_W), 64 * NRM_W, (size_t)NRM_W * D * 4, st>>>(X, N, D, Dp, Xn);
 }
 
 __global__ void k_init_keys(uint64_t* key, int64_t N) {
@@ -236,25 +264,163 @@ __global__ void k_unpack(const uint64_t* __restrict__ key, int64_t N, float* __r
     }
 }
 
-__global__ void k_classify(const float* __restrict__ Xn, const float* __restrict__ Rn, int64_t N, int C, int Dp,
-                           float* __restrict__ mn, int64_t* __restrict__ arg) {
-    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= N) return;
-    float best = 3.4e38f;
-    int bk = 0;
-    for (int c = 0; c < C; c++) {
-        float s = 0.f;
-        for (int k = 0; k < Dp; k++) s = fmaf(Xn[i * Dp + k], Rn[(int64_t)c * Dp + k], s);
-        float d = fminf(fmaxf(1.0f - s, 0.f), 2.f);
-        if (d < best) {
-            best = d;
-            bk = c;
-        }
-    }
-    mn[i] = best;
-    arg[i] = bk;
+// ---- classify (grouping.py:50-53): cosine_distances(X, R) in sklearn's bits -------------------
+// X_n @ R_n.T is numpy matmul on two buffers (OpenBLAS 0.3.29 SkylakeX kernels; probed by
+// absorption and checked bit for bit against sklearn in the survey container: oracle/
+// grouping_oracle.c, tests/test_oracle.py::test_classify_restatement_vs_sklearn):
+//   CL_BLOCKED  sgemm, blocked kernel: K blocks of gemm's rule (sk_order.hpp), one fmaf chain per
+//               block from 0, G += block;
+//   CL_SMALL    sgemm small-matrix kernel (N C D <= 1e6, C N <= 1200, D >= 32): 16 lanes over
+//               d mod 16, one fmaf chain each; adjacent-pair lane tree, halving tree on the edge
+//               block (row >= N - N % 4 and class >= C - C % 4);
+//   CL_GEMV     one side a single row: sgemv_t, each output by one of three kernels: 4x4 (8 lanes
+//               over d mod 8, fmaf), 4x2 (4 lanes, product then add), 4x1 (8 lanes, product then
+//               add); lane trees (l_u + l_{u+4}) then (a0 + a1) + (a2 + a3), resp.
+//               (l0 + l1) + (l2 + l3).  Outputs are split over OpenBLAS's threads when D n >=
+//               460800 (8 threads in the survey container), 4x4 groups first in every range;
+//   CL_DOT      a single row each: sdot, 64 lanes over d mod 64 (8 accumulators of 8 lanes),
+//               (((c0 + c1) + (c2 + c3)) + (c4 + c5)) + (c6 + c7), then the 8 lanes as in 4x4.
+// Then d = clip(1 - G, 0, 2) (S *= -1; S += 1; np.clip keeps NaN) and numpy's min / first argmin
+// (a NaN wins both).
+enum { CL_BLOCKED = 1, CL_SMALL = 2, CL_GEMV = 3, CL_DOT = 4 };
+constexpr int CL_BLAS_THREADS = 8;  // OpenBLAS threads of the survey container (its 8 cores)
+
+__host__ __device__ inline int classify_mode(int64_t N, int64_t C, int64_t D) {
+    if (N == 1 && C == 1) return CL_DOT;
+    if (N == 1 || C == 1) return CL_GEMV;
+    return ((double)N * C * D <= 1e6 && C * N <= 1200 && D >= 32) ? CL_SMALL : CL_BLOCKED;
 }
 
+// sgemv_t kernel of output o of n: 0 = 4x4, 1 = 4x2, 2 = 4x1
+__device__ inline int gemv_kernel(int64_t o, int64_t n, int64_t D) {
+    const int T = (double)n * D >= 460800.0 ? CL_BLAS_THREADS : 1;
+    int64_t a = 0;
+    for (int t = 0; a < n; t++) {
+        int64_t w = T - t > 1 ? (n - a + (T - t) - 1) / (T - t) : n - a;
+        w = min(max(w, (int64_t)4), n - a);
+        if (o < a + w) {
+            const int64_t r = o - a, q = w / 4 * 4;
+            if (r < q) return 0;
+            return (w & 2) && r < q + 2 ? 1 : 2;
+        }
+        a += w;
+    }
+    return 0;
+}
+
+constexpr int CL_R = 16, CL_C = 16, CL_K = 64;
+template <int MODE>
+__global__ __launch_bounds__(256) void k_classify(const float* __restrict__ Xn, const float* __restrict__ Rn, int64_t N,
+                                                  int C, int D, int Dp, float* __restrict__ mn,
+                                                  int64_t* __restrict__ arg, float* __restrict__ dist) {
+    __shared__ float sX[CL_R][CL_K + 1], sR[CL_C][CL_K + 1];
+    __shared__ float sD[CL_R][CL_C];
+    const int tid = threadIdx.x, r = tid >> 4, cj = tid & 15;
+    const int64_t i0 = (int64_t)blockIdx.x * CL_R, i = i0 + r;
+    float best = 0.f;
+    int bk = -1;
+    for (int c0 = 0; c0 < C; c0 += CL_C) {
+        const int c = c0 + cj;
+        constexpr int L = MODE == CL_DOT ? 64 : (MODE == CL_SMALL ? 16 : 8);
+        float l[L];
+#pragma unroll
+        for (int u = 0; u < L; u++) l[u] = 0.f;
+        float acc = 0.f, tot = 0.f;
+        int kb_end = blas_kblock(D, false);
+        int gk = 0;  // CL_GEMV: this output's kernel
+        if (MODE == CL_GEMV) gk = C == 1 ? gemv_kernel(i, N, D) : gemv_kernel(c, C, D);
+        for (int t0 = 0; t0 < Dp; t0 += CL_K) {
+            for (int e = tid; e < CL_R * CL_K; e += 256) {  // rows of 64 floats: coalesced
+                const int rr = e / CL_K, tt = e % CL_K;
+                sX[rr][tt] = i0 + rr < N ? Xn[(i0 + rr) * Dp + t0 + tt] : 0.f;
+                sR[rr][tt] = c0 + rr < C ? Rn[(int64_t)(c0 + rr) * Dp + t0 + tt] : 0.f;
+            }
+            __syncthreads();
+            const int tn = min(CL_K, D - t0);
+#pragma unroll
+            for (int tt = 0; tt < CL_K; tt++) {
+                if (tt < tn) {
+                    const float a = sX[r][tt], b = sR[cj][tt];
+                    if (MODE == CL_BLOCKED) {
+                        acc = fmaf(a, b, acc);
+                        if (t0 + tt + 1 == kb_end) {  // end of a K block: G += block
+                            tot = __fadd_rn(tot, acc);
+                            acc = 0.f;
+                            kb_end += blas_kblock(D - kb_end, false);
+                        }
+                    } else if (MODE == CL_GEMV) {
+                        if (gk == 0) {
+                            l[tt & 7] = fmaf(a, b, l[tt & 7]);
+                        } else {
+                            const float p = __fmul_rn(a, b);
+                            if (gk == 1) l[tt & 3] = __fadd_rn(l[tt & 3], p);
+                            else l[tt & 7] = __fadd_rn(l[tt & 7], p);
+                        }
+                    } else {
+                        l[tt % L] = fmaf(a, b, l[tt % L]);
+                    }
+                }
+            }
+            __syncthreads();
+        }
+        float g;
+        if (MODE == CL_BLOCKED) {
+            g = tot;
+        } else if (MODE == CL_SMALL) {
+            if (i >= N - N % 4 && c >= C - C % 4) {  // edge block of the C tile: halving tree
+#pragma unroll
+                for (int w = 8; w >= 1; w >>= 1)
+#pragma unroll
+                    for (int u = 0; u < w; u++) l[u] = __fadd_rn(l[u], l[u + w]);
+            } else {  // adjacent pairs
+#pragma unroll
+                for (int w = 1; w < 16; w <<= 1)
+#pragma unroll
+                    for (int u = 0; u < 16; u += 2 * w) l[u] = __fadd_rn(l[u], l[u + w]);
+            }
+            g = l[0];
+        } else {
+            float v[8];
+            if (MODE == CL_DOT) {
+#pragma unroll
+                for (int u = 0; u < 8; u++) {
+                    const float c01 = __fadd_rn(l[u], l[8 + u]), c23 = __fadd_rn(l[16 + u], l[24 + u]);
+                    const float c45 = __fadd_rn(l[32 + u], l[40 + u]), c67 = __fadd_rn(l[48 + u], l[56 + u]);
+                    v[u] = __fadd_rn(__fadd_rn(__fadd_rn(c01, c23), c45), c67);
+                }
+            } else {
+#pragma unroll
+                for (int u = 0; u < 8; u++) v[u] = l[u];
+            }
+            if (MODE == CL_GEMV && gk == 1) {
+                g = __fadd_rn(__fadd_rn(v[0], v[1]), __fadd_rn(v[2], v[3]));
+            } else {
+                const float a0 = __fadd_rn(v[0], v[4]), a1 = __fadd_rn(v[1], v[5]);
+                const float a2 = __fadd_rn(v[2], v[6]), a3 = __fadd_rn(v[3], v[7]);
+                g = __fadd_rn(__fadd_rn(a0, a1), __fadd_rn(a2, a3));
+            }
+        }
+        float d = __fsub_rn(1.0f, g);
+        d = d < 0.f ? 0.f : (d > 2.f ? 2.f : d);  // (NaN stays NaN, as np.clip)
+        sD[r][cj] = d;
+        if (dist && i < N && c < C) dist[i * C + c] = d;  // (the full matrix: classify's CSV log)
+        __syncthreads();
+        if (cj == 0 && mn) {  // numpy min / first argmin over the row, chunk by chunk in class order
+            for (int q = 0; q < CL_C && c0 + q < C; q++) {
+                const float v = sD[r][q];
+                if (bk < 0 || (best == best && (v != v || v < best))) {
+                    best = v;
+                    bk = c0 + q;
+                }
+            }
+        }
+        __syncthreads();
+    }
+    if (cj == 0 && i < N && mn) {
+        mn[i] = best;
+        arg[i] = bk;
+    }
+}
 
 }  // namespace vtf
 
@@ -274,7 +440,7 @@ static void cosine_dedupe_rows(const float* d_X, int64_t N, int64_t D, int64_t r
     float* Xn = ar.get<float>(0, N * Dp);
     uint64_t* key = ar.get<uint64_t>(1, r1 - r0);
     // rows r1.. are never read (tiles pair a row block with itself and earlier blocks only)
-    k_row_normalize<<<cdiv(r1, 64), 64, 0, st>>>(d_X, r1, (int)D, Dp, Xn);
+    row_normalize(d_X, r1, (int)D, Dp, Xn, st);
     k_init_keys<<<cdiv(r1 - r0, 256), 256, 0, st>>>(key, r1 - r0);
     const int64_t b0 = r0 / CT, b1 = (r1 + CT - 1) / CT;
     const int64_t t0 = b0 * (b0 + 1) / 2, t1 = b1 * (b1 + 1) / 2;
@@ -308,22 +474,43 @@ int vtf_cosine_dedupe_rows(const float* d_X, int64_t N, int64_t D, int64_t row_b
     });
 }
 
+static void cosine_classify(const float* d_X, int64_t N, const float* d_R, int64_t C, int64_t D, float* d_min,
+                            int64_t* d_arg, float* d_dist, hipStream_t st) {
+    VTF_CHECK(N >= 0 && C > 0 && D > 0, VTF_E_ARG, "bad argument");
+    if (N == 0) return;
+    VTF_CHECK(d_X && d_R && (d_dist || (d_min && d_arg)), VTF_E_ARG, "null argument");
+    VTF_CHECK(C < (int64_t)1 << 31 && D < (int64_t)1 << 30, VTF_E_ARG, "bad argument");
+    StreamScratch sc = stream_scratch(st);
+    Arena& ar = *sc.ar;
+    const int Dp = (int)((D + CL_K - 1) / CL_K * CL_K);
+    float* Xn = ar.get<float>(2, N * Dp);
+    float* Rn = ar.get<float>(3, C * Dp);
+    row_normalize(d_X, N, (int)D, Dp, Xn, st);
+    row_normalize(d_R, C, (int)D, Dp, Rn, st);
+    const unsigned grid = (unsigned)cdiv(N, CL_R);
+    const int c = (int)C, d = (int)D;
+    switch (classify_mode(N, C, D)) {
+        case CL_BLOCKED: k_classify<CL_BLOCKED><<<grid, 256, 0, st>>>(Xn, Rn, N, c, d, Dp, d_min, d_arg, d_dist); break;
+        case CL_SMALL: k_classify<CL_SMALL><<<grid, 256, 0, st>>>(Xn, Rn, N, c, d, Dp, d_min, d_arg, d_dist); break;
+        case CL_GEMV: k_classify<CL_GEMV><<<grid, 256, 0, st>>>(Xn, Rn, N, c, d, Dp, d_min, d_arg, d_dist); break;
+        default: k_classify<CL_DOT><<<grid, 256, 0, st>>>(Xn, Rn, N, c, d, Dp, d_min, d_arg, d_dist); break;
+    }
+    VTF_HIP(hipGetLastError());
+}
+
 int vtf_cosine_classify(const float* d_X, int64_t N, const float* d_R, int64_t C, int64_t D, float* d_min,
                         int64_t* d_arg, void* hip_stream) {
     return guarded_on(stream_device((hipStream_t)hip_stream), [&] {
-        VTF_CHECK(N >= 0 && C > 0 && D > 0, VTF_E_ARG, "bad argument");
-        if (N == 0) return;
-        VTF_CHECK(d_X && d_R && d_min && d_arg, VTF_E_ARG, "null argument");
-        hipStream_t st = (hipStream_t)hip_stream;
-        StreamScratch sc = stream_scratch(st);
-        Arena& ar = *sc.ar;
-        int Dp = (int)((D + CK - 1) / CK * CK);
-        float* Xn = ar.get<float>(2, N * Dp);
-        float* Rn = ar.get<float>(3, C * Dp);
-        k_row_normalize<<<cdiv(N, 64), 64, 0, st>>>(d_X, N, (int)D, Dp, Xn);
-        k_row_normalize<<<cdiv(C, 64), 64, 0, st>>>(d_R, C, (int)D, Dp, Rn);
-        k_classify<<<cdiv(N, 128), 128, 0, st>>>(Xn, Rn, N, (int)C, Dp, d_min, d_arg);
-        VTF_HIP(hipGetLastError());
+        VTF_CHECK(d_min && d_arg, VTF_E_ARG, "null argument");
+        cosine_classify(d_X, N, d_R, C, D, d_min, d_arg, nullptr, (hipStream_t)hip_stream);
+    });
+}
+
+int vtf_cosine_distances_xr(const float* d_X, int64_t N, const float* d_R, int64_t C, int64_t D, float* d_dist,
+                            void* hip_stream) {
+    return guarded_on(stream_device((hipStream_t)hip_stream), [&] {
+        VTF_CHECK(d_dist, VTF_E_ARG, "null argument");
+        cosine_classify(d_X, N, d_R, C, D, nullptr, nullptr, d_dist, (hipStream_t)hip_stream);
     });
 }
 

@@ -77,6 +77,7 @@ SIGNATURES = {
     'vtf_yolo_postprocess': [_p, _p, _p, _p, _i32, _i32, _i32, _p, _p, _p, _i64, _p],
     'vtf_yolo_profile': [_p, _i32, _p, _p, _p, _p],
     'vtf_cosine_classify': [_p, _i64, _p, _i64, _i64, _p, _p, _p],
+    'vtf_cosine_distances_xr': [_p, _i64, _p, _i64, _i64, _p, _p],
     'vtf_ahash_crops': [_p, _i32, _i32, _i32, _i64, _i64, _p, _i64, _p, _p],
     'vtf_iom_nms': [_p, _p, _p, _i64, _f32, _p, _p, _p],
     'vtf_boxes_to_crops': [_p, _p, _i32, _i32, _i32, _p, _i32, _p, _p, _p, _i64, _p, _p],

@@ -54,8 +54,8 @@ def encode_faces(paths, model, bs, area):
 
 
 def cosine_classify_device(X, R, device=None):
-    """classify's distances (grouping.py:51-53): min / argmin over the reference rows of the
-    cosine distance, on `device` (default cuda:0)."""
+    """classify's distances (grouping.py:51-55): min / first argmin over the reference rows of
+    sklearn's cosine_distances(X, R), in sklearn's bits, on `device` (default cuda:0)."""
     dev = nat.require_gpu(device)
     Xd = torch.from_numpy(np.ascontiguousarray(X, np.float32)).to(dev)
     Rd = torch.from_numpy(np.ascontiguousarray(R, np.float32)).to(dev)
@@ -67,18 +67,25 @@ def cosine_classify_device(X, R, device=None):
     return mins.cpu().numpy(), inds.cpu().numpy()
 
 
+def cosine_distances_device(X, R, device=None):
+    """sklearn.metrics.pairwise.cosine_distances(X, R) (grouping.py:51) in sklearn's bits, [N, C]."""
+    dev = nat.require_gpu(device)
+    Xd = torch.from_numpy(np.ascontiguousarray(X, np.float32)).to(dev)
+    Rd = torch.from_numpy(np.ascontiguousarray(R, np.float32)).to(dev)
+    n, d = Xd.shape
+    dist = torch.empty((n, Rd.shape[0]), dtype=torch.float32, device=dev)
+    nat.check(nat.lib().vtf_cosine_distances_xr(nat.ptr(Xd), n, nat.ptr(Rd), Rd.shape[0], d, nat.ptr(dist),
+                                                nat.stream_ptr(dev)))
+    return dist.cpu().numpy()
+
+
 def classify(X, R, classes, thr, log, paths, out_dir, device=None):
     mins, inds = cosine_classify_device(X, R, device)
     if thr and thr != -1:
         inds[mins >= thr] = len(classes)
         classes.append('other')
     if log:
-        # the per-class distances of the CSV: the same device kernel against one class at a time
-        # (fp32 on the device; sklearn's cosine_distances rounds differently in the last bits --
-        # the CSV prints them with '%.4f', so the logged text matches wherever a value is not
-        # within ~1e-7 of a rounding boundary of the 4th decimal)
-        R = np.asarray(R, np.float32)
-        dist = np.stack([cosine_classify_device(X, R[c:c + 1], device)[0] for c in range(R.shape[0])], 1)
+        dist = cosine_distances_device(X, R, device)  # the same bits as the reference's dist
         fnames = [osp.basename(p) for p in paths]
         with open(osp.join(out_dir, 'faces', 'log_classification.csv'), 'w') as f:
             extra = '(other_threshold=%s)' % str(thr) if thr else ''
