@@ -446,6 +446,11 @@ static int conv_group_m() {
 // split factor: grids far below the CU count (FaceNet Block17/Block8, YOLO/R-CNN deep stages at
 // small batch) are split along K into up to 8 slices so ~2 workgroups land on every CU. bf16
 // (perf) mode only: the fp32 parity mode keeps the single-pass summation order.
+bool splitk_disabled() {
+    const char* e = std::getenv("VTF_NO_SPLITK");
+    return e && std::atoi(e) != 0;
+}
+
 static int pick_split(int64_t tiles, int KT, bool bf16, bool fp32_split) {
     // bf16: grids below 192 tiles; fp32 callers that accept a slice-order reduction
     // (split_fp32: ONet's dense layer, 120 tiles of K = 1152: 72 -> 51 us with the epilogue
@@ -459,7 +464,7 @@ static int pick_split(int64_t tiles, int KT, bool bf16, bool fp32_split) {
         const char* e = std::getenv("VTF_SPLIT_WG");
         return e ? std::atoi(e) : 512;
     }();
-    if (!(bf16 || fp32_split) || tiles >= (bf16 ? thr : 160) || KT < 8) return 1;
+    if (!(bf16 || fp32_split) || tiles >= (bf16 ? thr : 160) || KT < 8 || splitk_disabled()) return 1;
     int s = (int)std::min<int64_t>(8, ((bf16 ? tgt : 512) + tiles - 1) / tiles);
     s = std::min(s, KT / 4);
     return s < 2 ? 1 : s;

@@ -55,6 +55,9 @@ struct ConvParams {
 };
 
 void launch_conv(const ConvParams& p, bool bf16, hipStream_t st);
+// VTF_NO_SPLITK=1 (read per launch): no conv splits K into slices, so every output is one
+// k-ordered MFMA chain (the fused FaceNet blocks' order: the bit-identity test's reference path)
+bool splitk_disabled();
 // LDS-DMA implicit-GEMM conv (conv_dma.hip): bf16 operands, or split-pair operands (in_sp, fp32-grade)
 bool conv_dma_ok(const ConvParams& p);
 // bf16 layer -> 0 k_conv, 1 conv_dma large tiles, 2 conv_dma 64 x 64 3-stage tiles (measured per shape)

@@ -1046,7 +1046,7 @@ void launch_dma_t(ConvParams p, hipStream_t st) {
     p.dp_tiles = T;
     p.tail_split = 1;
     p.split = 1;
-    if (MODE == 0 || p.split_fp32) {
+    if ((MODE == 0 || p.split_fp32) && !splitk_disabled()) {
         if (T > slots) {
             // a last round of only a few tiles: split those along K over the free slots
             const int R = T % slots;
@@ -1106,7 +1106,7 @@ void launch_dma3_t(ConvParams p, hipStream_t st) {
     p.dp_tiles = T;
     p.tail_split = 1;
     p.split = 1;
-    if (p.split_fp32) {
+    if (p.split_fp32 && !splitk_disabled()) {
         if (T > slots) {
             const int R = T % slots;
             const int S = R > 0 ? std::min(slots / R, KT / 4) : 0;

@@ -13,7 +13,8 @@
 //   stage 4  Y[64][896] = ReLU(0.1 (B1 W_o^T + b_o) + X)            -> HBM, 7 passes of 128 channels
 // Every GEMM runs the unfused kernels' k order -- 32-deep v_mfma_f32_16x16x32_bf16 chunks in
 // ascending k from a zero accumulator -- and the same epilogue arithmetic (conv_dev.hpp
-// conv_epilogue8); the unfused launches split K on small grids, so the two paths agree to bf16
+// conv_epilogue8); the unfused launches split K on small grids (VTF_NO_SPLITK=1 turns that off: then
+// the two paths are bit-identical), so by default the two paths agree to bf16
 // rounding (identical at small batches; tests/test_facenet_gpu.py).  LDS images are padded (row
 // strides 16 B past a multiple of 256 B) so the 16 rows of a fragment read land on 16 distinct
 // bank slots.
@@ -695,8 +696,9 @@ static int cus() {
 bool launch_conv_patch(const ConvParams& q, hipStream_t st) {
     if (q.Cin != CP_CIN || q.KH != 3 || q.KW != 3 || q.sh != 1 || q.sw != 1 || q.ph != q.pw || q.ph > 1 ||
         (q.Cout != 32 && q.Cout != 64) || q.in_cstride || q.out_cstride != q.Cout || q.out_coff || q.res || q.bias ||
-        !q.alpha || !q.relu || q.n_split)
-        return false;
+        !q.alpha || !q.relu || q.n_split || q.scale != 1.f || q.leaky || q.prelu || q.gelu || q.s3 || q.res_post ||
+        q.up2 || q.res_up2 || q.out_f32 || q.f16x || q.out_sp || q.in_sp)
+        return false;  // (k_conv_patch applies only fmaf(acc, alpha, beta) then ReLU)
     CPatchP p;
     p.in = (const __bf16*)q.in;
     p.out = (__bf16*)q.out;
