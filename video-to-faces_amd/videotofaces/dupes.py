@@ -18,16 +18,17 @@ import torch
 from . import _native as nat
 
 
-def cosine_dedupe_device(X, sharded=False):
+def cosine_dedupe_device(X, sharded=False, replicated=False):
     """X: CUDA fp32 [N,D] -> (mins f32 [N], inds i64 [N]) exactly as dupes.py:60-64 computes
     them, in sklearn's bits: min / first argmin over j < i of clip(1 - cos(X_i, X_j), 0, 2);
     row 0 -> (10000, 0).  sharded=True (a collective: every rank of the default process group
     must call it with the same X, which is checked) splits the rows across the ranks
-    (cosine_dedupe_sharded)."""
+    (cosine_dedupe_sharded); replicated=True: the caller has already checked that."""
     X = X.to(torch.float32).contiguous()
     if sharded and _world() > 1:
-        from .parallel import check_replicated
-        check_replicated(X.cpu().numpy(), 'cosine_dedupe_device')
+        if not replicated:
+            from .parallel import check_replicated
+            check_replicated(X.cpu().numpy(), 'cosine_dedupe_device')
         return cosine_dedupe_sharded(X)
     return cosine_dedupe_rows(X, 0, X.shape[0])
 

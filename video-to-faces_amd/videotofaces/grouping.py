@@ -96,7 +96,7 @@ def classify(X, R, classes, thr, log, paths, out_dir, device=None):
     return inds, classes
 
 
-def cluster_sweep(X, clusters, random_state, grouper=None, device=None, sharded=False):
+def cluster_sweep(X, clusters, random_state, grouper=None, device=None, sharded=False, replicated=False):
     """KMeans + (silhouette, CH, DB) for every k in `clusters`, in order -- cluster_faces'
     loops (grouping.py:97-107).  sharded=True (a collective over the default process group:
     every rank passes the same X, which is checked) splits the work across the ranks
@@ -107,7 +107,8 @@ def cluster_sweep(X, clusters, random_state, grouper=None, device=None, sharded=
         silhouette_samples for EVERY k at once (no N x N matrix anywhere); the per-row values
         are all-gathered and averaged in row order as silhouette_score's np.mean does;
       * CH / DB by k, like the fits.
-    `grouper` defaults to the device Grouper (videotofaces.kmeans); tests pass a CPU stand-in."""
+    `grouper` defaults to the device Grouper (videotofaces.kmeans); tests pass a CPU stand-in.
+    replicated=True: the caller has already checked that every rank holds X (no digest here)."""
     import torch
     import torch.distributed as dist
     if grouper is None:
@@ -119,7 +120,8 @@ def cluster_sweep(X, clusters, random_state, grouper=None, device=None, sharded=
     rank = dist.get_rank() if world > 1 else 0
     if world > 1:
         from .parallel import all_gather_cpu, all_gather_slots, check_replicated
-        check_replicated(X, 'cluster_sweep')
+        if not replicated:
+            check_replicated(X, 'cluster_sweep')
     prep = g.prepare(X)
     K, n = len(clusters), X.shape[0]
     idx = [i for i in range(K) if i % world == rank]
