@@ -15,6 +15,7 @@ import torch  # noqa: E402
 def main():
     from videotofaces.encoders.facenet import InceptionResnetV1
     reps = int(sys.argv[1]) if len(sys.argv) > 1 else 20
+    # modes: comma-separated; a mode is '1' / '0' (VTF_FN_FUSED) or NAME=V[+NAME=V...] env settings
     modes = sys.argv[2].split(',') if len(sys.argv) > 2 else ['1', '0']
     m = InceptionResnetV1('cuda:0', precision='bf16')
     u8 = torch.from_numpy(np.random.default_rng(0).integers(0, 256, (128, 3, 160, 160), dtype=np.uint8))
@@ -22,7 +23,9 @@ def main():
     res = {}
     for rnd in range(3):
         for mode in modes:
-            os.environ['VTF_FN_FUSED'] = mode
+            for kv in (mode.split('+') if '=' in mode else ['VTF_FN_FUSED=' + mode]):
+                k, v = kv.split('=')
+                os.environ[k] = v
             m(x)
             torch.cuda.synchronize()
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -33,7 +36,8 @@ def main():
             torch.cuda.synchronize()
             res.setdefault(mode, []).append(e0.elapsed_time(e1) / reps)
     for mode, v in res.items():
-        print('VTF_FN_FUSED=%s: forward per 128 faces %s ms' % (mode, ' '.join('%.3f' % t for t in v)))
+        print('%s: forward per 128 faces %s ms' % (mode if '=' in mode else 'VTF_FN_FUSED=' + mode,
+                                                   ' '.join('%.3f' % t for t in v)))
 
 
 if __name__ == '__main__':

@@ -39,18 +39,21 @@ def test_bf16_drift_reported(g):
     assert cos.min() > 0.99
 
 
-@pytest.mark.parametrize('n', [128, 5, 1])
-def test_bf16_fused_blocks_bit_identical(n, g, monkeypatch):
+@pytest.mark.parametrize('n,split', [(128, '1'), (5, '1'), (1, '1'), (128, '0'), (5, '0')])
+def test_bf16_fused_blocks_bit_identical(n, split, g, monkeypatch):
     """The fused bf16 blocks (csrc/facenet_fused.hip: Block17 and the Block35 branches one launch
     per block with the activations in LDS, the stem's 32-channel 3x3 convs as patch convs) run the
     unfused kernels' MFMA k order and epilogue arithmetic: with the unfused launches' small-grid
     split-K turned off in both runs (VTF_NO_SPLITK=1, every output one k-ordered chain) the two
-    paths give the same embeddings bit for bit.  Both stay within the drift bar of the fp32 golden."""
+    paths give the same embeddings bit for bit.  Block17's stage 4 runs as its own GEMM launch over
+    the batch (VTF_B17_SPLIT=1, default) or inside the per-image launch (0).  Both paths stay within
+    the drift bar of the fp32 golden."""
     from videotofaces.encoders.facenet import InceptionResnetV1
     m = InceptionResnetV1('cuda:0', precision='bf16')
     u8 = torch.from_numpy(np.random.default_rng(n).integers(0, 256, (n, 3, 160, 160), dtype=np.uint8))
     x = (u8.float() - 127.5) * (1 / 128)
     monkeypatch.setenv('VTF_NO_SPLITK', '1')  # both runs: the layers outside the fused blocks too
+    monkeypatch.setenv('VTF_B17_SPLIT', split)
     fused = m(x).cpu().numpy()
     monkeypatch.setenv('VTF_FN_FUSED', '0')
     plain = m(x).cpu().numpy()

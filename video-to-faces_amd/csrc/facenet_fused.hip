@@ -101,6 +101,10 @@ __device__ inline void reg_ring(L load, C comp) {
     }
 }
 
+// HEAD: stages 1-3 only, the concat B1 [64][256] to p.y ([N][64][256]); stage 4 then runs as one
+// GEMM launch over the whole batch (facenet_runtime: all CUs share Wo instead of every image's
+// workgroup streaming it)
+template <bool HEAD>
 __global__ __launch_bounds__(256, 1) void k_block17(B17P p) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -216,6 +220,16 @@ __global__ __launch_bounds__(256, 1) void k_block17(B17P p) {
     conv7(p.wb, false, B2, B2S, 0, p.alb, p.beb, B1 + 128 * 2, B1S);
     stamp(3);
 
+    if (HEAD) {  // the concat to HBM: 64 rows x 512 B, 16-B pieces
+        char* Y = (char*)(p.y + (int64_t)img * 64 * 256);
+#pragma unroll
+        for (int u = 0; u < 8; u++) {
+            const int e = tid + 256 * u;
+            *(bf16x8*)(Y + (e >> 5) * 512 + (e & 31) * 16) = *(const bf16x8*)(B1 + (e >> 5) * B1S + (e & 31) * 16);
+        }
+        stamp(4);
+        return;
+    }
     // ---- stage 4: B1[64][256] x W_o^T + b_o, x scale, + X, ReLU -> Y; 7 passes of 128 channels
     //      (8 chunks each); two register sets: pass q + 1's weights load during pass q's MFMAs and
     //      epilogue
@@ -602,7 +616,8 @@ __global__ __launch_bounds__(256, 2) void k_conv_patch(CPatchP p) {
 // one Block17 (bf16 NHWC [N, 8, 8, 896] -> same): weights as FaceNet's layer table holds them
 void launch_block17_fused(const void* x, void* y, int N, const void* wm, const float* alm, const float* bem,
                           const void* wa, const float* ala, const float* bea, const void* wb, const float* alb,
-                          const float* beb, const void* wo, const float* bo, float scale, hipStream_t st) {
+                          const float* beb, const void* wo, const float* bo, float scale, hipStream_t st,
+                          bool head_only) {
     if (N <= 0) return;
     B17P p;
     p.x = (const __bf16*)x;
@@ -621,7 +636,8 @@ void launch_block17_fused(const void* x, void* y, int N, const void* wm, const f
     p.scale = scale;
     p.clk = nullptr;
     static bool attr = [] {
-        VTF_HIP(hipFuncSetAttribute((const void*)k_block17, hipFuncAttributeMaxDynamicSharedMemorySize, K17_LDS));
+        VTF_HIP(hipFuncSetAttribute((const void*)k_block17<false>, hipFuncAttributeMaxDynamicSharedMemorySize, K17_LDS));
+        VTF_HIP(hipFuncSetAttribute((const void*)k_block17<true>, hipFuncAttributeMaxDynamicSharedMemorySize, K17_LDS));
         return true;
     }();
     (void)attr;
@@ -631,7 +647,10 @@ void launch_block17_fused(const void* x, void* y, int N, const void* wm, const f
         VTF_HIP(hipMallocAsync((void**)&p.clk, (size_t)N * 5 * 8, st));
         hc.resize((size_t)N * 5);
     }
-    k_block17<<<N, 256, K17_LDS, st>>>(p);
+    if (head_only)
+        k_block17<true><<<N, 256, K17_LDS, st>>>(p);
+    else
+        k_block17<false><<<N, 256, K17_LDS, st>>>(p);
     VTF_HIP(hipGetLastError());
     if (p.clk) {
         VTF_HIP(hipMemcpyAsync(hc.data(), p.clk, hc.size() * 8, hipMemcpyDeviceToHost, st));

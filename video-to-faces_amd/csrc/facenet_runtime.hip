@@ -18,7 +18,8 @@ namespace vtf {
 
 void launch_block17_fused(const void* x, void* y, int N, const void* wm, const float* alm, const float* bem,
                           const void* wa, const float* ala, const float* bea, const void* wb, const float* alb,
-                          const float* beb, const void* wo, const float* bo, float scale, hipStream_t st);
+                          const float* beb, const void* wo, const float* bo, float scale, hipStream_t st,
+                          bool head_only);
 
 void launch_block35_branches(const void* x, void* cat, int N, const void* wm, const float* alm, const float* bem,
                              const void* w1, const float* al1, const float* be1, const void* w2a, const float* al2a,
@@ -30,6 +31,12 @@ bool launch_conv_patch(const ConvParams& q, hipStream_t st);
 // bf16 Block17 as one launch per block (facenet_fused.hip); VTF_FN_FUSED=0: the four launches
 static bool fused_blocks() {
     const char* e = std::getenv("VTF_FN_FUSED");  // (read per forward: tests switch it in-process)
+    return !(e && std::atoi(e) == 0);
+}
+// Block17 stage 4 (1x1 256 -> 896 + residual) as its own GEMM launch over the batch (1, default)
+// or inside the per-image launch (VTF_B17_SPLIT=0)
+static bool b17_split() {
+    const char* e = std::getenv("VTF_B17_SPLIT");
     return !(e && std::atoi(e) == 0);
 }
 
@@ -390,9 +397,13 @@ static void forward(Facenet& F, const void* x, int N, float* emb) {
                 if (e.first == li) lm = &e.second;
             VTF_CHECK(lm, VTF_E_ARG, "facenet: no merged Block17 head");
             const Layer &la = F.L[li + 2], &lb = F.L[li + 3], &lo = F.L[li + 4];
-            launch_block17_fused(X.p, Y, N, lm->w, lm->alpha, lm->beta, la.w, la.alpha, la.beta, lb.w, lb.alpha,
-                                 lb.beta, lo.w, lo.b, 0.10f, F.st);
-            li += 5;
+            const bool split = b17_split();
+            launch_block17_fused(X.p, split ? CAT : Y, N, lm->w, lm->alpha, lm->beta, la.w, la.alpha, la.beta, lb.w,
+                                 lb.alpha, lb.beta, lo.w, lo.b, 0.10f, F.st, split);
+            li += 4;
+            if (split)  // the tail: the unfused path's conv (same k order and epilogue)
+                conv(F, li, Act{CAT, X.H, X.W, 256}, N, Y, 896, 0, X.p, 0.10f, true);
+            li++;
             swap(896);
             continue;
         }

@@ -1460,7 +1460,10 @@ __global__ __launch_bounds__(256, PnLds<X || PR>::GPC) void k_pnet(const uint8_t
                             hc = __builtin_amdgcn_mfma_f32_32x32x16_f16(hw[0][s], x1h[s], hc, 0, 0, 0);
                             hc = __builtin_amdgcn_mfma_f32_32x32x16_f16(hw[1][s], x0h[s], hc, 0, 0, 0);
                         }
-                        hc = hc * 0.00048828125f;
+                        // (only registers 0..3 hold head rows -- 0..3 in lane half 0, 4, 5 in half 1;
+                        //  the rest are the zero rows >= 8 -- so only they are scaled)
+#pragma unroll
+                        for (int r = 0; r < 4; r++) hc[r] = hc[r] * 0.00048828125f;
 #pragma unroll
                         for (int s = 0; s < 2; s++)
                             hc = __builtin_amdgcn_mfma_f32_32x32x16_f16(hw[0][s], x0h[s], hc, 0, 0, 0);
@@ -1913,7 +1916,38 @@ __global__ __launch_bounds__(NT) void k_cand_front(const int3* __restrict__ sat,
         __syncthreads();
         const int npr = min(PB, P - pr0);
         bool bad = false;
-        for (int i = tid; i < ((dbg & 4) ? 0 : npr * P * 32); i += NT) {
+        if (ovf) {
+            // split-pair output (gemm_x3.hpp: 32-B chunks [x0 x 8 | x1 x 8] of 8 channels): one
+            // thread per (pooled position, 8-channel chunk), two 16-B stores
+            for (int i = tid; i < ((dbg & 4) ? 0 : npr * P * 4); i += NT) {
+                const int cg = i & 3, t = i >> 2;
+                const int px = t % P, pyl = t / P;
+                int xo[3], yo[3];
+#pragma unroll
+                for (int d = 0; d < 3; d++) {
+                    xo[d] = min(2 * px + d, O - 1);
+                    yo[d] = (min(2 * (pr0 + pyl) + d, O - 1) % BR) * O;
+                }
+                f16x8 h0, h1;
+#pragma unroll
+                for (int c8 = 0; c8 < 8; c8++) {
+                    const float* cr = cv + (8 * cg + c8) * CS;
+                    float m = cr[yo[0] + xo[0]];
+#pragma unroll
+                    for (int dy = 0; dy < 3; dy++)
+#pragma unroll
+                        for (int dx = 0; dx < 3; dx++)
+                            if (dy | dx) m = fmaxf(m, cr[yo[dy] + xo[dx]]);
+                    h0[c8] = (_Float16)m;
+                    h1[c8] = (_Float16)((m - (float)h0[c8]) * 2048.f);
+                    bad |= !(fabsf(m) < 16384.f);
+                }
+                f16x8* ch = (f16x8*)(o + ((pr0 + pyl) * P + px) * 32 + 8 * cg);
+                ch[0] = h0;
+                ch[1] = h1;
+            }
+        }
+        for (int i = tid; i < ((dbg & 4) || ovf ? 0 : npr * P * 32); i += NT) {
             const int c = i & 31, t = i >> 5;
             const int px = t % P, pyl = t / P;
             // ceil-mode windows clipped at the map edge: a clipped index is clamped onto the

@@ -136,7 +136,14 @@ struct Mtcnn {
     // RNet / ONet on the LDS-DMA conv kernel's split mode with split-pair activations
     // (VTF_MTCNN_SP=0: k_conv's staging-split mode)
     bool sp = true;
+    // VTF_PNET_PRIO=1: k_pnet on a lowest-priority stream of this handle (the other lanes' stage-2/3
+    // and encoder kernels are dispatched ahead of its workgroups); joined back by events
+    hipStream_t pst = nullptr;
+    hipEvent_t pev[2] = {nullptr, nullptr};
     ~Mtcnn() {
+        if (pst) (void)hipStreamDestroy(pst);
+        for (hipEvent_t e : pev)
+            if (e) (void)hipEventDestroy(e);
         for (void* p : allocs) (void)hipFree(p);
         if (ev0) (void)hipEventDestroy(ev0);
         if (ev1) (void)hipEventDestroy(ev1);
@@ -911,13 +918,29 @@ static void detect(Mtcnn& m, const uint8_t* frames, int on_dev, int B, int H, in
     if (po.dbg & 256) po.clk = m.ar.get<unsigned long long>(S_CLK, 16);
     if (po.clk) VTF_HIP(hipMemsetAsync(po.clk, 0, 128, st));
     const int64_t x_tiles = pnet_exact_tiles(lv, H, W, tiles);
-    if (m.prof) VTF_HIP(hipEventRecord(m.ev0, st));
-    launch_pnet(false, fr, fstride, rstride, H, W, d_lv, NL, tiles, m.pw, po, d_cnt + NL + 1, st,
+    static const bool lowprio = [] {
+        const char* e = std::getenv("VTF_PNET_PRIO");
+        return e && std::atoi(e) != 0;
+    }();
+    hipStream_t pst = st;
+    if (lowprio) {
+        if (!m.pst) {
+            int lo = 0, hi = 0;
+            VTF_HIP(hipDeviceGetStreamPriorityRange(&lo, &hi));
+            VTF_HIP(hipStreamCreateWithPriority(&m.pst, hipStreamNonBlocking, lo));
+            VTF_HIP(hipEventCreateWithFlags(&m.pev[0], hipEventDisableTiming));
+        }
+        pst = m.pst;
+        VTF_HIP(hipEventRecord(m.pev[0], st));
+        VTF_HIP(hipStreamWaitEvent(pst, m.pev[0], 0));
+    }
+    if (m.prof) VTF_HIP(hipEventRecord(m.ev0, pst));
+    launch_pnet(false, fr, fstride, rstride, H, W, d_lv, NL, tiles, m.pw, po, d_cnt + NL + 1, pst,
                 x_tiles, pnet_pre_from(lv, tiles));
-    if (m.prof) VTF_HIP(hipEventRecord(m.ev1, st));
+    if (m.prof) VTF_HIP(hipEventRecord(m.ev1, pst));
     Arena::Mail mc = m.ar.mail(M_COUNT, (size_t)(NL + 1) * 4);
-    k_mail_u32<<<1, 256, 0, st>>>(d_cnt, (uint32_t*)mc.d, NL + 1);
-    VTF_HIP(hipStreamSynchronize(st));
+    k_mail_u32<<<1, 256, 0, pst>>>(d_cnt, (uint32_t*)mc.d, NL + 1);
+    VTF_HIP(hipStreamSynchronize(pst));  // (the host sync joins pst back: st's later work follows it)
     std::vector<uint32_t> cnt((const uint32_t*)mc.h, (const uint32_t*)mc.h + NL + 1);
     if (po.clk) {  // debug: average workgroup clocks per tile and phase (k_pnet mark() points)
         unsigned long long c[16];

@@ -36,7 +36,7 @@ namespace vtf {
 __global__ void k_nms_prep(const uint8_t* __restrict__ mail, uint8_t* __restrict__ tables, int bytes,
                            const float4* __restrict__ boxes, size_t o_cbeg, size_t o_cn, size_t o_van, size_t o_trick,
                            int C, float* __restrict__ call_max, int32_t* __restrict__ ovf_flag,
-                           int32_t* __restrict__ seg_ctr, int n_ctr) {
+                           int32_t* __restrict__ seg_ctr, int n_ctr, int32_t* __restrict__ dtie) {
     if (blockIdx.x == 0) {
         if (threadIdx.x == 0) *ovf_flag = 0;
         for (int i = threadIdx.x; i < n_ctr; i += blockDim.x) seg_ctr[i] = 0;  // segment counters
@@ -48,6 +48,7 @@ __global__ void k_nms_prep(const uint8_t* __restrict__ mail, uint8_t* __restrict
         for (int c = threadIdx.x; c < C; c += blockDim.x) {
             if (van[c] || cn[c] == 0) call_max[c] = 0.f;
             ovf_flag[1 + c] = 0;  // tie flags
+            dtie[c] = 0;          // (device copy)
         }
         return;
     }
@@ -638,13 +639,17 @@ __global__ __launch_bounds__(256) void k_nms_out(const uint64_t* __restrict__ kl
                                                  const int64_t* __restrict__ sstart, const uint32_t* __restrict__ seg_hi,
                                                  const int32_t* __restrict__ seg_base, int sbits, int n_img,
                                                  const uint8_t* __restrict__ van, int S, int C, int64_t N,
-                                                 int32_t* __restrict__ keep, int32_t* __restrict__ res) {
+                                                 int32_t* __restrict__ keep, int32_t* __restrict__ res,
+                                                 int32_t* __restrict__ coff, int32_t* __restrict__ dtie) {
     extern __shared__ int32_t koff[];  // [S + 1]
     __shared__ int32_t part[256];
     const int tid = threadIdx.x, g = tid & (OUT_G - 1);
     block_prefix<256>(kcnt, S, koff, part);
     if (blockIdx.x == 0)
-        for (int c = tid; c < C; c += 256) res[c] = koff[seg_base[c + 1]] - koff[seg_base[c]];
+        for (int c = tid; c <= C; c += 256) {
+            if (c < C) res[c] = koff[seg_base[c + 1]] - koff[seg_base[c]];
+            coff[c] = koff[seg_base[c]];  // the call's first output position (device copy)
+        }
     const int64_t p = ((int64_t)blockIdx.x * 256 + tid) / OUT_G;  // this lane group's element
     if (p >= N) return;  // (uniform over the group)
     int lo = 0, hi = S - 1;  // last segment starting at or before p
@@ -684,8 +689,35 @@ __global__ __launch_bounds__(256) void k_nms_out(const uint64_t* __restrict__ kl
     if (g == 0) {
         tie |= i > 0 && (klist[p - 1] >> 32) == (key >> 32);
         keep[koff[s0] + i + rank] = (int32_t)(uint32_t)key;
-        if (tie) res[C + 1 + c] = 1;
+        if (tie) res[C + 1 + c] = 1, dtie[c] = 1;
     }
+}
+
+// The outputs of the calls with equal kept scores (dtie) -> the host mailbox as (element, score)
+// pairs: the host reorders them like torch's unstable sort after the call's one sync, and
+// k_tie_import writes the order back (no runtime blit copy, no extra sync).
+__device__ inline int call_of_output(const int32_t* __restrict__ coff, int C, int q) {
+    int lo = 0, hi = C - 1;  // last call starting at or before q
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (coff[mid] <= q) lo = mid; else hi = mid - 1;
+    }
+    return lo;
+}
+__global__ void k_tie_export(const int32_t* __restrict__ keep, const float* __restrict__ scores,
+                             const int32_t* __restrict__ coff, const int32_t* __restrict__ dtie, int C,
+                             int2* __restrict__ mail) {
+    const int q = blockIdx.x * blockDim.x + threadIdx.x;
+    if (q >= coff[C]) return;
+    if (!dtie[call_of_output(coff, C, q)]) return;
+    const int32_t e = keep[q];
+    mail[q] = make_int2(e, __float_as_int(scores[e]));
+}
+__global__ void k_tie_import(const int32_t* __restrict__ mail, const int32_t* __restrict__ coff,
+                             const int32_t* __restrict__ dtie, int C, int32_t* __restrict__ keep) {
+    const int q = blockIdx.x * blockDim.x + threadIdx.x;
+    if (q >= coff[C]) return;
+    if (dtie[call_of_output(coff, C, q)]) keep[q] = mail[q];
 }
 
 // host staging of several small tables for one H2D copy (16-B aligned members)
@@ -813,9 +845,11 @@ void nms_multi(Arena& ar, const float* d_boxes, const float* d_scores, const int
     for (int c = 0; c < C; c++) segbound = std::max(segbound, call_n[c]);
     const bool lds_sort = segbound <= NMS_SORT_BOUND;
     int32_t* d_sctr = ar.get<int32_t>(45, 2 * (size_t)S);
+    int32_t* d_tie = ar.get<int32_t>(44, (size_t)2 * C + 1);  // [C] tie flags, [C + 1] call output offsets
+    int32_t* d_coff = d_tie + C;
     k_nms_prep<<<1 + (int)trick.size(), 256, 0, st>>>((const uint8_t*)mt.d, d_t1, tbytes, (const float4*)d_boxes, o_cbeg,
                                                       o_cn, o_van, o_trick, C, d_cmax, d_res + C, d_sctr,
-                                                      lds_sort ? 2 * S : 0);
+                                                      lds_sort ? 2 * S : 0, d_tie);
 
     // sort 1: (call, segment image, score desc), stable over position order -> ck (desc score key |
     // element index) and ord (element index), segment starts
@@ -894,27 +928,49 @@ void nms_multi(Arena& ar, const float* d_boxes, const float* d_scores, const int
     }
     // output order, kept counts and vanilla tie flags in one launch
     k_nms_out<<<cdiv(N * OUT_G, 256), 256, (size_t)(S + 1) * 4, st>>>(d_klist, d_kcnt, d_sstart, d_seghi, d_sbase, sbits, n_img,
-                                                              d_van, S, C, N, d_keep, d_res);
+                                                              d_van, S, C, N, d_keep, d_res, d_coff, d_tie);
     bool any_van = false;
     for (int c = 0; c < C; c++) any_van |= vanilla[c] != 0;
+    int2* h_pairs = nullptr;
+    int32_t* d_fix = nullptr;
+    if (any_van) {  // flagged calls' outputs to the host, in the same sync
+        Arena::Mail mp = ar.mail(42, (size_t)N * 8);
+        Arena::Mail mf = ar.mail(43, (size_t)N * 4);
+        h_pairs = (int2*)mp.h;
+        d_fix = (int32_t*)mf.d;
+        k_tie_export<<<cdiv(N, 256), 256, 0, st>>>(d_keep, d_scores, d_coff, d_tie, C, (int2*)mp.d);
+        VTF_HIP(hipGetLastError());
+    }
     VTF_HIP(hipStreamSynchronize(st));
     VTF_CHECK(h_res[C] == 0, VTF_E_LIMIT, "nms_multi: a segment exceeds 1.3M boxes");
     for (int c = 0; c < C; c++) nkeep[c] = h_res[c];
-    // torch's unstable final sort on the (rare) vanilla calls with equal kept scores
+    // torch's unstable final sort on the vanilla calls with equal kept scores: reordered on the host
+    // from the exported pairs, written back by k_tie_import (queued, no sync)
+    bool fixed = false;
     int64_t off = 0;
     for (int c = 0; c < C; c++) {
         if (any_van && h_res[C + 1 + c] && nkeep[c] > 1) {
+            std::vector<std::pair<int32_t, float>> ps(nkeep[c]);
+            for (int64_t t = 0; t < nkeep[c]; t++) ps[t] = {h_pairs[off + t].x, __builtin_bit_cast(float, h_pairs[off + t].y)};
+            std::sort(ps.begin(), ps.end(), [](const std::pair<int32_t, float>& a, const std::pair<int32_t, float>& b) {
+                return a.first < b.first;
+            });
             std::vector<int32_t> hk(nkeep[c]);
-            std::vector<float> hs(call_n[c]);
-            VTF_HIP(hipMemcpyAsync(hk.data(), d_keep + off, nkeep[c] * 4, hipMemcpyDeviceToHost, st));
-            VTF_HIP(hipMemcpyAsync(hs.data(), d_scores + call_beg[c], call_n[c] * 4, hipMemcpyDeviceToHost, st));
-            VTF_HIP(hipStreamSynchronize(st));
-            const int64_t b = call_beg[c];
-            torch_unstable_desc_order(hk, [&](int32_t e) { return hs[e - b]; });
-            VTF_HIP(hipMemcpyAsync(d_keep + off, hk.data(), nkeep[c] * 4, hipMemcpyHostToDevice, st));
-            VTF_HIP(hipStreamSynchronize(st));
+            for (int64_t t = 0; t < nkeep[c]; t++) hk[t] = ps[t].first;
+            torch_unstable_desc_order(hk, [&](int32_t e) {
+                return std::lower_bound(ps.begin(), ps.end(), e, [](const std::pair<int32_t, float>& a, int32_t v) {
+                           return a.first < v;
+                       })->second;
+            });
+            int32_t* h_fix = (int32_t*)ar.mptr[43].h;
+            std::memcpy(h_fix + off, hk.data(), hk.size() * 4);
+            fixed = true;
         }
         off += nkeep[c];
+    }
+    if (fixed) {
+        k_tie_import<<<cdiv(off, 256), 256, 0, st>>>(d_fix, d_coff, d_tie, C, d_keep);
+        VTF_HIP(hipGetLastError());
     }
 }
 
