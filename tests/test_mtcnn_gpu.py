@@ -255,3 +255,20 @@ def test_span_pool_fusion_matches_separate_pool(ms, monkeypatch):
     assert sum(x.shape[0] for x in a) > 0
     for x, y in zip(a, b):
         np.testing.assert_allclose(x, y, rtol=1e-5, atol=2e-3)
+
+
+@pytest.mark.parametrize('ms', [5, 20])
+def test_wave_front_bit_identical(ms, monkeypatch):
+    """The RNet candidate front as one wave per candidate (k_cand_front_w24, default) against one
+    workgroup per candidate (VTF_FRONT_WAVE=0): the same crop bins, conv1 MFMA chains, PReLU, pool
+    and split, so the detections are identical bit for bit."""
+    from videotofaces import synth
+    from videotofaces.detectors.mtcnn import MTCNN
+    fr = torch.from_numpy(synth.make_frames(4, seed=31)).cuda()
+    m = MTCNN('cuda:0')
+    a = m(fr, ms)
+    monkeypatch.setenv('VTF_FRONT_WAVE', '0')
+    b = m(fr, ms)
+    assert sum(x.shape[0] for x in a) > 0
+    for x, y in zip(a, b):
+        np.testing.assert_array_equal(x, y)

@@ -57,6 +57,7 @@ struct ResampleLevels {  // precomputed pyramid levels of one det-batch (k_resam
     int split;  // 1: [B][lh][lw] fp16 split pixels (x0 RGB | x1 RGB, 12 B), else fp32 [B][3][lh][lw]
     int lh[MAXL], lw[MAXL];
     int64_t beg[MAXL + 1];  // first output element (b, y, x) of each level in the flattened grid
+    int64_t tbeg[MAXL + 1]; // first 2-D tile of each level (k_resample_sat_multi's grid; set by the launcher)
     float* out[MAXL];       // [B][3][lh][lw]
 };
 void launch_resample_sat_multi(const int3* sat, int B, int H, int W, const ResampleLevels& lv, hipStream_t st);

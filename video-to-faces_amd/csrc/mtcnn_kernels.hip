@@ -208,41 +208,61 @@ void launch_resample_sat(const int3* sat, int B, int H, int W, int lh, int lw, f
     k_resample_sat<<<cdiv(n, 256), 256, 0, st>>>(sat, B, H, W, lh, lw, out);
 }
 
-// every precomputed level of a det-batch in one launch (the small levels alone are launch-bound)
-__global__ void k_resample_sat_multi(const int3* __restrict__ sat, int B, int H, int W, ResampleLevels lv) {
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= lv.beg[lv.n]) return;
+// every precomputed level of a det-batch in one launch (the small levels alone are launch-bound).
+// A workgroup takes a 2-D tile of RS_TH level rows x RS_TW pixels (each thread two pixels, rows r
+// and r + RS_TH / 2): the SAT rows a level row's bins end on are the next row's bin starts, and
+// corner columns repeat between neighbours, so a tile's corner reads come from the workgroup's own
+// L1 / its XCD's L2 instead of HBM (a row-major strip of 256 pixels per workgroup put the next
+// level row on another XCD: 960 MB fetched per det-batch for 260 MB of output)
+constexpr int RS_TH = 8, RS_TW = 64;
+__global__ __launch_bounds__(256) void k_resample_sat_multi(const int3* __restrict__ sat, int B, int H, int W,
+                                                            ResampleLevels lv) {
+    const int64_t bid = blockIdx.x;
     int l = 0;
-    while (l + 1 < lv.n && i >= lv.beg[l + 1]) l++;
+    while (l + 1 < lv.n && bid >= lv.tbeg[l + 1]) l++;
     const int lh = lv.lh[l], lw = lv.lw[l];
-    const int64_t j = i - lv.beg[l];
-    const int lx = (int)(j % lw);
-    const int ly = (int)((j / lw) % lh);
-    const int b = (int)(j / ((int64_t)lw * lh));
-    const int y0 = (int)(((int64_t)ly * H) / lh), y1 = (int)(((int64_t)(ly + 1) * H + lh - 1) / lh);
+    const int txn = (lw + RS_TW - 1) / RS_TW, tyn = (lh + RS_TH - 1) / RS_TH;
+    const int64_t t = bid - lv.tbeg[l];
+    const int b = (int)(t / ((int64_t)txn * tyn));
+    const int tt = (int)(t - (int64_t)b * txn * tyn);
+    const int ty = tt / txn, tx = tt - ty * txn;
+    const int lx = tx * RS_TW + (threadIdx.x & (RS_TW - 1));
     const int x0 = (int)(((int64_t)lx * W) / lw), x1 = (int)(((int64_t)(lx + 1) * W + lw - 1) / lw);
-    const int4 s = sat_box(sat + (int64_t)b * (H + 1) * (W + 1), W + 1, y0, y1, x0, x1);
-    if (lv.split) {  // fp16 split pixels [B][lh][lw] x (x0 RGB | x1 RGB), k_pnet's level-tile halves
-        _Float16 r0, r1, g0, g1, b0, b1;
-        split_f16(bin_avg(s.x, y1 - y0, x1 - x0), r0, r1);
-        split_f16(bin_avg(s.y, y1 - y0, x1 - x0), g0, g1);
-        split_f16(bin_avg(s.z, y1 - y0, x1 - x0), b0, b1);
-        // 12 bytes (no pad halves): r0 g0 | b0 r1 | g1 b1
-        auto hb = [](_Float16 h) { return (uint32_t)__builtin_bit_cast(uint16_t, h); };
-        ((uint3*)lv.out[l])[j] = make_uint3(hb(r0) | hb(g0) << 16, hb(b0) | hb(r1) << 16, hb(g1) | hb(b1) << 16);
-        return;
+    const int3* sb = sat + (int64_t)b * (H + 1) * (W + 1);
+#pragma unroll
+    for (int h = 0; h < 2; h++) {
+        const int ly = ty * RS_TH + (threadIdx.x >> 6) + h * (RS_TH / 2);
+        if (ly >= lh || lx >= lw) continue;
+        const int64_t j = ((int64_t)b * lh + ly) * lw + lx;
+        const int y0 = (int)(((int64_t)ly * H) / lh), y1 = (int)(((int64_t)(ly + 1) * H + lh - 1) / lh);
+        const int4 s = sat_box(sb, W + 1, y0, y1, x0, x1);
+        if (lv.split) {  // fp16 split pixels [B][lh][lw] x (x0 RGB | x1 RGB), k_pnet's level-tile halves
+            _Float16 r0, r1, g0, g1, b0, b1;
+            split_f16(bin_avg(s.x, y1 - y0, x1 - x0), r0, r1);
+            split_f16(bin_avg(s.y, y1 - y0, x1 - x0), g0, g1);
+            split_f16(bin_avg(s.z, y1 - y0, x1 - x0), b0, b1);
+            // 12 bytes (no pad halves): r0 g0 | b0 r1 | g1 b1
+            auto hb = [](_Float16 q) { return (uint32_t)__builtin_bit_cast(uint16_t, q); };
+            ((uint3*)lv.out[l])[j] = make_uint3(hb(r0) | hb(g0) << 16, hb(b0) | hb(r1) << 16, hb(g1) | hb(b1) << 16);
+            continue;
+        }
+        const int64_t plane = (int64_t)lh * lw, o = (int64_t)b * 3 * plane + (int64_t)ly * lw + lx;
+        float* out = lv.out[l];
+        out[o] = bin_avg(s.x, y1 - y0, x1 - x0);
+        out[o + plane] = bin_avg(s.y, y1 - y0, x1 - x0);
+        out[o + 2 * plane] = bin_avg(s.z, y1 - y0, x1 - x0);
     }
-    const int64_t plane = (int64_t)lh * lw, o = (int64_t)b * 3 * plane + (int64_t)ly * lw + lx;
-    float* out = lv.out[l];
-    out[o] = bin_avg(s.x, y1 - y0, x1 - x0);
-    out[o + plane] = bin_avg(s.y, y1 - y0, x1 - x0);
-    out[o + 2 * plane] = bin_avg(s.z, y1 - y0, x1 - x0);
 }
 
-void launch_resample_sat_multi(const int3* sat, int B, int H, int W, const ResampleLevels& lv, hipStream_t st) {
-    VTF_CHECK(lv.n >= 0 && lv.n <= ResampleLevels::MAXL, VTF_E_LIMIT, "mtcnn: too many precomputed levels");
-    if (lv.n == 0 || lv.beg[lv.n] == 0) return;
-    k_resample_sat_multi<<<cdiv(lv.beg[lv.n], 256), 256, 0, st>>>(sat, B, H, W, lv);
+void launch_resample_sat_multi(const int3* sat, int B, int H, int W, const ResampleLevels& lv0, hipStream_t st) {
+    VTF_CHECK(lv0.n >= 0 && lv0.n <= ResampleLevels::MAXL, VTF_E_LIMIT, "mtcnn: too many precomputed levels");
+    if (lv0.n == 0 || lv0.beg[lv0.n] == 0) return;
+    ResampleLevels lv = lv0;
+    lv.tbeg[0] = 0;
+    for (int l = 0; l < lv.n; l++)
+        lv.tbeg[l + 1] = lv.tbeg[l] + (int64_t)B * ((lv.lh[l] + RS_TH - 1) / RS_TH) * ((lv.lw[l] + RS_TW - 1) / RS_TW);
+    VTF_CHECK(lv.tbeg[lv.n] < (int64_t)1 << 31, VTF_E_LIMIT, "mtcnn: resample grid too large");
+    k_resample_sat_multi<<<(unsigned)lv.tbeg[lv.n], 256, 0, st>>>(sat, B, H, W, lv);
 }
 
 // ----------------------------------------------------------------------------------- PNet
@@ -1983,7 +2003,173 @@ __global__ __launch_bounds__(NT) void k_cand_front(const int3* __restrict__ sat,
     }
 }
 
+// RNet front (S = 24) as one WAVE per candidate, NWV candidates per workgroup, each wave on its own
+// LDS slices with no workgroup barrier: the one-workgroup-per-candidate kernel above spends most of
+// its ~46k cycles per candidate in dependent phases (box -> SAT gathers -> 4 bands of conv / pool,
+// 8 barriers) that the few workgroups per CU do not overlap.  Same arithmetic, bit for bit: the
+// crop's bin averages, conv1 on the split-fp16 16x16x32 MFMA chains (k_pnet conv1's K layout,
+// cross terms 2^-11-scaled into the main chain), PReLU, the clamped ceil-mode 3x3/2 max-pool, the
+// split-pair output and the fp16-range flag.  Conv rows go to a ring of 3 rows per channel (slot =
+// row % 3); pooled row py needs conv rows 2 py .. 2 py + 2.
+__device__ inline void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+template <int NWV>
+__global__ __launch_bounds__(64 * NWV) void k_cand_front_w24(const int3* __restrict__ sat, int H, int W,
+                                                             const float4* __restrict__ boxes,
+                                                             const int32_t* __restrict__ img, int64_t n,
+                                                             const _Float16* __restrict__ w1h,
+                                                             const float* __restrict__ b1, const float* __restrict__ a1,
+                                                             float* __restrict__ out, int32_t* __restrict__ err,
+                                                             int* __restrict__ ovf) {
+    constexpr int S = 24, O = S - 2, P = (O - 3 + 1) / 2 + 1;  // 22, 11
+    constexpr int CS = (3 * O) | 1;                             // ring channel stride (odd: 32 banks)
+    typedef __attribute__((ext_vector_type(4))) _Float16 h4;
+    __shared__ h4 crop_s[NWV][2][S * S + 1];
+    __shared__ float cv_s[NWV][32 * CS];
+    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63, lr = lane & 15, lk = lane >> 4;
+    const int64_t k = (int64_t)blockIdx.x * NWV + wv;
+    if (k >= n) return;  // (wave-uniform; no workgroup barrier below)
+    h4* cp0 = crop_s[wv][0];
+    h4* cp1 = crop_s[wv][1];
+    float* cv = cv_s[wv];
+    float* o = out + k * (P * P * 32);
+    int y0, x0, hc, wc;
+    if (!crop_rect(boxes[k], H, W, y0, x0, hc, wc)) {
+        if (lane == 0) atomicAdd(err, 1);
+        for (int i = lane; i < P * P * 32; i += 64) o[i] = 0.f;
+        return;
+    }
+    const bool exact = hc <= S && wc <= S;
+    if (lane == 0) {
+        const h4 z = {(_Float16)0.f, (_Float16)0.f, (_Float16)0.f, (_Float16)0.f};
+        cp0[S * S] = z;
+        cp1[S * S] = z;
+    }
+    // crop: 9 pixels per lane in 3 rounds of 3 (12 SAT corner loads in flight per round)
+    const int3* sk = sat + (int64_t)img[k] * (H + 1) * (W + 1);
+#pragma unroll
+    for (int rd = 0; rd < 3; rd++) {
+        int3 cn[3][4];
+        int kh[3], kw[3];
+#pragma unroll
+        for (int j = 0; j < 3; j++) {
+            const int i = lane + 64 * (3 * rd + j);
+            const int r = i / S, q = i - r * S;
+            const int ys = (r * hc) / S, ye = ((r + 1) * hc + S - 1) / S;
+            const int xs = (q * wc) / S, xe = ((q + 1) * wc + S - 1) / S;
+            kh[j] = ye - ys;
+            kw[j] = xe - xs;
+            const int3* a = sk + (int64_t)(y0 + ys) * (W + 1) + x0;
+            const int3* b = sk + (int64_t)(y0 + ye) * (W + 1) + x0;
+            cn[j][0] = a[xs];
+            cn[j][1] = a[xe];
+            cn[j][2] = b[xs];
+            cn[j][3] = b[xe];
+        }
+#pragma unroll
+        for (int j = 0; j < 3; j++) {
+            const int i = lane + 64 * (3 * rd + j);
+            const int3 &a = cn[j][0], &b = cn[j][1], &c = cn[j][2], &d = cn[j][3];
+            _Float16 r0, r1, g0, g1, c0, c1;
+            split_f16(bin_avg(d.x - b.x - c.x + a.x, kh[j], kw[j]), r0, r1);
+            split_f16(bin_avg(d.y - b.y - c.y + a.y, kh[j], kw[j]), g0, g1);
+            split_f16(bin_avg(d.z - b.z - c.z + a.z, kh[j], kw[j]), c0, c1);
+            cp0[i] = h4{r0, g0, c0, (_Float16)0.f};
+            if (!exact) cp1[i] = h4{r1, g1, c1, (_Float16)0.f};
+        }
+    }
+    // conv1 weights: split planes [2][32][64] as the B operand, channel block nb = co / 16
+    f16x8 wh0[2][2], wh1[2][2];
+#pragma unroll
+    for (int s2 = 0; s2 < 2; s2++)
+#pragma unroll
+        for (int nb = 0; nb < 2; nb++) {
+            const _Float16* src = w1h + (16 * nb + lr) * 64 + 32 * s2 + 8 * lk;
+            wh0[s2][nb] = *(const f16x8*)src;
+            wh1[s2][nb] = *(const f16x8*)(src + 32 * 64);
+        }
+    const float bb0 = b1[lr], bb1 = b1[16 + lr], aa0 = a1[lr], aa1 = a1[16 + lr];
+    wave_sync();
+    const _Float16* c0p = (const _Float16*)cp0;
+    bool bad = false;
+    for (int py = 0; py < P; py++) {
+        // conv rows [r_lo, r_hi] into the ring (row 2 py is the previous pooled row's last)
+        const int r_lo = py == 0 ? 0 : 2 * py + 1, r_hi = min(2 * py + 2, O - 1);
+        const int npos = (r_hi - r_lo + 1) * O;
+        for (int f = 0; f * 16 < npos; f++) {
+            const int p = min(f * 16 + lr, npos - 1);
+            const int y = r_lo + p / O, x = p % O;
+            f32x4 c0 = {0.f, 0.f, 0.f, 0.f}, c1 = c0, d0 = c0, d1 = c0;
+#pragma unroll
+            for (int s2 = 0; s2 < 2; s2++) {
+                const int ky = min(2 * s2 + (lk >> 1), 2);
+                const int pix = (y + ky) * S + x + 2 * (lk & 1);
+                const f16x8 xa = ld_h8(c0p + pix * 4);
+                c0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(xa, wh0[s2][0], c0, 0, 0, 0);
+                c1 = __builtin_amdgcn_mfma_f32_16x16x32_f16(xa, wh0[s2][1], c1, 0, 0, 0);
+                d0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(xa, wh1[s2][0], d0, 0, 0, 0);
+                d1 = __builtin_amdgcn_mfma_f32_16x16x32_f16(xa, wh1[s2][1], d1, 0, 0, 0);
+                if (!exact) {
+                    const f16x8 xb = ld_h8(c0p + (S * S + 1) * 4 + pix * 4);
+                    d0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(xb, wh0[s2][0], d0, 0, 0, 0);
+                    d1 = __builtin_amdgcn_mfma_f32_16x16x32_f16(xb, wh0[s2][1], d1, 0, 0, 0);
+                }
+            }
+#pragma unroll
+            for (int i = 0; i < 4; i++) {
+                const int q = f * 16 + 4 * lk + i;
+                if (q < npos) {
+                    const int yq = r_lo + q / O;
+                    const int slot = (yq % 3) * O + (q - (yq - r_lo) * O);
+                    cv[lr * CS + slot] = prelu(__builtin_fmaf(d0[i], 0.00048828125f, c0[i]) + bb0, aa0);
+                    cv[(16 + lr) * CS + slot] = prelu(__builtin_fmaf(d1[i], 0.00048828125f, c1[i]) + bb1, aa1);
+                }
+            }
+        }
+        wave_sync();
+        // pooled row py: 11 columns x 4 chunks of 8 channels (44 lanes), split-pair 32-B chunks
+        if (lane < P * 4) {
+            const int cg = lane & 3, px = lane >> 2;
+            int xo[3], yo[3];
+#pragma unroll
+            for (int d = 0; d < 3; d++) {
+                xo[d] = min(2 * px + d, O - 1);
+                yo[d] = (min(2 * py + d, O - 1) % 3) * O;
+            }
+            f16x8 h0, h1;
+#pragma unroll
+            for (int c8 = 0; c8 < 8; c8++) {
+                const float* cr = cv + (8 * cg + c8) * CS;
+                float m = cr[yo[0] + xo[0]];
+#pragma unroll
+                for (int dy = 0; dy < 3; dy++)
+#pragma unroll
+                    for (int dx = 0; dx < 3; dx++)
+                        if (dy | dx) m = fmaxf(m, cr[yo[dy] + xo[dx]]);
+                h0[c8] = (_Float16)m;
+                h1[c8] = (_Float16)((m - (float)h0[c8]) * 2048.f);
+                bad |= !(fabsf(m) < 16384.f);
+            }
+            f16x8* ch = (f16x8*)(o + (py * P + px) * 32 + 8 * cg);
+            ch[0] = h0;
+            ch[1] = h1;
+        }
+        wave_sync();  // the ring rows are rewritten by the next pooled row
+    }
+    if (__ballot(bad) && lane == 0) atomicOr(ovf, 1);
+}
+
 int cand_front_side(bool onet) { return onet ? 23 : 11; }
+
+// RNet front as one wave per candidate (1, default) or one workgroup per candidate (VTF_FRONT_WAVE=0);
+// read per launch (the tests run both)
+static bool wave_front() {
+    const char* e = std::getenv("VTF_FRONT_WAVE");
+    return !(e && std::atoi(e) == 0);
+}
 
 void launch_cand_front(bool onet, const int3* sat, int H, int W, const float4* boxes, const int32_t* img, int64_t n,
                        const float* w1, const _Float16* w1h, const float* b1, const float* a1, float* out, int32_t* err,
@@ -2007,6 +2193,8 @@ void launch_cand_front(bool onet, const int3* sat, int H, int W, const float4* b
         k_cand_front<48, 1, 512, true><<<(unsigned)n, 512, 0, st>>>(sat, H, W, boxes, img, w1, w1h, b1, a1, out, err, dbg, ovf);
     else if (onet)
         k_cand_front<48, 1, 512, false><<<(unsigned)n, 512, 0, st>>>(sat, H, W, boxes, img, w1, w1h, b1, a1, out, err, dbg, ovf);
+    else if (w1h && ovf && wave_front() && !dbg)
+        k_cand_front_w24<4><<<(unsigned)cdiv(n, 4), 256, 0, st>>>(sat, H, W, boxes, img, n, w1h, b1, a1, out, err, ovf);
     else if (w1h)
         k_cand_front<24, 3, 256, true><<<(unsigned)n, 256, 0, st>>>(sat, H, W, boxes, img, w1, w1h, b1, a1, out, err, dbg, ovf);
     else
