@@ -33,6 +33,12 @@ import sys
 import threading
 import time
 
+# Four det-batch lanes (streams) per GPU, each on its own hardware queue: HIP maps a process's
+# streams onto GPU_MAX_HW_QUEUES queues (4 by default), so the fourth lane would share one.  Set
+# before anything initialises HIP; a value in the environment wins.  (c2, one box, default run:
+# 3 lanes 9,778 / 9,804 faces/s, 4 lanes on 8 queues 10,109 / 10,137; profiles/r05ln2_lanes_ab.txt)
+os.environ.setdefault('GPU_MAX_HW_QUEUES', '8')
+
 ROOT = os.path.dirname(os.path.abspath(__file__))
 for _p in (ROOT, os.path.join(ROOT, 'video-to-faces_amd')):
     if _p not in sys.path:
@@ -82,7 +88,7 @@ def parse(argv=None):
     ap.add_argument('--pool', type=int, default=None,
                     help='distinct synthetic frames of the global frame sequence, cycled (default 32; c5: 0 = '
                          'every frame of the run distinct, generated on the device)')
-    ap.add_argument('--lanes', type=int, default=3, help='concurrent det-batch pipelines (threads + HIP streams) per GPU')
+    ap.add_argument('--lanes', type=int, default=4, help='concurrent det-batch pipelines (threads + HIP streams) per GPU')
     ap.add_argument('--sustain-frames', type=int, default=10000,
                     help='frames of the sustained leg (BASELINE config 2: 10k frames), 0 = skip')
     ap.add_argument('--cpu-frames', type=int, default=None,
