@@ -34,10 +34,21 @@ import threading
 import time
 
 # Four det-batch lanes (streams) per GPU, each on its own hardware queue: HIP maps a process's
-# streams onto GPU_MAX_HW_QUEUES queues (4 by default), so the fourth lane would share one.  Set
-# before anything initialises HIP; a value in the environment wins.  (c2, one box, default run:
-# 3 lanes 9,778 / 9,804 faces/s, 4 lanes on 8 queues 10,109 / 10,137; profiles/r05ln2_lanes_ab.txt)
-os.environ.setdefault('GPU_MAX_HW_QUEUES', '8')
+# streams onto GPU_MAX_HW_QUEUES queues (4 on the GPU boxes' environment), so the fourth lane would
+# share one.  Set before anything initialises HIP (--hw-queues, default 8; 0 keeps the
+# environment's value).  (c2, one box, default run: 3 lanes 9,778 / 9,804 faces/s, 4 lanes on 4
+# queues ~9,440, on 8 queues 10,109 / 10,137; profiles/r05ln2_lanes_ab.txt)
+def _hw_queues(argv):
+    for i, t in enumerate(argv):
+        if t == '--hw-queues' and i + 1 < len(argv):
+            return int(argv[i + 1])
+        if t.startswith('--hw-queues='):
+            return int(t.split('=', 1)[1])
+    return 8
+
+
+if _hw_queues(sys.argv[1:]) > 0:
+    os.environ['GPU_MAX_HW_QUEUES'] = str(_hw_queues(sys.argv[1:]))
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 for _p in (ROOT, os.path.join(ROOT, 'video-to-faces_amd')):
@@ -89,6 +100,8 @@ def parse(argv=None):
                     help='distinct synthetic frames of the global frame sequence, cycled (default 32; c5: 0 = '
                          'every frame of the run distinct, generated on the device)')
     ap.add_argument('--lanes', type=int, default=4, help='concurrent det-batch pipelines (threads + HIP streams) per GPU')
+    ap.add_argument('--hw-queues', type=int, default=8,
+                    help='GPU_MAX_HW_QUEUES for this process (set before HIP starts; 0 = keep the environment)')
     ap.add_argument('--sustain-frames', type=int, default=10000,
                     help='frames of the sustained leg (BASELINE config 2: 10k frames), 0 = skip')
     ap.add_argument('--cpu-frames', type=int, default=None,
@@ -789,7 +802,7 @@ def run_gpu(args):
                     'to a few face-sized detections per frame, encoders calibrated to spread embeddings)' % args.frame,
             'config': {'workload': workload, 'baseline_config': args.config, 'det_batch': args.det_batch if det else None,
                        'enc_batch': args.enc_batch, 'frames_per_step_per_gpu': args.det_batch if det else 0,
-                       'lanes': getattr(pipe, 'L', 1),
+                       'lanes': getattr(pipe, 'L', 1), 'hw_queues': os.environ.get('GPU_MAX_HW_QUEUES'),
                        'parallelism': 'dp%d (frame-sharded, RCCL all-gather of embeddings)' % ctx.world,
                        # the reference writes face crops as JPEG files and re-reads them for the
                        # encoder (detection.py -> encoders); here crops go from HBM frames to the

@@ -1,5 +1,5 @@
 """Per-launch timeline of the FaceNet forwards in a rocprofv3 results db: span/busy of every
-forward (k_blob ... k_l2_normalize) and the per-kernel listing of the largest one."""
+forward (k_blob or k_stem_head ... k_l2_normalize) and the per-kernel listing of the largest one."""
 import glob, re, sqlite3, sys
 p = sys.argv[1]
 if not p.endswith('.db'):
@@ -10,7 +10,7 @@ heads = [i for i, r in enumerate(rows) if 'k_l2_normalize' in r[0] or 'k_facenet
 fw = []
 for h in heads:
     s = h
-    while s > 0 and 'k_blob' not in rows[s][0]:
+    while s > 0 and 'k_blob' not in rows[s][0] and 'k_stem_head' not in rows[s][0]:
         s -= 1
     seq = [r for r in rows[s:h + 1] if r[8] == rows[h][8]]
     fw.append((sum(r[3] for r in seq), seq))

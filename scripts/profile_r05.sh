@@ -1,10 +1,11 @@
 #!/bin/bash
 # End-of-round evidence on one box: GPU tests + smoke, the default bench line (config 2), kernel
-# traces (1 and 3 lanes), SQ / FETCH_SIZE / WRITE_SIZE passes (1 lane), dispatch counts, and the
-# config 3 / 4 / 5 bench lines (with their CPU baselines).  bash scripts/profile_r05.sh TAG [skip-tests]
+# traces (1 and 4 lanes), SQ / FETCH_SIZE / WRITE_SIZE passes (1 lane), dispatch counts, and the
+# config 3 / 4 / 5 bench lines (with their CPU baselines).  bash scripts/profile_r05.sh TAG [skip-tests|main|configs]
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 O=gpurun_out/p5_${1:-a}
 mkdir -p $O
+if [ "${2:-}" != configs ]; then
 if [ "${2:-}" != skip-tests ]; then
   timeout -k 10 800 python -u -m pytest -v -rA --timeout 300 --timeout-method thread -m gpu tests > $O/tests.log 2>&1
   rc=$?
@@ -21,7 +22,7 @@ B="--no-cpu-baseline --no-extras --sustain-frames 0"
 SQ="SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_VALU_MFMA_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE GRBM_GUI_ACTIVE"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/c2_trace -o run -- python3 bench.py --steps 10 --warmup 3 $B > $O/c2_trace.json 2> $O/c2_trace.err || exit $?
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/c2_trace1 -o run -- python3 bench.py --steps 32 --warmup 3 --lanes 1 $B > $O/c2_trace1.json 2> $O/c2_trace1.err || exit $?
-python3 scripts/kstats.py $O/c2_trace 40 > $O/c2_kernel_stats_3lane.txt 2>&1
+python3 scripts/kstats.py $O/c2_trace 40 > $O/c2_kernel_stats_4lane.txt 2>&1
 python3 scripts/kstats.py $O/c2_trace1 70 > $O/c2_kernel_stats_1lane.txt 2>&1
 python3 scripts/dispatch_counts.py $O/c2_trace1 > $O/dispatch_counts.txt 2>&1
 timeout -s KILL 240 rocprofv3 --pmc $SQ --kernel-trace --output-format csv -d $O/c2_pmc_sq -o run -- python3 bench.py --steps 3 --warmup 1 --lanes 1 $B > /dev/null 2> $O/c2_pmc_sq.err || exit $?
@@ -33,6 +34,8 @@ find $O -name '*.db' -delete
 head -8 $O/c2_kernel_stats_1lane.txt
 cat $O/dispatch_counts.txt
 head -6 $O/c2_pmc_table.txt
+[ "${2:-}" = main ] && exit 0
+fi
 for c in c3 c4 c5; do
   timeout -k 10 600 python3 bench.py --config $c > $O/bench_$c.json 2> $O/bench_$c.err || exit $?
   python3 -c "

@@ -67,6 +67,37 @@ def test_bf16_fused_blocks_bit_identical(n, split, g, monkeypatch):
         assert (e * g['emb']).sum(1).min() > 0.99, mode
 
 
+@pytest.mark.parametrize('n', [128, 7])
+def test_bf16_stem_head_bit_identical(n, monkeypatch):
+    """k_stem_head (csrc/facenet_fused.hip: the blob of the device crops and conv2d_1a in one launch,
+    the 160x160 blob kept in LDS) computes k_blob's pixels and k_conv's MFMA chain / epilogue for
+    that layer: with split-K off in both runs the embeddings equal the unfused path's (k_blob to
+    HBM, then k_conv) bit for bit.  Crops: 160x160 (the direct-copy case), smaller / larger than the
+    blob, 1-pixel wide, at the frame edges and partly outside, and (device crops) a frame index
+    outside the frames (a zero image)."""
+    from videotofaces import synth
+    from videotofaces.encoders.facenet import InceptionResnetV1
+    m = InceptionResnetV1('cuda:0', precision='bf16')
+    fr = torch.from_numpy(synth.make_frames(3, 240, 320, seed=5)).cuda()
+    rng = np.random.default_rng(n)
+    fixed = [[0, 0, 0, 160, 160], [1, 10, 20, 110, 130], [2, 100, 50, 320, 240], [0, 5, 5, 6, 200],
+             [1, 300, 200, 340, 260], [2, 0, 0, 320, 240], [7, 0, 0, 50, 50]]
+    rows = []
+    for i in range(n):
+        if i < len(fixed):
+            rows.append(fixed[i])
+            continue
+        x1, y1 = int(rng.integers(0, 300)), int(rng.integers(0, 220))
+        rows.append([int(rng.integers(0, 3)), x1, y1, x1 + int(rng.integers(1, 260)), y1 + int(rng.integers(1, 200))])
+    crops = torch.tensor(rows, dtype=torch.int32, device='cuda')
+    monkeypatch.setenv('VTF_NO_SPLITK', '1')
+    fused = m.encode_crops(fr, crops).cpu().numpy()
+    monkeypatch.setenv('VTF_FN_FUSED', '0')
+    plain = m.encode_crops(fr, crops).cpu().numpy()
+    print('stem head vs blob + k_conv: max |diff| %.3g' % np.abs(fused - plain).max())
+    np.testing.assert_array_equal(fused, plain)
+
+
 def test_blob_kernel_matches_restated_inter_linear():
     from videotofaces.encoders.facenet import blob_from_images
     from oracle.facenet import resize_linear_u8

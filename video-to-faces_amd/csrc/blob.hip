@@ -34,18 +34,8 @@ __global__ void k_blob(const uint8_t* __restrict__ frames, int F, int H, int W, 
     int dx = (int)(i % S);
     int dy = (int)((i / S) % S);
     int64_t n = i / ((int64_t)S * S);
-    const int32_t* c = crops + n * 5;
-    int f = c[0], x1 = c[1], y1 = c[2], x2 = c[3], y2 = c[4];
-    // numpy slice semantics of img[y1:y2, x1:x2] for in-frame boxes (adjust_boxes clamps); a
-    // frame index outside [0, F) (only possible for device-side crop lists, host lists are
-    // validated) encodes a zero image instead of reading outside the frames
-    x1 = max(0, min(x1, W));
-    x2 = max(x1, min(x2, W));
-    y1 = max(0, min(y1, H));
-    y2 = max(y1, min(y2, H));
-    int w = x2 - x1, h = y2 - y1;
-    if (f < 0 || f >= F) w = h = 0;
-    const uint8_t* base = frames + (int64_t)(w > 0 && h > 0 ? f : 0) * fstride + (int64_t)y1 * rstride + (int64_t)x1 * 3;
+    int w, h;
+    const uint8_t* base = blob_crop(frames, F, H, W, fstride, rstride, crops + n * 5, w, h);
     int v[3];
     if (w <= 0 || h <= 0) {
         v[0] = v[1] = v[2] = 0;
@@ -63,15 +53,24 @@ __global__ void k_blob(const uint8_t* __restrict__ frames, int F, int H, int W, 
         const uint8_t* r0 = base + (int64_t)sy0 * rstride;
         const uint8_t* r1 = base + (int64_t)sy1 * rstride;
 #pragma unroll
-        for (int ch = 0; ch < 3; ch++) {
-            int h0 = ex ? r0[sx0 * 3 + ch] * 2048 : r0[sx0 * 3 + ch] * a0 + r0[sx1 * 3 + ch] * a1;
-            int h1 = ex ? r1[sx0 * 3 + ch] * 2048 : r1[sx0 * 3 + ch] * a0 + r1[sx1 * 3 + ch] * a1;
-            int t = (((h0 >> 4) * b0) >> 16) + (((h1 >> 4) * b1) >> 16);
-            t = (t + 2) >> 2;
-            v[ch] = min(255, max(0, t));
-        }
+        for (int ch = 0; ch < 3; ch++) v[ch] = blob_lin(r0, r1, sx0, sx1, a0, a1, ex, b0, b1, ch);
     }
     // swapRB: output channel 0 = R = BGR byte 2
+    if (LAYOUT == 1 && Cp == 8) {
+        // the pixel's 8 channels (3 values, 5 zeros) as one vector store (16 B bf16 / 32 B fp32)
+        // instead of eight scalar ones
+        T px[8];
+#pragma unroll
+        for (int oc = 0; oc < 8; oc++) px[oc] = cvt_out<T>(oc < 3 ? ((float)v[2 - oc] - mean) * scale : 0.f);
+        T* o = out + ((n * S + dy) * S + dx) * 8;
+        if constexpr (sizeof(T) == 2) {
+            *(uint4*)o = __builtin_bit_cast(uint4, px);
+        } else {
+            ((uint4*)o)[0] = make_uint4(__float_as_uint(px[0]), __float_as_uint(px[1]), __float_as_uint(px[2]), __float_as_uint(px[3]));
+            ((uint4*)o)[1] = make_uint4(0u, 0u, 0u, 0u);
+        }
+        return;
+    }
     for (int oc = 0; oc < 3; oc++) {
         float val = ((float)v[2 - oc] - mean) * scale;
         if (LAYOUT == 0)

@@ -583,10 +583,46 @@ __global__ void k_maxpool(const T* __restrict__ in, int N, int H, int W, int C, 
     out[(((int64_t)n * OH + oh) * OW + ow) * out_cstride + out_coff + c] = from_f<T>(m);
 }
 
+// bf16, 8 channels per thread (C, out_cstride, out_coff multiples of 8): 16-byte loads and stores
+// (the max is exact, so the same bits as k_maxpool)
+__global__ void k_maxpool_bf16x8(const __bf16* __restrict__ in, int N, int H, int W, int C, int OH, int OW,
+                                 __bf16* __restrict__ out, int out_cstride, int out_coff) {
+    const int C8 = C >> 3;
+    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= (int64_t)N * OH * OW * C8) return;
+    const int c8 = (int)(i % C8);
+    int64_t t = i / C8;
+    const int ow = (int)(t % OW);
+    t /= OW;
+    const int oh = (int)(t % OH);
+    const int n = (int)(t / OH);
+    float m[8];
+#pragma unroll
+    for (int e = 0; e < 8; e++) m[e] = -3.402823466e38f;
+    const __bf16* src = in + (((int64_t)n * H + 2 * oh) * W + 2 * ow) * C + 8 * c8;
+#pragma unroll
+    for (int dy = 0; dy < 3; dy++)
+#pragma unroll
+        for (int dx = 0; dx < 3; dx++) {
+            const bf16x8 v = *(const bf16x8*)(src + ((int64_t)dy * W + dx) * C);
+#pragma unroll
+            for (int e = 0; e < 8; e++) m[e] = fmaxf(m[e], (float)v[e]);
+        }
+    bf16x8 o;
+#pragma unroll
+    for (int e = 0; e < 8; e++) o[e] = (__bf16)m[e];
+    *(bf16x8*)(out + (((int64_t)n * OH + oh) * OW + ow) * out_cstride + out_coff + 8 * c8) = o;
+}
+
 void launch_maxpool(const void* in, int N, int H, int W, int C, void* out, int out_cstride, int out_coff, bool bf16,
                     hipStream_t st) {
     int OH = (H - 3) / 2 + 1, OW = (W - 3) / 2 + 1;
     int64_t tot = (int64_t)N * OH * OW * C;
+    if (bf16 && C % 8 == 0 && out_cstride % 8 == 0 && out_coff % 8 == 0) {
+        k_maxpool_bf16x8<<<cdiv(tot / 8, 256), 256, 0, st>>>((const __bf16*)in, N, H, W, C, OH, OW, (__bf16*)out,
+                                                             out_cstride, out_coff);
+        return;
+    }
     if (bf16)
         k_maxpool<__bf16><<<cdiv(tot, 256), 256, 0, st>>>((const __bf16*)in, N, H, W, C, OH, OW, (__bf16*)out,
                                                            out_cstride, out_coff);

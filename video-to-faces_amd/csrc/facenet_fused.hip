@@ -29,6 +29,7 @@
 #include <cstdlib>
 #include <vector>
 
+#include "blob.hpp"
 #include "common.hpp"
 #include "conv.hpp"
 #include "conv_dev.hpp"
@@ -611,6 +612,133 @@ __global__ __launch_bounds__(256, 2) void k_conv_patch(CPatchP p) {
     }
 }
 
+// ---------------------------------------------------------------------------------------------
+// FaceNet stem head: blobFromImages of the device crops (k_blob's INTER_LINEAR and normalisation,
+// facenet.py:179) straight into conv2d_1a (3x3 stride 2, 3 -> 32, BN + ReLU, facenet.py:126): a
+// tile of 8 x 16 output pixels computes its 17 x 33 blob patch into LDS (8 bf16 per pixel, the
+// blob's NHWC layout: 3 values + 5 zeros) and runs the conv from there, so the 160 x 160 blob never
+// goes through HBM.  The conv is k_conv's (conv.hip) for this layer bit for bit: the same
+// v_mfma_f32_16x16x32_bf16 chain over k = 0..127 (taps 9..15 zero; K = 72 in two 64-deep k-tiles),
+// the same lane -> k mapping, and the same fmaf(acc, alpha, beta) + ReLU epilogue.
+constexpr int SH_TH = 8, SH_TW = 16, SH_PH = 2 * SH_TH + 1, SH_PW = 2 * SH_TW + 1;  // patch 17 x 33
+constexpr int SH_S = 160, SH_OUT = 79, SH_COUT = 32;
+// patch image: per row the 17 even columns, then the 16 odd ones (16 B each): a fragment's lanes
+// (output columns tx, input column 2 tx + kx) read consecutive 16-byte slots
+constexpr int SH_RS = SH_PW * 16;
+
+struct StemP {
+    const uint8_t* frames;
+    int F, H, W;
+    int64_t fstride, rstride;
+    const int32_t* crops;
+    const __bf16* w;  // [32][72] (k = tap * 8 + c)
+    const float *al, *be;
+    __bf16* out;      // [N][79][79][32]
+    float mean, scale;
+    int tiles_x, tiles_per_img;
+};
+
+__device__ inline int sh_slot(int r, int c) { return r * SH_RS + ((c & 1) ? (SH_PW / 2 + 1) * 16 : 0) + (c >> 1) * 16; }
+
+__global__ __launch_bounds__(256) void k_stem_head(StemP p) {
+    __shared__ __attribute__((aligned(16))) char P[SH_PH * SH_RS];
+    __shared__ __attribute__((aligned(16))) __bf16 E[SH_TH * SH_TW * SH_COUT];
+    __shared__ int4 ycf[SH_PH], xcf[SH_PW];  // (s0, s1, c0, c1) per patch row / column; x: edge flag in s1's sign
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int n = blockIdx.x / p.tiles_per_img, t = blockIdx.x - n * p.tiles_per_img;
+    const int ty = t / p.tiles_x, oy0 = ty * SH_TH, ox0 = (t - ty * p.tiles_x) * SH_TW;
+    int w, h;
+    const uint8_t* base = blob_crop(p.frames, p.F, p.H, p.W, p.fstride, p.rstride, p.crops + (int64_t)n * 5, w, h);
+    const bool empty = w <= 0 || h <= 0, same = w == SH_S && h == SH_S;
+    if (!empty && !same) {
+        if (tid < SH_PH) {
+            const int d = min(2 * oy0 + tid, SH_S - 1);
+            int s0, s1, c0, c1;
+            bool e;
+            lin_coef(d, h, SH_S, s0, s1, c0, c1, e);
+            ycf[tid] = make_int4(s0, s1, c0, c1);
+        } else if (tid >= 64 && tid < 64 + SH_PW) {
+            const int d = min(2 * ox0 + tid - 64, SH_S - 1);
+            int s0, s1, c0, c1;
+            bool e;
+            lin_coef(d, w, SH_S, s0, s1, c0, c1, e);
+            xcf[tid - 64] = make_int4(s0, e ? -1 - s1 : s1, c0, c1);
+        }
+    }
+    // the B operands (weights) meanwhile: lane (channel 16 j + (lane & 15), k = 32 s + 8 (lane >> 4) ..)
+    bf16x8 wb[4][2];
+#pragma unroll
+    for (int s = 0; s < 4; s++)
+#pragma unroll
+        for (int j = 0; j < 2; j++) {
+            const int k = 32 * s + 8 * (lane >> 4);
+            wb[s][j] = k < 72 ? *(const bf16x8*)(p.w + (16 * j + (lane & 15)) * 72 + k) : bf16x8{};
+        }
+    __syncthreads();
+    for (int e = tid; e < SH_PH * SH_PW; e += 256) {
+        const int r = e / SH_PW, c = e - r * SH_PW;
+        const int dy = 2 * oy0 + r, dx = 2 * ox0 + c;
+        int v[3] = {0, 0, 0};
+        if (!empty && dy < SH_S && dx < SH_S) {
+            if (same) {
+                const uint8_t* q = base + (int64_t)dy * p.rstride + dx * 3;
+                v[0] = q[0], v[1] = q[1], v[2] = q[2];
+            } else {
+                const int4 yc = ycf[r], xc = xcf[c];
+                const bool ex = xc.y < 0;
+                const int sx1 = ex ? -1 - xc.y : xc.y;
+                const uint8_t* r0 = base + (int64_t)yc.x * p.rstride;
+                const uint8_t* r1 = base + (int64_t)yc.y * p.rstride;
+#pragma unroll
+                for (int ch = 0; ch < 3; ch++) v[ch] = blob_lin(r0, r1, xc.x, sx1, xc.z, xc.w, ex, yc.z, yc.w, ch);
+            }
+        }
+        // (k_blob: swapRB, ((float)v - mean) * scale, bf16; outside the blob: zero)
+        bf16x8 px = {};
+        if (dy < SH_S && dx < SH_S)
+#pragma unroll
+            for (int oc = 0; oc < 3; oc++) px[oc] = (__bf16)(((float)v[2 - oc] - p.mean) * p.scale);
+        *(bf16x8*)(P + sh_slot(r, c)) = px;
+    }
+    __syncthreads();
+    // wave w: output rows 2 w, 2 w + 1 of the tile (one 16-pixel fragment each)
+    f4 acc[2][2];
+#pragma unroll
+    for (int i = 0; i < 2; i++) acc[i][0] = acc[i][1] = f4{0.f, 0.f, 0.f, 0.f};
+    const int tx = lane & 15, g = lane >> 4;
+#pragma unroll
+    for (int s = 0; s < 4; s++) {
+        const int tap = 4 * s + g;
+        const int ky = tap / 3, kx = tap - 3 * ky;
+#pragma unroll
+        for (int i = 0; i < 2; i++) {
+            const bf16x8 a = tap < 9 ? *(const bf16x8*)(P + sh_slot(2 * (2 * wave + i) + ky, 2 * tx + kx)) : bf16x8{};
+#pragma unroll
+            for (int j = 0; j < 2; j++) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, wb[s][j], acc[i][j], 0, 0, 0);
+        }
+    }
+    // BN + ReLU -> bf16 staging [128][32] -> 16-byte stores of the in-bounds pixels
+#pragma unroll
+    for (int j = 0; j < 2; j++) {
+        const int ch = 16 * j + (lane & 15);
+        const float a = p.al[ch], b = p.be[ch];
+#pragma unroll
+        for (int i = 0; i < 2; i++)
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                const int m = 16 * (2 * wave + i) + 4 * g + q;
+                E[m * SH_COUT + ch] = (__bf16)relu_bf(fmaf(acc[i][j][q], a, b));
+            }
+    }
+    __syncthreads();
+    for (int e = tid; e < SH_TH * SH_TW * SH_COUT / 8; e += 256) {
+        const int m = e >> 2, c = e & 3;
+        const int oy = oy0 + (m >> 4), ox = ox0 + (m & 15);
+        if (oy < SH_OUT && ox < SH_OUT)
+            *(bf16x8*)(p.out + (((int64_t)n * SH_OUT + oy) * SH_OUT + ox) * SH_COUT + 8 * c) = *(const bf16x8*)(E + m * SH_COUT + 8 * c);
+    }
+}
+
 }  // namespace
 
 // one Block17 (bf16 NHWC [N, 8, 8, 896] -> same): weights as FaceNet's layer table holds them
@@ -749,6 +877,35 @@ bool launch_conv_patch(const ConvParams& q, hipStream_t st) {
         k_conv_patch<64><<<grid, 256, lds, st>>>(p);
     VTF_HIP(hipGetLastError());
     return true;
+}
+
+}  // namespace vtf
+
+namespace vtf {
+
+// FaceNet stem head (bf16): crops of the uint8 frames -> conv2d_1a output [N, 79, 79, 32]
+void launch_stem_head(const uint8_t* frames, int F, int H, int W, int64_t fstride, int64_t rstride,
+                      const int32_t* d_crops, int N, const void* w, const float* al, const float* be, void* out,
+                      hipStream_t st) {
+    if (N <= 0) return;
+    StemP p;
+    p.frames = frames;
+    p.F = F;
+    p.H = H;
+    p.W = W;
+    p.fstride = fstride;
+    p.rstride = rstride;
+    p.crops = d_crops;
+    p.w = (const __bf16*)w;
+    p.al = al;
+    p.be = be;
+    p.out = (__bf16*)out;
+    p.mean = 127.5f;
+    p.scale = 0.0078125f;
+    p.tiles_x = (SH_OUT + SH_TW - 1) / SH_TW;
+    p.tiles_per_img = p.tiles_x * ((SH_OUT + SH_TH - 1) / SH_TH);
+    k_stem_head<<<(unsigned)(N * p.tiles_per_img), 256, 0, st>>>(p);
+    VTF_HIP(hipGetLastError());
 }
 
 }  // namespace vtf

@@ -28,6 +28,19 @@ void launch_block35_branches(const void* x, void* cat, int N, const void* wm, co
 
 bool launch_conv_patch(const ConvParams& q, hipStream_t st);
 
+void launch_stem_head(const uint8_t* frames, int F, int H, int W, int64_t fstride, int64_t rstride,
+                      const int32_t* d_crops, int N, const void* w, const float* al, const float* be, void* out,
+                      hipStream_t st);
+
+// device crops of uint8 frames (vtf_facenet_encode_crops): the bf16 fused mode runs the blob and
+// conv2d_1a as one launch (k_stem_head)
+struct StemIn {
+    const uint8_t* frames;
+    int F, H, W;
+    int64_t fstride, rstride;
+    const int32_t* crops;
+};
+
 // bf16 Block17 as one launch per block (facenet_fused.hip); VTF_FN_FUSED=0: the four launches
 static bool fused_blocks() {
     const char* e = std::getenv("VTF_FN_FUSED");  // (read per forward: tests switch it in-process)
@@ -320,8 +333,9 @@ static void conv_merged(Facenet& F, int li, const Act& in, int N, void* out, int
     launch_conv(p, F.bf16, F.st);
 }
 
-// x: NHWC [N,160,160,8] (precision dtype) -> emb [N,512] fp32
-static void forward(Facenet& F, const void* x, int N, float* emb) {
+// x: NHWC [N,160,160,8] (precision dtype) -> emb [N,512] fp32; or (stem) the crops, blob and
+// conv2d_1a fused
+static void forward(Facenet& F, const void* x, int N, float* emb, const StemIn* stem = nullptr) {
     const size_t es = F.bf16 ? 2 : 4;
     const size_t big = (size_t)N * 77 * 77 * 64;  // largest activation (stem conv2)
     const size_t tmp = (size_t)N * 17 * 17 * 192;  // largest branch temp (Mixed_6a)
@@ -334,7 +348,15 @@ static void forward(Facenet& F, const void* x, int N, float* emb) {
     Act a{(void*)x, 160, 160, 8}, b{};
     int li = 0;
     // stem (facenet.py:126-134)
-    conv(F, li++, a, N, P0, 32, 0, nullptr, 1.f, true, &b);
+    if (stem) {
+        const Layer& l0 = F.L[0];
+        launch_stem_head(stem->frames, stem->F, stem->H, stem->W, stem->fstride, stem->rstride, stem->crops, N, l0.w,
+                         l0.alpha, l0.beta, P0, F.st);
+        b = Act{P0, 79, 79, 32};
+        li++;
+    } else {
+        conv(F, li++, a, N, P0, 32, 0, nullptr, 1.f, true, &b);
+    }
     conv(F, li++, b, N, P1, 32, 0, nullptr, 1.f, true, &a);
     conv(F, li++, a, N, P0, 64, 0, nullptr, 1.f, true, &b);
     launch_maxpool(P0, N, b.H, b.W, 64, P1, 64, 0, F.bf16, F.st);
@@ -515,6 +537,12 @@ int vtf_facenet_encode_crops(vtf_facenet_t h, const uint8_t* d_frames, int n_fra
             int32_t* d = F.ar.get<int32_t>(6, N * 5);
             VTF_HIP(hipMemcpyAsync(d, crops, N * 5 * 4, hipMemcpyHostToDevice, F.st));
             dc = d;
+        }
+        if (F.bf16 && fused_blocks()) {
+            const StemIn si{d_frames, n_frames, H, W, frame_stride, row_stride, dc};
+            forward(F, nullptr, (int)N, d_emb, &si);
+            VTF_HIP(hipGetLastError());
+            return;
         }
         void* xin = F.ar.get(5, (size_t)N * 160 * 160 * 8 * (F.bf16 ? 2 : 4));
         // blobFromImages(images, 1/128, (160,160), (127.5,)*3, swapRB=True) (facenet.py:179)
