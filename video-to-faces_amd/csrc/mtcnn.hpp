@@ -31,6 +31,10 @@ struct PNetW {
     // PReLU slope classes (host): bit 0 every conv2 slope in [0, 1], bit 1 every conv3 slope in
     // [0, 1] -- PReLU is then max(v, a v), two instructions instead of three
     int unit_slopes;
+    // 1: the exact-levels variant's conv1 on 16x16x32 matrix cores with the main and cross products
+    // in one chain (w0 pre-scaled by 2^11 on the device: the host checked 2^11 |w0| < 2^15), 0: the
+    // 32x32x16 [w0 | w1] layout (env VTF_PNET_C1K=0)
+    int c1k;
 };
 struct PNetOut {
     // sparse (candidate) mode

@@ -978,6 +978,93 @@ __global__ __launch_bounds__(256, PnLds<X || PR>::GPC) void k_pnet(const uint8_t
                     else
                         conv1_frags(F{}, F{}, I1{}, NF1 / 2 * h + wv);
                 }
+            } else if (X && wg.c1k) {
+                // exact levels (x1 = 0) on v_mfma_f32_16x16x32_f16, the main and cross products in
+                // ONE chain: A row = (cell, corner) of a 1 x 4 run of pooled cells (lane & 15 ->
+                // cell (lane & 15) >> 2, corner lane & 3), K = 3 steps x 4 lane groups of pixel pairs
+                // (kx 0,1 | 2,3 of tap row ky; 4 halves a pixel): pairs 0..5 = (ky, kx pair) against
+                // 2^11 w0, pairs 6..11 the same pixels against w1, so the accumulator is u = 2048 v
+                // directly (the 32x32 layout needs a lane swap + fma per corner to combine its [w0 |
+                // w1] columns).  The D layout hands each lane the 4 corners of one cell (lane >> 4) for
+                // one channel (lane & 15): the max-pool is in-register.
+                constexpr int FB4 = PP_W / 4, NF4 = PP_H * FB4;
+                static_assert(PP_W % 4 == 0, "conv1 runs of 4 pooled cells");
+                const int g4 = ln >> 4, r16 = ln & 15, crn = r16 & 3;
+                const int abase = ((crn >> 1) * PL_W + 2 * (r16 >> 2) + (crn & 1)) * 4;
+                int ko[3];
+                f16x8 wk[3];
+#pragma unroll
+                for (int s = 0; s < 3; s++) {
+                    const int i = 4 * s + g4, q = i < 6 ? i : i - 6;
+                    ko[s] = ((q >> 1) * PL_W + 2 * (q & 1)) * 4;
+                    const f16x8 w = __builtin_bit_cast(
+                        f16x8, __builtin_amdgcn_raw_buffer_load_b128(rw1h, ((r16 + (i < 6 ? 0 : 16)) * 64 + (q >> 1) * 16 + (q & 1) * 8) * 2, 0, 0));
+                    wk[s] = i < 6 ? w * (_Float16)2048.f : w;
+                }
+                const int cq = ln >> 4;  // the D cell of this lane
+                auto c1k_frags = [&](auto fp_t, auto nu_t, int f0) -> int {
+                    constexpr bool FP = decltype(fp_t)::value;
+                    constexpr int NU = decltype(nu_t)::value;
+                    for (; f0 + 4 * (NU - 1) < NF4; f0 += 4 * NU) {
+                        int py[NU], px0[NU];
+                        f16x8 xa[3][NU];
+#pragma unroll
+                        for (int u = 0; u < NU; u++) {
+                            const int f = f0 + 4 * u, r = f / FB4;
+                            py[u] = r;
+                            px0[u] = 4 * (f - r * FB4);
+                            const int fo = (2 * r * PL_W + 2 * px0[u]) * 4 + abase;
+#pragma unroll
+                            for (int s = 0; s < 3; s++) xa[s][u] = ld_h8(sL + fo + ko[s]);
+                        }
+                        f32x4 acc[NU];
+#pragma unroll
+                        for (int u = 0; u < NU; u++) acc[u] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                        for (int s = 0; s < 3; s++)
+#pragma unroll
+                            for (int u = 0; u < NU; u++)
+                                acc[u] = __builtin_amdgcn_mfma_f32_16x16x32_f16(xa[s][u], wk[s], acc[u], 0, 0, 0);
+#pragma unroll
+                        for (int u = 0; u < NU; u++) {
+                            const int px = px0[u] + cq;
+                            float out;
+                            if (FP) {
+                                const float v = fmaxf(fmaxf(acc[u][0], acc[u][1]), fmaxf(acc[u][2], acc[u][3])) + b1s;
+                                out = fmaxf(v, a1 * v);
+                            } else if (fastpool) {
+                                out = prelu(fmaxf(fmaxf(acc[u][0], acc[u][1]), fmaxf(acc[u][2], acc[u][3])) + b1s, a1);
+                            } else {
+                                const int gy = 2 * (oy0 + py[u]), gx = 2 * (ox0 + px);
+                                float m = -3.402823466e38f;
+                                bool any = false;
+#pragma unroll
+                                for (int i = 0; i < 4; i++) {
+                                    const bool ok = (gy + (i >> 1) < L1h) && (gx + (i & 1) < L1w);
+                                    const float v = prelu(acc[u][i] + b1s, a1);
+                                    if (ok) {
+                                        m = fmaxf(m, v);
+                                        any = true;
+                                    }
+                                }
+                                out = any ? m : 0.f;  // outside the valid pooled map: keep finite
+                            }
+                            _Float16 x0, x1;
+                            split_u(out, x0, x1);
+                            if (r16 < PQ_C) {
+                                _Float16* qp = sQ + (py[u] * PP_W + px) * PQ_C + r16;
+                                qp[0] = x0;
+                                qp[NPP * PQ_C] = x1;
+                            }
+                        }
+                    }
+                    return f0;
+                };
+                using I4 = std::integral_constant<int, 4>;
+                if (fastpool && unit_slope)
+                    c1k_frags(T{}, I1{}, c1k_frags(T{}, I4{}, wv));
+                else
+                    c1k_frags(F{}, I1{}, c1k_frags(F{}, I2{}, wv));
             } else if (exact) {
                 if (fastpool && unit_slope)
                     conv1_frags(T{}, T{}, I1{}, conv1_frags(T{}, T{}, I2{}, wv));

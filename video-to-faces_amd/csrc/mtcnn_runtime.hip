@@ -459,6 +459,12 @@ static void build_weights(Mtcnn& m, const float* params, int64_t n_params) {
             return true;
         };
         m.pw.unit_slopes = (unit(5, 16) ? 1 : 0) | (unit(8, 32) ? 2 : 0);  // p2 [16], p3 [32]
+        // k_pnet's merged-chain conv1 scales the fp16 w0 plane by 2^11 on the device: exact when
+        // every |w| < 16 (2^11 * 16 = 2^15 < 65504)
+        bool small = true;
+        for (int i = 0; i < 270; i++) small = small && std::fabs(raw[0][i]) < 16.f;
+        const char* ck = std::getenv("VTF_PNET_C1K");
+        m.pw.c1k = small && !(ck && ck[0] == '0') ? 1 : 0;
     }
     // k_pnet addresses the PNet weights from two bases with constant offsets (mtcnn_kernels.hip
     // PW_* / PH_*): the fp32 tensors are the first 13 of the packed buffer; the fp16 split
