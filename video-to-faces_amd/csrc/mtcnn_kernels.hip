@@ -493,8 +493,9 @@ __global__ __launch_bounds__(256, PnLds<X || PR>::GPC) void k_pnet(const uint8_t
         s_tile = (int)(tile_base + atomicAdd(tile_ctr, (uint32_t)chunk));
         s_cend = s_tile + chunk;
     }
+    // (the first tile's barrier; later tiles start behind the previous tile's closing barrier)
+    __syncthreads();
     for (;;) {
-        __syncthreads();
         mark(0);  // 0: end-of-tile prefetch store + loop barrier
         // (wave-uniform: the level table and tile geometry below become scalar loads)
         // thread coordinates laundered per tile: everything derived from them below is recomputed
@@ -568,7 +569,10 @@ __global__ __launch_bounds__(256, PnLds<X || PR>::GPC) void k_pnet(const uint8_t
         const bool staged = !P.pre && (int64_t)(fy1 - fy0) * pw3 <= LP::PATCH;
         uint8_t* patch = (uint8_t*)sP;
         // (gathers below issue 8 loads per thread before the first use: latency-bound otherwise)
-        if (staged && !(o.dbg & 64)) {
+        // (nothing left to stage -- the whole patch came with the previous tile's prefetch, the
+        //  common case on the upsampled levels -- needs no barrier: block-uniform condition)
+        const bool stage_more = staged && !(o.dbg & 64) && (fy1 - fy0) * pw3 > (pf_done ? 256 * 8 : 0);
+        if (stage_more) {
             // 8 consecutive patch bytes per thread (one 8-byte LDS store); the first 2 KB were
             // prefetched during the previous tile when pf_done
             const int nbytes = (fy1 - fy0) * pw3;
@@ -587,8 +591,8 @@ __global__ __launch_bounds__(256, PnLds<X || PR>::GPC) void k_pnet(const uint8_t
                 for (int u = 0; u < 4; u++)
                     if (i0 + u * 2048 < nbytes) *(uint2*)(patch + i0 + u * 2048) = pv[u];
             }
+            __syncthreads();
         }
-        __syncthreads();
         mark(2);  // 2: frame patch staging
         if (!X && !PR && P.pre && P.pad == 1) {
             // downsampled level precomputed by k_resample_sat_multi as fp16 split pixels (12 B:
