@@ -232,6 +232,182 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void k_gemm_x3(GemmX3Params p) {
     }
 }
 
+// Ping-pong variant: 256 x 128 tiles, 8 waves in two groups of four by M half (group g = wave >> 2
+// holds rows 128 g .. +127 as 2 x 2 waves of 64 x 64; waves w and w + 4 share a SIMD), three LDS
+// stages (144 KB, one workgroup per CU).  A k-step is two phases per wave -- fragment reads, then
+// 24 MFMAs -- each closed by a workgroup barrier, and group 1 runs one barrier behind group 0: at
+// every barrier the groups swap roles, so each SIMD's matrix pipe alternates between its two
+// waves while the other one reads LDS.  The DMA of step k + 2 is issued in the second read phase
+// of step k and waited for with a counted vmcnt before the barrier that precedes every read of it
+// (group 0 after its second MFMA phase, group 1 after its second read phase: the same barrier).
+// Same LDS image, MFMA chains and order per output as k_gemm_x3 (bit-identical results); the
+// tail split and slab layout are k_gemm_x3<256, 128, 8>'s.
+__device__ inline void pp_barrier() { asm volatile("s_barrier" ::: "memory"); }
+
+__global__ __launch_bounds__(512, 1) void k_gemm_x3_pp(GemmX3Params p) {
+    constexpr int BM = 256, BN = 128, NW = 8, NT = 512, NS = 3;
+    constexpr int RB = 128, A_ST = BM * RB, ST = (BM + BN) * RB, LDE = BN + 4, ER = 128;
+    constexpr int SM = NS * ST;
+    constexpr int FN = 4, PA = BM / (8 * NW), PB = BN / (8 * NW), P = PA + PB;
+    static_assert(SM <= 160 * 1024 && ER * LDE * 4 <= SM && P == 6, "ping-pong tile");
+    __shared__ __attribute__((aligned(16))) char smem[SM];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int grp = wave >> 2, wmg = wave >> 1, wn = wave & 1;  // wmg: 64-row block 0..3
+    const int bid = blockIdx.x;
+    const bool tail = bid >= p.dp_tiles;
+    int t, slice = 0;
+    if (!tail) {
+        const int xcd = bid & 7, loc = bid >> 3, per = p.dp_tiles >> 3, rem = p.dp_tiles & 7;
+        t = xcd < rem ? xcd * (per + 1) + loc : rem * (per + 1) + (xcd - rem) * per + loc;
+    } else {
+        t = p.dp_tiles + (bid - p.dp_tiles) / p.tail_split;
+        slice = (bid - p.dp_tiles) % p.tail_split;
+    }
+    const int gm = p.group_m > 0 ? p.group_m : p.gx;
+    const int span = gm * p.gy, first = (t / span) * gm, gsz = min(p.gx - first, gm);
+    const int tile_m = first + (t % span) % gsz, tile_n = (t % span) / gsz;
+    const int64_t m0 = (int64_t)tile_m * BM;
+    const int n0 = tile_n * BN;
+    const int src = (lane & 7) ^ (((lane >> 4) + 4 * (wave & 1)) & 7);
+    const int soff = (src & 3) * 32 + (src >> 2) * 16;
+    const int64_t rowb = (int64_t)p.K * 4;
+    const char* ga[PA];
+    const char* gb[PB];
+#pragma unroll
+    for (int j = 0; j < PA; j++) {
+        const int64_t m = min(m0 + 8 * (wave + NW * j) + (lane >> 3), p.M - 1);
+        ga[j] = (const char*)p.a + m * rowb + soff;
+    }
+#pragma unroll
+    for (int j = 0; j < PB; j++) {
+        const int64_t n = min(n0 + 8 * (wave + NW * j) + (lane >> 3), p.N - 1);
+        gb[j] = (const char*)p.b + n * rowb + soff;
+    }
+    auto issue = [&](int kt, int s) {
+        const int64_t kb = (int64_t)kt * RB;
+        char* base = smem + s * ST;
+#pragma unroll
+        for (int j = 0; j < PA; j++)
+            __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)(ga[j] + kb),
+                                             (void __attribute__((address_space(3)))*)(base + (wave + NW * j) * 1024), 16,
+                                             0, 0);
+#pragma unroll
+        for (int j = 0; j < PB; j++)
+            __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)(gb[j] + kb),
+                                             (void __attribute__((address_space(3)))*)(base + A_ST + (wave + NW * j) * 1024),
+                                             16, 0, 0);
+    };
+    // wait until at most `newer` later steps' DMA pieces of this wave are outstanding
+    auto wait_dma = [&](int newer) {
+        if (newer > 0)
+            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(P) : "memory");
+        else
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    };
+    f4 acc[4][FN], accx[4][FN];
+#pragma unroll
+    for (int i = 0; i < 4; i++)
+#pragma unroll
+        for (int j = 0; j < FN; j++) {
+            acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
+            accx[i][j] = f4{0.f, 0.f, 0.f, 0.f};
+        }
+    const int hsw = (lane & 15) >> 1;
+    const int o0 = (lane & 15) * RB + (((lane >> 4) ^ hsw) << 4);
+    const int o1 = (lane & 15) * RB + (((4 + (lane >> 4)) ^ hsw) << 4);
+    const int KT = p.K / 32;
+    const int kt0 = tail ? (int)((int64_t)slice * KT / p.tail_split) : 0;
+    const int kt1 = tail ? (int)((int64_t)(slice + 1) * KT / p.tail_split) : KT;
+    issue(kt0, 0);
+    if (kt0 + 1 < kt1) issue(kt0 + 1, 1);
+    wait_dma(kt0 + 1 < kt1 ? 1 : 0);
+    pp_barrier();  // step kt0 visible to every wave
+    if (grp) pp_barrier();  // the stagger: group 1 one barrier behind
+    for (int kt = kt0; kt < kt1; kt++) {
+        const int sb = (kt - kt0) % NS;
+        const char* As = smem + sb * ST + wmg * 64 * RB;
+        const char* Bs = smem + sb * ST + A_ST + wn * 64 * RB;
+        h8 b0[FN], b1[FN], a0[2], a1[2];
+        // ---- phase 1: B and A rows 0, 1 -> 24 MFMAs
+#pragma unroll
+        for (int j = 0; j < FN; j++) {
+            b0[j] = *(const h8*)(Bs + j * 16 * RB + o0);
+            b1[j] = *(const h8*)(Bs + j * 16 * RB + o1);
+        }
+#pragma unroll
+        for (int i = 0; i < 2; i++) {
+            a0[i] = *(const h8*)(As + i * 16 * RB + o0);
+            a1[i] = *(const h8*)(As + i * 16 * RB + o1);
+        }
+        pp_barrier();
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int i = 0; i < 2; i++)
+#pragma unroll
+            for (int j = 0; j < FN; j++) {
+                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a0[i], b0[j], acc[i][j], 0, 0, 0);
+                accx[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a0[i], b1[j], accx[i][j], 0, 0, 0);
+                accx[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a1[i], b0[j], accx[i][j], 0, 0, 0);
+            }
+        __builtin_amdgcn_s_setprio(0);
+        pp_barrier();
+        // ---- phase 2: the DMA of step kt + 2 (its stage was last read in step kt - 1, by every
+        //      wave before the barrier that opened this step's first MFMA phase... of group 1), A
+        //      rows 2, 3 -> 24 MFMAs
+        if (kt + 2 < kt1) issue(kt + 2, (kt - kt0 + 2) % NS);
+#pragma unroll
+        for (int i = 0; i < 2; i++) {
+            a0[i] = *(const h8*)(As + (i + 2) * 16 * RB + o0);
+            a1[i] = *(const h8*)(As + (i + 2) * 16 * RB + o1);
+        }
+        if (grp && kt + 1 < kt1) wait_dma(kt + 2 < kt1 ? 1 : 0);  // step kt + 1 (group 1)
+        pp_barrier();
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int i = 0; i < 2; i++)
+#pragma unroll
+            for (int j = 0; j < FN; j++) {
+                acc[i + 2][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a0[i], b0[j], acc[i + 2][j], 0, 0, 0);
+                accx[i + 2][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a0[i], b1[j], accx[i + 2][j], 0, 0, 0);
+                accx[i + 2][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a1[i], b0[j], accx[i + 2][j], 0, 0, 0);
+            }
+        __builtin_amdgcn_s_setprio(0);
+        if (!grp && kt + 1 < kt1) wait_dma(kt + 2 < kt1 ? 1 : 0);  // step kt + 1 (group 0)
+        pp_barrier();
+    }
+    if (!grp) pp_barrier();  // (group 1's extra barrier at the start)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();  // no DMA outstanding; every wave is done with the stages
+    if (tail) {
+        f4* slab = (f4*)(p.ws + ((int64_t)(t - p.dp_tiles) * p.tail_split + slice) * (BM * BN));
+#pragma unroll
+        for (int i = 0; i < 4; i++)
+#pragma unroll
+            for (int j = 0; j < FN; j++) slab[((wave * 4 + i) * FN + j) * 64 + lane] = acc[i][j] + accx[i][j] * 0.00048828125f;
+        return;
+    }
+    float* E = (float*)smem;
+#pragma unroll
+    for (int ph = 0; ph < BM / ER; ph++) {
+        if (ph) __syncthreads();
+        if (wmg * 64 / ER == ph) {
+#pragma unroll
+            for (int j = 0; j < FN; j++)
+#pragma unroll
+                for (int i = 0; i < 4; i++) {
+                    const f4 v = acc[i][j] + accx[i][j] * 0.00048828125f;
+#pragma unroll
+                    for (int q = 0; q < 4; q++)
+                        E[(wmg * 64 - ph * ER + i * 16 + 4 * (lane >> 4) + q) * LDE + wn * 64 + j * 16 + (lane & 15)] = v[q];
+                }
+        }
+        __syncthreads();
+        tile_epilogue<ER, BN, NT>(p, E, m0 + ph * ER, n0);
+    }
+}
+
 // tail tiles: 8 workgroups per tile, each sums the K slices of one 16-row block (the 8 fragments
 // with that wm, i: 2 f4 per thread) in slice order (deterministic) into an LDS image of the
 // block, then the shared epilogue over those 16 rows
@@ -327,16 +503,21 @@ int device_cu_count() {
 
 template <int BM, int BN, int NW>
 void launch_t(GemmX3Params p, hipStream_t st);
+void launch_pp(GemmX3Params p, hipStream_t st);
 
 // 256 x 128 tiles of 8 waves for large M: a third less operand traffic per FLOP than 128 x 128,
 // but one workgroup per CU whose 8 waves share every barrier -- measured slower on ViT-L c4
 // (6.3-6.5k vs 6.8k faces/s, profiles/r02o_*), so opt-in (VTF_GEMM_BIG=1)
-static bool big_tiles() {
-    static bool on = [] {
+// VTF_GEMM_BIG: 1 = 256 x 128 / 8 waves / 2 stages; 5 = the ping-pong kernel (k_gemm_x3_pp); 0 =
+// 128 x 128 / 4 waves / 2 stages at two workgroups per CU.  c4 on one box (scripts/r05_gemm.sh):
+// 0: 7.12-7.39k, ping-pong 7.24k, 256 x 128 / 3 stages 6.77-6.78k, 128 x 128 at one workgroup
+// per CU with 3 / 4 stages 5.78-5.79k / 5.72-5.76k faces/s (profiles/r05_gemm_variants_ab.txt)
+static int big_tiles() {
+    static int v = [] {
         const char* e = std::getenv("VTF_GEMM_BIG");
-        return e && std::atoi(e) == 1;
+        return e ? std::atoi(e) : 0;
     }();
-    return on;
+    return v;
 }
 
 void launch_gemm_x3(const GemmX3Params& p0, hipStream_t st) {
@@ -346,7 +527,9 @@ void launch_gemm_x3(const GemmX3Params& p0, hipStream_t st) {
     VTF_CHECK(!p0.res || (p0.ldr >= p0.N && p0.ldr % 4 == 0), VTF_E_ARG, "gemm_x3: residual stride");
     GemmX3Params p = p0;
     p.group_m = gemm_group_m();
-    if (p.M >= 4096 && big_tiles()) launch_t<256, 128, 8>(p, st);
+    const int big = p.M >= 4096 ? big_tiles() : 0;
+    if (big == 1) launch_t<256, 128, 8>(p, st);
+    else if (big == 5) launch_pp(p, st);
     else launch_t<128, 128, 4>(p, st);
 }
 
@@ -374,6 +557,29 @@ void launch_t(GemmX3Params p, hipStream_t st) {
     const int64_t grid = (int64_t)p.dp_tiles + (int64_t)(T - p.dp_tiles) * p.tail_split;
     k_gemm_x3<BM, BN, NW><<<(unsigned)grid, 64 * NW, 0, st>>>(p);
     if (p.dp_tiles < T) k_gemm_x3_tail<BM, BN, NW><<<(unsigned)(T - p.dp_tiles) * (BM / 16), 256, 0, st>>>(p);
+}
+
+// the ping-pong kernel on the tile / tail plan of the 256 x 128 tiles at one workgroup per CU
+void launch_pp(GemmX3Params p, hipStream_t st) {
+    constexpr int BM = 256, BN = 128;
+    p.gx = (int)cdiv(p.M, BM);
+    p.gy = (int)cdiv(p.N, BN);
+    const int T = p.gx * p.gy, KT = p.K / 32;
+    const int slots = device_cu_count();
+    p.dp_tiles = T;
+    p.tail_split = 1;
+    if (gemm_tail_on() && T > slots) {
+        const int R = T % slots;
+        const int S = R > 0 ? std::min(slots / R, KT / 4) : 0;
+        if (R > 0 && R <= slots / 2 && S >= 2) {
+            p.dp_tiles = T - R;
+            p.tail_split = S;
+            p.ws = tail_ws(st, (size_t)R * S * BM * BN * 4);
+        }
+    }
+    const int64_t grid = (int64_t)p.dp_tiles + (int64_t)(T - p.dp_tiles) * p.tail_split;
+    k_gemm_x3_pp<<<(unsigned)grid, 512, 0, st>>>(p);
+    if (p.dp_tiles < T) k_gemm_x3_tail<BM, BN, 8><<<(unsigned)(T - p.dp_tiles) * (BM / 16), 256, 0, st>>>(p);
 }
 
 void launch_split_rows(const float* x, int64_t rows, int K, int64_t ld, void* out, int* ovf, hipStream_t st) {
