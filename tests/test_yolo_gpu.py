@@ -134,3 +134,25 @@ def test_bf16_detect_close(g):
         assert rel < 0.1
     b, s, _ = m(synth.make_frames(2, seed=0))
     print('bf16 counts', [len(t) for t in s], 'fp32 golden', list(g['counts']))
+
+
+@pytest.mark.parametrize('hw', [(720, 1280), (342, 608), (100, 160), (1080, 1920)])
+def test_x3_stem_head_bit_identical(hw, monkeypatch):
+    """k_yolo_stem (csrc/yolo.hip: the letterbox computed inside Darknet's first conv, its canvas
+    kept in LDS) runs k_letterbox_s3's arithmetic and k_conv_dma3's MFMA chains / epilogue for that
+    layer: the detections equal the letterbox -> k_conv_dma3 path (VTF_YOLO_STEM=0) bit for bit,
+    on resized (720p, 1080p, upsampled 100x160) and unresized (342x608, the canvas size) frames."""
+    from videotofaces.detectors.yolo import YOLOv3
+    from videotofaces import synth
+    m = YOLOv3('cuda:0', precision='x3')
+    fr = synth.make_frames(3, hw[0], hw[1], seed=21)
+    monkeypatch.setenv('VTF_YOLO_STEM', '1')
+    b1, s1, c1 = m(fr)
+    monkeypatch.setenv('VTF_YOLO_STEM', '0')
+    b0, s0, c0 = m(fr)
+    print('stem head: boxes per frame', [len(t) for t in s1])
+    assert [len(t) for t in s1] == [len(t) for t in s0]
+    for x, y in zip(b1, b0):
+        np.testing.assert_array_equal(x, y)
+    for x, y in zip(s1, s0):
+        np.testing.assert_array_equal(x, y)

@@ -18,6 +18,7 @@
 //              then top-100 and scale_boxes (bbox.py:63-67) in k_yolo_final.
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <numeric>
 #include <vector>
@@ -273,6 +274,136 @@ __global__ void k_letterbox_s3(const uint8_t* __restrict__ frames, int64_t fstri
     s3_store8(out + i * 48, v);
 }
 
+// ------------------------------------------------------------------ stem head (bf16x3)
+// The letterbox (k_letterbox_s3's arithmetic: OpenCV INTER_LINEAR restated, / 255, the S3 split)
+// straight into Darknet's first conv (3x3, stride 1, pad 1, 3 -> 32, BN + LeakyReLU(0.1)):
+// a tile of 8 x 16 canvas pixels computes its 10 x 18 letterboxed input patch into LDS (48-byte
+// S3 pixels: a 16-lane group reads 16 consecutive pixels over all 64 banks) and runs the conv from
+// there with k_conv_dma3's MFMA chains (the same k-steps, lane -> k map, six products per step in
+// the same order, acc + accx, the same epilogue and S3 stores): bit-identical to letterbox ->
+// k_conv_dma3, without the canvas (329 MB per 32 720p frames) going through HBM and with the
+// conv's small tiles at many workgroups per CU instead of 73 KB of DMA stages.
+constexpr int YS_TH = 8, YS_TW = 16, YS_PH = YS_TH + 2, YS_PW = YS_TW + 2, YS_COUT = 32;
+typedef __attribute__((ext_vector_type(4))) float f4;
+
+struct YStemP {
+    const uint8_t* frames;
+    int64_t fstride, rstride;
+    int H, W, h, w, Hp, Wp, tiles_x, tiles_per_img;
+    const char* w3;  // conv weights, S3 [32][9 chunks][48 B] (k = tap * 8 + c)
+    const float *al, *be;
+    char* out;       // S3 [B][Hp][Wp][32]
+};
+
+__global__ __launch_bounds__(256) void k_yolo_stem(YStemP p) {
+    __shared__ __attribute__((aligned(16))) char P[YS_PH * YS_PW * 48];
+    __shared__ __attribute__((aligned(16))) float E[YS_TH * YS_TW * (YS_COUT + 4)];
+    __shared__ int4 ycf[YS_PH], xcf[YS_PW];  // lin_coef (s0, s1, c0, c1); x: the edge flag in s1's sign
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int b = blockIdx.x / p.tiles_per_img, t = blockIdx.x - b * p.tiles_per_img;
+    const int ty = t / p.tiles_x, oy0 = ty * YS_TH, ox0 = (t - ty * p.tiles_x) * YS_TW;
+    const bool direct = p.h == p.H && p.w == p.W;
+    if (!direct) {
+        if (tid < YS_PH) {
+            const int dy = min(max(oy0 - 1 + tid, 0), p.h - 1);
+            int s0, s1, c0, c1;
+            bool e;
+            lin_coef(dy, p.H, p.h, s0, s1, c0, c1, e);
+            ycf[tid] = make_int4(s0, s1, c0, c1);
+        } else if (tid >= 64 && tid < 64 + YS_PW) {
+            const int dx = min(max(ox0 - 1 + tid - 64, 0), p.w - 1);
+            int s0, s1, c0, c1;
+            bool e;
+            lin_coef(dx, p.W, p.w, s0, s1, c0, c1, e);
+            xcf[tid - 64] = make_int4(s0, e ? -1 - s1 : s1, c0, c1);
+        }
+    }
+    __syncthreads();
+    const uint8_t* base = p.frames + (int64_t)b * p.fstride;
+    for (int e = tid; e < YS_PH * YS_PW; e += 256) {
+        const int r = e / YS_PW, c = e - r * YS_PW;
+        const int dy = oy0 - 1 + r, dx = ox0 - 1 + c;
+        float v[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+        if (dy >= 0 && dx >= 0 && dy < p.h && dx < p.w) {
+            int u[3];
+            if (direct) {
+                const uint8_t* q = base + (int64_t)dy * p.rstride + dx * 3;
+                u[0] = q[0], u[1] = q[1], u[2] = q[2];
+            } else {
+                const int4 yc = ycf[r], xc = xcf[c];
+                const bool ex = xc.y < 0;
+                const int sx1 = ex ? -1 - xc.y : xc.y;
+                const uint8_t* r0 = base + (int64_t)yc.x * p.rstride;
+                const uint8_t* r1 = base + (int64_t)yc.y * p.rstride;
+#pragma unroll
+                for (int ch = 0; ch < 3; ch++) u[ch] = blob_lin(r0, r1, xc.x, sx1, xc.z, xc.w, ex, yc.z, yc.w, ch);
+            }
+            for (int oc = 0; oc < 3; oc++) v[oc] = __fdiv_rn((float)u[2 - oc], 255.f);
+        }
+        s3_store8(P + e * 48, v);
+    }
+    // B (weights): lane (channel 16 j + (lane & 15), chunk 4 s + (lane >> 4)), three planes
+    const int g = lane >> 4, n16 = lane & 15;
+    f4 acc[2][2], accx[2][2];
+#pragma unroll
+    for (int i = 0; i < 2; i++)
+#pragma unroll
+        for (int j = 0; j < 2; j++) acc[i][j] = accx[i][j] = f4{0.f, 0.f, 0.f, 0.f};
+    __syncthreads();
+#pragma unroll
+    for (int s = 0; s < 3; s++) {
+        const int tap = 4 * s + g, ky = tap / 3, kx = tap - 3 * ky;
+        bf16x8 bw[2][3];
+#pragma unroll
+        for (int j = 0; j < 2; j++)
+#pragma unroll
+            for (int pl = 0; pl < 3; pl++)
+                bw[j][pl] = tap < 9 ? *(const bf16x8*)(p.w3 + ((16 * j + n16) * 9 + tap) * 48 + 16 * pl) : bf16x8{};
+#pragma unroll
+        for (int i = 0; i < 2; i++) {
+            // fragment i of this wave: tile row 2 wave + i, pixel n16 of it
+            bf16x8 a[3];
+            const char* q = P + ((2 * wave + i + ky) * YS_PW + n16 + kx) * 48;
+#pragma unroll
+            for (int pl = 0; pl < 3; pl++) a[pl] = tap < 9 ? *(const bf16x8*)(q + 16 * pl) : bf16x8{};
+#pragma unroll
+            for (int j = 0; j < 2; j++) {
+                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], bw[j][0], acc[i][j], 0, 0, 0);
+                accx[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], bw[j][1], accx[i][j], 0, 0, 0);
+                accx[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[1], bw[j][0], accx[i][j], 0, 0, 0);
+                accx[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], bw[j][2], accx[i][j], 0, 0, 0);
+                accx[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[1], bw[j][1], accx[i][j], 0, 0, 0);
+                accx[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[2], bw[j][0], accx[i][j], 0, 0, 0);
+            }
+        }
+    }
+    constexpr int LDE = YS_COUT + 4;
+#pragma unroll
+    for (int i = 0; i < 2; i++)
+#pragma unroll
+        for (int j = 0; j < 2; j++) {
+            const f4 v = acc[i][j] + accx[i][j];
+#pragma unroll
+            for (int q = 0; q < 4; q++) E[(16 * (2 * wave + i) + 4 * g + q) * LDE + 16 * j + n16] = v[q];
+        }
+    __syncthreads();
+    // conv_epilogue8 (BN fmaf, LeakyReLU(0.1)) and the S3 store of 8 channels per item
+    for (int it = tid; it < YS_TH * YS_TW * (YS_COUT / 8); it += 256) {
+        const int m = it >> 2, c8 = it & 3;
+        const int oy = oy0 + (m >> 4), ox = ox0 + (m & 15);
+        float v[8];
+#pragma unroll
+        for (int e = 0; e < 8; e++) {
+            float x = E[m * LDE + 8 * c8 + e];
+            x = fmaf(x, p.al[8 * c8 + e], p.be[8 * c8 + e]);
+            x = x > 0.f ? x : x * 0.1f;
+            v[e] = x;
+        }
+        const int64_t gm = ((int64_t)b * p.Hp + oy) * p.Wp + ox;
+        s3_store8(p.out + (gm * YS_COUT + 8 * c8) / 8 * 48, v);
+    }
+}
+
 // NCHW fp32 (C <= 8) -> split-triple NHWC with 8 channels (vtf_yolo_net's input)
 __global__ void k_nchw_to_s3(const float* __restrict__ in, int64_t N, int C, int H, int W, char* __restrict__ out) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -364,8 +495,22 @@ static void unit(Yolo& Y, int li, const void* in, int in_cs, int N, int H, int W
     Y.launches++;
 }
 
-// x0: NHWC [B,Hp,Wp,8] -> maps NHWC fp32 [B,Hp/32,Wp/32,18], [.., /16, ..], [.., /8, ..]
-static void net(Yolo& Y, const void* x0, int B, int Hp, int Wp, float* maps[3]) {
+// the frames a fused stem head letterboxes itself (bf16x3 mode)
+struct YStemIn {
+    const uint8_t* frames;
+    int64_t fstride, rstride;
+    int H, W, h, w;
+};
+
+// bf16x3 stem head on by default (VTF_YOLO_STEM=0: letterbox + the first conv's launch)
+static bool stem_on() {
+    const char* e = std::getenv("VTF_YOLO_STEM");  // (read per call: tests switch it in-process)
+    return !(e && std::atoi(e) == 0);
+}
+
+// x0: NHWC [B,Hp,Wp,8] -> maps NHWC fp32 [B,Hp/32,Wp/32,18], [.., /16, ..], [.., /8, ..]; or
+// (stem, bf16x3 mode) the frames, letterboxed inside the first conv's launch
+static void net(Yolo& Y, const void* x0, int B, int Hp, int Wp, float* maps[3], const YStemIn* stem = nullptr) {
     VTF_CHECK(Hp % 32 == 0 && Wp % 32 == 0 && Hp > 0 && Wp > 0, VTF_E_ARG, "yolo: input must be padded to x32");
     const size_t es = Y.es();
     const size_t full = (size_t)B * Hp * Wp * 32;
@@ -384,7 +529,33 @@ static void net(Yolo& Y, const void* x0, int B, int Hp, int Wp, float* maps[3]) 
     if (Y.prof) VTF_HIP(hipEventRecord(Y.ev0, Y.st));
     int li = 0;
     // Darknet53 (yolo.py:34-54)
-    unit(Y, li++, x0, 8, B, Hp, Wp, A, 32, 0);
+    if (stem) {
+        const YUnit& u = Y.U[0];
+        VTF_CHECK(Y.x3 && u.k == 3 && u.s == 1 && u.cin_pad == 8 && u.cout_p == 32 && !u.bias, VTF_E_ARG,
+                  "yolo: stem head shape");
+        YStemP sp;
+        sp.frames = stem->frames;
+        sp.fstride = stem->fstride;
+        sp.rstride = stem->rstride;
+        sp.H = stem->H;
+        sp.W = stem->W;
+        sp.h = stem->h;
+        sp.w = stem->w;
+        sp.Hp = Hp;
+        sp.Wp = Wp;
+        sp.tiles_x = Wp / YS_TW;
+        sp.tiles_per_img = sp.tiles_x * (Hp / YS_TH);
+        sp.w3 = (const char*)u.w;
+        sp.al = u.alpha;
+        sp.be = u.beta;
+        sp.out = A;
+        k_yolo_stem<<<(unsigned)((int64_t)B * sp.tiles_per_img), 256, 0, Y.st>>>(sp);
+        Y.flops += 2.0 * (double)B * Hp * Wp * u.cout * 9 * u.cin;
+        Y.launches++;
+        li++;
+    } else {
+        unit(Y, li++, x0, 8, B, Hp, Wp, A, 32, 0);
+    }
     char* cur = A;
     int cur_cs = 32, H = Hp, W = Wp;
     const int L[5] = {1, 2, 8, 8, 4}, C[5] = {64, 128, 256, 512, 1024};
@@ -643,11 +814,17 @@ static void detect(Yolo& Y, const uint8_t* frames, int on_dev, int B, int H, int
     int h, w;
     used_size(H, W, h, w);
     const int Hp = (h + 31) / 32 * 32, Wp = (w + 31) / 32 * 32;
-    void* x0 = Y.ar.get(105, (size_t)B * Hp * Wp * 8 * Y.es());
-    launch_letterbox(fr, fstride, rstride, B, H, W, h, w, Hp, Wp, Y.bf16, x0, st, Y.x3);
     float* maps[3];
-    maps_alloc(Y, B, Hp, Wp, maps);
-    net(Y, x0, B, Hp, Wp, maps);
+    if (Y.x3 && stem_on()) {
+        maps_alloc(Y, B, Hp, Wp, maps);
+        const YStemIn si{fr, fstride, rstride, H, W, h, w};
+        net(Y, nullptr, B, Hp, Wp, maps, &si);
+    } else {
+        void* x0 = Y.ar.get(105, (size_t)B * Hp * Wp * 8 * Y.es());
+        launch_letterbox(fr, fstride, rstride, B, H, W, h, w, Hp, Wp, Y.bf16, x0, st, Y.x3);
+        maps_alloc(Y, B, Hp, Wp, maps);
+        net(Y, x0, B, Hp, Wp, maps);
+    }
     postprocess(Y, maps, B, Hp, Wp, H, W, out);
 }
 
