@@ -613,6 +613,121 @@ __global__ __launch_bounds__(256, 2) void k_conv_patch(CPatchP p) {
 }
 
 // ---------------------------------------------------------------------------------------------
+// Block8 branch 1 middle (facenet.py:64-68): the 1x3 then the 3x1 conv (192 -> 192, BN + ReLU
+// each) on the 3x3 maps as ONE launch for G = 7 images per workgroup (63 pixel rows = 4 MFMA row
+// fragments): the branch head's output T1 is staged in LDS, the 1x3 conv's output stays in LDS
+// and the 3x1 conv writes CAT[:, 192:384].  Each output's MFMA chain is the unfused launches'
+// (k_conv_dma MODE 0 without split-K: nine 64-deep k-steps of (tap, 64-channel block), two
+// v_mfma_f32_16x16x32_bf16 per step, the same lane -> k map; taps in the zero padding run with
+// zero A), and the epilogue is its fmaf(acc, alpha, beta) + ReLU: bit-identical to the two launches
+// (and their split-K tails) it replaces.  Waves own 3 of the 12 output-channel fragments and read
+// their weight fragments straight from L2.
+constexpr int B8_C = 192, B8_RS = B8_C * 2 + 16;  // LDS row: 384 B + 16 pad
+
+struct B8P {
+    const __bf16* t1;   // [N][9][192]
+    __bf16* cat;        // [N][9][384]
+    const __bf16 *wa, *wb;  // [192][3 * 192]: 1x3 (k = kx * 192 + ci), 3x1 (k = ky * 192 + ci)
+    const float *ala, *bea, *alb, *beb;
+    int N;
+};
+
+template <int B8_G>
+__global__ __launch_bounds__(256) void k_block8_mid(B8P p) {
+    constexpr int B8_PX = 9 * B8_G, NF = (B8_PX + 15) / 16, NR = 16 * NF;
+    __shared__ __attribute__((aligned(16))) char X[NR * B8_RS];   // T1 rows (padding rows: zeros)
+    __shared__ __attribute__((aligned(16))) char Y[NR * B8_RS];   // 1x3 output rows
+    __shared__ __attribute__((aligned(16))) char Z[16];           // zero fragment source
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int n0 = blockIdx.x * B8_G, ng = min(B8_G, p.N - n0);
+    for (int e = tid; e < NR * (B8_C / 8); e += 256) {
+        const int r = e / (B8_C / 8), c = e - r * (B8_C / 8);
+        bf16x8 v = {};
+        if (r < 9 * ng) v = *(const bf16x8*)(p.t1 + ((int64_t)n0 * 9 + r) * B8_C + 8 * c);
+        *(bf16x8*)(X + r * B8_RS + 16 * c) = v;
+    }
+    if (tid == 0) *(uint4*)Z = make_uint4(0u, 0u, 0u, 0u);
+    __syncthreads();
+    const int r16 = lane & 15, g = lane >> 4;
+    // the lane's A rows: pixel 16 i + r16 (image (.) / 9, y, x) of fragment i
+    int py[NF], px[NF];
+#pragma unroll
+    for (int i = 0; i < NF; i++) {
+        const int pix = 16 * i + r16, q = pix % 9;
+        py[i] = pix < B8_PX ? q / 3 : -100;  // the padding row reads zeros for every tap
+        px[i] = q % 3;
+    }
+    auto conv = [&](const char* src, const __bf16* w, const float* al, const float* be, bool vertical, int stage) {
+        f4 acc[NF][3];
+#pragma unroll
+        for (int i = 0; i < NF; i++)
+#pragma unroll
+            for (int j = 0; j < 3; j++) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
+        const int nb = 48 * wave;  // this wave's first output channel
+        // weight fragments B8_PF k-steps ahead (the loop is unrolled: a register ring with static
+        // indices), so the L2 latency of the streamed weights hides behind the MFMAs
+        constexpr int B8_PF = 3;
+        bf16x8 wr0[B8_PF][3], wr1[B8_PF][3];
+        auto load_w = [&](int s, bf16x8 (&d0)[3], bf16x8 (&d1)[3]) {
+            const int tap = s / 3, cb = s - 3 * tap;
+#pragma unroll
+            for (int j = 0; j < 3; j++) {
+                const __bf16* wr = w + (int64_t)(nb + 16 * j + r16) * (3 * B8_C) + tap * B8_C + 64 * cb + 8 * g;
+                d0[j] = *(const bf16x8*)wr;
+                d1[j] = *(const bf16x8*)(wr + 32);
+            }
+        };
+#pragma unroll
+        for (int q = 0; q < B8_PF; q++) load_w(q, wr0[q], wr1[q]);
+#pragma unroll
+        for (int s = 0; s < 9; s++) {
+            const int tap = s / 3, cb = s - 3 * tap;  // k = tap * 192 + 64 cb + ..
+            bf16x8 b0[3], b1[3];
+#pragma unroll
+            for (int j = 0; j < 3; j++) {
+                b0[j] = wr0[s % B8_PF][j];
+                b1[j] = wr1[s % B8_PF][j];
+            }
+            if (s + B8_PF < 9) load_w(s + B8_PF, wr0[s % B8_PF], wr1[s % B8_PF]);
+#pragma unroll
+            for (int i = 0; i < NF; i++) {
+                const int yy = vertical ? py[i] + tap - 1 : py[i], xx = vertical ? px[i] : px[i] + tap - 1;
+                const bool ok = yy >= 0 && yy < 3 && xx >= 0 && xx < 3;
+                const int row = 16 * i + r16 + (vertical ? 3 * (tap - 1) : tap - 1);  // same image: +-3 / +-1
+                const char* a = ok ? src + row * B8_RS + (64 * cb + 8 * g) * 2 : Z;
+                const bf16x8 a0 = *(const bf16x8*)a;
+                const bf16x8 a1 = ok ? *(const bf16x8*)(a + 64) : bf16x8{};
+#pragma unroll
+                for (int j = 0; j < 3; j++) {
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, b0[j], acc[i][j], 0, 0, 0);
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1, b1[j], acc[i][j], 0, 0, 0);
+                }
+            }
+        }
+        // BN + ReLU -> bf16: stage 0 into the LDS rows of Y, stage 1 into CAT[:, 192:384]
+#pragma unroll
+        for (int j = 0; j < 3; j++) {
+            const int ch = nb + 16 * j + r16;
+            const float a = al[ch], b = be[ch];
+#pragma unroll
+            for (int i = 0; i < NF; i++)
+#pragma unroll
+                for (int q = 0; q < 4; q++) {
+                    const int pix = 16 * i + 4 * g + q;
+                    const __bf16 v = (__bf16)relu_bf(fmaf(acc[i][j][q], a, b));
+                    if (stage == 0 && pix < NR)
+                        *(__bf16*)(Y + pix * B8_RS + ch * 2) = v;
+                    else if (pix < 9 * ng)
+                        p.cat[((int64_t)n0 * 9 + pix) * (2 * B8_C) + B8_C + ch] = v;
+                }
+        }
+    };
+    conv(X, p.wa, p.ala, p.bea, false, 0);  // 1x3 (pad (0, 1))
+    __syncthreads();
+    conv(Y, p.wb, p.alb, p.beb, true, 1);   // 3x1 (pad (1, 0))
+}
+
+// ---------------------------------------------------------------------------------------------
 // FaceNet stem head: blobFromImages of the device crops (k_blob's INTER_LINEAR and normalisation,
 // facenet.py:179) straight into conv2d_1a (3x3 stride 2, 3 -> 32, BN + ReLU, facenet.py:126): a
 // tile of 8 x 16 output pixels computes its 17 x 33 blob patch into LDS (8 bf16 per pixel, the
@@ -905,6 +1020,38 @@ void launch_stem_head(const uint8_t* frames, int F, int H, int W, int64_t fstrid
     p.tiles_x = (SH_OUT + SH_TW - 1) / SH_TW;
     p.tiles_per_img = p.tiles_x * ((SH_OUT + SH_TH - 1) / SH_TH);
     k_stem_head<<<(unsigned)(N * p.tiles_per_img), 256, 0, st>>>(p);
+    VTF_HIP(hipGetLastError());
+}
+
+}  // namespace vtf
+
+namespace vtf {
+
+// Block8 branch-1 middle convs (bf16): T1 [N, 3, 3, 192] -> CAT[:, :, :, 192:384]
+void launch_block8_mid(const void* t1, void* cat, int N, const void* wa, const float* ala, const float* bea,
+                       const void* wb, const float* alb, const float* beb, hipStream_t st) {
+    if (N <= 0) return;
+    B8P p;
+    p.t1 = (const __bf16*)t1;
+    p.cat = (__bf16*)cat;
+    p.wa = (const __bf16*)wa;
+    p.wb = (const __bf16*)wb;
+    p.ala = ala;
+    p.bea = bea;
+    p.alb = alb;
+    p.beb = beb;
+    p.N = N;
+    // images per workgroup (VTF_B8_G: 1, 3 or 7, experiments)
+    static const int gsel = [] {
+        const char* e = std::getenv("VTF_B8_G");
+        return e ? std::atoi(e) : 1;
+    }();
+    if (gsel == 7)
+        k_block8_mid<7><<<(unsigned)((N + 6) / 7), 256, 0, st>>>(p);
+    else if (gsel == 3)
+        k_block8_mid<3><<<(unsigned)((N + 2) / 3), 256, 0, st>>>(p);
+    else
+        k_block8_mid<1><<<(unsigned)N, 256, 0, st>>>(p);
     VTF_HIP(hipGetLastError());
 }
 

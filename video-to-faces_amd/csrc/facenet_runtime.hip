@@ -32,6 +32,9 @@ void launch_stem_head(const uint8_t* frames, int F, int H, int W, int64_t fstrid
                       const int32_t* d_crops, int N, const void* w, const float* al, const float* be, void* out,
                       hipStream_t st);
 
+void launch_block8_mid(const void* t1, void* cat, int N, const void* wa, const float* ala, const float* bea,
+                       const void* wb, const float* alb, const float* beb, hipStream_t st);
+
 // device crops of uint8 frames (vtf_facenet_encode_crops): the bf16 fused mode runs the blob and
 // conv2d_1a as one launch (k_stem_head)
 struct StemIn {
@@ -460,9 +463,17 @@ static void forward(Facenet& F, const void* x, int N, float* emb, const StemIn* 
         bool last = k == 5;
         conv_merged(F, li, X, N, CAT, 384, 0, 192, T1, 192, 0);
         li += 2;
-        t1 = Act{T1, X.H, X.W, 192};
-        conv(F, li++, t1, N, T2, 192, 0, nullptr, 1.f, true, &t2);
-        conv(F, li++, t2, N, CAT, 384, 192);
+        const char* b8e = std::getenv("VTF_B8_MID");  // 0: the two launches (A/B; read per forward)
+        if (F.bf16 && fused_blocks() && !(b8e && std::atoi(b8e) == 0) && X.H == 3 && X.W == 3 && X.C == 1792) {
+            // the branch's 1x3 and 3x1 convs as one launch (facenet_fused.hip)
+            const Layer &la = F.L[li], &lb = F.L[li + 1];
+            launch_block8_mid(T1, CAT, N, la.w, la.alpha, la.beta, lb.w, lb.alpha, lb.beta, F.st);
+            li += 2;
+        } else {
+            t1 = Act{T1, X.H, X.W, 192};
+            conv(F, li++, t1, N, T2, 192, 0, nullptr, 1.f, true, &t2);
+            conv(F, li++, t2, N, CAT, 384, 192);
+        }
         conv(F, li++, Act{CAT, X.H, X.W, 384}, N, Y, 1792, 0, X.p, last ? 1.0f : 0.20f, !last);
         swap(1792);
     }
