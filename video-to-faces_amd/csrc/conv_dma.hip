@@ -102,6 +102,33 @@ __device__ inline void dma_epilogue(const ConvParams& p, const float* E, int row
     if (p.out_sp && p.ovf && __ballot(bad) && (threadIdx.x & 63) == 0) atomicOr(p.ovf, 1);
 }
 
+// the same epilogue over `cols` columns [c_lo, c_lo + cols) of the LDS tile image E [rows][BN + 4]
+template <typename T, int BN, int COLS>
+__device__ inline void dma_epilogue_cols(const ConvParams& p, const float* E, int rows, int64_t m0, int n0, int c_lo) {
+    constexpr int LDE = BN + 4, G = COLS / 8;
+    static_assert(256 % G == 0, "epilogue groups");
+    const int tid = threadIdx.x, g = tid % G, c0 = n0 + c_lo + 8 * g;
+    bool bad = false;
+    if (c0 < p.Cout) {
+        float b8[8], al8[8], be8[8], pr8[8];
+#pragma unroll
+        for (int e = 0; e < 8; e++) {
+            b8[e] = p.bias ? p.bias[c0 + e] : 0.f;
+            al8[e] = p.alpha ? p.alpha[c0 + e] : 1.f;
+            be8[e] = p.alpha ? p.beta[c0 + e] : 0.f;
+            pr8[e] = p.prelu ? p.prelu[c0 + e] : 0.f;
+        }
+        for (int r = tid / G; r < rows; r += 256 / G) {
+            const int64_t m = m0 + r;
+            if (m >= p.M) break;
+            const f4 lo = *(const f4*)(E + r * LDE + c_lo + 8 * g), hi = *(const f4*)(E + r * LDE + c_lo + 8 * g + 4);
+            float v[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+            conv_epilogue8<T>(p, m, c0, v, b8, al8, be8, pr8, &bad);
+        }
+    }
+    if (p.out_sp && p.ovf && __ballot(bad) && (threadIdx.x & 63) == 0) atomicOr(p.ovf, 1);
+}
+
 // s_waitcnt vmcnt(N) then the workgroup barrier (LDS reads stay after it)
 template <int N>
 __device__ inline void wait_vm_barrier() {
@@ -917,20 +944,23 @@ __global__ __launch_bounds__(256, 2) void k_conv_dma3(ConvParams p) {
     dma_epilogue<float, BN>(p, E, BM, m0, n0);
 }
 
-// tail tiles: one workgroup per (tile, 16-row block) sums the block's K slices in slice order
-// (deterministic) into an LDS image, then the epilogue of those 16 rows
+// tail tiles: one workgroup per (tile, 16-row block, 64-column half when BN = 128) sums the
+// block's K slices in slice order (deterministic) into an LDS image, then the epilogue of those
+// rows (one f4 of partial sums per thread)
 template <int MODE, int BM, int BN, int WGM, int OCC, int NSTG>
 __global__ __launch_bounds__(256) void k_conv_dma_tail(ConvParams p) {
     using C = DCfg<MODE, BM, BN, WGM, OCC, NSTG>;
     using T = typename std::conditional<MODE == 0, __bf16, float>::type;
-    constexpr int NB = BM / 16, FM = C::FM, FN = C::FN, LDE = C::LDE;
+    constexpr int NH = BN * 4 / 256 > 1 ? BN * 4 / 256 : 1;  // workgroups per 16-row block
+    constexpr int NB = BM / 16 * NH, FM = C::FM, FN = C::FN, LDE = C::LDE;
     __shared__ __attribute__((aligned(16))) float E[16 * LDE];
     const int tid = threadIdx.x;
-    const int tt = blockIdx.x / NB, rb = blockIdx.x % NB, wm = rb / FM, i = rb % FM;
+    const int tt = blockIdx.x / NB, rb = (blockIdx.x % NB) / NH, hpart = (blockIdx.x % NB) % NH;
+    const int wm = rb / FM, i = rb % FM;
     int tile_m, tile_n;
     tile_of(p, p.dp_tiles + tt, tile_m, tile_n);
     const f4* s0 = (const f4*)(p.ws + (int64_t)tt * p.tail_split * (BM * BN));
-    for (int f = tid; f < BN * 4; f += 256) {  // fragments (wn, j) x 64 lanes of this 16-row block
+    for (int f = tid + 256 * hpart; f < min(BN * 4, 256 * (hpart + 1)); f += 256) {  // (wn, j) x 64 lanes
         const int wn = f / (FN * 64), j = (f / 64) % FN, lane = f & 63;
         const int idx = (((wm * C::WGN + wn) * FM + i) * FN + j) * 64 + lane;
         f4 v = s0[idx];
@@ -939,7 +969,12 @@ __global__ __launch_bounds__(256) void k_conv_dma_tail(ConvParams p) {
         for (int q = 0; q < 4; q++) E[(4 * (lane >> 4) + q) * LDE + wn * C::WN + j * 16 + (lane & 15)] = v[q];
     }
     __syncthreads();
-    dma_epilogue<T, BN>(p, E, 16, (int64_t)tile_m * BM + wm * C::WM + i * 16, tile_n * BN);
+    if constexpr (NH == 1) {
+        dma_epilogue<T, BN>(p, E, 16, (int64_t)tile_m * BM + wm * C::WM + i * 16, tile_n * BN);
+    } else {
+        // this workgroup's columns: [256 hpart / 4, + 64) of the tile (E rows keep the tile's stride)
+        dma_epilogue_cols<T, BN, 64>(p, E, 16, (int64_t)tile_m * BM + wm * C::WM + i * 16, tile_n * BN, 64 * hpart);
+    }
 }
 
 // per-(device, stream) tail workspace: grows x1.5.  An outgrown buffer may still be read by
@@ -1067,7 +1102,7 @@ void launch_dma_t(ConvParams p, hipStream_t st) {
     const int nt = T - p.dp_tiles;
     p.ws = nt ? dma_ws(st, (size_t)nt * p.tail_split * BM * BN * 4) : nullptr;
     k_conv_dma<MODE, BM, BN, WGM, OCC, NSTG><<<(unsigned)(p.dp_tiles + nt * p.tail_split), 256, 0, st>>>(p);
-    if (nt) k_conv_dma_tail<MODE, BM, BN, WGM, OCC, NSTG><<<(unsigned)(nt * (BM / 16)), 256, 0, st>>>(p);
+    if (nt) k_conv_dma_tail<MODE, BM, BN, WGM, OCC, NSTG><<<(unsigned)(nt * (BM / 16) * (BN > 64 ? BN / 64 : 1)), 256, 0, st>>>(p);
 }
 
 template <int Q, int BM, int BN, int WGM, int SPAN, int OCC, int NS>
@@ -1126,7 +1161,7 @@ void launch_dma3_t(ConvParams p, hipStream_t st) {
     p.ws = nt ? dma_ws(st, (size_t)nt * p.tail_split * BM * BN * 4) : nullptr;
     k_conv_dma3<BM, BN, WGM><<<(unsigned)(p.dp_tiles + nt * p.tail_split), 256, 0, st>>>(p);
     // the slab layout (wave, fragment, lane) is MODE 1's for the same tile / wave grid
-    if (nt) k_conv_dma_tail<1, BM, BN, WGM, 2, 2><<<(unsigned)(nt * (BM / 16)), 256, 0, st>>>(p);
+    if (nt) k_conv_dma_tail<1, BM, BN, WGM, 2, 2><<<(unsigned)(nt * (BM / 16) * (BN > 64 ? BN / 64 : 1)), 256, 0, st>>>(p);
 }
 
 }  // namespace

@@ -408,33 +408,31 @@ __global__ __launch_bounds__(512, 1) void k_gemm_x3_pp(GemmX3Params p) {
     }
 }
 
-// tail tiles: 8 workgroups per tile, each sums the K slices of one 16-row block (the 8 fragments
-// with that wm, i: 2 f4 per thread) in slice order (deterministic) into an LDS image of the
-// block, then the shared epilogue over those 16 rows
+// tail tiles: 2 x BM / 16 workgroups per tile, each sums the K slices of one 16-row x 64-column
+// block (the 4 fragments with that wm, i, wn: one f4 per thread) in slice order (deterministic)
+// into an LDS image of the block, then the shared epilogue over those 16 rows x 64 columns
 template <int BM, int BN, int NW>
 __global__ __launch_bounds__(256) void k_gemm_x3_tail(GemmX3Params p) {
-    constexpr int LDE = BN + 4, WM = 64, WN = BN / 2, FM = WM / 16, FN = WN / 16, NB = BM / 16;
+    constexpr int WN = BN / 2, LDE = WN + 4, WM = 64, FM = WM / 16, FN = WN / 16, NB = 2 * BM / 16;
     static_assert(BN == 128, "tail reduce layout: 16-row blocks of 2 waves x 4 fragments");
     __shared__ __attribute__((aligned(16))) float E[16 * LDE];
     const int tid = threadIdx.x;
-    const int tt = blockIdx.x / NB, part = blockIdx.x % NB, wm = part / FM, i = part % FM;
+    const int tt = blockIdx.x / NB, part = blockIdx.x % NB, wn = part & 1, wm = (part >> 1) / FM, i = (part >> 1) % FM;
     const int t = p.dp_tiles + tt;
     const int gm = p.group_m > 0 ? p.group_m : p.gx;
     const int span = gm * p.gy, first = (t / span) * gm, gsz = min(p.gx - first, gm);
     const int tile_m = first + (t % span) % gsz, tile_n = (t % span) / gsz;
     const f4* s0 = (const f4*)(p.ws + (int64_t)tt * p.tail_split * (BM * BN));
-#pragma unroll
-    for (int h = 0; h < 2; h++) {
-        const int f = tid + 256 * h;  // 512 f4: wn (1 bit) | j (2 bits) | lane (6 bits)
-        const int wn = f >> 8, j = (f >> 6) & 3, lane = f & 63;
+    {
+        const int j = tid >> 6, lane = tid & 63;  // 256 f4: j (2 bits) | lane (6 bits)
         const int idx = (((2 * wm + wn) * FM + i) * FN + j) * 64 + lane;
         f4 v = s0[idx];
         for (int z = 1; z < p.tail_split; z++) v = v + s0[(int64_t)z * (BM * BN / 4) + idx];
 #pragma unroll
-        for (int q = 0; q < 4; q++) E[(4 * (lane >> 4) + q) * LDE + wn * WN + j * 16 + (lane & 15)] = v[q];
+        for (int q = 0; q < 4; q++) E[(4 * (lane >> 4) + q) * LDE + j * 16 + (lane & 15)] = v[q];
     }
     __syncthreads();
-    tile_epilogue<16, BN>(p, E, (int64_t)tile_m * BM + wm * WM + i * 16, tile_n * BN);
+    tile_epilogue<16, WN>(p, E, (int64_t)tile_m * BM + wm * WM + i * 16, tile_n * BN + wn * WN);
 }
 
 // one thread per 8-element chunk
@@ -556,7 +554,7 @@ void launch_t(GemmX3Params p, hipStream_t st) {
     }
     const int64_t grid = (int64_t)p.dp_tiles + (int64_t)(T - p.dp_tiles) * p.tail_split;
     k_gemm_x3<BM, BN, NW><<<(unsigned)grid, 64 * NW, 0, st>>>(p);
-    if (p.dp_tiles < T) k_gemm_x3_tail<BM, BN, NW><<<(unsigned)(T - p.dp_tiles) * (BM / 16), 256, 0, st>>>(p);
+    if (p.dp_tiles < T) k_gemm_x3_tail<BM, BN, NW><<<(unsigned)(T - p.dp_tiles) * (2 * BM / 16), 256, 0, st>>>(p);
 }
 
 // the ping-pong kernel on the tile / tail plan of the 256 x 128 tiles at one workgroup per CU
@@ -579,7 +577,7 @@ void launch_pp(GemmX3Params p, hipStream_t st) {
     }
     const int64_t grid = (int64_t)p.dp_tiles + (int64_t)(T - p.dp_tiles) * p.tail_split;
     k_gemm_x3_pp<<<(unsigned)grid, 512, 0, st>>>(p);
-    if (p.dp_tiles < T) k_gemm_x3_tail<BM, BN, 8><<<(unsigned)(T - p.dp_tiles) * (BM / 16), 256, 0, st>>>(p);
+    if (p.dp_tiles < T) k_gemm_x3_tail<BM, BN, 8><<<(unsigned)(T - p.dp_tiles) * (2 * BM / 16), 256, 0, st>>>(p);
 }
 
 void launch_split_rows(const float* x, int64_t rows, int K, int64_t ld, void* out, int* ovf, hipStream_t st) {
