@@ -353,6 +353,9 @@ static void forward(Facenet& F, const void* x, int N, float* emb, const StemIn* 
     // stem (facenet.py:126-134)
     if (stem) {
         const Layer& l0 = F.L[0];
+        VTF_CHECK(F.bf16 && l0.cin_pad == 8 && l0.cout == 32 && l0.kh == 3 && l0.kw == 3 && l0.sh == 2 && l0.sw == 2 &&
+                      l0.ph == 0 && l0.pw == 0 && !l0.bias,
+                  VTF_E_ARG, "facenet: stem head shape");
         launch_stem_head(stem->frames, stem->F, stem->H, stem->W, stem->fstride, stem->rstride, stem->crops, N, l0.w,
                          l0.alpha, l0.beta, P0, F.st);
         b = Act{P0, 79, 79, 32};
@@ -467,6 +470,9 @@ static void forward(Facenet& F, const void* x, int N, float* emb, const StemIn* 
         if (F.bf16 && fused_blocks() && !(b8e && std::atoi(b8e) == 0) && X.H == 3 && X.W == 3 && X.C == 1792) {
             // the branch's 1x3 and 3x1 convs as one launch (facenet_fused.hip)
             const Layer &la = F.L[li], &lb = F.L[li + 1];
+            VTF_CHECK(la.cin_pad == 192 && la.cout == 192 && la.kh == 1 && la.kw == 3 && la.pw == 1 && lb.cin_pad == 192 &&
+                          lb.cout == 192 && lb.kh == 3 && lb.kw == 1 && lb.ph == 1,
+                      VTF_E_ARG, "facenet: Block8 middle shape");
             launch_block8_mid(T1, CAT, N, la.w, la.alpha, la.beta, lb.w, lb.alpha, lb.beta, F.st);
             li += 2;
         } else {

@@ -2116,10 +2116,12 @@ __global__ __launch_bounds__(64 * NWV) void k_cand_front_w24(const int3* __restr
                                                              float* __restrict__ out, int32_t* __restrict__ err,
                                                              int* __restrict__ ovf) {
     constexpr int S = 24, O = S - 2, P = (O - 3 + 1) / 2 + 1;  // 22, 11
-    constexpr int CS = (3 * O) | 1;                             // ring channel stride (odd: 32 banks)
+    // conv ring: [3 rows x 22 columns][32 channels + 4 pad] fp32, channel-contiguous so the pool
+    // reads 8 channels of a window position as two ds_read_b128 (72 scalar reads before)
+    constexpr int RS = 36;
     typedef __attribute__((ext_vector_type(4))) _Float16 h4;
     __shared__ h4 crop_s[NWV][2][S * S + 1];
-    __shared__ float cv_s[NWV][32 * CS];
+    __shared__ __attribute__((aligned(16))) float cv_s[NWV][3 * O * RS];
     const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63, lr = lane & 15, lk = lane >> 4;
     const int64_t k = (int64_t)blockIdx.x * NWV + wv;
     if (k >= n) return;  // (wave-uniform; no workgroup barrier below)
@@ -2215,8 +2217,8 @@ __global__ __launch_bounds__(64 * NWV) void k_cand_front_w24(const int3* __restr
                 if (q < npos) {
                     const int yq = r_lo + q / O;
                     const int slot = (yq % 3) * O + (q - (yq - r_lo) * O);
-                    cv[lr * CS + slot] = prelu(__builtin_fmaf(d0[i], 0.00048828125f, c0[i]) + bb0, aa0);
-                    cv[(16 + lr) * CS + slot] = prelu(__builtin_fmaf(d1[i], 0.00048828125f, c1[i]) + bb1, aa1);
+                    cv[slot * RS + lr] = prelu(__builtin_fmaf(d0[i], 0.00048828125f, c0[i]) + bb0, aa0);
+                    cv[slot * RS + 16 + lr] = prelu(__builtin_fmaf(d1[i], 0.00048828125f, c1[i]) + bb1, aa1);
                 }
             }
         }
@@ -2231,18 +2233,25 @@ __global__ __launch_bounds__(64 * NWV) void k_cand_front_w24(const int3* __restr
                 yo[d] = (min(2 * py + d, O - 1) % 3) * O;
             }
             f16x8 h0, h1;
+            float m[8];
+#pragma unroll
+            for (int dy = 0; dy < 3; dy++)
+#pragma unroll
+                for (int dx = 0; dx < 3; dx++) {
+                    const float* cr = cv + (yo[dy] + xo[dx]) * RS + 8 * cg;
+                    const f32x4 lo = *(const f32x4*)cr, hi = *(const f32x4*)(cr + 4);
+#pragma unroll
+                    for (int c = 0; c < 4; c++) {
+                        // (the same max order per channel as the scalar version: (0,0) first)
+                        m[c] = (dy | dx) ? fmaxf(m[c], lo[c]) : lo[c];
+                        m[4 + c] = (dy | dx) ? fmaxf(m[4 + c], hi[c]) : hi[c];
+                    }
+                }
 #pragma unroll
             for (int c8 = 0; c8 < 8; c8++) {
-                const float* cr = cv + (8 * cg + c8) * CS;
-                float m = cr[yo[0] + xo[0]];
-#pragma unroll
-                for (int dy = 0; dy < 3; dy++)
-#pragma unroll
-                    for (int dx = 0; dx < 3; dx++)
-                        if (dy | dx) m = fmaxf(m, cr[yo[dy] + xo[dx]]);
-                h0[c8] = (_Float16)m;
-                h1[c8] = (_Float16)((m - (float)h0[c8]) * 2048.f);
-                bad |= !(fabsf(m) < 16384.f);
+                h0[c8] = (_Float16)m[c8];
+                h1[c8] = (_Float16)((m[c8] - (float)h0[c8]) * 2048.f);
+                bad |= !(fabsf(m[c8]) < 16384.f);
             }
             f16x8* ch = (f16x8*)(o + (py * P + px) * 32 + 8 * cg);
             ch[0] = h0;
