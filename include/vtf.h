@@ -219,6 +219,17 @@ int vtf_ahash_crops(const uint8_t* d_frames, int F, int H, int W, int64_t frame_
  * d_arg int64 [N]. */
 int vtf_hamming_dedupe(const uint64_t* d_hashes, int64_t N, int32_t* d_min, int64_t* d_arg, void* hip_stream);
 
+/* ---------------------------------------------------------------- video frames
+ * The decode side of process_video (src/videotofaces/detection.py:68-111, which hands the
+ * detector cv2.VideoCapture / decord BGR frames [B,H,W,3]): planar YUV frames in HBM (as a
+ * YUV4MPEG2 stream stores them: Y [H][W], then U and V planes of the chroma size) -> uint8 BGR.
+ * d_yuv: n frames at in_frame_stride bytes; chroma 420 / 422 / 444 / 400 (mono, U = V = 128);
+ * full_range 0 = BT.601 limited range (OpenCV's COLOR_YUV2BGR_I420 integer transform), 1 = full
+ * range; chroma sampled nearest.  d_bgr: [n][H][W][3] at the given frame / row strides (bytes).
+ * Asynchronous on hip_stream. */
+int vtf_yuv_to_bgr(const uint8_t* d_yuv, int64_t n, int H, int W, int chroma, int full_range, int64_t in_frame_stride,
+                   uint8_t* d_bgr, int64_t out_frame_stride, int64_t out_row_stride, void* hip_stream);
+
 /* ---------------------------------------------------------------- YOLOv3 detector
  * Replaces RealYOLO / YOLOv3.forward (src/videotofaces/detectors/yolo.py:131-191), called by
  * detection.py:131 `detout = model(frames)`.

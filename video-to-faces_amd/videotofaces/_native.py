@@ -85,6 +85,7 @@ SIGNATURES = {
     'vtf_yolo_detect_crops': [_p, _p, _i32, _i32, _i32, _i32, _i64, _i64, _p, _i32, _p, _p, _i64, _p],
     'vtf_rcnn_detect_crops': [_p, _p, _i32, _i32, _i32, _i32, _i64, _i64, _p, _i32, _p, _p, _i64, _p],
     'vtf_hamming_dedupe': [_p, _i64, _p, _p, _p],
+    'vtf_yuv_to_bgr': [_p, _i64, _i32, _i32, _i32, _i32, _i64, _p, _i64, _i64, _p],
     'vtf_rcnn_create': [_p, _i64, _i32, _i32, _p],
     'vtf_rcnn_destroy': [_p],
     'vtf_rcnn_set_stream': [_p, _p],

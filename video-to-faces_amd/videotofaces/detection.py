@@ -120,9 +120,11 @@ def detect_crops(model, frames_dev, frame_offset=0, mscore=0.4, msize=50, mborde
 
 
 # ------------------------------------------------------------------ detection stage (detection.py:32-158)
-def frame_source(path, video_reader='opencv'):
+def frame_source(path, video_reader='opencv', device=None):
     """(n_frames, fps, read(indices) -> uint8 [B,H,W,3] BGR) for a video file (OpenCV, as
-    detection.py:82-111), a .npy file of frames, or an in-memory uint8 array (fps 1)."""
+    detection.py:82-111), a YUV4MPEG2 stream (.y4m: decoded frames converted on the GPU, read()
+    returns them in HBM of `device`, videotofaces/video.py), a .npy file of frames, or an
+    in-memory uint8 array (fps 1)."""
     import numpy as np
     if isinstance(path, np.ndarray):
         arr = path
@@ -130,6 +132,10 @@ def frame_source(path, video_reader='opencv'):
     if str(path).lower().endswith('.npy'):
         arr = np.load(path, mmap_mode='r')
         return arr.shape[0], 1, lambda idx: np.ascontiguousarray(arr[idx])
+    if str(path).lower().endswith('.y4m'):
+        from .video import Y4MReader
+        r = Y4MReader(path)
+        return r.n_frames, r.fps, lambda idx: r.read(idx, device)
     try:
         import cv2
     except ImportError:
@@ -156,6 +162,24 @@ def frame_source(path, video_reader='opencv'):
     return n, fps, read
 
 
+class _HostFrames:
+    """frames[fi][y1:y2, x1:x2] of device frames: only the face crops come back to the host."""
+
+    def __init__(self, dev):
+        self.dev = dev
+
+    def __getitem__(self, fi):
+        return _HostFrame(self.dev[fi])
+
+
+class _HostFrame:
+    def __init__(self, t):
+        self.t = t
+
+    def __getitem__(self, key):
+        return self.t[key].cpu().numpy()
+
+
 def process_frames_batch(frames, indices, model, det_params, save_params, hash_thr, hashes):
     """detection.py:126-158 with the frames uploaded to HBM once: detect and filter/adjust the
     boxes on device (detect_crops), average hashes of the crops on device, nearest-5 hash
@@ -168,7 +192,11 @@ def process_frames_batch(frames, indices, model, det_params, save_params, hash_t
     from . import _native as nat
     _, mscore, msize, mborder, scale, square = det_params
     out_dir, out_prefix, resize_to, _, _, _ = save_params
-    fr_dev = torch.from_numpy(np.ascontiguousarray(frames)).to(nat.device_of(model))
+    if isinstance(frames, torch.Tensor):  # frames already in HBM (a .y4m source; strided views are fine)
+        fr_dev = frames.to(nat.device_of(model))
+        frames = _HostFrames(fr_dev)
+    else:
+        fr_dev = torch.from_numpy(np.ascontiguousarray(frames)).to(nat.device_of(model))
     # detector + box post-processing on device; only the crop rectangles come back for the
     # JPEG slices and file names
     with torch.inference_mode():
@@ -200,6 +228,7 @@ def detect_faces(files, model, vid_params, det_params, save_params, hash_thr):
     import os.path as osp
     import numpy as np
     from .dupes import remove_dupes_overall, unpack_hash
+    from . import _native as nat
     video_step, video_fragment, video_area, video_reader = vid_params
     bs = det_params[0]
     out_dir, out_prefix = save_params[0], save_params[1]
@@ -210,7 +239,7 @@ def detect_faces(files, model, vid_params, det_params, save_params, hash_thr):
     for k, f in enumerate(files):
         print('Processing ' + (f if isinstance(f, str) else 'in-memory frames'))
         sp = (out_dir, out_prefix + ('' if len(files) == 1 else '%02d_' % (k + 1)), *save_params[2:])
-        n, fps, read = frame_source(f, video_reader)
+        n, fps, read = frame_source(f, video_reader, nat.device_of(model))
         step = max(1, round(fps * video_step))
         bgn = step if not video_fragment or video_fragment[0] < 0 else max(step, round(60 * video_fragment[0] * fps))
         end = n if not video_fragment or video_fragment[1] < 0 else min(n, round(60 * video_fragment[1] * fps + 1))
