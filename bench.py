@@ -327,11 +327,20 @@ class DetEncPipeline:
             j = (self.offset + i * self.B) % self.pool_n
             src, off = self.frames[j:j + self.B], j
         else:  # frames from pinned host memory: async H2D on the lane stream into a ring slot
-            pinned, ring, R = self.host
+            pinned, ring, R = self.host[:3]
             j = (i * self.B) % pinned.shape[0]
             slot = lane * R + (i // self.L) % R
             off = slot * self.B
-            ring[off:off + self.B].copy_(pinned[j:j + self.B], non_blocking=True)
+            if len(self.host) == 3:
+                ring[off:off + self.B].copy_(pinned[j:j + self.B], non_blocking=True)
+            else:  # 4:2:0 planes (the .y4m read path): H2D of 1.5 B/px, then k_yuv_to_bgr into the slot
+                from videotofaces import _native as nat
+                yring = self.host[3]
+                yring[off:off + self.B].copy_(pinned[j:j + self.B], non_blocking=True)
+                dst = ring[off:off + self.B]
+                nat.check(nat.lib().vtf_yuv_to_bgr(nat.ptr(yring[off:off + self.B]), self.B, dst.shape[1], dst.shape[2],
+                                                   420, 0, yring.stride(0), nat.ptr(dst), dst.stride(0), dst.stride(1),
+                                                   nat.stream_ptr(self.dev)))
             src = ring[off:off + self.B]
         if self.args.det_model == 'yolo':
             crops, _ = det.detect_crops(src, self.bp, off)
@@ -412,15 +421,21 @@ class DetEncPipeline:
         self.solo_stats = [st for st in stats if st is not None]
         return d.profile(False)
 
-    def host_frames(self, ring_slots=4):
-        """Switch to frames in pinned host memory (None restores HBM-resident frames)."""
+    def host_frames(self, ring_slots=4, yuv=False):
+        """Switch to frames in pinned host memory (None restores HBM-resident frames); yuv=True:
+        the frames as 4:2:0 planes (synth.bgr_to_yuv420), converted on the device per det-batch."""
         if ring_slots is None:
             self.host = None
             return
-        pinned = torch.from_numpy(self.frames_np).pin_memory()
         ring = torch.empty((self.L * ring_slots * self.B,) + tuple(self.frames_np.shape[1:]), dtype=torch.uint8,
                            device=self.dev)
-        self.host = (pinned, ring, ring_slots)
+        if not yuv:
+            self.host = (torch.from_numpy(self.frames_np).pin_memory(), ring, ring_slots)
+            return
+        from videotofaces import synth
+        planes = torch.from_numpy(synth.bgr_to_yuv420(self.frames_np)).pin_memory()
+        yring = torch.empty((ring.shape[0], planes.shape[1]), dtype=torch.uint8, device=self.dev)
+        self.host = (planes, ring, ring_slots, yring)
 
     def drift(self, steps=2):
         """bf16 / split-fp16 perf modes vs the fp32 parity modes on the same det-batches: detector
@@ -755,6 +770,18 @@ def run_gpu(args):
         out['host_frames'] = {'value': round(f_h / t_h, 2), 'ms_per_step': round(t_h * 1e3 / args.steps, 3),
                               'note': 'frames start in pinned host memory; H2D (%.1f MB per det-batch) inside the '
                                       'timed region' % (args.det_batch * args.H * args.W * 3 / 1e6)}
+        # the .y4m frame source's device half: 4:2:0 planes in pinned host memory, H2D of 1.5 B/px
+        # and k_yuv_to_bgr per det-batch (videotofaces/video.py; the file gather is host work)
+        if args.det_model == 'mtcnn' and args.H % 2 == 0 and args.W % 2 == 0:
+            pipe.host_frames(4, yuv=True)
+            f_y, t_y, _, _ = measure(pipe, args.steps, pipe.L, ctx)
+            pipe.host_frames(None)
+            out['host_yuv_frames'] = {
+                'value': round(f_y / t_y, 2), 'ms_per_step': round(t_y * 1e3 / args.steps, 3),
+                'faces_per_frame': round(f_y / max(1, ctx.world * args.steps * args.det_batch), 3),
+                'note': 'frames start as 4:2:0 planes in pinned host memory (the .y4m read path): H2D (%.1f MB per '
+                        'det-batch) + k_yuv_to_bgr inside the timed region; the decoded frames differ from the BGR '
+                        'originals by the 4:2:0 round trip' % (args.det_batch * args.H * args.W * 1.5 / 1e6)}
         if ctx.rank == 0:
             out['bf16_drift'] = pipe.drift(2)
     elif det:

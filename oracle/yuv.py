@@ -3,8 +3,8 @@
 The frame-source side of process_video (src/videotofaces/detection.py:68-111): the reference's
 cv2.VideoCapture / decord return uint8 BGR frames; here decoded frames arrive as planar YUV (a
 YUV4MPEG2 stream) and vtf_yuv_to_bgr (csrc/video.hip) converts them on the GPU.  This module
-restates that conversion in numpy integer arithmetic and writes / parses the container, so the
-GPU path is checked bit for bit against it:
+restates that conversion in numpy integer arithmetic (and process_video's frame sampling), so
+the GPU path is checked bit for bit against it:
   * BT.601 limited range with OpenCV's fixed-point constants (ITUR_BT_601_CY 1220542, CVR
     1673527, CVG -852492, CUG -409993, CUB 2116026, shift 20, the cvtColor(COLOR_YUV2BGR_I420)
     transform), or full range (1470104, -748826, -360853, 1858077); chroma nearest.
@@ -51,34 +51,6 @@ def yuv_to_bgr(planes, H, W, chroma=420, full_range=False):
         r, g, b = y + 1673527 * v, y - 852492 * v - 409993 * u, y + 2116026 * u
     out = np.stack([b, g, r], -1) >> 20
     return np.clip(out, 0, 255).astype(np.uint8)
-
-
-def bgr_to_yuv420(frames):
-    """test-data maker: uint8 BGR [B,H,W,3] -> 4:2:0 limited-range planes [B, frame_bytes]
-    (BT.601, 2x2 chroma averages; any encoder will do -- the check is on the decode side)."""
-    f = np.asarray(frames, np.float64)
-    B, H, W = f.shape[:3]
-    b, g, r = f[..., 0], f[..., 1], f[..., 2]
-    Y = 16 + 0.257 * r + 0.504 * g + 0.098 * b
-    U = 128 - 0.148 * r - 0.291 * g + 0.439 * b
-    V = 128 + 0.439 * r - 0.368 * g - 0.071 * b
-    ch, cw = chroma_size(H, W, 420)
-    pad = ((0, 0), (0, 2 * ch - H), (0, 2 * cw - W))
-    Uq = np.pad(U, pad, mode='edge').reshape(B, ch, 2, cw, 2).mean((2, 4))
-    Vq = np.pad(V, pad, mode='edge').reshape(B, ch, 2, cw, 2).mean((2, 4))
-    q = lambda a: np.clip(np.rint(a), 0, 255).astype(np.uint8).reshape(B, -1)
-    return np.concatenate([q(Y), q(Uq), q(Vq)], 1)
-
-
-def write_y4m(path, planes, H, W, fps='30:1', chroma=420, frame_params=None, extra=''):
-    """A YUV4MPEG2 file of the given planes; frame_params: per-frame header suffixes (or None)."""
-    ctag = {420: 'C420jpeg', 422: 'C422', 444: 'C444', 400: 'Cmono'}[chroma]
-    p = np.asarray(planes, np.uint8).reshape(-1, frame_bytes(H, W, chroma))
-    with open(path, 'wb') as f:
-        f.write(('YUV4MPEG2 W%d H%d F%s Ip A1:1 %s%s\n' % (W, H, fps, ctag, extra)).encode())
-        for i, fr in enumerate(p):
-            f.write(b'FRAME' + ((' ' + frame_params[i]).encode() if frame_params and frame_params[i] else b'') + b'\n')
-            f.write(fr.tobytes())
 
 
 def sample_indices(n_frames, fps, video_step, video_fragment=None):

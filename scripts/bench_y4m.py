@@ -46,7 +46,7 @@ def main():
            'bytes_per_launch': bytes_per_launch}
     res['frac'] = res['achieved_GBps'] / res['peak_GBps']
     # the whole read() of 16 sampled frames (step 2) from a 64-frame file in the page cache
-    from oracle.yuv import write_y4m
+    from videotofaces.video import write_y4m
     with tempfile.TemporaryDirectory() as d:
         f = os.path.join(d, 'clip.y4m')
         write_y4m(f, rng.integers(0, 256, (64, fb), dtype=np.uint8), H, W, fps='30:1')

@@ -11,6 +11,11 @@ import pytest
 from oracle import yuv as oy
 
 
+def write_y4m(*a, **k):
+    from videotofaces.video import write_y4m as w
+    return w(*a, **k)
+
+
 def _planes(rng, B, H, W, chroma):
     return rng.integers(0, 256, (B, oy.frame_bytes(H, W, chroma)), dtype=np.uint8)
 
@@ -21,7 +26,7 @@ def test_y4m_parse_and_offsets(tmp_path):
     H, W = 9, 17  # odd: chroma 5 x 9
     p = _planes(rng, 4, H, W, 420)
     f = str(tmp_path / 'a.y4m')
-    oy.write_y4m(f, p, H, W, fps='30000:1001', frame_params=[None, 'Ip', None, 'XFOO=1'])
+    write_y4m(f, p, H, W, fps='30000:1001', frame_params=[None, 'Ip', None, 'XFOO=1'])
     r = Y4MReader(f)
     assert (r.width, r.height, r.chroma, r.fps, r.n_frames, r.full_range) == (W, H, 420, 30, 4, False)
     assert r.frame_bytes == H * W + 2 * 5 * 9
@@ -34,7 +39,7 @@ def test_y4m_parse_and_offsets(tmp_path):
     for chroma in (422, 444, 400):
         g = str(tmp_path / ('c%d.y4m' % chroma))
         q = _planes(rng, 2, 6, 10, chroma)
-        oy.write_y4m(g, q, 6, 10, chroma=chroma, extra=' XCOLORRANGE=FULL')
+        write_y4m(g, q, 6, 10, chroma=chroma, extra=' XCOLORRANGE=FULL')
         r = Y4MReader(g)
         assert (r.chroma, r.full_range, r.n_frames, r.frame_bytes) == (chroma, True, 2, oy.frame_bytes(6, 10, chroma))
         np.testing.assert_array_equal(r.planes([1]), q[1:2])
@@ -62,7 +67,8 @@ def test_oracle_conversion_anchors():
     ref = np.stack([yy + 2.018 * (U - 128), yy - 0.813 * (V - 128) - 0.391 * (U - 128), yy + 1.596 * (V - 128)], -1)
     assert np.abs(got - np.clip(np.floor(ref + 0.5), 0, 255)).max() <= 1
     x = np.tile(np.linspace(40, 200, 16).astype(np.uint8)[None, None, :, None], (1, 16, 1, 3))
-    back = oy.yuv_to_bgr(oy.bgr_to_yuv420(x), 16, 16).astype(int)
+    from videotofaces import synth
+    back = oy.yuv_to_bgr(synth.bgr_to_yuv420(x), 16, 16).astype(int)
     assert np.abs(back - x).max() <= 3
 
 
@@ -118,7 +124,7 @@ def test_y4m_read_sampled_frames(tmp_path):
     H, W = 72, 128
     p = _planes(rng, 7, H, W, 420)
     f = str(tmp_path / 'v.y4m')
-    oy.write_y4m(f, p, H, W, fps='25:1')
+    write_y4m(f, p, H, W, fps='25:1')
     r = Y4MReader(f)
     idx = [6, 1, 3]
     got = r.read(idx).cpu().numpy()
@@ -134,9 +140,9 @@ def test_video_to_faces_on_y4m_matches_decoded_frames(tmp_path):
     from videotofaces import synth, video_to_faces
     src = synth.make_frames(12, seed=5)
     H, W = src.shape[1:3]
-    planes = oy.bgr_to_yuv420(src)
+    planes = synth.bgr_to_yuv420(src)
     f = str(tmp_path / 'clip.y4m')
-    oy.write_y4m(f, planes, H, W, fps='2:1')
+    write_y4m(f, planes, H, W, fps='2:1')
     dec = oy.yuv_to_bgr(planes, H, W)
     # in-memory frames run at fps 1 with frame indices 0..: give them the y4m's sampled frames
     idx = oy.sample_indices(12, 2, 1.0)

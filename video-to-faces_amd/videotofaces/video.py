@@ -19,6 +19,26 @@ import numpy as np
 _CHROMA = {'420jpeg': 420, '420paldv': 420, '420mpeg2': 420, '420': 420, '422': 422, '444': 444, 'mono': 400}
 
 
+def frame_bytes(H, W, chroma=420):
+    """bytes of one frame's planes: Y [H][W] + U, V of the chroma size (none for mono)."""
+    if chroma == 400:
+        return H * W
+    sx, sy = (0 if chroma == 444 else 1), (1 if chroma == 420 else 0)
+    return H * W + 2 * ((W + sx) >> sx) * ((H + sy) >> sy)
+
+
+def write_y4m(path, planes, H, W, fps='30:1', chroma=420, frame_params=None, extra=''):
+    """A YUV4MPEG2 file of uint8 planes [F, frame_bytes] (the layout Y4MReader reads);
+    frame_params: per-frame header suffixes (or None), extra: more header tags."""
+    ctag = {420: 'C420jpeg', 422: 'C422', 444: 'C444', 400: 'Cmono'}[chroma]
+    p = np.asarray(planes, np.uint8).reshape(-1, frame_bytes(H, W, chroma))
+    with open(path, 'wb') as f:
+        f.write(('YUV4MPEG2 W%d H%d F%s Ip A1:1 %s%s\n' % (W, H, fps, ctag, extra)).encode())
+        for i, fr in enumerate(p):
+            f.write(b'FRAME' + ((' ' + frame_params[i]).encode() if frame_params and frame_params[i] else b'') + b'\n')
+            f.write(fr.tobytes())
+
+
 class Y4MReader:
     """A YUV4MPEG2 file: .n_frames, .fps (rounded as detection.py:84 rounds CAP_PROP_FPS),
     .height, .width, read(indices, device) -> uint8 CUDA tensor [B,H,W,3] BGR."""
@@ -49,13 +69,7 @@ class Y4MReader:
             raise ValueError('%s: chroma C%s not supported (8-bit 420 / 422 / 444 / mono only)' % (path, ctag))
         self.chroma = _CHROMA[ctag]
         self.full_range = any(x.upper() == 'COLORRANGE=FULL' for x in fields.get('X', []))
-        W, H = self.width, self.height
-        if self.chroma == 400:
-            cw = ch = 0
-        else:
-            sx, sy = (0 if self.chroma == 444 else 1), (1 if self.chroma == 420 else 0)
-            cw, ch = (W + sx) >> sx, (H + sy) >> sy
-        self.frame_bytes = H * W + 2 * cw * ch
+        self.frame_bytes = frame_bytes(self.height, self.width, self.chroma)
         # frame payload offsets (FRAME headers may carry parameters: walk them)
         offs, p = [], end + 1
         while p < size:
@@ -68,7 +82,7 @@ class Y4MReader:
             p = e + 1 + self.frame_bytes
         self.offsets = np.asarray(offs, np.int64)
         self.n_frames = len(offs)
-        self._buf = self._pinned = None
+        self._pinned = None
 
     def close(self):
         if self._mm is not None:
