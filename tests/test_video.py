@@ -81,7 +81,8 @@ def test_sampling_matches_reference_rule():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize('H,W,chroma,full', [(720, 1280, 420, False), (9, 17, 420, False), (8, 12, 422, False),
+@pytest.mark.parametrize('H,W,chroma,full', [(720, 1280, 420, False), (9, 17, 420, False), (9, 16, 420, False),
+                                             (8, 12, 422, False), (8, 12, 420, True),
                                              (6, 8, 444, True), (5, 7, 400, False), (1080, 1920, 420, True)])
 def test_yuv_to_bgr_bit_exact(H, W, chroma, full):
     import torch
@@ -150,6 +151,8 @@ def test_video_to_faces_on_y4m_matches_decoded_frames(tmp_path):
     kw = dict(mode='detection', style='live', det_batch_size=4, det_min_size=10, video_step=1.0)
     out_a = tmp_path / 'a'
     out_b = tmp_path / 'b'
+    out_a.mkdir()
+    out_b.mkdir()
     video_to_faces(f, out_dir=str(out_a), **kw)
     video_to_faces(np.ascontiguousarray(dec[[0] + idx]), out_dir=str(out_b), **kw)
     fa = sorted(os.listdir(out_a / 'faces'))
