@@ -7,8 +7,8 @@
 // the container and uploads each sampled frame's planes as they lie in the file: 1.5 bytes per
 // pixel over PCIe for 4:2:0 instead of 3) -- and the colour conversion runs on the GPU:
 //
-//   k_yuv420_to_bgr_8x2 (4:2:0, W % 8 == 0: one thread per 8 x 2 block, 8-byte accesses) or
-//   k_yuv_to_bgr (any layout: one thread per 4 pixels of a row); chroma sampled nearest (each
+//   k_yuv_to_bgr: one thread per 4 pixels of a row (4-byte luma load and BGR stores when W % 4
+//   == 0 and the strides allow); chroma sampled nearest (each
 //   4:2:0 chroma sample covers its 2 x 2 luma block, as cv2.cvtColor(COLOR_YUV2BGR_I420) reads
 //   it) and the BT.601 integer transform with 20 fractional bits:
 //     limited range: y = max(0, Y - 16) * 1220542,  R = (y + 2^19 + 1673527 V') >> 20,
@@ -31,24 +31,33 @@ struct YuvGeom {
     int64_t in_stride, out_fstride, out_rstride;
 };
 
-__device__ inline void yuv_px(int Y, int U, int V, bool full, uint8_t& b, uint8_t& g, uint8_t& r) {
+// (x >> 20) saturated to [0, 255], materialised as a 32-bit value: the empty asm keeps the
+// compiler from fusing shift + saturate + byte packing into v_ashr_pk_u8_i32, whose packed result
+// was OR-ed with the neighbouring bytes as if its upper half were zero -- measured wrong bytes 2 / 3
+// of the packed words on the GPU (ROCm 7.2 hipcc, gfx950)
+__device__ inline uint8_t sat_u8(int x) {
+    int v = min(255, max(0, x >> 20));
+    asm volatile("" : "+v"(v));
+    return (uint8_t)v;
+}
+
+template <bool FULL>
+__device__ inline void yuv_px(int Y, int U, int V, uint8_t& b, uint8_t& g, uint8_t& r) {
     const int u = U - 128, v = V - 128;
-    int y, cr, cgu, cgv, cb;
-    if (full) {
-        y = Y << 20;
-        cr = 1470104, cgv = -748826, cgu = -360853, cb = 1858077;
-    } else {
-        y = max(0, Y - 16) * 1220542;
-        cr = 1673527, cgv = -852492, cgu = -409993, cb = 2116026;
-    }
-    y += 1 << 19;
-    r = (uint8_t)min(255, max(0, (y + cr * v) >> 20));
-    g = (uint8_t)min(255, max(0, (y + cgv * v + cgu * u) >> 20));
-    b = (uint8_t)min(255, max(0, (y + cb * u) >> 20));
+    const int y = (FULL ? Y << 20 : max(0, Y - 16) * 1220542) + (1 << 19);
+    const int cr = FULL ? 1470104 : 1673527, cgv = FULL ? -748826 : -852492;
+    const int cgu = FULL ? -360853 : -409993, cb = FULL ? 1858077 : 2116026;
+    r = sat_u8(y + cr * v);
+    g = sat_u8(y + cgv * v + cgu * u);
+    b = sat_u8(y + cb * u);
+}
+
+__device__ inline uint32_t pack4(const uint8_t* q) {
+    return (uint32_t)q[0] | (uint32_t)q[1] << 8 | (uint32_t)q[2] << 16 | (uint32_t)q[3] << 24;
 }
 
 // VEC: W % 4 == 0 and every stride a multiple of 4 -> one 4-byte luma load, three 4-byte stores
-template <bool VEC>
+template <bool VEC, bool FULL>
 __global__ __launch_bounds__(256) void k_yuv_to_bgr(const uint8_t* __restrict__ in, int64_t n, YuvGeom g,
                                                     uint8_t* __restrict__ out) {
     const int qw = (g.W + 3) >> 2;
@@ -74,55 +83,12 @@ __global__ __launch_bounds__(256) void k_yuv_to_bgr(const uint8_t* __restrict__ 
         const int Y = VEC ? (int)((yv >> (8 * k)) & 255u) : Yp[(int64_t)y * g.W + x];
         const int U = mono ? 128 : Up[crow + (x >> g.sx)];
         const int V = mono ? 128 : Vp[crow + (x >> g.sx)];
-        yuv_px(Y, U, V, g.full != 0, px[3 * k], px[3 * k + 1], px[3 * k + 2]);
+        yuv_px<FULL>(Y, U, V, px[3 * k], px[3 * k + 1], px[3 * k + 2]);
         if (!VEC) o[3 * k] = px[3 * k], o[3 * k + 1] = px[3 * k + 1], o[3 * k + 2] = px[3 * k + 2];
     }
     if (VEC) {
-        uint32_t w[3];
-#pragma unroll
-        for (int j = 0; j < 3; j++)
-            w[j] = (uint32_t)px[4 * j] | (uint32_t)px[4 * j + 1] << 8 | (uint32_t)px[4 * j + 2] << 16 |
-                   (uint32_t)px[4 * j + 3] << 24;
         uint32_t* o4 = (uint32_t*)o;
-        o4[0] = w[0], o4[1] = w[1], o4[2] = w[2];
-    }
-}
-
-// 4:2:0 with W % 8 == 0 and 8-byte aligned planes / strides: one thread per 8 x 2 pixel block --
-// two 8-byte luma loads, one 4-byte load per chroma plane (the block's 4 x 1 chroma samples),
-// six 8-byte stores
-__global__ __launch_bounds__(256) void k_yuv420_to_bgr_8x2(const uint8_t* __restrict__ in, int64_t n, YuvGeom g,
-                                                           uint8_t* __restrict__ out) {
-    const int gw = g.W >> 3, rp = (g.H + 1) >> 1;
-    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    const int64_t per = (int64_t)rp * gw;
-    if (i >= n * per) return;
-    const int64_t f = i / per;
-    const int rem = (int)(i - f * per);
-    const int r = rem / gw, x0 = (rem - r * gw) * 8;
-    const uint8_t* Yp = in + f * g.in_stride;
-    const uint8_t* Up = Yp + (int64_t)g.H * g.W;
-    const uint8_t* Vp = Up + (int64_t)g.cw * g.ch;
-    const uint32_t uv = *(const uint32_t*)(Up + r * g.cw + (x0 >> 1));
-    const uint32_t vv = *(const uint32_t*)(Vp + r * g.cw + (x0 >> 1));
-#pragma unroll
-    for (int h = 0; h < 2; h++) {
-        const int y = 2 * r + h;
-        if (y >= g.H) break;
-        const uint64_t yv = *(const uint64_t*)(Yp + (int64_t)y * g.W + x0);
-        uint8_t px[24];
-#pragma unroll
-        for (int k = 0; k < 8; k++)
-            yuv_px((int)((yv >> (8 * k)) & 255u), (int)((uv >> (8 * (k >> 1))) & 255u), (int)((vv >> (8 * (k >> 1))) & 255u),
-                   g.full != 0, px[3 * k], px[3 * k + 1], px[3 * k + 2]);
-        uint64_t* o = (uint64_t*)(out + f * g.out_fstride + (int64_t)y * g.out_rstride + (int64_t)x0 * 3);
-#pragma unroll
-        for (int j = 0; j < 3; j++) {
-            uint64_t w = 0;
-#pragma unroll
-            for (int b = 0; b < 8; b++) w |= (uint64_t)px[8 * j + b] << (8 * b);
-            o[j] = w;
-        }
+        o4[0] = pack4(px), o4[1] = pack4(px + 4), o4[2] = pack4(px + 8);
     }
 }
 
@@ -156,21 +122,17 @@ extern "C" int vtf_yuv_to_bgr(const uint8_t* d_yuv, int64_t n, int H, int W, int
         const int64_t items = n * H * (int64_t)((W + 3) / 4);
         VTF_CHECK(items / 256 < (int64_t)1 << 31, VTF_E_LIMIT, "yuv_to_bgr: too many frames in one call");
         hipStream_t st = (hipStream_t)hip_stream;
-        const bool v8 = chroma == 420 && W % 8 == 0 && in_frame_stride % 8 == 0 && out_frame_stride % 8 == 0 &&
-                        out_row_stride % 8 == 0 && ((uintptr_t)d_yuv & 7) == 0 && ((uintptr_t)d_bgr & 7) == 0;
-        if (v8) {
-            const int64_t blocks = n * ((H + 1) / 2) * (int64_t)(W / 8);
-            k_yuv420_to_bgr_8x2<<<(unsigned)((blocks + 255) / 256), 256, 0, st>>>(d_yuv, n, g, d_bgr);
-            VTF_HIP(hipGetLastError());
-            return;
-        }
         const bool vec = W % 4 == 0 && in_frame_stride % 4 == 0 && out_frame_stride % 4 == 0 && out_row_stride % 4 == 0 &&
                          ((uintptr_t)d_yuv & 3) == 0 && ((uintptr_t)d_bgr & 3) == 0;
         const unsigned grid = (unsigned)((items + 255) / 256);
-        if (vec)
-            k_yuv_to_bgr<true><<<grid, 256, 0, st>>>(d_yuv, n, g, d_bgr);
+        if (vec && g.full)
+            k_yuv_to_bgr<true, true><<<grid, 256, 0, st>>>(d_yuv, n, g, d_bgr);
+        else if (vec)
+            k_yuv_to_bgr<true, false><<<grid, 256, 0, st>>>(d_yuv, n, g, d_bgr);
+        else if (g.full)
+            k_yuv_to_bgr<false, true><<<grid, 256, 0, st>>>(d_yuv, n, g, d_bgr);
         else
-            k_yuv_to_bgr<false><<<grid, 256, 0, st>>>(d_yuv, n, g, d_bgr);
+            k_yuv_to_bgr<false, false><<<grid, 256, 0, st>>>(d_yuv, n, g, d_bgr);
         VTF_HIP(hipGetLastError());
     });
 }
