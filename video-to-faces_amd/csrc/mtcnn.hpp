@@ -52,19 +52,23 @@ struct PNetOut {
     unsigned long long* clk;  // [8] summed shader clocks per phase over workgroups (null: off)
 };
 
-void launch_sat(const uint8_t* frames, int64_t frame_stride, int64_t row_stride, int B, int H, int W, int3* sat,
-                hipStream_t st, uint32_t* zero = nullptr, int nzero = 0);
-void launch_resample_sat(const int3* sat, int B, int H, int W, int lh, int lw, float* out, hipStream_t st);
+// the det-batch's summed-area table (mtcnn_dev.hpp): int3 entries, or packed uint64 (pk) when
+// sat_pack_ok says every bin the det-batch reads is small enough
+void launch_sat(const uint8_t* frames, int64_t frame_stride, int64_t row_stride, int B, int H, int W, void* sat,
+                hipStream_t st, uint32_t* zero = nullptr, int nzero = 0, int pk = 0);
+bool sat_pack_ok(int H, int W, int min_lh, int min_lw);
+void launch_resample_sat(const void* sat, int pk, int B, int H, int W, int lh, int lw, float* out, hipStream_t st);
 struct ResampleLevels {  // precomputed pyramid levels of one det-batch (k_resample_sat_multi)
     static constexpr int MAXL = 32;
     int n;
     int split;  // 1: [B][lh][lw] fp16 split pixels (x0 RGB | x1 RGB, 12 B), else fp32 [B][3][lh][lw]
+    int pk;     // the SAT is in the packed layout
     int lh[MAXL], lw[MAXL];
     int64_t beg[MAXL + 1];  // first output element (b, y, x) of each level in the flattened grid
     int64_t tbeg[MAXL + 1]; // first 2-D tile of each level (k_resample_sat_multi's grid; set by the launcher)
     float* out[MAXL];       // [B][3][lh][lw]
 };
-void launch_resample_sat_multi(const int3* sat, int B, int H, int W, const ResampleLevels& lv, hipStream_t st);
+void launch_resample_sat_multi(const void* sat, int B, int H, int W, const ResampleLevels& lv, hipStream_t st);
 void launch_pnet(bool dense, const uint8_t* frames, int64_t frame_stride, int64_t row_stride, int H, int W,
                  const PNetLevel* d_levels, int n_levels, int64_t total_tiles, const PNetW& w, const PNetOut& o,
                  uint32_t* d_tile_ctr, hipStream_t st, int64_t exact_tiles = 0,
@@ -74,9 +78,9 @@ int64_t pnet_pre_from(const std::vector<PNetLevel>& lv, int64_t total_tiles);
 // leading tiles of the level plan that k_pnet's exact-levels variant takes (see launch_pnet)
 int64_t pnet_exact_tiles(const std::vector<PNetLevel>& lv, int H, int W, int64_t total_tiles);
 int cand_front_side(bool onet);
-void launch_cand_front(bool onet, const int3* sat, int H, int W, const float4* boxes, const int32_t* img, int64_t n,
-                       const float* w1, const _Float16* w1h, const float* b1, const float* a1, float* out, int32_t* err,
-                       hipStream_t st, int* ovf = nullptr);
+void launch_cand_front(bool onet, const void* sat, int pk, int H, int W, const float4* boxes, const int32_t* img,
+                       int64_t n, const float* w1, const _Float16* w1h, const float* b1, const float* a1, float* out,
+                       int32_t* err, hipStream_t st, int* ovf = nullptr);
 // Fused RNet / ONet front half (mtcnn_cand.hip): crop + conv1 + PReLU + pool + conv2 + PReLU +
 // pool on split-fp16 matrix cores -> pool2 map [n, P2, P2, 48 | 64] fp32 (P2 = 4 | 10).
 // w1h: conv1 split planes [2][32][64] (k = ky*16 + kx*4 + c), w2h: conv2 [2][C2][288]
@@ -88,8 +92,8 @@ struct CandFusedW {
     const float *b2, *a2;
 };
 int cand_fused_side(bool onet);
-void launch_cand_fused(bool onet, const int3* sat, int H, int W, const float4* boxes, const int32_t* img, int64_t n,
-                       const CandFusedW& w, float* out, int32_t* err, int32_t* ovf, hipStream_t st);
+void launch_cand_fused(bool onet, const void* sat, int pk, int H, int W, const float4* boxes, const int32_t* img,
+                       int64_t n, const CandFusedW& w, float* out, int32_t* err, int32_t* ovf, hipStream_t st);
 void launch_heads(const float* x, int64_t n, int D, const float* w1, const float* b1, const float* w2,
                   const float* b2, const float* w3, const float* b3, float* prob, float4* reg, float* lm,
                   hipStream_t st);

@@ -71,7 +71,7 @@ __device__ inline int p1_index(int pix, int c) { return pix * 32 + ((((c >> 3) ^
 
 template <int S, int C2, int PB1, int PB2, int MG>
 __global__ __launch_bounds__((Cfg<S, C2, PB1, PB2, MG>::NT)) void k_cand_fused(
-    const int3* __restrict__ sat, int H, int W, const float4* __restrict__ boxes, const int32_t* __restrict__ img,
+    const void* __restrict__ sat, int pk, int H, int W, const float4* __restrict__ boxes, const int32_t* __restrict__ img,
     int64_t n, const _Float16* __restrict__ w1h, const float* __restrict__ b1, const float* __restrict__ a1,
     const _Float16* __restrict__ w2h, const float* __restrict__ b2, const float* __restrict__ a2,
     float* __restrict__ out, int32_t* __restrict__ err, int32_t* __restrict__ ovf, int dbg) {
@@ -108,19 +108,17 @@ __global__ __launch_bounds__((Cfg<S, C2, PB1, PB2, MG>::NT)) void k_cand_fused(
             continue;  // uniform: every thread of the workgroup takes it
         }
         // ---- crop: S x S adaptive-pool bins from the SAT, split into the two planes
-        const int3* sk = sat + (int64_t)img[k] * (H + 1) * (W + 1);
+        const int64_t sk = (int64_t)img[k] * (H + 1) * (W + 1);
         for (int i = tid; i < CP * CP; i += NT) {
             const int r = i / CP, q = i - r * CP;
             h4 v0 = {0, 0, 0, 0}, v1 = {0, 0, 0, 0};
             if (r < S && q < S && !(dbg & 1)) {
                 const int ys = (r * hc) / S, ye = ((r + 1) * hc + S - 1) / S;
                 const int xs = (q * wc) / S, xe = ((q + 1) * wc + S - 1) / S;
-                const int3* ra = sk + (int64_t)(y0 + ys) * (W + 1) + x0;
-                const int3* rb = sk + (int64_t)(y0 + ye) * (W + 1) + x0;
-                const int3 a = ra[xs], b = ra[xe], c = rb[xs], d = rb[xe];
-                const float c0 = bin_avg(d.x - b.x - c.x + a.x, ye - ys, xe - xs);
-                const float c1 = bin_avg(d.y - b.y - c.y + a.y, ye - ys, xe - xs);
-                const float c2 = bin_avg(d.z - b.z - c.z + a.z, ye - ys, xe - xs);
+                const int3 sm = sat_box_any(sat, pk, sk + x0, W + 1, y0 + ys, y0 + ye, xs, xe);
+                const float c0 = bin_avg(sm.x, ye - ys, xe - xs);
+                const float c1 = bin_avg(sm.y, ye - ys, xe - xs);
+                const float c2 = bin_avg(sm.z, ye - ys, xe - xs);
                 _Float16 h0, h1;
                 split_f16(c0, h0, h1);
                 v0[0] = h0;
@@ -255,8 +253,8 @@ __global__ __launch_bounds__((Cfg<S, C2, PB1, PB2, MG>::NT)) void k_cand_fused(
 }
 
 template <int S, int C2, int PB1, int PB2, int MG>
-void launch_t(const int3* sat, int H, int W, const float4* boxes, const int32_t* img, int64_t n, const CandFusedW& w,
-              float* out, int32_t* err, int32_t* ovf, hipStream_t st) {
+void launch_t(const void* sat, int pk, int H, int W, const float4* boxes, const int32_t* img, int64_t n,
+              const CandFusedW& w, float* out, int32_t* err, int32_t* ovf, hipStream_t st) {
     using C = Cfg<S, C2, PB1, PB2, MG>;
     static_assert(C::SMEM <= 160 * 1024, "LDS budget");
     int dev = 0, cus = 256;
@@ -273,7 +271,7 @@ void launch_t(const int3* sat, int H, int W, const float4* boxes, const int32_t*
         const char* e = std::getenv("VTF_CAND_DEBUG");  // 4 pool1, 8 conv2, 16 pool2
         return e ? std::atoi(e) : 0;
     }();
-    k_cand_fused<S, C2, PB1, PB2, MG><<<(unsigned)grid, C::NT, 0, st>>>(sat, H, W, boxes, img, n, w.w1h, w.b1, w.a1,
+    k_cand_fused<S, C2, PB1, PB2, MG><<<(unsigned)grid, C::NT, 0, st>>>(sat, pk, H, W, boxes, img, n, w.w1h, w.b1, w.a1,
                                                                          w.w2h, w.b2, w.a2, out, err, ovf, dbg);
     VTF_HIP(hipGetLastError());
 }
@@ -282,13 +280,13 @@ void launch_t(const int3* sat, int H, int W, const float4* boxes, const int32_t*
 
 int cand_fused_side(bool onet) { return onet ? Cfg<48, 64, 2, 2, 3>::P2 : Cfg<24, 48, 3, 4, 2>::P2; }
 
-void launch_cand_fused(bool onet, const int3* sat, int H, int W, const float4* boxes, const int32_t* img, int64_t n,
-                       const CandFusedW& w, float* out, int32_t* err, int32_t* ovf, hipStream_t st) {
+void launch_cand_fused(bool onet, const void* sat, int pk, int H, int W, const float4* boxes, const int32_t* img,
+                       int64_t n, const CandFusedW& w, float* out, int32_t* err, int32_t* ovf, hipStream_t st) {
     if (n <= 0) return;
     if (onet)
-        launch_t<48, 64, 2, 2, 3>(sat, H, W, boxes, img, n, w, out, err, ovf, st);
+        launch_t<48, 64, 2, 2, 3>(sat, pk, H, W, boxes, img, n, w, out, err, ovf, st);
     else
-        launch_t<24, 48, 3, 4, 2>(sat, H, W, boxes, img, n, w, out, err, ovf, st);
+        launch_t<24, 48, 3, 4, 2>(sat, pk, H, W, boxes, img, n, w, out, err, ovf, st);
 }
 
 }  // namespace vtf

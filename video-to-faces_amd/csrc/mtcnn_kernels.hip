@@ -39,13 +39,9 @@ typedef __attribute__((ext_vector_type(8))) _Float16 f16x8;
 // in fp32, and so is every partial sum of such values over an adaptive-pool bin (|sum| < 2^16
 // with 8 fractional bits), so the reference's sequential fp32 bin sum (adaptive_avg_pool2d,
 // row-major) equals the integer box sum of v = 2u - 255 times 2^-8, bit for bit.
-// sat[b][y][x] = (R, G, B) sums over rows < y, cols < x; y in [0,H], x in [0,W] (12 bytes per
-// entry: the SAT passes and every corner read are HBM / MALL-bound, a pad word was a quarter of it).
-__device__ inline int4 sat_box(const int3* __restrict__ s, int W1, int y0, int y1, int x0, int x1) {
-    const int3 a = s[(int64_t)y0 * W1 + x0], b = s[(int64_t)y0 * W1 + x1];
-    const int3 c = s[(int64_t)y1 * W1 + x0], d = s[(int64_t)y1 * W1 + x1];
-    return make_int4(d.x - b.x - c.x + a.x, d.y - b.y - c.y + a.y, d.z - b.z - c.z + a.z, 0);
-}
+// sat[b][y][x] = (R, G, B) sums over rows < y, cols < x; y in [0,H], x in [0,W], as 12-byte int3
+// or, when every bin of the det-batch is small enough, 8-byte packed entries (mtcnn_dev.hpp): the
+// SAT passes and every corner read are HBM / MALL-bound.
 
 // bin average from an exact integer bin sum: s / kh / kw with the reference's roundings
 // PNet weight layout (mtcnn_runtime.hip build_weights checks it): the fp32 tensors are packed
@@ -176,17 +172,108 @@ __global__ __launch_bounds__(SAT_COLS * SAT_MAXG) void k_sat_cols(int H, int W, 
     }
 }
 
-void launch_sat(const uint8_t* frames, int64_t frame_stride, int64_t row_stride, int B, int H, int W, int3* sat,
-                hipStream_t st, uint32_t* zero, int nzero) {
-    k_sat_rows<<<(unsigned)((int64_t)B * H), 256, 0, st>>>(frames, frame_stride, row_stride, H, W, sat, zero, nzero);
+// the packed layout (mtcnn_dev.hpp): the same two passes on uint64 prefix sums of packed u
+// (8 B per entry instead of 12: the passes and every corner read move two thirds of the bytes)
+__global__ __launch_bounds__(256) void k_sat_rows_pk(const uint8_t* __restrict__ frames, int64_t frame_stride,
+                                                     int64_t row_stride, int H, int W, uint64_t* __restrict__ sat,
+                                                     uint32_t* __restrict__ zero, int nzero) {
+    if (blockIdx.x == 0)
+        for (int i = threadIdx.x; i < nzero; i += 256) zero[i] = 0u;
+    const int y = blockIdx.x % H, b = blockIdx.x / H;
+    const int W1 = W + 1;
+    const uint8_t* row = frames + (int64_t)b * frame_stride + (int64_t)y * row_stride;
+    uint64_t* out = sat + ((int64_t)b * (H + 1) + y + 1) * W1;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    __shared__ uint64_t wt[2][4];
+    uint64_t carry = 0, np = tid < W ? sat_pack_px(row + 3 * tid) : 0;
+    for (int x0 = 0, it = 0; x0 < W; x0 += 256, it++) {
+        uint64_t p = np;
+        const int xn = x0 + 256 + tid;
+        np = xn < W ? sat_pack_px(row + 3 * xn) : 0;
+        for (int off = 1; off < 64; off <<= 1) {  // inclusive wave scan
+            const uint64_t t = __shfl_up(p, off);
+            if (lane >= off) p += t;
+        }
+        if (lane == 63) wt[it & 1][wave] = p;
+        __syncthreads();
+        uint64_t wb = carry;
+        for (int w = 0; w < 4; w++) {
+            const uint64_t t = wt[it & 1][w];
+            if (w < wave) wb += t;
+            carry += t;
+        }
+        const int x = x0 + tid;
+        if (x < W) out[x + 1] = wb + p;
+    }
+    if (tid == 0) out[0] = 0;
+    if (y == 0) {
+        uint64_t* r0 = sat + (int64_t)b * (H + 1) * W1;
+        for (int x = tid; x < W1; x += 256) r0[x] = 0;
+    }
+}
+
+__global__ __launch_bounds__(SAT_COLS * SAT_MAXG) void k_sat_cols_pk(int H, int W, uint64_t* __restrict__ sat) {
+    const int W1 = W + 1;
+    const int G = blockDim.x / SAT_COLS;
+    const int ncb = (W1 + SAT_COLS - 1) / SAT_COLS;
+    const int b = blockIdx.x / ncb, cb = blockIdx.x % ncb;
+    const int c = threadIdx.x % SAT_COLS, g = threadIdx.x / SAT_COLS;
+    const int x = cb * SAT_COLS + c;
+    const int per = (H + G - 1) / G;
+    const int ys = 1 + g * per, ye = min(H + 1, ys + per);
+    uint64_t* col = sat + (int64_t)b * (H + 1) * W1 + min(x, W1 - 1);
+    extern __shared__ uint64_t tot_q[];
+    uint64_t (*tot)[SAT_COLS] = (uint64_t (*)[SAT_COLS])tot_q;
+    uint64_t v[SAT_PER];
+    uint64_t acc = 0;
+#pragma unroll
+    for (int i = 0; i < SAT_PER; i++) {
+        v[i] = (x < W1 && ys + i < ye) ? col[(int64_t)(ys + i) * W1] : 0;
+        acc += v[i];
+    }
+    tot[g][c] = acc;
+    __syncthreads();
+    uint64_t off = 0;
+    for (int k = 0; k < g; k++) off += tot[k][c];
+#pragma unroll
+    for (int i = 0; i < SAT_PER; i++) {
+        off += v[i];
+        if (x < W1 && ys + i < ye) col[(int64_t)(ys + i) * W1] = off;
+    }
+}
+
+void launch_sat(const uint8_t* frames, int64_t frame_stride, int64_t row_stride, int B, int H, int W, void* sat,
+                hipStream_t st, uint32_t* zero, int nzero, int pk) {
     const int G = (H + SAT_PER - 1) / SAT_PER;
     VTF_CHECK(G <= SAT_MAXG, VTF_E_LIMIT, "mtcnn: frames taller than 1536 rows");
-    k_sat_cols<<<(unsigned)(B * ((W + SAT_COLS) / SAT_COLS)), SAT_COLS * G, (size_t)G * SAT_COLS * sizeof(int3), st>>>(H, W, sat);
+    const unsigned gc = (unsigned)(B * ((W + SAT_COLS) / SAT_COLS));
+    if (pk) {
+        k_sat_rows_pk<<<(unsigned)((int64_t)B * H), 256, 0, st>>>(frames, frame_stride, row_stride, H, W, (uint64_t*)sat,
+                                                                    zero, nzero);
+        k_sat_cols_pk<<<gc, SAT_COLS * G, (size_t)G * SAT_COLS * sizeof(uint64_t), st>>>(H, W, (uint64_t*)sat);
+        return;
+    }
+    k_sat_rows<<<(unsigned)((int64_t)B * H), 256, 0, st>>>(frames, frame_stride, row_stride, H, W, (int3*)sat, zero, nzero);
+    k_sat_cols<<<gc, SAT_COLS * G, (size_t)G * SAT_COLS * sizeof(int3), st>>>(H, W, (int3*)sat);
+}
+
+// the packed layout is exact for boxes of at most 8223 pixels (255 * area < 2^21 per channel):
+// the largest bin a det-batch reads -- the downsampled pyramid levels' bins and the 24 / 48 crops
+// of candidate boxes clipped to the frame -- must stay below that (VTF_SAT_PACK=0: int3 always)
+bool sat_pack_ok(int H, int W, int min_lh, int min_lw) {
+    static const bool on = [] {
+        const char* e = std::getenv("VTF_SAT_PACK");
+        return !(e && std::atoi(e) == 0);
+    }();
+    auto bin = [](int64_t L, int64_t l) { return (L + l - 1) / l + 1; };
+    const int64_t crop = bin(H, 24) * bin(W, 24);
+    const int64_t lvl = bin(H, std::max(1, min_lh)) * bin(W, std::max(1, min_lw));
+    return on && std::max(crop, lvl) * 255 < ((int64_t)1 << 21);
 }
 
 // MTCNN._resample of the preprocessed frames (mtcnn.py:133-139, 150-151) from the SAT:
 // out [B][3][lh][lw], one thread per level pixel (all three channels)
-__global__ void k_resample_sat(const int3* __restrict__ sat, int B, int H, int W, int lh, int lw,
+__global__ void k_resample_sat(const void* __restrict__ sat, int pk, int B, int H, int W, int lh, int lw,
                                float* __restrict__ out) {
     int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     int64_t n = (int64_t)B * lh * lw;
@@ -196,16 +283,16 @@ __global__ void k_resample_sat(const int3* __restrict__ sat, int B, int H, int W
     const int b = (int)(i / ((int64_t)lw * lh));
     const int y0 = (int)(((int64_t)ly * H) / lh), y1 = (int)(((int64_t)(ly + 1) * H + lh - 1) / lh);
     const int x0 = (int)(((int64_t)lx * W) / lw), x1 = (int)(((int64_t)(lx + 1) * W + lw - 1) / lw);
-    const int4 s = sat_box(sat + (int64_t)b * (H + 1) * (W + 1), W + 1, y0, y1, x0, x1);
+    const int3 s = sat_box_any(sat, pk, (int64_t)b * (H + 1) * (W + 1), W + 1, y0, y1, x0, x1);
     const int64_t plane = (int64_t)lh * lw, o = (int64_t)b * 3 * plane + (int64_t)ly * lw + lx;
     out[o] = bin_avg(s.x, y1 - y0, x1 - x0);
     out[o + plane] = bin_avg(s.y, y1 - y0, x1 - x0);
     out[o + 2 * plane] = bin_avg(s.z, y1 - y0, x1 - x0);
 }
 
-void launch_resample_sat(const int3* sat, int B, int H, int W, int lh, int lw, float* out, hipStream_t st) {
+void launch_resample_sat(const void* sat, int pk, int B, int H, int W, int lh, int lw, float* out, hipStream_t st) {
     int64_t n = (int64_t)B * lh * lw;
-    k_resample_sat<<<cdiv(n, 256), 256, 0, st>>>(sat, B, H, W, lh, lw, out);
+    k_resample_sat<<<cdiv(n, 256), 256, 0, st>>>(sat, pk, B, H, W, lh, lw, out);
 }
 
 // every precomputed level of a det-batch in one launch (the small levels alone are launch-bound).
@@ -215,7 +302,7 @@ void launch_resample_sat(const int3* sat, int B, int H, int W, int lh, int lw, f
 // L1 / its XCD's L2 instead of HBM (a row-major strip of 256 pixels per workgroup put the next
 // level row on another XCD: 960 MB fetched per det-batch for 260 MB of output)
 constexpr int RS_TH = 8, RS_TW = 64;
-__global__ __launch_bounds__(256) void k_resample_sat_multi(const int3* __restrict__ sat, int B, int H, int W,
+__global__ __launch_bounds__(256) void k_resample_sat_multi(const void* __restrict__ sat, int B, int H, int W,
                                                             ResampleLevels lv) {
     const int64_t bid = blockIdx.x;
     int l = 0;
@@ -228,14 +315,14 @@ __global__ __launch_bounds__(256) void k_resample_sat_multi(const int3* __restri
     const int ty = tt / txn, tx = tt - ty * txn;
     const int lx = tx * RS_TW + (threadIdx.x & (RS_TW - 1));
     const int x0 = (int)(((int64_t)lx * W) / lw), x1 = (int)(((int64_t)(lx + 1) * W + lw - 1) / lw);
-    const int3* sb = sat + (int64_t)b * (H + 1) * (W + 1);
+    const int64_t sb = (int64_t)b * (H + 1) * (W + 1);
 #pragma unroll
     for (int h = 0; h < 2; h++) {
         const int ly = ty * RS_TH + (threadIdx.x >> 6) + h * (RS_TH / 2);
         if (ly >= lh || lx >= lw) continue;
         const int64_t j = ((int64_t)b * lh + ly) * lw + lx;
         const int y0 = (int)(((int64_t)ly * H) / lh), y1 = (int)(((int64_t)(ly + 1) * H + lh - 1) / lh);
-        const int4 s = sat_box(sb, W + 1, y0, y1, x0, x1);
+        const int3 s = sat_box_any(sat, lv.pk, sb, W + 1, y0, y1, x0, x1);
         if (lv.split) {  // fp16 split pixels [B][lh][lw] x (x0 RGB | x1 RGB), k_pnet's level-tile halves
             _Float16 r0, r1, g0, g1, b0, b1;
             split_f16(bin_avg(s.x, y1 - y0, x1 - x0), r0, r1);
@@ -254,7 +341,7 @@ __global__ __launch_bounds__(256) void k_resample_sat_multi(const int3* __restri
     }
 }
 
-void launch_resample_sat_multi(const int3* sat, int B, int H, int W, const ResampleLevels& lv0, hipStream_t st) {
+void launch_resample_sat_multi(const void* sat, int B, int H, int W, const ResampleLevels& lv0, hipStream_t st) {
     VTF_CHECK(lv0.n >= 0 && lv0.n <= ResampleLevels::MAXL, VTF_E_LIMIT, "mtcnn: too many precomputed levels");
     if (lv0.n == 0 || lv0.beg[lv0.n] == 0) return;
     ResampleLevels lv = lv0;
@@ -1858,7 +1945,7 @@ void launch_pnet(bool dense, const uint8_t* frames, int64_t frame_stride, int64_
 // ring of 2*PB+1 rows (the pool window's shared row is kept, not recomputed).
 // w1: [28][32] (k, co; row 27 and channels >= Cout zero); b1, a1: [32].
 template <int S, int PB, int NT, bool XS>
-__global__ __launch_bounds__(NT) void k_cand_front(const int3* __restrict__ sat, int H, int W,
+__global__ __launch_bounds__(NT) void k_cand_front(const void* __restrict__ sat, int pk, int H, int W,
                                                    const float4* __restrict__ boxes, const int32_t* __restrict__ img,
                                                    const float* __restrict__ w1, const _Float16* __restrict__ w1h,
                                                    const float* __restrict__ b1, const float* __restrict__ a1,
@@ -1901,33 +1988,23 @@ __global__ __launch_bounds__(NT) void k_cand_front(const int3* __restrict__ sat,
     }
     // crop bins from the SAT: every thread issues all of its corner loads before using any
     // (the gathers are latency-bound; PIX * 4 loads in flight per thread)
-    const int3* sk = sat + (int64_t)img[k] * (H + 1) * (W + 1);
+    const int64_t sk = (int64_t)img[k] * (H + 1) * (W + 1);
     if (!(dbg & 1)) {
-        int3 cn[PIX][4];
-        int kh[PIX], kw[PIX];
+        int idx[PIX], kh[PIX], kw[PIX];
+        int3 sm[PIX];
 #pragma unroll
-        for (int j = 0; j < PIX; j++) {
-            const int i = min(tid + j * NT, S * S - 1);
-            const int r = i / S, q = i - r * S;
-            const int ys = (r * hc) / S, ye = ((r + 1) * hc + S - 1) / S;
-            const int xs = (q * wc) / S, xe = ((q + 1) * wc + S - 1) / S;
-            kh[j] = ye - ys;
-            kw[j] = xe - xs;
-            const int3* a = sk + (int64_t)(y0 + ys) * (W + 1) + x0;
-            const int3* b = sk + (int64_t)(y0 + ye) * (W + 1) + x0;
-            cn[j][0] = a[xs];
-            cn[j][1] = a[xe];
-            cn[j][2] = b[xs];
-            cn[j][3] = b[xe];
-        }
+        for (int j = 0; j < PIX; j++) idx[j] = min(tid + j * NT, S * S - 1);
+        if (pk)
+            crop_bins<PIX, S, true>(sat, sk, W + 1, y0, x0, hc, wc, idx, sm, kh, kw);
+        else
+            crop_bins<PIX, S, false>(sat, sk, W + 1, y0, x0, hc, wc, idx, sm, kh, kw);
 #pragma unroll
         for (int j = 0; j < PIX; j++) {
             const int i = tid + j * NT;
             if (i < S * S) {
-                const int3 &a = cn[j][0], &b = cn[j][1], &c = cn[j][2], &d = cn[j][3];
-                const float r = bin_avg(d.x - b.x - c.x + a.x, kh[j], kw[j]);
-                const float g = bin_avg(d.y - b.y - c.y + a.y, kh[j], kw[j]);
-                const float bl = bin_avg(d.z - b.z - c.z + a.z, kh[j], kw[j]);
+                const float r = bin_avg(sm[j].x, kh[j], kw[j]);
+                const float g = bin_avg(sm[j].y, kh[j], kw[j]);
+                const float bl = bin_avg(sm[j].z, kh[j], kw[j]);
                 if (XS) {
                     _Float16 r0, r1, g0, g1, b0, b1_;
                     split_f16(r, r0, r1);
@@ -2108,7 +2185,7 @@ __device__ inline void wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 template <int NWV>
-__global__ __launch_bounds__(64 * NWV) void k_cand_front_w24(const int3* __restrict__ sat, int H, int W,
+__global__ __launch_bounds__(64 * NWV) void k_cand_front_w24(const void* __restrict__ sat, int pk, int H, int W,
                                                              const float4* __restrict__ boxes,
                                                              const int32_t* __restrict__ img, int64_t n,
                                                              const _Float16* __restrict__ w1h,
@@ -2142,34 +2219,24 @@ __global__ __launch_bounds__(64 * NWV) void k_cand_front_w24(const int3* __restr
         cp1[S * S] = z;
     }
     // crop: 9 pixels per lane in 3 rounds of 3 (12 SAT corner loads in flight per round)
-    const int3* sk = sat + (int64_t)img[k] * (H + 1) * (W + 1);
+    const int64_t sk = (int64_t)img[k] * (H + 1) * (W + 1);
 #pragma unroll
     for (int rd = 0; rd < 3; rd++) {
-        int3 cn[3][4];
-        int kh[3], kw[3];
+        int idx[3], kh[3], kw[3];
+        int3 sm[3];
+#pragma unroll
+        for (int j = 0; j < 3; j++) idx[j] = lane + 64 * (3 * rd + j);
+        if (pk)
+            crop_bins<3, S, true>(sat, sk, W + 1, y0, x0, hc, wc, idx, sm, kh, kw);
+        else
+            crop_bins<3, S, false>(sat, sk, W + 1, y0, x0, hc, wc, idx, sm, kh, kw);
 #pragma unroll
         for (int j = 0; j < 3; j++) {
-            const int i = lane + 64 * (3 * rd + j);
-            const int r = i / S, q = i - r * S;
-            const int ys = (r * hc) / S, ye = ((r + 1) * hc + S - 1) / S;
-            const int xs = (q * wc) / S, xe = ((q + 1) * wc + S - 1) / S;
-            kh[j] = ye - ys;
-            kw[j] = xe - xs;
-            const int3* a = sk + (int64_t)(y0 + ys) * (W + 1) + x0;
-            const int3* b = sk + (int64_t)(y0 + ye) * (W + 1) + x0;
-            cn[j][0] = a[xs];
-            cn[j][1] = a[xe];
-            cn[j][2] = b[xs];
-            cn[j][3] = b[xe];
-        }
-#pragma unroll
-        for (int j = 0; j < 3; j++) {
-            const int i = lane + 64 * (3 * rd + j);
-            const int3 &a = cn[j][0], &b = cn[j][1], &c = cn[j][2], &d = cn[j][3];
+            const int i = idx[j];
             _Float16 r0, r1, g0, g1, c0, c1;
-            split_f16(bin_avg(d.x - b.x - c.x + a.x, kh[j], kw[j]), r0, r1);
-            split_f16(bin_avg(d.y - b.y - c.y + a.y, kh[j], kw[j]), g0, g1);
-            split_f16(bin_avg(d.z - b.z - c.z + a.z, kh[j], kw[j]), c0, c1);
+            split_f16(bin_avg(sm[j].x, kh[j], kw[j]), r0, r1);
+            split_f16(bin_avg(sm[j].y, kh[j], kw[j]), g0, g1);
+            split_f16(bin_avg(sm[j].z, kh[j], kw[j]), c0, c1);
             cp0[i] = h4{r0, g0, c0, (_Float16)0.f};
             if (!exact) cp1[i] = h4{r1, g1, c1, (_Float16)0.f};
         }
@@ -2271,9 +2338,9 @@ static bool wave_front() {
     return !(e && std::atoi(e) == 0);
 }
 
-void launch_cand_front(bool onet, const int3* sat, int H, int W, const float4* boxes, const int32_t* img, int64_t n,
-                       const float* w1, const _Float16* w1h, const float* b1, const float* a1, float* out, int32_t* err,
-                       hipStream_t st, int* ovf) {
+void launch_cand_front(bool onet, const void* sat, int pk, int H, int W, const float4* boxes, const int32_t* img,
+                       int64_t n, const float* w1, const _Float16* w1h, const float* b1, const float* a1, float* out,
+                       int32_t* err, hipStream_t st, int* ovf) {
     if (n <= 0) return;
     static const int dbg = [] {  // phase-skip mask for profiling (VTF_FRONT_DEBUG): 1 crop, 2 conv1, 4 pool
         const char* e = std::getenv("VTF_FRONT_DEBUG");
@@ -2286,19 +2353,19 @@ void launch_cand_front(bool onet, const int3* sat, int H, int W, const float4* b
     const int pb = pbe ? std::atoi(pbe) : 3;
     // w1h (split conv1 planes) selects conv1 on fp16 matrix cores; null keeps the fp32 MFMA path
     if (onet && w1h && pb == 2)
-        k_cand_front<48, 2, 512, true><<<(unsigned)n, 512, 0, st>>>(sat, H, W, boxes, img, w1, w1h, b1, a1, out, err, dbg, ovf);
+        k_cand_front<48, 2, 512, true><<<(unsigned)n, 512, 0, st>>>(sat, pk, H, W, boxes, img, w1, w1h, b1, a1, out, err, dbg, ovf);
     else if (onet && w1h && pb == 3)
-        k_cand_front<48, 3, 512, true><<<(unsigned)n, 512, 0, st>>>(sat, H, W, boxes, img, w1, w1h, b1, a1, out, err, dbg, ovf);
+        k_cand_front<48, 3, 512, true><<<(unsigned)n, 512, 0, st>>>(sat, pk, H, W, boxes, img, w1, w1h, b1, a1, out, err, dbg, ovf);
     else if (onet && w1h)
-        k_cand_front<48, 1, 512, true><<<(unsigned)n, 512, 0, st>>>(sat, H, W, boxes, img, w1, w1h, b1, a1, out, err, dbg, ovf);
+        k_cand_front<48, 1, 512, true><<<(unsigned)n, 512, 0, st>>>(sat, pk, H, W, boxes, img, w1, w1h, b1, a1, out, err, dbg, ovf);
     else if (onet)
-        k_cand_front<48, 1, 512, false><<<(unsigned)n, 512, 0, st>>>(sat, H, W, boxes, img, w1, w1h, b1, a1, out, err, dbg, ovf);
+        k_cand_front<48, 1, 512, false><<<(unsigned)n, 512, 0, st>>>(sat, pk, H, W, boxes, img, w1, w1h, b1, a1, out, err, dbg, ovf);
     else if (w1h && ovf && wave_front() && !dbg)
-        k_cand_front_w24<4><<<(unsigned)cdiv(n, 4), 256, 0, st>>>(sat, H, W, boxes, img, n, w1h, b1, a1, out, err, ovf);
+        k_cand_front_w24<4><<<(unsigned)cdiv(n, 4), 256, 0, st>>>(sat, pk, H, W, boxes, img, n, w1h, b1, a1, out, err, ovf);
     else if (w1h)
-        k_cand_front<24, 3, 256, true><<<(unsigned)n, 256, 0, st>>>(sat, H, W, boxes, img, w1, w1h, b1, a1, out, err, dbg, ovf);
+        k_cand_front<24, 3, 256, true><<<(unsigned)n, 256, 0, st>>>(sat, pk, H, W, boxes, img, w1, w1h, b1, a1, out, err, dbg, ovf);
     else
-        k_cand_front<24, 3, 256, false><<<(unsigned)n, 256, 0, st>>>(sat, H, W, boxes, img, w1, w1h, b1, a1, out, err, dbg, ovf);
+        k_cand_front<24, 3, 256, false><<<(unsigned)n, 256, 0, st>>>(sat, pk, H, W, boxes, img, w1, w1h, b1, a1, out, err, dbg, ovf);
 }
 
 // heads: x [n, D] -> softmax(x W1^T + b1)[:, 1], x W2^T + b2 (4), optional x W3^T + b3 (10).

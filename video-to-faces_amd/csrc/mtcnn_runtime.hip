@@ -98,6 +98,7 @@ __global__ void k_gather_rows(const int32_t* idx, int64_t n, const float* in, in
 
 struct Mtcnn {
     int device = 0;
+    int sat_pk = 0;  // the current det-batch's SAT layout (mtcnn_dev.hpp; launch_sat)
     hipStream_t st = 0;
     float* d_w = nullptr;
     PNetW pw{};
@@ -668,7 +669,7 @@ static void run_candidates_sp(Mtcnn& m, bool onet, const void* x0, int64_t n, fl
 // deferred != null: the caller zeroed d_ovf / err in the stage's opening launch and reads the guard
 // back with its compaction sync (*deferred = true when the guarded split path ran); it then calls
 // cand_rerun_fp32 if the guard tripped.
-static void cand_nets(Mtcnn& m, bool onet, const int3* sat, int H, int W, const float4* boxes, const int32_t* img,
+static void cand_nets(Mtcnn& m, bool onet, const void* sat, int H, int W, const float4* boxes, const int32_t* img,
                       int64_t n, float4* reg, float* lm, float* prob, int32_t* err, bool* deferred = nullptr) {
     if (n <= 0) return;
     hipStream_t st = m.st;
@@ -677,7 +678,7 @@ static void cand_nets(Mtcnn& m, bool onet, const int3* sat, int H, int W, const 
         const int P2 = cand_fused_side(onet), C2 = onet ? 64 : 48;
         float* x2 = m.ar.get<float>(S_CROP, (size_t)n * P2 * P2 * C2);
         VTF_HIP(hipMemsetAsync(m.d_ovf + 1, 0, 4, st));
-        launch_cand_fused(onet, sat, H, W, boxes, img, n, m.cf[net], x2, err, m.d_ovf + 1, st);
+        launch_cand_fused(onet, sat, m.sat_pk, H, W, boxes, img, n, m.cf[net], x2, err, m.d_ovf + 1, st);
         run_candidates(m, onet, x2, n, reg, lm, prob, 2);
         int f_ovf = 0;
         VTF_HIP(hipMemcpyAsync(&f_ovf, m.d_ovf + 1, 4, hipMemcpyDeviceToHost, st));
@@ -693,7 +694,7 @@ static void cand_nets(Mtcnn& m, bool onet, const int3* sat, int H, int W, const 
     if (sp_ok) {
         // split-pair path: front end writes split pairs, layers on the LDS-DMA conv kernel
         if (!deferred) VTF_HIP(hipMemsetAsync(m.d_ovf, 0, 4, st));
-        launch_cand_front(onet, sat, H, W, boxes, img, n, m.fw[rl], m.cf[net].w1h, onet ? m.ol[0].b : m.rl[0].b,
+        launch_cand_front(onet, sat, m.sat_pk, H, W, boxes, img, n, m.fw[rl], m.cf[net].w1h, onet ? m.ol[0].b : m.rl[0].b,
                           onet ? m.ol[0].a : m.rl[0].a, x0, err, st, m.d_ovf);
         run_candidates_sp(m, onet, x0, n, reg, lm, prob);
         if (m.cand_x[net] == 1) return;  // operand range proven from the weights
@@ -706,14 +707,14 @@ static void cand_nets(Mtcnn& m, bool onet, const int3* sat, int H, int W, const 
         VTF_HIP(hipStreamSynchronize(st));
         if (!ovf) return;
         VTF_HIP(hipMemsetAsync(err, 0, 4, st));  // the fp32 re-run counts invalid boxes again
-        launch_cand_front(onet, sat, H, W, boxes, img, n, m.fw[rl], nullptr, onet ? m.ol[0].b : m.rl[0].b,
+        launch_cand_front(onet, sat, m.sat_pk, H, W, boxes, img, n, m.fw[rl], nullptr, onet ? m.ol[0].b : m.rl[0].b,
                           onet ? m.ol[0].a : m.rl[0].a, x0, err, st);
         run_candidates(m, onet, x0, n, reg, lm, prob, 1, 1);
         return;
     }
     // conv1 on split fp16 unless the fp32 paths are forced (crop values lie in [-1, 1]: no range
     // guard needed)
-    launch_cand_front(onet, sat, H, W, boxes, img, n, m.fw[rl], m.cand_x[net] != 0 ? m.cf[net].w1h : nullptr,
+    launch_cand_front(onet, sat, m.sat_pk, H, W, boxes, img, n, m.fw[rl], m.cand_x[net] != 0 ? m.cf[net].w1h : nullptr,
                       onet ? m.ol[0].b : m.rl[0].b, onet ? m.ol[0].a : m.rl[0].a, x0, err, st);
     run_candidates(m, onet, x0, n, reg, lm, prob, 1, m.fused && m.cand_x[net] != 0 ? 1 : 0);
 }
@@ -770,14 +771,14 @@ static void d2h_sync(void* dst, const void* src, size_t bytes, hipStream_t st) {
 
 // the guarded split path tripped (an operand reached the fp16 range): the stage's nets again on
 // the fp32 path (the error counter recounts out-of-frame candidates)
-static void cand_rerun_fp32(Mtcnn& m, bool onet, const int3* sat, int H, int W, const float4* boxes,
+static void cand_rerun_fp32(Mtcnn& m, bool onet, const void* sat, int H, int W, const float4* boxes,
                             const int32_t* img, int64_t n, float4* reg, float* lm, float* prob, int32_t* err) {
     hipStream_t st = m.st;
     const int net = onet ? 1 : 0;
     const int P = cand_front_side(onet);
     float* x0 = m.ar.get<float>(S_CROP, (size_t)n * P * P * 32);
     VTF_HIP(hipMemsetAsync(err, 0, 4, st));
-    launch_cand_front(onet, sat, H, W, boxes, img, n, m.fw[net], nullptr, onet ? m.ol[0].b : m.rl[0].b,
+    launch_cand_front(onet, sat, m.sat_pk, H, W, boxes, img, n, m.fw[net], nullptr, onet ? m.ol[0].b : m.rl[0].b,
                       onet ? m.ol[0].a : m.rl[0].a, x0, err, st);
     run_candidates(m, onet, x0, n, reg, lm, prob, 1, 1);
 }
@@ -869,8 +870,14 @@ static void detect(Mtcnn& m, const uint8_t* frames, int on_dev, int B, int H, in
     // tile kernel their long serial bin sums would leave a few workgroups as a long tail.
     // summed-area table of the preprocessed frames: O(1) exact bin sums for the downsampled
     // levels and the stage-2/3 candidate crops
+    // (12 B per entry allocated: either layout fits)
     int3* sat = m.ar.get<int3>(S_SAT, (size_t)B * (H + 1) * (W + 1));
-    launch_sat(fr, fstride, rstride, B, H, W, sat, st, d_cnt, NL + 4);
+    {
+        int min_lh = H, min_lw = W;
+        for (auto& L : lv) min_lh = std::min(min_lh, L.lh), min_lw = std::min(min_lw, L.lw);
+        m.sat_pk = sat_pack_ok(H, W, min_lh, min_lw) ? 1 : 0;
+    }
+    launch_sat(fr, fstride, rstride, B, H, W, sat, st, d_cnt, NL + 4, m.sat_pk);
     {
         // split mode: every downsampled level is precomputed as fp16 split pixels (12 B; k_pnet's
         // fill is then a straight 12-byte copy -- the in-kernel bin sums of these levels were
@@ -886,6 +893,7 @@ static void detect(Mtcnn& m, const uint8_t* frames, int on_dev, int B, int H, in
         float* pre = pre_elems ? m.ar.get<float>(S_PRE, pre_elems) : nullptr;
         ResampleLevels rl{};
         rl.split = split ? 1 : 0;
+        rl.pk = m.sat_pk;
         for (auto& L : lv) {
             L.pre = nullptr;
             L.pad = 0;
@@ -1250,9 +1258,10 @@ int vtf_mtcnn_pnet_level(vtf_mtcnn_t h, const uint8_t* d_frames, int B, int H, i
                   VTF_E_LIMIT, "mtcnn: pyramid level too large for PNet's 32-bit bin math");
         if ((int64_t)H > 2 * (int64_t)lh) {
             int3* sat = h->m.ar.get<int3>(S_SAT, (size_t)B * (H + 1) * (W + 1));
-            launch_sat(d_frames, frame_stride, row_stride, B, H, W, sat, h->m.st);
+            const int pk = sat_pack_ok(H, W, lh, lw) ? 1 : 0;
+            launch_sat(d_frames, frame_stride, row_stride, B, H, W, sat, h->m.st, nullptr, 0, pk);
             float* pre = h->m.ar.get<float>(S_PRE, (int64_t)B * 3 * lh * lw);
-            launch_resample_sat(sat, B, H, W, lh, lw, pre, h->m.st);
+            launch_resample_sat(sat, pk, B, H, W, lh, lw, pre, h->m.st);
             L.pre = pre;
         }
         PNetLevel* d_lv = h->m.ar.get<PNetLevel>(S_LEVELS, 1);
@@ -1273,8 +1282,9 @@ int vtf_mtcnn_resample(vtf_mtcnn_t h, const uint8_t* d_frames, int B, int H, int
     return guarded_on(h ? h->m.device : -1, [&] {
         VTF_CHECK(h && d_frames && d_out, VTF_E_ARG, "null argument");
         int3* sat = h->m.ar.get<int3>(S_SAT, (size_t)B * (H + 1) * (W + 1));
-        launch_sat(d_frames, frame_stride, row_stride, B, H, W, sat, h->m.st);
-        launch_resample_sat(sat, B, H, W, lh, lw, d_out, h->m.st);
+        const int pk = sat_pack_ok(H, W, lh, lw) ? 1 : 0;
+        launch_sat(d_frames, frame_stride, row_stride, B, H, W, sat, h->m.st, nullptr, 0, pk);
+        launch_resample_sat(sat, pk, B, H, W, lh, lw, d_out, h->m.st);
         VTF_HIP(hipStreamSynchronize(h->m.st));
     });
 }
