@@ -88,6 +88,23 @@ def test_mtcnn_b16_device_crops(g):
     np.testing.assert_array_equal(got, ref)
 
 
+def test_mtcnn_sat_layouts_bit_identical(g, monkeypatch):
+    """The packed 8-byte SAT (default when every bin is under 8224 px) and the int3 SAT
+    (VTF_SAT_PACK=0, the fallback for larger bins) give identical detections on config 2's
+    det-batch: the box sums are exact integers either way (mtcnn_dev.hpp)."""
+    from videotofaces import synth
+    from videotofaces.detectors.mtcnn import MTCNN
+    frames = torch.from_numpy(synth.make_frames(16, seed=100)).cuda()
+    m = MTCNN('cuda:0')
+    packed = m(frames, 5)
+    monkeypatch.setenv('VTF_SAT_PACK', '0')
+    wide = m(frames, 5)
+    assert [r.shape[0] for r in packed] == [r.shape[0] for r in wide]
+    for a, b in zip(packed, wide):
+        np.testing.assert_array_equal(a, b)
+    np.testing.assert_array_equal([r.shape[0] for r in packed], g['mtcnn_b16_ms5_counts'])
+
+
 @pytest.mark.parametrize('env', [{'VTF_PNET_PR': '0'}, {'VTF_PNET_X': '0', 'VTF_PNET_PR': '0'}])
 def test_mtcnn_b16_pnet_variants(g, env, monkeypatch):
     """k_pnet's launch plans on config 2's det-batch against the same reference golden: the default

@@ -261,10 +261,8 @@ void launch_sat(const uint8_t* frames, int64_t frame_stride, int64_t row_stride,
 // the largest bin a det-batch reads -- the downsampled pyramid levels' bins and the 24 / 48 crops
 // of candidate boxes clipped to the frame -- must stay below that (VTF_SAT_PACK=0: int3 always)
 bool sat_pack_ok(int H, int W, int min_lh, int min_lw) {
-    static const bool on = [] {
-        const char* e = std::getenv("VTF_SAT_PACK");
-        return !(e && std::atoi(e) == 0);
-    }();
+    const char* e = std::getenv("VTF_SAT_PACK");  // (read per det-batch: the tests run both layouts)
+    const bool on = !(e && std::atoi(e) == 0);
     auto bin = [](int64_t L, int64_t l) { return (L + l - 1) / l + 1; };
     const int64_t crop = bin(H, 24) * bin(W, 24);
     const int64_t lvl = bin(H, std::max(1, min_lh)) * bin(W, std::max(1, min_lw));
