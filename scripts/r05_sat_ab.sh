@@ -11,7 +11,7 @@ B="--no-cpu-baseline --no-extras --sustain-frames 0"
 for v in base new; do
   if [ $v = base ]; then export VTF_HIP_LIB=$GRAFT_REPO_ROOT/video-to-faces_amd/lib/libvtf_hip_base.so; else unset VTF_HIP_LIB; fi
   timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/tr_$v -o run -- python3 bench.py --steps 32 --warmup 3 --lanes 1 $B > $O/tr_$v.json 2> $O/tr_$v.err || exit $?
-  python3 scripts/kstats.py $O/tr_$v 12 > $O/kstats_$v.txt 2>&1
+  python3 scripts/kstats.py $O/tr_$v 60 > $O/kstats_$v.txt 2>&1
   echo "== $v"; echo "$(grep -E 'k_sat_|k_resample_sat|k_cand_front' $O/kstats_$v.txt)"
 done
 unset VTF_HIP_LIB
