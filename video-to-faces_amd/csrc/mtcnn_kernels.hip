@@ -212,6 +212,65 @@ __global__ __launch_bounds__(256) void k_sat_rows_pk(const uint8_t* __restrict__
     }
 }
 
+// one WAVE per frame row (4 rows per workgroup, no workgroup barrier), staged through the wave's
+// LDS slice both ways so every global access is lane-contiguous: the row's bytes in as dwords, the
+// lane's 20 consecutive pixels packed and prefix-summed in registers, one wave scan of the lane
+// totals, the row's 1281 sums out as 8-byte stores.  For W <= 1280 with 4-byte aligned rows and
+// W * 3 % 4 == 0 (launch_sat checks).
+__device__ inline void wave_lds_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+__global__ __launch_bounds__(256) void k_sat_rows_pkw(const uint8_t* __restrict__ frames, int64_t frame_stride,
+                                                      int64_t row_stride, int H, int W, int64_t rows,
+                                                      uint64_t* __restrict__ sat, uint32_t* __restrict__ zero,
+                                                      int nzero) {
+    constexpr int PPL = 20;
+    __shared__ uint64_t stage_s[4][64 * PPL];
+    if (blockIdx.x == 0)
+        for (int i = threadIdx.x; i < nzero; i += 256) zero[i] = 0u;
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int64_t rid = (int64_t)blockIdx.x * 4 + wv;
+    if (rid >= rows) return;  // (wave-uniform)
+    const int y = (int)(rid % H), b = (int)(rid / H);
+    const int W1 = W + 1;
+    const uint32_t* row = (const uint32_t*)(frames + (int64_t)b * frame_stride + (int64_t)y * row_stride);
+    uint64_t* out = sat + ((int64_t)b * (H + 1) + y + 1) * W1;
+    uint64_t* stage = stage_s[wv];
+    uint32_t* bytes = (uint32_t*)stage;  // the row's bytes first, then the sums
+    const int nd = W * 3 / 4;
+    for (int d = lane; d < nd; d += 64) bytes[d] = row[d];
+    wave_lds_sync();
+    const int x0 = lane * PPL;
+    uint32_t w[PPL * 3 / 4];
+#pragma unroll
+    for (int d = 0; d < PPL * 3 / 4; d++) w[d] = x0 * 3 / 4 + d < nd ? bytes[x0 * 3 / 4 + d] : 0u;
+    const uint8_t* px = (const uint8_t*)w;
+    uint64_t v[PPL], run = 0;
+#pragma unroll
+    for (int k = 0; k < PPL; k++) {
+        run += x0 + k < W ? sat_pack_px(px + 3 * k) : 0;
+        v[k] = run;
+    }
+    uint64_t incl = run;
+    for (int off = 1; off < 64; off <<= 1) {
+        const uint64_t t = __shfl_up(incl, off);
+        if (lane >= off) incl += t;
+    }
+    const uint64_t excl = incl - run;
+    wave_lds_sync();  // every lane has its bytes in registers
+#pragma unroll
+    for (int k = 0; k < PPL; k++) stage[x0 + k] = excl + v[k];
+    wave_lds_sync();
+    for (int x = lane; x < W; x += 64) out[x + 1] = stage[x];
+    if (lane == 0) out[0] = 0;
+    if (y == 0) {
+        uint64_t* r0 = sat + (int64_t)b * (H + 1) * W1;
+        for (int x = lane; x < W1; x += 64) r0[x] = 0;
+    }
+}
+
 __global__ __launch_bounds__(SAT_COLS * SAT_MAXG) void k_sat_cols_pk(int H, int W, uint64_t* __restrict__ sat) {
     const int W1 = W + 1;
     const int G = blockDim.x / SAT_COLS;
@@ -281,10 +340,15 @@ void launch_sat(const uint8_t* frames, int64_t frame_stride, int64_t row_stride,
     VTF_CHECK(G <= SAT_MAXG, VTF_E_LIMIT, "mtcnn: frames taller than 1536 rows");
     const unsigned gc = (unsigned)(B * ((W + SAT_COLS) / SAT_COLS));
     if (pk) {
-        // (a wave-per-row variant -- 20 pixels per lane in registers, no barrier -- measured
-        //  54.5 -> 79.3 us: its per-lane 160-byte store runs do not coalesce)
-        k_sat_rows_pk<<<(unsigned)((int64_t)B * H), 256, 0, st>>>(frames, frame_stride, row_stride, H, W, (uint64_t*)sat,
-                                                                    zero, nzero);
+        // (the wave-per-row pass without the LDS staging measured 54.5 -> 79.3 us: per-lane 160-byte
+        //  store runs do not coalesce)
+        const int64_t rows = (int64_t)B * H;
+        if (W <= 1280 && W * 3 % 4 == 0 && frame_stride % 4 == 0 && row_stride % 4 == 0 && ((uintptr_t)frames & 3) == 0)
+            k_sat_rows_pkw<<<(unsigned)((rows + 3) / 4), 256, 0, st>>>(frames, frame_stride, row_stride, H, W, rows,
+                                                                        (uint64_t*)sat, zero, nzero);
+        else
+            k_sat_rows_pk<<<(unsigned)rows, 256, 0, st>>>(frames, frame_stride, row_stride, H, W, (uint64_t*)sat, zero,
+                                                          nzero);
         const int GP = (H + SATP_PER - 1) / SATP_PER;
         if (GP <= SATP_MAXG)
             k_sat_cols_pk32<<<(unsigned)(B * ((W + SATP_COLS) / SATP_COLS)), SATP_COLS * GP,
