@@ -41,7 +41,7 @@ def main():
     torch.cuda.synchronize()
     k_ms = e0.elapsed_time(e1) / n
     bytes_per_launch = B * H * W * 4.5
-    res = {'kernel': 'k_yuv_to_bgr<true,false>', 'frames_per_launch': B, 'size': [H, W],
+    res = {'kernel': 'k_yuv420_to_bgr_8x2<false>', 'frames_per_launch': B, 'size': [H, W],
            'avg_launch_us': k_ms * 1e3, 'achieved_GBps': bytes_per_launch / (k_ms * 1e-3) / 1e9, 'peak_GBps': 8000,
            'bytes_per_launch': bytes_per_launch}
     res['frac'] = res['achieved_GBps'] / res['peak_GBps']

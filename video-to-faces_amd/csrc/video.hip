@@ -7,8 +7,9 @@
 // the container and uploads each sampled frame's planes as they lie in the file: 1.5 bytes per
 // pixel over PCIe for 4:2:0 instead of 3) -- and the colour conversion runs on the GPU:
 //
-//   k_yuv_to_bgr: one thread per 4 pixels of a row (4-byte luma load and BGR stores when W % 4
-//   == 0 and the strides allow); chroma sampled nearest (each
+//   k_yuv420_to_bgr_8x2 (4:2:0, W % 8 == 0: one thread per 8 x 2 block, 8-byte accesses) or
+//   k_yuv_to_bgr (any layout: one thread per 4 pixels of a row, 4-byte accesses when W % 4 == 0
+//   and the strides allow); chroma sampled nearest (each
 //   4:2:0 chroma sample covers its 2 x 2 luma block, as cv2.cvtColor(COLOR_YUV2BGR_I420) reads
 //   it) and the BT.601 integer transform with 20 fractional bits:
 //     limited range: y = max(0, Y - 16) * 1220542,  R = (y + 2^19 + 1673527 V') >> 20,
@@ -92,6 +93,40 @@ __global__ __launch_bounds__(256) void k_yuv_to_bgr(const uint8_t* __restrict__ 
     }
 }
 
+// 4:2:0 with W % 8 == 0 and 8-byte aligned planes / strides: one thread per 8 x 2 pixel block --
+// two 8-byte luma loads, one 4-byte load per chroma plane (the block's 4 x 1 chroma samples),
+// six 8-byte stores
+template <bool FULL>
+__global__ __launch_bounds__(256) void k_yuv420_to_bgr_8x2(const uint8_t* __restrict__ in, int64_t n, YuvGeom g,
+                                                           uint8_t* __restrict__ out) {
+    const int gw = g.W >> 3, rp = (g.H + 1) >> 1;
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    const int64_t per = (int64_t)rp * gw;
+    if (i >= n * per) return;
+    const int64_t f = i / per;
+    const int rem = (int)(i - f * per);
+    const int r = rem / gw, x0 = (rem - r * gw) * 8;
+    const uint8_t* Yp = in + f * g.in_stride;
+    const uint8_t* Up = Yp + (int64_t)g.H * g.W;
+    const uint8_t* Vp = Up + (int64_t)g.cw * g.ch;
+    const uint32_t uv = *(const uint32_t*)(Up + r * g.cw + (x0 >> 1));
+    const uint32_t vv = *(const uint32_t*)(Vp + r * g.cw + (x0 >> 1));
+#pragma unroll
+    for (int h = 0; h < 2; h++) {
+        const int y = 2 * r + h;
+        if (y >= g.H) break;
+        const uint64_t yv = *(const uint64_t*)(Yp + (int64_t)y * g.W + x0);
+        uint8_t px[24];
+#pragma unroll
+        for (int k = 0; k < 8; k++)
+            yuv_px<FULL>((int)((yv >> (8 * k)) & 255u), (int)((uv >> (8 * (k >> 1))) & 255u),
+                         (int)((vv >> (8 * (k >> 1))) & 255u), px[3 * k], px[3 * k + 1], px[3 * k + 2]);
+        uint64_t* o = (uint64_t*)(out + f * g.out_fstride + (int64_t)y * g.out_rstride + (int64_t)x0 * 3);
+#pragma unroll
+        for (int j = 0; j < 3; j++) o[j] = (uint64_t)pack4(px + 8 * j) | (uint64_t)pack4(px + 8 * j + 4) << 32;
+    }
+}
+
 }  // namespace
 
 }  // namespace vtf
@@ -122,6 +157,18 @@ extern "C" int vtf_yuv_to_bgr(const uint8_t* d_yuv, int64_t n, int H, int W, int
         const int64_t items = n * H * (int64_t)((W + 3) / 4);
         VTF_CHECK(items / 256 < (int64_t)1 << 31, VTF_E_LIMIT, "yuv_to_bgr: too many frames in one call");
         hipStream_t st = (hipStream_t)hip_stream;
+        const bool v8 = chroma == 420 && W % 8 == 0 && in_frame_stride % 8 == 0 && out_frame_stride % 8 == 0 &&
+                        out_row_stride % 8 == 0 && ((uintptr_t)d_yuv & 7) == 0 && ((uintptr_t)d_bgr & 7) == 0;
+        if (v8) {
+            const int64_t blocks = n * ((H + 1) / 2) * (int64_t)(W / 8);
+            const unsigned grid8 = (unsigned)((blocks + 255) / 256);
+            if (g.full)
+                k_yuv420_to_bgr_8x2<true><<<grid8, 256, 0, st>>>(d_yuv, n, g, d_bgr);
+            else
+                k_yuv420_to_bgr_8x2<false><<<grid8, 256, 0, st>>>(d_yuv, n, g, d_bgr);
+            VTF_HIP(hipGetLastError());
+            return;
+        }
         const bool vec = W % 4 == 0 && in_frame_stride % 4 == 0 && out_frame_stride % 4 == 0 && out_row_stride % 4 == 0 &&
                          ((uintptr_t)d_yuv & 3) == 0 && ((uintptr_t)d_bgr & 3) == 0;
         const unsigned grid = (unsigned)((items + 255) / 256);
