@@ -105,6 +105,23 @@ def test_mtcnn_sat_layouts_bit_identical(g, monkeypatch):
     np.testing.assert_array_equal([r.shape[0] for r in packed], g['mtcnn_b16_ms5_counts'])
 
 
+def test_mtcnn_strided_view_matches_contiguous():
+    """A video_area-style view (rows and columns cropped in place: the frame base 9 bytes past a
+    4-byte boundary) runs the block-per-row SAT pass, its contiguous copy the wave-per-row pass
+    with LDS staging: identical detections either way."""
+    from videotofaces import synth
+    from videotofaces.detectors.mtcnn import MTCNN
+    frames = torch.from_numpy(synth.make_frames(8, seed=7)).cuda()
+    view = frames[:, 10:710, 3:1279]
+    m = MTCNN('cuda:0')
+    a = m(view, 5)
+    b = m(view.contiguous(), 5)
+    assert sum(r.shape[0] for r in a) > 0
+    assert [r.shape[0] for r in a] == [r.shape[0] for r in b]
+    for x, y in zip(a, b):
+        np.testing.assert_array_equal(x, y)
+
+
 @pytest.mark.parametrize('env', [{'VTF_PNET_PR': '0'}, {'VTF_PNET_X': '0', 'VTF_PNET_PR': '0'}])
 def test_mtcnn_b16_pnet_variants(g, env, monkeypatch):
     """k_pnet's launch plans on config 2's det-batch against the same reference golden: the default
