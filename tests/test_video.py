@@ -168,3 +168,27 @@ def _map_name(name, idx):
     file name '<frame %06d>_<face>.jpg' of one run in the other's numbering."""
     stem, rest = name.split('_', 1)
     return '%06d' % (idx.index(int(stem)) + 1) + '_' + rest
+
+
+@pytest.mark.gpu
+def test_video_to_faces_on_y4m_with_video_area(tmp_path):
+    """video_area on a .y4m source crops the device frames as a strided view (no copy): the faces
+    equal the same call on the restatement's decoded frames with the same area."""
+    from videotofaces import synth, video_to_faces
+    src = synth.make_frames(8, seed=9)
+    H, W = src.shape[1:3]
+    planes = synth.bgr_to_yuv420(src)
+    f = str(tmp_path / 'clip.y4m')
+    write_y4m(f, planes, H, W, fps='1:1')
+    dec = oy.yuv_to_bgr(planes, H, W)
+    area = (101, 37, 1181, 683)
+    kw = dict(mode='detection', style='live', det_batch_size=4, det_min_size=10, video_step=1.0, video_area=area)
+    out_a, out_b = tmp_path / 'a', tmp_path / 'b'
+    out_a.mkdir()
+    out_b.mkdir()
+    video_to_faces(f, out_dir=str(out_a), **kw)
+    video_to_faces(np.ascontiguousarray(dec), out_dir=str(out_b), **kw)
+    fa, fb = sorted(os.listdir(out_a / 'faces')), sorted(os.listdir(out_b / 'faces'))
+    assert fa and fa == fb
+    for x in fa:
+        assert (out_a / 'faces' / x).read_bytes() == (out_b / 'faces' / x).read_bytes()
