@@ -599,11 +599,13 @@ struct SPCfg {
     static_assert(SPAN % 8 == 0 && FM >= 1 && NS >= 2 && NS <= 4 && SM * 2 <= 160 * 1024, "span-pool tile");
 };
 
-// NS B stages: NS - 1 weight k-steps in flight
-template <int BM, int BN, int SPAN, int NS>
+// NS B stages: NS - 1 weight k-steps in flight; FNU: the 16-column fragments computed (RNet's
+// 48 output channels: 3 of the tile's 4 -- the weight rows past Cout are staged but never used)
+template <int BM, int BN, int SPAN, int NS, int FNU = BN / 16>
 __global__ __launch_bounds__(256, 2) void k_conv_span_pool(ConvParams p, SpanPool sp) {
     using C = SPCfg<BM, BN, SPAN, NS>;
-    constexpr int FM = C::FM, FN = C::FN, PB = C::PB;
+    static_assert(FNU >= 1 && FNU <= C::FN, "fragments used");
+    constexpr int FM = C::FM, FN = FNU, PB = C::PB;
     __shared__ __attribute__((aligned(16))) char smem[C::SM];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int t = blockIdx.x;
@@ -1219,6 +1221,8 @@ bool launch_conv_span_pool(ConvParams p, int k, int s, void* pout, int& POH, int
         k_conv_span_pool<SPOOL_BM, 64, SPOOL_SPAN, 3><<<(unsigned)grid, 256, 0, st>>>(p, sp);
     else if (ns == 4)
         k_conv_span_pool<SPOOL_BM, 64, SPOOL_SPAN, 4><<<(unsigned)grid, 256, 0, st>>>(p, sp);
+    else if (p.Cout <= 48)
+        k_conv_span_pool<SPOOL_BM, 64, SPOOL_SPAN, 2, 3><<<(unsigned)grid, 256, 0, st>>>(p, sp);
     else
         k_conv_span_pool<SPOOL_BM, 64, SPOOL_SPAN, 2><<<(unsigned)grid, 256, 0, st>>>(p, sp);
     POH = sp.POH;
