@@ -69,9 +69,9 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E (MI355X_MICROARCH.md)
 VIT_GFLOP = {'vit_b': 11.27, 'vit_l': 39.78}  # per face at 128x128
 ENC_NAMES = {'facenet': 'FaceNet', 'vit_b': 'ViT-B/16', 'vit_l': 'ViT-L/16'}
 CONFIGS = {
-    'c2': dict(det_model='mtcnn', enc_model='facenet', enc_precision='bf16', frame='720p', det_batch=16),
+    'c2': dict(det_model='mtcnn', enc_model='facenet', enc_precision='bf16', frame='720p', det_batch=16, pool=0),
     'c3': dict(det_model='yolo', det_precision='x3', enc_model='facenet', enc_precision='bf16', frame='720p',
-               det_batch=32),
+               det_batch=32, pool=0),
     'c4': dict(det_model='none', enc_model='vit_l', enc_precision='f16x', frame='224'),
     'c5': dict(det_model='yolo', det_precision='x3', enc_model='vit_l', enc_precision='f16x', frame='1080p',
                det_batch=32, grouping=True, pool=0),
@@ -97,16 +97,16 @@ def parse(argv=None):
     ap.add_argument('--frame', choices=['720p', '1080p', '224'])
     ap.add_argument('--min-face-size', type=float, default=5.0)
     ap.add_argument('--pool', type=int, default=None,
-                    help='distinct synthetic frames of the global frame sequence, cycled (default 32; c5: 0 = '
-                         'every frame of the run distinct, generated on the device)')
+                    help='distinct synthetic frames of the global frame sequence, cycled; 0 (the detector '
+                         'configs\' default) = every frame of the timed region distinct, generated on the device')
     ap.add_argument('--lanes', type=int, default=4, help='concurrent det-batch pipelines (threads + HIP streams) per GPU')
     ap.add_argument('--hw-queues', type=int, default=8,
                     help='GPU_MAX_HW_QUEUES for this process (set before HIP starts; 0 = keep the environment)')
     ap.add_argument('--sustain-frames', type=int, default=10000,
                     help='frames of the sustained leg (BASELINE config 2: 10k frames), 0 = skip')
     ap.add_argument('--cpu-frames', type=int, default=None,
-                    help='frames per repeat of the bounded CPU-baseline sample (default 8 mtcnn / 16 yolo; '
-                         'warm-up 1 frame, min of --cpu-repeats)')
+                    help='frames per repeat of the CPU-baseline sample (default: BASELINE config 1\'s 64 for '
+                         'MTCNN, 16 for YOLO; warm-up 1 frame, min of --cpu-repeats)')
     ap.add_argument('--cpu-repeats', type=int, default=3)
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--no-extras', action='store_true', help='skip the solo / sustained / host-frame / drift legs')
@@ -134,7 +134,7 @@ def parse(argv=None):
     if a.steps is None:
         a.steps = max(1, -(-a.sustain_frames // a.det_batch)) if a.det_model != 'none' and a.sustain_frames > 0 else 20
     if a.cpu_frames is None:
-        a.cpu_frames = 16 if yolo else 8
+        a.cpu_frames = 16 if yolo else 64
     a.H, a.W = {'720p': (720, 1280), '1080p': (1080, 1920), '224': (224, 224)}[a.frame]
     return a
 
@@ -270,8 +270,8 @@ def _make_detector(args, dev, fp32=False):
 def rank_frames(args, ctx, n_steps, seed=1000):
     """This rank's part of ONE global synthetic frame sequence: the run's world * n_steps
     det-batches split by parallel.shard_batches (whole det-batches, rank order = frame order).
-    Returns (frames on the device, offset of the rank's first frame in them, host copy of up to
-    32 of the frames for the CPU-baseline / host-frame / drift legs).
+    Returns (frames on the device, offset of the rank's first frame in them, host copy of the
+    first max(32, cpu_frames) frames for the CPU-baseline / host-frame / drift legs).
       pool > 0: the sequence cycles `pool` frames (synth.make_frames, seeded; frame g is pool
                 frame g % pool), kept on the device once;
       pool = 0: every frame distinct (synth.make_frames_device: frame g's content depends only on
@@ -285,7 +285,8 @@ def rank_frames(args, ctx, n_steps, seed=1000):
         frames_np = synth.make_frames(pool_n, args.H, args.W, seed=seed)
         return torch.from_numpy(frames_np).to(ctx.device), lo % pool_n, frames_np
     frames = synth.make_frames_device(lo, hi, args.H, args.W, seed=seed, device=ctx.device)
-    return frames, 0, frames[:max(B, 32 // B * B)].cpu().numpy()
+    n_host = max(B, -(-max(32, args.cpu_frames) // B) * B)
+    return frames, 0, frames[:n_host].cpu().numpy()
 
 
 class DetEncPipeline:
@@ -485,7 +486,9 @@ class EncodePipeline:
     def __init__(self, args, dev, rank):
         from videotofaces import synth
         self.args, self.dev, self.B = args, dev, args.enc_batch
-        self.pool_n = max(self.B, 4 * self.B)
+        # every crop of the warm-up + timed steps distinct (2,944 crops = 443 MB at the defaults:
+        # larger than the 256 MB Infinity Cache, so the reads come from HBM)
+        self.pool_n = max(self.B, (max(args.warmup, 1) + args.steps) * self.B)
         self.crops_u8 = torch.from_numpy(synth.make_crops(self.pool_n, 224, seed=1 + rank)).to(dev)
         self.boxes = torch.tensor([[i, 0, 0, 224, 224] for i in range(self.pool_n)], dtype=torch.int32, device=dev)
         self.enc = _make_encoder(args, dev)

@@ -85,6 +85,12 @@ int vtf_mtcnn_detect_crops(vtf_mtcnn_t h, const uint8_t* frames, int frames_on_d
  * [7] final faces. */
 int vtf_mtcnn_stats(vtf_mtcnn_t h, int64_t* out8);
 
+/* Parity introspection (tests): enable = 1 / 0 turns recording of the stage-1 candidate set on /
+ * off for later detect calls (-1 leaves it), then the last call's stage-1 keys -- (level << 32 |
+ * (b * ph + y) * pw + x) of every cell with p >= 0.6, ascending = the reference's per-level
+ * nonzero() order (mtcnn.py:183-186) -- are copied to out (up to cap) and their count to *out_n. */
+int vtf_mtcnn_stage1_keys(vtf_mtcnn_t h, int enable, uint64_t* out, int64_t cap, int64_t* out_n);
+
 /* Kernel timing of the dominant kernel (fused pyramid+PNet) with HIP events recorded on the
  * handle's stream around each launch.  enable=1 resets and starts accumulating; the call
  * returns the totals so far: elapsed ms, launches, algorithmic FLOPs (2*MAC of conv1-3 and

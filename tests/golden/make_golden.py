@@ -542,6 +542,155 @@ def gen_b1():
     np.savez_compressed(os.path.join(HERE, 'b1.npz'), **out)
 
 
+# MTCNN's float -> integer gates, per golden frame: the stage-1 / -2 / -3 score gates (p >= 0.6,
+# s > 0.7: mtcnn.py:183, 215, 230), every batched_nms IoU against its threshold (0.5 / 0.7: 196,
+# 205, 219) and the final IoM against 0.7 (242, 295-297).  A frame is flagged when one of its
+# candidates sits within the device's tolerance of a gate: a score within FLAG_SCORE (5x the P/R/
+# O-Net parity bar 2e-5), an IoU / IoM within FLAG_OVR of the threshold on refined boxes (stage 2
+# / 3: box error <= 2e-3 px) or exactly ON it on stage 1's integer-grid boxes (bit-exact there).
+FLAG_SCORE, FLAG_OVR, FLAG_OVR_EXACT = 1e-4, 1e-3, 1e-6
+# stage-1 cells within NEAR_P of the p >= 0.6 gate (the PNet parity bar, test_pnet_level_vs_oracle)
+# are recorded by key: the device's stage-1 set may differ from the reference's only there
+NEAR_P = 2e-5
+MTCNN_FLAG_RUNS = (('mtcnn_b16_ms5', 16, 100, 5), ('mtcnn_b4_ms20', 4, 101, 20),
+                   ('b1_110', 1, 110, 5), ('b1_111', 1, 111, 5), ('b1_112', 1, 112, 5), ('b1_113', 1, 113, 5))
+
+
+def _pair_margin(b, grp, thr, iom, plus1):
+    """min |overlap - thr| over the same-group pairs (torchvision IoU: no +1, fp32 as nms_kernel;
+    _nms_vectorized IoM: +1 widths, pairs with a positive intersection) per group id"""
+    out = {}
+    b = b.astype(np.float32)
+    one = np.float32(1 if plus1 else 0)
+    for gid in np.unique(grp):
+        q = b[grp == gid]
+        if len(q) < 2:
+            continue
+        best = np.inf
+        area = (q[:, 2] - q[:, 0] + one) * (q[:, 3] - q[:, 1] + one)
+        for i0 in range(0, len(q), 512):
+            a = q[i0:i0 + 512, None]
+            w = np.minimum(a[..., 2], q[None, :, 2]) - np.maximum(a[..., 0], q[None, :, 0]) + one
+            h = np.minimum(a[..., 3], q[None, :, 3]) - np.maximum(a[..., 1], q[None, :, 1]) + one
+            if iom:
+                ok = (w > 0) & (h > 0)
+                ov = (w * h) / np.minimum(area[i0:i0 + 512, None], area[None, :])
+            else:
+                w, h = np.maximum(w, 0), np.maximum(h, 0)
+                inter = w * h
+                ov = inter / ((area[i0:i0 + 512, None] + area[None, :]) - inter)
+                ok = np.ones_like(ov, bool)
+            ii = np.arange(i0, min(i0 + 512, len(q)))[:, None] < np.arange(len(q))[None, :]  # i < j pairs
+            m = np.abs(ov.astype(np.float64) - thr)[ok & ii]
+            if m.size:
+                best = min(best, float(m.min()))
+        out[int(gid)] = best
+    return out
+
+
+def gen_mtcnn_flags():
+    """Near-threshold report of the MTCNN goldens (shapes.npz b16 / b4, b1.npz): the reference's
+    forward on the same frames with its gates instrumented (wrappers around PNet / RNet / ONet,
+    the candidate crops, torchvision.ops.batched_nms and _nms_vectorized record every decision's
+    distance to its threshold per frame).  Saved per run: the flagged frames and each frame's
+    smallest score / IoU / IoM margins; the GPU tests assert those frames' rows (all frames are
+    asserted; the flagged ones are the ones a less precise kernel would lose first)."""
+    load_ref()
+    m = importlib.import_module('ref_vtf.detectors.mtcnn')
+    net = _load(m.MTCNN('cpu'), synth.make_params('mtcnn'))
+    ops = sys.modules['torchvision.ops']
+    out = {}
+    for name, n, seed, ms in MTCNN_FLAG_RUNS:
+        rec = {'score': np.full(n, np.inf), 'iou': np.full(n, np.inf), 'iom': np.full(n, np.inf)}
+        exact_iou = [True]  # stage-1 calls (integer-grid boxes) until the first RNet call
+        cand_img = []
+        ev = []  # the gates' integer outcomes in call order: (stage event, count)
+        s1_keys, s1_near, s1_near_p = [], [], []
+
+        def note(kind, img, marg):
+            for i, v in zip(img, marg):
+                rec[kind][int(i)] = min(rec[kind][int(i)], float(v))
+
+        pnet_f, rnet_f, onet_f = net.pnet.forward, net.rnet.forward, net.onet.forward
+        crop_f, nms_v, bnms = net._get_cropped_candidates, net._nms_vectorized, ops.batched_nms
+
+        def pnet(x):
+            reg, prob = pnet_f(x)
+            d = np.abs(prob.numpy().astype(np.float64) - 0.6).reshape(prob.shape[0], -1).min(1)
+            note('score', range(prob.shape[0]), d)
+            ev.append(('mask', int((prob >= 0.6).sum())))
+            lvl = sum(1 for e in ev if e[0] == 'mask') - 1
+            pn = prob.numpy()
+            lin = np.arange(pn.size, dtype=np.uint64).reshape(pn.shape)  # (b * ph + y) * pw + x
+            s1_keys.append((np.uint64(lvl) << np.uint64(32)) | lin[pn >= 0.6])
+            near = np.abs(pn.astype(np.float64) - 0.6) < NEAR_P
+            s1_near.append((np.uint64(lvl) << np.uint64(32)) | lin[near])
+            s1_near_p.append(pn[near])
+            return reg, prob
+
+        def crops(x, imgidx, boxes, size):
+            exact_iou[0] = False
+            cand_img.append(imgidx.numpy().copy())
+            ev.append(('crops', int(imgidx.shape[0])))
+            return crop_f(x, imgidx, boxes, size)
+
+        def scored(f):
+            def g(x):
+                r = f(x)
+                s_ = r[-1].numpy().astype(np.float64)
+                note('score', cand_img[-1], np.abs(s_ - 0.7))
+                ev.append(('pass', int((r[-1] > 0.7).sum())))
+                return r
+            return g
+
+        def batched(boxes, scores, idxs, thr):
+            for gid, v in _pair_margin(boxes.numpy(), idxs.numpy(), thr, False, False).items():
+                if not exact_iou[0] or v <= FLAG_OVR_EXACT:
+                    rec['iou'][gid] = min(rec['iou'][gid], v)
+            k = bnms(boxes, scores, idxs, thr)
+            ev.append(('nms', int(k.shape[0])))
+            return k
+
+        def vect(boxes, scores, classes, thresh, method, chain_suppression=True):
+            for gid, v in _pair_margin(boxes.numpy(), classes.numpy(), thresh, True, True).items():
+                rec['iom'][gid] = min(rec['iom'][gid], v)
+            k = nms_v(boxes, scores, classes, thresh, method, chain_suppression)
+            ev.append(('iom', int(k.shape[0])))
+            return k
+
+        net.pnet.forward, net.rnet.forward, net.onet.forward = pnet, scored(rnet_f), scored(onet_f)
+        net._get_cropped_candidates, net._nms_vectorized, ops.batched_nms = crops, vect, batched
+        try:
+            with torch.inference_mode():
+                res = net(list(synth.make_frames(n, seed=seed)), ms)
+        finally:
+            del net.pnet.forward, net.rnet.forward, net.onet.forward, net._get_cropped_candidates, net._nms_vectorized
+            ops.batched_nms = bnms
+        flagged = [f for f in range(n) if rec['score'][f] < FLAG_SCORE or rec['iou'][f] < FLAG_OVR
+                   or rec['iom'][f] < FLAG_OVR]
+        out[name + '_flagged'] = np.array(flagged, np.int64)
+        out[name + '_counts'] = np.array([r.shape[0] for r in res], np.int64)
+        # the device's stage counters (vtf_mtcnn_stats 1..7): stage-1 cells through the gate, kept
+        # by the per-level NMS, by the cross-level NMS; RNet passes, kept by its NMS; ONet passes;
+        # kept by the IoM NMS
+        c1 = ev.index(next(e for e in ev if e[0] == 'crops'))
+        nms1 = [v for k_, v in ev[:c1] if k_ == 'nms']
+        rest = ev[c1:]
+        st = [sum(v for k_, v in ev[:c1] if k_ == 'mask'), sum(nms1[:-1]), nms1[-1],
+              [v for k_, v in rest if k_ == 'pass'][0], [v for k_, v in rest if k_ == 'nms'][0],
+              [v for k_, v in rest if k_ == 'pass'][1], [v for k_, v in rest if k_ == 'iom'][0]]
+        out[name + '_stage_counts'] = np.array(st, np.int64)
+        out[name + '_s1_keys'] = np.concatenate(s1_keys)
+        out[name + '_s1_near_keys'] = np.concatenate(s1_near)
+        out[name + '_s1_near_p'] = np.concatenate(s1_near_p).astype(np.float32)
+        for k in ('score', 'iou', 'iom'):
+            out[name + '_margin_' + k] = rec[k]
+        print(name, 'stage counts', st, 'flagged', flagged, 'min margins score %.3g iou %.3g iom %.3g'
+              % (rec['score'].min(), rec['iou'].min(), rec['iom'].min()), flush=True)
+    out['thresholds'] = np.array([FLAG_SCORE, FLAG_OVR, FLAG_OVR_EXACT, NEAR_P])
+    np.savez_compressed(os.path.join(HERE, 'mtcnn_flags.npz'), **out)
+
+
 # BASELINE config 5 chain: YOLO on 1080p frames -> box filter/adjust -> ViT-L on the crops ->
 # cosine dedupe -> KMeans k=2..16 + scores; bench settings of the box filter
 # (frames = synth.make_frame_sets(sets, per_set, 1080, 1920, seed, faces_per_frame): 128 frames)
@@ -630,6 +779,71 @@ def gen_chain():
           'flagged frames', flagged,
           'best k', ks[int(np.argmax([s[0] for s in scores]))],
           'sklearn 1 vs %d threads: rows differing per k' % os.cpu_count(), (labels != labels_mt).sum(1).tolist())
+
+
+# BASELINE config 4's chain at N >= 10k: ViT-L/16 on 10,368 face crops (the blobs of 864 720p
+# synthetic frames, 12 per frame: synth.make_frame_sets / face_rects; config 4's pre-cropped
+# synth.make_crops patches of one background are near-duplicates of each other under the
+# synthetic ViT-L -- the dedupe keeps 7 of 10,240 -- so they cannot exercise the sweep) ->
+# remove_dupes_overall('enc') -> cluster_faces' KMeans sweep k = 2..16 + scores on the kept rows
+C4CHAIN = dict(sets=54, per_set=16, faces_per_frame=12, seed=4100, thr=0.25, ks=list(range(2, 17)), sample=64)
+
+
+def gen_c4chain():
+    """Config-4-shaped grouping chain at N >= 10k with the reference's own ViT-L (AnimeVIT's blob
+    restated: INTER_LINEAR to 128, parity-unpinned step) and dupes.remove_dupes_overall, then
+    sklearn's KMeans / scores as cluster_faces calls them (1 OpenMP thread, and every core).
+    Stored: a hash of the frames, the crop rectangles, every `sample`-th embedding row (the
+    encoder's 1e-4 check), the dedupe result, int8 labels and the scores.  `perturbed_rows`:
+    rows whose label moves when the kept X gets N(0, 1e-5) noise (the sweep's sensitivity at
+    the encoder's tolerance; the device test reports its own)."""
+    import hashlib
+    import json
+    import sklearn.metrics
+    load_ref()
+    sys.path.insert(0, ROOT)
+    from oracle.facenet import resize_linear_u8
+    c = C4CHAIN
+    v = importlib.import_module('ref_vtf.encoders.vit')
+    dupes = importlib.import_module('ref_vtf.dupes')
+    vnet = _load(v.ViT('cpu', 128, 16, 1024, 24), synth.make_params('vit_l'))
+    frames, faces = synth.make_frame_sets(c['sets'], c['per_set'], 720, 1280, c['seed'], c['faces_per_frame'],
+                                          return_faces=True)
+    rects = synth.face_rects(faces, 720, 1280)
+    X = []
+    for i in range(0, len(rects), 64):
+        blobs = [(torch.from_numpy(np.ascontiguousarray(resize_linear_u8(frames[f, y1:y2, x1:x2], 128)[:, :, ::-1]
+                                                        .transpose(2, 0, 1))).float() - 127.5) * np.float32(1 / 127.5)
+                 for f, x1, y1, x2, y2 in rects[i:i + 64]]
+        with torch.inference_mode():
+            X.append(vnet(torch.stack(blobs)).numpy())
+        if i % 1024 == 0:
+            print('c4chain: encoded', i, flush=True)
+    X = np.concatenate(X)
+    names = ['f%05d.jpg' % i for i in range(len(X))]
+    with tempfile.TemporaryDirectory() as td:
+        os.makedirs(os.path.join(td, 'faces'))
+        for n in names:
+            open(os.path.join(td, 'faces', n), 'w').close()
+        Xk, goods = dupes.remove_dupes_overall(X.copy(), names, ('enc', c['thr'], False, td))
+    keep = np.array([int(n[1:6]) for n in goods], np.int64)
+    ks = [k for k in c['ks'] if k < len(Xk)]
+    labels = _sk_kmeans_sweep(Xk, ks, 1)
+    labels_mt = _sk_kmeans_sweep(Xk, ks, os.cpu_count())
+    scores = [(sklearn.metrics.silhouette_score(Xk, lb), sklearn.metrics.calinski_harabasz_score(Xk, lb),
+               sklearn.metrics.davies_bouldin_score(Xk, lb)) for lb in labels]
+    rng = np.random.default_rng(0)
+    Xp = (Xk + rng.normal(0, 1e-5, Xk.shape)).astype(np.float32)
+    pert = (_sk_kmeans_sweep(Xp, ks, 1) != labels).sum(1)
+    np.savez_compressed(os.path.join(HERE, 'c4chain.npz'), params_json=np.array(json.dumps(c)),
+                        frames_sha256=np.frombuffer(hashlib.sha256(frames.tobytes()).digest(), np.uint8),
+                        rects=rects, X_sample=X[::c['sample']], dedupe_keep=keep.astype(np.int32), k=np.array(ks),
+                        labels=labels.astype(np.int8), labels_mt=labels_mt.astype(np.int8),
+                        mt_threads=np.array(os.cpu_count()), scores=np.array(scores, np.float64),
+                        perturbed_rows=pert.astype(np.int64))
+    print('c4chain: N', len(X), 'kept', len(keep), 'best k', ks[int(np.argmax([s[0] for s in scores]))],
+          'sklearn 1 vs %d threads: rows differing per k' % os.cpu_count(), (labels != labels_mt).sum(1).tolist(),
+          'rows moved by 1e-5 noise per k', pert.tolist())
 
 
 C3 = dict(frames=32, seed=110, mscore=0.4, msize=50, mborder=5, scale=(1.5, 1.5, 2.2, 1.2), square=True)

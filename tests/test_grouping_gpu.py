@@ -125,6 +125,23 @@ def test_classify_nan_rows_vs_oracle():
     np.testing.assert_array_equal(inds, ref.argmin(1))
 
 
+def test_wide_rows_vs_oracle():
+    """Rows wider than k_row_normalize's LDS staging (D > 4096: the four staged rows would pass the
+    64 KB dynamic-LDS default) take the global-memory form, same bits: dedupe minima / argmins and
+    the classify distance matrix vs the restatement (oracle/grouping_oracle.c)."""
+    from videotofaces import dupes, grouping, synth
+    from oracle import grouping as og
+    rng = np.random.default_rng(21)
+    X = rng.normal(0, 1, (400, 4160)).astype(np.float32)
+    X[300:310] = X[0:10] + 1e-3
+    mins, inds = dupes.cosine_dedupe_device(torch.from_numpy(X).cuda())
+    rm, ri = og.cosine_dedupe(X)
+    np.testing.assert_array_equal(mins, rm)
+    np.testing.assert_array_equal(inds, ri)
+    Xc, R = synth.classify_set(64, 4, 4160, 0.9, seed=3)
+    np.testing.assert_array_equal(grouping.cosine_distances_device(Xc, R), og.classify_distances_exact(Xc, R))
+
+
 @pytest.fixture(scope='module')
 def km():
     from videotofaces import synth

@@ -156,6 +156,39 @@ def test_batched_nms_nan_scores_exact(n):
     assert got.tolist() == ref.tolist()
 
 
+@pytest.mark.parametrize('n,base,spread', [(3000, 20000, 7), (900, 20000, 3), (17000, 5, 17000)])
+def test_batched_nms_large_and_many_class_ids(n, base, spread):
+    """Category ids far above the box count (torchvision takes any id): the vanilla path (n > 1000)
+    groups by id only, so the library remaps the ids to dense ranks; the coordinate-trick path
+    (900 boxes) keeps the values, which set its offsets' fp32 rounding.  17,000 distinct ids give
+    more segments than k_nms_out's LDS prefix holds (15,000): the prefix comes from global memory
+    and the call takes the merge sort."""
+    from videotofaces.detectors.mtcnn import batched_nms
+    from oracle import nms as onms
+    b, s, _ = _random_boxes(n, 1, seed=n + spread, grid=True)
+    rng = np.random.default_rng(n)
+    ids = rng.permutation(n) if spread >= n else rng.integers(0, spread, n)  # (all distinct: S = n)
+    i = torch.from_numpy((base + ids).astype(np.int64))
+    ref = onms.batched_nms(b, s, i, 0.5)
+    got = batched_nms(b.cuda(), s.cuda(), i.cuda(), 0.5).cpu()
+    assert got.tolist() == ref.tolist()
+
+
+@pytest.mark.parametrize('n', [3000, 900])
+def test_batched_nms_signed_zero_scores_exact(n):
+    """-0 and +0 scores compare equal in torch's sort: a stable order keeps them by index and the
+    vanilla path's final unstable sort treats them as a tie (desc_key maps -0 to +0's key)."""
+    from videotofaces.detectors.mtcnn import batched_nms
+    from oracle import nms as onms
+    b, s, i = _random_boxes(n, 3, seed=17, grid=True)
+    s = s.clone()
+    s[::5] = -0.0
+    s[1::5] = 0.0
+    ref = onms.batched_nms(b, s, i, 0.5)
+    got = batched_nms(b.cuda(), s.cuda(), i.cuda(), 0.5).cpu()
+    assert got.tolist() == ref.tolist()
+
+
 def _match(res, counts, boxes, atol):
     k = 0
     for r, c in zip(res, counts):

@@ -39,24 +39,61 @@ def _u8(seed, shape):
     return np.random.default_rng(seed).integers(0, 256, shape, dtype=np.uint8)
 
 
+@pytest.fixture(scope='module')
+def mflags():
+    return np.load(os.path.join(GOLDEN, 'mtcnn_flags.npz'))
+
+
+def _mtcnn_gates(mflags, name, model, res, ref_rows):
+    """Integer outcomes of every MTCNN gate vs the reference (make_golden.py gen_mtcnn_flags).
+    Stage 1: the device's candidate set (cells with p >= 0.6, by key; recording enabled before the
+    call) equals the reference's except on cells the reference puts within 2e-5 of the gate (the
+    PNet parity bar) -- there the fp32 summation order decides, and the reference's own rounding is
+    of that size; when the sets are equal, every later counter (kept by the per-level and
+    cross-level NMS, RNet / ONet passes, kept by the stage-2 and the IoM NMS) is exact.  Then the
+    golden's flagged frames (a score within 1e-4 of its gate, an IoU / IoM within 1e-3 of its
+    threshold, or exactly on it for stage 1's integer boxes) row for row."""
+    keys = model.stage1_keys()
+    ref, near = mflags[name + '_s1_keys'], mflags[name + '_s1_near_keys']
+    diff = np.setxor1d(keys, ref)
+    assert np.isin(diff, near).all(), ('stage-1 candidates differ away from the gate', diff[~np.isin(diff, near)][:8])
+    if diff.size == 0:
+        np.testing.assert_array_equal(model.last_stats[1:8], mflags[name + '_stage_counts'], err_msg='stage counts')
+    else:
+        p = mflags[name + '_s1_near_p'][np.searchsorted(near, diff)]
+        print('%s: %d stage-1 cell(s) on the other side of the gate, |p - 0.6| = %s' % (name, diff.size, np.abs(p.astype(np.float64) - 0.6)))
+    fl = mflags[name + '_flagged']
+    for f in fl:
+        assert res[f].shape == ref_rows[f].shape, (name, f)
+        np.testing.assert_allclose(res[f], ref_rows[f], rtol=1e-5, atol=2e-3, err_msg='flagged frame %d' % f)
+    print('%s: stage counts %s (device %s); stage-1 cells within 2e-5 of the gate %d, differing %d; flagged frames '
+          '%d of %d, smallest margins: score %.2g, IoU %.2g, IoM %.2g'
+          % (name, mflags[name + '_stage_counts'].tolist(), model.last_stats[1:8].tolist(), near.size, diff.size, len(fl),
+             len(res), mflags[name + '_margin_score'].min(), mflags[name + '_margin_iou'].min(), mflags[name + '_margin_iom'].min()))
+
+
 @pytest.mark.parametrize('name,n,seed,ms', [('mtcnn_b16_ms5', 16, 100, 5), ('mtcnn_b4_ms20', 4, 101, 20)])
-def test_mtcnn_benchmark_batches(g, name, n, seed, ms):
+def test_mtcnn_benchmark_batches(g, mflags, name, n, seed, ms):
     from videotofaces import synth
     from videotofaces.detectors.mtcnn import MTCNN
     frames = synth.make_frames(n, seed=seed)
-    res = MTCNN('cuda:0')(torch.from_numpy(frames).cuda(), ms)
+    m = MTCNN('cuda:0')
+    m.stage1_keys(1)
+    res = m(torch.from_numpy(frames).cuda(), ms)
     np.testing.assert_array_equal([r.shape[0] for r in res], g[name + '_counts'])
     np.testing.assert_allclose(np.concatenate(res), g[name + '_boxes'], rtol=1e-5, atol=2e-3)
+    _mtcnn_gates(mflags, name, m, res, np.split(g[name + '_boxes'], np.cumsum(g[name + '_counts'])[:-1]))
 
 
-def test_mtcnn_det_batch1_720p():
+def test_mtcnn_det_batch1_720p(mflags):
     """BASELINE config 1's shape: MTCNN on single 720p frames (det-batch 1, min_face_size 5),
     four calls, against the reference module (tests/golden/make_golden.py gen_b1): counts exact,
-    boxes 2e-3 px, landmarks 2e-3 px."""
+    boxes 2e-3 px, landmarks 2e-3 px, every gate's integer outcome (stage counters) exact."""
     from videotofaces import synth
     from videotofaces.detectors.mtcnn import MTCNN
     gb = np.load(os.path.join(GOLDEN, 'b1.npz'))
     m = MTCNN('cuda:0')
+    m.stage1_keys(1)
     for seed in gb['seeds']:
         frames = synth.make_frames(1, seed=int(seed))
         res, ldm = m(torch.from_numpy(frames).cuda(), 5, return_landmarks=True)
@@ -64,6 +101,7 @@ def test_mtcnn_det_batch1_720p():
         assert res[0].shape == ref.shape, (seed, res[0].shape, ref.shape)
         np.testing.assert_allclose(res[0], ref, rtol=1e-5, atol=2e-3)
         np.testing.assert_allclose(ldm[0], gb['b1_%d_landmarks' % seed], rtol=1e-5, atol=2e-3)
+        _mtcnn_gates(mflags, 'b1_%d' % seed, m, res, [ref])
 
 
 def test_mtcnn_b16_device_crops(g):
@@ -287,17 +325,55 @@ def test_config5_chain(chain, precision):
     np.testing.assert_array_equal(np.nonzero(~(mins <= 0.25))[0], chain['dedupe_keep'])
     ks = [int(k) for k in chain['k']]
     # on the golden's own embeddings (bit-exact input) the labels equal sklearn's (1 OpenMP
-    # thread; sklearn with every core agrees on these rows); the device embeddings (within
-    # 1e-4 of them) are reported
+    # thread; sklearn with every core agrees on these rows)
     Xk = chain['X'][chain['dedupe_keep']]
     assert np.array_equal(chain['labels'], chain['labels_mt'])
     labels, scores = cluster_sweep(Xk, ks, 0)
     for i, k in enumerate(ks):
         np.testing.assert_array_equal(labels[i], chain['labels'][i], err_msg='k=%d' % k)
     np.testing.assert_allclose(np.array([s[1:] for s in scores]), chain['scores'], rtol=1e-5)
+    # the device embeddings (within 1e-4 of the golden's) -> the same labels for every k
     labels_dev, _ = cluster_sweep(X.cpu().numpy()[chain['dedupe_keep']], ks, 0)
     print('device embeddings: rows whose label differs per k',
           [int((a != b).sum()) for a, b in zip(labels_dev, chain['labels'])])
+    for i, k in enumerate(ks):
+        np.testing.assert_array_equal(labels_dev[i], chain['labels'][i], err_msg='device embeddings, k=%d' % k)
+
+
+@pytest.mark.parametrize('precision', ['fp32', 'f16x'])
+def test_config4_chain_10k(precision):
+    """Config 4's encoder -> grouping chain at N = 10,368: ViT-L/16 on the device over the face
+    crops of 864 synthetic 720p frames (regenerated here, hash-checked; the golden's crop
+    rectangles) -> fused cosine dedupe -> KMeans k = 2..16 on the kept rows, against the
+    reference's ViT-L + remove_dupes_overall + sklearn (make_golden.py gen_c4chain): sampled
+    embeddings within 1e-4, the keep set and every k's labels exact on the DEVICE embeddings,
+    silhouette / CH / DB within 1e-3."""
+    import hashlib
+    from videotofaces import synth, dupes
+    from videotofaces.encoders.vit import ViT
+    from videotofaces.grouping import cluster_sweep
+    gc = np.load(os.path.join(GOLDEN, 'c4chain.npz'))
+    c = json.loads(str(gc['params_json']))
+    frames = synth.make_frame_sets(c['sets'], c['per_set'], 720, 1280, c['seed'], c['faces_per_frame'], threads=16)
+    assert hashlib.sha256(frames.tobytes()).digest() == gc['frames_sha256'].tobytes()
+    fd = torch.from_numpy(frames).cuda()
+    rects = torch.from_numpy(gc['rects']).cuda()
+    n = rects.shape[0]
+    enc = ViT('cuda:0', synth.make_params('vit_l'), isL=True, precision=precision)
+    X = torch.cat([enc.encode_crops(fd, rects[i:i + 128]) for i in range(0, n, 128)])
+    Xh = X.cpu().numpy()
+    np.testing.assert_allclose(Xh[::c['sample']], gc['X_sample'], rtol=0, atol=1e-4)
+    mins, _ = dupes.cosine_dedupe_device(X)
+    keep = np.nonzero(~(mins <= c['thr']))[0]
+    np.testing.assert_array_equal(keep, gc['dedupe_keep'])
+    ks = [int(k) for k in gc['k']]
+    labels, scores = cluster_sweep(Xh[keep], ks, 0)
+    print('c4 chain (%s): N %d, kept %d; rows whose label differs per k %s (sklearn under 1e-5 noise: %s)'
+          % (precision, n, len(keep), [int((a != b).sum()) for a, b in zip(labels, gc['labels'])],
+             gc['perturbed_rows'].tolist()))
+    for i, k in enumerate(ks):
+        np.testing.assert_array_equal(labels[i], gc['labels'][i], err_msg='k=%d' % k)
+    np.testing.assert_allclose(np.array([s[1:] for s in scores]), gc['scores'], rtol=1e-3)
 
 
 def test_cosine_dedupe_keep_set_10k():

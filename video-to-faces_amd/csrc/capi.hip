@@ -1,4 +1,5 @@
 // C-ABI glue: error state, version, standalone box ops (include/vtf.h).
+#include <algorithm>
 #include <map>
 #include <memory>
 #include <mutex>
@@ -105,15 +106,27 @@ int vtf_batched_nms(const float* d_boxes, const float* d_scores, const int64_t* 
         int32_t* keep = ar.get<int32_t>(2, n);
         k_i64_to_i32<<<cdiv(n, 256), 256, 0, st>>>(d_idxs, n, img);
         VTF_HIP(hipMemsetAsync(call, 0, n * 4, st));
-        // number of distinct class ids bounds the vanilla segment count: use max id + 1
+        // the vanilla segment count is max id + 1.  Above torchvision's coordinate-trick bound
+        // (n * 4 > 4000: one NMS per distinct id, results merged by score) the id values only
+        // group the boxes, so they are remapped to their ranks among the distinct ids (any
+        // category id works, as in torchvision); the trick path keeps them: its offsets are
+        // idx * (max coordinate + 1), so the values set the fp32 rounding
         int32_t mx = 0;
-        {
-            std::vector<int32_t> h(n);
-            VTF_HIP(hipMemcpyAsync(h.data(), img, n * 4, hipMemcpyDeviceToHost, st));
-            VTF_HIP(hipStreamSynchronize(st));
-            for (int32_t v : h) {
-                VTF_CHECK(v >= 0, VTF_E_ARG, "batched_nms: negative class ids are not supported");
-                mx = v > mx ? v : mx;
+        std::vector<int32_t> h(n);
+        VTF_HIP(hipMemcpyAsync(h.data(), img, n * 4, hipMemcpyDeviceToHost, st));
+        VTF_HIP(hipStreamSynchronize(st));
+        for (int32_t v : h) {
+            VTF_CHECK(v >= 0, VTF_E_ARG, "batched_nms: negative class ids are not supported");
+            mx = v > mx ? v : mx;
+        }
+        if (n * 4 > 4000 && mx >= 1) {
+            std::vector<int32_t> u(h);
+            std::sort(u.begin(), u.end());
+            u.erase(std::unique(u.begin(), u.end()), u.end());
+            if ((int64_t)u.size() < (int64_t)mx + 1) {
+                for (auto& v : h) v = (int32_t)(std::lower_bound(u.begin(), u.end(), v) - u.begin());
+                mx = (int32_t)u.size() - 1;
+                VTF_HIP(hipMemcpyAsync(img, h.data(), n * 4, hipMemcpyHostToDevice, st));
             }
         }
         std::vector<int64_t> nk;

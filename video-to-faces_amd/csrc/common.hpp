@@ -178,9 +178,10 @@ inline uint16_t f2bf(float f) {
 }
 
 // descending-order sort key of a float; every NaN maps to one key above +inf, as torch's sort
-// treats NaNs as equal and greater than every number
+// treats NaNs as equal and greater than every number, and -0 maps to +0's key (torch compares
+// them equal: a stable sort keeps them in index order, and the tie checks see them as a tie)
 __host__ __device__ inline uint32_t desc_key(float f) {
-    uint32_t u = f != f ? 0x7fc00000u : f2u(f);
+    uint32_t u = f != f ? 0x7fc00000u : (f == 0.f ? 0u : f2u(f));
     uint32_t asc = (u & 0x80000000u) ? ~u : (u | 0x80000000u);
     return ~asc;
 }

@@ -24,6 +24,8 @@
 // ties resolve to the smallest j = numpy's first argmin.  Nothing N x N ever touches HBM.
 // classify (grouping.py:50-66): argmin / min over C references of cosine distance, in sklearn's
 // bits (k_classify below).
+#include <cstdlib>
+
 #include "common.hpp"
 #include "sk_order.hpp"
 
@@ -34,18 +36,26 @@ typedef __attribute__((ext_vector_type(4))) float f32x4;
 // Xn [N][Dp] = X / ||X|| in sklearn normalize's bits (zero norm -> 1), zero-padded to Dp.  One
 // wave per row: the row is read coalesced into LDS, lanes 0-3 run numpy einsum's four sequential
 // chains over it (sk_order.hpp's order), every lane writes the normalised row coalesced.
+// Rows wider than NRM_LDS_D (the four staged rows would pass the 64 KB dynamic-LDS default) are
+// read from global memory directly (G): the same chains, the same bits.
 constexpr int NRM_W = 4;  // rows (waves) per block
+constexpr int NRM_LDS_D = 4096;
+template <bool G>
 __global__ __launch_bounds__(64 * NRM_W) void k_row_normalize(const float* __restrict__ X, int64_t N, int D, int Dp,
                                                                float* __restrict__ Xn) {
-    extern __shared__ float srow[];  // [NRM_W][D]
+    extern __shared__ float srow[];  // [NRM_W][D] (!G)
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int64_t i = (int64_t)blockIdx.x * NRM_W + w;
     const bool valid = i < N;
-    float* r = srow + w * D;
     const float* x = X + (valid ? i : 0) * D;
-    if (valid)
-        for (int k = lane; k < D; k += 64) r[k] = x[k];
-    __syncthreads();
+    const float* r = x;
+    if (!G) {
+        float* rs = srow + w * D;
+        if (valid)
+            for (int k = lane; k < D; k += 64) rs[k] = x[k];
+        __syncthreads();
+        r = rs;
+    }
     float l = 0.f;  // lane u < 4: numpy's SSE lane u
     if (lane < 4) {
         int t = 0;
@@ -66,7 +76,10 @@ __global__ __launch_bounds__(64 * NRM_W) void k_row_normalize(const float* __res
         for (int k = lane; k < Dp; k += 64) Xn[i * Dp + k] = k < D ? __fdiv_rn(r[k], nrm) : 0.f;
 }
 static void row_normalize(const float* X, int64_t N, int D, int Dp, float* Xn, hipStream_t st) {
-    k_row_normalize<<<cdiv(N, NRM_W), 64 * NRM_W, (size_t)NRM_W * D * 4, st>>>(X, N, D, Dp, Xn);
+    if (D <= NRM_LDS_D)
+        k_row_normalize<false><<<cdiv(N, NRM_W), 64 * NRM_W, (size_t)NRM_W * D * 4, st>>>(X, N, D, Dp, Xn);
+    else
+        k_row_normalize<true><<<cdiv(N, NRM_W), 64 * NRM_W, 0, st>>>(X, N, D, Dp, Xn);
 }
 
 __global__ void k_init_keys(uint64_t* key, int64_t N) {
@@ -283,7 +296,15 @@ __global__ void k_unpack(const uint64_t* __restrict__ key, int64_t N, float* __r
 // Then d = clip(1 - G, 0, 2) (S *= -1; S += 1; np.clip keeps NaN) and numpy's min / first argmin
 // (a NaN wins both).
 enum { CL_BLOCKED = 1, CL_SMALL = 2, CL_GEMV = 3, CL_DOT = 4 };
-constexpr int CL_BLAS_THREADS = 8;  // OpenBLAS threads of the survey container (its 8 cores)
+// OpenBLAS threads of the sgemv output split: the survey container's 8 (its 8 cores) unless
+// VTF_BLAS_THREADS names the reference host's count.  Only CL_GEMV at D n >= 460800 depends on it:
+// its bit parity with sklearn assumes that host's thread count
+constexpr int CL_BLAS_THREADS = 8;
+static int blas_threads() {
+    const char* e = std::getenv("VTF_BLAS_THREADS");
+    const int v = e ? std::atoi(e) : 0;
+    return v >= 1 && v <= 1024 ? v : CL_BLAS_THREADS;
+}
 
 __host__ __device__ inline int classify_mode(int64_t N, int64_t C, int64_t D) {
     if (N == 1 && C == 1) return CL_DOT;
@@ -292,8 +313,8 @@ __host__ __device__ inline int classify_mode(int64_t N, int64_t C, int64_t D) {
 }
 
 // sgemv_t kernel of output o of n: 0 = 4x4, 1 = 4x2, 2 = 4x1
-__device__ inline int gemv_kernel(int64_t o, int64_t n, int64_t D) {
-    const int T = (double)n * D >= 460800.0 ? CL_BLAS_THREADS : 1;
+__device__ inline int gemv_kernel(int64_t o, int64_t n, int64_t D, int threads) {
+    const int T = (double)n * D >= 460800.0 ? threads : 1;
     int64_t a = 0;
     for (int t = 0; a < n; t++) {
         int64_t w = T - t > 1 ? (n - a + (T - t) - 1) / (T - t) : n - a;
@@ -312,7 +333,7 @@ constexpr int CL_R = 16, CL_C = 16, CL_K = 64;
 template <int MODE>
 __global__ __launch_bounds__(256) void k_classify(const float* __restrict__ Xn, const float* __restrict__ Rn, int64_t N,
                                                   int C, int D, int Dp, float* __restrict__ mn,
-                                                  int64_t* __restrict__ arg, float* __restrict__ dist) {
+                                                  int64_t* __restrict__ arg, float* __restrict__ dist, int threads) {
     __shared__ float sX[CL_R][CL_K + 1], sR[CL_C][CL_K + 1];
     __shared__ float sD[CL_R][CL_C];
     const int tid = threadIdx.x, r = tid >> 4, cj = tid & 15;
@@ -328,7 +349,7 @@ __global__ __launch_bounds__(256) void k_classify(const float* __restrict__ Xn, 
         float acc = 0.f, tot = 0.f;
         int kb_end = blas_kblock(D, false);
         int gk = 0;  // CL_GEMV: this output's kernel
-        if (MODE == CL_GEMV) gk = C == 1 ? gemv_kernel(i, N, D) : gemv_kernel(c, C, D);
+        if (MODE == CL_GEMV) gk = C == 1 ? gemv_kernel(i, N, D, threads) : gemv_kernel(c, C, D, threads);
         for (int t0 = 0; t0 < Dp; t0 += CL_K) {
             for (int e = tid; e < CL_R * CL_K; e += 256) {  // rows of 64 floats: coalesced
                 const int rr = e / CL_K, tt = e % CL_K;
@@ -488,12 +509,12 @@ static void cosine_classify(const float* d_X, int64_t N, const float* d_R, int64
     row_normalize(d_X, N, (int)D, Dp, Xn, st);
     row_normalize(d_R, C, (int)D, Dp, Rn, st);
     const unsigned grid = (unsigned)cdiv(N, CL_R);
-    const int c = (int)C, d = (int)D;
+    const int c = (int)C, d = (int)D, bt = blas_threads();
     switch (classify_mode(N, C, D)) {
-        case CL_BLOCKED: k_classify<CL_BLOCKED><<<grid, 256, 0, st>>>(Xn, Rn, N, c, d, Dp, d_min, d_arg, d_dist); break;
-        case CL_SMALL: k_classify<CL_SMALL><<<grid, 256, 0, st>>>(Xn, Rn, N, c, d, Dp, d_min, d_arg, d_dist); break;
-        case CL_GEMV: k_classify<CL_GEMV><<<grid, 256, 0, st>>>(Xn, Rn, N, c, d, Dp, d_min, d_arg, d_dist); break;
-        default: k_classify<CL_DOT><<<grid, 256, 0, st>>>(Xn, Rn, N, c, d, Dp, d_min, d_arg, d_dist); break;
+        case CL_BLOCKED: k_classify<CL_BLOCKED><<<grid, 256, 0, st>>>(Xn, Rn, N, c, d, Dp, d_min, d_arg, d_dist, bt); break;
+        case CL_SMALL: k_classify<CL_SMALL><<<grid, 256, 0, st>>>(Xn, Rn, N, c, d, Dp, d_min, d_arg, d_dist, bt); break;
+        case CL_GEMV: k_classify<CL_GEMV><<<grid, 256, 0, st>>>(Xn, Rn, N, c, d, Dp, d_min, d_arg, d_dist, bt); break;
+        default: k_classify<CL_DOT><<<grid, 256, 0, st>>>(Xn, Rn, N, c, d, Dp, d_min, d_arg, d_dist, bt); break;
     }
     VTF_HIP(hipGetLastError());
 }

@@ -50,7 +50,12 @@ struct PNetOut {
     int dbg;  // phase-skip mask for profiling (env VTF_PNET_DEBUG): 1 fill, 2 conv1, 4 conv2, 8 conv3,
               // 16 no candidate output, 32 no heads, 64 no frame-patch staging; 256 = phase clocks
     unsigned long long* clk;  // [8] summed shader clocks per phase over workgroups (null: off)
+    // k_pnet's vertical-reuse slots (VR_SLOT = 6144 B per workgroup of the exact-levels launch) and
+    // their count: launch_pnet runs the reuse variant when its grid fits (env VTF_PNET_VR=0: off)
+    uint8_t* vr;
+    int64_t vr_slots;
 };
+constexpr int PNET_VR_SLOT = 6144;
 
 // the det-batch's summed-area table (mtcnn_dev.hpp): int3 entries, or packed uint64 (pk) when
 // sat_pack_ok says every bin the det-batch reads is small enough
@@ -73,6 +78,8 @@ void launch_pnet(bool dense, const uint8_t* frames, int64_t frame_stride, int64_
                  const PNetLevel* d_levels, int n_levels, int64_t total_tiles, const PNetW& w, const PNetOut& o,
                  uint32_t* d_tile_ctr, hipStream_t st, int64_t exact_tiles = 0,
                  int64_t pre_from = INT64_MAX);  // d_tile_ctr: 3 zeroed words
+// grid of k_pnet's exact-levels launch over that many tiles (= vertical-reuse slots it needs)
+int64_t pnet_x_grid(int64_t exact_tiles);
 // first tile of the trailing levels precomputed as fp16 split pixels (k_pnet's PR variant)
 int64_t pnet_pre_from(const std::vector<PNetLevel>& lv, int64_t total_tiles);
 // leading tiles of the level plan that k_pnet's exact-levels variant takes (see launch_pnet)

@@ -614,17 +614,49 @@ struct PnLds {
                   "exact-levels k_pnet LDS plan");
 };
 
+// VR (vertical reuse, round 6; the exact-levels variant): a level's tiles are numbered column by
+// column (ty fastest), so a workgroup's consecutive tiles are vertically adjacent.  A tile whose
+// predecessor in its column was the workgroup's previous tile ("continuing") takes that tile's
+// pooled conv1 rows 16..19 and conv2 rows 16, 17 as its own rows 0..3 / 0, 1 -- the same values:
+// the same level pixels through the same arithmetic -- and computes only the rest: level rows
+// 8..41, conv1 on pooled rows 4..19 (80 of 100 fragments), conv2 on rows 2..17 (18 of 21
+// fragments).  The kept rows go through a per-workgroup slot in global memory (written after
+// the tile's conv1 / conv2 with 16-byte stores, read back by LDS-DMA into rows 0..3 / 0, 1 after
+// the next tile's fill / conv1), so the LDS plan is unchanged (four workgroups per CU).
+constexpr int VR_POOL_BYTES = 2 * 4 * PP_W * PQ_C * 2;  // pooled rows 16..19 of both planes: 3840 B
+constexpr int VR_C2_BYTES = 2 * 2 * PC_W * 16 * 2;      // conv2 rows 16, 17 of both planes: 2304 B
+constexpr int VR_SLOT = VR_POOL_BYTES + VR_C2_BYTES;
+constexpr int VR_LROW = 8;                              // first level row a continuing tile fills
+static_assert(VR_POOL_BYTES == 3840 && VR_C2_BYTES == 2304, "VR slot pieces (the DMA piece split below)");
+
+struct TileGeo {
+    int b, ty, tx;
+};
+// tile t of a level -> (frame, tile row, tile column): row-major, or column-major (VR)
+template <bool VR>
+__device__ inline TileGeo tile_geo(int t, const PNetLevel& P) {
+    const int tpi = P.tiles_x * P.tiles_y;
+    const int b = udiv_est(t, tpi), tt = t - b * tpi;
+    if (VR) {
+        const int tx = udiv_est(tt, P.tiles_y);
+        return TileGeo{b, tt - tx * P.tiles_y, tx};
+    }
+    const int ty = udiv_est(tt, P.tiles_x);
+    return TileGeo{b, ty, tt - ty * P.tiles_x};
+}
+
 // PR: the pre-resampled variant (round 3) -- tiles of the downsampled levels, all precomputed as
 // fp16 split pixels by k_resample_sat_multi, on the exact-levels LDS plan (four workgroups per CU):
 // the two-plane level tile (28 KB) does not fit beside the pooled map, so conv1 runs in two halves
 // of 10 pooled rows, each on 22 level rows (14.8 KB) loaded straight from the precomputed level.
-template <bool DENSE, bool X, bool PR = false>
+template <bool DENSE, bool X, bool PR = false, bool VR = false>
 __global__ __launch_bounds__(256, PnLds<X || PR>::GPC) void k_pnet(const uint8_t* __restrict__ frames, int64_t frame_stride,
                                                  int64_t row_stride, int H, int W,
                                                  const PNetLevel* __restrict__ lv, int n_levels,
                                                  int64_t total_tiles, uint32_t* __restrict__ tile_ctr, PNetW wg,
                                                  PNetOut o, int64_t tile_base, int max_chunks, int chunk) {
     using LP = PnLds<X || PR>;
+    static_assert(!VR || (X && !DENSE), "vertical reuse is an exact-levels variant");
     const VTF_CONST float* wf = cptr(wg.c1w);  // fp32 weights (scalar loads at constant offsets)
     // conv / head weights through buffer loads: one lane VGPR offset + constant SGPR offsets,
     // instead of a 64-bit address per k-step (which the compiler would keep live across tiles);
@@ -648,6 +680,7 @@ __global__ __launch_bounds__(256, PnLds<X || PR>::GPC) void k_pnet(const uint8_t
     bool pf_done = false;  // the first 2 KB of this tile's frame patch were staged by the previous tile
     int n_chunks = 0;      // chunks taken after the first (thread 0)
     int L_prev = 0;
+    int64_t blk_prev = -2;  // (VR) the workgroup's previous tile
     // phase timing (debug): thread 0 reads the shader clock after each phase's closing barrier
     const bool clk_on = o.clk != nullptr;
     __shared__ unsigned long long s_tlast;  // (in LDS: a 64-bit register live across the tile loop otherwise)
@@ -721,12 +754,13 @@ __global__ __launch_bounds__(256, PnLds<X || PR>::GPC) void k_pnet(const uint8_t
         const PNetLevel P = load_level(lvc + L);
         L_prev = L;
         // (tile indices are < 2^31: launch_pnet)
-        const int t = (int)(blk - P.tile_beg);
-        const int tiles_per_img = P.tiles_x * P.tiles_y;
-        const int b = udiv_est(t, tiles_per_img);
-        const int tt = t - b * tiles_per_img;
-        const int ty = udiv_est(tt, P.tiles_x);
-        const int oy0 = ty * PT_H, ox0 = (tt - ty * P.tiles_x) * PT_W;
+        const TileGeo tg = tile_geo<VR>((int)(blk - P.tile_beg), P);
+        const int b = tg.b;
+        const int oy0 = tg.ty * PT_H, ox0 = tg.tx * PT_W;
+        // (VR) continuing tile: the previous one was the tile above it, computed by this workgroup
+        const bool cont = VR && blk == blk_prev + 1 && tg.ty > 0;
+        const int lr0 = cont ? VR_LROW : 0;  // first level row to fill
+        blk_prev = blk;
         const uint8_t* fr = frames + (int64_t)b * frame_stride;
         const int L1h = P.lh - 2, L1w = P.lw - 2;
         // lane coordinates laundered per tile: per-lane addressing below is recomputed inside the
@@ -748,7 +782,7 @@ __global__ __launch_bounds__(256, PnLds<X || PR>::GPC) void k_pnet(const uint8_t
         __syncthreads();
         mark(1);  // 1: tile index, level lookup, bins
         // frame patch covering every bin of the tile; staged to LDS with coalesced loads when it fits
-        int fy0 = ybin[0].x, fx0 = xbin[0].x, fy1 = fy0, fx1 = fx0;
+        int fy0 = ybin[lr0].x, fx0 = xbin[0].x, fy1 = fy0, fx1 = fx0;
         {
             int ry = min(PL_H - 1, P.lh - 1 - 2 * oy0), rx = min(PL_W - 1, P.lw - 1 - 2 * ox0);
             fy1 = ybin[ry].y;
@@ -879,7 +913,7 @@ __global__ __launch_bounds__(256, PnLds<X || PR>::GPC) void k_pnet(const uint8_t
             if (tid == 0) lvl[PL_H * PL_W] = h4{(_Float16)0.f, (_Float16)0.f, (_Float16)0.f, (_Float16)0.f};
             // s / kh / kw with kh, kw in {1, 2}: a power-of-two scale, exact
             const float scw = nq > 1 ? 0.001953125f : 0.00390625f;
-            for (int r = fr0; r < PL_H; r += 6) {
+            for (int r = fr0 + lr0; r < PL_H; r += 6) {
                 const ushort2 yb = ybin[r];
                 const int kh = yb.y - yb.x;
                 const s16x4* h = hs + (kh ? yb.x - fy0 : 0) * PL_W + fq;
@@ -964,8 +998,22 @@ __global__ __launch_bounds__(256, PnLds<X || PR>::GPC) void k_pnet(const uint8_t
             store_level(sA, split3, i, in ? div_bin(div_bin(s0, kh), kw) : 0.f, in ? div_bin(div_bin(s1, kh), kw) : 0.f,
                         in ? div_bin(div_bin(s2, kh), kw) : 0.f);
         }
+        // (VR) the previous tile's slot stores (issued long before) have completed before any wave
+        // of this workgroup reads the slot back
+        if (VR && cont) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
         mark(3);  // 3: level tile fill
+        // (VR) pooled rows 0..3 <- the previous tile's rows 16..19 from the workgroup's slot: plane p
+        // rows 0..3 are bytes [p 9600, p 9600 + 1920) of sP; one 1 KB LDS-DMA piece per wave (the
+        // patch and row sums that used sP are dead), waited for before conv1's closing barrier
+        uint8_t* vslot = VR ? o.vr + (int64_t)blockIdx.x * VR_SLOT : nullptr;
+        if (VR && cont) {
+            const int w = __builtin_amdgcn_readfirstlane(wave), pl = w >> 1, hf = w & 1;
+            if (!hf || lane < (VR_POOL_BYTES / 2 - 1024) / 16)
+                __builtin_amdgcn_global_load_lds(
+                    (const void __attribute__((address_space(1)))*)(vslot + pl * (VR_POOL_BYTES / 2) + hf * 1024 + lane * 16),
+                    (void __attribute__((address_space(3)))*)((uint8_t*)sP + pl * (PP_H * PP_W * PQ_C * 2) + hf * 1024), 16, 0, 0);
+        }
 
         // ---- 2. conv1 (3->10, 3x3) + PReLU + maxpool 2x2 ceil.  Default: fp16 matrix cores on
         //         split operands (below).  fp32 fallback: the VALU -- with N = 10 output channels
@@ -1254,10 +1302,11 @@ __global__ __launch_bounds__(256, PnLds<X || PR>::GPC) void k_pnet(const uint8_t
                     return f0;
                 };
                 using I4 = std::integral_constant<int, 4>;
+                const int f0 = wv + (cont ? 4 * FB4 : 0);  // (VR) continuing tile: pooled rows 4..19
                 if (fastpool && unit_slope)
-                    c1k_frags(T{}, I1{}, c1k_frags(T{}, I4{}, wv));
+                    c1k_frags(T{}, I1{}, c1k_frags(T{}, I4{}, f0));
                 else
-                    c1k_frags(F{}, I1{}, c1k_frags(F{}, I2{}, wv));
+                    c1k_frags(F{}, I1{}, c1k_frags(F{}, I2{}, f0));
             } else if (exact) {
                 if (fastpool && unit_slope)
                     conv1_frags(T{}, T{}, I1{}, conv1_frags(T{}, T{}, I2{}, wv));
@@ -1335,8 +1384,26 @@ __global__ __launch_bounds__(256, PnLds<X || PR>::GPC) void k_pnet(const uint8_t
                 }
             }
         }
+        if (VR && cont) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the pooled rows' LDS-DMA
         __syncthreads();
         mark(4);  // 4: conv1 + pool
+        // (VR) does the next tile continue this one (the tile below it, next in this workgroup)?
+        const bool vr_next = VR && __builtin_amdgcn_readfirstlane(s_next) == blk + 1 && tg.ty + 1 < P.tiles_y;
+        if (VR && vr_next && tid < VR_POOL_BYTES / 16) {
+            // pooled rows 16..19 of both planes -> the slot (read again after the next tile's fill)
+            const int pl = tid / (VR_POOL_BYTES / 32), q = tid - pl * (VR_POOL_BYTES / 32);
+            const uint4 v = *(const uint4*)((const uint8_t*)sP + pl * (PP_H * PP_W * PQ_C * 2) + 16 * PP_W * PQ_C * 2 + q * 16);
+            *(uint4*)(vslot + tid * 16) = v;
+        }
+        if (VR && cont) {
+            // conv2 rows 0, 1 <- the previous tile's rows 16, 17 (plane p rows 0, 1 = sA bytes [p 10368,
+            // + 1152)); the level tile there is dead after conv1's barrier; waited for before conv2's
+            const int w = __builtin_amdgcn_readfirstlane(wave), pl = w >> 1, hf = w & 1;
+            if (!hf || lane < (VR_C2_BYTES / 2 - 1024) / 16)
+                __builtin_amdgcn_global_load_lds(
+                    (const void __attribute__((address_space(1)))*)(vslot + VR_POOL_BYTES + pl * (VR_C2_BYTES / 2) + hf * 1024 + lane * 16),
+                    (void __attribute__((address_space(3)))*)((uint8_t*)sA + pl * (PC_H * PC_W * 32) + hf * 1024), 16, 0, 0);
+        }
 
         // ---- 3. conv2 (10->16, 3x3) + PReLU on MFMA: 18 x 18 positions (21 frags of 16), 16
         //         output channels, K = 90; operands gathered from the pooled map.
@@ -1377,12 +1444,15 @@ __global__ __launch_bounds__(256, PnLds<X || PR>::GPC) void k_pnet(const uint8_t
                     aa[i] = wf[PW_P2 + 4 * lkx + i];
                 }
                 _Float16* sO = (_Float16*)sA;
+                // (VR) continuing tile: rows 2..17 only (positions 36.., 18 fragments)
+                const int pb = cont ? 2 * PC_W : 0, nf = cont ? (NPOS - 2 * PC_W) / 16 : NF;
+                static_assert((NPOS - 2 * PC_W) % 16 == 0, "continuing-tile conv2 fragments");
                 auto conv2_frags = [&](auto u_t) {
                 constexpr bool U2 = decltype(u_t)::value;
-                for (int f0 = wave; f0 < NF; f0 += 8) {
+                for (int f0 = wave; f0 < nf; f0 += 8) {
                     const int f1 = f0 + 4;
-                    const bool two = f1 < NF;
-                    const int p0 = min(f0 * 16 + lrx, NPOS - 1), p1 = min((two ? f1 : f0) * 16 + lrx, NPOS - 1);
+                    const bool two = f1 < nf;
+                    const int p0 = min(pb + f0 * 16 + lrx, NPOS - 1), p1 = min(pb + (two ? f1 : f0) * 16 + lrx, NPOS - 1);
                     const int ab0 = ((p0 / PC_W) * PP_W + (p0 % PC_W)) * PQ_C, ab1 = ((p1 / PC_W) * PP_W + (p1 % PC_W)) * PQ_C;
                     f16x8 x[3][2][2];  // [step][fragment][plane]
 #pragma unroll
@@ -1422,7 +1492,7 @@ __global__ __launch_bounds__(256, PnLds<X || PR>::GPC) void k_pnet(const uint8_t
                     }
 #pragma unroll
                     for (int h = 0; h < 2; h++) {
-                        const int q = (h ? f1 : f0) * 16 + lrx;
+                        const int q = pb + (h ? f1 : f0) * 16 + lrx;
                         if (q < NPOS && (h == 0 || two)) {
                             f16x4 v0, v1;
 #pragma unroll
@@ -1511,7 +1581,14 @@ __global__ __launch_bounds__(256, PnLds<X || PR>::GPC) void k_pnet(const uint8_t
                 }
             }
         }
+        if (VR && cont) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // conv2 rows 0, 1 (LDS-DMA)
         __syncthreads();
+        if (VR && vr_next && tid < VR_C2_BYTES / 16) {
+            // conv2 rows 16, 17 of both planes -> the slot (conv3 only reads sA from here on)
+            const int pl = tid / (VR_C2_BYTES / 32), q = tid - pl * (VR_C2_BYTES / 32);
+            const uint4 v = *(const uint4*)((const uint8_t*)sA + pl * (PC_H * PC_W * 32) + 16 * PC_W * 32 + q * 16);
+            *(uint4*)(vslot + VR_POOL_BYTES + tid * 16) = v;
+        }
         if (split3) {
             // conv3's split weights [2][32][144] halves (18 KB, L2-resident) -> the pooled buffer,
             // now free: 18 lane-linear 1 KB LDS-DMA pieces, waited for by the barrier
@@ -1599,13 +1676,13 @@ __global__ __launch_bounds__(256, PnLds<X || PR>::GPC) void k_pnet(const uint8_t
                     while (L2 + 1 < n_levels && nt >= lvc[L2 + 1].tile_beg) L2++;
                     const PNetLevel Q = load_level(lvc + L2);
                     if (!Q.pre) {
-                        const int t2 = (int)(nt - Q.tile_beg);
-                        const int tpi = Q.tiles_x * Q.tiles_y;
-                        const int b2i = udiv_est(t2, tpi), tt2 = t2 - b2i * tpi;
-                        const int ty2 = udiv_est(tt2, Q.tiles_x);
-                        const int oy2 = ty2 * PT_H, ox2 = (tt2 - ty2 * Q.tiles_x) * PT_W;
+                        const TileGeo g2 = tile_geo<VR>((int)(nt - Q.tile_beg), Q);
+                        const int b2i = g2.b;
+                        const int oy2 = g2.ty * PT_H, ox2 = g2.tx * PT_W;
+                        // (the next tile's first level row: VR_LROW when it continues this one)
+                        const int lr2 = VR && nt == blk + 1 && g2.ty > 0 ? VR_LROW : 0;
                         const int ry = min(PL_H - 1, Q.lh - 1 - 2 * oy2), rx = min(PL_W - 1, Q.lw - 1 - 2 * ox2);
-                        const int gy0 = udiv_est(2 * oy2 * H, Q.lh), gy1 = udiv_est((2 * oy2 + ry + 1) * H + Q.lh - 1, Q.lh);
+                        const int gy0 = udiv_est((2 * oy2 + lr2) * H, Q.lh), gy1 = udiv_est((2 * oy2 + ry + 1) * H + Q.lh - 1, Q.lh);
                         const int gx0 = udiv_est(2 * ox2 * W, Q.lw), gx1 = udiv_est((2 * ox2 + rx + 1) * W + Q.lw - 1, Q.lw);
                         const int w3 = (gx1 - gx0) * 3, nb = (gy1 - gy0) * w3;
                         if ((int64_t)(gy1 - gy0) * w3 <= LP::PATCH && nb > 0) {
@@ -1958,6 +2035,42 @@ int64_t pnet_exact_tiles(const std::vector<PNetLevel>& lv, int H, int W, int64_t
     return total_tiles;
 }
 
+static_assert(PNET_VR_SLOT == VR_SLOT, "mtcnn.hpp's VR slot size");
+
+// tiles per atomic chunk (VTF_PNET_CHUNK) and chunks per workgroup (VTF_PNET_QUOTA, 0 = persistent)
+static void pnet_chunking(int& chunk, int& quota) {
+    // (clamped: the kernel keeps tile indices and chunk ends in int)
+    const char* ce = std::getenv("VTF_PNET_CHUNK");
+    chunk = ce && std::atoi(ce) > 0 ? std::min(64, std::atoi(ce)) : PNET_TILE_CHUNK;
+    // (chunk x quota at 8 tiles per workgroup, full default run: 4 x 2 12.26-12.30k, 2 x 4
+    // 12.19-12.21k, 1 x 8 12.18k faces/s)
+    const char* qe = std::getenv("VTF_PNET_QUOTA");
+    quota = qe ? std::min(1 << 16, std::max(0, std::atoi(qe))) : 2;
+}
+
+static int pnet_cus() {
+    int dev = 0, cus = 256;
+    VTF_HIP(hipGetDevice(&dev));
+    VTF_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+    return cus;
+}
+
+static int pnet_wgs(const char* name, int mx) {
+    const char* e = std::getenv(name);
+    const int v = e ? std::atoi(e) : 0;
+    return v >= 1 && v <= mx ? v : mx;
+}
+
+// grid of the exact-levels launch over `exact_tiles` tiles (the vertical-reuse slots it needs)
+int64_t pnet_x_grid(int64_t exact_tiles) {
+    if (exact_tiles <= 0) return 0;
+    int chunk = 0, quota = 0;
+    pnet_chunking(chunk, quota);
+    int64_t grid = std::min<int64_t>(exact_tiles, (int64_t)pnet_cus() * pnet_wgs("VTF_PNET_X_WG_PER_CU", PnLds<true>::GPC));
+    if (quota > 0) grid = std::max<int64_t>(grid, (exact_tiles + (int64_t)quota * chunk - 1) / ((int64_t)quota * chunk));
+    return grid;
+}
+
 void launch_pnet(bool dense, const uint8_t* frames, int64_t frame_stride, int64_t row_stride, int H, int W,
                  const PNetLevel* d_levels, int n_levels, int64_t total_tiles, const PNetW& w, const PNetOut& o,
                  uint32_t* d_tile_ctr, hipStream_t st, int64_t exact_tiles, int64_t pre_from) {
@@ -1968,19 +2081,13 @@ void launch_pnet(bool dense, const uint8_t* frames, int64_t frame_stride, int64_
     // frame patches are read through 32-bit buffer offsets (patch_bytes8)
     VTF_CHECK(row_stride > 0 && row_stride < (int64_t)1 << 24, VTF_E_LIMIT, "mtcnn: frame row stride too large");
     // (level sizes: checked where the level plan is built, mtcnn_runtime)
-    int dev = 0, cus = 256;
-    VTF_HIP(hipGetDevice(&dev));
-    VTF_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+    const int cus = pnet_cus();
     // persistent workgroups per CU: the variant's LDS limit fills every CU; a smaller count leaves
     // room for concurrently running lanes' kernels (env VTF_PNET_WG_PER_CU / VTF_PNET_X_WG_PER_CU,
     // experiments).  Tiles [0, exact_tiles) -- the leading upsampled levels, checked on the host --
     // run on the exact-levels variant (X, four workgroups per CU) when the split mode is on
     // (VTF_PNET_X=0: one launch of the general kernel).
-    auto wgs = [](const char* name, int mx) {
-        const char* e = std::getenv(name);
-        const int v = e ? std::atoi(e) : 0;
-        return v >= 1 && v <= mx ? v : mx;
-    };
+    auto wgs = pnet_wgs;
     const char* xe = std::getenv("VTF_PNET_X");
     // chunks per workgroup (VTF_PNET_QUOTA, 0 = persistent: every workgroup runs to the end of the
     // tile range): with a quota the grid is ~tiles / (quota * chunk) workgroups that retire as they
@@ -1988,22 +2095,21 @@ void launch_pnet(bool dense, const uint8_t* frames, int64_t frame_stride, int64_
     // persistent launch holds every CU's registers and LDS for its whole ~4.5 ms).  c2 3 lanes:
     // persistent 11.60-11.80k, quota 16 / 8 / 4 / 2: 11.98-11.99k / 12.20-12.23k / 12.34-12.39k /
     // 12.31-12.37k faces/s (same box)
-    // tiles per atomic chunk (VTF_PNET_CHUNK, default PNET_TILE_CHUNK)
-    const char* ce = std::getenv("VTF_PNET_CHUNK");
-    // (clamped: the kernel keeps tile indices and chunk ends in int)
-    const int chunk = ce && std::atoi(ce) > 0 ? std::min(64, std::atoi(ce)) : PNET_TILE_CHUNK;
-    const char* qe = std::getenv("VTF_PNET_QUOTA");
-    // (chunk x quota at 8 tiles per workgroup, full default run: 4 x 2 12.26-12.30k, 2 x 4
-    // 12.19-12.21k, 1 x 8 12.18k faces/s)
-    const int quota = qe ? std::min(1 << 16, std::max(0, std::atoi(qe))) : 2;
+    int chunk = 0, quota = 0;
+    pnet_chunking(chunk, quota);
     if (!w.c3h || !w.hh || dense || (xe && std::atoi(xe) == 0)) exact_tiles = 0;
     exact_tiles = std::min(exact_tiles, total_tiles);
     // (d_tile_ctr: three counters the caller zeroed, one per launch -- no fill kernels here)
     if (exact_tiles > 0) {
-        int64_t grid = std::min<int64_t>(exact_tiles, (int64_t)cus * wgs("VTF_PNET_X_WG_PER_CU", PnLds<true>::GPC));
-        if (quota > 0) grid = std::max<int64_t>(grid, (exact_tiles + (int64_t)quota * chunk - 1) / ((int64_t)quota * chunk));
-        k_pnet<false, true><<<(unsigned)grid, 256, 0, st>>>(frames, frame_stride, row_stride, H, W, d_levels, n_levels,
-                                                             exact_tiles, d_tile_ctr, w, o, 0, quota, chunk);
+        const int64_t grid = pnet_x_grid(exact_tiles);
+        // vertical reuse (VTF_PNET_VR=1: on) when the caller provided a slot per workgroup
+        const char* ve = std::getenv("VTF_PNET_VR");
+        if (o.vr && grid <= o.vr_slots && ve && std::atoi(ve) != 0)
+            k_pnet<false, true, false, true><<<(unsigned)grid, 256, 0, st>>>(
+                frames, frame_stride, row_stride, H, W, d_levels, n_levels, exact_tiles, d_tile_ctr, w, o, 0, quota, chunk);
+        else
+            k_pnet<false, true><<<(unsigned)grid, 256, 0, st>>>(frames, frame_stride, row_stride, H, W, d_levels, n_levels,
+                                                                 exact_tiles, d_tile_ctr, w, o, 0, quota, chunk);
     }
     if (exact_tiles >= total_tiles) return;
     // the trailing levels precomputed as split pixels run on the PR variant (four workgroups per CU)

@@ -114,6 +114,9 @@ struct Mtcnn {
     const float *oh1w, *oh1b, *oh2w, *oh2b, *oh3w, *oh3b;      // onet dense6_1 / 6_2 / 6_3
     Arena ar;
     int64_t stats[8] = {0};
+    // parity introspection (vtf_mtcnn_stage1_keys): the last call's stage-1 candidate keys
+    bool keep_s1 = false;
+    std::vector<uint64_t> s1_keys;
     // kernel timing (vtf_mtcnn_profile)
     bool prof = false;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
@@ -156,8 +159,9 @@ struct Mtcnn {
 enum Slot {
     S_FRAMES = 0, S_LEVELS, S_COUNT, S_KEY, S_SCORE, S_REGV, S_KEY2, S_SLOT, S_SLOT2, S_B1, S_S1, S_R1, S_I1, S_C1,
     S_KEEP, S_B2, S_S2, S_R2, S_I2, S_C2, S_PROB, S_REG, S_LM, S_ERR, S_FLAG, S_INCL, S_IDX, S_LMK, S_OUTB, S_OUTS,
-    S_OUTL, S_OUTI, S_SORT, S_SCAN, S_PRE, S_CROP, S_SAT, S_LVC
+    S_OUTL, S_OUTI, S_SORT, S_SCAN, S_PRE, S_CROP, S_SAT, S_LVC, S_VR
 };
+static_assert(S_VR < 40, "nms_multi owns arena slots 40-63");
 // host mailboxes (Arena::mail): stage-1 counts, stage-2/3 compaction results, final rows, box post
 enum MailSlot { M_COUNT = 0, M_STAGE = 1, M_ROWS = 2, M_BOXES = 3 };
 
@@ -859,6 +863,7 @@ static void detect(Mtcnn& m, const uint8_t* frames, int on_dev, int B, int H, in
     plan_levels(B, H, W, minsize, lv, tiles, cells);
     const int NL = (int)lv.size();
     m.stats[0] = NL;
+    m.s1_keys.clear();
     if (NL == 0) return;
     VTF_CHECK(NL < 4096 && cells < (int64_t)1 << 31, VTF_E_LIMIT, "mtcnn: pyramid too large for one call");
     VTF_CHECK(B <= 4096, VTF_E_LIMIT, "mtcnn: at most 4096 frames per call");
@@ -932,6 +937,8 @@ static void detect(Mtcnn& m, const uint8_t* frames, int on_dev, int B, int H, in
     if (po.dbg & 256) po.clk = m.ar.get<unsigned long long>(S_CLK, 16);
     if (po.clk) VTF_HIP(hipMemsetAsync(po.clk, 0, 128, st));
     const int64_t x_tiles = pnet_exact_tiles(lv, H, W, tiles);
+    po.vr_slots = pnet_x_grid(x_tiles);  // one vertical-reuse slot per exact-levels workgroup
+    if (po.vr_slots > 0) po.vr = (uint8_t*)m.ar.get(S_VR, (size_t)po.vr_slots * PNET_VR_SLOT);
     static const bool lowprio = [] {
         const char* e = std::getenv("VTF_PNET_PRIO");
         return e && std::atoi(e) != 0;
@@ -991,6 +998,11 @@ static void detect(Mtcnn& m, const uint8_t* frames, int on_dev, int B, int H, in
     int lvl_bits = 1;
     while ((1 << lvl_bits) < NL) lvl_bits++;
     sort_u64_pairs(m.ar, S_SORT, po.key, key2, slot, slot2, n1, 32 + lvl_bits, st);
+    if (m.keep_s1) {  // (tests only: one extra sync)
+        m.s1_keys.resize(n1);
+        VTF_HIP(hipMemcpyAsync(m.s1_keys.data(), key2, n1 * 8, hipMemcpyDeviceToHost, st));
+        VTF_HIP(hipStreamSynchronize(st));
+    }
     float4* b1 = m.ar.get<float4>(S_B1, n1);
     float* s1 = m.ar.get<float>(S_S1, n1);
     float4* r1 = m.ar.get<float4>(S_R1, n1);
@@ -1137,6 +1149,16 @@ int vtf_mtcnn_stats(vtf_mtcnn_t h, int64_t* out8) {
     return guarded_on(h ? h->m.device : -1, [&] {
         VTF_CHECK(h && out8, VTF_E_ARG, "null argument");
         std::memcpy(out8, h->m.stats, sizeof(h->m.stats));
+    });
+}
+
+int vtf_mtcnn_stage1_keys(vtf_mtcnn_t h, int enable, uint64_t* out, int64_t cap, int64_t* out_n) {
+    return guarded_on(h ? h->m.device : -1, [&] {
+        VTF_CHECK(h && out_n && cap >= 0 && (out || cap == 0), VTF_E_ARG, "bad argument");
+        Mtcnn& m = h->m;
+        if (enable >= 0) m.keep_s1 = enable != 0;
+        *out_n = (int64_t)m.s1_keys.size();
+        std::memcpy(out, m.s1_keys.data(), (size_t)std::min<int64_t>(cap, *out_n) * 8);
     });
 }
 

@@ -8,7 +8,7 @@
 //   * NMS: stable descending score order; areas (x2-x1)*(y2-y1) in fp32; keep i unless
 //     suppressed; suppress j if inter / ((area_i + area_j) - inter) > thr (fp32 IoU promoted
 //     to double).  Output: keep indices ordered by (score desc, index asc).
-// Design (MI355X): a stable merge sort by (call, image, score desc) gives every segment's order;
+// Design (MI355X): a stable sort by (call, image, score desc) gives every segment's order;
 // an IoU bitmask kernel (one wave per 64-row block x column-block chunk, boxes broadcast through
 // LDS) writes u64 suppression words; one workgroup per segment resolves the greedy chain 64 rows
 // per step (fixed-point diagonal, one barrier per step) and writes the segment's kept list; one
@@ -18,9 +18,6 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
-#include <rocprim/device/device_merge_sort.hpp>
-#include <rocprim/device/device_radix_sort.hpp>
-#include <rocprim/device/device_scan.hpp>
 
 #include <algorithm>
 
@@ -632,19 +629,27 @@ __device__ inline int lower_bound_u64(const uint64_t* __restrict__ l, int n, uin
 // score sort.  An equal-score entry with a smaller index in any list of the call flags the call
 // for the host's unstable-order fix (torch sorts the vanilla result unstably).  Block 0 also
 // writes the per-call kept counts.  koff: exclusive prefix of the kept counts over the segments
-// (call-major), recomputed in LDS by every block (S <= NMS_OUT_MAXS).
+// (call-major), recomputed in LDS by every block while S <= NMS_OUT_MAXS; above that (a vanilla
+// call over more distinct class ids) k_seg_prefix computes it once into global memory (GK).
 constexpr int NMS_OUT_MAXS = 15000;  // (S + 1) x 4 B of dynamic LDS (+ static) within the 64 KB default
 constexpr int OUT_G = 16;             // lanes per element: each searches every 16th image list
+__global__ __launch_bounds__(256) void k_seg_prefix(const int32_t* __restrict__ kcnt, int S, int32_t* __restrict__ koff) {
+    __shared__ int32_t part[256];
+    block_prefix<256>(kcnt, S, koff, part);
+}
+template <bool GK>
 __global__ __launch_bounds__(256) void k_nms_out(const uint64_t* __restrict__ klist, const int32_t* __restrict__ kcnt,
                                                  const int64_t* __restrict__ sstart, const uint32_t* __restrict__ seg_hi,
                                                  const int32_t* __restrict__ seg_base, int sbits, int n_img,
                                                  const uint8_t* __restrict__ van, int S, int C, int64_t N,
                                                  int32_t* __restrict__ keep, int32_t* __restrict__ res,
-                                                 int32_t* __restrict__ coff, int32_t* __restrict__ dtie) {
-    extern __shared__ int32_t koff[];  // [S + 1]
+                                                 int32_t* __restrict__ coff, int32_t* __restrict__ dtie,
+                                                 const int32_t* __restrict__ koff_g) {
+    extern __shared__ int32_t koff_s[];  // [S + 1] (!GK)
     __shared__ int32_t part[256];
     const int tid = threadIdx.x, g = tid & (OUT_G - 1);
-    block_prefix<256>(kcnt, S, koff, part);
+    const int32_t* koff = GK ? koff_g : koff_s;
+    if (!GK) block_prefix<256>(kcnt, S, koff_s, part);
     if (blockIdx.x == 0)
         for (int c = tid; c <= C; c += 256) {
             if (c < C) res[c] = koff[seg_base[c + 1]] - koff[seg_base[c]];
@@ -732,38 +737,6 @@ struct HostPack {
     }
 };
 
-template <class K, class V>
-static void radix_pairs(Arena& ar, int slot, const K* kin, K* kout, const V* vin, V* vout, int64_t n, int end_bit,
-                        hipStream_t st) {
-    size_t tmp = 0;
-    VTF_HIP(rocprim::radix_sort_pairs(nullptr, tmp, kin, kout, vin, vout, (size_t)n, 0, end_bit, st));
-    void* t = ar.get(slot, tmp);
-    VTF_HIP(rocprim::radix_sort_pairs(t, tmp, kin, kout, vin, vout, (size_t)n, 0, end_bit, st));
-}
-
-// stable merge sort (block sort + independent merge passes): no decoupled look-back, so it does
-// not stall when another lane's persistent kernel holds the CUs (the radix sort's look-back
-// blocks waited up to ~0.2 ms per call under 2 lanes); used for nms_multi's two sorts
-void merge_pairs_u64(Arena& ar, int slot, const uint64_t* kin, uint64_t* kout, const int32_t* vin,
-                            int32_t* vout, int64_t n, hipStream_t st) {
-    size_t tmp = 0;
-    VTF_HIP(rocprim::merge_sort(nullptr, tmp, kin, kout, vin, vout, (size_t)n, rocprim::less<uint64_t>(), st));
-    void* t = ar.get(slot, tmp);
-    VTF_HIP(rocprim::merge_sort(t, tmp, kin, kout, vin, vout, (size_t)n, rocprim::less<uint64_t>(), st));
-}
-
-void sort_u64_pairs(Arena& ar, int slot, const uint64_t* kin, uint64_t* kout, const int32_t* vin, int32_t* vout,
-                    int64_t n, int end_bit, hipStream_t st) {
-    radix_pairs(ar, slot, kin, kout, vin, vout, n, end_bit, st);
-}
-
-void inclusive_scan_i32(Arena& ar, int slot, const int32_t* in, int32_t* out, int64_t n, hipStream_t st) {
-    size_t tmp = 0;
-    VTF_HIP(rocprim::inclusive_scan(nullptr, tmp, in, out, (size_t)n, rocprim::plus<int32_t>(), st));
-    void* t = ar.get(slot, tmp);
-    VTF_HIP(rocprim::inclusive_scan(t, tmp, in, out, (size_t)n, rocprim::plus<int32_t>(), st));
-}
-
 // the division-free IoU test's constants for threshold thr (k_iou_mask)
 static IouThr iou_thr(double thr) {
     VTF_CHECK(std::isfinite(thr) && std::fabs(thr) < 1e30, VTF_E_ARG, "nms: iou threshold must be finite");
@@ -783,7 +756,10 @@ static bool nms_debug() {
     return on;
 }
 
-// Arena slots used here: 40..63 (device), mailboxes 40, 41
+// Arena slots used here: 40..63 (device), mailboxes 40-43: 40 the call / segment tables, 41 the
+// results, 42 the tie export pairs, 43 the host's tie order (k_tie_import reads it after this
+// function returns: queued, so mailbox 43 must not be freed meanwhile -- Arena retires grown
+// mailboxes instead of freeing them, which keeps the queued read valid)
 void nms_multi(Arena& ar, const float* d_boxes, const float* d_scores, const int32_t* d_img,
                const int32_t* d_elem_call, const std::vector<int64_t>& call_n, int n_img, double thr,
                int32_t* d_keep, std::vector<int64_t>& nkeep, hipStream_t st) {
@@ -822,7 +798,6 @@ void nms_multi(Arena& ar, const float* d_boxes, const float* d_scores, const int
     HostPack pk;
     const size_t o_cbeg = pk.add(call_beg.data(), C * 8), o_cn = pk.add(call_n.data(), C * 8);
     const size_t o_van = pk.add(vanilla.data(), C), o_sbase = pk.add(seg_base.data(), (C + 1) * 4);
-    VTF_CHECK(S <= NMS_OUT_MAXS, VTF_E_LIMIT, "nms_multi: too many segments (calls x images)");
     const size_t o_trick = pk.add(trick.data(), trick.size() * 4), o_seghi = pk.add(seg_hi.data(), S * 4);
     const int tbytes = (int)((pk.buf.size() + 3) & ~(size_t)3);
     Arena::Mail mt = ar.mail(40, tbytes);
@@ -843,7 +818,8 @@ void nms_multi(Arena& ar, const float* d_boxes, const float* d_scores, const int
     // boxes); otherwise the device-wide merge sort
     int64_t segbound = 0;
     for (int c = 0; c < C; c++) segbound = std::max(segbound, call_n[c]);
-    const bool lds_sort = segbound <= NMS_SORT_BOUND;
+    // (k_seg_scatter keeps the S + 1 segment offsets in dynamic LDS: 64 KB bound it)
+    const bool lds_sort = segbound <= NMS_SORT_BOUND && S < 16000;
     int32_t* d_sctr = ar.get<int32_t>(45, 2 * (size_t)S);
     int32_t* d_tie = ar.get<int32_t>(44, (size_t)2 * C + 1);  // [C] tie flags, [C + 1] call output offsets
     int32_t* d_coff = d_tie + C;
@@ -927,8 +903,15 @@ void nms_multi(Arena& ar, const float* d_boxes, const float* d_scores, const int
                 (long long)mx, (long long)nbs, (long long)pairs);
     }
     // output order, kept counts and vanilla tie flags in one launch
-    k_nms_out<<<cdiv(N * OUT_G, 256), 256, (size_t)(S + 1) * 4, st>>>(d_klist, d_kcnt, d_sstart, d_seghi, d_sbase, sbits, n_img,
-                                                              d_van, S, C, N, d_keep, d_res, d_coff, d_tie);
+    if (S <= NMS_OUT_MAXS) {
+        k_nms_out<false><<<cdiv(N * OUT_G, 256), 256, (size_t)(S + 1) * 4, st>>>(
+            d_klist, d_kcnt, d_sstart, d_seghi, d_sbase, sbits, n_img, d_van, S, C, N, d_keep, d_res, d_coff, d_tie, nullptr);
+    } else {
+        int32_t* d_koff = ar.get<int32_t>(59, (size_t)S + 1);
+        k_seg_prefix<<<1, 256, 0, st>>>(d_kcnt, S, d_koff);
+        k_nms_out<true><<<cdiv(N * OUT_G, 256), 256, 0, st>>>(d_klist, d_kcnt, d_sstart, d_seghi, d_sbase, sbits, n_img, d_van,
+                                                              S, C, N, d_keep, d_res, d_coff, d_tie, d_koff);
+    }
     bool any_van = false;
     for (int c = 0; c < C; c++) any_van |= vanilla[c] != 0;
     int2* h_pairs = nullptr;

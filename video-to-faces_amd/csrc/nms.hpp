@@ -39,7 +39,9 @@ inline void torch_unstable_desc_order(std::vector<int32_t>& keep, F score_of) {
     keep.swap(ord);
 }
 
-// stable merge sort of (u64 key, i32 value) pairs, no decoupled look-back (multi-lane friendly)
+// prims.hip: (u64 key, i32 value) pairs ascending by (key, value) -- a stable sort by key for
+// the callers' position-ordered values -- and an inclusive int32 scan, hand-written (LDS tile
+// sort + merge-path passes; tile sums + tile scans): no decoupled look-back (multi-lane friendly)
 void merge_pairs_u64(Arena& ar, int slot, const uint64_t* kin, uint64_t* kout, const int32_t* vin, int32_t* vout,
                      int64_t n, hipStream_t st);
 void sort_u64_pairs(Arena& ar, int slot, const uint64_t* kin, uint64_t* kout, const int32_t* vin, int32_t* vout,

@@ -33,6 +33,7 @@ SIGNATURES = {
     'vtf_mtcnn_set_stream': [_p, _p],
     'vtf_mtcnn_detect': [_p, _p, _i32, _i32, _i32, _i32, _i64, _i64, _f64, _p, _p, _p, _i64, _p],
     'vtf_mtcnn_stats': [_p, _p],
+    'vtf_mtcnn_stage1_keys': [_p, _i32, _p, _i64, _p],
     'vtf_mtcnn_profile': [_p, _i32, _p, _p, _p, _p],
     'vtf_mtcnn_pnet_level': [_p, _p, _i32, _i32, _i32, _i64, _i64, _i32, _i32, _p, _p],
     'vtf_mtcnn_resample': [_p, _p, _i32, _i32, _i32, _i64, _i64, _i32, _i32, _p],

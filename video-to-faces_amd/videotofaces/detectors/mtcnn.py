@@ -90,6 +90,15 @@ class MTCNN:
         self.last_stats = st
         return out
 
+    def stage1_keys(self, enable=-1):
+        """Parity introspection: enable (1 / 0) recording of the stage-1 candidate set for later
+        calls; returns the last call's keys (uint64 level << 32 | (b * ph + y) * pw + x, ascending)."""
+        n = ctypes.c_int64(0)
+        nat.check(nat.lib().vtf_mtcnn_stage1_keys(self._h, int(enable), None, 0, ctypes.byref(n)))
+        out = np.empty(max(1, n.value), np.uint64)
+        nat.check(nat.lib().vtf_mtcnn_stage1_keys(self._h, -1, out.ctypes.data, n.value, ctypes.byref(n)))
+        return out[:n.value]
+
     def profile(self, enable):
         """Start (enable=True, resets) or stop kernel timing of the fused pyramid+PNet kernel;
         returns (ms, launches, algorithmic flops, frames) accumulated so far."""
