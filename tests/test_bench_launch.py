@@ -239,5 +239,5 @@ def test_rank_frames_one_global_sequence():
     assert (lo, hi) == (20, 40) and off == lo % 8 and frames.shape[0] == 8 and fnp.shape[0] == 8
     a.pool = 0
     frames, off, fnp = bench.rank_frames(a, ctx, 5)
-    ref = synth.make_frames_device(0, 60, 24, 32, seed=1000)
+    ref = synth.make_frames_device(0, 60, 24, 32, seed=1000, style='blobs')
     assert off == 0 and torch.equal(frames, ref[20:40])

@@ -50,6 +50,11 @@ struct B17P {
     const __bf16 *wm, *wa, *wb, *wo;  // [256][896], [128][896], [128][896], [896][256]
     const float *alm, *bem, *ala, *bea, *alb, *beb, *bo;
     float scale;
+    // row stride (elements) of wm / wa / wb: 896, or padded (facenet_runtime: a stride that is a
+    // multiple of 128 B puts the 16 rows one load instruction reads -- 64 B each -- at the same
+    // offset in their cache lines, and the block ran ~25 % slower, scripts/r06_b17ws.py)
+    int ws;
+    int wos;  // row stride (elements) of wo: 256, or padded likewise
     unsigned long long* clk;  // debug (VTF_B17_CLK): thread 0's shader clock at the stage ends, [N][5]
 };
 
@@ -125,14 +130,13 @@ __global__ __launch_bounds__(256, 1) void k_block17(B17P p) {
     // wait on one HBM miss per XCD; one dword per 128-B line of a 1/16 slice of the block's
     // weights (workgroups go to the 8 XCDs round-robin: the 16 of one XCD cover all of them),
     // consumed (kept live) only after stage 1
-    uint32_t wv[3];
+    uint32_t wv[4];
     {
-        constexpr int LM = 256 * 896 * 2 / 128, LA = 128 * 896 * 2 / 128, LO = 896 * 256 * 2 / 128;
-        constexpr int LW = LM + 2 * LA + LO, SL = (LW + 15) / 16;
-        static_assert(SL <= 3 * 256, "warm-up loads per thread");
+        const int LM = 256 * p.ws * 2 / 128, LA = 128 * p.ws * 2 / 128, LO = 896 * p.wos * 2 / 128;
+        const int LW = LM + 2 * LA + LO, SL = (LW + 15) / 16;  // (SL <= 4 * 256: the host bounds the strides)
         const int j = (img >> 3) & 15;
 #pragma unroll
-        for (int u = 0; u < 3; u++) {
+        for (int u = 0; u < 4; u++) {
             const int l = min(j * SL + tid + 256 * u, LW - 1);
             const char* a = l < LM ? (const char*)p.wm + l * 128
                           : l < LM + LA ? (const char*)p.wa + (l - LM) * 128
@@ -165,12 +169,13 @@ __global__ __launch_bounds__(256, 1) void k_block17(B17P p) {
         for (int i = 0; i < 4; i++)
 #pragma unroll
             for (int j = 0; j < 4; j++) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
-        const __bf16* wrow = p.wm + (int64_t)(64 * wave + r) * 896 + kq;
+        const int ws = p.ws;
+        const __bf16* wrow = p.wm + (int64_t)(64 * wave + r) * ws + kq;
         bf16x8 b[8][4];
         reg_ring<28, 8>(
             [&](int c, int sl) {
 #pragma unroll
-                for (int j = 0; j < 4; j++) b[sl][j] = *(const bf16x8*)(wrow + j * 16 * 896 + 32 * c);
+                for (int j = 0; j < 4; j++) b[sl][j] = *(const bf16x8*)(wrow + j * 16 * ws + 32 * c);
             },
             [&](int c, int sl) {
 #pragma unroll
@@ -181,7 +186,7 @@ __global__ __launch_bounds__(256, 1) void k_block17(B17P p) {
                 }
             });
         bn_relu_to_lds<4, 4>(acc, p.alm, p.bem, 64 * wave, B1, B1S, lane);
-        asm volatile("" ::"v"(wv[0] | wv[1] | wv[2]));
+        asm volatile("" ::"v"(wv[0] | wv[1] | wv[2] | wv[3]));
     }
     __syncthreads();  // B1 complete; the X image is dead (B2 / E take its place)
     stamp(1);
@@ -194,12 +199,13 @@ __global__ __launch_bounds__(256, 1) void k_block17(B17P p) {
         for (int i = 0; i < 4; i++)
 #pragma unroll
             for (int j = 0; j < 2; j++) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
-        const __bf16* wrow = w + (int64_t)(32 * wave + r) * 896 + kq;
+        const int ws = p.ws;
+        const __bf16* wrow = w + (int64_t)(32 * wave + r) * ws + kq;
         bf16x8 b[8][2];
         reg_ring<28, 8>(
             [&](int c, int sl) {
 #pragma unroll
-                for (int j = 0; j < 2; j++) b[sl][j] = *(const bf16x8*)(wrow + j * 16 * 896 + 32 * c);
+                for (int j = 0; j < 2; j++) b[sl][j] = *(const bf16x8*)(wrow + j * 16 * ws + 32 * c);
             },
             [&](int c, int sl) {
                 const int t = c >> 2, ch = in_coff + 32 * (c & 3) + kq;
@@ -243,7 +249,7 @@ __global__ __launch_bounds__(256, 1) void k_block17(B17P p) {
             for (int cc = 0; cc < 8; cc++)
 #pragma unroll
                 for (int j = 0; j < 2; j++)
-                    b[cc][j] = *(const bf16x8*)(p.wo + (int64_t)(pass * 128 + 32 * wave + 16 * j + r) * 256 + 32 * cc + kq);
+                    b[cc][j] = *(const bf16x8*)(p.wo + (int64_t)(pass * 128 + 32 * wave + 16 * j + r) * p.wos + 32 * cc + kq);
         };
         auto runp = [&](int pass, const bf16x8(&b)[8][2]) {
             bf16x8 rx[4];  // this pass's residual rows (used by its epilogue)
@@ -630,6 +636,7 @@ struct B8P {
     const __bf16 *wa, *wb;  // [192][3 * 192]: 1x3 (k = kx * 192 + ci), 3x1 (k = ky * 192 + ci)
     const float *ala, *bea, *alb, *beb;
     int N;
+    int ws;  // weight row stride (elements): 576, or padded (see B17P::ws)
 };
 
 template <int B8_G>
@@ -672,7 +679,7 @@ __global__ __launch_bounds__(256) void k_block8_mid(B8P p) {
             const int tap = s / 3, cb = s - 3 * tap;
 #pragma unroll
             for (int j = 0; j < 3; j++) {
-                const __bf16* wr = w + (int64_t)(nb + 16 * j + r16) * (3 * B8_C) + tap * B8_C + 64 * cb + 8 * g;
+                const __bf16* wr = w + (int64_t)(nb + 16 * j + r16) * p.ws + tap * B8_C + 64 * cb + 8 * g;
                 d0[j] = *(const bf16x8*)wr;
                 d1[j] = *(const bf16x8*)(wr + 32);
             }
@@ -860,7 +867,7 @@ __global__ __launch_bounds__(256) void k_stem_head(StemP p) {
 void launch_block17_fused(const void* x, void* y, int N, const void* wm, const float* alm, const float* bem,
                           const void* wa, const float* ala, const float* bea, const void* wb, const float* alb,
                           const float* beb, const void* wo, const float* bo, float scale, hipStream_t st,
-                          bool head_only) {
+                          bool head_only, int ws, int wos) {
     if (N <= 0) return;
     B17P p;
     p.x = (const __bf16*)x;
@@ -878,6 +885,11 @@ void launch_block17_fused(const void* x, void* y, int N, const void* wm, const f
     p.bo = bo;
     p.scale = scale;
     p.clk = nullptr;
+    p.ws = ws;
+    p.wos = wos;
+    // (the L2 warm-up covers at most 4 x 256 lines per slice: the strides below keep it there)
+    VTF_CHECK(ws >= 896 && ws <= 1024 && ws % 8 == 0 && wos >= 256 && wos <= 384 && wos % 8 == 0, VTF_E_ARG,
+              "block17: weight row strides");
     static bool attr = [] {
         VTF_HIP(hipFuncSetAttribute((const void*)k_block17<false>, hipFuncAttributeMaxDynamicSharedMemorySize, K17_LDS));
         VTF_HIP(hipFuncSetAttribute((const void*)k_block17<true>, hipFuncAttributeMaxDynamicSharedMemorySize, K17_LDS));
@@ -1029,9 +1041,11 @@ namespace vtf {
 
 // Block8 branch-1 middle convs (bf16): T1 [N, 3, 3, 192] -> CAT[:, :, :, 192:384]
 void launch_block8_mid(const void* t1, void* cat, int N, const void* wa, const float* ala, const float* bea,
-                       const void* wb, const float* alb, const float* beb, hipStream_t st) {
+                       const void* wb, const float* alb, const float* beb, hipStream_t st, int ws) {
     if (N <= 0) return;
+    VTF_CHECK(ws >= 3 * B8_C && ws % 8 == 0, VTF_E_ARG, "block8 middle: weight row stride");
     B8P p;
+    p.ws = ws;
     p.t1 = (const __bf16*)t1;
     p.cat = (__bf16*)cat;
     p.wa = (const __bf16*)wa;

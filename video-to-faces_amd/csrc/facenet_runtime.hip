@@ -19,7 +19,7 @@ namespace vtf {
 void launch_block17_fused(const void* x, void* y, int N, const void* wm, const float* alm, const float* bem,
                           const void* wa, const float* ala, const float* bea, const void* wb, const float* alb,
                           const float* beb, const void* wo, const float* bo, float scale, hipStream_t st,
-                          bool head_only);
+                          bool head_only, int ws, int wos);
 
 void launch_block35_branches(const void* x, void* cat, int N, const void* wm, const float* alm, const float* bem,
                              const void* w1, const float* al1, const float* be1, const void* w2a, const float* al2a,
@@ -33,7 +33,7 @@ void launch_stem_head(const uint8_t* frames, int F, int H, int W, int64_t fstrid
                       hipStream_t st);
 
 void launch_block8_mid(const void* t1, void* cat, int N, const void* wa, const float* ala, const float* bea,
-                       const void* wb, const float* alb, const float* beb, hipStream_t st);
+                       const void* wb, const float* alb, const float* beb, hipStream_t st, int ws);
 
 // device crops of uint8 frames (vtf_facenet_encode_crops): the bf16 fused mode runs the blob and
 // conv2d_1a as one launch (k_stem_head)
@@ -61,6 +61,10 @@ struct Layer {
     bool bias;       // conv2d with bias (block tail) instead of ConvUnit (BN + ReLU)
     int cin_pad;
     void* w;         // [cout][kh*kw*cin_pad], element = precision
+    // (bf16) the same rows at a padded stride of ws elements, for the fused Block17 / Block8
+    // kernels that stream weights straight into registers (pad_rows)
+    void* wp = nullptr;
+    int ws = 0;
     float* b;        // bias
     float* alpha;    // BN
     float* beta;
@@ -96,6 +100,32 @@ struct G {
     int cin, cout, kh, kw, sh, sw, ph, pw;
     bool bias;
 };
+
+// Row stride (elements) for the weights the fused bf16 blocks stream from L2 into registers: their
+// load instructions read 16 rows x 64 B, and with K * 2 a multiple of 128 B every row's piece sits
+// at the same offset of its cache line -- Block17 ran ~25 % slower that way (FaceNet forward
+// 1.888 -> 1.800 ms per 128 faces at K + 112, bit-identical, scripts/r06_b17ws.py).
+// VTF_FN_WPAD: the pad in elements (multiple of 8; 0 = dense rows)
+static int fused_wpad() {
+    const char* e = std::getenv("VTF_FN_WPAD");
+    const int v = e ? std::atoi(e) : 112;
+    return v > 0 && v % 8 == 0 && v <= 128 ? v : 0;
+}
+
+static void pad_rows(Facenet& F, Layer& l, int rows, int K) {
+    const int pad = fused_wpad();
+    l.wp = l.w;
+    l.ws = K;
+    if (!pad) return;
+    const int ws = K + pad;
+    void* d = nullptr;
+    VTF_HIP(hipMalloc(&d, (size_t)rows * ws * 2 + 16));
+    F.allocs.push_back(d);
+    VTF_HIP(hipMemset(d, 0, (size_t)rows * ws * 2 + 16));
+    VTF_HIP(hipMemcpy2D(d, (size_t)ws * 2, l.w, (size_t)K * 2, (size_t)K * 2, rows, hipMemcpyDeviceToDevice));
+    l.wp = d;
+    l.ws = ws;
+}
 
 static std::vector<G> facenet_geometry() {
     std::vector<G> g = {{3, 32, 3, 3, 2, 2, 0, 0, 0},    {32, 32, 3, 3, 1, 1, 0, 0, 0},
@@ -237,6 +267,21 @@ static void build(Facenet& F, const float* params, int64_t n_params) {
     for (int k = 0; k < 10; k++) merge({45 + 5 * k, 46 + 5 * k});         // Block17 branches 0, 1
     merge({95, 97, 99});                                                   // Mixed_7a branches 0, 1, 2
     for (int k = 0; k < 6; k++) merge({102 + 5 * k, 103 + 5 * k});        // Block8 branches 0, 1
+    if (F.bf16) {
+        // padded-stride copies for the fused Block17 (merged head 896 -> 256, 1x7, 7x1) and Block8
+        // middle (1x3, 3x1) kernels
+        for (int k = 0; k < 10; k++) {
+            for (auto& e : F.LM)
+                if (e.first == 45 + 5 * k) pad_rows(F, e.second, 256, 896);
+            pad_rows(F, F.L[47 + 5 * k], 128, 896);
+            pad_rows(F, F.L[48 + 5 * k], 128, 896);
+            pad_rows(F, F.L[49 + 5 * k], 896, 256);  // the 1x1 256 -> 896 (stage 4 in the per-image form)
+        }
+        for (int k = 0; k < 6; k++) {
+            pad_rows(F, F.L[104 + 5 * k], 192, 576);
+            pad_rows(F, F.L[105 + 5 * k], 192, 576);
+        }
+    }
     const float* hw = take(512 * 1792);
     F.head_w = F.upload(std::vector<float>(hw, hw + 512 * 1792));
     const float* bw = take(512);
@@ -426,8 +471,10 @@ static void forward(Facenet& F, const void* x, int N, float* emb, const StemIn* 
             VTF_CHECK(lm, VTF_E_ARG, "facenet: no merged Block17 head");
             const Layer &la = F.L[li + 2], &lb = F.L[li + 3], &lo = F.L[li + 4];
             const bool split = b17_split();
-            launch_block17_fused(X.p, split ? CAT : Y, N, lm->w, lm->alpha, lm->beta, la.w, la.alpha, la.beta, lb.w,
-                                 lb.alpha, lb.beta, lo.w, lo.b, 0.10f, F.st, split);
+            VTF_CHECK(lm->wp && la.wp && lb.wp && lo.wp && lm->ws == la.ws && la.ws == lb.ws, VTF_E_ARG,
+                      "facenet: Block17 padded weights");
+            launch_block17_fused(X.p, split ? CAT : Y, N, lm->wp, lm->alpha, lm->beta, la.wp, la.alpha, la.beta, lb.wp,
+                                 lb.alpha, lb.beta, lo.wp, lo.b, 0.10f, F.st, split, la.ws, lo.ws);
             li += 4;
             if (split)  // the tail: the unfused path's conv (same k order and epilogue)
                 conv(F, li, Act{CAT, X.H, X.W, 256}, N, Y, 896, 0, X.p, 0.10f, true);
@@ -473,7 +520,8 @@ static void forward(Facenet& F, const void* x, int N, float* emb, const StemIn* 
             VTF_CHECK(la.cin_pad == 192 && la.cout == 192 && la.kh == 1 && la.kw == 3 && la.pw == 1 && lb.cin_pad == 192 &&
                           lb.cout == 192 && lb.kh == 3 && lb.kw == 1 && lb.ph == 1,
                       VTF_E_ARG, "facenet: Block8 middle shape");
-            launch_block8_mid(T1, CAT, N, la.w, la.alpha, la.beta, lb.w, lb.alpha, lb.beta, F.st);
+            VTF_CHECK(la.wp && lb.wp && la.ws == lb.ws, VTF_E_ARG, "facenet: Block8 padded weights");
+            launch_block8_mid(T1, CAT, N, la.wp, la.alpha, la.beta, lb.wp, lb.alpha, lb.beta, F.st, la.ws);
             li += 2;
         } else {
             t1 = Act{T1, X.H, X.W, 192};

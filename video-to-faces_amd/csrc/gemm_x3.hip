@@ -127,13 +127,13 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void k_gemm_x3(GemmX3Params p) {
     // of row 8 (wave + NW j) + (lane >> 3) takes source slot (lane & 7) ^ h, h = (row >> 1) & 7
     const int src = (lane & 7) ^ (((lane >> 4) + 4 * (wave & 1)) & 7);
     const int soff = (src & 3) * 32 + (src >> 2) * 16;
-    const int64_t rowb = (int64_t)p.K * 4;
+    const int64_t rowa = p.lda, rowb = p.ldb;
     const char* ga[PA];
     const char* gb[PB];
 #pragma unroll
     for (int j = 0; j < PA; j++) {
         const int64_t m = min(m0 + 8 * (wave + NW * j) + (lane >> 3), p.M - 1);
-        ga[j] = (const char*)p.a + m * rowb + soff;
+        ga[j] = (const char*)p.a + m * rowa + soff;
     }
 #pragma unroll
     for (int j = 0; j < PB; j++) {
@@ -270,13 +270,13 @@ __global__ __launch_bounds__(512, 1) void k_gemm_x3_pp(GemmX3Params p) {
     const int n0 = tile_n * BN;
     const int src = (lane & 7) ^ (((lane >> 4) + 4 * (wave & 1)) & 7);
     const int soff = (src & 3) * 32 + (src >> 2) * 16;
-    const int64_t rowb = (int64_t)p.K * 4;
+    const int64_t rowa = p.lda, rowb = p.ldb;
     const char* ga[PA];
     const char* gb[PB];
 #pragma unroll
     for (int j = 0; j < PA; j++) {
         const int64_t m = min(m0 + 8 * (wave + NW * j) + (lane >> 3), p.M - 1);
-        ga[j] = (const char*)p.a + m * rowb + soff;
+        ga[j] = (const char*)p.a + m * rowa + soff;
     }
 #pragma unroll
     for (int j = 0; j < PB; j++) {
@@ -525,6 +525,10 @@ void launch_gemm_x3(const GemmX3Params& p0, hipStream_t st) {
     VTF_CHECK(!p0.res || (p0.ldr >= p0.N && p0.ldr % 4 == 0), VTF_E_ARG, "gemm_x3: residual stride");
     GemmX3Params p = p0;
     p.group_m = gemm_group_m();
+    if (p.lda == 0) p.lda = (int64_t)p.K * 4;
+    if (p.ldb == 0) p.ldb = (int64_t)p.K * 4;
+    VTF_CHECK(p.lda >= (int64_t)p.K * 4 && p.ldb >= (int64_t)p.K * 4 && p.lda % 16 == 0 && p.ldb % 16 == 0, VTF_E_ARG,
+              "gemm_x3: operand row strides");
     const int big = p.M >= 4096 ? big_tiles() : 0;
     if (big == 1) launch_t<256, 128, 8>(p, st);
     else if (big == 5) launch_pp(p, st);

@@ -24,6 +24,7 @@ struct GemmX3Params {
     int dp_tiles;        // work items < dp_tiles are whole tiles
     int tail_split;      // the remaining tiles run as tail_split K slices each
     float* ws;           // tail partial sums [tail tiles][tail_split][BM * BN] (k_gemm_x3_tail reduces)
+    int64_t lda, ldb;    // row strides of a / b in bytes (0: K * 4, dense)
 };
 
 // C = A B^T (+ bias) (+ res) (GELU): K % 32 == 0, N % 8 == 0

@@ -656,7 +656,7 @@ __global__ __launch_bounds__(256, PnLds<X || PR>::GPC) void k_pnet(const uint8_t
                                                  int64_t total_tiles, uint32_t* __restrict__ tile_ctr, PNetW wg,
                                                  PNetOut o, int64_t tile_base, int max_chunks, int chunk) {
     using LP = PnLds<X || PR>;
-    static_assert(!VR || (X && !DENSE), "vertical reuse is an exact-levels variant");
+    static_assert(!VR || ((X || PR) && !DENSE), "vertical reuse: the exact-levels and PR variants");
     const VTF_CONST float* wf = cptr(wg.c1w);  // fp32 weights (scalar loads at constant offsets)
     // conv / head weights through buffer loads: one lane VGPR offset + constant SGPR offsets,
     // instead of a 64-bit address per k-step (which the compiler would keep live across tiles);
@@ -745,7 +745,7 @@ __global__ __launch_bounds__(256, PnLds<X || PR>::GPC) void k_pnet(const uint8_t
                 next_tile = (uint32_t)(tile_base + atomicAdd(tile_ctr, (uint32_t)chunk));
                 next_cend = next_tile + chunk;
             }
-            s_next = (int)next_tile;  // read at conv3 (several barriers later) for the prefetch
+            s_next = (int)next_tile;  // read after conv1 (VR) and at conv3 (prefetch)
         }
         // a workgroup's tiles come in increasing order, so its level only moves forward
         int L = L_prev;
@@ -1194,16 +1194,18 @@ __global__ __launch_bounds__(256, PnLds<X || PR>::GPC) void k_pnet(const uint8_t
                 pln = HR * PL_W * 4;
                 for (int h = 0; h < 2; h++) {
                     if (h) __syncthreads();  // the first half's fragments have read sA
+                    // (VR) a continuing tile's first half: level rows 8..21 for pooled rows 4..9
+                    const int rb = h == 0 ? lr0 : 0;
                     uint3 v[4];
 #pragma unroll
                     for (int j = 0; j < 4; j++) {
-                        const int r = min(fr0 + 6 * j, HR - 1), ly = 2 * oy0 + 20 * h + r;
+                        const int r = min(rb + fr0 + 6 * j, HR - 1), ly = 2 * oy0 + 20 * h + r;
                         const uint3 t = pre3[(int64_t)min(ly, P.lh - 1) * P.lw + cx];
                         v[j] = inx && ly < P.lh ? t : make_uint3(0u, 0u, 0u);
                     }
 #pragma unroll
                     for (int j = 0; j < 4; j++) {
-                        const int r = fr0 + 6 * j;
+                        const int r = rb + fr0 + 6 * j;
                         if (r < HR) {
                             lvl[r * PL_W + fq] = u32x2{v[j].x, v[j].y & 0xffffu};
                             lvl[HR * PL_W + r * PL_W + fq] = u32x2{(v[j].y >> 16) | (v[j].z << 16), v[j].z >> 16};
@@ -1214,10 +1216,11 @@ __global__ __launch_bounds__(256, PnLds<X || PR>::GPC) void k_pnet(const uint8_t
                     __syncthreads();
                     f_end = NF1 / 2 * (h + 1);
                     lrow0 = 20 * h;
+                    const int f0 = NF1 / 2 * h + wv + (h == 0 && cont ? 2 * FB : 0);  // (VR) pooled rows 4..
                     if (fastpool && unit_slope)
-                        conv1_frags(F{}, T{}, I1{}, conv1_frags(F{}, T{}, I2{}, NF1 / 2 * h + wv));
+                        conv1_frags(F{}, T{}, I1{}, conv1_frags(F{}, T{}, I2{}, f0));
                     else
-                        conv1_frags(F{}, F{}, I1{}, NF1 / 2 * h + wv);
+                        conv1_frags(F{}, F{}, I1{}, f0);
                 }
             } else if (X && wg.c1k) {
                 // exact levels (x1 = 0) on v_mfma_f32_16x16x32_f16, the main and cross products in
@@ -1449,7 +1452,8 @@ __global__ __launch_bounds__(256, PnLds<X || PR>::GPC) void k_pnet(const uint8_t
                 static_assert((NPOS - 2 * PC_W) % 16 == 0, "continuing-tile conv2 fragments");
                 auto conv2_frags = [&](auto u_t) {
                 constexpr bool U2 = decltype(u_t)::value;
-                for (int f0 = wave; f0 < nf; f0 += 8) {
+                // (wave index through readfirstlane: `two` is then a scalar branch, not an exec mask)
+                for (int f0 = __builtin_amdgcn_readfirstlane(wave); f0 < nf; f0 += 8) {
                     const int f1 = f0 + 4;
                     const bool two = f1 < nf;
                     const int p0 = min(pb + f0 * 16 + lrx, NPOS - 1), p1 = min(pb + (two ? f1 : f0) * 16 + lrx, NPOS - 1);
@@ -2134,9 +2138,15 @@ void launch_pnet(bool dense, const uint8_t* frames, int64_t frame_stride, int64_
         const int64_t rest = total_tiles - pre_from;
         int64_t grid = std::min<int64_t>(rest, (int64_t)cus * PnLds<true>::GPC);
         if (quota > 0) grid = std::max<int64_t>(grid, (rest + (int64_t)quota * chunk - 1) / ((int64_t)quota * chunk));
-        k_pnet<false, false, true><<<(unsigned)grid, 256, 0, st>>>(frames, frame_stride, row_stride, H, W, d_levels,
-                                                                    n_levels, total_tiles, d_tile_ctr + 2, w, og, pre_from,
-                                                                    quota, chunk);
+        const char* ve = std::getenv("VTF_PNET_VR");
+        if (o.vr && grid <= o.vr_slots && ve && std::atoi(ve) != 0)
+            k_pnet<false, false, true, true><<<(unsigned)grid, 256, 0, st>>>(
+                frames, frame_stride, row_stride, H, W, d_levels, n_levels, total_tiles, d_tile_ctr + 2, w, og, pre_from,
+                quota, chunk);
+        else
+            k_pnet<false, false, true><<<(unsigned)grid, 256, 0, st>>>(frames, frame_stride, row_stride, H, W, d_levels,
+                                                                        n_levels, total_tiles, d_tile_ctr + 2, w, og,
+                                                                        pre_from, quota, chunk);
     }
 }
 

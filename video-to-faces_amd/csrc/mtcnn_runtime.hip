@@ -937,7 +937,9 @@ static void detect(Mtcnn& m, const uint8_t* frames, int on_dev, int B, int H, in
     if (po.dbg & 256) po.clk = m.ar.get<unsigned long long>(S_CLK, 16);
     if (po.clk) VTF_HIP(hipMemsetAsync(po.clk, 0, 128, st));
     const int64_t x_tiles = pnet_exact_tiles(lv, H, W, tiles);
-    po.vr_slots = pnet_x_grid(x_tiles);  // one vertical-reuse slot per exact-levels workgroup
+    // one vertical-reuse slot per workgroup of the exact-levels or the PR launch (the same grid
+    // rule; the two run one after the other on the stream and share the slots)
+    po.vr_slots = std::max(pnet_x_grid(x_tiles), pnet_x_grid(tiles - pnet_pre_from(lv, tiles)));
     if (po.vr_slots > 0) po.vr = (uint8_t*)m.ar.get(S_VR, (size_t)po.vr_slots * PNET_VR_SLOT);
     static const bool lowprio = [] {
         const char* e = std::getenv("VTF_PNET_PRIO");
