@@ -46,8 +46,10 @@ def test_bf16_fused_blocks_bit_identical(n, split, g, monkeypatch):
     unfused kernels' MFMA k order and epilogue arithmetic: with the unfused launches' small-grid
     split-K turned off in both runs (VTF_NO_SPLITK=1, every output one k-ordered chain) the two
     paths give the same embeddings bit for bit.  Block17's stage 4 runs as its own GEMM launch over
-    the batch (VTF_B17_SPLIT=1, default) or inside the per-image launch (0).  Both paths stay within
-    the drift bar of the fp32 golden."""
+    the batch (VTF_B17_SPLIT=1, default) or inside the per-image launch (0).  The fused Block17 and
+    Block8-middle kernels stream their weights from padded-stride copies (facenet_runtime.hip
+    pad_rows, VTF_FN_WPAD), the unfused launches from the dense rows: equal bits check those too.
+    Both paths stay within the drift bar of the fp32 golden."""
     from videotofaces.encoders.facenet import InceptionResnetV1
     m = InceptionResnetV1('cuda:0', precision='bf16')
     u8 = torch.from_numpy(np.random.default_rng(n).integers(0, 256, (n, 3, 160, 160), dtype=np.uint8))
