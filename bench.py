@@ -849,7 +849,13 @@ def run_gpu(args):
                        # the reference writes face crops as JPEG files and re-reads them for the
                        # encoder (detection.py -> encoders); here crops go from HBM frames to the
                        # encoder without that round trip, as without video decode
-                       'excluded': 'video decode, JPEG write/read of crops, file moves'},
+                       'excluded': 'video decode, JPEG write/read of crops, file moves',
+                       'pool': args.pool,
+                       'frame_source': ('every frame distinct, generated on the device from (seed, frame index) '
+                                        'before the timed region (--pool 0, style %s)' % ('ids' if args.grouping else 'blobs')
+                                        if det and args.pool == 0 else
+                                        ('a %d-frame pool cycled (--pool %d)' % (args.pool, args.pool) if det else
+                                         'pre-cropped faces'))},
             'faces_per_frame': round(faces / max(1, frames_all), 3) if det else None,
             'frames_per_s': round(frames_all / elapsed, 2) if det else None,
             'embeddings_gathered': int(gathered.shape[0]),
