@@ -6,8 +6,9 @@
 //   sort_u64_pairs / merge_pairs_u64: (key, value) pairs ascending by (key, value).  Every caller
 //     passes values that increase with the input position among equal keys (element indices,
 //     positions inside a level), so this IS the stable sort by key that the reference's torch
-//     sorts / nonzero orders need.  4096-pair tiles are sorted in LDS by one 1024-thread workgroup
-//     each (bitonic network on the pair order, padding = +inf), then ceil(log2(tiles)) merge
+//     sorts / nonzero orders need.  2048-pair tiles are sorted by one 256-thread workgroup each
+//     (bitonic network on the pair order, padding = +inf: in registers, across lanes by shuffles,
+//     across waves through LDS), then ceil(log2(tiles)) merge
 //     passes: each thread finds its 8-output window of a run pair by a merge-path binary search
 //     and merges it sequentially (no atomics, no look-back: nothing waits on another workgroup,
 //     so the passes do not stall behind other lanes' persistent kernels).
@@ -20,13 +21,20 @@
 
 namespace vtf {
 
-constexpr int PS_T = 1024, PS_TILE = 4096;  // tile sort: threads, pairs per tile (48 KB LDS)
-constexpr int PM_E = 8, PM_T = 256;        // merge pass: outputs per thread, threads per block
+// tile sort: 256 threads x 8 pairs = 2048-pair tiles (24 KB of LDS for the cross-wave stages).
+// Small on purpose: a 1024-thread, 48-KB workgroup found no room next to a running k_pnet (its
+// four workgroups fill a CU's LDS and registers) and waited ~0.75 ms per sort under four
+// pipeline lanes; 256 threads with <= 38 KB fit beside three of them.
+constexpr int PS_T = 256, PS_E = 8, PS_TILE = PS_T * PS_E;
+constexpr int PM_E = 8, PM_T = 256;  // merge pass: outputs per thread, threads per block
 
 __device__ inline bool pair_lt(uint64_t ka, int32_t va, uint64_t kb, int32_t vb) {
     return ka < kb || (ka == kb && va < vb);
 }
 
+// bitonic network over the tile: thread t holds pairs 8 t .. 8 t + 7 in registers.  Partner
+// distance j < 8: inside the thread; 8 <= j < 512: another lane of the same wave (lane ^ j / 8,
+// shuffles); j >= 512: another wave (the pairs through LDS, one barrier per distance)
 __global__ __launch_bounds__(PS_T) void k_tile_sort(const uint64_t* __restrict__ kin, const int32_t* __restrict__ vin,
                                                     int64_t n, uint64_t* __restrict__ kout, int32_t* __restrict__ vout) {
     __shared__ uint64_t sk[PS_TILE];
@@ -34,33 +42,85 @@ __global__ __launch_bounds__(PS_T) void k_tile_sort(const uint64_t* __restrict__
     const int tid = threadIdx.x;
     const int64_t base = (int64_t)blockIdx.x * PS_TILE;
     const int m = (int)min((int64_t)PS_TILE, n - base);
-    int P = 1;
-    while (P < m) P <<= 1;
-    for (int i = tid; i < P; i += PS_T) {
+    uint64_t k[PS_E];
+    int32_t v[PS_E];
+#pragma unroll
+    for (int r = 0; r < PS_E; r++) {
+        const int i = PS_E * tid + r;
         const bool in = i < m;
-        sk[i] = in ? kin[base + i] : ~0ull;
-        sv[i] = in ? vin[base + i] : INT_MAX;
+        k[r] = in ? kin[base + i] : ~0ull;  // padding sorts last (values: INT_MAX > any index)
+        v[r] = in ? vin[base + i] : INT_MAX;
     }
-    __syncthreads();
-    for (int k = 2; k <= P; k <<= 1)
-        for (int j = k >> 1; j > 0; j >>= 1) {
-            for (int i = tid; i < P; i += PS_T) {
-                const int l = i ^ j;
-                if (l > i) {
-                    const uint64_t a = sk[i], b = sk[l];
-                    const int32_t va = sv[i], vb = sv[l];
-                    const bool up = (i & k) == 0;
-                    if (up ? pair_lt(b, vb, a, va) : pair_lt(a, va, b, vb)) {
-                        sk[i] = b, sk[l] = a;
-                        sv[i] = vb, sv[l] = va;
-                    }
-                }
+    auto cas = [](uint64_t& ka, int32_t& va, uint64_t& kb, int32_t& vb, bool asc) {
+        // (ka, va) <- the smaller of the two when asc, the larger otherwise
+        const bool sw = asc ? pair_lt(kb, vb, ka, va) : pair_lt(ka, va, kb, vb);
+        if (sw) {
+            const uint64_t tk = ka;
+            const int32_t tv = va;
+            ka = kb, va = vb, kb = tk, vb = tv;
+        }
+    };
+    for (int kk = 2; kk <= PS_TILE; kk <<= 1) {
+        int j = kk >> 1;
+        if (j >= 64 * PS_E) {
+#pragma unroll
+            for (int r = 0; r < PS_E; r++) {
+                sk[PS_E * tid + r] = k[r];
+                sv[PS_E * tid + r] = v[r];
             }
             __syncthreads();
+            for (; j >= 64 * PS_E; j >>= 1) {
+#pragma unroll
+                for (int u = 0; u < PS_TILE / 2 / PS_T; u++) {
+                    const int q = tid + PS_T * u;
+                    const int i = ((q & ~(j - 1)) << 1) | (q & (j - 1)), p = i | j;
+                    uint64_t ka = sk[i], kb = sk[p];
+                    int32_t va = sv[i], vb = sv[p];
+                    cas(ka, va, kb, vb, (i & kk) == 0);
+                    sk[i] = ka, sk[p] = kb;
+                    sv[i] = va, sv[p] = vb;
+                }
+                __syncthreads();
+            }
+#pragma unroll
+            for (int r = 0; r < PS_E; r++) {
+                k[r] = sk[PS_E * tid + r];
+                v[r] = sv[PS_E * tid + r];
+            }
+            __syncthreads();  // (the next distance's stores overwrite these slots)
         }
-    for (int i = tid; i < m; i += PS_T) {
-        kout[base + i] = sk[i];
-        vout[base + i] = sv[i];
+        for (; j >= PS_E; j >>= 1) {
+            const int lm = j / PS_E;  // partner lane: lane ^ lm
+            const bool lower = (tid & lm) == 0;
+#pragma unroll
+            for (int r = 0; r < PS_E; r++) {
+                const int i = PS_E * tid + r;
+                const uint32_t lo = __shfl_xor((uint32_t)k[r], lm), hi = __shfl_xor((uint32_t)(k[r] >> 32), lm);
+                const int32_t pv = __shfl_xor(v[r], lm);
+                const uint64_t pk = ((uint64_t)hi << 32) | lo;
+                const bool asc = (i & kk) == 0;
+                // the lower index keeps the smaller pair in an ascending run, the larger otherwise
+                const bool take_min = lower == asc;
+                const bool p_less = pair_lt(pk, pv, k[r], v[r]);
+                if (take_min ? p_less : !p_less) {
+                    k[r] = pk;
+                    v[r] = pv;
+                }
+            }
+        }
+        for (; j > 0; j >>= 1) {
+#pragma unroll
+            for (int r = 0; r < PS_E; r++)
+                if ((r & j) == 0) cas(k[r], v[r], k[r | j], v[r | j], ((PS_E * tid + r) & kk) == 0);
+        }
+    }
+#pragma unroll
+    for (int r = 0; r < PS_E; r++) {
+        const int i = PS_E * tid + r;
+        if (i < m) {
+            kout[base + i] = k[r];
+            vout[base + i] = v[r];
+        }
     }
 }
 
