@@ -50,8 +50,9 @@ struct PNetOut {
     int dbg;  // phase-skip mask for profiling (env VTF_PNET_DEBUG): 1 fill, 2 conv1, 4 conv2, 8 conv3,
               // 16 no candidate output, 32 no heads, 64 no frame-patch staging; 256 = phase clocks
     unsigned long long* clk;  // [8] summed shader clocks per phase over workgroups (null: off)
-    // k_pnet's vertical-reuse slots (VR_SLOT = 6144 B per workgroup of the exact-levels launch) and
-    // their count: launch_pnet runs the reuse variant when its grid fits (env VTF_PNET_VR=0: off)
+    // k_pnet's vertical-reuse slots (VR_SLOT = 6144 B per workgroup of the exact-levels or the PR
+    // launch) and their count: with env VTF_PNET_VR=1 launch_pnet runs the reuse variants when
+    // their grid fits (opt-in: measured neutral)
     uint8_t* vr;
     int64_t vr_slots;
 };
