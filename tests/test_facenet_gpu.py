@@ -49,6 +49,8 @@ def test_bf16_fused_blocks_bit_identical(n, split, g, monkeypatch):
     the batch (VTF_B17_SPLIT=1, default) or inside the per-image launch (0).  The fused Block17 and
     Block8-middle kernels stream their weights from padded-stride copies (facenet_runtime.hip
     pad_rows, VTF_FN_WPAD), the unfused launches from the dense rows: equal bits check those too.
+    The Block35 launch also runs its block tail (1x1 96 -> 256 + residual) on the rows it just
+    wrote (VTF_B35_TAIL, default on) with the unfused conv's chain and epilogue.
     Both paths stay within the drift bar of the fp32 golden."""
     from videotofaces.encoders.facenet import InceptionResnetV1
     m = InceptionResnetV1('cuda:0', precision='bf16')
