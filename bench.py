@@ -362,12 +362,25 @@ class DetEncPipeline:
         eb = self.args.enc_batch
         frames_of = (lambda: self.host[1]) if self.host is not None else (lambda: self.frames)
 
+        # start-up stagger (experiment, VTF_LANE_STAGGER=1): lane l > 0 starts once lane l - 1 has
+        # finished its first det-batch, so the lanes enter their pyramid kernels one after another
+        # (as in steady state) instead of all at once
+        stagger = os.environ.get('VTF_LANE_STAGGER', '0') == '1' and self.L > 1
+        stagger_s = float(os.environ.get('VTF_LANE_STAGGER_MS', '0')) / 1e3  # or lane l starts l x this late
+        started = [threading.Event() for _ in range(self.L)]
+
         def lane_fn(lane):
             try:
                 enc = self.encs[lane]
+                if stagger and lane > 0:
+                    started[lane - 1].wait()
+                if stagger_s > 0 and lane > 0:
+                    time.sleep(lane * stagger_s)
                 with self._stream(lane):
                     pend, npend, slots = [], 0, []
                     for k in range(lane, n, self.L):
+                        if stagger and k >= lane + self.L:
+                            started[lane].set()
                         if self.host is not None and npend:
                             # the ring slot this step overwrites still holds pending faces: flush
                             R = self.host[2]
@@ -393,6 +406,8 @@ class DetEncPipeline:
                         lane_embs[lane].append(enc.encode_crops(frames_of(), torch.cat(pend)))
             except BaseException as e:  # surfaced after join
                 errs.append(e)
+            finally:
+                started[lane].set()
         ths = [threading.Thread(target=lane_fn, args=(lane,)) for lane in range(self.L)]
         for t in ths:
             t.start()
