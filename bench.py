@@ -321,6 +321,13 @@ class DetEncPipeline:
         self.streams = [torch.cuda.Stream(dev) if self.gpu else None for _ in range(self.L)]
         self.bp = _box_params(args) if self.gpu else None
         self.host = None  # host-frame leg: (pinned frames, device ring per lane, slots per lane)
+        # lane start-up stagger: lane l starts its first det-batch l x stagger_s after lane 0, so the
+        # lanes' pyramid kernels and host syncs are out of step from the first det-batch on, as they
+        # are in steady state (all four starting together ran the first det-batches' latency-bound
+        # stages 2-3 at the same time: 20-det-batch windows 8.5k -> 9.3k faces/s with 2 ms,
+        # 625-det-batch runs unchanged, profiles/r06_lane_stagger_ab.txt); env VTF_LANE_STAGGER_MS
+        default_ms = '2' if args.det_model == 'mtcnn' else '0'
+        self.stagger_s = max(0.0, float(os.environ.get('VTF_LANE_STAGGER_MS', default_ms))) / 1e3
         self.minsize = args.min_face_size
 
     def _stream(self, lane):
@@ -362,25 +369,16 @@ class DetEncPipeline:
         eb = self.args.enc_batch
         frames_of = (lambda: self.host[1]) if self.host is not None else (lambda: self.frames)
 
-        # start-up stagger (experiment, VTF_LANE_STAGGER=1): lane l > 0 starts once lane l - 1 has
-        # finished its first det-batch, so the lanes enter their pyramid kernels one after another
-        # (as in steady state) instead of all at once
-        stagger = os.environ.get('VTF_LANE_STAGGER', '0') == '1' and self.L > 1
-        stagger_s = float(os.environ.get('VTF_LANE_STAGGER_MS', '0')) / 1e3  # or lane l starts l x this late
-        started = [threading.Event() for _ in range(self.L)]
+        stagger_s = self.stagger_s
 
         def lane_fn(lane):
             try:
                 enc = self.encs[lane]
-                if stagger and lane > 0:
-                    started[lane - 1].wait()
                 if stagger_s > 0 and lane > 0:
-                    time.sleep(lane * stagger_s)
+                    time.sleep(lane * stagger_s)  # (inside the timed region: the start-up policy's cost counts)
                 with self._stream(lane):
                     pend, npend, slots = [], 0, []
                     for k in range(lane, n, self.L):
-                        if stagger and k >= lane + self.L:
-                            started[lane].set()
                         if self.host is not None and npend:
                             # the ring slot this step overwrites still holds pending faces: flush
                             R = self.host[2]
@@ -406,8 +404,6 @@ class DetEncPipeline:
                         lane_embs[lane].append(enc.encode_crops(frames_of(), torch.cat(pend)))
             except BaseException as e:  # surfaced after join
                 errs.append(e)
-            finally:
-                started[lane].set()
         ths = [threading.Thread(target=lane_fn, args=(lane,)) for lane in range(self.L)]
         for t in ths:
             t.start()
@@ -860,6 +856,7 @@ def run_gpu(args):
             'config': {'workload': workload, 'baseline_config': args.config, 'det_batch': args.det_batch if det else None,
                        'enc_batch': args.enc_batch, 'frames_per_step_per_gpu': args.det_batch if det else 0,
                        'lanes': getattr(pipe, 'L', 1), 'hw_queues': os.environ.get('GPU_MAX_HW_QUEUES'),
+                       'lane_stagger_ms': round(getattr(pipe, 'stagger_s', 0.0) * 1e3, 3),
                        'parallelism': 'dp%d (frame-sharded, RCCL all-gather of embeddings)' % ctx.world,
                        # the reference writes face crops as JPEG files and re-reads them for the
                        # encoder (detection.py -> encoders); here crops go from HBM frames to the
