@@ -325,8 +325,9 @@ class DetEncPipeline:
         # lanes' pyramid kernels and host syncs are out of step from the first det-batch on, as they
         # are in steady state (all four starting together ran the first det-batches' latency-bound
         # stages 2-3 at the same time: 20-det-batch windows 8.5k -> 9.3k faces/s with 2 ms,
-        # 625-det-batch runs unchanged, profiles/r06_lane_stagger_ab.txt); env VTF_LANE_STAGGER_MS
-        default_ms = '2' if args.det_model == 'mtcnn' else '0'
+        # 625-det-batch runs unchanged, profiles/r06_lane_stagger_ab.txt; YOLO's 20 ms det-batches
+        # of 32: 10 ms, c3 2,468 -> 2,548); env VTF_LANE_STAGGER_MS
+        default_ms = {'mtcnn': '2', 'yolo': '10'}.get(args.det_model, '0')
         self.stagger_s = max(0.0, float(os.environ.get('VTF_LANE_STAGGER_MS', default_ms))) / 1e3
         self.minsize = args.min_face_size
 
