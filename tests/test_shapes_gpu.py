@@ -160,13 +160,15 @@ def test_mtcnn_strided_view_matches_contiguous():
         np.testing.assert_array_equal(x, y)
 
 
-@pytest.mark.parametrize('env', [{'VTF_PNET_PR': '0'}, {'VTF_PNET_X': '0', 'VTF_PNET_PR': '0'}])
+@pytest.mark.parametrize('env', [{'VTF_PNET_PR': '0'}, {'VTF_PNET_X': '0', 'VTF_PNET_PR': '0'}, {'VTF_PNET_VR': '1'}])
 def test_mtcnn_b16_pnet_variants(g, env, monkeypatch):
     """k_pnet's launch plans on config 2's det-batch against the same reference golden: the default
     (exact-levels variant + the PR variant on the levels precomputed as split pixels), the general
-    variant instead of PR (VTF_PNET_PR=0) and one general launch for every tile (VTF_PNET_X=0 too)
-    -- counts exact, boxes 2e-3 px each; the plans read the same level values (bit-identical
-    fills), so they also agree with each other to the same tolerance."""
+    variant instead of PR (VTF_PNET_PR=0), one general launch for every tile (VTF_PNET_X=0 too)
+    and the vertical-reuse variants of both launches (VTF_PNET_VR=1: a continuing tile's shared
+    pooled / conv2 rows reloaded from its workgroup's slot) -- counts exact, boxes 2e-3 px each;
+    the plans read the same level values (bit-identical fills), so they also agree with each
+    other to the same tolerance."""
     from videotofaces import synth
     from videotofaces.detectors.mtcnn import MTCNN
     frames = torch.from_numpy(synth.make_frames(16, seed=100)).cuda()

@@ -2047,9 +2047,11 @@ static void pnet_chunking(int& chunk, int& quota) {
     const char* ce = std::getenv("VTF_PNET_CHUNK");
     chunk = ce && std::atoi(ce) > 0 ? std::min(64, std::atoi(ce)) : PNET_TILE_CHUNK;
     // (chunk x quota at 8 tiles per workgroup, full default run: 4 x 2 12.26-12.30k, 2 x 4
-    // 12.19-12.21k, 1 x 8 12.18k faces/s)
+    // 12.19-12.21k, 1 x 8 12.18k faces/s; round 6, distinct frames and the 2 ms lane stagger:
+    // 4 x 1 10.00-10.03k against 4 x 2 9.91-9.97k, 4 x 4 9.80-9.85k, and the pair solo 4.229 vs
+    // 4.282 ms -- profiles/r06_pnet_quota_ab.txt)
     const char* qe = std::getenv("VTF_PNET_QUOTA");
-    quota = qe ? std::min(1 << 16, std::max(0, std::atoi(qe))) : 2;
+    quota = qe ? std::min(1 << 16, std::max(0, std::atoi(qe))) : 1;
 }
 
 static int pnet_cus() {

@@ -939,7 +939,11 @@ static void detect(Mtcnn& m, const uint8_t* frames, int on_dev, int B, int H, in
     const int64_t x_tiles = pnet_exact_tiles(lv, H, W, tiles);
     // one vertical-reuse slot per workgroup of the exact-levels or the PR launch (the same grid
     // rule; the two run one after the other on the stream and share the slots)
-    po.vr_slots = std::max(pnet_x_grid(x_tiles), pnet_x_grid(tiles - pnet_pre_from(lv, tiles)));
+    // (allocated only when the opt-in variant is on: VTF_PNET_VR=1, read per det-batch as
+    // launch_pnet reads it)
+    const char* vre = std::getenv("VTF_PNET_VR");
+    const bool vr_on = vre && std::atoi(vre) != 0;
+    po.vr_slots = vr_on ? std::max(pnet_x_grid(x_tiles), pnet_x_grid(tiles - pnet_pre_from(lv, tiles))) : 0;
     if (po.vr_slots > 0) po.vr = (uint8_t*)m.ar.get(S_VR, (size_t)po.vr_slots * PNET_VR_SLOT);
     static const bool lowprio = [] {
         const char* e = std::getenv("VTF_PNET_PRIO");
