@@ -46,7 +46,7 @@ def test_bf16_fused_blocks_bit_identical(n, split, g, monkeypatch):
     unfused kernels' MFMA k order and epilogue arithmetic: with the unfused launches' small-grid
     split-K turned off in both runs (VTF_NO_SPLITK=1, every output one k-ordered chain) the two
     paths give the same embeddings bit for bit.  Block17's stage 4 runs as its own GEMM launch over
-    the batch (VTF_B17_SPLIT=1, default) or inside the per-image launch (0).  The fused Block17 and
+    the batch (VTF_B17_SPLIT=1) or inside the per-image launch (0, default).  The fused Block17 and
     Block8-middle kernels stream their weights from padded-stride copies (facenet_runtime.hip
     pad_rows, VTF_FN_WPAD), the unfused launches from the dense rows: equal bits check those too.
     The Block35 launch also runs its block tail (1x1 96 -> 256 + residual) on the rows it just

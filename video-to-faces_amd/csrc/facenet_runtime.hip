@@ -49,11 +49,13 @@ static bool fused_blocks() {
     const char* e = std::getenv("VTF_FN_FUSED");  // (read per forward: tests switch it in-process)
     return !(e && std::atoi(e) == 0);
 }
-// Block17 stage 4 (1x1 256 -> 896 + residual) as its own GEMM launch over the batch (1, default)
-// or inside the per-image launch (VTF_B17_SPLIT=0)
+// Block17 stage 4 (1x1 256 -> 896 + residual) inside the per-image launch (default since round 6:
+// with its weights at a padded stride the per-image stream costs less than the batch launch --
+// solo forward equal, c2 +0.8 %, profiles/r06_b17_split_c2_ab.txt) or as its own GEMM launch
+// over the batch (VTF_B17_SPLIT=1)
 static bool b17_split() {
     const char* e = std::getenv("VTF_B17_SPLIT");
-    return !(e && std::atoi(e) == 0);
+    return e && std::atoi(e) != 0;
 }
 
 struct Layer {
