@@ -795,8 +795,10 @@ def run_gpu(args):
         f_h, t_h, _, _ = measure(pipe, args.steps, pipe.L, ctx)
         pipe.host_frames(None)
         out['host_frames'] = {'value': round(f_h / t_h, 2), 'ms_per_step': round(t_h * 1e3 / args.steps, 3),
-                              'note': 'frames start in pinned host memory; H2D (%.1f MB per det-batch) inside the '
-                                      'timed region' % (args.det_batch * args.H * args.W * 3 / 1e6)}
+                              'faces_per_frame': round(f_h / max(1, ctx.world * args.steps * args.det_batch), 3),
+                              'note': 'frames start in pinned host memory (the host frame pool, cycled: its content '
+                                      'differs from the distinct device frames, compare ms_per_step); H2D (%.1f MB '
+                                      'per det-batch) inside the timed region' % (args.det_batch * args.H * args.W * 3 / 1e6)}
         # the .y4m frame source's device half: 4:2:0 planes in pinned host memory, H2D of 1.5 B/px
         # and k_yuv_to_bgr per det-batch (videotofaces/video.py; the file gather is host work)
         if args.det_model == 'mtcnn' and args.H % 2 == 0 and args.W % 2 == 0:
