@@ -1132,6 +1132,14 @@ bool conv_span_ok(const ConvParams& p) {
            conv_span_max(p, SPAN_BM) <= SPAN_ROWS;
 }
 
+// VTF_DMA3_WIDE_TAIL=1 (read per launch): bf16x3 convs also split last rounds of more than half
+// the slots.  One lane: the 840-tile convs 415 -> 390 us; four lanes (c3): -3.5 %, the other lanes'
+// work already fills those slots and the slices add slab traffic (profiles/r06_dma3_wide_tail_ab.txt)
+bool dma3_wide_tail() {
+    const char* e = std::getenv("VTF_DMA3_WIDE_TAIL");
+    return e && std::atoi(e) != 0;
+}
+
 template <int BM, int BN, int WGM>
 void launch_dma3_t(ConvParams p, hipStream_t st) {
     p.gx = (int)cdiv(p.M, BM);
@@ -1150,6 +1158,23 @@ void launch_dma3_t(ConvParams p, hipStream_t st) {
             if (R > 0 && R <= slots / 2 && S >= 2) {
                 p.dp_tiles = T - R;
                 p.tail_split = S;
+            } else if (R > slots / 2 && dma3_wide_tail()) {
+                // a last round of more than half the slots (YOLO's 13x13-scale 3x3 convs: 840 tiles
+                // on 512 slots, the second round 64 % full): split those R tiles into S K-slices,
+                // S chosen for the fewest tile-rounds ceil(R S / slots) / S (840: S = 3, 2 -> 1.67)
+                int best = 1;
+                double cost = 1.0;
+                for (int s = 2; s <= 8 && KT / s >= 4; s++) {
+                    const double c = (double)((R * s + slots - 1) / slots) / s;
+                    if (c < cost - 1e-9) {
+                        cost = c;
+                        best = s;
+                    }
+                }
+                if (best > 1 && cost <= 0.85) {
+                    p.dp_tiles = T - R;
+                    p.tail_split = best;
+                }
             }
         } else {
             const int S = std::min(std::min(slots / T, KT / 4), 16);
