@@ -845,8 +845,11 @@ __global__ __launch_bounds__(256, PnLds<X || PR>::GPC) void k_pnet(const uint8_t
                     lvl[PL_H * PL_W + r * PL_W + fq] = u32x2{(v[j].y >> 16) | (v[j].z << 16), v[j].z >> 16};
                 }
             }
-        } else if (!X && P.pre) {
-            // large-bin level precomputed by k_resample_sat (fp32 planes; bit-identical values)
+        } else if (!X && !PR && P.pre) {
+            // large-bin level precomputed by k_resample_sat (fp32 planes; bit-identical values).
+            // (the PR variant loads its split levels inside conv1; until round 6 it also ran this
+            //  fill on them -- 21 KB of misread fp32 planes per tile into LDS that conv1 then
+            //  overwrote: 564 of the launch's 1,166 MB fetched, profiles/r06_pr_fetch_masks.txt)
             const float* pre = P.pre + (int64_t)b * 3 * P.lh * P.lw;
             const int64_t pl = (int64_t)P.lh * P.lw;
             for (int i0 = tid; i0 < ((o.dbg & 1) ? 0 : PL_H * PL_W); i0 += 256 * 4) {
