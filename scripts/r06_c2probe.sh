@@ -1,5 +1,5 @@
-# NOTE: VTF_PNET_DEBUG 512 / 1024 existed only in the probe build of this experiment (profiles/r06_pnet_ldsconf_phases.txt)
 #!/bin/bash
+# NOTE: VTF_PNET_DEBUG 512 / 1024 existed only in the probe build of this experiment (profiles/r06_pnet_ldsconf_phases.txt)
 # k_pnet conv2 LDS-conflict probes (VTF_PNET_DEBUG 512: 4-byte operand reads at one tap; 1024: the
 # 16-byte ones; results wrong, timing and counters only): pair solo by events + conflict counters
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
