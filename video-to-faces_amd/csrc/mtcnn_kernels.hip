@@ -398,12 +398,13 @@ void launch_resample_sat(const void* sat, int pk, int B, int H, int W, int lh, i
 }
 
 // every precomputed level of a det-batch in one launch (the small levels alone are launch-bound).
-// A workgroup takes a 2-D tile of RS_TH level rows x RS_TW pixels (each thread two pixels, rows r
-// and r + RS_TH / 2): the SAT rows a level row's bins end on are the next row's bin starts, and
+// A workgroup takes a 2-D tile of RS_TH level rows x RS_TW pixels (each thread RS_TH / 4 pixels,
+// rows r, r + 4, ...): the SAT rows a level row's bins end on are the next row's bin starts, and
 // corner columns repeat between neighbours, so a tile's corner reads come from the workgroup's own
 // L1 / its XCD's L2 instead of HBM (a row-major strip of 256 pixels per workgroup put the next
 // level row on another XCD: 960 MB fetched per det-batch for 260 MB of output)
-constexpr int RS_TH = 8, RS_TW = 64;
+constexpr int RS_TW = 64;
+template <int RS_TH>
 __global__ __launch_bounds__(256) void k_resample_sat_multi(const void* __restrict__ sat, int B, int H, int W,
                                                             ResampleLevels lv) {
     const int64_t bid = blockIdx.x;
@@ -419,8 +420,8 @@ __global__ __launch_bounds__(256) void k_resample_sat_multi(const void* __restri
     const int x0 = (int)(((int64_t)lx * W) / lw), x1 = (int)(((int64_t)(lx + 1) * W + lw - 1) / lw);
     const int64_t sb = (int64_t)b * (H + 1) * (W + 1);
 #pragma unroll
-    for (int h = 0; h < 2; h++) {
-        const int ly = ty * RS_TH + (threadIdx.x >> 6) + h * (RS_TH / 2);
+    for (int h = 0; h < RS_TH / 4; h++) {
+        const int ly = ty * RS_TH + (threadIdx.x >> 6) + 4 * h;
         if (ly >= lh || lx >= lw) continue;
         const int64_t j = ((int64_t)b * lh + ly) * lw + lx;
         const int y0 = (int)(((int64_t)ly * H) / lh), y1 = (int)(((int64_t)(ly + 1) * H + lh - 1) / lh);
@@ -447,11 +448,18 @@ void launch_resample_sat_multi(const void* sat, int B, int H, int W, const Resam
     VTF_CHECK(lv0.n >= 0 && lv0.n <= ResampleLevels::MAXL, VTF_E_LIMIT, "mtcnn: too many precomputed levels");
     if (lv0.n == 0 || lv0.beg[lv0.n] == 0) return;
     ResampleLevels lv = lv0;
+    // level rows per workgroup tile (VTF_RS_TH = 8 / 16 / 32, read per launch): 32 by default since
+    // round 6 -- one SAT row re-read per 32 level rows instead of 8: 655 -> 632 MB fetched, 157 -> 150
+    // us per c2 det-batch (profiles/r06_resample_tile_rows_ab.txt)
+    const char* e = std::getenv("VTF_RS_TH");
+    const int th = e && (std::atoi(e) == 8 || std::atoi(e) == 16) ? std::atoi(e) : 32;
     lv.tbeg[0] = 0;
     for (int l = 0; l < lv.n; l++)
-        lv.tbeg[l + 1] = lv.tbeg[l] + (int64_t)B * ((lv.lh[l] + RS_TH - 1) / RS_TH) * ((lv.lw[l] + RS_TW - 1) / RS_TW);
+        lv.tbeg[l + 1] = lv.tbeg[l] + (int64_t)B * ((lv.lh[l] + th - 1) / th) * ((lv.lw[l] + RS_TW - 1) / RS_TW);
     VTF_CHECK(lv.tbeg[lv.n] < (int64_t)1 << 31, VTF_E_LIMIT, "mtcnn: resample grid too large");
-    k_resample_sat_multi<<<(unsigned)lv.tbeg[lv.n], 256, 0, st>>>(sat, B, H, W, lv);
+    if (th == 32) k_resample_sat_multi<32><<<(unsigned)lv.tbeg[lv.n], 256, 0, st>>>(sat, B, H, W, lv);
+    else if (th == 16) k_resample_sat_multi<16><<<(unsigned)lv.tbeg[lv.n], 256, 0, st>>>(sat, B, H, W, lv);
+    else k_resample_sat_multi<8><<<(unsigned)lv.tbeg[lv.n], 256, 0, st>>>(sat, B, H, W, lv);
 }
 
 // ----------------------------------------------------------------------------------- PNet
